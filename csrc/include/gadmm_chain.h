@@ -1,0 +1,69 @@
+// Shared host/device layout of the chain engine (GADMM / D-GADMM / logistic GADMM).
+#pragma once
+#include <stdint.h>
+
+// Device-resident control block of one solve. Everything the iteration kernels need to decide
+// "what iteration is this / are we done" lives here, so captured hipGraphs replay without host
+// involvement and the host only polls `done`.
+struct ChainCtl {
+  int iter;        // next iteration to run (1-based, reference numbering)
+  int done;        // 0 running, 1 converged (gap < tol), 2 hit max_iter, 3 numerical failure
+  int conv_iter;   // first iteration whose gap < tol (reference `Iter`)
+  int pending;     // heads' end-of-iteration dual update still to apply (lazy dual, see phase kernel)
+  unsigned ticket; // arrival counter of the current phase kernel
+  int monitored;   // last iteration whose global objective has been checked
+  int pad[2];
+};
+
+// One slot of a phase plan: the local worker that updates in this phase and its chain neighbours.
+struct PhaseSlot {
+  int li;     // local worker index (row of the per-worker device arrays)
+  int gid;    // global worker id (row of the theta table)
+  int left;   // global id of the left chain neighbour, -1 at the chain head
+  int right;  // global id of the right chain neighbour, -1 at the chain tail
+};
+
+enum PhaseFlags : int {
+  PH_PRE_DUAL = 1,   // apply the pending (lazy) dual update of this slot's worker first (static chain heads)
+  PH_POST_DUAL = 2,  // apply this slot's dual update after the solve (tails: both neighbours are fresh)
+  PH_OBJ = 4,        // write the worker's local objective f_n(theta_n)
+  PH_FINISH = 8,     // last arriving block closes the iteration (objective sum / stop / iter++)
+  PH_LOCAL_STOP = 16 // this rank owns every worker: decide convergence on the spot
+};
+
+enum ModelKind : int { MODEL_LINEAR = 0, MODEL_LOGISTIC = 1 };
+
+// One point-to-point message of the chain exchange: a row of the theta table to/from a peer rank.
+struct XchgOp {
+  int peer;     // rank
+  int row;      // row of the theta table (global worker id)
+  int is_send;  // 1 send, 0 recv
+  int count;    // doubles (0 -> d)
+};
+
+// Arguments of one phase launch (passed by value; every pointer is a device address).
+struct PhaseArgs {
+  int d, n_slots, n_local, nvar;
+  int deg_to_var[3];
+  int flags, model;
+  const PhaseSlot* slots;
+  const double* Minv;  // [n_local][nvar][d][d]
+  const double* A;     // [n_local][d][d]
+  const double* b;     // [n_local][d]
+  const double* yy;    // [n_local]
+  double* mu;          // [n_local][d]
+  double* theta;       // [n_total][d]
+  double rho;
+  double* objw;        // [n_local]
+  ChainCtl* ctl;
+  double* trace;       // [max_iter]
+  double* part;        // [ring]
+  int ring, max_iter;
+  double obj0, tol;
+  // logistic
+  const double* X;     // [n_local][m][d]
+  const double* Y;     // [n_local][m]
+  int m, max_inner;
+  double lam, step, inner_tol;
+  int* inner_iters;    // [n_local] diagnostics: inner GD steps used in the last update
+};

@@ -1,0 +1,57 @@
+// Common definitions for the gfx950 (MI355X / CDNA4) kernels of gadmm_amd.
+//
+// All arithmetic is IEEE float64: the reference's stopping rule is an absolute objective gap of
+// 1e-4 .. 1e-8 on objectives of O(1e2), i.e. ~5e-11 relative, which rules out any
+// f32/bf16 path on the iterate.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define GADMM_WAVE 64
+
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+
+#define GADMM_CHECK(expr)                                                              \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess) {                                                            \
+      gadmm_set_error("%s:%d %s -> %s", __FILE__, __LINE__, #expr, hipGetErrorString(_e)); \
+      return (int)_e;                                                                  \
+    }                                                                                  \
+  } while (0)
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+void gadmm_set_error(const char* fmt, ...);
+const char* gadmm_last_error(void);
+#ifdef __cplusplus
+}
+#endif
+
+// Wave-level f64 sum (64 lanes) using cross-lane shuffles.
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// Block-level f64 sum; `scratch` must hold >= blockDim.x/64 doubles. Result valid on all threads.
+__device__ __forceinline__ double block_sum_f64(double v, double* scratch) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  v = wave_sum_f64(v);
+  __syncthreads();
+  if (lane == 0) scratch[wid] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int i = 0; i < nw; ++i) t += scratch[i];  // fixed order -> deterministic
+  return t;
+}
+
+// Bijective XCD-aware remap of a linear workgroup id (cdna_hip_programming.md §5, T1): blocks that
+// the dispatcher deals to the same XCD (b % 8 equal) get consecutive logical ids, so neighbouring
+// tiles share that XCD's L2. Placement only changes speed, never results.
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}

@@ -1,0 +1,507 @@
+// Fused per-phase kernels of the chain engine for small/medium d (<= 256): one workgroup per
+// updating worker. Kernels K3+K2-apply+K4+K5 (linear) and K8+K6 (logistic) of SURVEY.md §2.5.
+//
+// One launch = one GADMM phase (all heads, or all tails, of this rank):
+//   [lazy dual]  mu_n += rho (th_n - th_r) - rho (th_l - th_n)        (heads: pending from last iter)
+//   rhs          r_n = b_n - mu_n + rho th_l + rho th_r               (dynamic_group_ADMM_closedForm.m:84-86)
+//   solve        th_n = (A_n + deg rho I)^{-1} r_n                    (one symmetric GEMV, inverse cached)
+//   [post dual]  tails update mu right after their solve (both neighbours are fresh heads)
+//   objective    f_n = 1/2 th^T A th - b^T th + 1/2 y^T y              (group_ADMM_closedForm.m:96-101)
+//   [finish]     last arriving workgroup sums f_n in a fixed order, records the trace, decides
+//                convergence (|obj - obj0| < tol, :105-108) and advances the device iteration
+//                counter; every later launch sees `done` and returns at once.
+// The per-worker dual mu_n (= lambda_n - lambda_{n-1} in edge form) is the D-GADMM
+// parameterisation (dynamic_group_ADMM_closedForm.m:153-168); it equals the edge-dual GADMM of
+// group_ADMM_closedForm.m:93-95 for the identity chain.
+//
+// "Lazy dual": the reference updates every dual after the tail phase. A head's update needs the
+// tails' fresh theta, so it is deferred to the start of the next head phase, where the head reads
+// exactly the same values (nothing changes in between). When the chain changes (D-GADMM) the
+// engine first runs chain_dual_flush_kernel with the OLD chain.
+//
+// GEMV: lanes own output rows i = lane + 64c and the 4 waves split the summation index; since the
+// cached matrices are symmetric, row j of the matrix is read as column j (coalesced 8-B loads of a
+// contiguous row per j). Partial sums combine in LDS in a fixed order -> bitwise reproducible.
+//
+// Inter-workgroup hand-off (finish): every storing wave drains (s_waitcnt vmcnt(0)), workgroup
+// barrier, one lane releases at agent scope and takes a ticket; the last arriver acquires at agent
+// scope before reading other workgroups' results (cdna_hip_programming.md §6 Guideline 16).
+#include "gadmm_common.h"
+#include "gadmm_chain.h"
+
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int NW = NT / 64;
+
+__device__ __forceinline__ void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// out[i] = sum_j M[j*d + i] * x[j]  (M symmetric), for i < d. x, out in LDS; red: NW*64*NC.
+template <int NC>
+__device__ __forceinline__ void symv_cols(const double* __restrict__ M, const double* x, double* out,
+                                          double* red, int d) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double acc[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) acc[c] = 0.0;
+  int j = w;
+  // 2-way unrolled over j for memory-level parallelism
+  for (; j + NW < d; j += 2 * NW) {
+    const double x0 = x[j], x1 = x[j + NW];
+    const double* r0 = M + (long)j * d;
+    const double* r1 = M + (long)(j + NW) * d;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int i = lane + 64 * c;
+      if (i < d) acc[c] = fma(r1[i], x1, fma(r0[i], x0, acc[c]));
+    }
+  }
+  for (; j < d; j += NW) {
+    const double x0 = x[j];
+    const double* r0 = M + (long)j * d;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int i = lane + 64 * c;
+      if (i < d) acc[c] = fma(r0[i], x0, acc[c]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NC; ++c) red[w * 64 * NC + c * 64 + lane] = acc[c];
+  __syncthreads();
+  for (int i = threadIdx.x; i < d; i += NT) {
+    const int c = i >> 6, l = i & 63;
+    double s = 0.0;
+#pragma unroll
+    for (int ww = 0; ww < NW; ++ww) s += red[ww * 64 * NC + c * 64 + l];
+    out[i] = s;
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ double softplus(double t) {  // log(1 + exp(t)), stable
+  return t > 30.0 ? t + log1p(exp(-t)) : log1p(exp(t));
+}
+
+// Close the phase: release + ticket; the last arriver acquires and runs `finish`.
+__device__ __forceinline__ bool phase_arrive(ChainCtl* ctl, int n_slots, int* flag_lds) {
+  drain_vmem();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    drain_vmem();
+    const unsigned t = __hip_atomic_fetch_add(&ctl->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (t == (unsigned)(n_slots - 1));
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      drain_vmem();
+    }
+    *flag_lds = last;
+  }
+  __syncthreads();
+  return *flag_lds != 0;
+}
+
+__device__ void finish_iteration(const PhaseArgs& a, int it) {
+  if (threadIdx.x != 0) return;
+  ChainCtl* ctl = a.ctl;
+  double s = 0.0;
+  for (int i = 0; i < a.n_local; ++i) s += a.objw[i];  // fixed order: deterministic
+  if (a.flags & PH_LOCAL_STOP) {
+    if (it - 1 < a.max_iter) a.trace[it - 1] = s;
+    const double gap = fabs(s - a.obj0);
+    if (!(s == s) || isinf(s)) {
+      ctl->done = 3;
+      ctl->conv_iter = it;
+    } else if (gap < a.tol) {
+      ctl->done = 1;
+      ctl->conv_iter = it;
+    } else if (it >= a.max_iter) {
+      ctl->done = 2;
+      ctl->conv_iter = it;
+    }
+    ctl->monitored = it;
+  } else {
+    a.part[(it - 1) % a.ring] = s;
+  }
+  ctl->pending = 1;
+  ctl->ticket = 0u;
+  ctl->iter = it + 1;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// Linear regression phase kernel.
+template <int NC>
+__global__ void __launch_bounds__(NT) chain_phase_linear(PhaseArgs a) {
+  __shared__ __attribute__((aligned(16))) double sh_r[64 * NC];
+  __shared__ __attribute__((aligned(16))) double sh_t[64 * NC];
+  __shared__ __attribute__((aligned(16))) double sh_q[64 * NC];
+  __shared__ __attribute__((aligned(16))) double red[NW * 64 * NC];
+  __shared__ double scratch[NW];
+  __shared__ int flag_lds;
+  ChainCtl* ctl = a.ctl;
+  if (ctl->done) return;
+  const int it = ctl->iter;
+  const int pending = ctl->pending;
+  const PhaseSlot sl = a.slots[blockIdx.x];
+  const int d = a.d;
+  const double rho = a.rho;
+  double* th = a.theta;
+  const double* thw = th + (long)sl.gid * d;
+  const double* thl = sl.left >= 0 ? th + (long)sl.left * d : nullptr;
+  const double* thr = sl.right >= 0 ? th + (long)sl.right * d : nullptr;
+  double* mu = a.mu + (long)sl.li * d;
+  const double* b = a.b + (long)sl.li * d;
+  const int deg = (thl != nullptr) + (thr != nullptr);
+
+  for (int j = threadIdx.x; j < d; j += NT) {
+    double m = mu[j];
+    if ((a.flags & PH_PRE_DUAL) && pending) {
+      if (thl) m = m - rho * (thl[j] - thw[j]);
+      if (thr) m = m + rho * (thw[j] - thr[j]);
+      mu[j] = m;
+    }
+    double r = b[j] - m;
+    if (thl) r = r + rho * thl[j];
+    if (thr) r = r + rho * thr[j];
+    sh_r[j] = r;
+  }
+  __syncthreads();
+  const double* Mi = a.Minv + ((long)sl.li * a.nvar + a.deg_to_var[deg]) * (long)d * d;
+  symv_cols<NC>(Mi, sh_r, sh_t, red, d);
+  double* thw_out = th + (long)sl.gid * d;
+  for (int j = threadIdx.x; j < d; j += NT) {
+    const double t = sh_t[j];
+    thw_out[j] = t;
+    if (a.flags & PH_POST_DUAL) {
+      double m = mu[j];
+      if (thl) m = m - rho * (thl[j] - t);
+      if (thr) m = m + rho * (t - thr[j]);
+      mu[j] = m;
+    }
+  }
+  if (a.flags & PH_OBJ) {
+    symv_cols<NC>(a.A + (long)sl.li * d * d, sh_t, sh_q, red, d);
+    double part = 0.0;
+    for (int j = threadIdx.x; j < d; j += NT) part += (0.5 * sh_q[j] - b[j]) * sh_t[j];
+    const double f = block_sum_f64(part, scratch) + 0.5 * a.yy[sl.li];
+    if (threadIdx.x == 0) a.objw[sl.li] = f;
+  }
+  if (a.flags & PH_FINISH) {
+    if (phase_arrive(ctl, a.n_slots, &flag_lds)) finish_iteration(a, it);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Logistic regression phase kernel: inexact local solve by <= max_inner GD steps with the proximal
+// terms frozen at the pre-update iterate (group_ADMM_logistic_GD.m:30,39,82,85; logReg_GD.m:3-23),
+// the shard resident in LDS (row-major X and its transpose, so both GEMVs read contiguously).
+template <int NC, int MC, bool LDSX>
+__global__ void __launch_bounds__(NT) chain_phase_logistic(PhaseArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double dyn[];  // LDSX: X [m][d], XT [d][m]
+  __shared__ __attribute__((aligned(16))) double sh_x[64 * NC];
+  __shared__ __attribute__((aligned(16))) double sh_g[64 * NC];
+  __shared__ __attribute__((aligned(16))) double sh_shift[64 * NC];
+  __shared__ __attribute__((aligned(16))) double sh_z[64 * MC];
+  __shared__ __attribute__((aligned(16))) double sh_y[64 * MC];
+  __shared__ __attribute__((aligned(16))) double red[NW * 64 * (NC > MC ? NC : MC)];
+  __shared__ double scratch[NW];
+  __shared__ int flag_lds;
+  __shared__ int conv_lds;
+  ChainCtl* ctl = a.ctl;
+  if (ctl->done) return;
+  const int it = ctl->iter;
+  const int pending = ctl->pending;
+  const PhaseSlot sl = a.slots[blockIdx.x];
+  const int d = a.d, m = a.m;
+  const double rho = a.rho;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double* th = a.theta;
+  const double* thw = th + (long)sl.gid * d;
+  const double* thl = sl.left >= 0 ? th + (long)sl.left * d : nullptr;
+  const double* thr = sl.right >= 0 ? th + (long)sl.right * d : nullptr;
+  double* mu = a.mu + (long)sl.li * d;
+  const double* Xg = a.X + (long)sl.li * m * d;
+  const double* Yg = a.Y + (long)sl.li * m;
+  double* Xs = dyn;
+  double* XTs = dyn + (long)m * d;
+
+  if (LDSX) {
+    for (int e = threadIdx.x; e < m * d; e += NT) {
+      const double v = Xg[e];
+      Xs[e] = v;
+      XTs[(e % d) * m + e / d] = v;
+    }
+  }
+  for (int i = threadIdx.x; i < m; i += NT) sh_y[i] = Yg[i];
+  for (int j = threadIdx.x; j < d; j += NT) {
+    double mm = mu[j];
+    if ((a.flags & PH_PRE_DUAL) && pending) {
+      if (thl) mm = mm - rho * (thl[j] - thw[j]);
+      if (thr) mm = mm + rho * (thw[j] - thr[j]);
+      mu[j] = mm;
+    }
+    const double x0 = thw[j];
+    double s = mm;  // = -C1 + C2 in edge form
+    if (thl) s = s + rho * (x0 - thl[j]);
+    if (thr) s = s + rho * (x0 - thr[j]);
+    sh_shift[j] = s;
+    sh_x[j] = x0;
+  }
+  __syncthreads();
+
+  auto compute_z = [&]() {  // z = X x  (m outputs)
+    if (LDSX) {
+      double acc[MC];
+#pragma unroll
+      for (int c = 0; c < MC; ++c) acc[c] = 0.0;
+      for (int j = w; j < d; j += NW) {
+        const double xj = sh_x[j];
+        const double* row = XTs + (long)j * m;
+#pragma unroll
+        for (int c = 0; c < MC; ++c) {
+          const int i = lane + 64 * c;
+          if (i < m) acc[c] = fma(row[i], xj, acc[c]);
+        }
+      }
+#pragma unroll
+      for (int c = 0; c < MC; ++c) red[w * 64 * MC + c * 64 + lane] = acc[c];
+      __syncthreads();
+      for (int i = threadIdx.x; i < m; i += NT) {
+        double s = 0.0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ++ww) s += red[ww * 64 * MC + (i >> 6) * 64 + (i & 63)];
+        sh_z[i] = s;
+      }
+      __syncthreads();
+    } else {
+      // wave per row, lanes over columns
+      for (int i = w; i < m; i += NW) {
+        const double* row = Xg + (long)i * d;
+        double acc = 0.0;
+        for (int j = lane; j < d; j += 64) acc = fma(row[j], sh_x[j], acc);
+        acc = wave_sum_f64(acc);
+        if (lane == 0) sh_z[i] = acc;
+      }
+      __syncthreads();
+    }
+  };
+
+  int used = 0;
+  for (int k = 0; k < a.max_inner; ++k) {
+    compute_z();
+    for (int i = threadIdx.x; i < m; i += NT) {
+      const double yi = sh_y[i];
+      sh_z[i] = yi / (1.0 + exp(yi * sh_z[i]));  // s_i
+    }
+    if (threadIdx.x == 0) conv_lds = 1;
+    __syncthreads();
+    // g = -X^T s + lam x + shift
+    double acc[NC];
+#pragma unroll
+    for (int c = 0; c < NC; ++c) acc[c] = 0.0;
+    for (int i = w; i < m; i += NW) {
+      const double si = sh_z[i];
+      const double* row = LDSX ? (Xs + (long)i * d) : (Xg + (long)i * d);
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int j = lane + 64 * c;
+        if (j < d) acc[c] = fma(row[j], si, acc[c]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NC; ++c) red[w * 64 * NC + c * 64 + lane] = acc[c];
+    __syncthreads();
+    for (int j = threadIdx.x; j < d; j += NT) {
+      double s = 0.0;
+#pragma unroll
+      for (int ww = 0; ww < NW; ++ww) s += red[ww * 64 * NC + (j >> 6) * 64 + (j & 63)];
+      const double xj = sh_x[j];
+      const double g = -s + a.lam * xj + sh_shift[j];
+      const double xn = xj - a.step * g;
+      if (!(fabs(xn - xj) < a.inner_tol)) conv_lds = 0;
+      sh_x[j] = xn;
+    }
+    __syncthreads();
+    used = k + 1;
+    if (conv_lds) break;
+  }
+  // final local objective at the new iterate
+  compute_z();
+  double part = 0.0;
+  for (int i = threadIdx.x; i < m; i += NT) part += softplus(-sh_y[i] * sh_z[i]);
+  double xx = 0.0;
+  for (int j = threadIdx.x; j < d; j += NT) xx += sh_x[j] * sh_x[j];
+  const double lossv = block_sum_f64(part, scratch);
+  const double xnorm = block_sum_f64(xx, scratch);
+  double* thw_out = th + (long)sl.gid * d;
+  for (int j = threadIdx.x; j < d; j += NT) {
+    const double t = sh_x[j];
+    thw_out[j] = t;
+    if (a.flags & PH_POST_DUAL) {
+      double mm = mu[j];
+      if (thl) mm = mm - rho * (thl[j] - t);
+      if (thr) mm = mm + rho * (t - thr[j]);
+      mu[j] = mm;
+    }
+  }
+  if (threadIdx.x == 0) {
+    a.objw[sl.li] = a.lam * 0.5 * xnorm + lossv;
+    if (a.inner_iters) a.inner_iters[sl.li] = used;
+  }
+  if (a.flags & PH_FINISH) {
+    if (phase_arrive(ctl, a.n_slots, &flag_lds)) finish_iteration(a, it);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+// Apply the pending heads' dual updates with the chain they were computed on (used before a
+// re-chain and before checkpointing). One workgroup per slot of the OLD head plan.
+__global__ void __launch_bounds__(NT) chain_dual_flush_kernel(const PhaseSlot* slots, int n_slots, int d,
+                                                              double rho, const double* theta, double* mu_all,
+                                                              ChainCtl* ctl, int clear_pending) {
+  if (!ctl->pending) return;
+  const PhaseSlot sl = slots[blockIdx.x];
+  const double* thw = theta + (long)sl.gid * d;
+  const double* thl = sl.left >= 0 ? theta + (long)sl.left * d : nullptr;
+  const double* thr = sl.right >= 0 ? theta + (long)sl.right * d : nullptr;
+  double* mu = mu_all + (long)sl.li * d;
+  for (int j = threadIdx.x; j < d; j += NT) {
+    double m = mu[j];
+    if (thl) m = m - rho * (thl[j] - thw[j]);
+    if (thr) m = m + rho * (thw[j] - thr[j]);
+    mu[j] = m;
+  }
+  (void)n_slots;
+  (void)clear_pending;
+}
+
+__global__ void chain_clear_pending_kernel(ChainCtl* ctl) {
+  if (threadIdx.x == 0) ctl->pending = 0;
+}
+
+// Multi-rank monitor: `reduced` holds the all-reduced per-iteration objective ring. Checks every
+// iteration finished since the last monitor call, in order, exactly like the reference stop rule.
+__global__ void chain_monitor_kernel(ChainCtl* ctl, const double* reduced, int ring, double* trace, int max_iter,
+                                     double obj0, double tol) {
+  if (threadIdx.x != 0) return;
+  if (ctl->done) return;
+  const int last = ctl->iter - 1;
+  for (int j = ctl->monitored + 1; j <= last; ++j) {
+    const double s = reduced[(j - 1) % ring];
+    if (j - 1 < max_iter) trace[j - 1] = s;
+    ctl->monitored = j;
+    if (!(s == s) || isinf(s)) {
+      ctl->done = 3;
+      ctl->conv_iter = j;
+      return;
+    }
+    if (fabs(s - obj0) < tol) {
+      ctl->done = 1;
+      ctl->conv_iter = j;
+      return;
+    }
+    if (j >= max_iter) {
+      ctl->done = 2;
+      ctl->conv_iter = j;
+      return;
+    }
+  }
+}
+
+__global__ void chain_reset_kernel(ChainCtl* ctl, int start_iter, int pending) {
+  if (threadIdx.x != 0) return;
+  ctl->iter = start_iter;
+  ctl->done = 0;
+  ctl->conv_iter = 0;
+  ctl->pending = pending;
+  ctl->ticket = 0u;
+  ctl->monitored = start_iter - 1;
+}
+
+// ------------------------------------------------------------------------------------------------
+extern "C" {
+
+int gadmm_chain_phase(const PhaseArgs* args, hipStream_t st) {
+  const PhaseArgs& a = *args;
+  if (a.n_slots <= 0) return 0;
+  if (a.d > 256) {
+    gadmm_set_error("chain_phase: d=%d > 256 needs the row-blocked engine path", a.d);
+    return -1;
+  }
+  const int nc = (a.d + 63) / 64;
+  if (a.model == MODEL_LINEAR) {
+    switch (nc) {
+      case 1: hipLaunchKernelGGL(chain_phase_linear<1>, dim3(a.n_slots), dim3(NT), 0, st, a); break;
+      case 2: hipLaunchKernelGGL(chain_phase_linear<2>, dim3(a.n_slots), dim3(NT), 0, st, a); break;
+      default: hipLaunchKernelGGL(chain_phase_linear<4>, dim3(a.n_slots), dim3(NT), 0, st, a); break;
+    }
+  } else {
+    const bool ldsx = (long)a.m * a.d <= 8192 && a.m <= 256;
+    const size_t lds = ldsx ? (size_t)2 * a.m * a.d * sizeof(double) : 0;
+    const int mc = (a.m + 63) / 64;
+#define GADMM_LOG_LAUNCH(NCv, MCv, L)                                                                  \
+  do {                                                                                               \
+    auto kfn = chain_phase_logistic<NCv, MCv, L>;                                                    \
+    if (lds > 65536) GADMM_CHECK(hipFuncSetAttribute((const void*)kfn,                               \
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)); \
+    hipLaunchKernelGGL(kfn, dim3(a.n_slots), dim3(NT), lds, st, a);                                  \
+  } while (0)
+    if (ldsx) {
+      if (nc == 1 && mc == 1) GADMM_LOG_LAUNCH(1, 1, true);
+      else if (nc <= 2 && mc <= 2) GADMM_LOG_LAUNCH(2, 2, true);
+      else GADMM_LOG_LAUNCH(4, 4, true);
+    } else {
+      if (a.m > 256) {
+        // sh_z / sh_y hold the whole shard's margins; larger shards use the row-blocked path.
+        gadmm_set_error("chain_phase logistic: m=%d > 256 needs the row-blocked engine path", a.m);
+        return -1;
+      }
+      if (nc == 1) GADMM_LOG_LAUNCH(1, 4, false);
+      else GADMM_LOG_LAUNCH(4, 4, false);
+    }
+#undef GADMM_LOG_LAUNCH
+  }
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+int gadmm_chain_dual_flush(const PhaseSlot* slots, int n_slots, int d, double rho, const double* theta, double* mu,
+                           ChainCtl* ctl, hipStream_t st) {
+  if (n_slots > 0)
+    hipLaunchKernelGGL(chain_dual_flush_kernel, dim3(n_slots), dim3(NT), 0, st, slots, n_slots, d, rho, theta, mu,
+                       ctl, 1);
+  hipLaunchKernelGGL(chain_clear_pending_kernel, dim3(1), dim3(64), 0, st, ctl);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+int gadmm_chain_monitor(ChainCtl* ctl, const double* reduced, int ring, double* trace, int max_iter, double obj0,
+                        double tol, hipStream_t st) {
+  hipLaunchKernelGGL(chain_monitor_kernel, dim3(1), dim3(64), 0, st, ctl, reduced, ring, trace, max_iter, obj0, tol);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+int gadmm_chain_reset(ChainCtl* ctl, int start_iter, int pending, hipStream_t st) {
+  hipLaunchKernelGGL(chain_reset_kernel, dim3(1), dim3(64), 0, st, ctl, start_iter, pending);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"
+
+// Close an iteration on a rank that owns no tail worker (multi-rank chains can leave a rank with
+// heads only): sums the local objectives and advances the counter exactly like the tail's FINISH.
+__global__ void chain_close_kernel(PhaseArgs a) {
+  if (a.ctl->done) return;
+  finish_iteration(a, a.ctl->iter);
+}
+
+extern "C" int gadmm_chain_close(const PhaseArgs* args, hipStream_t st) {
+  hipLaunchKernelGGL(chain_close_kernel, dim3(1), dim3(64), 0, st, *args);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}

@@ -1,0 +1,245 @@
+// Batched augmented Gram (SYRK) on f64 MFMA — kernel K1 of SURVEY.md §2.5.
+//
+// For every local worker n with shard H_n (m x d, row-major) and labels y_n (m):
+//     A_n = H_n^T H_n  (d x d, full symmetric),  b_n = H_n^T y_n,  yy_n = y_n^T y_n
+// computed as ONE lower-triangular SYRK of the augmented matrix [H_n | y_n] (D = d+1 columns), so
+// the shard is streamed exactly once. The reference recomputes H^T H inside every closed-form solve
+// (group_ADMM_closedForm.m:43,45,82,84); here it is loop-invariant set-up.
+//
+// Tiling (gfx950): a 256-thread workgroup owns one BT x BT tile of the lower triangle; its 4 waves
+// are 2 x 2, each wave (BT/2) x (BT/2) as (BT/32)^2 tiles of v_mfma_f64_16x16x4_f64. K is staged
+// through LDS in BK = 16-row slabs (rows padded by 16 doubles: conflict-free ds_read_b64 — lanes
+// 0..15 read row r and lanes 16..31 row r+1 of the same half-wave), with the next slab prefetched
+// into registers while the MFMAs of the current one issue. Tall shards are split along K into
+// `ksplit` partial slabs that a second kernel reduces in a fixed order (deterministic; no f64
+// atomics). Workgroup ids are XCD-remapped so consecutive tiles share an L2.
+//
+// f64 MFMA fragment maps (cdna_hip_programming.md §3): A/B one f64 per lane, A[i=l&15][k=l>>4],
+// B[k=l>>4][j=l&15]; C/D col = l&15, row = (l>>4) + 4*reg.
+#include "gadmm_common.h"
+
+namespace {
+
+constexpr int BK = 16;
+constexpr int PAD = 16;
+
+template <int BT>
+struct GramTile {
+  static constexpr int WT = BT / 2;        // wave tile edge
+  static constexpr int TM = WT / 16;       // MFMA tiles per wave edge
+  static constexpr int LDSROW = BT + PAD;  // doubles per LDS row
+  static constexpr int PER_THREAD = BK * BT / 256;
+};
+
+__device__ __forceinline__ double aug_load(const double* __restrict__ H, const double* __restrict__ y,
+                                           long k, int c, int d, long kend) {
+  if (k >= kend) return 0.0;
+  if (c < d) return H[k * (long)d + c];
+  if (c == d) return y[k];
+  return 0.0;
+}
+
+template <int BT>
+__global__ void __launch_bounds__(256)
+gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int m, int d,
+                int ntiles, int ksplit, long rows_per_split,
+                double* __restrict__ A, double* __restrict__ B, double* __restrict__ YY,
+                double* __restrict__ slab) {
+  using T = GramTile<BT>;
+  __shared__ __attribute__((aligned(16))) double lds[2 * BK * T::LDSROW];
+  double* Li = lds;
+  double* Lj = lds + BK * T::LDSROW;
+
+  const int nwg = gridDim.x;
+  const int gid = xcd_remap(blockIdx.x, nwg);
+  const int tile = gid % ntiles;
+  const int rest = gid / ntiles;
+  const int split = rest % ksplit;
+  const int n = rest / ksplit;
+
+  // lower-triangular tile id -> (ti, tj), ti >= tj
+  int ti = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+  while ((ti + 1) * (ti + 2) / 2 <= tile) ++ti;
+  while (ti * (ti + 1) / 2 > tile) --ti;
+  const int tj = tile - ti * (ti + 1) / 2;
+  const bool diag = (ti == tj);
+  const int row0 = ti * BT, col0 = tj * BT;
+
+  const double* H = X + (long)n * m * d;
+  const double* yv = Y + (long)n * m;
+  const long kbeg = (long)split * rows_per_split;
+  long kend = kbeg + rows_per_split;
+  if (kend > m) kend = m;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int D = d + 1;
+
+  f64x4 acc[T::TM][T::TM];
+#pragma unroll
+  for (int a = 0; a < T::TM; ++a)
+#pragma unroll
+    for (int b = 0; b < T::TM; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
+
+  // staging: thread t loads slab element e = t + 256*p  (row = e / BT, col = e % BT)
+  double ri[T::PER_THREAD], rj[T::PER_THREAD];
+  auto fetch = [&](long k0) {
+#pragma unroll
+    for (int p = 0; p < T::PER_THREAD; ++p) {
+      const int e = tid + 256 * p;
+      const int r = e / BT, c = e % BT;
+      ri[p] = (row0 + c < D) ? aug_load(H, yv, k0 + r, row0 + c, d, kend) : 0.0;
+      if (!diag) rj[p] = (col0 + c < D) ? aug_load(H, yv, k0 + r, col0 + c, d, kend) : 0.0;
+    }
+  };
+  auto stash = [&]() {
+#pragma unroll
+    for (int p = 0; p < T::PER_THREAD; ++p) {
+      const int e = tid + 256 * p;
+      const int r = e / BT, c = e % BT;
+      Li[r * T::LDSROW + c] = ri[p];
+      if (!diag) Lj[r * T::LDSROW + c] = rj[p];
+    }
+  };
+
+  const double* Lb = diag ? Li : Lj;
+  if (kbeg < kend) fetch(kbeg);
+  for (long k0 = kbeg; k0 < kend; k0 += BK) {
+    __syncthreads();  // previous slab fully consumed
+    stash();
+    __syncthreads();
+    if (k0 + BK < kend) fetch(k0 + BK);  // prefetch next slab into registers (overlaps MFMAs)
+#pragma unroll
+    for (int ks = 0; ks < BK / 4; ++ks) {
+      const int kr = ks * 4 + (lane >> 4);
+      double a[T::TM], b[T::TM];
+#pragma unroll
+      for (int t = 0; t < T::TM; ++t) {
+        a[t] = Li[kr * T::LDSROW + wr * T::WT + t * 16 + (lane & 15)];
+        b[t] = Lb[kr * T::LDSROW + wc * T::WT + t * 16 + (lane & 15)];
+      }
+#pragma unroll
+      for (int x = 0; x < T::TM; ++x)
+#pragma unroll
+        for (int yq = 0; yq < T::TM; ++yq)
+          acc[x][yq] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[x], b[yq], acc[x][yq], 0, 0, 0);
+    }
+  }
+
+  // epilogue
+#pragma unroll
+  for (int x = 0; x < T::TM; ++x)
+#pragma unroll
+    for (int yq = 0; yq < T::TM; ++yq)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int lr = wr * T::WT + x * 16 + (lane >> 4) + 4 * reg;  // row within tile
+        const int lc = wc * T::WT + yq * 16 + (lane & 15);          // col within tile
+        const double v = acc[x][yq][reg];
+        if (ksplit > 1) {
+          slab[(((long)n * ntiles + tile) * ksplit + split) * (BT * BT) + lr * BT + lc] = v;
+          continue;
+        }
+        const int r = row0 + lr, c = col0 + lc;
+        if (r >= D || c >= D || c > r) continue;  // lower triangle (incl. diagonal) only
+        if (r < d && c < d) {
+          double* An = A + (long)n * d * d;
+          An[(long)r * d + c] = v;
+          An[(long)c * d + r] = v;
+        } else if (r == d && c < d) {
+          B[(long)n * d + c] = v;
+        } else if (r == d && c == d) {
+          YY[n] = v;
+        }
+      }
+}
+
+// Fixed-order reduction of the split-K slabs + symmetric scatter into (A, b, yy).
+template <int BT>
+__global__ void __launch_bounds__(256)
+gram_reduce_kernel(const double* __restrict__ slab, int d, int ntiles, int ksplit,
+                   double* __restrict__ A, double* __restrict__ B, double* __restrict__ YY) {
+  const int tile = blockIdx.x, n = blockIdx.y;
+  int ti = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
+  while ((ti + 1) * (ti + 2) / 2 <= tile) ++ti;
+  while (ti * (ti + 1) / 2 > tile) --ti;
+  const int tj = tile - ti * (ti + 1) / 2;
+  const int D = d + 1;
+  const double* s = slab + ((long)n * ntiles + tile) * ksplit * (BT * BT);
+  for (int e = threadIdx.x; e < BT * BT; e += blockDim.x) {
+    const int lr = e / BT, lc = e % BT;
+    const int r = ti * BT + lr, c = tj * BT + lc;
+    if (r >= D || c >= D || c > r) continue;
+    double v = 0.0;
+    for (int k = 0; k < ksplit; ++k) v += s[(long)k * BT * BT + e];
+    if (r < d && c < d) {
+      double* An = A + (long)n * d * d;
+      An[(long)r * d + c] = v;
+      An[(long)c * d + r] = v;
+    } else if (r == d && c < d) {
+      B[(long)n * d + c] = v;
+    } else if (r == d && c == d) {
+      YY[n] = v;
+    }
+  }
+}
+
+template <int BT>
+int launch_gram(const double* X, const double* Y, int N, int m, int d, int ksplit, double* A,
+                double* B, double* YY, double* slab, hipStream_t st) {
+  const int D = d + 1;
+  const int nt = (D + BT - 1) / BT;
+  const int ntiles = nt * (nt + 1) / 2;
+  if (ksplit < 1) ksplit = 1;
+  long rows = ((long)m + ksplit - 1) / ksplit;
+  rows = ((rows + BK - 1) / BK) * BK;
+  ksplit = (int)(((long)m + rows - 1) / rows);
+  if (ksplit < 1) ksplit = 1;
+  const long nwg = (long)ntiles * ksplit * N;
+  hipLaunchKernelGGL(gram_aug_kernel<BT>, dim3((unsigned)nwg), dim3(256), 0, st, X, Y, m, d, ntiles,
+                     ksplit, rows, A, B, YY, slab);
+  if (ksplit > 1) {
+    hipLaunchKernelGGL(gram_reduce_kernel<BT>, dim3(ntiles, N), dim3(256), 0, st, slab, d, ntiles,
+                       ksplit, A, B, YY);
+  }
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+// Workspace (doubles) needed for a given split; 0 when ksplit == 1.
+long gadmm_gram_workspace(int N, int m, int d, int ksplit) {
+  if (ksplit <= 1) return 0;
+  const int BT = (d + 1 <= 64) ? 64 : 128;
+  const int nt = (d + 1 + BT - 1) / BT;
+  return (long)N * (nt * (nt + 1) / 2) * ksplit * BT * BT;
+}
+
+// Heuristic split so that the grid covers the chip (>= ~2 workgroups per CU) for tall shards.
+int gadmm_gram_pick_ksplit(int N, int m, int d) {
+  const int BT = (d + 1 <= 64) ? 64 : 128;
+  const int nt = (d + 1 + BT - 1) / BT;
+  const long tiles = (long)N * (nt * (nt + 1) / 2);
+  long want = (512 + tiles - 1) / tiles;
+  long maxk = (m + 255) / 256;  // keep >= 256 rows per split
+  if (want > maxk) want = maxk;
+  if (want < 1) want = 1;
+  if (want > 1024) want = 1024;
+  return (int)want;
+}
+
+int gadmm_gram_f64(const double* X, const double* Y, int N, int m, int d, int ksplit, double* A,
+                   double* B, double* YY, double* slab, hipStream_t st) {
+  if (N <= 0 || m <= 0 || d <= 0) return 0;
+  if (ksplit > 1 && slab == nullptr) {
+    gadmm_set_error("gram: ksplit=%d needs a workspace", ksplit);
+    return -1;
+  }
+  if (d + 1 <= 64) return launch_gram<64>(X, Y, N, m, d, ksplit, A, B, YY, slab, st);
+  return launch_gram<128>(X, Y, N, m, d, ksplit, A, B, YY, slab, st);
+}
+
+}  // extern "C"

@@ -1,0 +1,301 @@
+// Chain engine: the GADMM / D-GADMM / logistic-GADMM iteration loop on one MI355X rank.
+//
+// Per iteration (reference group_ADMM_closedForm.m:11-108 / dynamic_group_ADMM_closedForm.m:16-182):
+//   head phase kernel  ->  [RCCL grouped send/recv of boundary theta]  ->  tail phase kernel
+//   ->  [RCCL exchange]  ->  (every `block` iterations, multi-rank only) all-reduce of the
+//   per-iteration partial-objective ring + monitor kernel.
+// The sequence for `block` iterations is captured once into a hipGraph and replayed; the iteration
+// counter, the stop decision and the objective trace live in device memory (ChainCtl), so a replay
+// needs no host input and every kernel of an iteration past convergence returns at once. The host
+// polls `done` one replay behind (async D2H into pinned memory + event), so the GPU never idles on
+// the host. With several ranks every rank launches exactly the same number of replays: the stop
+// decision comes from identical all-reduced values, so RCCL calls always match.
+#include <hip/hip_runtime.h>
+#include <string.h>
+#include <vector>
+#include <chrono>
+
+#include "gadmm_common.h"
+#include "gadmm_chain.h"
+
+extern "C" {
+int gadmm_chain_phase(const PhaseArgs* args, hipStream_t st);
+int gadmm_chain_close(const PhaseArgs* args, hipStream_t st);
+int gadmm_chain_monitor(ChainCtl* ctl, const double* reduced, int ring, double* trace, int max_iter, double obj0,
+                        double tol, hipStream_t st);
+int gadmm_chain_reset(ChainCtl* ctl, int start_iter, int pending, hipStream_t st);
+int gadmm_chain_dual_flush(const PhaseSlot* slots, int n_slots, int d, double rho, const double* theta, double* mu,
+                           ChainCtl* ctl, hipStream_t st);
+int gadmm_rccl_exchange_rows(void* h, const XchgOp* ops, int nops, double* table, int d, hipStream_t st);
+int gadmm_rccl_allreduce_sum_f64(void* h, const double* send, double* recv, long count, hipStream_t st);
+}
+
+struct EngineDesc {
+  PhaseArgs base;          // pointers, model params; slots / n_slots / flags filled per phase
+  PhaseSlot* d_slots;      // device buffer, capacity >= 2 * n_local (head plan then tail plan)
+  double* reduced;         // device [ring] (multi-rank)
+  void* comm;              // RcclComm* or null (single rank)
+  hipStream_t stream;
+  int nranks;
+};
+
+struct RunStats {
+  int iters;               // reference `Iter` (first iteration with gap < tol, or last run)
+  int done;                // ChainCtl::done
+  int iterations_launched; // iterations enqueued (>= iters; the rest returned early)
+  int replays;
+  double wall_ms;
+  long long p2p_bytes;     // bytes this rank sent over the chain, iterations 1..iters
+  long long p2p_msgs;
+  long long monitor_bytes; // all-reduce payload of the stopping monitor
+};
+
+struct ChainEngine {
+  EngineDesc desc;
+  std::vector<PhaseSlot> head, tail;
+  std::vector<XchgOp> xh, xt;
+  int plan_version = 0;
+  hipGraphExec_t exec = nullptr;
+  hipGraph_t graph = nullptr;
+  int graph_block = 0, graph_plan = -1;
+  ChainCtl* h_ctl = nullptr;  // pinned [2]
+  hipEvent_t ev[2];
+  bool graph_ok = true;
+
+  int flags_head() const {
+    int f = PH_PRE_DUAL | PH_OBJ;
+    return f;
+  }
+  int flags_tail() const {
+    int f = PH_POST_DUAL | PH_OBJ | PH_FINISH;
+    if (desc.nranks <= 1) f |= PH_LOCAL_STOP;
+    return f;
+  }
+
+  int enqueue_iteration() {
+    PhaseArgs a = desc.base;
+    hipStream_t st = desc.stream;
+    // head phase
+    a.slots = desc.d_slots;
+    a.n_slots = (int)head.size();
+    a.flags = flags_head();
+    if (a.n_slots > 0) {
+      int r = gadmm_chain_phase(&a, st);
+      if (r) return r;
+    }
+    if (desc.comm && !xh.empty()) {
+      int r = gadmm_rccl_exchange_rows(desc.comm, xh.data(), (int)xh.size(), a.theta, a.d, st);
+      if (r) return r;
+    }
+    // tail phase (also closes the iteration: FINISH needs >= 1 block, see run())
+    a.slots = desc.d_slots + head.size();
+    a.n_slots = (int)tail.size();
+    a.flags = flags_tail();
+    if (a.n_slots > 0) {
+      int r = gadmm_chain_phase(&a, st);
+      if (r) return r;
+    } else {
+      int r = gadmm_chain_close(&a, st);
+      if (r) return r;
+    }
+    if (desc.comm && !xt.empty()) {
+      int r = gadmm_rccl_exchange_rows(desc.comm, xt.data(), (int)xt.size(), a.theta, a.d, st);
+      if (r) return r;
+    }
+    return 0;
+  }
+
+  int enqueue_block(int block) {
+    for (int i = 0; i < block; ++i) {
+      int r = enqueue_iteration();
+      if (r) return r;
+    }
+    if (desc.nranks > 1) {
+      int r = gadmm_rccl_allreduce_sum_f64(desc.comm, desc.base.part, desc.reduced, desc.base.ring, desc.stream);
+      if (r) return r;
+      r = gadmm_chain_monitor(desc.base.ctl, desc.reduced, desc.base.ring, desc.base.trace, desc.base.max_iter,
+                              desc.base.obj0, desc.base.tol, desc.stream);
+      if (r) return r;
+    }
+    return 0;
+  }
+
+  void drop_graph() {
+    if (exec) hipGraphExecDestroy(exec);
+    if (graph) hipGraphDestroy(graph);
+    exec = nullptr;
+    graph = nullptr;
+    graph_plan = -1;
+  }
+
+  int ensure_graph(int block) {
+    if (exec && graph_block == block && graph_plan == plan_version) return 0;
+    drop_graph();
+    hipError_t e = hipStreamBeginCapture(desc.stream, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) {
+      graph_ok = false;
+      return 0;
+    }
+    int r = enqueue_block(block);
+    hipGraph_t g = nullptr;
+    e = hipStreamEndCapture(desc.stream, &g);
+    if (r || e != hipSuccess || g == nullptr) {
+      if (g) hipGraphDestroy(g);
+      (void)hipGetLastError();
+      graph_ok = false;  // fall back to eager launches (e.g. a communicator without capture support)
+      return 0;
+    }
+    e = hipGraphInstantiate(&exec, g, nullptr, nullptr, 0);
+    if (e != hipSuccess) {
+      hipGraphDestroy(g);
+      (void)hipGetLastError();
+      graph_ok = false;
+      return 0;
+    }
+    graph = g;
+    graph_block = block;
+    graph_plan = plan_version;
+    return 0;
+  }
+};
+
+extern "C" {
+
+void* gadmm_chain_engine_create(const EngineDesc* desc) {
+  ChainEngine* e = new ChainEngine();
+  e->desc = *desc;
+  if (hipHostMalloc((void**)&e->h_ctl, 2 * sizeof(ChainCtl), hipHostMallocDefault) != hipSuccess) {
+    gadmm_set_error("hipHostMalloc failed");
+    delete e;
+    return nullptr;
+  }
+  memset(e->h_ctl, 0, 2 * sizeof(ChainCtl));
+  hipEventCreateWithFlags(&e->ev[0], hipEventDisableTiming);
+  hipEventCreateWithFlags(&e->ev[1], hipEventDisableTiming);
+  return e;
+}
+
+void gadmm_chain_engine_destroy(void* h) {
+  ChainEngine* e = (ChainEngine*)h;
+  if (!e) return;
+  e->drop_graph();
+  hipEventDestroy(e->ev[0]);
+  hipEventDestroy(e->ev[1]);
+  if (e->h_ctl) hipHostFree(e->h_ctl);
+  delete e;
+}
+
+// Install a chain plan: this rank's head slots, tail slots and the p2p messages after each phase.
+int gadmm_chain_engine_set_plan(void* h, int n_head, const PhaseSlot* head, int n_tail, const PhaseSlot* tail,
+                                int n_xh, const XchgOp* xh, int n_xt, const XchgOp* xt) {
+  ChainEngine* e = (ChainEngine*)h;
+  e->head.assign(head, head + n_head);
+  e->tail.assign(tail, tail + n_tail);
+  e->xh.assign(xh, xh + n_xh);
+  e->xt.assign(xt, xt + n_xt);
+  std::vector<PhaseSlot> all(e->head);
+  all.insert(all.end(), e->tail.begin(), e->tail.end());
+  if (!all.empty())
+    GADMM_CHECK(hipMemcpyAsync(e->desc.d_slots, all.data(), all.size() * sizeof(PhaseSlot), hipMemcpyHostToDevice,
+                               e->desc.stream));
+  GADMM_CHECK(hipStreamSynchronize(e->desc.stream));
+  e->plan_version++;
+  return 0;
+}
+
+int gadmm_chain_engine_set_scalars(void* h, double rho, double obj0, double tol, int max_iter) {
+  ChainEngine* e = (ChainEngine*)h;
+  e->desc.base.rho = rho;
+  e->desc.base.obj0 = obj0;
+  e->desc.base.tol = tol;
+  e->desc.base.max_iter = max_iter;
+  e->drop_graph();
+  return 0;
+}
+
+int gadmm_chain_engine_reset(void* h, int start_iter, int pending) {
+  ChainEngine* e = (ChainEngine*)h;
+  return gadmm_chain_reset(e->desc.base.ctl, start_iter, pending, e->desc.stream);
+}
+
+// Apply the pending head duals with the CURRENT plan (before a re-chain / checkpoint).
+int gadmm_chain_engine_flush(void* h) {
+  ChainEngine* e = (ChainEngine*)h;
+  const PhaseArgs& a = e->desc.base;
+  return gadmm_chain_dual_flush(e->desc.d_slots, (int)e->head.size(), a.d, a.rho, a.theta, a.mu, a.ctl,
+                                e->desc.stream);
+}
+
+// Run until convergence, max_iter, or until the device iteration counter passes `stop_iter`
+// (stop_iter <= 0: no limit). `block` iterations per graph replay. Returns 0 on success.
+int gadmm_chain_engine_run(void* h, int block, int stop_iter, int use_graph, RunStats* out) {
+  ChainEngine* e = (ChainEngine*)h;
+  hipStream_t st = e->desc.stream;
+  if (block < 1) block = 1;
+  auto t0 = std::chrono::steady_clock::now();
+  bool graph = use_graph && e->graph_ok;
+  if (graph) {
+    int r = e->ensure_graph(block);
+    if (r) return r;
+    graph = e->graph_ok && e->exec;
+  }
+  // Bound iterations per call so a D-GADMM epoch stops exactly at its boundary.
+  int replays = 0, launched = 0;
+  ChainCtl last{};
+  // read the starting iteration
+  GADMM_CHECK(hipMemcpyAsync(&e->h_ctl[0], e->desc.base.ctl, sizeof(ChainCtl), hipMemcpyDeviceToHost, st));
+  GADMM_CHECK(hipStreamSynchronize(st));
+  const int start = e->h_ctl[0].iter;
+  if (e->h_ctl[0].done) {
+    last = e->h_ctl[0];
+  } else {
+    int budget = stop_iter > 0 ? stop_iter - start + 1 : 0x7fffffff;
+    if (budget <= 0) budget = 0;
+    int k = 0;
+    bool stop = false;
+    while (!stop) {
+      int nb = block;
+      if (budget < nb) nb = budget;
+      if (nb <= 0) break;
+      if (graph && nb == block) {
+        GADMM_CHECK(hipGraphLaunch(e->exec, st));
+      } else {
+        int r = e->enqueue_block(nb);
+        if (r) return r;
+      }
+      budget -= nb;
+      launched += nb;
+      replays++;
+      GADMM_CHECK(hipMemcpyAsync(&e->h_ctl[k & 1], e->desc.base.ctl, sizeof(ChainCtl), hipMemcpyDeviceToHost, st));
+      GADMM_CHECK(hipEventRecord(e->ev[k & 1], st));
+      if (k > 0) {
+        GADMM_CHECK(hipEventSynchronize(e->ev[(k - 1) & 1]));
+        if (e->h_ctl[(k - 1) & 1].done) stop = true;  // one replay in flight beyond the decision
+      }
+      if (budget <= 0) stop = true;
+      ++k;
+    }
+    GADMM_CHECK(hipStreamSynchronize(st));
+    last = e->h_ctl[(k - 1) & 1];
+  }
+  auto t1 = std::chrono::steady_clock::now();
+  out->wall_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+  out->done = last.done;
+  out->iters = last.done ? last.conv_iter : last.iter - 1;
+  out->iterations_launched = launched;
+  out->replays = replays;
+  long long per_iter = 0, msgs = 0;
+  for (auto& o : e->xh)
+    if (o.is_send) { per_iter += (long long)(o.count > 0 ? o.count : e->desc.base.d) * 8; msgs++; }
+  for (auto& o : e->xt)
+    if (o.is_send) { per_iter += (long long)(o.count > 0 ? o.count : e->desc.base.d) * 8; msgs++; }
+  const int ran = out->iters - start + 1 > 0 ? out->iters - start + 1 : 0;
+  out->p2p_bytes = per_iter * ran;
+  out->p2p_msgs = msgs * ran;
+  out->monitor_bytes = e->desc.nranks > 1 ? (long long)replays * e->desc.base.ring * 8 : 0;
+  return 0;
+}
+
+int gadmm_chain_engine_graph_ok(void* h) { return ((ChainEngine*)h)->graph_ok ? 1 : 0; }
+
+}  // extern "C"

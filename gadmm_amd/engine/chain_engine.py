@@ -1,0 +1,248 @@
+"""Python front-end of the native chain engine (csrc/runtime/chain_engine.cpp).
+
+One instance per rank. It owns the device state of the rank's logical workers:
+
+* ``theta``  (N_total, d)  primal table; rows of local workers are authoritative, other rows are
+  ghost copies of chain neighbours refreshed by the RCCL exchange;
+* ``mu``     (N_local, d)  per-worker aggregated duals (D-GADMM form, == edge duals of GADMM);
+* linear model: Gram ``A`` (N_local, d, d), ``b``, ``yy`` and the cached inverses
+  ``(A + c rho I)^{-1}`` for chain degree c in {1, 2};
+* logistic model: the shards themselves (inner GD reads them every step);
+* ``ctl`` (ChainCtl), the objective ``trace`` and the multi-rank partial-objective ring.
+
+The iteration loop itself runs in C++ (graph-captured kernels + RCCL), so a solve is one call.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..ops import native
+from ..ops.linalg import gram, spd_inverse
+from ..parallel.topology import Placement, chain_plan, RankPlan
+
+
+@dataclass
+class EngineRun:
+    iters: int
+    done: int
+    iterations_launched: int
+    replays: int
+    wall_ms: float
+    p2p_bytes: int
+    p2p_msgs: int
+    monitor_bytes: int
+
+    @property
+    def converged(self) -> bool:
+        return self.done == 1
+
+
+class NativeChainEngine:
+    def __init__(self, X_loc: torch.Tensor, y_loc: torch.Tensor, local_ids: Sequence[int], n_total: int,
+                 model: str = "linear", rho: float = 1.0, obj0: float = 0.0, tol: float = 1e-4,
+                 max_iter: int = 1000, lam: float = 0.0, step: float = 0.0, max_inner: int = 100,
+                 inner_tol: float = 1e-4, comm=None, block: int = 16, stream: Optional[torch.cuda.Stream] = None,
+                 precomputed=None):
+        if not X_loc.is_cuda:
+            raise ValueError("NativeChainEngine runs on a HIP device; use the torch algorithms on CPU")
+        self.lib = native.require()
+        self.device = X_loc.device
+        self.model = model
+        self.local_ids = [int(w) for w in local_ids]
+        self.n_local = len(self.local_ids)
+        self.n_total = int(n_total)
+        self.d = int(X_loc.shape[2])
+        self.m = int(X_loc.shape[1])
+        self.comm = comm
+        self.nranks = 1 if comm is None else comm.nranks
+        self.block = int(block)
+        self.ring = max(self.block, 1)
+        # A dedicated (non-legacy) stream: hipGraph capture is not permitted on the null stream.
+        self.stream = stream if stream is not None else torch.cuda.Stream(self.device)
+        self.stream.wait_stream(torch.cuda.current_stream(self.device))
+        self.rho, self.obj0, self.tol, self.max_iter = float(rho), float(obj0), float(tol), int(max_iter)
+        dev, f64 = self.device, torch.float64
+        d, nl = self.d, self.n_local
+
+        with torch.cuda.stream(self.stream):
+            self.theta = torch.zeros((self.n_total, d), dtype=f64, device=dev)
+            self.mu = torch.zeros((nl, d), dtype=f64, device=dev)
+            self.objw = torch.zeros((nl,), dtype=f64, device=dev)
+            self.trace = torch.full((self.max_iter,), float("nan"), dtype=f64, device=dev)
+            self.part = torch.zeros((self.ring,), dtype=f64, device=dev)
+            self.reduced = torch.zeros((self.ring,), dtype=f64, device=dev)
+            self.ctl = torch.zeros((8,), dtype=torch.int32, device=dev)
+            self.slots = torch.zeros((max(2 * nl, 2) * 4,), dtype=torch.int32, device=dev)
+            self.inner_iters = torch.zeros((max(nl, 1),), dtype=torch.int32, device=dev)
+            self.A = self.b = self.yy = self.Minv = None
+            self.X = self.Y = None
+            if model == "linear":
+                if precomputed is not None:
+                    self.A, self.b, self.yy = precomputed
+                else:
+                    self.A, self.b, self.yy = gram(X_loc, y_loc)
+                self._build_inverses()
+            elif model == "logistic":
+                self.X = X_loc.contiguous()
+                self.Y = y_loc.contiguous()
+            else:
+                raise ValueError("unknown model %r" % model)
+
+        args = native.PhaseArgs()
+        args.d, args.n_local = d, nl
+        args.nvar = self.nvar if model == "linear" else 1
+        for i, v in enumerate(self.deg_to_var if model == "linear" else (0, 0, 0)):
+            args.deg_to_var[i] = v
+        args.model = native.MODEL_LINEAR if model == "linear" else native.MODEL_LOGISTIC
+        args.Minv = native.ptr(self.Minv)
+        args.A = native.ptr(self.A)
+        args.b = native.ptr(self.b)
+        args.yy = native.ptr(self.yy)
+        args.mu = self.mu.data_ptr()
+        args.theta = self.theta.data_ptr()
+        args.rho = self.rho
+        args.objw = self.objw.data_ptr()
+        args.ctl = self.ctl.data_ptr()
+        args.trace = self.trace.data_ptr()
+        args.part = self.part.data_ptr()
+        args.ring = self.ring
+        args.max_iter = self.max_iter
+        args.obj0, args.tol = self.obj0, self.tol
+        args.X = native.ptr(self.X)
+        args.Y = native.ptr(self.Y)
+        args.m = self.m
+        args.max_inner = int(max_inner)
+        args.lam, args.step, args.inner_tol = float(lam), float(step), float(inner_tol)
+        args.inner_iters = self.inner_iters.data_ptr()
+        desc = native.EngineDesc()
+        desc.base = args
+        desc.d_slots = self.slots.data_ptr()
+        desc.reduced = self.reduced.data_ptr()
+        desc.comm = comm.handle if comm is not None else None
+        desc.stream = self.stream.cuda_stream
+        desc.nranks = self.nranks
+        self._desc = desc
+        self.handle = self.lib.gadmm_chain_engine_create(ctypes.byref(desc))
+        if not self.handle:
+            native.check(-1, "chain_engine_create")
+        self.plan: Optional[RankPlan] = None
+
+    # ---------------------------------------------------------------------------------------------
+    def _build_inverses(self):
+        rho = self.rho
+        if self.n_total == 1:
+            shifts, self.deg_to_var = [0.0], (0, 0, 0)
+        else:
+            shifts, self.deg_to_var = [rho, 2.0 * rho], (0, 0, 1)
+        self.nvar = len(shifts)
+        self.Minv = spd_inverse(self.A, torch.tensor(shifts, dtype=torch.float64, device=self.device))
+
+    def set_rho(self, rho: float):
+        """Change rho (re-inverts; the Gram is kept)."""
+        self.rho = float(rho)
+        if self.model == "linear":
+            with torch.cuda.stream(self.stream):
+                self._build_inverses()
+            self._desc.base.Minv = self.Minv.data_ptr()
+        self._desc.base.rho = self.rho
+        self._recreate()
+
+    def _recreate(self):
+        self.lib.gadmm_chain_engine_destroy(self.handle)
+        self.handle = self.lib.gadmm_chain_engine_create(ctypes.byref(self._desc))
+        if self.plan is not None:
+            self._install(self.plan)
+
+    def set_targets(self, obj0: float, tol: float, max_iter: Optional[int] = None):
+        self.obj0, self.tol = float(obj0), float(tol)
+        if max_iter is not None and max_iter != self.max_iter:
+            raise ValueError("max_iter is fixed at construction (trace buffer size)")
+        native.check(self.lib.gadmm_chain_engine_set_scalars(self.handle, self.rho, self.obj0, self.tol,
+                                                             self.max_iter), "set_scalars")
+        self._desc.base.obj0, self._desc.base.tol = self.obj0, self.tol
+
+    # ---------------------------------------------------------------------------------------------
+    def set_path(self, path: Sequence[int], placement: Placement, rank: int):
+        """Install the chain ``path`` (position -> global worker id) for this rank."""
+        plan = chain_plan(path, placement, rank)
+        lidx = {w: i for i, w in enumerate(self.local_ids)}
+        for s in plan.head + plan.tail:
+            if self.local_ids[s.li] != s.gid or lidx[s.gid] != s.li:
+                raise ValueError("placement/local_ids mismatch")
+        self._install(plan)
+        self.plan = plan
+
+    def _install(self, plan: RankPlan):
+        def slots(lst):
+            arr = (native.PhaseSlot * max(len(lst), 1))()
+            for i, s in enumerate(lst):
+                arr[i].li, arr[i].gid, arr[i].left, arr[i].right = s.li, s.gid, s.left, s.right
+            return arr
+
+        def ops(lst):
+            arr = (native.XchgOp * max(len(lst), 1))()
+            for i, (peer, row, snd) in enumerate(lst):
+                arr[i].peer, arr[i].row, arr[i].is_send, arr[i].count = peer, row, snd, 0
+            return arr
+
+        if len(plan.head) + len(plan.tail) > 2 * max(self.n_local, 1):
+            raise ValueError("plan larger than slot buffer")
+        rc = self.lib.gadmm_chain_engine_set_plan(self.handle, len(plan.head), slots(plan.head), len(plan.tail),
+                                                  slots(plan.tail), len(plan.xchg_head), ops(plan.xchg_head),
+                                                  len(plan.xchg_tail), ops(plan.xchg_tail))
+        native.check(rc, "set_plan")
+
+    def reset(self, start_iter: int = 1, pending: int = 0, zero_state: bool = True):
+        with torch.cuda.stream(self.stream):
+            if zero_state:
+                self.theta.zero_()
+                self.mu.zero_()
+                self.trace.fill_(float("nan"))
+                self.part.zero_()
+        native.check(self.lib.gadmm_chain_engine_reset(self.handle, int(start_iter), int(pending)), "reset")
+
+    def flush_duals(self):
+        """Apply pending head duals with the current chain (before re-chain / checkpoint)."""
+        native.check(self.lib.gadmm_chain_engine_flush(self.handle), "flush")
+
+    def run(self, stop_iter: int = 0, use_graph: bool = True, block: Optional[int] = None) -> EngineRun:
+        st = native.RunStats()
+        blk = self.block if block is None else int(block)
+        if blk > self.ring and self.nranks > 1:
+            raise ValueError("block must be <= ring for multi-rank runs")
+        rc = self.lib.gadmm_chain_engine_run(self.handle, blk, int(stop_iter), 1 if use_graph else 0,
+                                             ctypes.byref(st))
+        native.check(rc, "chain_engine_run")
+        return EngineRun(st.iters, st.done, st.iterations_launched, st.replays, st.wall_ms, st.p2p_bytes,
+                         st.p2p_msgs, st.monitor_bytes)
+
+    def graph_ok(self) -> bool:
+        return bool(self.lib.gadmm_chain_engine_graph_ok(self.handle))
+
+    def ctl_state(self) -> dict:
+        c = self.ctl.cpu().tolist()
+        return {"iter": c[0], "done": c[1], "conv_iter": c[2], "pending": c[3], "ticket": c[4], "monitored": c[5]}
+
+    def objective_trace(self, upto: Optional[int] = None) -> np.ndarray:
+        t = self.trace.cpu().numpy()
+        return t if upto is None else t[:upto]
+
+    def local_theta(self) -> torch.Tensor:
+        idx = torch.tensor(self.local_ids, dtype=torch.long, device=self.device)
+        return self.theta.index_select(0, idx)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.gadmm_chain_engine_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,82 @@
+"""Dense f64 linear-algebra ops with a HIP path (gfx950) and a PyTorch CPU path.
+
+* ``gram(X, y)``: per-worker ``A = X^T X``, ``b = X^T y``, ``yy = y^T y`` (kernel K1: one f64-MFMA
+  SYRK of the augmented shard ``[X | y]``, csrc/kernels/gram.hip).
+* ``spd_inverse(A, shifts)``: ``(A_n + s_{n,v} I)^{-1}`` for every worker n and shift v
+  (kernel K2: in-LDS Gauss-Jordan for d <= 128, csrc/kernels/spd_inverse.hip; rocSOLVER Cholesky
+  for larger d, which is one-time set-up).
+
+CUDA tensors always take the native path (and raise if the library is missing); CPU tensors use
+torch, which is also the fp64 reference the kernels are tested against.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from . import native
+
+
+def gram_torch(X: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    Xt = X.transpose(1, 2)
+    A = torch.bmm(Xt, X)
+    b = torch.bmm(Xt, y.unsqueeze(-1)).squeeze(-1)
+    yy = (y * y).sum(dim=1)
+    return A, b, yy
+
+
+def gram(X: torch.Tensor, y: torch.Tensor, ksplit: Optional[int] = None
+         ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Batched augmented Gram. ``X``: (N, m, d) f64 contiguous, ``y``: (N, m)."""
+    if X.dtype != torch.float64 or y.dtype != torch.float64:
+        raise TypeError("gram expects float64")
+    if not X.is_cuda:
+        return gram_torch(X, y)
+    lib = native.require()
+    X = X.contiguous()
+    y = y.contiguous()
+    N, m, d = X.shape
+    A = torch.empty((N, d, d), dtype=torch.float64, device=X.device)
+    b = torch.empty((N, d), dtype=torch.float64, device=X.device)
+    yy = torch.empty((N,), dtype=torch.float64, device=X.device)
+    if ksplit is None:
+        ksplit = int(lib.gadmm_gram_pick_ksplit(N, m, d))
+    ws_n = int(lib.gadmm_gram_workspace(N, m, d, ksplit))
+    ws = torch.empty((max(ws_n, 1),), dtype=torch.float64, device=X.device) if ws_n > 0 else None
+    rc = lib.gadmm_gram_f64(X.data_ptr(), y.data_ptr(), N, m, d, ksplit, A.data_ptr(), b.data_ptr(),
+                            yy.data_ptr(), ws.data_ptr() if ws is not None else None, native.stream_handle())
+    native.check(rc, "gram_f64")
+    return A, b, yy
+
+
+def spd_inverse_torch(A: torch.Tensor, shifts: torch.Tensor) -> torch.Tensor:
+    N, d, _ = A.shape
+    V = shifts.shape[1]
+    eye = torch.eye(d, dtype=A.dtype, device=A.device)
+    M = A.unsqueeze(1) + shifts.to(A.dtype).view(N, V, 1, 1) * eye
+    L = torch.linalg.cholesky(M.reshape(N * V, d, d))
+    inv = torch.cholesky_inverse(L)
+    inv = 0.5 * (inv + inv.transpose(-1, -2))
+    return inv.reshape(N, V, d, d)
+
+
+def spd_inverse(A: torch.Tensor, shifts: torch.Tensor) -> torch.Tensor:
+    """``(N, V, d, d)`` inverses of ``A_n + shifts[n, v] I`` (all SPD)."""
+    shifts = torch.as_tensor(shifts, dtype=torch.float64, device=A.device)
+    if shifts.dim() == 1:
+        shifts = shifts.unsqueeze(0).expand(A.shape[0], -1)
+    shifts = shifts.contiguous()
+    N, d, _ = A.shape
+    V = shifts.shape[1]
+    if not A.is_cuda or d > 128:
+        return spd_inverse_torch(A, shifts)
+    lib = native.require()
+    out = torch.empty((N, V, d, d), dtype=torch.float64, device=A.device)
+    status = torch.zeros((1,), dtype=torch.int32, device=A.device)
+    rc = lib.gadmm_spd_inverse_small_f64(A.contiguous().data_ptr(), shifts.data_ptr(), N, d, V, out.data_ptr(),
+                                         status.data_ptr(), native.stream_handle())
+    native.check(rc, "spd_inverse_small_f64")
+    if int(status.item()) != 0:
+        raise FloatingPointError("spd_inverse: matrix is not positive definite")
+    return out

@@ -1,0 +1,168 @@
+"""ctypes binding of ``libgadmm_native.so`` (HIP kernels + C++ runtime for gfx950).
+
+The library has a plain C ABI; tensors are passed as raw device pointers and HIP streams as the
+``torch.cuda.Stream.cuda_stream`` handle. ``torch`` is always imported first so the library's
+``libamdhip64.so.7`` / ``librccl.so.1`` dependencies bind to the copies torch already loaded (one HIP
+runtime per process).
+
+On a machine with a GPU, a missing or stale library is an error (``require()`` raises): GPU code
+paths never fall back silently to PyTorch.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import torch  # noqa: F401  (must be loaded before the native library)
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native",
+                         "libgadmm_native.so")
+_lib: Optional[ctypes.CDLL] = None
+_load_error: Optional[str] = None
+
+c_int, c_long, c_double, c_void_p, c_char_p = ctypes.c_int, ctypes.c_long, ctypes.c_double, ctypes.c_void_p, ctypes.c_char_p
+c_longlong = ctypes.c_longlong
+
+
+class PhaseSlot(ctypes.Structure):
+    _fields_ = [("li", c_int), ("gid", c_int), ("left", c_int), ("right", c_int)]
+
+
+class XchgOp(ctypes.Structure):
+    _fields_ = [("peer", c_int), ("row", c_int), ("is_send", c_int), ("count", c_int)]
+
+
+class ChainCtl(ctypes.Structure):
+    _fields_ = [("iter", c_int), ("done", c_int), ("conv_iter", c_int), ("pending", c_int),
+                ("ticket", ctypes.c_uint), ("monitored", c_int), ("pad", c_int * 2)]
+
+
+class PhaseArgs(ctypes.Structure):
+    _fields_ = [
+        ("d", c_int), ("n_slots", c_int), ("n_local", c_int), ("nvar", c_int),
+        ("deg_to_var", c_int * 3),
+        ("flags", c_int), ("model", c_int),
+        ("slots", c_void_p), ("Minv", c_void_p), ("A", c_void_p), ("b", c_void_p), ("yy", c_void_p),
+        ("mu", c_void_p), ("theta", c_void_p),
+        ("rho", c_double),
+        ("objw", c_void_p), ("ctl", c_void_p), ("trace", c_void_p), ("part", c_void_p),
+        ("ring", c_int), ("max_iter", c_int),
+        ("obj0", c_double), ("tol", c_double),
+        ("X", c_void_p), ("Y", c_void_p),
+        ("m", c_int), ("max_inner", c_int),
+        ("lam", c_double), ("step", c_double), ("inner_tol", c_double),
+        ("inner_iters", c_void_p),
+    ]
+
+
+class EngineDesc(ctypes.Structure):
+    _fields_ = [("base", PhaseArgs), ("d_slots", c_void_p), ("reduced", c_void_p), ("comm", c_void_p),
+                ("stream", c_void_p), ("nranks", c_int)]
+
+
+class RunStats(ctypes.Structure):
+    _fields_ = [("iters", c_int), ("done", c_int), ("iterations_launched", c_int), ("replays", c_int),
+                ("wall_ms", c_double), ("p2p_bytes", c_longlong), ("p2p_msgs", c_longlong),
+                ("monitor_bytes", c_longlong)]
+
+
+MODEL_LINEAR, MODEL_LOGISTIC = 0, 1
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    sig = {
+        "gadmm_last_error": (c_char_p, []),
+        "gadmm_native_version": (c_int, []),
+        "gadmm_device_info": (c_int, [c_int, c_char_p, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_longlong),
+                                      ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+        "gadmm_gram_f64": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p]),
+        "gadmm_gram_workspace": (c_long, [c_int, c_int, c_int, c_int]),
+        "gadmm_gram_pick_ksplit": (c_int, [c_int, c_int, c_int]),
+        "gadmm_spd_inverse_small_f64": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                                c_void_p]),
+        "gadmm_chain_phase": (c_int, [ctypes.POINTER(PhaseArgs), c_void_p]),
+        "gadmm_chain_reset": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+        "gadmm_chain_engine_create": (c_void_p, [ctypes.POINTER(EngineDesc)]),
+        "gadmm_chain_engine_destroy": (None, [c_void_p]),
+        "gadmm_chain_engine_set_plan": (c_int, [c_void_p, c_int, ctypes.POINTER(PhaseSlot), c_int,
+                                                ctypes.POINTER(PhaseSlot), c_int, ctypes.POINTER(XchgOp), c_int,
+                                                ctypes.POINTER(XchgOp)]),
+        "gadmm_chain_engine_set_scalars": (c_int, [c_void_p, c_double, c_double, c_double, c_int]),
+        "gadmm_chain_engine_reset": (c_int, [c_void_p, c_int, c_int]),
+        "gadmm_chain_engine_flush": (c_int, [c_void_p]),
+        "gadmm_chain_engine_run": (c_int, [c_void_p, c_int, c_int, c_int, ctypes.POINTER(RunStats)]),
+        "gadmm_chain_engine_graph_ok": (c_int, [c_void_p]),
+        "gadmm_rccl_unique_id": (c_int, [ctypes.c_char_p]),
+        "gadmm_rccl_version": (c_int, []),
+        "gadmm_rccl_init": (c_void_p, [ctypes.c_char_p, c_int, c_int, c_int]),
+        "gadmm_rccl_destroy": (c_int, [c_void_p]),
+        "gadmm_rccl_exchange_rows": (c_int, [c_void_p, ctypes.POINTER(XchgOp), c_int, c_void_p, c_int, c_void_p]),
+        "gadmm_rccl_allreduce_sum_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_void_p]),
+        "gadmm_rccl_reduce_sum_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_int, c_void_p]),
+        "gadmm_rccl_bcast_f64": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p]),
+        "gadmm_rccl_counters": (c_int, [c_void_p, ctypes.POINTER(c_longlong)]),
+        "gadmm_rccl_reset_counters": (c_int, [c_void_p]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            continue
+        fn.restype = res
+        fn.argtypes = args
+
+
+def library_path() -> str:
+    return _LIB_PATH
+
+
+def load(build_if_missing: bool = True) -> Optional[ctypes.CDLL]:
+    """Load (building first when missing/stale and a toolchain is available)."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    try:
+        if build_if_missing:
+            from .. import _build
+            try:
+                _build.build(verbose=False)
+            except Exception as e:  # toolchain missing: fine if a built library exists
+                if not os.path.exists(_LIB_PATH):
+                    raise RuntimeError("native build failed: %s" % e)
+        lib = ctypes.CDLL(_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        _declare(lib)
+        _lib = lib
+    except Exception as e:  # pragma: no cover - depends on the box
+        _load_error = str(e)
+        _lib = None
+    return _lib
+
+
+def available() -> bool:
+    return load() is not None
+
+
+def require() -> ctypes.CDLL:
+    lib = load()
+    if lib is None:
+        raise RuntimeError("gadmm_amd native library unavailable (%s): build it with "
+                           "`python -m gadmm_amd._build`" % _load_error)
+    return lib
+
+
+def check(rc: int, what: str = "native call") -> None:
+    if rc != 0:
+        msg = require().gadmm_last_error()
+        raise RuntimeError("%s failed (rc=%d): %s" % (what, rc, msg.decode() if msg else "?"))
+
+
+def ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    if t is None:
+        return None
+    return t.data_ptr()
+
+
+def stream_handle(stream: Optional[torch.cuda.Stream] = None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream

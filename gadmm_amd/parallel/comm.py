@@ -1,0 +1,286 @@
+"""Communication backends behind one small interface (SURVEY.md §2.6 call-site inventory).
+
+* ``LocalComm``   — one rank owns every logical worker; neighbour "messages" are reads of the local
+  theta table (the analogue of the reference's column reads, ``out(:,ii-1)``), but bytes and
+  message counts are still recorded as if each logical worker were its own node.
+* ``TorchDistComm`` — ``torch.distributed`` point-to-point + collectives. With the ``gloo`` backend
+  this is the CPU plumbing config of BASELINE.json (configs[0]); with ``nccl`` (= RCCL on ROCm) it
+  runs on MI355X ranks.
+* ``RcclComm``    — the native RCCL communicator of ``libgadmm_native`` (one ``ncclComm_t`` per
+  process, ops enqueued on a HIP stream, capturable into the engine's hipGraph). Fast path on GPU.
+
+All exchange APIs move *rows of a row-major table* (theta or Z, shape (N_total, d)) so the same plan
+(``topology.chain_plan``) drives every backend.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+Op = Tuple[int, int, int]  # (peer, row, is_send)
+
+
+class CommStats:
+    def __init__(self):
+        self.bytes_sent = 0
+        self.bytes_recv = 0
+        self.msgs_sent = 0
+        self.coll_bytes = 0
+
+    def as_dict(self):
+        return {"bytes_sent": self.bytes_sent, "bytes_recv": self.bytes_recv, "msgs_sent": self.msgs_sent,
+                "coll_bytes": self.coll_bytes}
+
+
+class Comm:
+    rank: int = 0
+    nranks: int = 1
+    backend: str = "base"
+
+    def __init__(self):
+        self.stats = CommStats()
+
+    # point to point on table rows
+    def exchange_rows(self, table: torch.Tensor, ops: Sequence[Op]) -> None:
+        raise NotImplementedError
+
+    def send_tensor(self, t: torch.Tensor, peer: int) -> None:
+        raise NotImplementedError
+
+    def recv_tensor(self, t: torch.Tensor, peer: int) -> None:
+        raise NotImplementedError
+
+    # collectives
+    def allreduce_sum(self, t: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError
+
+    def reduce_sum(self, t: torch.Tensor, root: int) -> torch.Tensor:
+        raise NotImplementedError
+
+    def broadcast(self, t: torch.Tensor, root: int) -> torch.Tensor:
+        raise NotImplementedError
+
+    def barrier(self) -> None:
+        pass
+
+    def allreduce_max_scalar(self, v: float) -> float:
+        t = torch.tensor([float(v)], dtype=torch.float64)
+        return float(self._allreduce_max(t).item())
+
+    def _allreduce_max(self, t):
+        return t
+
+
+class LocalComm(Comm):
+    backend = "local"
+
+    def __init__(self):
+        super().__init__()
+        self.rank, self.nranks = 0, 1
+
+    def exchange_rows(self, table, ops):
+        if ops:
+            raise RuntimeError("LocalComm cannot exchange with peers")
+
+    def send_tensor(self, t, peer):
+        raise RuntimeError("LocalComm has no peers")
+
+    recv_tensor = send_tensor
+
+    def allreduce_sum(self, t):
+        return t
+
+    def reduce_sum(self, t, root):
+        return t
+
+    def broadcast(self, t, root):
+        return t
+
+
+class TorchDistComm(Comm):
+    """torch.distributed backend (gloo on CPU, nccl/RCCL on GPU)."""
+
+    def __init__(self, group=None):
+        super().__init__()
+        if not dist.is_initialized():
+            raise RuntimeError("torch.distributed is not initialised")
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.nranks = dist.get_world_size(group)
+        self.backend = "torch-" + str(dist.get_backend(group))
+
+    def exchange_rows(self, table, ops):
+        if not ops:
+            return
+        p2p = []
+        recv_bufs = []
+        for peer, row, snd in ops:
+            if snd:
+                buf = table[row].contiguous()
+                p2p.append(dist.P2POp(dist.isend, buf, peer, self.group))
+                self.stats.bytes_sent += buf.numel() * buf.element_size()
+                self.stats.msgs_sent += 1
+            else:
+                buf = torch.empty_like(table[row])
+                recv_bufs.append((row, buf))
+                p2p.append(dist.P2POp(dist.irecv, buf, peer, self.group))
+                self.stats.bytes_recv += buf.numel() * buf.element_size()
+        for r in dist.batch_isend_irecv(p2p):
+            r.wait()
+        for row, buf in recv_bufs:
+            table[row].copy_(buf)
+
+    def send_tensor(self, t, peer):
+        t = t.contiguous()
+        dist.send(t, peer, group=self.group)
+        self.stats.bytes_sent += t.numel() * t.element_size()
+        self.stats.msgs_sent += 1
+
+    def recv_tensor(self, t, peer):
+        buf = torch.empty_like(t)
+        dist.recv(buf, peer, group=self.group)
+        t.copy_(buf)
+        self.stats.bytes_recv += t.numel() * t.element_size()
+
+    def allreduce_sum(self, t):
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+        self.stats.coll_bytes += t.numel() * t.element_size()
+        return t
+
+    def reduce_sum(self, t, root):
+        dist.reduce(t, dst=root, op=dist.ReduceOp.SUM, group=self.group)
+        self.stats.coll_bytes += t.numel() * t.element_size()
+        return t
+
+    def broadcast(self, t, root):
+        dist.broadcast(t, src=root, group=self.group)
+        self.stats.coll_bytes += t.numel() * t.element_size()
+        return t
+
+    def barrier(self):
+        dist.barrier(group=self.group)
+
+    def _allreduce_max(self, t):
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return t
+
+
+class RcclComm(Comm):
+    """Native RCCL communicator (libgadmm_native). The unique id travels over an existing
+    torch.distributed group (the gloo control plane)."""
+
+    backend = "rccl"
+
+    def __init__(self, device: torch.device, control_group=None):
+        super().__init__()
+        from ..ops import native
+
+        self.lib = native.require()
+        self.native = native
+        self.rank = dist.get_rank(control_group)
+        self.nranks = dist.get_world_size(control_group)
+        self.device = torch.device(device)
+        idbuf = ctypes.create_string_buffer(128)
+        if self.rank == 0:
+            native.check(self.lib.gadmm_rccl_unique_id(idbuf), "rccl_unique_id")
+        obj = [bytes(idbuf.raw)]
+        dist.broadcast_object_list(obj, src=0, group=control_group)
+        idbytes = ctypes.create_string_buffer(obj[0], 128)
+        self.control_group = control_group
+        self.handle = self.lib.gadmm_rccl_init(idbytes, self.nranks, self.rank, self.device.index or 0)
+        if not self.handle:
+            native.check(-1, "rccl_init")
+
+    def _stream(self):
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def exchange_rows(self, table, ops):
+        if not ops:
+            return
+        arr = (self.native.XchgOp * len(ops))()
+        for i, (peer, row, snd) in enumerate(ops):
+            arr[i].peer, arr[i].row, arr[i].is_send, arr[i].count = peer, row, snd, 0
+        d = table.shape[1]
+        self.native.check(self.lib.gadmm_rccl_exchange_rows(self.handle, arr, len(ops), table.data_ptr(), d,
+                                                            self._stream()), "rccl_exchange_rows")
+        for peer, row, snd in ops:
+            if snd:
+                self.stats.bytes_sent += d * 8
+                self.stats.msgs_sent += 1
+            else:
+                self.stats.bytes_recv += d * 8
+
+    def send_tensor(self, t, peer):
+        self._raw([(peer, 1, t)])
+
+    def recv_tensor(self, t, peer):
+        self._raw([(peer, 0, t)])
+
+    def _raw(self, items):
+        n = len(items)
+        peers = (ctypes.c_int * n)(*[p for p, _, _ in items])
+        sends = (ctypes.c_int * n)(*[s for _, s, _ in items])
+        bufs = (ctypes.c_void_p * n)(*[t.data_ptr() for _, _, t in items])
+        counts = (ctypes.c_long * n)(*[t.numel() for _, _, t in items])
+        fn = self.lib.gadmm_rccl_sendrecv_raw
+        fn.restype = ctypes.c_int
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
+                       ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_long), ctypes.c_void_p]
+        self.native.check(fn(self.handle, n, peers, sends, bufs, counts, self._stream()), "rccl_sendrecv")
+        for p, s, t in items:
+            if s:
+                self.stats.bytes_sent += t.numel() * 8
+                self.stats.msgs_sent += 1
+            else:
+                self.stats.bytes_recv += t.numel() * 8
+
+    def allreduce_sum(self, t):
+        self.native.check(self.lib.gadmm_rccl_allreduce_sum_f64(self.handle, t.data_ptr(), t.data_ptr(), t.numel(),
+                                                                self._stream()), "rccl_allreduce")
+        self.stats.coll_bytes += t.numel() * 8
+        return t
+
+    def reduce_sum(self, t, root):
+        self.native.check(self.lib.gadmm_rccl_reduce_sum_f64(self.handle, t.data_ptr(), t.data_ptr(), t.numel(), root,
+                                                             self._stream()), "rccl_reduce")
+        self.stats.coll_bytes += t.numel() * 8
+        return t
+
+    def broadcast(self, t, root):
+        self.native.check(self.lib.gadmm_rccl_bcast_f64(self.handle, t.data_ptr(), t.numel(), root, self._stream()),
+                          "rccl_bcast")
+        self.stats.coll_bytes += t.numel() * 8
+        return t
+
+    def barrier(self):
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=self.control_group)
+
+    def _allreduce_max(self, t):
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.control_group)
+        return t
+
+    def close(self):
+        if getattr(self, "handle", None):
+            self.lib.gadmm_rccl_destroy(self.handle)
+            self.handle = None
+
+
+def init_distributed(backend: Optional[str] = None):
+    """Initialise torch.distributed from torchrun-style env vars (MASTER_ADDR defaults to 127.0.0.1).
+    Returns (rank, world_size, local_rank)."""
+    if dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29511")
+    if backend is None:
+        backend = "gloo"
+    dist.init_process_group(backend=backend, rank=rank, world_size=world)
+    return rank, world, local_rank

@@ -1,0 +1,237 @@
+"""Communication topologies: chain (GADMM / D-GADMM), star (parameter server), node geometry.
+
+Reference components:
+
+* ``find_path``  — ``findPath.m``: N nodes uniform in a 50x50 square, greedy nearest-unvisited chain
+  from node 1, hop cost = squared distance.
+* ``find_path2`` — ``findPath2.m``: nodes in 250x250, radio-energy hop cost
+  ``P(n,m) = d^2 * eta * B * 2^(R/B)``; also the star energies ``P_central(n) = 1/2 d_c^2 eta B 2^(2R/B)``
+  towards the node nearest the area centre.
+* ``calc_cost``  — ``calc_cost.m``: cost of a fixed chain under a new geometry.
+
+The reference draws positions with MATLAB's unseeded ``rand``; here every draw comes from an explicit
+``numpy.random.Generator`` so all ranks (and tests) reproduce the same paths without messages
+("all ranks use a shared seeded RNG, with no message").
+
+Indices are 0-based throughout (reference worker ``ii`` == our worker ``ii-1``).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+ETA = 1e-6
+RATE = 10e6
+BANDWIDTH = 2e6
+
+
+@dataclass
+class Geometry:
+    x: np.ndarray
+    y: np.ndarray
+
+    @property
+    def d_square(self) -> np.ndarray:
+        dx = self.x[:, None] - self.x[None, :]
+        dy = self.y[:, None] - self.y[None, :]
+        d2 = dx * dx + dy * dy
+        np.fill_diagonal(d2, 0.0)
+        return d2
+
+
+def random_geometry(n: int, side: float, rng: np.random.Generator) -> Geometry:
+    """Node positions; the reference draws x(n) then y(n) per node (findPath.m:3-6)."""
+    xy = rng.random((n, 2)) * side
+    return Geometry(x=xy[:, 0].copy(), y=xy[:, 1].copy())
+
+
+def greedy_chain(d_square: np.ndarray, start: int = 0) -> List[int]:
+    """Greedy nearest-unvisited path from ``start`` (findPath.m:16-30). Ties -> lowest index."""
+    n = d_square.shape[0]
+    path = [start]
+    visited = np.zeros(n, dtype=bool)
+    visited[start] = True
+    while len(path) < n:
+        cur = path[-1]
+        row = np.where(visited, np.inf, d_square[cur])
+        row[cur] = np.inf
+        nxt = int(np.argmin(row))
+        path.append(nxt)
+        visited[nxt] = True
+    return path
+
+
+def find_path(n: int, rng: np.random.Generator) -> Tuple[List[int], np.ndarray, np.ndarray]:
+    """``[path, pathCost, d_square] = findPath(N)``: squared-distance hop costs, 50x50 area."""
+    g = random_geometry(n, 50.0, rng)
+    d2 = g.d_square
+    path = greedy_chain(d2)
+    cost = np.array([d2[path[k], path[k + 1]] for k in range(n - 1)])
+    return path, cost, d2
+
+
+def link_energy(d2: np.ndarray) -> np.ndarray:
+    return d2 * ETA * BANDWIDTH * 2.0 ** (RATE / BANDWIDTH)
+
+
+def find_path2(n: int, rng: np.random.Generator):
+    """``[path, pathCost, d_square, P_central, center] = findPath2(N)`` (radio-energy costs)."""
+    side = 250.0
+    g = random_geometry(n, side, rng)
+    dist_c = np.sqrt((g.x - side / 2) ** 2 + (g.y - side / 2) ** 2)
+    center = int(np.argmin(dist_c))
+    d2c = (g.x - g.x[center]) ** 2 + (g.y - g.y[center]) ** 2
+    p_central = 0.5 * d2c * ETA * BANDWIDTH * 2.0 ** (2 * RATE / BANDWIDTH)
+    d2 = g.d_square
+    P = link_energy(d2)
+    path = greedy_chain(d2)
+    cost = np.array([P[path[k], path[k + 1]] for k in range(n - 1)])
+    return path, cost, d2, p_central, center
+
+
+def calc_cost(grid: np.ndarray, path0: Sequence[int]) -> np.ndarray:
+    """Hop costs of the fixed chain ``path0`` under geometry ``grid`` (calc_cost.m:1-10)."""
+    return np.array([grid[path0[k], path0[k + 1]] for k in range(len(path0) - 1)])
+
+
+def star_cost(p_central: np.ndarray) -> float:
+    """Per-iteration star energy = uplink sum + downlink max (LinearRegression_gadmm_vs_admm.m:84-87)."""
+    return float(np.sum(p_central) + np.max(p_central))
+
+
+def rechain_iteration(it: int, coherence: float) -> bool:
+    """D-GADMM refresh rule ``i > 1 && mod(i, coherence_Time) == 0`` (dynamic_group_ADMM_closedForm.m:18)."""
+    if coherence is None or coherence <= 0 or not np.isfinite(coherence):
+        return False
+    c = int(coherence)
+    return it > 1 and c > 0 and it % c == 0
+
+
+class PathSchedule:
+    """Deterministic sequence of chains for D-GADMM.
+
+    ``kind='findPath2'`` re-draws a geometry and greedy chain at every refresh (the reference's
+    ``dynamic_group_ADMM_closedForm.m:20``); ``kind='matrix'`` consumes pre-generated rows
+    (``dynamic_group_ADMM_closedForm_v0.m:16-26``).
+    """
+
+    def __init__(self, n: int, initial_path: Sequence[int], initial_cost: Sequence[float], coherence: float,
+                 kind: str = "findPath2", seed: int = 1234, path_matrix=None, cost_matrix=None):
+        self.n = n
+        self.coherence = coherence
+        self.kind = kind
+        self.rng = np.random.default_rng(seed)
+        self.path = list(initial_path)
+        self.cost = np.asarray(initial_cost, dtype=np.float64)
+        self.path_matrix = path_matrix
+        self.cost_matrix = cost_matrix
+        self.k = 1  # next row of the matrices
+
+    def step(self, it: int) -> bool:
+        """Advance to iteration ``it``; returns True if the chain changed."""
+        if not rechain_iteration(it, self.coherence):
+            return False
+        if self.kind == "matrix":
+            self.path = list(self.path_matrix[self.k])
+            self.cost = np.asarray(self.cost_matrix[self.k])
+            self.k += 1
+        elif self.kind == "findPath":
+            p, c, _ = find_path(self.n, self.rng)
+            self.path, self.cost = p, c
+        else:
+            p, c, _, _, _ = find_path2(self.n, self.rng)
+            self.path, self.cost = p, c
+        return True
+
+
+# -------------------------------------------------------------------------------------------------
+# Placement and per-rank phase plans
+# -------------------------------------------------------------------------------------------------
+
+@dataclass
+class Placement:
+    """Logical worker -> rank map. Default: contiguous blocks of workers per rank (so a static
+    identity chain crosses a device boundary only at segment ends)."""
+
+    owner: np.ndarray          # (N,) rank of each global worker
+    nranks: int
+
+    @staticmethod
+    def contiguous(n_workers: int, nranks: int) -> "Placement":
+        if nranks > n_workers:
+            raise ValueError("more ranks (%d) than workers (%d)" % (nranks, n_workers))
+        base, extra = divmod(n_workers, nranks)
+        owner = []
+        for r in range(nranks):
+            owner += [r] * (base + (1 if r < extra else 0))
+        return Placement(owner=np.asarray(owner, dtype=np.int64), nranks=nranks)
+
+    def local_workers(self, rank: int) -> List[int]:
+        return [int(w) for w in np.nonzero(self.owner == rank)[0]]
+
+    def local_index(self, rank: int) -> Dict[int, int]:
+        return {w: i for i, w in enumerate(self.local_workers(rank))}
+
+
+@dataclass
+class Slot:
+    li: int
+    gid: int
+    left: int
+    right: int
+
+
+@dataclass
+class RankPlan:
+    head: List[Slot] = field(default_factory=list)
+    tail: List[Slot] = field(default_factory=list)
+    # (peer, row, is_send) messages after the head / tail phase
+    xchg_head: List[Tuple[int, int, int]] = field(default_factory=list)
+    xchg_tail: List[Tuple[int, int, int]] = field(default_factory=list)
+
+    def send_rows(self) -> int:
+        return sum(1 for _, _, s in self.xchg_head if s) + sum(1 for _, _, s in self.xchg_tail if s)
+
+
+def chain_plan(path: Sequence[int], placement: Placement, rank: int) -> RankPlan:
+    """Head/tail slots of ``rank`` for the chain ``path`` (position -> worker) and the neighbour
+    messages that must cross ranks after each phase.
+
+    Heads are chain positions 0, 2, 4, ... (MATLAB ``jj = 1:2:N``), tails 1, 3, 5, ...
+    After the head phase every head sends its fresh theta to each neighbour that lives on another
+    rank (C2); after the tail phase every tail does the same (C1). One message per (worker, peer
+    rank) pair even when both neighbours live on the same peer.
+    """
+    n = len(path)
+    lidx = placement.local_index(rank)
+    plan = RankPlan()
+    for pos, w in enumerate(path):
+        left = path[pos - 1] if pos > 0 else -1
+        right = path[pos + 1] if pos < n - 1 else -1
+        phase_is_head = (pos % 2 == 0)
+        if w in lidx:
+            s = Slot(li=lidx[w], gid=int(w), left=int(left), right=int(right))
+            (plan.head if phase_is_head else plan.tail).append(s)
+        # messages
+        owner_w = int(placement.owner[w])
+        peers = sorted({int(placement.owner[u]) for u in (left, right) if u >= 0} - {owner_w})
+        lst = plan.xchg_head if phase_is_head else plan.xchg_tail
+        for p in peers:
+            if owner_w == rank:
+                lst.append((p, int(w), 1))
+            elif p == rank:
+                lst.append((owner_w, int(w), 0))
+    return plan
+
+
+def chain_message_count(path: Sequence[int], placement: Placement) -> int:
+    """Total cross-rank messages per GADMM iteration for ``path`` (all ranks)."""
+    total = 0
+    for pos, w in enumerate(path):
+        nb = [path[pos - 1]] if pos > 0 else []
+        if pos < len(path) - 1:
+            nb.append(path[pos + 1])
+        total += len({int(placement.owner[u]) for u in nb} - {int(placement.owner[w])})
+    return total
