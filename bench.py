@@ -1,0 +1,161 @@
+"""Headline benchmark: wall-clock and communication bytes to a 1e-8 objective gap (BASELINE.json).
+
+Config (BASELINE.json configs[1], BASELINE.md "GADMM lin-syn iterations to 1e-8"): the
+LinearRegression_Synthetic problem of the reference — N = 24 logical workers, d = 50 features,
+m = 50 samples per worker, X_n = 1.3^(n-1) q_n q_n^T + I (rebuilt from the reference's shipped
+inputData.mat), closed-form local solves, GADMM with rho = 3, stop at |obj - obj0| < 1e-8.
+The 24 workers form one chain laid over the N GPUs in contiguous segments (24/N workers per GPU);
+boundary theta crosses GPUs by RCCL send/recv over xGMI. Total work is fixed as N grows
+(strong scaling).
+
+One *step* = one complete solve from the raw shards already resident on the GPU: Gram + b + y^T y
+(f64 MFMA), cached inverses (A + c rho I)^{-1}, then GADMM iterations from theta = mu = 0 until the
+device-side stopping rule fires (1373 iterations at rho = 3, checked against the reference count).
+`value` is seconds per solve (lower is better); `vs_baseline` = value / 1.13 s, the CPU wall time
+of the same loop ([measured-here] row).
+
+    python bench.py                      # 1 GPU
+    torchrun --nproc-per-node 8 bench.py --gpus 8
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+BASELINE_S = 1.13  # CPU wall time of the GADMM loop to 1e-8, rho = 3
+EXPECTED_ITERS = {3.0: 1373, 5.0: 758, 7.0: 428}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--rho", type=float, default=3.0)
+    ap.add_argument("--tol", type=float, default=1e-8)
+    ap.add_argument("--workers", type=int, default=24)
+    ap.add_argument("--block", type=int, default=0, help="iterations per graph replay (0: auto)")
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print("bench.py: --gpus %d needs a torchrun launch with %d processes" % (args.gpus, args.gpus),
+                  file=sys.stderr)
+            sys.exit(2)
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+
+    from gadmm_amd.data import linear_synthetic
+    from gadmm_amd.oracle.reference import opt_linear
+    from gadmm_amd.engine.chain_engine import NativeChainEngine
+    from gadmm_amd.parallel.topology import Placement, chain_message_count
+
+    comm = None
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from gadmm_amd.parallel.comm import RcclComm
+        comm = RcclComm(device)
+
+    ds = linear_synthetic(args.workers)
+    Xf, yf = ds.stacked()
+    obj0 = opt_linear(Xf.numpy(), yf.numpy())
+    placement = Placement.contiguous(args.workers, world)
+    local = placement.local_workers(rank)
+    X_loc = ds.X[local].to(device).contiguous()
+    y_loc = ds.y[local].to(device).contiguous()
+    block = args.block if args.block > 0 else (32 if world == 1 else 16)
+    max_iter = 20000
+    eng = NativeChainEngine(X_loc, y_loc, local, args.workers, "linear", rho=args.rho, obj0=obj0, tol=args.tol,
+                            max_iter=max_iter, comm=comm, block=block)
+    path = list(range(args.workers))
+    eng.set_path(path, placement, rank)
+
+    def barrier():
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+
+    def solve():
+        eng.refresh(X_loc, y_loc)
+        eng.reset()
+        return eng.run(use_graph=not args.no_graph)
+
+    runs = []
+    for _ in range(args.warmup):
+        runs.append(solve())
+    barrier()
+    t0 = time.perf_counter()
+    last = None
+    for _ in range(args.steps):
+        last = solve()
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    barrier()
+    ms = (t1 - t0) * 1e3 / max(args.steps, 1)
+    iters = last.iters if last is not None else 0
+    p2p = last.p2p_bytes if last is not None else 0
+    mon = last.monitor_bytes if last is not None else 0
+    if world > 1:
+        t = torch.tensor([ms, float(p2p), float(mon)], dtype=torch.float64)
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = t.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        ms = float(mx[0])
+        p2p, mon = int(sm[1]), int(sm[2])
+    tr = eng.objective_trace(iters)
+    gap = abs(float(tr[iters - 1]) - obj0) if iters > 0 else float("nan")
+    expect = EXPECTED_ITERS.get(float(args.rho)) if args.workers == 24 and args.tol == 1e-8 else None
+    if rank == 0:
+        value = ms / 1e3
+        out = {
+            "metric": "wall-clock to 1e-8 objective gap, GADMM linear regression (LinearRegression_Synthetic)",
+            "value": round(value, 6),
+            "unit": "s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": False,
+            "scaling": "strong",
+            "vs_baseline": round(value / BASELINE_S, 6),
+            "dtype": "fp64",
+            "data": "synthetic (reference LinearRegression_Synthetic design rebuilt from shipped inputData.mat)",
+            "config": {"model": "LinearRegression_Synthetic GADMM closed-form", "workers": args.workers,
+                       "features": ds.dim, "samples_per_worker": ds.rows_per_worker, "rho": args.rho,
+                       "tol": args.tol, "global_batch": args.workers * ds.rows_per_worker, "seq_len": 1,
+                       "parallelism": "chain%d-over-%dgpu" % (args.workers, world)},
+            "iterations_to_tol": iters,
+            "expected_iterations": expect,
+            "iterations_match_reference": (iters == expect) if expect else None,
+            "final_gap": gap,
+            "comm_bytes_per_solve": p2p,
+            "monitor_bytes_per_solve": mon,
+            "p2p_messages_per_iteration": chain_message_count(path, placement),
+            "us_per_iteration": round(ms * 1e3 / max(iters, 1), 3),
+            "graph": eng.graph_ok(),
+            "baseline_s": BASELINE_S,
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if comm is not None:
+        comm.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

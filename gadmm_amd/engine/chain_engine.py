@@ -133,14 +133,29 @@ class NativeChainEngine:
         self.plan: Optional[RankPlan] = None
 
     # ---------------------------------------------------------------------------------------------
-    def _build_inverses(self):
+    def _build_inverses(self, in_place: bool = False, check: bool = True):
         rho = self.rho
         if self.n_total == 1:
             shifts, self.deg_to_var = [0.0], (0, 0, 0)
         else:
             shifts, self.deg_to_var = [rho, 2.0 * rho], (0, 0, 1)
         self.nvar = len(shifts)
-        self.Minv = spd_inverse(self.A, torch.tensor(shifts, dtype=torch.float64, device=self.device))
+        sh = torch.tensor(shifts, dtype=torch.float64, device=self.device)
+        if in_place and self.Minv is not None:
+            spd_inverse(self.A, sh, out=self.Minv, check_status=check)
+        else:
+            self.Minv = spd_inverse(self.A, sh, check_status=check)
+
+    def refresh(self, X_loc: torch.Tensor, y_loc: torch.Tensor):
+        """Recompute the loop-invariant set-up (Gram + cached inverses) from the raw shards, in place
+        (device pointers, hence captured graphs, stay valid). No host synchronisation."""
+        with torch.cuda.stream(self.stream):
+            if self.model == "linear":
+                gram(X_loc, y_loc, out=(self.A, self.b, self.yy))
+                self._build_inverses(in_place=True, check=False)
+            else:
+                self.X.copy_(X_loc)
+                self.Y.copy_(y_loc)
 
     def set_rho(self, rho: float):
         """Change rho (re-inverts; the Gram is kept)."""

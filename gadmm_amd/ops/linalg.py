@@ -26,20 +26,29 @@ def gram_torch(X: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.Te
     return A, b, yy
 
 
-def gram(X: torch.Tensor, y: torch.Tensor, ksplit: Optional[int] = None
+def gram(X: torch.Tensor, y: torch.Tensor, ksplit: Optional[int] = None, out=None
          ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-    """Batched augmented Gram. ``X``: (N, m, d) f64 contiguous, ``y``: (N, m)."""
+    """Batched augmented Gram. ``X``: (N, m, d) f64 contiguous, ``y``: (N, m).
+    ``out``: optional preallocated ``(A, b, yy)`` written in place."""
     if X.dtype != torch.float64 or y.dtype != torch.float64:
         raise TypeError("gram expects float64")
     if not X.is_cuda:
-        return gram_torch(X, y)
+        res = gram_torch(X, y)
+        if out is not None:
+            for o, r in zip(out, res):
+                o.copy_(r)
+            return out
+        return res
     lib = native.require()
     X = X.contiguous()
     y = y.contiguous()
     N, m, d = X.shape
-    A = torch.empty((N, d, d), dtype=torch.float64, device=X.device)
-    b = torch.empty((N, d), dtype=torch.float64, device=X.device)
-    yy = torch.empty((N,), dtype=torch.float64, device=X.device)
+    if out is not None:
+        A, b, yy = out
+    else:
+        A = torch.empty((N, d, d), dtype=torch.float64, device=X.device)
+        b = torch.empty((N, d), dtype=torch.float64, device=X.device)
+        yy = torch.empty((N,), dtype=torch.float64, device=X.device)
     if ksplit is None:
         ksplit = int(lib.gadmm_gram_pick_ksplit(N, m, d))
     ws_n = int(lib.gadmm_gram_workspace(N, m, d, ksplit))
@@ -61,8 +70,9 @@ def spd_inverse_torch(A: torch.Tensor, shifts: torch.Tensor) -> torch.Tensor:
     return inv.reshape(N, V, d, d)
 
 
-def spd_inverse(A: torch.Tensor, shifts: torch.Tensor) -> torch.Tensor:
-    """``(N, V, d, d)`` inverses of ``A_n + shifts[n, v] I`` (all SPD)."""
+def spd_inverse(A: torch.Tensor, shifts: torch.Tensor, out: Optional[torch.Tensor] = None,
+                check_status: bool = True) -> torch.Tensor:
+    """``(N, V, d, d)`` inverses of ``A_n + shifts[n, v] I`` (all SPD); ``out`` written in place."""
     shifts = torch.as_tensor(shifts, dtype=torch.float64, device=A.device)
     if shifts.dim() == 1:
         shifts = shifts.unsqueeze(0).expand(A.shape[0], -1)
@@ -70,13 +80,18 @@ def spd_inverse(A: torch.Tensor, shifts: torch.Tensor) -> torch.Tensor:
     N, d, _ = A.shape
     V = shifts.shape[1]
     if not A.is_cuda or d > 128:
-        return spd_inverse_torch(A, shifts)
+        res = spd_inverse_torch(A, shifts)
+        if out is not None:
+            out.copy_(res)
+            return out
+        return res
     lib = native.require()
-    out = torch.empty((N, V, d, d), dtype=torch.float64, device=A.device)
+    if out is None:
+        out = torch.empty((N, V, d, d), dtype=torch.float64, device=A.device)
     status = torch.zeros((1,), dtype=torch.int32, device=A.device)
     rc = lib.gadmm_spd_inverse_small_f64(A.contiguous().data_ptr(), shifts.data_ptr(), N, d, V, out.data_ptr(),
                                          status.data_ptr(), native.stream_handle())
     native.check(rc, "spd_inverse_small_f64")
-    if int(status.item()) != 0:
+    if check_status and int(status.item()) != 0:
         raise FloatingPointError("spd_inverse: matrix is not positive definite")
     return out
