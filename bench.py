@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--workers", type=int, default=24)
     ap.add_argument("--block", type=int, default=0, help="iterations per graph replay (0: auto)")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--engine", choices=["auto", "persistent", "graph"], default="auto",
+                    help="auto: persistent single-launch kernel when eligible (1 GPU), else graph-replayed phases")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -88,9 +90,13 @@ def main():
         if world > 1:
             dist.barrier()
 
+    persistent = args.engine == "persistent" or (args.engine == "auto" and eng.persistent_eligible())
+
     def solve():
         eng.refresh(X_loc, y_loc)
         eng.reset()
+        if persistent:
+            return eng.run_persistent()
         return eng.run(use_graph=not args.no_graph)
 
     runs = []
@@ -146,7 +152,7 @@ def main():
             "monitor_bytes_per_solve": mon,
             "p2p_messages_per_iteration": chain_message_count(path, placement),
             "us_per_iteration": round(ms * 1e3 / max(iters, 1), 3),
-            "graph": eng.graph_ok(),
+            "engine": "persistent" if persistent else ("graph" if eng.graph_ok() and not args.no_graph else "eager"),
             "baseline_s": BASELINE_S,
         }
         print(json.dumps(out), flush=True)

@@ -131,6 +131,8 @@ class NativeChainEngine:
         if not self.handle:
             native.check(-1, "chain_engine_create")
         self.plan: Optional[RankPlan] = None
+        self.path: Optional[List[int]] = None
+        self._pbuf = None
 
     # ---------------------------------------------------------------------------------------------
     def _build_inverses(self, in_place: bool = False, check: bool = True):
@@ -191,6 +193,7 @@ class NativeChainEngine:
                 raise ValueError("placement/local_ids mismatch")
         self._install(plan)
         self.plan = plan
+        self.path = [int(w) for w in path]
 
     def _install(self, plan: RankPlan):
         def slots(lst):
@@ -235,6 +238,63 @@ class NativeChainEngine:
         native.check(rc, "chain_engine_run")
         return EngineRun(st.iters, st.done, st.iterations_launched, st.replays, st.wall_ms, st.p2p_bytes,
                          st.p2p_msgs, st.monitor_bytes)
+
+    # ---------------------------------------------------------------------------------------------
+    # Persistent single-launch solve (csrc/kernels/chain_persistent.hip)
+    def persistent_eligible(self) -> bool:
+        if self.nranks != 1 or self.model != "linear" or self.plan is None or self.path is None:
+            return False
+        if self.n_total + 1 > 256 or self.n_local != self.n_total:
+            return False
+        return int(self.lib.gadmm_chain_persistent_lds(self.d, self._obj_mode())) > 0
+
+    def _obj_mode(self) -> int:
+        # exact objective (second GEMV with the Gram in LDS) whenever both matrices fit in LDS
+        return 0 if int(self.lib.gadmm_chain_persistent_lds(self.d, 0)) > 0 else 1
+
+    def run_persistent(self, lag: int = 4, timeout_s: float = 20.0, start_iter: int = 1,
+                       pending_in: int = 0) -> EngineRun:
+        """Whole solve in one launch. State must be reset (``reset()``) or resumed by the caller."""
+        if not self.persistent_eligible():
+            raise RuntimeError("persistent kernel not eligible for this engine/config")
+        ring = lag + 4
+        dev = self.device
+        if getattr(self, "_pbuf", None) is None or self._pbuf[0] != ring:
+            with torch.cuda.stream(self.stream):
+                thg = torch.zeros((self.n_total * self.d * 4,), dtype=torch.int32, device=dev)
+                objg = torch.zeros((ring * self.n_total * 4,), dtype=torch.int32, device=dev)
+                decg = torch.zeros((ring,), dtype=torch.int64, device=dev)
+            self._pbuf = (ring, thg, objg, decg)
+        _, thg, objg, decg = self._pbuf
+        path_t = torch.tensor(self.path, dtype=torch.int32, device=dev)
+        pa = native.PersistArgs()
+        pa.d, pa.n, pa.start_iter, pa.max_iter = self.d, self.n_total, int(start_iter), self.max_iter
+        pa.lag, pa.ring, pa.nvar, pa.obj_mode = int(lag), ring, self.nvar, self._obj_mode()
+        for i, v in enumerate(self.deg_to_var):
+            pa.deg_to_var[i] = v
+        pa.pending_in = int(pending_in)
+        pa.rho, pa.obj0, pa.tol = self.rho, self.obj0, self.tol
+        pa.timeout_ticks = int(timeout_s * 1e8)
+        pa.path = path_t.data_ptr()
+        pa.Minv, pa.A, pa.b, pa.yy = self.Minv.data_ptr(), self.A.data_ptr(), self.b.data_ptr(), self.yy.data_ptr()
+        pa.theta, pa.mu = self.theta.data_ptr(), self.mu.data_ptr()
+        pa.thg, pa.objg, pa.decg = thg.data_ptr(), objg.data_ptr(), decg.data_ptr()
+        pa.trace, pa.ctl = self.trace.data_ptr(), self.ctl.data_ptr()
+        import time as _time
+        with torch.cuda.stream(self.stream):
+            thg.zero_()
+            objg.zero_()
+            decg.zero_()
+            t0 = _time.perf_counter()
+            native.check(self.lib.gadmm_chain_persistent_launch(ctypes.byref(pa), self.stream.cuda_stream),
+                         "chain_persistent_launch")
+            self.stream.synchronize()
+            t1 = _time.perf_counter()
+        c = self.ctl.cpu().tolist()
+        done, conv, nxt = c[1], c[2], c[0]
+        if done == 4:
+            raise RuntimeError("persistent chain kernel timed out (hand-off never completed)")
+        return EngineRun(conv, done, nxt - start_iter, 1, (t1 - t0) * 1e3, 0, 0, 0)
 
     def graph_ok(self) -> bool:
         return bool(self.lib.gadmm_chain_engine_graph_ok(self.handle))

@@ -67,6 +67,17 @@ class RunStats(ctypes.Structure):
                 ("monitor_bytes", c_longlong)]
 
 
+class PersistArgs(ctypes.Structure):
+    _fields_ = [
+        ("d", c_int), ("n", c_int), ("start_iter", c_int), ("max_iter", c_int), ("lag", c_int), ("ring", c_int),
+        ("nvar", c_int), ("obj_mode", c_int), ("deg_to_var", c_int * 3), ("pending_in", c_int),
+        ("rho", c_double), ("obj0", c_double), ("tol", c_double), ("timeout_ticks", c_longlong),
+        ("path", c_void_p), ("Minv", c_void_p), ("A", c_void_p), ("b", c_void_p), ("yy", c_void_p),
+        ("theta", c_void_p), ("mu", c_void_p), ("thg", c_void_p), ("objg", c_void_p), ("decg", c_void_p),
+        ("trace", c_void_p), ("ctl", c_void_p),
+    ]
+
+
 MODEL_LINEAR, MODEL_LOGISTIC = 0, 1
 
 
@@ -94,6 +105,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_chain_engine_flush": (c_int, [c_void_p]),
         "gadmm_chain_engine_run": (c_int, [c_void_p, c_int, c_int, c_int, ctypes.POINTER(RunStats)]),
         "gadmm_chain_engine_graph_ok": (c_int, [c_void_p]),
+        "gadmm_chain_persistent_lds": (c_long, [c_int, c_int]),
+        "gadmm_chain_persistent_launch": (c_int, [ctypes.POINTER(PersistArgs), c_void_p]),
         "gadmm_rccl_unique_id": (c_int, [ctypes.c_char_p]),
         "gadmm_rccl_version": (c_int, []),
         "gadmm_rccl_init": (c_void_p, [ctypes.c_char_p, c_int, c_int, c_int]),

@@ -58,3 +58,18 @@ for rho, want in ((2e-4, 53), (3e-4, 274)):
     torch.cuda.synchronize(); t0 = time.perf_counter(); r = eng.run(); torch.cuda.synchronize()
     print("logistic rho", rho, "iters", r.iters, "want", want, "ms", round((time.perf_counter() - t0) * 1e3, 3), flush=True)
 print("OK")
+# persistent
+for rho, e4, e8 in ((3, 784, 1373), (5, 434, 758), (7, 248, 428)):
+    eng = NativeChainEngine(X, y, list(range(24)), 24, "linear", rho=rho, obj0=obj0, tol=1e-4, max_iter=3000, block=16)
+    eng.set_path(list(range(24)), pl, 0)
+    eng.reset(); r4 = eng.run_persistent()
+    eng.set_targets(obj0, 1e-8)
+    best = 1e9
+    for k in range(5):
+        eng.reset(); torch.cuda.synchronize(); t0 = time.perf_counter(); r8 = eng.run_persistent(); torch.cuda.synchronize(); best = min(best, time.perf_counter() - t0)
+    tr = eng.objective_trace(r8.iters)
+    ref = R.gadmm_linear(ds.X.numpy(), ds.y.numpy(), rho, 40, obj0, 1e-30)
+    print("persistent rho", rho, "iters", r4.iters, r8.iters, "want", e4, e8, "best ms", round(best * 1e3, 3),
+          "us/iter", round(best * 1e6 / r8.iters, 3), "trace diff", np.max(np.abs(tr[:40] - np.array(ref.obj)) / np.abs(np.array(ref.obj))), flush=True)
+    eng.close()
+print("OK2")
