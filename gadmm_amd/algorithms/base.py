@@ -1,0 +1,95 @@
+"""Run results and small helpers shared by every algorithm."""
+from __future__ import annotations
+
+import time
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+
+
+@dataclass
+class RunResult:
+    """What every algorithm returns (the reference's ``[obj, loss, Iter, time(, com_cost)]`` plus
+    the communication accounting the MI355X build adds).
+
+    * ``obj``/``loss``: per-iteration global objective and ``|obj - obj0|`` (reference arrays);
+    * ``iters``: the reference ``Iter`` (first iteration with loss < acc, else the budget);
+    * ``comm_units``: cumulative reference communication units per iteration (1 per worker
+      transmission: GADMM ``iter*N``, GD ``iter*N + iter``, LAG ``uploads + iter``;
+      LinearRegression_Synthetic.m:100-142);
+    * ``com_cost``: cumulative energy/distance cost where the reference tracks one (D-GADMM, E7);
+    * ``wall_s``/``time_trace``: real wall clock (cumulative per iteration);
+    * ``bytes_sent``: actual bytes this rank put on the fabric; ``bytes_total`` summed over ranks.
+    """
+
+    algorithm: str
+    obj: np.ndarray
+    loss: np.ndarray
+    iters: int
+    converged: bool
+    wall_s: float
+    time_trace: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    comm_units: np.ndarray = field(default_factory=lambda: np.zeros(0))
+    com_cost: Optional[np.ndarray] = None
+    bytes_sent: int = 0
+    bytes_total: int = 0
+    extra: Dict[str, Any] = field(default_factory=dict)
+    theta: Optional[np.ndarray] = None
+
+    def summary(self) -> Dict[str, Any]:
+        return {
+            "algorithm": self.algorithm,
+            "iters": int(self.iters),
+            "converged": bool(self.converged),
+            "final_obj": float(self.obj[self.iters - 1]) if self.iters > 0 and len(self.obj) >= self.iters else None,
+            "final_loss": float(self.loss[self.iters - 1]) if self.iters > 0 and len(self.loss) >= self.iters else None,
+            "wall_s": float(self.wall_s),
+            "comm_units": float(self.comm_units[self.iters - 1]) if len(self.comm_units) >= self.iters > 0 else None,
+            "bytes_sent": int(self.bytes_sent),
+            "bytes_total": int(self.bytes_total),
+            **{k: v for k, v in self.extra.items() if isinstance(v, (int, float, str, bool))},
+        }
+
+    def first_below(self, tol: float) -> Optional[int]:
+        idx = np.nonzero(self.loss < tol)[0]
+        return int(idx[0]) + 1 if len(idx) else None
+
+
+class Stopper:
+    """Reference stop rule ``loss < acc`` -> Iter = i (group_ADMM_closedForm.m:105-108)."""
+
+    def __init__(self, obj0: float, tol: float, max_iter: int):
+        self.obj0, self.tol, self.max_iter = float(obj0), float(tol), int(max_iter)
+        self.obj: List[float] = []
+        self.loss: List[float] = []
+        self.times: List[float] = []
+        self.t0 = time.perf_counter()
+
+    def record(self, obj: float) -> bool:
+        self.obj.append(float(obj))
+        self.loss.append(abs(float(obj) - self.obj0))
+        self.times.append(time.perf_counter() - self.t0)
+        return self.loss[-1] < self.tol
+
+    def arrays(self):
+        return np.asarray(self.obj), np.asarray(self.loss), np.asarray(self.times)
+
+
+def total_bytes(comm) -> int:
+    """Sum of bytes sent over all ranks (one scalar all-reduce, outside any timed loop)."""
+    import torch
+
+    b = int(comm.stats.bytes_sent) + int(comm.stats.coll_bytes)
+    if comm.nranks <= 1:
+        return b
+    t = torch.tensor([float(b)], dtype=torch.float64)
+    if getattr(comm, "backend", "").startswith("torch"):
+        import torch.distributed as dist
+
+        dist.all_reduce(t, group=comm.group)
+    else:
+        import torch.distributed as dist
+
+        dist.all_reduce(t, group=getattr(comm, "control_group", None))
+    return int(t.item())

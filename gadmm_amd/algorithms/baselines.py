@@ -1,0 +1,372 @@
+"""First-order baselines of the reference: GD, DGD, LAG-PS, LAG-WK, cyclic IAG, randomized IAG
+(``GD_DGD_LAG.m`` linear, ``GD_DGD_LAG_logistic.m`` logistic).
+
+Realisation on the fabric:
+* GD: the server step ``theta -= alpha * sum_n grad_n(theta)`` is an all-reduce of the local
+  gradient sums; theta stays replicated on every rank.
+* DGD: each worker steps on the average of its own and its chain neighbours' gradients; boundary
+  gradients cross ranks by p2p (the same chain plan as GADMM).
+* LAG-PS / LAG-WK: rank 0 plays the server and keeps the table of the latest uploaded gradient of
+  every worker. Every iteration each rank sends a 1-double trigger count and, only if non-zero, the
+  (row id, gradient) rows of its triggered workers (conditional, data-dependent uploads); the server
+  steps with the table sum and broadcasts theta. Bytes are counted exactly.
+* cIAG / RIAG: one worker refreshes per iteration and uploads its row to the server. RIAG's draw
+  uses an RNG seeded identically on every rank (no message).
+
+Faithful quirks (``faithful=True``): gradients start as ``ones`` (GD_DGD_LAG.m:44-67);
+LAG-PS refreshes worker 1 every iteration (timing side effect, :204-209); LAG does nothing before
+``iter > triggerslot = 10``; a communication unit is still counted every 1000 quiet iterations
+(:246-251); logistic GD's first step uses worker 1's gradient (GD_DGD_LAG_logistic.m:97); logistic
+LAG/IAG stop at ``accuracy``, GD/DGD never stop early.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..parallel.comm import Comm, LocalComm
+from ..parallel.topology import Placement, chain_plan
+from .base import RunResult, Stopper, total_bytes
+
+TRIGGERSLOT = 10
+
+
+class _Ctx:
+    def __init__(self, model, local_ids, n_total, comm, placement):
+        self.model = model
+        self.comm = comm if comm is not None else LocalComm()
+        self.placement = placement if placement is not None else Placement.contiguous(n_total, self.comm.nranks)
+        self.local_ids = [int(w) for w in local_ids]
+        self.n_total = n_total
+        self.d = model.d
+        self.dev = model.device
+        self.lidx = {w: i for i, w in enumerate(self.local_ids)}
+
+    def allsum(self, t: torch.Tensor) -> torch.Tensor:
+        t = t.contiguous()
+        if self.comm.nranks > 1:
+            self.comm.allreduce_sum(t)
+        return t
+
+    def grad_sum(self, theta: torch.Tensor) -> torch.Tensor:
+        """sum over ALL workers of grad f_n(theta) (theta replicated)."""
+        g = self.model.gradient(theta.unsqueeze(0).expand(len(self.local_ids), -1).contiguous()).sum(0)
+        return self.allsum(g.clone())
+
+    def obj(self, theta: torch.Tensor) -> float:
+        f = self.model.objective(theta.unsqueeze(0).expand(len(self.local_ids), -1).contiguous()).sum().reshape(1)
+        return float(self.allsum(f.clone()).item())
+
+    def obj_per_worker(self, theta_loc: torch.Tensor) -> float:
+        f = self.model.objective(theta_loc).sum().reshape(1)
+        return float(self.allsum(f.clone()).item())
+
+    def worker_grad(self, w: int, theta: torch.Tensor) -> torch.Tensor:
+        i = self.lidx[w]
+        return self.model.gradient(theta.unsqueeze(0), idx=[i])[0] if self.model.kind == "logistic" \
+            else (self.model.A[i] @ theta - self.model.b[i] + self.model.lam * theta)
+
+
+def global_constants(model, comm: Optional[Comm] = None) -> Dict[str, object]:
+    """Hmax per worker, Hmax_all and the GD step 1/Hmax_all (GD_DGD_LAG.m:19-47; logistic
+    GD_DGD_LAG_logistic.m:24). One all-reduce of the d x d Gram / all-gather of Hmax."""
+    comm = comm if comm is not None else LocalComm()
+    G = torch.bmm(model.X.transpose(1, 2), model.X).sum(0).contiguous()
+    if comm.nranks > 1:
+        comm.allreduce_sum(G)
+    ev = torch.linalg.eigvalsh(G)
+    if model.kind == "linear":
+        hmax_all = float(ev[-1])
+    else:
+        hmax_all = 0.25 * float(ev[-1]) + model.lam
+    hmax_loc = model.hmax()
+    return {"hmax_local": hmax_loc, "hmax_all": hmax_all, "stepsize": 1.0 / hmax_all,
+            "cond": float(ev[-1] / ev[0]) if float(ev[0]) > 0 else float("inf")}
+
+
+def _gather_hmax(ctx: _Ctx, hmax_local: torch.Tensor) -> torch.Tensor:
+    full = torch.zeros(ctx.n_total, dtype=torch.float64, device=ctx.dev)
+    for w, i in ctx.lidx.items():
+        full[w] = hmax_local[i]
+    return ctx.allsum(full)
+
+
+def _result(name, stop: Stopper, ctx: _Ctx, units: np.ndarray, converged: bool, iters: int, **extra):
+    obj, loss, times = stop.arrays()
+    return RunResult(algorithm=name, obj=obj, loss=loss, iters=iters, converged=converged,
+                     wall_s=float(times[-1]) if len(times) else 0.0, time_trace=times, comm_units=units,
+                     bytes_sent=int(ctx.comm.stats.bytes_sent + ctx.comm.stats.coll_bytes),
+                     bytes_total=total_bytes(ctx.comm), extra=extra)
+
+
+# ------------------------------------------------------------------------------------------------- GD
+def gradient_descent(model, local_ids, n_total, num_iter, obj0, stepsize, comm=None, placement=None,
+                     faithful=True, tol: Optional[float] = None) -> RunResult:
+    ctx = _Ctx(model, local_ids, n_total, comm, placement)
+    d = ctx.d
+    theta = torch.zeros(d, dtype=torch.float64, device=ctx.dev)
+    stop = Stopper(obj0, tol if tol is not None else -1.0, num_iter)
+    converged, iters = False, num_iter
+    for it in range(1, num_iter + 1):
+        if it == 1 and faithful:
+            if model.kind == "linear":
+                g = torch.ones(d, dtype=torch.float64, device=ctx.dev)
+            else:  # GD_DGD_LAG_logistic.m:97: the first step uses worker 1's gradient only
+                g = torch.zeros(d, dtype=torch.float64, device=ctx.dev)
+                if 0 in ctx.lidx:
+                    g = ctx.worker_grad(0, theta)
+                g = ctx.allsum(g.clone())
+        else:
+            g = ctx.grad_sum(theta)
+        hit = stop.record(ctx.obj(theta))
+        theta = theta - stepsize * g
+        if hit and tol is not None:
+            converged, iters = True, it
+            break
+    n = len(stop.obj)
+    units = np.arange(1, n + 1, dtype=np.float64) * (n_total + 1)
+    return _result("GD", stop, ctx, units, converged, iters if converged else n, final_theta=None)
+
+
+# ------------------------------------------------------------------------------------------------ DGD
+def decentralized_gd(model, local_ids, n_total, num_iter, obj0, stepsize, comm=None, placement=None,
+                     faithful=True, tol: Optional[float] = None) -> RunResult:
+    """DGD (GD_DGD_LAG.m:124-180): step stepsize/100 on the chain-neighbour average of gradients."""
+    ctx = _Ctx(model, local_ids, n_total, comm, placement)
+    d, dev = ctx.d, ctx.dev
+    nl = len(ctx.local_ids)
+    theta = torch.zeros((nl, d), dtype=torch.float64, device=dev)
+    G = torch.ones((n_total, d), dtype=torch.float64, device=dev) if faithful else \
+        torch.zeros((n_total, d), dtype=torch.float64, device=dev)
+    plan = chain_plan(list(range(n_total)), ctx.placement, ctx.comm.rank)
+    xchg = plan.xchg_head + plan.xchg_tail  # every boundary worker's gradient to its neighbour rank
+    ids = torch.tensor(ctx.local_ids, dtype=torch.long, device=dev)
+    step = stepsize / 100.0
+    stop = Stopper(obj0, tol if tol is not None else -1.0, num_iter)
+    converged, iters = False, num_iter
+    for it in range(1, num_iter + 1):
+        if it > 1 or not faithful:
+            G[ids] = model.gradient(theta)
+        ctx.comm.exchange_rows(G, xchg)
+        hit = stop.record(ctx.obj_per_worker(theta))
+        new = torch.empty_like(theta)
+        for k, w in enumerate(ctx.local_ids):
+            if n_total == 1:
+                new[k] = theta[k] - step * G[w]
+            elif w == 0:
+                new[k] = theta[k] - 0.5 * step * (G[w] + G[w + 1])
+            elif w == n_total - 1:
+                new[k] = theta[k] - 0.5 * step * (G[w] + G[w - 1])
+            else:
+                new[k] = theta[k] - (1.0 / 3.0) * step * (G[w] + G[w + 1] + G[w - 1])
+        theta = new
+        if hit and tol is not None:
+            converged, iters = True, it
+            break
+    n = len(stop.obj)
+    return _result("DGD", stop, ctx, np.arange(1, n + 1, dtype=np.float64) * n_total, converged,
+                   iters if converged else n)
+
+
+# ------------------------------------------------------------------------------------------------ LAG
+class _Server:
+    """Rank 0 holds the server's table of the latest uploaded gradient of every worker
+    (``grads`` in GD_DGD_LAG.m) and broadcasts theta; other ranks upload rows conditionally."""
+
+    def __init__(self, ctx: _Ctx, init: torch.Tensor):
+        self.ctx = ctx
+        self.table = init.clone() if ctx.comm.rank == 0 else None  # (N, d)
+
+    def upload(self, rows: torch.Tensor, vals: torch.Tensor) -> int:
+        """Every rank calls with its triggered (global row ids, gradients). Returns the total count."""
+        ctx, comm = self.ctx, self.ctx.comm
+        d, dev = ctx.d, ctx.dev
+        k = int(rows.numel())
+        if comm.nranks == 1:
+            if k:
+                self.table[rows] = vals
+            return k
+        if comm.rank == 0:
+            total = k
+            if k:
+                self.table[rows] = vals
+            cnt = torch.zeros(1, dtype=torch.float64, device=dev)
+            for r in range(1, comm.nranks):
+                comm.recv_tensor(cnt, r)
+                c = int(cnt.item())
+                if c:
+                    buf = torch.empty((c, d + 1), dtype=torch.float64, device=dev)
+                    comm.recv_tensor(buf, r)
+                    self.table[buf[:, 0].long()] = buf[:, 1:]
+                total += c
+            t = torch.tensor([float(total)], dtype=torch.float64, device=dev)
+        else:
+            comm.send_tensor(torch.tensor([float(k)], dtype=torch.float64, device=dev), 0)
+            if k:
+                comm.send_tensor(torch.cat([rows.double().unsqueeze(-1), vals], dim=1).contiguous(), 0)
+            t = torch.zeros(1, dtype=torch.float64, device=dev)
+        comm.broadcast(t, 0)
+        return int(t.item())
+
+    def step(self, theta: torch.Tensor, stepsize: float) -> torch.Tensor:
+        """theta <- theta - stepsize * sum(grads, 2) on the server, broadcast to every rank."""
+        comm = self.ctx.comm
+        if comm.rank == 0:
+            new = theta - stepsize * self.table.sum(0)
+        else:
+            new = torch.empty_like(theta)
+        if comm.nranks > 1:
+            comm.broadcast(new, 0)
+        return new
+
+
+def lag(model, local_ids, n_total, num_iter, obj0, stepsize, hmax_full: torch.Tensor, variant: str = "PS",
+        comm=None, placement=None, faithful=True, tol: Optional[float] = None) -> RunResult:
+    """LAG-PS (server-side trigger) / LAG-WK (worker-side trigger), GD_DGD_LAG.m:184-327."""
+    ctx = _Ctx(model, local_ids, n_total, comm, placement)
+    d, dev = ctx.d, ctx.dev
+    N = n_total
+    thrd = (10.0 if variant == "PS" else 1.0) / (stepsize ** 2 * N ** 2) / TRIGGERSLOT
+    ids = torch.tensor(ctx.local_ids, dtype=torch.long, device=dev)
+    nl = len(ctx.local_ids)
+    server = _Server(ctx, torch.ones((N, d), dtype=torch.float64, device=dev))
+    G = torch.ones((nl, d), dtype=torch.float64, device=dev)        # worker-side copy of its last upload
+    theta_hat = torch.zeros((nl, d), dtype=torch.float64, device=dev)
+    hloc = hmax_full[ids] ** 2
+    hist = [torch.zeros(d, dtype=torch.float64, device=dev)]        # theta^{iter-11..iter}
+    comm_iter = 1.0
+    comm_final = []
+    uploads = 0
+    stop = Stopper(obj0, tol if tol is not None else -1.0, num_iter)
+    converged, iters = False, num_iter
+    w0 = ctx.lidx.get(0)
+    for it in range(1, num_iter + 1):
+        theta = hist[-1]
+        rows, vals = [], []
+        grads_now = model.gradient(theta.unsqueeze(0).expand(nl, -1).contiguous())
+        forced = None
+        if variant == "PS" and faithful and it > 1 and w0 is not None:
+            forced = grads_now[w0]  # worker-1 refresh side effect (quirk 4): no upload counted
+        mask = torch.zeros(nl, dtype=torch.bool, device=dev)
+        if it > TRIGGERSLOT:
+            trig = sum(float((hist[-n] - hist[-n - 1]) @ (hist[-n] - hist[-n - 1])) for n in range(1, TRIGGERSLOT + 1))
+            if variant == "PS":
+                dd = ((theta_hat - theta) ** 2).sum(-1)
+                mask = hloc * dd > thrd * trig
+            else:
+                dd = ((grads_now - G) ** 2).sum(-1)
+                mask = dd > thrd * trig
+        if bool(mask.any()):
+            sel = mask.nonzero().flatten()
+            G[sel] = grads_now[sel]
+            if variant == "PS":
+                theta_hat[sel] = theta
+        upd = mask.clone()
+        if forced is not None:
+            G[w0] = forced
+            upd[w0] = True
+        sel = upd.nonzero().flatten()
+        server.upload(ids[sel], G[sel])
+        count = int(mask.sum())
+        c_all = count
+        if ctx.comm.nranks > 1:
+            t = torch.tensor([float(count)], dtype=torch.float64, device=dev)
+            ctx.comm.allreduce_sum(t)
+            c_all = int(t.item())
+        uploads += c_all
+        hit = stop.record(ctx.obj(theta))
+        if c_all > 0:
+            comm_iter += c_all
+        elif it % 1000 == 0:
+            comm_iter += 1
+        comm_final.append(comm_iter)
+        hist.append(server.step(theta, stepsize))
+        if len(hist) > TRIGGERSLOT + 2:
+            hist.pop(0)
+        if hit and tol is not None:
+            converged, iters = True, it
+            break
+    n = len(stop.obj)
+    units = np.asarray(comm_final) + np.arange(1, n + 1)
+    return _result("LAG-" + variant, stop, ctx, units, converged, iters if converged else n, uploads=uploads)
+
+
+# ------------------------------------------------------------------------------------------------ IAG
+def iag(model, local_ids, n_total, num_iter, obj0, stepsize, mode: str = "cyclic", hmax_full=None, seed: int = 7,
+        comm=None, placement=None, faithful=True, tol: Optional[float] = None) -> RunResult:
+    """Cyclic IAG (worker ``iter mod N`` refreshes) and non-uniform randomized IAG (worker drawn
+    with probability proportional to Hmax_i); step alpha/N (GD_DGD_LAG.m:330-371)."""
+    ctx = _Ctx(model, local_ids, n_total, comm, placement)
+    d, dev = ctx.d, ctx.dev
+    N = n_total
+    step = stepsize / N
+    server = _Server(ctx, torch.ones((N, d), dtype=torch.float64, device=dev))
+    theta = torch.zeros(d, dtype=torch.float64, device=dev)
+    rng = np.random.default_rng(seed)
+    if mode != "cyclic":
+        prob = np.asarray(hmax_full.cpu().numpy(), dtype=np.float64)
+        cum = np.cumsum(prob / prob.sum())
+    stop = Stopper(obj0, tol if tol is not None else -1.0, num_iter)
+    converged, iters = False, num_iter
+    empty_r = torch.zeros(0, dtype=torch.long, device=dev)
+    empty_v = torch.zeros((0, d), dtype=torch.float64, device=dev)
+    for it in range(1, num_iter + 1):
+        if mode == "cyclic":
+            w = it % N
+        else:
+            w = min(int(np.searchsorted(cum, rng.random(), side="left")), N - 1)
+        if it > 1:
+            if int(ctx.placement.owner[w]) == ctx.comm.rank:
+                g = ctx.worker_grad(w, theta)
+                server.upload(torch.tensor([w], dtype=torch.long, device=dev), g.unsqueeze(0))
+            else:
+                server.upload(empty_r, empty_v)
+        hit = stop.record(ctx.obj(theta))
+        theta = server.step(theta, step)
+        if hit and tol is not None:
+            converged, iters = True, it
+            break
+    n = len(stop.obj)
+    return _result("cIAG" if mode == "cyclic" else "R-IAG", stop, ctx, np.arange(1, n + 1, dtype=np.float64) * 2,
+                   converged, iters if converged else n)
+
+
+# ------------------------------------------------------------------------------------------- bundle
+def gd_dgd_lag(model, local_ids, n_total, num_iter, obj0: Optional[float], comm=None, placement=None,
+               faithful=True, accuracy: Optional[float] = None, which=("GD", "DGD", "LAG-PS", "LAG-WK", "cIAG", "R-IAG"),
+               seed: int = 7) -> Dict[str, object]:
+    """The reference bundle: ``GD_DGD_LAG`` (linear, obj0 given) or ``GD_DGD_LAG_logistic`` (obj0 =
+    final GD objective, returned as ``obj1``; LAG/IAG stop at ``accuracy``)."""
+    comm = comm if comm is not None else LocalComm()
+    consts = global_constants(model, comm)
+    step = consts["stepsize"]
+    ctx = _Ctx(model, local_ids, n_total, comm, placement)
+    hmax_full = _gather_hmax(ctx, consts["hmax_local"])
+    out: Dict[str, object] = {"stepsize": step, "hmax_all": consts["hmax_all"], "cond": consts["cond"]}
+    logistic = model.kind == "logistic"
+    if "GD" in which or logistic:
+        gd = gradient_descent(model, local_ids, n_total, num_iter, obj0 if obj0 is not None else 0.0, step, comm,
+                              placement, faithful)
+        if logistic and obj0 is None:
+            obj0 = float(gd.obj[-1])  # GD_DGD_LAG_logistic.m:131-133
+            gd.loss = np.abs(gd.obj - obj0)
+        out["GD"] = gd
+    out["obj0"] = obj0
+    tol_ = accuracy if logistic else None
+    if "DGD" in which:
+        out["DGD"] = decentralized_gd(model, local_ids, n_total, num_iter, obj0, step, comm, placement, faithful)
+    if "LAG-PS" in which:
+        out["LAG-PS"] = lag(model, local_ids, n_total, num_iter, obj0, step, hmax_full, "PS", comm, placement,
+                            faithful, tol_)
+    if "LAG-WK" in which:
+        out["LAG-WK"] = lag(model, local_ids, n_total, num_iter, obj0, step, hmax_full, "WK", comm, placement,
+                            faithful, tol_)
+    if "cIAG" in which:
+        out["cIAG"] = iag(model, local_ids, n_total, num_iter, obj0, step, "cyclic", None, seed, comm, placement,
+                          faithful, tol_)
+    if "R-IAG" in which:
+        out["R-IAG"] = iag(model, local_ids, n_total, num_iter, obj0, step, "random", hmax_full, seed, comm,
+                           placement, faithful, tol_)
+    return out

@@ -1,0 +1,313 @@
+"""Chain ADMM family: GADMM, D-GADMM, static-chain-with-cost, logistic variants.
+
+Reference components:
+  A1 ``group_ADMM_closedForm.m``        GADMM, linear, closed-form local solve
+  A2 ``group_ADMM_logistic_GD.m``       GADMM, logistic, inexact local GD (A3 ``logReg_GD.m``)
+  D2 ``group_ADMM_logistic.m``          GADMM, logistic, exact local solve (CVX) -> Newton here
+  A4 ``dynamic_group_ADMM_closedForm.m``    D-GADMM (re-chain via findPath2 every coherence_Time)
+  A5 ``dynamic_group_ADMM_closedForm_v0.m`` D-GADMM over pre-generated path/cost matrices
+  A6 ``static_group_ADMM_closedForm.m``     identity chain, moving-node cost matrix
+
+All of them are one algorithm on different chain schedules: heads (even chain positions) update in
+parallel, their theta goes to the neighbouring tails, tails update, their theta goes back, and every
+worker updates its aggregated dual ``mu_n`` (= lambda_n - lambda_{n-1}). Per-worker duals survive a
+re-chain (dynamic_group_ADMM_closedForm.m:40-49 keeps the reset commented out).
+
+Two executions of the same schedule:
+* ``backend='torch'``: batched torch ops per phase on any device with any ``Comm`` (gloo CPU
+  plumbing, torch.distributed on GPU, single process);
+* ``backend='native'``: the C++/HIP chain engine (graph-replayed fused phase kernels with RCCL
+  p2p, or the persistent single-launch kernel on one GPU). ``'auto'`` picks native on a HIP device.
+"""
+from __future__ import annotations
+
+import time
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..parallel.comm import Comm, LocalComm
+from ..parallel.topology import PathSchedule, Placement, chain_plan
+from .base import RunResult, Stopper, total_bytes
+
+
+def _gather_rows(theta: torch.Tensor, ids: List[int]) -> torch.Tensor:
+    idx = torch.tensor([max(i, 0) for i in ids], dtype=torch.long, device=theta.device)
+    rows = theta.index_select(0, idx)
+    mask = torch.tensor([1.0 if i >= 0 else 0.0 for i in ids], dtype=theta.dtype, device=theta.device)
+    return rows * mask.unsqueeze(-1), mask
+
+
+def chain_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: float, tol: float,
+               max_iter: int, comm: Optional[Comm] = None, placement: Optional[Placement] = None,
+               path: Optional[Sequence[int]] = None, schedule: Optional[PathSchedule] = None,
+               local_solver: Optional[str] = None, step: float = 1.0, max_inner: int = 100,
+               inner_tol: float = 1e-4, cost_quirk: bool = True, backend: str = "auto",
+               name: str = "GADMM", record_theta: bool = False, engine_opts: Optional[dict] = None,
+               state=None) -> RunResult:
+    """Run one chain-ADMM solve on this rank. ``model`` holds this rank's shards (local order =
+    ``local_ids``). ``schedule`` (D-GADMM) overrides ``path``; ``cost_quirk`` reproduces the
+    reference's per-head-worker accumulation of ``sum(pathCost)`` (dynamic_group_ADMM_closedForm.m:51-55).
+    ``state``: optional ``(theta_table, mu, start_iter)`` to resume from a checkpoint."""
+    comm = comm if comm is not None else LocalComm()
+    placement = placement if placement is not None else Placement.contiguous(n_total, comm.nranks)
+    if schedule is None:
+        p0 = list(path) if path is not None else list(range(n_total))
+        schedule = PathSchedule(n_total, p0, np.zeros(max(n_total - 1, 0)), coherence=0)
+    if local_solver is None:
+        local_solver = "closed" if model.kind == "linear" else "gd"
+    dev = model.device
+    use_native = False
+    if backend in ("auto", "native") and dev.type == "cuda" and local_solver in ("closed", "gd") and state is None:
+        from ..ops import native
+
+        if native.available() and (comm.nranks == 1 or getattr(comm, "backend", "") == "rccl"):
+            use_native = True
+        elif backend == "native":
+            raise RuntimeError("native backend requested but unavailable for this comm/device")
+    if use_native:
+        return _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, schedule,
+                                  local_solver, step, max_inner, inner_tol, cost_quirk, name, engine_opts or {})
+    return _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, schedule,
+                             local_solver, step, max_inner, inner_tol, cost_quirk, name, record_theta, state)
+
+
+def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, schedule,
+                      local_solver, step, max_inner, inner_tol, cost_quirk, name, record_theta, state):
+    rank = comm.rank
+    d = model.d
+    dev = model.device
+    local_ids = [int(w) for w in local_ids]
+    if state is not None:
+        theta = state[0].to(dev).clone()
+        mu = state[1].to(dev).clone()
+        start = int(state[2])
+    else:
+        theta = torch.zeros((n_total, d), dtype=torch.float64, device=dev)
+        mu = torch.zeros((len(local_ids), d), dtype=torch.float64, device=dev)
+        start = 1
+    stop = Stopper(obj0, tol, max_iter)
+    plan = chain_plan(schedule.path, placement, rank)
+    cc = 0.0
+    com_cost: List[float] = []
+    inner_used: List[float] = []
+    iters = max_iter
+    converged = False
+    for it in range(start, max_iter + 1):
+        if schedule.step(it):
+            plan = chain_plan(schedule.path, placement, rank)
+        n_heads = (n_total + 1) // 2
+        cc += float(np.sum(schedule.cost)) * (n_heads if cost_quirk else 1)
+        com_cost.append(cc)
+        for slots, xchg in ((plan.head, plan.xchg_head), (plan.tail, plan.xchg_tail)):
+            if slots:
+                li = torch.tensor([s.li for s in slots], dtype=torch.long, device=dev)
+                gid = [s.gid for s in slots]
+                thl, ml = _gather_rows(theta, [s.left for s in slots])
+                thr, mr = _gather_rows(theta, [s.right for s in slots])
+                deg = ml + mr
+                m_li = mu.index_select(0, li)
+                if local_solver == "closed":
+                    rhs = model.b.index_select(0, li) - m_li + rho * thl + rho * thr
+                    new = model.prox_solve(li, rhs, deg * rho)
+                elif local_solver == "gd":
+                    thw = theta.index_select(0, torch.tensor(gid, device=dev))
+                    shift = m_li + rho * (thw - thl) * ml.unsqueeze(-1) + rho * (thw - thr) * mr.unsqueeze(-1)
+                    new, used = model.inexact_gd(li, thw, shift, step, max_inner, inner_tol)
+                    inner_used.append(float(used.double().mean()))
+                elif local_solver == "newton":
+                    thw = theta.index_select(0, torch.tensor(gid, device=dev))
+                    quad = deg * rho
+                    center = (thl + thr) / torch.clamp(deg, min=1.0).unsqueeze(-1)
+                    new = model.newton_prox(li, thw, m_li, quad, center)
+                else:
+                    raise ValueError("unknown local solver %r" % local_solver)
+                theta[torch.tensor(gid, dtype=torch.long, device=dev)] = new
+            comm.exchange_rows(theta, xchg)
+        # dual update, reference order: mu - rho (th_l - th) + rho (th - th_r)
+        for slots in (plan.head, plan.tail):
+            if not slots:
+                continue
+            li = torch.tensor([s.li for s in slots], dtype=torch.long, device=dev)
+            thw = theta.index_select(0, torch.tensor([s.gid for s in slots], device=dev))
+            thl, ml = _gather_rows(theta, [s.left for s in slots])
+            thr, mr = _gather_rows(theta, [s.right for s in slots])
+            m = mu.index_select(0, li)
+            m = m - rho * (thl - thw) * ml.unsqueeze(-1)
+            m = m + rho * (thw - thr) * mr.unsqueeze(-1)
+            mu[li] = m
+        th_loc = theta.index_select(0, torch.tensor(local_ids, dtype=torch.long, device=dev))
+        f = model.objective(th_loc)
+        tot = f.sum().reshape(1).clone()
+        if comm.nranks > 1:
+            comm.allreduce_sum(tot)
+        if stop.record(float(tot.item())):
+            iters = it
+            converged = True
+            break
+    obj, loss, times = stop.arrays()
+    n_it = len(obj)
+    res = RunResult(algorithm=name, obj=obj, loss=loss, iters=iters if converged else (start - 1 + n_it),
+                    converged=converged, wall_s=float(times[-1]) if n_it else 0.0, time_trace=times,
+                    comm_units=np.arange(start, start + n_it, dtype=np.float64) * n_total,
+                    com_cost=np.asarray(com_cost), bytes_sent=int(comm.stats.bytes_sent),
+                    bytes_total=total_bytes(comm),
+                    extra={"backend": "torch", "rank": rank, "nranks": comm.nranks, "solver": local_solver,
+                           "inner_steps_mean": float(np.mean(inner_used)) if inner_used else 0.0})
+    res.extra["state"] = (theta, mu, (iters if converged else start - 1 + n_it) + 1)
+    if record_theta:
+        res.theta = theta.cpu().numpy()
+    return res
+
+
+def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, schedule, local_solver,
+                       step, max_inner, inner_tol, cost_quirk, name, opts):
+    from ..engine.chain_engine import NativeChainEngine
+
+    rank = comm.rank
+    rcomm = comm if comm.nranks > 1 else None
+    kind = "linear" if local_solver == "closed" else "logistic"
+    block = int(opts.get("block", 16 if comm.nranks > 1 else 32))
+    pre = (model.A, model.b, model.yy) if kind == "linear" else None
+    eng = NativeChainEngine(model.X, model.y, local_ids, n_total, kind, rho=rho, obj0=obj0, tol=tol,
+                            max_iter=max_iter, lam=getattr(model, "lam", 0.0), step=step, max_inner=max_inner,
+                            inner_tol=inner_tol, comm=rcomm, block=block, precomputed=pre)
+    eng.set_path(schedule.path, placement, rank)
+    eng.reset()
+    torch.cuda.synchronize(model.device)
+    t0 = time.perf_counter()
+    cc = 0.0
+    com_cost = []
+    n_heads = (n_total + 1) // 2
+    static = not schedule.coherence or not np.isfinite(schedule.coherence) or schedule.coherence <= 0 \
+        or schedule.coherence >= max_iter + 1
+    p2p = 0
+    mon = 0
+    if static:
+        persistent = opts.get("persistent", "auto")
+        if (persistent is True or persistent == "auto") and eng.persistent_eligible():
+            r = eng.run_persistent()
+            engine_kind = "persistent"
+        else:
+            r = eng.run(use_graph=opts.get("graph", True))
+            engine_kind = "graph" if eng.graph_ok() else "eager"
+        iters, done = r.iters, r.done
+        p2p, mon = r.p2p_bytes, r.monitor_bytes
+        per = float(np.sum(schedule.cost)) * (n_heads if cost_quirk else 1)
+        com_cost = list(np.arange(1, iters + 1) * per)
+    else:
+        # D-GADMM: run epoch by epoch; at a re-chain iteration flush the heads' pending duals with the
+        # old chain, install the new chain, continue. Every rank draws the same chain sequence.
+        engine_kind = "epochs"
+        it = 1
+        done = 0
+        iters = 0
+        while it <= max_iter and not done:
+            nxt = it + 1
+            while nxt <= max_iter and not _is_rechain(nxt, schedule.coherence):
+                nxt += 1
+            per = float(np.sum(schedule.cost)) * (n_heads if cost_quirk else 1)
+            r = eng.run(stop_iter=nxt - 1, use_graph=False)
+            p2p += r.p2p_bytes
+            mon += r.monitor_bytes
+            ran_to = r.iters
+            for _ in range(it, ran_to + 1):
+                cc += per
+                com_cost.append(cc)
+            done = r.done
+            iters = ran_to
+            if done or nxt > max_iter:
+                break
+            eng.flush_duals()
+            schedule.step(nxt)
+            eng.set_path(schedule.path, placement, rank)
+            it = nxt
+    torch.cuda.synchronize(model.device)
+    wall = time.perf_counter() - t0
+    tr = eng.objective_trace(iters)
+    loss = np.abs(tr - obj0)
+    bytes_tot = p2p
+    if comm.nranks > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([float(p2p)], dtype=torch.float64)
+        dist.all_reduce(t, group=getattr(comm, "control_group", None))
+        bytes_tot = int(t.item())
+    res = RunResult(algorithm=name, obj=tr, loss=loss, iters=iters, converged=(done == 1), wall_s=wall,
+                    time_trace=np.linspace(wall / max(iters, 1), wall, iters),
+                    comm_units=np.arange(1, iters + 1, dtype=np.float64) * n_total,
+                    com_cost=np.asarray(com_cost[:iters]), bytes_sent=int(p2p), bytes_total=bytes_tot,
+                    extra={"backend": "native", "engine": engine_kind, "rank": rank, "nranks": comm.nranks,
+                           "solver": local_solver, "monitor_bytes": int(mon)})
+    res.extra["engine_obj"] = eng
+    return res
+
+
+def _is_rechain(it: int, coherence) -> bool:
+    from ..parallel.topology import rechain_iteration
+
+    return rechain_iteration(it, coherence)
+
+
+# Convenience wrappers named after the reference functions -----------------------------------------
+
+def group_admm_closed_form(model, rho, obj0, acc, max_iter, **kw) -> RunResult:
+    """``group_ADMM_closedForm`` (A1) on all local workers (single rank unless comm given)."""
+    n_total = kw.pop("n_total", model.n_local)
+    local_ids = kw.pop("local_ids", list(range(model.n_local)))
+    return chain_admm(model, local_ids, n_total, rho, obj0, acc, max_iter, name="GADMM", **kw)
+
+
+def group_admm_logistic_gd(model, rho, obj0, acc, max_iter, step, **kw) -> RunResult:
+    """``group_ADMM_logistic_GD`` (A2 + A3)."""
+    n_total = kw.pop("n_total", model.n_local)
+    local_ids = kw.pop("local_ids", list(range(model.n_local)))
+    return chain_admm(model, local_ids, n_total, rho, obj0, acc, max_iter, local_solver="gd", step=step,
+                      name="GADMM-logistic-GD", **kw)
+
+
+def group_admm_logistic_exact(model, rho, obj0, acc, max_iter, **kw) -> RunResult:
+    """``group_ADMM_logistic`` (D2, CVX exact local solves) via Newton."""
+    n_total = kw.pop("n_total", model.n_local)
+    local_ids = kw.pop("local_ids", list(range(model.n_local)))
+    return chain_admm(model, local_ids, n_total, rho, obj0, acc, max_iter, local_solver="newton",
+                      name="GADMM-logistic-exact", **kw)
+
+
+def dynamic_group_admm(model, rho, obj0, acc, max_iter, path, path_cost, coherence, seed=1234,
+                       kind="findPath2", **kw) -> RunResult:
+    """``dynamic_group_ADMM_closedForm`` (A4): re-chain with findPath2 every ``coherence`` iterations."""
+    n_total = kw.pop("n_total", model.n_local)
+    local_ids = kw.pop("local_ids", list(range(model.n_local)))
+    sched = PathSchedule(n_total, path, path_cost, coherence, kind=kind, seed=seed)
+    return chain_admm(model, local_ids, n_total, rho, obj0, acc, max_iter, schedule=sched,
+                      name="D-GADMM(coh=%s)" % coherence, **kw)
+
+
+def dynamic_group_admm_v0(model, rho, obj0, acc, max_iter, path_matrix, cost_matrix, coherence,
+                          faithful_initial_cost=True, **kw) -> RunResult:
+    """``dynamic_group_ADMM_closedForm_v0`` (A5): consume pre-generated chains. With
+    ``faithful_initial_cost`` the initial cost is the reference's column slice
+    ``pathCost_matrix(:,1)`` (quirk 6, dynamic_group_ADMM_closedForm_v0.m:18)."""
+    n_total = kw.pop("n_total", model.n_local)
+    local_ids = kw.pop("local_ids", list(range(model.n_local)))
+    cm = np.asarray(cost_matrix)
+    c0 = cm[:, 0] if faithful_initial_cost else cm[0]
+    sched = PathSchedule(n_total, path_matrix[0], c0, coherence, kind="matrix", path_matrix=path_matrix,
+                         cost_matrix=cm)
+    return chain_admm(model, local_ids, n_total, rho, obj0, acc, max_iter, schedule=sched,
+                      name="D-GADMM-v0(coh=%s)" % coherence, **kw)
+
+
+def static_group_admm(model, rho, obj0, acc, max_iter, coherence, cost_static_matrix, **kw) -> RunResult:
+    """``static_group_ADMM_closedForm`` (A6): identity chain; its cost row changes with the node
+    geometry every ``coherence`` iterations."""
+    n_total = kw.pop("n_total", model.n_local)
+    local_ids = kw.pop("local_ids", list(range(model.n_local)))
+    cm = np.asarray(cost_static_matrix)
+    ident = list(range(n_total))
+    sched = PathSchedule(n_total, ident, cm[0], coherence, kind="matrix",
+                         path_matrix=[ident] * cm.shape[0], cost_matrix=cm)
+    return chain_admm(model, local_ids, n_total, rho, obj0, acc, max_iter, schedule=sched,
+                      name="GADMM-static(coh=%s)" % coherence, **kw)

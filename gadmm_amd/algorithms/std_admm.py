@@ -1,0 +1,75 @@
+"""Standard (star / parameter-server) ADMM — ``standared_ADMM.m``.
+
+Worker N (the last one) is the hub and also owns a shard. Per iteration:
+  1. workers 1..N-1 solve ``(A_i + rho I) x = b_i - lam_i + rho theta_hub``      (:42)
+  2. the hub gathers ``sum lam_i`` and ``sum theta_i`` (RCCL reduce to the hub rank)  (:66-71)
+  3. hub solves ``(A_N + (N-1) rho I) x = b_N + sum lam_i + rho sum theta_i``         (:73)
+  4. hub broadcasts theta_hub (RCCL broadcast)
+  5. ``lam_i += rho (theta_i - theta_hub)``                                           (:84-88)
+Reference comm units: N-1 uploads + N-1 downloads per iteration.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..parallel.comm import Comm, LocalComm
+from ..parallel.topology import Placement
+from .base import RunResult, Stopper, total_bytes
+
+
+def standard_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: float, tol: float,
+                  max_iter: int, comm: Optional[Comm] = None, placement: Optional[Placement] = None,
+                  name: str = "ADMM(star)") -> RunResult:
+    comm = comm if comm is not None else LocalComm()
+    placement = placement if placement is not None else Placement.contiguous(n_total, comm.nranks)
+    if model.kind != "linear":
+        raise NotImplementedError("the reference star ADMM is closed-form linear only")
+    dev = model.device
+    d = model.d
+    hub = n_total - 1
+    hub_rank = int(placement.owner[hub])
+    local_ids = [int(w) for w in local_ids]
+    lidx = {w: i for i, w in enumerate(local_ids)}
+    workers = [w for w in local_ids if w != hub]
+    wl = torch.tensor([lidx[w] for w in workers], dtype=torch.long, device=dev)
+    lam = torch.zeros((len(local_ids), d), dtype=torch.float64, device=dev)
+    theta = torch.zeros((len(local_ids), d), dtype=torch.float64, device=dev)
+    theta_hub = torch.zeros(d, dtype=torch.float64, device=dev)
+    stop = Stopper(obj0, tol, max_iter)
+    iters, converged = max_iter, False
+    for it in range(1, max_iter + 1):
+        if len(workers):
+            rhs = model.b.index_select(0, wl) - lam.index_select(0, wl) + rho * theta_hub
+            theta[wl] = model.prox_solve(wl, rhs, torch.full((len(workers),), rho, dtype=torch.float64, device=dev))
+        agg = torch.cat([lam.index_select(0, wl).sum(0), theta.index_select(0, wl).sum(0)]) if len(workers) \
+            else torch.zeros(2 * d, dtype=torch.float64, device=dev)
+        agg = agg.contiguous()
+        if comm.nranks > 1:
+            comm.reduce_sum(agg, hub_rank)
+        if comm.rank == hub_rank:
+            hl = torch.tensor([lidx[hub]], dtype=torch.long, device=dev)
+            rhs = model.b[lidx[hub]] + agg[:d] + rho * agg[d:]
+            th = model.prox_solve(hl, rhs.unsqueeze(0),
+                                  torch.tensor([(n_total - 1) * rho], dtype=torch.float64, device=dev))[0]
+            theta[lidx[hub]] = th
+            theta_hub.copy_(th)
+        if comm.nranks > 1:
+            comm.broadcast(theta_hub, hub_rank)
+        if len(workers):
+            lam[wl] = lam.index_select(0, wl) + rho * (theta.index_select(0, wl) - theta_hub)
+        f = model.objective(theta).sum().reshape(1).clone()
+        if comm.nranks > 1:
+            comm.allreduce_sum(f)
+        if stop.record(float(f.item())):
+            iters, converged = it, True
+            break
+    obj, loss, times = stop.arrays()
+    n = len(obj)
+    return RunResult(algorithm=name, obj=obj, loss=loss, iters=iters if converged else n, converged=converged,
+                     wall_s=float(times[-1]) if n else 0.0, time_trace=times,
+                     comm_units=np.arange(1, n + 1, dtype=np.float64) * 2 * (n_total - 1),
+                     bytes_sent=int(comm.stats.bytes_sent), bytes_total=total_bytes(comm),
+                     extra={"hub": hub, "hub_rank": hub_rank, "nranks": comm.nranks})

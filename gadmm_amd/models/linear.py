@@ -1,0 +1,110 @@
+"""Least-squares consensus problem ``min sum_n 1/2 ||X_n theta - y_n||^2`` (the reference's linear
+regression; objective ``group_ADMM_closedForm.m:96-101``, optimum ``opt_sol_closedForm.m:2-3``).
+
+A model instance holds the *local* shards of one rank (``X``: (n_loc, m, d)) and the loop-invariant
+sufficient statistics ``A_n = X_n^T X_n``, ``b_n = X_n^T y_n``, ``yy_n = y_n^T y_n`` (kernel K1). All
+per-iteration quantities are O(d^2) in these, independent of the shard height m.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ..ops.linalg import gram, spd_inverse
+
+
+class LinearRegression:
+    kind = "linear"
+
+    def __init__(self, X: torch.Tensor, y: torch.Tensor, lam: float = 0.0):
+        self.X = X
+        self.y = y
+        self.lam = float(lam)  # ridge per worker (the reference uses lambda = 0: GD_DGD_LAG.m:83)
+        self.A, self.b, self.yy = gram(X, y)
+        self.n_local, self.m, self.d = X.shape
+        self._chol = {}
+
+    @property
+    def device(self):
+        return self.X.device
+
+    # ---- objective / gradient -------------------------------------------------------------------
+    def objective(self, theta: torch.Tensor) -> torch.Tensor:
+        """Per-worker ``1/2 ||X_n theta_n - y_n||^2 (+ lam/2 ||theta_n||^2)`` via the quadratic form.
+        ``theta``: (n_loc, d)."""
+        At = torch.bmm(self.A, theta.unsqueeze(-1)).squeeze(-1)
+        f = 0.5 * (At * theta).sum(-1) - (self.b * theta).sum(-1) + 0.5 * self.yy
+        if self.lam:
+            f = f + 0.5 * self.lam * (theta * theta).sum(-1)
+        return f
+
+    def objective_direct(self, theta: torch.Tensor) -> torch.Tensor:
+        r = torch.bmm(self.X, theta.unsqueeze(-1)).squeeze(-1) - self.y
+        f = 0.5 * (r * r).sum(-1)
+        if self.lam:
+            f = f + 0.5 * self.lam * (theta * theta).sum(-1)
+        return f
+
+    def gradient(self, theta: torch.Tensor) -> torch.Tensor:
+        """``X_n^T X_n theta_n - X_n^T y_n (+ lam theta_n)`` (GD_DGD_LAG.m:95)."""
+        g = torch.bmm(self.A, theta.unsqueeze(-1)).squeeze(-1) - self.b
+        if self.lam:
+            g = g + self.lam * theta
+        return g
+
+    def hmax(self) -> torch.Tensor:
+        """Per-worker Lipschitz constants ``lambda_max(X_n^T X_n)`` (LinearRegression_Synthetic.m:33)."""
+        return torch.linalg.eigvalsh(self.A)[:, -1] + self.lam
+
+    def hmin(self) -> torch.Tensor:
+        return torch.linalg.eigvalsh(self.A)[:, 0] + self.lam
+
+    # ---- closed-form prox: argmin f_n(x) + <mu, x> + rho/2 sum ||x - th_nbr||^2 -------------------
+    def prox_factor(self, shift: float) -> torch.Tensor:
+        """Cholesky factors of ``A_n + (lam + shift) I`` (cached per shift)."""
+        key = float(shift)
+        if key not in self._chol:
+            eye = torch.eye(self.d, dtype=self.A.dtype, device=self.A.device)
+            self._chol[key] = torch.linalg.cholesky(self.A + (self.lam + key) * eye)
+        return self._chol[key]
+
+    def prox_solve(self, idx: torch.Tensor, rhs: torch.Tensor, shifts: torch.Tensor) -> torch.Tensor:
+        """Solve ``(A_n + shift_n I) x = rhs_n`` for local workers ``idx`` (batched Cholesky solves)."""
+        out = torch.empty_like(rhs)
+        for s in torch.unique(shifts).tolist():
+            sel = (shifts == s).nonzero().flatten()
+            L = self.prox_factor(s)[idx[sel]]
+            out[sel] = torch.cholesky_solve(rhs[sel].unsqueeze(-1), L).squeeze(-1)
+        return out
+
+    def inverses(self, shifts) -> torch.Tensor:
+        return spd_inverse(self.A, torch.as_tensor(shifts, dtype=torch.float64, device=self.A.device))
+
+    # ---- global oracle ----------------------------------------------------------------------------
+    def optimum(self, comm=None, n_total=None) -> float:
+        """Optimal objective of the stacked problem: ``(sum A_n)^{-1} sum b_n`` (one-time all-reduce
+        of the d x d Gram)."""
+        As = self.A.sum(0)
+        bs = self.b.sum(0)
+        yy = self.yy.sum()
+        if comm is not None and comm.nranks > 1:
+            buf = torch.cat([As.reshape(-1), bs, yy.reshape(1)]).contiguous()
+            comm.allreduce_sum(buf)
+            d = self.d
+            As = buf[: d * d].reshape(d, d)
+            bs = buf[d * d: d * d + d]
+            yy = buf[-1]
+        eye = torch.eye(self.d, dtype=As.dtype, device=As.device)
+        lam_tot = self.lam * (n_total if n_total is not None else self.n_local)
+        x = torch.linalg.solve(As + lam_tot * eye, bs)
+        return float(0.5 * x @ (As @ x) - bs @ x + 0.5 * yy + 0.5 * lam_tot * (x @ x))
+
+    def optimum_point(self, comm=None) -> torch.Tensor:
+        As, bs = self.A.sum(0), self.b.sum(0)
+        if comm is not None and comm.nranks > 1:
+            buf = torch.cat([As.reshape(-1), bs]).contiguous()
+            comm.allreduce_sum(buf)
+            As = buf[: self.d * self.d].reshape(self.d, self.d)
+            bs = buf[self.d * self.d:]
+        return torch.linalg.solve(As, bs)
