@@ -1,6 +1,9 @@
 // Shared host/device layout of the chain engine (GADMM / D-GADMM / logistic GADMM).
 #pragma once
 #include <stdint.h>
+#include <hip/hip_runtime.h>
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // Device-resident control block of one solve. Everything the iteration kernels need to decide
 // "what iteration is this / are we done" lives here, so captured hipGraphs replay without host
@@ -66,4 +69,47 @@ struct PhaseArgs {
   int m, max_inner;
   double lam, step, inner_tol;
   int* inner_iters;    // [n_local] diagnostics: inner GD steps used in the last update
+};
+
+// Engine construction arguments (Python mirrors it in gadmm_amd/ops/native.py).
+struct EngineDesc {
+  PhaseArgs base;          // pointers, model params; slots / n_slots / flags filled per phase
+  PhaseSlot* d_slots;      // device buffer, capacity >= 2 * n_local (head plan then tail plan)
+  double* reduced;         // device [ring] (multi-rank)
+  void* comm;              // RcclComm* or null (single rank)
+  hipStream_t stream;
+  int nranks;
+};
+
+struct RunStats {
+  int iters;               // reference `Iter` (first iteration with gap < tol, or last run)
+  int done;                // ChainCtl::done
+  int iterations_launched; // iterations enqueued (>= iters; the rest returned early)
+  int replays;
+  double wall_ms;
+  long long p2p_bytes;     // bytes this rank sent over the chain, iterations 1..iters
+  long long p2p_msgs;
+  long long monitor_bytes; // all-reduce payload of the stopping monitor
+};
+
+
+// Persistent single-launch solve (csrc/kernels/chain_persistent.hip).
+struct PersistArgs {
+  int d, n, start_iter, max_iter, lag, ring, nvar, obj_mode;
+  int deg_to_var[3];
+  int pending_in;
+  double rho, obj0, tol;
+  long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
+  const int* path;          // chain position -> worker
+  const double* Minv;       // [n][nvar][d][d]
+  const double* A;          // [n][d][d]   (obj_mode 0)
+  const double* b;          // [n][d]
+  const double* yy;         // [n]
+  double* theta;            // [n][d]   in: initial, out: final
+  double* mu;               // [n][d]   in/out
+  u32x4* thg;               // [n][d]   theta granules
+  u32x4* objg;              // [ring][n] objective granules
+  unsigned long long* decg; // [ring]   {iter << 32 | code}
+  double* trace;            // [max_iter]
+  ChainCtl* ctl;
 };

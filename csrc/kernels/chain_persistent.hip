@@ -23,27 +23,7 @@
 #include "gadmm_common.h"
 #include "gadmm_chain.h"
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-struct PersistArgs {
-  int d, n, start_iter, max_iter, lag, ring, nvar, obj_mode;
-  int deg_to_var[3];
-  int pending_in;
-  double rho, obj0, tol;
-  long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
-  const int* path;          // chain position -> worker
-  const double* Minv;       // [n][nvar][d][d]
-  const double* A;          // [n][d][d]   (obj_mode 0)
-  const double* b;          // [n][d]
-  const double* yy;         // [n]
-  double* theta;            // [n][d]   in: initial, out: final
-  double* mu;               // [n][d]   in/out
-  u32x4* thg;               // [n][d]   theta granules
-  u32x4* objg;              // [ring][n] objective granules
-  unsigned long long* decg; // [ring]   {iter << 32 | code}
-  double* trace;            // [max_iter]
-  ChainCtl* ctl;
-};
 
 namespace {
 

@@ -14,6 +14,7 @@
 #include <string.h>
 #include <vector>
 #include <chrono>
+#include <cstddef>
 
 #include "gadmm_common.h"
 #include "gadmm_chain.h"
@@ -29,26 +30,6 @@ int gadmm_chain_dual_flush(const PhaseSlot* slots, int n_slots, int d, double rh
 int gadmm_rccl_exchange_rows(void* h, const XchgOp* ops, int nops, double* table, int d, hipStream_t st);
 int gadmm_rccl_allreduce_sum_f64(void* h, const double* send, double* recv, long count, hipStream_t st);
 }
-
-struct EngineDesc {
-  PhaseArgs base;          // pointers, model params; slots / n_slots / flags filled per phase
-  PhaseSlot* d_slots;      // device buffer, capacity >= 2 * n_local (head plan then tail plan)
-  double* reduced;         // device [ring] (multi-rank)
-  void* comm;              // RcclComm* or null (single rank)
-  hipStream_t stream;
-  int nranks;
-};
-
-struct RunStats {
-  int iters;               // reference `Iter` (first iteration with gap < tol, or last run)
-  int done;                // ChainCtl::done
-  int iterations_launched; // iterations enqueued (>= iters; the rest returned early)
-  int replays;
-  double wall_ms;
-  long long p2p_bytes;     // bytes this rank sent over the chain, iterations 1..iters
-  long long p2p_msgs;
-  long long monitor_bytes; // all-reduce payload of the stopping monitor
-};
 
 struct ChainEngine {
   EngineDesc desc;
@@ -297,5 +278,31 @@ int gadmm_chain_engine_run(void* h, int block, int stop_iter, int use_graph, Run
 }
 
 int gadmm_chain_engine_graph_ok(void* h) { return ((ChainEngine*)h)->graph_ok ? 1 : 0; }
+
+// One eager exchange with the current plan (which = 0: after-head messages, 1: after-tail).
+int gadmm_chain_engine_exchange(void* h, int which) {
+  ChainEngine* e = (ChainEngine*)h;
+  if (!e->desc.comm) return 0;
+  auto& ops = which == 0 ? e->xh : e->xt;
+  if (ops.empty()) return 0;
+  int r = gadmm_rccl_exchange_rows(e->desc.comm, ops.data(), (int)ops.size(), e->desc.base.theta, e->desc.base.d,
+                                   e->desc.stream);
+  if (r) return r;
+  GADMM_CHECK(hipStreamSynchronize(e->desc.stream));
+  return 0;
+}
+
+// ABI self-description: sizes and a few offsets of every struct shared with Python (ctypes).
+int gadmm_abi_layout(long long* out, int n) {
+  long long v[] = {(long long)sizeof(PhaseSlot), (long long)sizeof(XchgOp), (long long)sizeof(ChainCtl),
+                   (long long)sizeof(PhaseArgs), (long long)offsetof(PhaseArgs, rho), (long long)offsetof(PhaseArgs, ring),
+                   (long long)offsetof(PhaseArgs, inner_iters), (long long)sizeof(EngineDesc),
+                   (long long)offsetof(EngineDesc, stream), (long long)sizeof(RunStats),
+                   (long long)sizeof(PersistArgs), (long long)offsetof(PersistArgs, rho),
+                   (long long)offsetof(PersistArgs, ctl)};
+  const int k = (int)(sizeof(v) / sizeof(v[0]));
+  for (int i = 0; i < n && i < k; ++i) out[i] = v[i];
+  return k;
+}
 
 }  // extern "C"

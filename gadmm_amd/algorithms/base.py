@@ -93,3 +93,16 @@ def total_bytes(comm) -> int:
 
         dist.all_reduce(t, group=getattr(comm, "control_group", None))
     return int(t.item())
+
+
+def global_objective(comm, f_local, local_ids, n_total: int) -> float:
+    """Sum of per-worker objectives, identical for every rank count: the N-vector of worker
+    objectives is all-reduced (each entry has one non-zero contributor, so the reduction is exact)
+    and summed in worker order."""
+    import torch
+
+    full = torch.zeros(n_total, dtype=torch.float64, device=f_local.device)
+    full[torch.as_tensor(list(local_ids), dtype=torch.long, device=f_local.device)] = f_local
+    if comm is not None and comm.nranks > 1:
+        comm.allreduce_sum(full)
+    return float(full.sum().item())

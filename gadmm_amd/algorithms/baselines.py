@@ -28,7 +28,7 @@ import torch
 
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.topology import Placement, chain_plan
-from .base import RunResult, Stopper, total_bytes
+from .base import RunResult, Stopper, total_bytes, global_objective
 
 TRIGGERSLOT = 10
 
@@ -56,12 +56,11 @@ class _Ctx:
         return self.allsum(g.clone())
 
     def obj(self, theta: torch.Tensor) -> float:
-        f = self.model.objective(theta.unsqueeze(0).expand(len(self.local_ids), -1).contiguous()).sum().reshape(1)
-        return float(self.allsum(f.clone()).item())
+        f = self.model.objective(theta.unsqueeze(0).expand(len(self.local_ids), -1).contiguous())
+        return global_objective(self.comm, f, self.local_ids, self.n_total)
 
     def obj_per_worker(self, theta_loc: torch.Tensor) -> float:
-        f = self.model.objective(theta_loc).sum().reshape(1)
-        return float(self.allsum(f.clone()).item())
+        return global_objective(self.comm, self.model.objective(theta_loc), self.local_ids, self.n_total)
 
     def worker_grad(self, w: int, theta: torch.Tensor) -> torch.Tensor:
         i = self.lidx[w]

@@ -19,7 +19,7 @@ import torch
 
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.topology import Placement
-from .base import RunResult, Stopper, total_bytes
+from .base import RunResult, Stopper, total_bytes, global_objective
 
 
 def dual_averaging(model, local_ids: Sequence[int], n_total: int, alpha: float, obj0: float, tol: float,
@@ -81,10 +81,7 @@ def dual_averaging(model, local_ids: Sequence[int], n_total: int, alpha: float, 
                     comm.send_tensor(Z[0], rank - 1)        # feeds rank-1's next sweep
                 if rank + 1 < R:
                     comm.recv_tensor(z_right, rank + 1)
-        f = model.objective(theta).sum().reshape(1).clone()
-        if R > 1:
-            comm.allreduce_sum(f)
-        if stop.record(float(f.item())):
+        if stop.record(global_objective(comm, model.objective(theta), local_ids, n_total)):
             iters, converged = it, True
             break
     obj, loss, times = stop.arrays()

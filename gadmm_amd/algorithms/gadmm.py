@@ -29,7 +29,7 @@ import torch
 
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.topology import PathSchedule, Placement, chain_plan
-from .base import RunResult, Stopper, total_bytes
+from .base import RunResult, Stopper, total_bytes, global_objective
 
 
 def _gather_rows(theta: torch.Tensor, ids: List[int]) -> torch.Tensor:
@@ -97,6 +97,8 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
     for it in range(start, max_iter + 1):
         if schedule.step(it):
             plan = chain_plan(schedule.path, placement, rank)
+            # new cross-rank neighbours: heads need their (new) tails' current theta first
+            comm.exchange_rows(theta, plan.xchg_tail)
         n_heads = (n_total + 1) // 2
         cc += float(np.sum(schedule.cost)) * (n_heads if cost_quirk else 1)
         com_cost.append(cc)
@@ -139,10 +141,7 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
             mu[li] = m
         th_loc = theta.index_select(0, torch.tensor(local_ids, dtype=torch.long, device=dev))
         f = model.objective(th_loc)
-        tot = f.sum().reshape(1).clone()
-        if comm.nranks > 1:
-            comm.allreduce_sum(tot)
-        if stop.record(float(tot.item())):
+        if stop.record(global_objective(comm, f, local_ids, n_total)):
             iters = it
             converged = True
             break
@@ -222,6 +221,8 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             eng.flush_duals()
             schedule.step(nxt)
             eng.set_path(schedule.path, placement, rank)
+            if comm.nranks > 1:
+                eng.exchange("tail")  # refresh ghost rows of the new cross-rank neighbours
             it = nxt
     torch.cuda.synchronize(model.device)
     wall = time.perf_counter() - t0

@@ -17,7 +17,7 @@ import torch
 
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.topology import Placement
-from .base import RunResult, Stopper, total_bytes
+from .base import RunResult, Stopper, total_bytes, global_objective
 
 
 def standard_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: float, tol: float,
@@ -60,10 +60,7 @@ def standard_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj
             comm.broadcast(theta_hub, hub_rank)
         if len(workers):
             lam[wl] = lam.index_select(0, wl) + rho * (theta.index_select(0, wl) - theta_hub)
-        f = model.objective(theta).sum().reshape(1).clone()
-        if comm.nranks > 1:
-            comm.allreduce_sum(f)
-        if stop.record(float(f.item())):
+        if stop.record(global_objective(comm, model.objective(theta), local_ids, n_total)):
             iters, converged = it, True
             break
     obj, loss, times = stop.arrays()

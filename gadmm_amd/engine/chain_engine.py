@@ -224,6 +224,10 @@ class NativeChainEngine:
                 self.part.zero_()
         native.check(self.lib.gadmm_chain_engine_reset(self.handle, int(start_iter), int(pending)), "reset")
 
+    def exchange(self, which: str = "tail"):
+        """Eager neighbour exchange with the current plan ('head' or 'tail' messages)."""
+        native.check(self.lib.gadmm_chain_engine_exchange(self.handle, 0 if which == "head" else 1), "exchange")
+
     def flush_duals(self):
         """Apply pending head duals with the current chain (before re-chain / checkpoint)."""
         native.check(self.lib.gadmm_chain_engine_flush(self.handle), "flush")

@@ -105,6 +105,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_chain_engine_flush": (c_int, [c_void_p]),
         "gadmm_chain_engine_run": (c_int, [c_void_p, c_int, c_int, c_int, ctypes.POINTER(RunStats)]),
         "gadmm_chain_engine_graph_ok": (c_int, [c_void_p]),
+        "gadmm_chain_engine_exchange": (c_int, [c_void_p, c_int]),
+        "gadmm_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
         "gadmm_chain_persistent_lds": (c_long, [c_int, c_int]),
         "gadmm_chain_persistent_launch": (c_int, [ctypes.POINTER(PersistArgs), c_void_p]),
         "gadmm_rccl_unique_id": (c_int, [ctypes.c_char_p]),

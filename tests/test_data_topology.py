@@ -1,0 +1,127 @@
+"""Data builders (E1/E3 designs from the shipped fixture) and topology (findPath/findPath2/calc_cost)."""
+import numpy as np
+import pytest
+import torch
+
+from gadmm_amd.data import linear_synthetic, logistic_synthetic, gaussian_regression, from_stacked, split_workers
+from gadmm_amd.data.synthetic import fixture_path
+from gadmm_amd.parallel import topology as T
+
+
+def test_fixture_present():
+    assert fixture_path() is not None
+
+
+def test_logistic_design_equals_fixture(log24):
+    from gadmm_amd.data.matfile import load_input_data
+
+    X, y = load_input_data(fixture_path())
+    Xs, ys = log24.stacked()
+    assert np.allclose(Xs.numpy(), X, atol=1e-15)
+    assert np.array_equal(ys.numpy(), np.tile(y[:50], 24))
+
+
+def test_linear_design_structure(lin24):
+    X = lin24.X.numpy()
+    for n in (0, 5, 23):
+        P = (X[n] - np.eye(50)) / 1.3 ** n  # rank-one projector
+        assert np.allclose(P @ P, P, atol=1e-10)
+        assert abs(np.trace(P) - 1.0) < 1e-10
+
+
+def test_more_workers_than_fixture():
+    ds = linear_synthetic(50)
+    X = ds.X.numpy()
+    Ps = (X - np.eye(50)[None]) / (1.3 ** np.arange(50))[:, None, None]
+    Q = np.stack([np.linalg.eigh(P)[1][:, -1] for P in Ps], 1)
+    assert np.allclose(Q.T @ Q, np.eye(50), atol=1e-8)
+
+
+def test_seeded_without_fixture():
+    a = linear_synthetic(10, seed=3, use_fixture=False)
+    b = linear_synthetic(10, seed=3, use_fixture=False)
+    assert torch.equal(a.X, b.X) and a.meta["source"].startswith("seeded")
+
+
+def test_gaussian_shards_reproducible_per_worker():
+    full = gaussian_regression(4, 20, 7, seed=5)
+    part = gaussian_regression(4, 20, 7, seed=5, worker_ids=[2, 3])
+    assert torch.equal(full.X[2:], part.X)
+    lab = gaussian_regression(2, 30, 5, seed=1, labels="logistic")
+    assert set(lab.y.unique().tolist()) <= {-1.0, 1.0}
+
+
+def test_stacked_split():
+    X = torch.randn(103, 4, dtype=torch.float64)
+    y = torch.randn(103, dtype=torch.float64)
+    ds = from_stacked(X, y, 25)
+    assert ds.num_workers == 4 and ds.rows_per_worker == 25
+    ds2 = split_workers(X, y, 10)
+    assert ds2.num_workers == 10 and ds2.rows_per_worker == 10
+
+
+def test_find_path_is_hamiltonian_from_node0():
+    rng = np.random.default_rng(0)
+    path, cost, d2 = T.find_path(24, rng)
+    assert path[0] == 0 and sorted(path) == list(range(24))
+    assert len(cost) == 23
+    assert np.allclose(cost, [d2[path[k], path[k + 1]] for k in range(23)])
+    # greedy property: each hop is the nearest unvisited node
+    seen = {0}
+    for k in range(23):
+        cand = [m for m in range(24) if m not in seen]
+        assert path[k + 1] == min(cand, key=lambda m: (d2[path[k], m], m))
+        seen.add(path[k + 1])
+
+
+def test_find_path2_energy_model():
+    rng = np.random.default_rng(1)
+    path, cost, d2, pc, center = T.find_path2(10, rng)
+    eta, R, B = 1e-6, 10e6, 2e6
+    for k in range(9):
+        assert np.isclose(cost[k], d2[path[k], path[k + 1]] * eta * B * 2 ** (R / B))
+    # findPath2.m:26-29: P_central = 1/2 d_c^2 eta B 2^(2R/B); the centre node costs 0
+    assert pc[center] == 0.0
+    assert np.all(pc >= 0)
+    assert T.star_cost(pc) == pytest.approx(pc.sum() + pc.max())
+
+
+def test_calc_cost_indexing():
+    grid = np.arange(16, dtype=float).reshape(4, 4)
+    assert list(T.calc_cost(grid, [2, 0, 3, 1])) == [grid[2, 0], grid[0, 3], grid[3, 1]]
+
+
+def test_rechain_rule():
+    assert not T.rechain_iteration(1, 1)
+    assert T.rechain_iteration(2, 1)
+    assert T.rechain_iteration(10, 10) and not T.rechain_iteration(11, 10)
+    assert not T.rechain_iteration(10 ** 6, 1e9)
+    assert not T.rechain_iteration(5, float("inf"))
+
+
+@pytest.mark.parametrize("n,r", [(24, 1), (24, 2), (24, 8), (7, 3), (5, 5)])
+def test_chain_plan_messages_are_consistent(n, r):
+    rng = np.random.default_rng(n * 7 + r)
+    pl = T.Placement.contiguous(n, r)
+    for path in (list(range(n)), list(rng.permutation(n))):
+        plans = [T.chain_plan(path, pl, k) for k in range(r)]
+        # every worker appears in exactly one slot on its owner
+        slots = [(k, s.gid) for k, p in enumerate(plans) for s in p.head + p.tail]
+        assert sorted(g for _, g in slots) == list(range(n))
+        assert all(pl.owner[g] == k for k, g in slots)
+        # every send has a matching receive on the peer, per phase
+        for phase in ("xchg_head", "xchg_tail"):
+            sends = sorted((k, peer, row) for k, p in enumerate(plans) for peer, row, s in getattr(p, phase) if s)
+            recvs = sorted((peer, k, row) for k, p in enumerate(plans) for peer, row, s in getattr(p, phase) if not s)
+            assert sends == recvs
+        assert T.chain_message_count(path, pl) == sum(p.send_rows() for p in plans)
+        if path == list(range(n)):
+            assert T.chain_message_count(path, pl) == 2 * (r - 1)
+
+
+def test_path_schedule_deterministic():
+    a = T.PathSchedule(8, list(range(8)), np.ones(7), 2, seed=9)
+    b = T.PathSchedule(8, list(range(8)), np.ones(7), 2, seed=9)
+    for it in range(1, 20):
+        assert a.step(it) == b.step(it)
+        assert a.path == b.path

@@ -1,0 +1,181 @@
+"""Multi-process (gloo, CPU) runs reproduce the single-process results: chain p2p schedule, star
+reduce/broadcast, LAG server uploads, dual-averaging pipeline (BASELINE.json configs[0])."""
+import numpy as np
+import pytest
+
+from gadmm_amd.parallel.launch import spawn
+
+
+def _rank_fn(rank, world, algo, params):
+    import torch
+    from gadmm_amd.data import linear_synthetic, logistic_synthetic
+    from gadmm_amd.models import LinearRegression, LogisticRegression
+    from gadmm_amd.parallel.comm import TorchDistComm
+    from gadmm_amd.parallel.topology import Placement
+    from gadmm_amd import algorithms as A
+
+    n = params.get("n", 24)
+    comm = TorchDistComm()
+    pl = Placement.contiguous(n, world)
+    local = pl.local_workers(rank)
+    if algo.startswith("log"):
+        ds = logistic_synthetic(n)
+        m = LogisticRegression(ds.X[local], ds.y[local], 1e-5)
+    else:
+        ds = linear_synthetic(n)
+        m = LinearRegression(ds.X[local], ds.y[local])
+    obj0 = params["obj0"]
+    if algo == "gadmm":
+        r = A.chain_admm(m, local, n, params["rho"], obj0, params["tol"], params["max_iter"], comm=comm,
+                         placement=pl, backend="torch", record_theta=True)
+    elif algo == "dgadmm":
+        from gadmm_amd.parallel.topology import PathSchedule
+        s = PathSchedule(n, params["path"], params["cost"], params["coh"], seed=params["seed"])
+        r = A.chain_admm(m, local, n, params["rho"], obj0, params["tol"], params["max_iter"], comm=comm,
+                         placement=pl, schedule=s, backend="torch")
+    elif algo == "loggd":
+        r = A.chain_admm(m, local, n, params["rho"], obj0, params["tol"], params["max_iter"], comm=comm,
+                         placement=pl, local_solver="gd", step=2.2, backend="torch")
+    elif algo == "star":
+        r = A.standard_admm(m, local, n, 1.0, obj0, 1e-4, 1000, comm=comm, placement=pl)
+    elif algo == "dualavg":
+        c = A.global_constants(m, comm)
+        r = A.dual_averaging(m, local, n, c["stepsize"], obj0, 1e-4, params["max_iter"], comm=comm, placement=pl)
+    elif algo == "lag":
+        c = A.global_constants(m, comm)
+        from gadmm_amd.algorithms.baselines import _Ctx, _gather_hmax
+        hm = _gather_hmax(_Ctx(m, local, n, comm, pl), c["hmax_local"])
+        r = A.lag(m, local, n, params["max_iter"], obj0, c["stepsize"], hm, params["variant"], comm=comm, placement=pl)
+    elif algo == "iag":
+        c = A.global_constants(m, comm)
+        from gadmm_amd.algorithms.baselines import _Ctx, _gather_hmax
+        hm = _gather_hmax(_Ctx(m, local, n, comm, pl), c["hmax_local"])
+        r = A.iag(m, local, n, params["max_iter"], obj0, c["stepsize"], params["mode"], hm, comm=comm, placement=pl)
+    elif algo == "dgd":
+        c = A.global_constants(m, comm)
+        r = A.decentralized_gd(m, local, n, params["max_iter"], obj0, c["stepsize"], comm=comm, placement=pl)
+    elif algo == "gd":
+        c = A.global_constants(m, comm)
+        r = A.gradient_descent(m, local, n, params["max_iter"], obj0, c["stepsize"], comm=comm, placement=pl)
+    elif algo == "optimum":
+        return m.optimum(comm, n_total=n)
+    else:
+        raise ValueError(algo)
+    out = {"iters": r.iters, "obj": r.obj, "bytes": r.bytes_sent, "bytes_total": r.bytes_total,
+           "extra": {k: v for k, v in r.extra.items() if isinstance(v, (int, float, str))}}
+    if r.theta is not None:
+        out["theta"] = r.theta
+    return out
+
+
+def _single(algo, params):
+    """Same computation in one process (LocalComm)."""
+    import torch.distributed as dist  # noqa: F401
+    from gadmm_amd.data import linear_synthetic, logistic_synthetic
+    from gadmm_amd.models import LinearRegression, LogisticRegression
+    from gadmm_amd import algorithms as A
+    n = params.get("n", 24)
+    if algo == "gadmm":
+        ds = linear_synthetic(n)
+        m = LinearRegression(ds.X, ds.y)
+        return A.chain_admm(m, list(range(n)), n, params["rho"], params["obj0"], params["tol"], params["max_iter"],
+                            backend="torch", record_theta=True)
+    raise ValueError(algo)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gadmm_gloo_matches_single_process(world, lin_obj0):
+    params = {"rho": 5.0, "tol": 1e-8, "max_iter": 2000, "obj0": lin_obj0}
+    res = spawn(_rank_fn, world, "gadmm", params)
+    single = _single("gadmm", params)
+    for r in res:
+        assert r["iters"] == single.iters == 758
+        assert np.allclose(r["obj"], single.obj, rtol=1e-12)
+    # local rows of theta are bit-identical to the single-process computation
+    from gadmm_amd.parallel.topology import Placement
+    pl = Placement.contiguous(24, world)
+    for k, r in enumerate(res):
+        loc = pl.local_workers(k)
+        assert np.array_equal(r["theta"][loc], single.theta[loc])
+    # bytes: 2 (world-1) boundary messages of d doubles per iteration
+    assert sum(r["bytes"] for r in res) == 2 * (world - 1) * 50 * 8 * 758
+
+
+def test_dgadmm_gloo(lin_obj0):
+    from gadmm_amd.parallel import topology as T
+    rng = np.random.default_rng(11)
+    p0, c0, _ = T.find_path(24, rng)
+    params = {"rho": 1.0, "tol": 1e-4, "max_iter": 800, "obj0": lin_obj0, "path": p0, "cost": c0, "coh": 10,
+              "seed": 4}
+    res = spawn(_rank_fn, 2, "dgadmm", params)
+    from gadmm_amd.data import linear_synthetic
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import dynamic_group_admm
+    ds = linear_synthetic(24)
+    single = dynamic_group_admm(LinearRegression(ds.X, ds.y), 1.0, lin_obj0, 1e-4, 800, p0, c0, 10, seed=4,
+                                backend="torch")
+    assert res[0]["iters"] == res[1]["iters"] == single.iters
+    assert np.allclose(res[0]["obj"], single.obj, rtol=1e-10)
+
+
+def test_logistic_gd_gloo(log_obj0):
+    res = spawn(_rank_fn, 2, "loggd", {"rho": 2e-4, "tol": 1e-4, "max_iter": 200, "obj0": log_obj0})
+    assert res[0]["iters"] == res[1]["iters"] == 53
+
+
+def test_star_admm_gloo(lin_obj0):
+    res = spawn(_rank_fn, 3, "star", {"obj0": lin_obj0})
+    assert all(r["iters"] == 348 for r in res)
+
+
+def test_dual_averaging_pipeline_gloo(lin_obj0):
+    from gadmm_amd.data import linear_synthetic
+    from gadmm_amd.oracle import reference as R
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import global_constants
+    res = spawn(_rank_fn, 3, "dualavg", {"obj0": lin_obj0, "max_iter": 150})
+    ds = linear_synthetic(24)
+    c = global_constants(LinearRegression(ds.X, ds.y))
+    X, y = ds.numpy()
+    o = R.dual_averaging(X, y, 150, lin_obj0, 1e-4, c["stepsize"])
+    for r in res:
+        assert np.allclose(r["obj"], o.obj, rtol=1e-11)
+
+
+@pytest.mark.parametrize("variant", ["PS", "WK"])
+def test_lag_server_uploads_gloo(variant, lin_obj0):
+    from gadmm_amd.data import linear_synthetic
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import lag, global_constants
+    res = spawn(_rank_fn, 2, "lag", {"obj0": lin_obj0, "max_iter": 400, "variant": variant})
+    ds = linear_synthetic(24)
+    m = LinearRegression(ds.X, ds.y)
+    c = global_constants(m)
+    single = lag(m, list(range(24)), 24, 400, lin_obj0, c["stepsize"], m.hmax(), variant)
+    for r in res:
+        assert np.allclose(r["obj"], single.obj, rtol=1e-9)
+        assert r["extra"]["uploads"] == single.extra["uploads"]
+
+
+def test_iag_dgd_gd_gloo(lin_obj0):
+    from gadmm_amd.data import linear_synthetic
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd import algorithms as A
+    ds = linear_synthetic(24)
+    m = LinearRegression(ds.X, ds.y)
+    c = A.global_constants(m)
+    for algo, kw, single in (
+            ("iag", {"mode": "random"}, lambda: A.iag(m, list(range(24)), 24, 200, lin_obj0, c["stepsize"], "random",
+                                                      m.hmax())),
+            ("dgd", {}, lambda: A.decentralized_gd(m, list(range(24)), 24, 200, lin_obj0, c["stepsize"])),
+            ("gd", {}, lambda: A.gradient_descent(m, list(range(24)), 24, 200, lin_obj0, c["stepsize"]))):
+        params = {"obj0": lin_obj0, "max_iter": 200, **kw}
+        res = spawn(_rank_fn, 2, algo, params)
+        s = single()
+        for r in res:
+            assert np.allclose(r["obj"], s.obj, rtol=1e-9), algo
+
+
+def test_global_optimum_allreduce(lin_obj0):
+    res = spawn(_rank_fn, 2, "optimum", {"obj0": lin_obj0})
+    assert res[0] == pytest.approx(lin_obj0, rel=1e-12)
