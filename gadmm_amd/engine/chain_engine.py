@@ -47,7 +47,7 @@ class NativeChainEngine:
                  model: str = "linear", rho: float = 1.0, obj0: float = 0.0, tol: float = 1e-4,
                  max_iter: int = 1000, lam: float = 0.0, step: float = 0.0, max_inner: int = 100,
                  inner_tol: float = 1e-4, comm=None, block: int = 16, stream: Optional[torch.cuda.Stream] = None,
-                 precomputed=None):
+                 precomputed=None, force_monitor: bool = False):
         if not X_loc.is_cuda:
             raise ValueError("NativeChainEngine runs on a HIP device; use the torch algorithms on CPU")
         self.lib = native.require()
@@ -60,6 +60,12 @@ class NativeChainEngine:
         self.m = int(X_loc.shape[1])
         self.comm = comm
         self.nranks = 1 if comm is None else comm.nranks
+        if force_monitor:
+            # exercise the multi-rank stop path (partial-objective ring + RCCL all-reduce + monitor
+            # kernel) with a 1-rank communicator: used by the single-GPU tests
+            if comm is None:
+                raise ValueError("force_monitor needs a communicator")
+            self.nranks = 2
         self.block = int(block)
         self.ring = max(self.block, 1)
         # A dedicated (non-legacy) stream: hipGraph capture is not permitted on the null stream.
