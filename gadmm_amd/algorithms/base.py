@@ -48,6 +48,9 @@ class RunResult:
             "comm_units": float(self.comm_units[self.iters - 1]) if len(self.comm_units) >= self.iters > 0 else None,
             "bytes_sent": int(self.bytes_sent),
             "bytes_total": int(self.bytes_total),
+            "logical_bytes": (float(self.comm_units[self.iters - 1]) * 8 * int(self.extra["dim"])
+                              if self.extra.get("dim") and len(self.comm_units) >= self.iters > 0
+                              and not self.extra.get("energy_units") else None),
             **{k: v for k, v in self.extra.items() if isinstance(v, (int, float, str, bool))},
         }
 
@@ -76,11 +79,17 @@ class Stopper:
         return np.asarray(self.obj), np.asarray(self.loss), np.asarray(self.times)
 
 
-def total_bytes(comm) -> int:
-    """Sum of bytes sent over all ranks (one scalar all-reduce, outside any timed loop)."""
+def run_bytes(comm, snap) -> int:
+    """This rank's algorithm bytes since ``snap`` (p2p + algorithmic collectives, no monitoring)."""
+    d = comm.stats.delta(snap)
+    return int(d["bytes_sent"] + d["coll_bytes"])
+
+
+def total_bytes(comm, snap=None) -> int:
+    """Algorithm bytes summed over all ranks (one scalar all-reduce, outside any timed loop)."""
     import torch
 
-    b = int(comm.stats.bytes_sent) + int(comm.stats.coll_bytes)
+    b = run_bytes(comm, snap) if snap is not None else int(comm.stats.bytes_sent) + int(comm.stats.coll_bytes)
     if comm.nranks <= 1:
         return b
     t = torch.tensor([float(b)], dtype=torch.float64)
@@ -105,4 +114,7 @@ def global_objective(comm, f_local, local_ids, n_total: int) -> float:
     full[torch.as_tensor(list(local_ids), dtype=torch.long, device=f_local.device)] = f_local
     if comm is not None and comm.nranks > 1:
         comm.allreduce_sum(full)
+        nb = full.numel() * full.element_size()
+        comm.stats.coll_bytes -= nb       # monitoring, not algorithm traffic
+        comm.stats.monitor_bytes += nb
     return float(full.sum().item())

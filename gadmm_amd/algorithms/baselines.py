@@ -28,7 +28,7 @@ import torch
 
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.topology import Placement, chain_plan
-from .base import RunResult, Stopper, total_bytes, global_objective
+from .base import RunResult, Stopper, total_bytes, global_objective, run_bytes
 
 TRIGGERSLOT = 10
 
@@ -43,6 +43,7 @@ class _Ctx:
         self.d = model.d
         self.dev = model.device
         self.lidx = {w: i for i, w in enumerate(self.local_ids)}
+        self.snap = self.comm.stats.snapshot()
 
     def allsum(self, t: torch.Tensor) -> torch.Tensor:
         t = t.contiguous()
@@ -96,8 +97,8 @@ def _result(name, stop: Stopper, ctx: _Ctx, units: np.ndarray, converged: bool, 
     obj, loss, times = stop.arrays()
     return RunResult(algorithm=name, obj=obj, loss=loss, iters=iters, converged=converged,
                      wall_s=float(times[-1]) if len(times) else 0.0, time_trace=times, comm_units=units,
-                     bytes_sent=int(ctx.comm.stats.bytes_sent + ctx.comm.stats.coll_bytes),
-                     bytes_total=total_bytes(ctx.comm), extra=extra)
+                     bytes_sent=run_bytes(ctx.comm, ctx.snap), bytes_total=total_bytes(ctx.comm, ctx.snap),
+                     extra=extra)
 
 
 # ------------------------------------------------------------------------------------------------- GD

@@ -19,7 +19,7 @@ import torch
 
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.topology import Placement
-from .base import RunResult, Stopper, total_bytes, global_objective
+from .base import RunResult, Stopper, total_bytes, global_objective, run_bytes
 
 
 def dual_averaging(model, local_ids: Sequence[int], n_total: int, alpha: float, obj0: float, tol: float,
@@ -39,6 +39,7 @@ def dual_averaging(model, local_ids: Sequence[int], n_total: int, alpha: float, 
     z_left = torch.zeros(d, dtype=torch.float64, device=dev)   # Z of worker first-1
     z_right = torch.zeros(d, dtype=torch.float64, device=dev)  # Z of worker last+1 (previous sweep)
     stop = Stopper(obj0, tol, max_iter)
+    snap = comm.stats.snapshot()
     iters, converged = max_iter, False
     for it in range(1, max_iter + 1):
         g_all = model.gradient(theta)
@@ -89,5 +90,5 @@ def dual_averaging(model, local_ids: Sequence[int], n_total: int, alpha: float, 
     return RunResult(algorithm=name, obj=obj, loss=loss, iters=iters if converged else n, converged=converged,
                      wall_s=float(times[-1]) if n else 0.0, time_trace=times,
                      comm_units=np.arange(1, n + 1, dtype=np.float64) * n_total,
-                     bytes_sent=int(comm.stats.bytes_sent), bytes_total=total_bytes(comm),
+                     bytes_sent=run_bytes(comm, snap), bytes_total=total_bytes(comm, snap),
                      extra={"jacobi": jacobi, "nranks": R})

@@ -29,7 +29,7 @@ import torch
 
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.topology import PathSchedule, Placement, chain_plan
-from .base import RunResult, Stopper, total_bytes, global_objective
+from .base import RunResult, Stopper, total_bytes, global_objective, run_bytes
 
 
 def _gather_rows(theta: torch.Tensor, ids: List[int]) -> torch.Tensor:
@@ -88,6 +88,7 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
         mu = torch.zeros((len(local_ids), d), dtype=torch.float64, device=dev)
         start = 1
     stop = Stopper(obj0, tol, max_iter)
+    snap = comm.stats.snapshot()
     plan = chain_plan(schedule.path, placement, rank)
     cc = 0.0
     com_cost: List[float] = []
@@ -150,10 +151,11 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
     res = RunResult(algorithm=name, obj=obj, loss=loss, iters=iters if converged else (start - 1 + n_it),
                     converged=converged, wall_s=float(times[-1]) if n_it else 0.0, time_trace=times,
                     comm_units=np.arange(start, start + n_it, dtype=np.float64) * n_total,
-                    com_cost=np.asarray(com_cost), bytes_sent=int(comm.stats.bytes_sent),
-                    bytes_total=total_bytes(comm),
+                    com_cost=np.asarray(com_cost), bytes_sent=run_bytes(comm, snap),
+                    bytes_total=total_bytes(comm, snap),
                     extra={"backend": "torch", "rank": rank, "nranks": comm.nranks, "solver": local_solver,
-                           "inner_steps_mean": float(np.mean(inner_used)) if inner_used else 0.0})
+                           "inner_steps_mean": float(np.mean(inner_used)) if inner_used else 0.0,
+                           "monitor_bytes": int(comm.stats.delta(snap)["monitor_bytes"])})
     res.extra["state"] = (theta, mu, (iters if converged else start - 1 + n_it) + 1)
     if record_theta:
         res.theta = theta.cpu().numpy()

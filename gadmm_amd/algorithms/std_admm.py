@@ -17,7 +17,7 @@ import torch
 
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.topology import Placement
-from .base import RunResult, Stopper, total_bytes, global_objective
+from .base import RunResult, Stopper, total_bytes, global_objective, run_bytes
 
 
 def standard_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: float, tol: float,
@@ -39,6 +39,7 @@ def standard_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj
     theta = torch.zeros((len(local_ids), d), dtype=torch.float64, device=dev)
     theta_hub = torch.zeros(d, dtype=torch.float64, device=dev)
     stop = Stopper(obj0, tol, max_iter)
+    snap = comm.stats.snapshot()
     iters, converged = max_iter, False
     for it in range(1, max_iter + 1):
         if len(workers):
@@ -68,5 +69,5 @@ def standard_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj
     return RunResult(algorithm=name, obj=obj, loss=loss, iters=iters if converged else n, converged=converged,
                      wall_s=float(times[-1]) if n else 0.0, time_trace=times,
                      comm_units=np.arange(1, n + 1, dtype=np.float64) * 2 * (n_total - 1),
-                     bytes_sent=int(comm.stats.bytes_sent), bytes_total=total_bytes(comm),
+                     bytes_sent=run_bytes(comm, snap), bytes_total=total_bytes(comm, snap),
                      extra={"hub": hub, "hub_rank": hub_rank, "nranks": comm.nranks})

@@ -1,0 +1,249 @@
+"""Shared machinery of the entry points: process/device set-up, per-rank data, model, oracle,
+GADMM sweeps, the baseline bundle, outputs.
+
+Launch forms:
+    python -m gadmm_amd LinearRegression_Synthetic                      # 1 process (GPU if present)
+    python -m gadmm_amd LinearRegression_Synthetic --device cpu --cpu-ranks 2   # gloo plumbing
+    torchrun --nproc-per-node 8 -m gadmm_amd LinearRegression_Synthetic      # 8 x MI355X, RCCL
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..config import ExperimentConfig, get_preset, parse_overrides
+from ..data import ShardedDataset, linear_synthetic, logistic_synthetic, gaussian_regression
+from ..data.sharding import from_stacked, split_workers
+from ..models import make_model
+from ..parallel.topology import Placement
+from ..utils.metrics import RunWriter, plot_three_panel
+
+
+class Session:
+    def __init__(self, rank: int, world: int, device: torch.device, comm):
+        self.rank, self.world, self.device, self.comm = rank, world, device, comm
+
+    @property
+    def is_root(self) -> bool:
+        return self.rank == 0
+
+    def log(self, *a):
+        if self.is_root:
+            print(*a, flush=True)
+
+
+def make_session(device: str = "auto") -> Session:
+    from ..parallel.comm import LocalComm
+    from ..parallel.launch import setup_rank
+
+    if device == "auto":
+        device = "cuda" if torch.cuda.is_available() else "cpu"
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if device == "cuda":
+        rank, world, local_rank, dev, comm = setup_rank("rccl")
+    else:
+        rank, world, local_rank, dev, comm = setup_rank("gloo")
+    return Session(rank, world, dev, comm)
+
+
+def full_dataset(cfg: ExperimentConfig) -> ShardedDataset:
+    if cfg.data == "linear_synthetic":
+        return linear_synthetic(cfg.num_workers, seed=cfg.seed)
+    if cfg.data == "logistic_synthetic":
+        return logistic_synthetic(cfg.num_workers, seed=cfg.seed)
+    if cfg.data in ("bodyfat", "derm"):
+        if cfg.data_dir:
+            from ..data.matfile import load_uci_dir
+
+            X, y = load_uci_dir(cfg.data_dir)
+            Xt, yt = torch.from_numpy(X), torch.from_numpy(y)
+            if cfg.data == "bodyfat":
+                return from_stacked(Xt, yt, cfg.rows_per_worker, name="bodyfat")
+            return split_workers(Xt, yt, cfg.num_workers, name="derm")
+        # real-shaped synthetic stand-in (the UCI files are not shipped with the reference)
+        if cfg.data == "bodyfat":
+            n = cfg.total_rows // cfg.rows_per_worker
+            return gaussian_regression(n, cfg.rows_per_worker, cfg.dim, seed=cfg.seed, labels="linear")
+        per = cfg.total_rows // cfg.num_workers
+        return gaussian_regression(cfg.num_workers, per, cfg.dim, seed=cfg.seed, labels="logistic")
+    if cfg.data == "gaussian":
+        return gaussian_regression(cfg.num_workers, cfg.rows_per_worker, cfg.dim, seed=cfg.seed,
+                                   labels="logistic" if cfg.model == "logistic" else "linear")
+    raise ValueError("unknown data %r" % cfg.data)
+
+
+class Problem:
+    """This rank's slice of an experiment: local shards, model, the global optimum."""
+
+    def __init__(self, cfg: ExperimentConfig, sess: Session, ds: Optional[ShardedDataset] = None):
+        ds = ds if ds is not None else full_dataset(cfg)
+        self.cfg = cfg
+        self.n_total = ds.num_workers
+        self.placement = Placement.contiguous(self.n_total, sess.world)
+        self.local_ids = self.placement.local_workers(sess.rank)
+        loc = ds.subset(self.local_ids).to(sess.device)
+        self.model = make_model(cfg.model, loc.X.contiguous(), loc.y.contiguous(), lam=cfg.lam)
+        self.dataset_meta = dict(ds.meta, name=ds.name, N=ds.num_workers, m=ds.rows_per_worker, d=ds.dim)
+        if cfg.model == "linear":
+            self.obj0 = self.model.optimum(sess.comm if sess.world > 1 else None, n_total=self.n_total)
+        else:
+            self.obj0 = self.model.optimum(sess.comm if sess.world > 1 else None, n_total=self.n_total)
+
+
+def parse_args(entry: str, argv=None):
+    ap = argparse.ArgumentParser(prog="python -m gadmm_amd %s" % entry,
+                                 description="Reference entry point %s on the MI355X framework" % entry)
+    ap.add_argument("--device", default="auto", choices=["auto", "cpu", "cuda"])
+    ap.add_argument("--cpu-ranks", type=int, default=0, help="spawn N gloo ranks on this host (CPU plumbing)")
+    ap.add_argument("--out", default=None, help="output directory (default runs/<entry>)")
+    ap.add_argument("--quick", action="store_true", help="reduced iteration budgets (smoke runs)")
+    ap.add_argument("--set", nargs="*", default=[], metavar="KEY=VALUE", help="override preset fields")
+    ap.add_argument("--no-baselines", action="store_true")
+    ap.add_argument("--no-plot", action="store_true")
+    ap.add_argument("--tol", type=float, default=None, help="override the stopping gap (reference: 1e-4)")
+    ap.add_argument("--backend", default="auto", choices=["auto", "torch", "native"])
+    ap.add_argument("--checkpoint", default=None, help="write per-worker checkpoints of the last GADMM run here")
+    a = ap.parse_args(argv)
+    cfg = parse_overrides(get_preset(entry), a.set)
+    if a.quick:
+        cfg = cfg.quick()
+    if a.no_baselines:
+        cfg = cfg.override(run_baselines=False, run_dualavg=False)
+    if a.tol is not None:
+        cfg = cfg.override(acc=a.tol)
+    return a, cfg
+
+
+def run_entry(entry: str, body, argv=None) -> Dict:
+    """Parse args, launch (optionally spawning gloo ranks), run ``body(cfg, sess, args) -> dict``."""
+    args, cfg = parse_args(entry, argv)
+    if args.cpu_ranks and args.cpu_ranks > 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        from ..parallel.launch import spawn
+
+        outs = spawn(_spawned, args.cpu_ranks, entry, body, argv_without_ranks(argv))
+        return outs[0]
+    sess = make_session(args.device)
+    return _run(entry, body, cfg, sess, args)
+
+
+def argv_without_ranks(argv):
+    import sys
+
+    argv = list(sys.argv[2:] if argv is None else argv)
+    out, skip = [], False
+    for i, a in enumerate(argv):
+        if skip:
+            skip = False
+            continue
+        if a == "--cpu-ranks":
+            skip = True
+            continue
+        if a.startswith("--cpu-ranks="):
+            continue
+        out.append(a)
+    return out + ["--device", "cpu"]
+
+
+def _spawned(rank, world, entry, body, argv):
+    from ..parallel.comm import TorchDistComm
+
+    args, cfg = parse_args(entry, argv)
+    sess = Session(rank, world, torch.device("cpu"), TorchDistComm())
+    return _run(entry, body, cfg, sess, args)
+
+
+def _run(entry, body, cfg, sess, args) -> Dict:
+    out_dir = args.out or os.path.join("runs", entry)
+    writer = RunWriter(out_dir, sess.rank)
+    t0 = time.perf_counter()
+    sess.log("[%s] device=%s ranks=%d  (reference: %s)" % (entry, sess.device, sess.world, cfg.reference))
+    res = body(cfg, sess, args, writer)
+    res["wall_s"] = time.perf_counter() - t0
+    dim = (res.get("dataset") or {}).get("d")
+    for k, r in res.get("runs", {}).items():
+        r.extra.setdefault("dim", dim)
+        writer.add(k, r)
+    summary = writer.close({"entry": entry, "config": cfg.__dict__, "device": str(sess.device), "ranks": sess.world,
+                            **{k: v for k, v in res.items() if k not in ("runs", "figure_groups")}})
+    if sess.is_root and not args.no_plot:
+        for title, group in res.get("figure_groups", {}).items():
+            plot_three_panel(group, os.path.join(out_dir, _fname(title) + ".png"), title=title)
+    if sess.is_root:
+        for k, r in res.get("runs", {}).items():
+            s = r.summary()
+            print("  %-34s iters=%-7s converged=%-5s gap=%-10.3g wall=%.3fs comm_units=%s bytes=%s" % (
+                k, s["iters"], s["converged"], s["final_loss"] if s["final_loss"] is not None else float("nan"),
+                s["wall_s"], s["comm_units"], s["bytes_total"]), flush=True)
+        print("[%s] summary -> %s" % (entry, summary), flush=True)
+    res["summary_path"] = summary
+    res.pop("figure_groups", None)
+    return {k: v for k, v in res.items() if k != "runs"} | {"runs": {k: r.summary() for k, r in res.get("runs", {}).items()}}
+
+
+def _fname(s: str) -> str:
+    return "".join(c if c.isalnum() or c in "-_" else "_" for c in s)
+
+
+# ----------------------------------------------------------------------------------- building blocks
+def gadmm_sweep(prob: Problem, sess: Session, backend: str = "auto") -> Dict[str, object]:
+    from ..algorithms import chain_admm
+
+    cfg = prob.cfg
+    out = {}
+    for rho in cfg.rhos:
+        solver = "closed" if cfg.model == "linear" else "gd"
+        r = chain_admm(prob.model, prob.local_ids, prob.n_total, rho, prob.obj0, cfg.acc, cfg.gadmm_iters,
+                       comm=sess.comm, placement=prob.placement, local_solver=solver, step=cfg.gd_step,
+                       max_inner=cfg.max_inner, backend=backend, name="GADMM(rho=%g)" % rho)
+        r.extra.pop("engine_obj", None)
+        out["GADMM_rho%g" % rho] = r
+    return out
+
+
+def baselines(prob: Problem, sess: Session) -> Dict[str, object]:
+    from ..algorithms import gd_dgd_lag, dual_averaging
+
+    cfg = prob.cfg
+    out: Dict[str, object] = {}
+    stepsize = None
+    if cfg.run_baselines:
+        b = gd_dgd_lag(prob.model, prob.local_ids, prob.n_total, cfg.baseline_iters,
+                       prob.obj0 if cfg.model == "linear" else None, comm=sess.comm, placement=prob.placement,
+                       accuracy=cfg.acc)
+        stepsize = b["stepsize"]
+        for k in ("GD", "DGD", "LAG-PS", "LAG-WK", "cIAG", "R-IAG"):
+            if k in b:
+                out[k] = b[k]
+        if cfg.model == "logistic":
+            # GD_DGD_LAG_logistic returns obj1 = last GD objective as the reference optimum
+            out["_obj0_gd"] = b["obj0"]
+    if cfg.run_dualavg:
+        if stepsize is None:
+            from ..algorithms import global_constants
+
+            stepsize = global_constants(prob.model, sess.comm)["stepsize"]
+        out["DualAvg"] = dual_averaging(prob.model, prob.local_ids, prob.n_total, stepsize, prob.obj0, cfg.acc,
+                                        cfg.dualavg_iters or cfg.baseline_iters, comm=sess.comm,
+                                        placement=prob.placement)
+    return out
+
+
+def maybe_checkpoint(args, sess: Session, prob: Problem, result, rho: float, name: str):
+    """Write per-worker checkpoints of a chain-ADMM result (torch backend state)."""
+    if not args.checkpoint:
+        return None
+    from ..utils.checkpoint import save_checkpoint
+
+    st = result.extra.get("state")
+    if st is None:
+        return None
+    theta, mu, nxt = st
+    save_checkpoint(args.checkpoint, sess.rank, prob.local_ids, theta, mu, nxt, list(range(prob.n_total)),
+                    {"algorithm": name, "rho": rho, "obj0": prob.obj0, "entry": prob.cfg.name})
+    return args.checkpoint

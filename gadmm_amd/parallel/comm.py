@@ -1,8 +1,9 @@
 """Communication backends behind one small interface (SURVEY.md §2.6 call-site inventory).
 
 * ``LocalComm``   — one rank owns every logical worker; neighbour "messages" are reads of the local
-  theta table (the analogue of the reference's column reads, ``out(:,ii-1)``), but bytes and
-  message counts are still recorded as if each logical worker were its own node.
+  theta table (the analogue of the reference's column reads, ``out(:,ii-1)``). No fabric bytes; the
+  per-worker ("logical") traffic is reported from the reference communication units
+  (``RunResult.summary()['logical_bytes']``).
 * ``TorchDistComm`` — ``torch.distributed`` point-to-point + collectives. With the ``gloo`` backend
   this is the CPU plumbing config of BASELINE.json (configs[0]); with ``nccl`` (= RCCL on ROCm) it
   runs on MI355X ranks.
@@ -25,15 +26,25 @@ Op = Tuple[int, int, int]  # (peer, row, is_send)
 
 
 class CommStats:
+    """Per-rank byte counters. ``bytes_sent``: point-to-point payload; ``coll_bytes``: payload this
+    rank contributed to collectives that belong to the algorithm (GD all-reduce, star reduce/bcast);
+    ``monitor_bytes``: collectives of the stopping monitor only (global objective), which the
+    reference computes for free in shared memory and a deployment would run every K iterations."""
+
+    FIELDS = ("bytes_sent", "bytes_recv", "msgs_sent", "coll_bytes", "monitor_bytes")
+
     def __init__(self):
-        self.bytes_sent = 0
-        self.bytes_recv = 0
-        self.msgs_sent = 0
-        self.coll_bytes = 0
+        for f in self.FIELDS:
+            setattr(self, f, 0)
 
     def as_dict(self):
-        return {"bytes_sent": self.bytes_sent, "bytes_recv": self.bytes_recv, "msgs_sent": self.msgs_sent,
-                "coll_bytes": self.coll_bytes}
+        return {f: getattr(self, f) for f in self.FIELDS}
+
+    def snapshot(self):
+        return self.as_dict()
+
+    def delta(self, snap):
+        return {f: getattr(self, f) - snap.get(f, 0) for f in self.FIELDS}
 
 
 class Comm:

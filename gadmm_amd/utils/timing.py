@@ -1,0 +1,91 @@
+"""Timing helpers (SURVEY.md §5 Tracing/profiling).
+
+* ``WallTimer``: host monotonic clock, synchronising the HIP device when one is in use.
+* ``EventTimer``: HIP events around device work (``torch.cuda.Event``).
+* ``modelled_time``: the reference's like-for-like clock model — ``2 * toc`` of worker 1's local
+  solve per iteration, i.e. heads then tails each take one local-solve time
+  (``group_ADMM_closedForm.m:39-42,53-55``). Useful to regenerate the paper's "clock time" panels;
+  real wall time (including communication) is what the framework reports by default.
+* ``roctx_range``: named ranges for rocprofv3 traces when roctx is available (no-op otherwise).
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+
+class WallTimer:
+    def __init__(self, device: Optional[torch.device] = None):
+        self.device = device
+        self.t0 = None
+        self.elapsed = 0.0
+
+    def _sync(self):
+        if self.device is not None and self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def __enter__(self):
+        self._sync()
+        self.t0 = time.perf_counter()
+        return self
+
+    def __exit__(self, *exc):
+        self._sync()
+        self.elapsed = time.perf_counter() - self.t0
+
+
+class EventTimer:
+    def __init__(self, stream: Optional[torch.cuda.Stream] = None):
+        self.stream = stream
+        self.start = torch.cuda.Event(enable_timing=True)
+        self.end = torch.cuda.Event(enable_timing=True)
+
+    def __enter__(self):
+        self.start.record(self.stream)
+        return self
+
+    def __exit__(self, *exc):
+        self.end.record(self.stream)
+
+    def ms(self) -> float:
+        self.end.synchronize()
+        return self.start.elapsed_time(self.end)
+
+
+def modelled_time(per_solve_s: float, iters: int) -> np.ndarray:
+    """Reference clock model: cumulative ``2 * t_local_solve`` per iteration (first entry 0)."""
+    t = np.arange(iters, dtype=np.float64) * 2.0 * per_solve_s
+    return t
+
+
+_roctx = None
+
+
+def _load_roctx():
+    global _roctx
+    if _roctx is None:
+        for name in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
+            try:
+                _roctx = ctypes.CDLL(name)
+                _roctx.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                break
+            except OSError:
+                _roctx = False
+    return _roctx or None
+
+
+@contextlib.contextmanager
+def roctx_range(name: str):
+    lib = _load_roctx()
+    if lib:
+        lib.roctxRangePushA(name.encode())
+    try:
+        yield
+    finally:
+        if lib:
+            lib.roctxRangePop()
