@@ -69,6 +69,10 @@ struct PhaseArgs {
   int m, max_inner;
   double lam, step, inner_tol;
   int* inner_iters;    // [n_local] diagnostics: inner GD steps used in the last update
+  // large-d (d > 256) row-blocked path
+  double* rbuf;        // [n_local][d] right-hand sides of the current phase
+  int obj_mode;        // 0: exact (second GEMV with A), 1: A th = r - deg rho th (no second matrix pass)
+  int pad_;
 };
 
 // Engine construction arguments (Python mirrors it in gadmm_amd/ops/native.py).

@@ -1,0 +1,195 @@
+// Large-d (d > 256) phase of the chain engine: the 10M x 10k "LinearRegression_Real-shaped" config
+// (BASELINE.json configs[4]). Per worker the cached inverse is 10k x 10k f64 = 800 MB, so one
+// phase is an HBM-streaming GEMV over the whole chip, split into three launches:
+//   chain_big_rhs   r_n = b_n - mu_n + rho th_l + rho th_r      (+ lazy head dual), one thread/elem
+//   chain_big_gemv  th_n = (A_n + deg rho I)^{-1} r_n            one wave per 2 rows, 16-B loads
+//   [chain_big_obj] (A_n th_n)_i -> per-workgroup objective partials   (exact objective mode)
+//   chain_big_post  tail dual update, local objective, last-arriver iteration close
+// Row-per-wave keeps every load of the matrix a contiguous 1-KiB wave access and the reduction
+// inside the wave (no split-K, deterministic). r (80 KB) is re-read from L2 by every wave.
+// Objective, exact mode: f = sum_i (1/2 (A th)_i - b_i) th_i + 1/2 y^T y with partials per workgroup
+// summed in a fixed order; identity mode uses A th = r - deg rho th (no second 800 MB pass).
+#include "gadmm_common.h"
+#include "gadmm_chain.h"
+#include "chain_device.h"
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int RPW = 2;               // rows per wave
+constexpr int ROWS_PER_WG = RPW * (NT / 64);
+
+__device__ __forceinline__ long rstride(int d) { return (long)d + (d + ROWS_PER_WG - 1) / ROWS_PER_WG + 1; }
+
+struct SlotView {
+  int li, gid, left, right, deg;
+};
+
+__device__ __forceinline__ SlotView slot_view(const PhaseArgs& a, int s) {
+  const PhaseSlot sl = a.slots[s];
+  SlotView v{sl.li, sl.gid, sl.left, sl.right, (sl.left >= 0) + (sl.right >= 0)};
+  return v;
+}
+
+// y[row] = sum_j M[row][j] x[j] for RPW consecutive rows per wave; returns sums on lane 0.
+__device__ __forceinline__ void wave_rows_dot(const double* __restrict__ M, const double* __restrict__ x, int d,
+                                              int row0, double (&out)[RPW]) {
+  const int lane = threadIdx.x & 63;
+  double acc[RPW];
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) acc[r] = 0.0;
+  if ((d & 1) == 0) {
+    const double2* x2 = reinterpret_cast<const double2*>(x);
+    const int d2 = d >> 1;
+    for (int j = lane; j < d2; j += 64) {
+      const double2 xv = x2[j];
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) {
+        if (row0 + r < d) {
+          const double2 mv = reinterpret_cast<const double2*>(M + (long)(row0 + r) * d)[j];
+          acc[r] = fma(mv.x, xv.x, fma(mv.y, xv.y, acc[r]));
+        }
+      }
+    }
+  } else {
+    for (int j = lane; j < d; j += 64) {
+      const double xv = x[j];
+#pragma unroll
+      for (int r = 0; r < RPW; ++r)
+        if (row0 + r < d) acc[r] = fma(M[(long)(row0 + r) * d + j], xv, acc[r]);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < RPW; ++r) out[r] = wave_sum_f64(acc[r]);
+}
+
+}  // namespace
+
+__global__ void __launch_bounds__(NT) chain_big_rhs(PhaseArgs a) {
+  if (a.ctl->done) return;
+  const int pending = a.ctl->pending;
+  const SlotView s = slot_view(a, blockIdx.y);
+  const int j = blockIdx.x * NT + threadIdx.x;
+  if (j >= a.d) return;
+  const long d = a.d;
+  const double* th = a.theta;
+  const double tw = th[s.gid * d + j];
+  const double tl = s.left >= 0 ? th[s.left * d + j] : 0.0;
+  const double tr = s.right >= 0 ? th[s.right * d + j] : 0.0;
+  double m = a.mu[s.li * d + j];
+  if ((a.flags & PH_PRE_DUAL) && pending) {
+    if (s.left >= 0) m = m - a.rho * (tl - tw);
+    if (s.right >= 0) m = m + a.rho * (tw - tr);
+    a.mu[s.li * d + j] = m;
+  }
+  double r = a.b[s.li * d + j] - m;
+  if (s.left >= 0) r = r + a.rho * tl;
+  if (s.right >= 0) r = r + a.rho * tr;
+  a.rbuf[s.li * rstride(a.d) + j] = r;
+}
+
+__global__ void __launch_bounds__(NT) chain_big_gemv(PhaseArgs a) {
+  if (a.ctl->done) return;
+  const SlotView s = slot_view(a, blockIdx.y);
+  const int d = a.d;
+  const int row0 = blockIdx.x * ROWS_PER_WG + (threadIdx.x >> 6) * RPW;
+  if (row0 >= d) return;
+  const double* Mi = a.Minv + ((long)s.li * a.nvar + a.deg_to_var[s.deg]) * (long)d * d;
+  const double* r = a.rbuf + s.li * rstride(d);
+  double out[RPW];
+  wave_rows_dot(Mi, r, d, row0, out);
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int q = 0; q < RPW; ++q)
+      if (row0 + q < d) a.theta[(long)s.gid * d + row0 + q] = out[q];
+  }
+}
+
+// exact objective: per-workgroup partial of sum_i (1/2 (A th)_i - b_i) th_i
+__global__ void __launch_bounds__(NT) chain_big_obj(PhaseArgs a) {
+  __shared__ double wsum[NT / 64];
+  if (a.ctl->done) return;
+  const SlotView s = slot_view(a, blockIdx.y);
+  const int d = a.d;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int row0 = blockIdx.x * ROWS_PER_WG + w * RPW;
+  const double* th = a.theta + (long)s.gid * d;
+  double part = 0.0;
+  if (row0 < d) {
+    double q[RPW];
+    wave_rows_dot(a.A + (long)s.li * d * d, th, d, row0, q);
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < RPW; ++k)
+        if (row0 + k < d) part += (0.5 * q[k] - a.b[(long)s.li * d + row0 + k]) * th[row0 + k];
+  }
+  if (lane == 0) wsum[w] = part;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int k = 0; k < NT / 64; ++k) t += wsum[k];
+    a.rbuf[s.li * rstride(d) + d + blockIdx.x] = t;
+  }
+}
+
+__global__ void __launch_bounds__(1024) chain_big_post(PhaseArgs a) {
+  __shared__ double scratch[16];
+  __shared__ int flag_lds;
+  if (a.ctl->done) return;
+  const int it = a.ctl->iter;
+  const SlotView s = slot_view(a, blockIdx.x);
+  const long d = a.d;
+  const double* th = a.theta;
+  const double* r = a.rbuf + s.li * rstride(a.d);
+  const double crho = s.deg * a.rho;
+  double part = 0.0;
+  for (long j = threadIdx.x; j < d; j += blockDim.x) {
+    const double t = th[s.gid * d + j];
+    if (a.flags & PH_POST_DUAL) {
+      double m = a.mu[s.li * d + j];
+      if (s.left >= 0) m = m - a.rho * (th[s.left * d + j] - t);
+      if (s.right >= 0) m = m + a.rho * (t - th[s.right * d + j]);
+      a.mu[s.li * d + j] = m;
+    }
+    if (a.obj_mode != 0) part += (0.5 * (r[j] - crho * t) - a.b[s.li * d + j]) * t;
+  }
+  double f;
+  if (a.obj_mode != 0) {
+    f = block_sum_f64(part, scratch);
+  } else {
+    // fixed-order sum of the per-workgroup partials of chain_big_obj
+    const int nblk = (a.d + ROWS_PER_WG - 1) / ROWS_PER_WG;
+    double t = 0.0;
+    if (threadIdx.x == 0)
+      for (int k = 0; k < nblk; ++k) t += r[d + k];
+    f = t;
+  }
+  if (threadIdx.x == 0) a.objw[s.li] = f + 0.5 * a.yy[s.li];
+  if (a.flags & PH_FINISH) {
+    if (phase_arrive(a.ctl, a.n_slots, &flag_lds)) finish_iteration(a, it);
+  }
+}
+
+extern "C" {
+
+long gadmm_chain_big_rbuf_stride(int d) { return (long)d + (d + ROWS_PER_WG - 1) / ROWS_PER_WG + 1; }
+
+int gadmm_chain_phase_big(const PhaseArgs* args, hipStream_t st) {
+  const PhaseArgs& a = *args;
+  if (a.n_slots <= 0) return 0;
+  if (a.rbuf == nullptr) {
+    gadmm_set_error("chain_phase_big: rbuf workspace missing");
+    return -1;
+  }
+  const int d = a.d;
+  hipLaunchKernelGGL(chain_big_rhs, dim3((d + NT - 1) / NT, a.n_slots), dim3(NT), 0, st, a);
+  const int nblk = (d + ROWS_PER_WG - 1) / ROWS_PER_WG;
+  hipLaunchKernelGGL(chain_big_gemv, dim3(nblk, a.n_slots), dim3(NT), 0, st, a);
+  if (a.obj_mode == 0 && (a.flags & PH_OBJ))
+    hipLaunchKernelGGL(chain_big_obj, dim3(nblk, a.n_slots), dim3(NT), 0, st, a);
+  hipLaunchKernelGGL(chain_big_post, dim3(a.n_slots), dim3(1024), 0, st, a);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"

@@ -28,14 +28,13 @@
 // scope before reading other workgroups' results (cdna_hip_programming.md §6 Guideline 16).
 #include "gadmm_common.h"
 #include "gadmm_chain.h"
+#include "chain_device.h"
 
 
 namespace {
 
 constexpr int NT = 256;
 constexpr int NW = NT / 64;
-
-__device__ __forceinline__ void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // out[i] = sum_j M[j*d + i] * x[j]  (M symmetric), for i < d. x, out in LDS; red: NW*64*NC.
 template <int NC>
@@ -77,56 +76,6 @@ __device__ __forceinline__ void symv_cols(const double* __restrict__ M, const do
     out[i] = s;
   }
   __syncthreads();
-}
-
-__device__ __forceinline__ double softplus(double t) {  // log(1 + exp(t)), stable
-  return t > 30.0 ? t + log1p(exp(-t)) : log1p(exp(t));
-}
-
-// Close the phase: release + ticket; the last arriver acquires and runs `finish`.
-__device__ __forceinline__ bool phase_arrive(ChainCtl* ctl, int n_slots, int* flag_lds) {
-  drain_vmem();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    drain_vmem();
-    const unsigned t = __hip_atomic_fetch_add(&ctl->ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = (t == (unsigned)(n_slots - 1));
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      drain_vmem();
-    }
-    *flag_lds = last;
-  }
-  __syncthreads();
-  return *flag_lds != 0;
-}
-
-__device__ void finish_iteration(const PhaseArgs& a, int it) {
-  if (threadIdx.x != 0) return;
-  ChainCtl* ctl = a.ctl;
-  double s = 0.0;
-  for (int i = 0; i < a.n_local; ++i) s += a.objw[i];  // fixed order: deterministic
-  if (a.flags & PH_LOCAL_STOP) {
-    if (it - 1 < a.max_iter) a.trace[it - 1] = s;
-    const double gap = fabs(s - a.obj0);
-    if (!(s == s) || isinf(s)) {
-      ctl->done = 3;
-      ctl->conv_iter = it;
-    } else if (gap < a.tol) {
-      ctl->done = 1;
-      ctl->conv_iter = it;
-    } else if (it >= a.max_iter) {
-      ctl->done = 2;
-      ctl->conv_iter = it;
-    }
-    ctl->monitored = it;
-  } else {
-    a.part[(it - 1) % a.ring] = s;
-  }
-  ctl->pending = 1;
-  ctl->ticket = 0u;
-  ctl->iter = it + 1;
 }
 
 }  // namespace
@@ -424,12 +373,17 @@ __global__ void chain_reset_kernel(ChainCtl* ctl, int start_iter, int pending) {
 // ------------------------------------------------------------------------------------------------
 extern "C" {
 
+int gadmm_chain_phase_big(const PhaseArgs* args, hipStream_t st);
+
 int gadmm_chain_phase(const PhaseArgs* args, hipStream_t st) {
   const PhaseArgs& a = *args;
   if (a.n_slots <= 0) return 0;
   if (a.d > 256) {
-    gadmm_set_error("chain_phase: d=%d > 256 needs the row-blocked engine path", a.d);
-    return -1;
+    if (a.model != MODEL_LINEAR) {
+      gadmm_set_error("chain_phase: logistic with d=%d > 256 is not supported by the fused kernels", a.d);
+      return -1;
+    }
+    return gadmm_chain_phase_big(args, st);
   }
   const int nc = (a.d + 63) / 64;
   if (a.model == MODEL_LINEAR) {

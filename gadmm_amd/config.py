@@ -82,6 +82,8 @@ PRESETS = {
 
 
 def get_preset(name: str) -> ExperimentConfig:
+    if name.lower() == "linearregression_realshaped":
+        from .entry import LinearRegression_RealShaped  # noqa: F401  (registers its preset)
     key = {k.lower(): k for k in PRESETS}.get(name.lower())
     if key is None:
         raise KeyError("unknown entry point %r (have: %s)" % (name, ", ".join(PRESETS)))

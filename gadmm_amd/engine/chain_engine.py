@@ -47,7 +47,7 @@ class NativeChainEngine:
                  model: str = "linear", rho: float = 1.0, obj0: float = 0.0, tol: float = 1e-4,
                  max_iter: int = 1000, lam: float = 0.0, step: float = 0.0, max_inner: int = 100,
                  inner_tol: float = 1e-4, comm=None, block: int = 16, stream: Optional[torch.cuda.Stream] = None,
-                 precomputed=None, force_monitor: bool = False):
+                 precomputed=None, force_monitor: bool = False, obj_mode: str = "exact"):
         if not X_loc.is_cuda:
             raise ValueError("NativeChainEngine runs on a HIP device; use the torch algorithms on CPU")
         self.lib = native.require()
@@ -87,6 +87,10 @@ class NativeChainEngine:
             self.inner_iters = torch.zeros((max(nl, 1),), dtype=torch.int32, device=dev)
             self.A = self.b = self.yy = self.Minv = None
             self.X = self.Y = None
+            self.rbuf = None
+            if d > 256:
+                stride = int(native.require().gadmm_chain_big_rbuf_stride(d))
+                self.rbuf = torch.zeros((max(nl, 1) * stride,), dtype=f64, device=dev)
             if model == "linear":
                 if precomputed is not None:
                     self.A, self.b, self.yy = precomputed
@@ -125,6 +129,8 @@ class NativeChainEngine:
         args.max_inner = int(max_inner)
         args.lam, args.step, args.inner_tol = float(lam), float(step), float(inner_tol)
         args.inner_iters = self.inner_iters.data_ptr()
+        args.rbuf = native.ptr(self.rbuf)
+        args.obj_mode = 0 if obj_mode == "exact" else 1
         desc = native.EngineDesc()
         desc.base = args
         desc.d_slots = self.slots.data_ptr()

@@ -53,6 +53,7 @@ class PhaseArgs(ctypes.Structure):
         ("m", c_int), ("max_inner", c_int),
         ("lam", c_double), ("step", c_double), ("inner_tol", c_double),
         ("inner_iters", c_void_p),
+        ("rbuf", c_void_p), ("obj_mode", c_int), ("pad_", c_int),
     ]
 
 
@@ -108,6 +109,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_chain_engine_exchange": (c_int, [c_void_p, c_int]),
         "gadmm_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
         "gadmm_chain_persistent_lds": (c_long, [c_int, c_int]),
+        "gadmm_chain_big_rbuf_stride": (c_long, [c_int]),
         "gadmm_chain_persistent_launch": (c_int, [ctypes.POINTER(PersistArgs), c_void_p]),
         "gadmm_rccl_unique_id": (c_int, [ctypes.c_char_p]),
         "gadmm_rccl_version": (c_int, []),
