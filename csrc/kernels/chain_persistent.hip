@@ -73,7 +73,25 @@ __device__ __forceinline__ void symv_lds(const double* M, const double* x, doubl
   double acc[NC];
 #pragma unroll
   for (int c = 0; c < NC; ++c) acc[c] = 0.0;
-  for (int j = w; j < d; j += NW) {
+  // 4 rows of M per batch per wave: the 4 (x NC) LDS loads issue together, one wait per batch
+  int j = w;
+  for (; j + 3 * NW < d; j += 4 * NW) {
+    double mv[4][NC], xv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      xv[q] = x[j + q * NW];
+#pragma unroll
+      for (int c = 0; c < NC; ++c) {
+        const int i = lane + 64 * c;
+        mv[q][c] = i < d ? M[(j + q * NW) * d + i] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int c = 0; c < NC; ++c) acc[c] = fma(mv[q][c], xv[q], acc[c]);
+  }
+  for (; j < d; j += NW) {
     const double xj = x[j];
 #pragma unroll
     for (int c = 0; c < NC; ++c) {

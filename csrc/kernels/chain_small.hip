@@ -26,6 +26,7 @@
 // Inter-workgroup hand-off (finish): every storing wave drains (s_waitcnt vmcnt(0)), workgroup
 // barrier, one lane releases at agent scope and takes a ticket; the last arriver acquires at agent
 // scope before reading other workgroups' results (cdna_hip_programming.md §6 Guideline 16).
+#include <stdlib.h>
 #include "gadmm_common.h"
 #include "gadmm_chain.h"
 #include "chain_device.h"
@@ -305,6 +306,163 @@ __global__ void __launch_bounds__(NT) chain_phase_logistic(PhaseArgs a) {
   }
 }
 
+// sum_k M[k * stride] * v[k], k < n: 8 independent LDS loads of each operand per batch (one wait per
+// batch instead of one per element), 4 partial sums combined in a fixed order.
+__device__ __forceinline__ double dot_strided8(const double* M, int stride, const double* v, int n) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  int k = 0;
+  for (; k + 8 <= n; k += 8) {
+    double mv[8], vv[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      mv[q] = M[(k + q) * stride];
+      vv[q] = v[k + q];
+    }
+    a0 = fma(mv[0], vv[0], a0);
+    a1 = fma(mv[1], vv[1], a1);
+    a2 = fma(mv[2], vv[2], a2);
+    a3 = fma(mv[3], vv[3], a3);
+    a0 = fma(mv[4], vv[4], a0);
+    a1 = fma(mv[5], vv[5], a1);
+    a2 = fma(mv[6], vv[6], a2);
+    a3 = fma(mv[7], vv[7], a3);
+  }
+  for (; k < n; ++k) a0 = fma(M[k * stride], v[k], a0);
+  return (a0 + a1) + (a2 + a3);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Logistic phase, one WAVE per worker (the inner GD is latency-bound: ~100 dependent steps of two
+// 50 x 50 GEMVs). Lane l owns margin row i = l + 64k and coordinate j = l + 64k; both GEMVs read
+// LDS contiguously across lanes (X^T for the margins, X for the gradient) with the other operand
+// broadcast from LDS; the all-coordinates stopping test of logReg_GD.m:21 is a wave vote. No
+// workgroup barriers beyond the single wave's own LDS ordering.
+template <int C>
+__global__ void __launch_bounds__(64) chain_phase_logistic_wave(PhaseArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double dyn[];  // X [m][d] | XT [d][m] | x [64C] | s [64C]
+  __shared__ double scratch[1];
+  __shared__ int flag_lds;
+  ChainCtl* ctl = a.ctl;
+  if (ctl->done) return;
+  const int it = ctl->iter;
+  const int pending = ctl->pending;
+  const PhaseSlot sl = a.slots[blockIdx.x];
+  const int d = a.d, m = a.m;
+  const double rho = a.rho, lam = a.lam, step = a.step;
+  const int lane = threadIdx.x;
+  double* th = a.theta;
+  const double* thw = th + (long)sl.gid * d;
+  const double* thl = sl.left >= 0 ? th + (long)sl.left * d : nullptr;
+  const double* thr = sl.right >= 0 ? th + (long)sl.right * d : nullptr;
+  double* mu = a.mu + (long)sl.li * d;
+  const double* Xg = a.X + (long)sl.li * m * d;
+  const double* Yg = a.Y + (long)sl.li * m;
+  double* Xs = dyn;
+  double* XTs = dyn + (long)m * d;
+  double* xs = XTs + (long)m * d;
+  double* ss = xs + 64 * C;
+  for (int e = lane; e < m * d; e += 64) {
+    const double v = Xg[e];
+    Xs[e] = v;
+    XTs[(e % d) * m + e / d] = v;
+  }
+  double x[C], sh[C], yv[C];
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int j = lane + 64 * c;
+    x[c] = 0.0;
+    sh[c] = 0.0;
+    yv[c] = 0.0;
+    if (j < d) {
+      double mm = mu[j];
+      if ((a.flags & PH_PRE_DUAL) && pending) {
+        if (thl) mm = mm - rho * (thl[j] - thw[j]);
+        if (thr) mm = mm + rho * (thw[j] - thr[j]);
+        mu[j] = mm;
+      }
+      const double x0 = thw[j];
+      double s = mm;  // -C1 + C2 (edge form) == mu
+      if (thl) s = s + rho * (x0 - thl[j]);
+      if (thr) s = s + rho * (x0 - thr[j]);
+      sh[c] = s;
+      x[c] = x0;
+      xs[j] = x0;
+    }
+    if (j < m) yv[c] = Yg[j];
+  }
+  __syncthreads();
+  int used = 0;
+  for (int k = 0; k < a.max_inner; ++k) {
+    // margins z_i = X[i,:] x  -> s_i = y_i / (1 + exp(y_i z_i))
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int i = lane + 64 * c;
+      if (i < m) {
+        const double z = dot_strided8(XTs + i, m, xs, d);
+        ss[i] = yv[c] / (1.0 + exp(yv[c] * z));
+      }
+    }
+    __syncthreads();
+    bool conv = true;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int j = lane + 64 * c;
+      if (j < d) {
+        const double g = -dot_strided8(Xs + j, d, ss, m) + lam * x[c] + sh[c];
+        const double xn = x[c] - step * g;
+        conv &= fabs(xn - x[c]) < a.inner_tol;
+        x[c] = xn;
+      }
+    }
+    __syncthreads();  // every lane has read ss / xs of this step
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const int j = lane + 64 * c;
+      if (j < d) xs[j] = x[c];
+    }
+    __syncthreads();
+    used = k + 1;
+    if (__all(conv)) break;
+  }
+  // local objective lam/2 |x|^2 + sum softplus(-y z) at the new iterate
+  double part = 0.0, xx = 0.0;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int i = lane + 64 * c;
+    if (i < m) {
+      const double z = dot_strided8(XTs + i, m, xs, d);
+      part += softplus(-yv[c] * z);
+    }
+    const int j = lane + 64 * c;
+    if (j < d) xx += x[c] * x[c];
+  }
+  part = wave_sum_f64(part);
+  xx = wave_sum_f64(xx);
+  double* thw_out = th + (long)sl.gid * d;
+#pragma unroll
+  for (int c = 0; c < C; ++c) {
+    const int j = lane + 64 * c;
+    if (j < d) {
+      const double t = x[c];
+      thw_out[j] = t;
+      if (a.flags & PH_POST_DUAL) {
+        double mm = mu[j];
+        if (thl) mm = mm - rho * (thl[j] - t);
+        if (thr) mm = mm + rho * (t - thr[j]);
+        mu[j] = mm;
+      }
+    }
+  }
+  if (lane == 0) {
+    a.objw[sl.li] = lam * 0.5 * xx + part;
+    if (a.inner_iters) a.inner_iters[sl.li] = used;
+  }
+  (void)scratch;
+  if (a.flags & PH_FINISH) {
+    if (phase_arrive(ctl, a.n_slots, &flag_lds)) finish_iteration(a, it);
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Apply the pending heads' dual updates with the chain they were computed on (used before a
 // re-chain and before checkpointing). One workgroup per slot of the OLD head plan.
@@ -404,7 +562,23 @@ int gadmm_chain_phase(const PhaseArgs* args, hipStream_t st) {
     hipLaunchKernelGGL(kfn, dim3(a.n_slots), dim3(NT), lds, st, a);                                  \
   } while (0)
     if (ldsx) {
-      if (nc == 1 && mc == 1) GADMM_LOG_LAUNCH(1, 1, true);
+      // one wave per worker (default); GADMM_LOGISTIC_BLOCK=1 selects the 4-wave variant
+      static const bool block4 = getenv("GADMM_LOGISTIC_BLOCK") != nullptr;
+      if (!block4) {
+        const int cmax = nc > mc ? nc : mc;
+        const size_t lw = lds + (size_t)2 * 64 * cmax * sizeof(double);
+#define GADMM_LOGW_LAUNCH(CV)                                                                           \
+  do {                                                                                                  \
+    auto kfn = chain_phase_logistic_wave<CV>;                                                           \
+    if (lw > 65536) GADMM_CHECK(hipFuncSetAttribute((const void*)kfn,                                   \
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lw)); \
+    hipLaunchKernelGGL(kfn, dim3(a.n_slots), dim3(64), lw, st, a);                                      \
+  } while (0)
+        if (cmax == 1) GADMM_LOGW_LAUNCH(1);
+        else if (cmax == 2) GADMM_LOGW_LAUNCH(2);
+        else GADMM_LOGW_LAUNCH(4);
+#undef GADMM_LOGW_LAUNCH
+      } else if (nc == 1 && mc == 1) GADMM_LOG_LAUNCH(1, 1, true);
       else if (nc <= 2 && mc <= 2) GADMM_LOG_LAUNCH(2, 2, true);
       else GADMM_LOG_LAUNCH(4, 4, true);
     } else {
