@@ -45,7 +45,10 @@ def main():
     ap.add_argument("--block", type=int, default=0, help="iterations per graph replay (0: auto)")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--engine", choices=["auto", "persistent", "graph"], default="auto",
-                    help="auto: persistent single-launch kernel when eligible (1 GPU), else graph-replayed phases")
+                    help="auto: persistent single-launch kernel when eligible, else graph-replayed phases")
+    ap.add_argument("--fabric", choices=["auto", "xgmi", "rccl"], default="auto",
+                    help="multi-GPU transport: xgmi = device-initiated granule pushes between persistent kernels "
+                         "(IPC fine-grained buffers), rccl = RCCL send/recv between graph-replayed phases")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -56,8 +59,12 @@ def main():
             print("bench.py: --gpus %d needs a torchrun launch with %d processes" % (args.gpus, args.gpus),
                   file=sys.stderr)
             sys.exit(2)
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    # GADMM_BENCH_SHARE_GPU=1: rehearsal of the multi-rank path with every rank on cuda:0 (one-GPU
+    # development box); RCCL refuses two ranks on one device, so only the xgmi fabric runs there.
+    share = os.environ.get("GADMM_BENCH_SHARE_GPU") == "1"
+    dev_index = 0 if share else local_rank
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
 
     from gadmm_amd.data import linear_synthetic
     from gadmm_amd.oracle.reference import opt_linear
@@ -68,8 +75,15 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        from gadmm_amd.parallel.comm import RcclComm
-        comm = RcclComm(device)
+        from gadmm_amd.parallel.comm import RcclComm, RankInfo
+        comm = RankInfo(rank, world) if share else RcclComm(device)
+
+    def all_ok(flag: bool) -> bool:
+        if world == 1:
+            return flag
+        t = torch.tensor([0.0 if flag else 1.0], dtype=torch.float64)
+        dist.all_reduce(t)
+        return float(t.item()) == 0.0
 
     ds = linear_synthetic(args.workers)
     Xf, yf = ds.stacked()
@@ -90,18 +104,51 @@ def main():
         if world > 1:
             dist.barrier()
 
-    persistent = args.engine == "persistent" or (args.engine == "auto" and eng.persistent_eligible())
+    fabric = None
+    fabric_kind = "local" if world == 1 else "rccl"
+    if world > 1 and args.fabric in ("auto", "xgmi") and args.engine != "graph":
+        ok = False
+        err = ""
+        try:
+            from gadmm_amd.parallel.xgmi import XgmiFabric
+            need = sorted({int(placement.owner[u]) for w in local for u in (w - 1, w + 1)
+                           if 0 <= u < args.workers} - {rank})
+            fabric = XgmiFabric(args.workers, ds.dim, 8, rank, world, device, peers_needed=need)
+            ok = eng.persistent_eligible(fabric)
+        except Exception as e:  # fall back to RCCL on every rank together
+            err = str(e)
+        if not all_ok(ok):
+            if rank == 0:
+                print("bench.py: xgmi fabric unavailable (%s); using RCCL" % (err or "not eligible"), file=sys.stderr)
+            if fabric is not None:
+                fabric.close()
+            fabric = None
+        else:
+            fabric_kind = "xgmi"
+    persistent = (args.engine in ("auto", "persistent")) and (
+        eng.persistent_eligible() if world == 1 else fabric is not None)
 
     def solve():
         eng.refresh(X_loc, y_loc)
         eng.reset()
         if persistent:
-            return eng.run_persistent()
+            return eng.run_persistent(fabric=fabric)
         return eng.run(use_graph=not args.no_graph)
 
     runs = []
     for _ in range(args.warmup):
-        runs.append(solve())
+        try:
+            r = solve()
+            good = r.done == 1
+        except RuntimeError as e:
+            good = False
+            print("bench.py[rank %d]: %s" % (rank, e), file=sys.stderr)
+        if persistent and world > 1 and not all_ok(good):
+            # a stalled device-initiated hand-off (done == 4) on any rank: every rank drops to RCCL
+            persistent, fabric_kind = False, "rccl(fallback)"
+            if rank == 0:
+                print("bench.py: xgmi solve failed; falling back to RCCL", file=sys.stderr)
+        runs.append(None)
     barrier()
     t0 = time.perf_counter()
     last = None
@@ -114,6 +161,11 @@ def main():
     iters = last.iters if last is not None else 0
     p2p = last.p2p_bytes if last is not None else 0
     mon = last.monitor_bytes if last is not None else 0
+    if persistent and world > 1:
+        # device-initiated pushes: one d-vector per cross-GPU neighbour relation per phase
+        p2p = chain_message_count(path, placement) * ds.dim * 8 * iters // world  # per-rank share, summed below
+        n_remote = sum(1 for w in range(args.workers) if int(placement.owner[w]) != 0)
+        mon = (n_remote * 8 + world * 8) * iters // world
     if world > 1:
         t = torch.tensor([ms, float(p2p), float(mon)], dtype=torch.float64)
         mx = t.clone()
@@ -153,10 +205,13 @@ def main():
             "p2p_messages_per_iteration": chain_message_count(path, placement),
             "us_per_iteration": round(ms * 1e3 / max(iters, 1), 3),
             "engine": "persistent" if persistent else ("graph" if eng.graph_ok() and not args.no_graph else "eager"),
+            "fabric": fabric_kind,
             "baseline_s": BASELINE_S,
         }
         print(json.dumps(out), flush=True)
     eng.close()
+    if fabric is not None:
+        fabric.close()
     if comm is not None:
         comm.close()
     if world > 1:

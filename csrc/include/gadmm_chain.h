@@ -97,23 +97,31 @@ struct RunStats {
 };
 
 
-// Persistent single-launch solve (csrc/kernels/chain_persistent.hip).
+// Persistent single-launch solve (csrc/kernels/chain_persistent.hip). One workgroup per local worker
+// (+ the stop-rule monitor on the monitor rank). Multi-GPU ("xgmi" fabric): every granule buffer is
+// fine-grained device memory shared by IPC; boundary theta is pushed into the neighbour GPU's table,
+// objective granules into the monitor's ring, decisions into every rank's ring.
 struct PersistArgs {
-  int d, n, start_iter, max_iter, lag, ring, nvar, obj_mode;
+  int d, n, n_local, start_iter, max_iter, lag, ring, nvar, obj_mode;
   int deg_to_var[3];
-  int pending_in;
+  int pending_in, has_monitor, nranks, sys_scope;
+  unsigned epoch;           // salts every tag: tag = epoch << 20 | iteration (no re-zeroing between solves)
+  int pad_;
   double rho, obj0, tol;
   long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
-  const int* path;          // chain position -> worker
-  const double* Minv;       // [n][nvar][d][d]
-  const double* A;          // [n][d][d]   (obj_mode 0)
-  const double* b;          // [n][d]
-  const double* yy;         // [n]
-  double* theta;            // [n][d]   in: initial, out: final
-  double* mu;               // [n][d]   in/out
-  u32x4* thg;               // [n][d]   theta granules
-  u32x4* objg;              // [ring][n] objective granules
-  unsigned long long* decg; // [ring]   {iter << 32 | code}
-  double* trace;            // [max_iter]
+  const PhaseSlot* slots;   // [n_local] (li, gid, left, right) in launch order
+  const int* pos;           // [n_local] chain position of each slot (even = head)
+  const double* Minv;       // [n_local][nvar][d][d]
+  const double* A;          // [n_local][d][d]   (obj_mode 0)
+  const double* b;          // [n_local][d]
+  const double* yy;         // [n_local]
+  double* theta;            // [n][d]   in: initial (local + ghost rows), out: final local rows
+  double* mu;               // [n_local][d]   in/out
+  u32x4* thg;               // [n][d]   this rank's theta granule table
+  u32x4* const* push;       // [n_local * 2] remote theta tables this worker also publishes into
+  u32x4* objg;              // [ring][n] the monitor rank's objective ring (remote unless monitor rank)
+  unsigned long long* decg; // [ring]  this rank's decision ring
+  unsigned long long* const* dec_push;  // [nranks] every rank's decision ring (monitor only)
+  double* trace;            // [max_iter] (monitor rank)
   ChainCtl* ctl;
 };

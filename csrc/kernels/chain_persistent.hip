@@ -1,4 +1,4 @@
-// Persistent single-launch GADMM (linear, closed form) for one MI355X: the whole solve in ONE kernel.
+// Persistent single-launch GADMM (linear, closed form): the whole solve in ONE kernel per GPU.
 //
 // Why: at the reference shapes (N = 24..50 workers, d = 50) an iteration is two dependent phases of
 // ~1 us of arithmetic each; as separate launches every phase pays a kernel boundary and re-reads
@@ -13,17 +13,20 @@
 //   every worker then publishes f_n(theta_n^i); the monitor workgroup sums them in worker order,
 //   records the trace and posts the stop decision for iteration i (|obj - obj0| < tol).
 //   A worker starts iteration i only after the decision of iteration i - LAG is known, so all
-//   workers leave at the same iteration boundary; the reported iteration count is exact.
+//   workers (on every GPU) leave at the same iteration boundary; the reported count is exact.
 //
 // Hand-offs use the data-is-flag granule form of cdna_hip_programming.md §6 Guideline 16 (R2): each
-// double travels as one 16-byte {tag, lo, tag, hi} write-through (sc1) store; the consumer re-reads
-// its 16-byte sc1 granule until both tags equal the expected iteration. No flags, no fences, no
-// counters. Every spin is bounded by a wall-clock deadline (s_memrealtime); on timeout the kernel
-// records done = 4 and every workgroup exits.
+// double travels as one 16-byte {tag, lo, tag, hi} write-through store; the consumer re-reads its
+// 16-byte granule until both tags equal the expected tag (a torn 16-B store is two 8-B halves, each
+// carrying its own tag, so tearing is always detected). No flags, no fences, no counters.
+// Single GPU: sc1 (agent) granules in hipMalloc memory. Multi-GPU (xgmi fabric): sc0|sc1 (system)
+// granules in fine-grained uncached memory shared by IPC; remote stores travel over xGMI.
+// Tags are salted with a per-solve epoch, so buffers need no re-zeroing between solves.
+// Every spin is bounded by a wall-clock deadline (s_memrealtime); on timeout the kernel records
+// done = 4 and every workgroup exits.
 #include "gadmm_common.h"
 #include "gadmm_chain.h"
-
-
+#include <string.h>
 
 namespace {
 
@@ -34,34 +37,52 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
 }
 
+template <bool SYS>
 __device__ __forceinline__ void store_granule(__amdgpu_buffer_rsrc_t rs, int byte_off, unsigned tag, double v) {
   const unsigned long long bits = __double_as_longlong(v);
   u32x4 g = {tag, (unsigned)(bits & 0xffffffffull), tag, (unsigned)(bits >> 32)};
-  __builtin_amdgcn_raw_buffer_store_b128(g, rs, byte_off, 0, 16 /* sc1 */);
+  if (SYS) __builtin_amdgcn_raw_buffer_store_b128(g, rs, byte_off, 0, 17 /* sc0 sc1 */);
+  else __builtin_amdgcn_raw_buffer_store_b128(g, rs, byte_off, 0, 16 /* sc1 */);
 }
 
+template <bool SYS>
 __device__ __forceinline__ bool load_granule(__amdgpu_buffer_rsrc_t rs, int byte_off, unsigned tag, double* v) {
-  const u32x4 g = __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16 /* sc1 */);
+  const u32x4 g = SYS ? __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 17)
+                      : __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16);
   *v = __longlong_as_double((long long)(((unsigned long long)g.w << 32) | g.y));
   return g.x == tag && g.z == tag;
 }
 
+template <bool SYS>
+__device__ __forceinline__ void store_dec(unsigned long long* p, unsigned long long v) {
+  if (SYS) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <bool SYS>
+__device__ __forceinline__ unsigned long long load_dec(unsigned long long* p) {
+  if (SYS) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ unsigned long long now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
 
-// Every lane of the block polls the granules of its elements of `src_row` until all carry `tag`.
-template <int NC>
+__device__ __forceinline__ unsigned make_tag(unsigned epoch, int it) { return (epoch << 20) | ((unsigned)it & 0xfffffu); }
+
+// Every lane of wave 0 polls the granules of its elements of table row `row` until all carry `tag`.
+template <int NC, bool SYS>
 __device__ __forceinline__ bool wait_row(__amdgpu_buffer_rsrc_t rs, int row, int d, unsigned tag, double (&out)[NC],
-                                         unsigned long long deadline, volatile int* abort_lds) {
+                                         unsigned long long deadline) {
   const int lane = threadIdx.x & 63;
   for (;;) {
     bool ok = true;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int i = lane + 64 * c;
-      if (i < d) ok &= load_granule(rs, (row * d + i) * 16, tag, &out[c]);
+      if (i < d) ok &= load_granule<SYS>(rs, (row * d + i) * 16, tag, &out[c]);
     }
     if (__all(ok)) return true;
-    if (now_ticks() > deadline || *abort_lds) return false;
+    if (now_ticks() > deadline) return false;
     __builtin_amdgcn_s_sleep(1);
   }
 }
@@ -114,7 +135,7 @@ __device__ __forceinline__ void symv_lds(const double* M, const double* x, doubl
 
 }  // namespace
 
-template <int NC>
+template <int NC, bool SYS>
 __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int abort_lds;
@@ -131,17 +152,17 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
   }
   __syncthreads();
 
-  if ((int)blockIdx.x == n) {
+  if (a.has_monitor && (int)blockIdx.x == a.n_local) {
     // ---------------------------------------------------------------- monitor workgroup
     double* vals = lds;  // [n]
     for (int it = a.start_iter;; ++it) {
-      const unsigned tag = (unsigned)it;
+      const unsigned tag = make_tag(a.epoch, it);
       const int slot = it % a.ring;
       if (w0) {
         for (int w = lane; w < n; w += 64) {
           double v = 0.0;
           for (;;) {
-            if (load_granule(rob, (slot * n + w) * 16, tag, &v)) break;
+            if (load_granule<SYS>(rob, (slot * n + w) * 16, tag, &v)) break;
             if (now_ticks() > deadline) {
               abort_lds = 1;
               break;
@@ -164,16 +185,9 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
           else if (fabs(s - a.obj0) < a.tol) code = 1;
           else if (it >= a.max_iter) code = 2;
         }
-        __hip_atomic_store(&a.decg[slot], ((unsigned long long)tag << 32) | code, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        if (code) {
-          a.ctl->done = (int)code;
-          a.ctl->conv_iter = it;
-          a.ctl->iter = it + a.lag;
-          a.ctl->pending = 1;
-          a.ctl->monitored = it;
-          stop_lds = 1;
-        }
+        const unsigned long long dv = ((unsigned long long)tag << 32) | code;
+        for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
+        if (code) stop_lds = 1;
       }
       __syncthreads();
       if (stop_lds) return;
@@ -181,24 +195,27 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
   }
 
   // ------------------------------------------------------------------ worker workgroup
-  const int pos = blockIdx.x;
-  const int w = a.path[pos];
-  const int left = pos > 0 ? a.path[pos - 1] : -1;
-  const int right = pos < n - 1 ? a.path[pos + 1] : -1;
+  const PhaseSlot sl = a.slots[blockIdx.x];
+  const int pos = a.pos[blockIdx.x];
+  const int li = sl.li, w = sl.gid, left = sl.left, right = sl.right;
   const bool head = (pos % 2) == 0;
   const int deg = (left >= 0) + (right >= 0);
   const double rho = a.rho;
   const double crho = deg * rho;
+  u32x4* const p0 = a.push ? a.push[2 * blockIdx.x] : nullptr;
+  u32x4* const p1 = a.push ? a.push[2 * blockIdx.x + 1] : nullptr;
+  const __amdgpu_buffer_rsrc_t rp0 = rsrc_of(p0 ? (const void*)p0 : (const void*)a.thg);
+  const __amdgpu_buffer_rsrc_t rp1 = rsrc_of(p1 ? (const void*)p1 : (const void*)a.thg);
 
   double* Ml = lds;                                            // d*d
   double* Al = lds + (long)d * d;                              // d*d (obj_mode 0)
   double* xv = lds + (long)(a.obj_mode == 0 ? 2 : 1) * d * d;  // [64*NC] rhs / theta staging
   double* red = xv + 64 * NC;                                  // [NW*NC*64]
 
-  const double* Mg = a.Minv + ((long)w * a.nvar + a.deg_to_var[deg]) * (long)d * d;
+  const double* Mg = a.Minv + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)d * d;
   for (int e = threadIdx.x; e < d * d; e += NT) Ml[e] = Mg[e];
   if (a.obj_mode == 0) {
-    const double* Ag = a.A + (long)w * d * d;
+    const double* Ag = a.A + (long)li * d * d;
     for (int e = threadIdx.x; e < d * d; e += NT) Al[e] = Ag[e];
   }
   // worker state, meaningful in wave 0 (lane owns elements i = lane + 64c)
@@ -208,24 +225,27 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
     const int i = lane + 64 * c;
     const bool in = w0 && i < d;
     th[c] = in ? a.theta[(long)w * d + i] : 0.0;
-    mu[c] = in ? a.mu[(long)w * d + i] : 0.0;
-    bb[c] = in ? a.b[(long)w * d + i] : 0.0;
+    mu[c] = in ? a.mu[(long)li * d + i] : 0.0;
+    bb[c] = in ? a.b[(long)li * d + i] : 0.0;
     tl[c] = (in && left >= 0) ? a.theta[(long)left * d + i] : 0.0;
     tr[c] = (in && right >= 0) ? a.theta[(long)right * d + i] : 0.0;
   }
-  const double half_yy = 0.5 * a.yy[w];
+  const double half_yy = 0.5 * a.yy[li];
   int pending = a.pending_in;
+  int stop_code = 0, stop_iter = 0;
   __syncthreads();
 
-  for (int it = a.start_iter;; ++it) {
+  int it = a.start_iter;
+  for (;; ++it) {
     // -- stop rule: decision of iteration it - lag (all workers leave at the same boundary)
     if (it - a.start_iter >= a.lag) {
       const int j = it - a.lag;
       if (threadIdx.x == 0) {
+        const unsigned tj = make_tag(a.epoch, j);
         unsigned long long v;
         for (;;) {
-          v = __hip_atomic_load(&a.decg[j % a.ring], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((unsigned)(v >> 32) == (unsigned)j) break;
+          v = load_dec<SYS>(&a.decg[j % a.ring]);
+          if ((unsigned)(v >> 32) == tj) break;
           if (now_ticks() > deadline) {
             v = 4;
             abort_lds = 1;
@@ -233,7 +253,12 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
           }
           __builtin_amdgcn_s_sleep(2);
         }
-        stop_lds = ((unsigned)(v & 0xffffffffu)) != 0u;
+        const unsigned code = (unsigned)(v & 0xffffffffu);
+        stop_lds = code != 0u;
+        if (code) {
+          stop_code = (int)code;
+          stop_iter = j;
+        }
       }
       __syncthreads();
       if (stop_lds) break;
@@ -245,8 +270,9 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
       bool ok = true;
       if (head) {
         if (it > a.start_iter) {
-          if (left >= 0) ok &= wait_row<NC>(rth, left, d, (unsigned)(it - 1), tl, deadline, &abort_lds);
-          if (ok && right >= 0) ok &= wait_row<NC>(rth, right, d, (unsigned)(it - 1), tr, deadline, &abort_lds);
+          const unsigned tp = make_tag(a.epoch, it - 1);
+          if (left >= 0) ok &= wait_row<NC, SYS>(rth, left, d, tp, tl, deadline);
+          if (ok && right >= 0) ok &= wait_row<NC, SYS>(rth, right, d, tp, tr, deadline);
         }
         if (pending) {  // lazy end-of-iteration dual (reference order: -rho(th_l - th) then +rho(th - th_r))
 #pragma unroll
@@ -258,8 +284,9 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
           }
         }
       } else {
-        if (left >= 0) ok &= wait_row<NC>(rth, left, d, (unsigned)it, tl, deadline, &abort_lds);
-        if (ok && right >= 0) ok &= wait_row<NC>(rth, right, d, (unsigned)it, tr, deadline, &abort_lds);
+        const unsigned tc = make_tag(a.epoch, it);
+        if (left >= 0) ok &= wait_row<NC, SYS>(rth, left, d, tc, tl, deadline);
+        if (ok && right >= 0) ok &= wait_row<NC, SYS>(rth, right, d, tc, tr, deadline);
       }
       if (!ok && lane == 0) abort_lds = 1;
 #pragma unroll
@@ -279,10 +306,15 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
     symv_lds<NC>(Ml, xv, tn, red, d);
     double part = 0.0;
     if (w0) {
+      const unsigned tag = make_tag(a.epoch, it);
 #pragma unroll
-      for (int c = 0; c < NC; ++c) {  // publish theta^it: one 16-B sc1 granule per element
+      for (int c = 0; c < NC; ++c) {  // publish theta^it: local table + remote neighbours' tables
         const int i = lane + 64 * c;
-        if (i < d) store_granule(rth, (w * d + i) * 16, (unsigned)it, tn[c]);
+        if (i < d) {
+          store_granule<SYS>(rth, (w * d + i) * 16, tag, tn[c]);
+          if (p0) store_granule<SYS>(rp0, (w * d + i) * 16, tag, tn[c]);
+          if (p1) store_granule<SYS>(rp1, (w * d + i) * 16, tag, tn[c]);
+        }
       }
       if (!head) {  // tails: both neighbours are this iteration's heads -> dual update now
 #pragma unroll
@@ -325,7 +357,7 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
     }
     if (w0) {
       const double f = wave_sum_f64(part) + half_yy;
-      if (lane == 0) store_granule(rob, ((it % a.ring) * n + w) * 16, (unsigned)it, f);
+      if (lane == 0) store_granule<SYS>(rob, ((it % a.ring) * n + w) * 16, make_tag(a.epoch, it), f);
 #pragma unroll
       for (int c = 0; c < NC; ++c) th[c] = tn[c];
     }
@@ -339,11 +371,21 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
       const int i = lane + 64 * c;
       if (i < d) {
         a.theta[(long)w * d + i] = th[c];
-        a.mu[(long)w * d + i] = mu[c];
+        a.mu[(long)li * d + i] = mu[c];
       }
     }
   }
-  if (abort_lds && threadIdx.x == 0) a.ctl->done = 4;
+  if (threadIdx.x == 0) {
+    if (abort_lds) {
+      a.ctl->done = 4;
+    } else if (blockIdx.x == 0 && stop_code) {
+      a.ctl->done = stop_code;
+      a.ctl->conv_iter = stop_iter;
+      a.ctl->iter = it;
+      a.ctl->pending = 1;
+      a.ctl->monitored = stop_iter;
+    }
+  }
 }
 
 extern "C" {
@@ -365,29 +407,74 @@ int gadmm_chain_persistent_launch(const PersistArgs* args, hipStream_t st) {
     gadmm_set_error("persistent chain kernel: d=%d not eligible", a.d);
     return -1;
   }
-  if (a.n + 1 > 256) {
-    gadmm_set_error("persistent chain kernel: %d workers exceed one workgroup per CU", a.n);
+  const int blocks = a.n_local + (a.has_monitor ? 1 : 0);
+  if (blocks > 256) {
+    gadmm_set_error("persistent chain kernel: %d workgroups exceed one per CU", blocks);
     return -1;
   }
   if (a.ring <= a.lag + 1) {
     gadmm_set_error("persistent chain kernel: ring must exceed lag + 1");
     return -1;
   }
+  if (a.start_iter + a.max_iter + a.lag >= (1 << 20)) {
+    gadmm_set_error("persistent chain kernel: iteration tags limited to 2^20");
+    return -1;
+  }
   const long monitor_lds = (long)a.n * 8;
   const size_t shm = (size_t)(lds > monitor_lds ? lds : monitor_lds);
+#define GADMM_P_LAUNCH(NCv, SYSv)                                                                  \
+  do {                                                                                             \
+    auto kfn = chain_persistent_kernel<NCv, SYSv>;                                                 \
+    if (shm > 65536)                                                                               \
+      GADMM_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                      (int)shm));                                                  \
+    hipLaunchKernelGGL(kfn, dim3(blocks), dim3(NT), shm, st, a);                                   \
+  } while (0)
   if (a.d <= 64) {
-    if (shm > 65536)
-      GADMM_CHECK(hipFuncSetAttribute((const void*)chain_persistent_kernel<1>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-    hipLaunchKernelGGL(chain_persistent_kernel<1>, dim3(a.n + 1), dim3(NT), shm, st, a);
+    if (a.sys_scope) GADMM_P_LAUNCH(1, true);
+    else GADMM_P_LAUNCH(1, false);
   } else {
-    if (shm > 65536)
-      GADMM_CHECK(hipFuncSetAttribute((const void*)chain_persistent_kernel<2>,
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-    hipLaunchKernelGGL(chain_persistent_kernel<2>, dim3(a.n + 1), dim3(NT), shm, st, a);
+    if (a.sys_scope) GADMM_P_LAUNCH(2, true);
+    else GADMM_P_LAUNCH(2, false);
   }
+#undef GADMM_P_LAUNCH
   GADMM_CHECK(hipGetLastError());
   return 0;
+}
+
+// ---- xGMI fabric buffers: fine-grained (uncached) device memory exported by IPC -----------------
+int gadmm_xgmi_alloc(size_t bytes, void** ptr, char* handle64) {
+  GADMM_CHECK(hipExtMallocWithFlags(ptr, bytes, hipDeviceMallocUncached));
+  GADMM_CHECK(hipMemset(*ptr, 0, bytes));
+  hipIpcMemHandle_t h;
+  GADMM_CHECK(hipIpcGetMemHandle(&h, *ptr));
+  static_assert(sizeof(hipIpcMemHandle_t) == 64, "unexpected IPC handle size");
+  memcpy(handle64, &h, 64);
+  GADMM_CHECK(hipDeviceSynchronize());
+  return 0;
+}
+
+int gadmm_xgmi_open(const char* handle64, void** ptr) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle64, 64);
+  GADMM_CHECK(hipIpcOpenMemHandle(ptr, h, hipIpcMemLazyEnablePeerAccess));
+  return 0;
+}
+
+int gadmm_xgmi_close(void* ptr) {
+  GADMM_CHECK(hipIpcCloseMemHandle(ptr));
+  return 0;
+}
+
+int gadmm_xgmi_free(void* ptr) {
+  GADMM_CHECK(hipFree(ptr));
+  return 0;
+}
+
+int gadmm_device_can_access_peer(int dev, int peer) {
+  int ok = 0;
+  if (hipDeviceCanAccessPeer(&ok, dev, peer) != hipSuccess) return -1;
+  return ok;
 }
 
 }  // extern "C"

@@ -206,6 +206,8 @@ class NativeChainEngine:
         self._install(plan)
         self.plan = plan
         self.path = [int(w) for w in path]
+        self.rank = rank
+        self._placement_owner = [int(o) for o in placement.owner]
 
     def _install(self, plan: RankPlan):
         def slots(lst):
@@ -257,10 +259,12 @@ class NativeChainEngine:
 
     # ---------------------------------------------------------------------------------------------
     # Persistent single-launch solve (csrc/kernels/chain_persistent.hip)
-    def persistent_eligible(self) -> bool:
-        if self.nranks != 1 or self.model != "linear" or self.plan is None or self.path is None:
+    def persistent_eligible(self, fabric=None) -> bool:
+        if self.model != "linear" or self.plan is None or self.path is None:
             return False
-        if self.n_total + 1 > 256 or self.n_local != self.n_total:
+        if self.nranks != 1 and fabric is None:
+            return False
+        if self.n_local + 1 > 256:
             return False
         return int(self.lib.gadmm_chain_persistent_lds(self.d, self._obj_mode())) > 0
 
@@ -269,38 +273,70 @@ class NativeChainEngine:
         return 0 if int(self.lib.gadmm_chain_persistent_lds(self.d, 0)) > 0 else 1
 
     def run_persistent(self, lag: int = 4, timeout_s: float = 20.0, start_iter: int = 1,
-                       pending_in: int = 0) -> EngineRun:
-        """Whole solve in one launch. State must be reset (``reset()``) or resumed by the caller."""
-        if not self.persistent_eligible():
+                       pending_in: int = 0, fabric=None) -> EngineRun:
+        """Whole solve in one launch per GPU. State must be reset (``reset()``) or resumed by the
+        caller. ``fabric``: an ``XgmiFabric`` for the multi-GPU device-initiated transport."""
+        if not self.persistent_eligible(fabric):
             raise RuntimeError("persistent kernel not eligible for this engine/config")
         ring = lag + 4
         dev = self.device
-        if getattr(self, "_pbuf", None) is None or self._pbuf[0] != ring:
+        slots = sorted(self.plan.head + self.plan.tail, key=lambda s: self.path.index(s.gid))
+        pos = [self.path.index(s.gid) for s in slots]
+        key = (ring, tuple((s.li, s.gid, s.left, s.right) for s in slots), id(fabric))
+        if getattr(self, "_pbuf", None) is None or self._pbuf[0] != key:
             with torch.cuda.stream(self.stream):
-                thg = torch.zeros((self.n_total * self.d * 4,), dtype=torch.int32, device=dev)
-                objg = torch.zeros((ring * self.n_total * 4,), dtype=torch.int32, device=dev)
-                decg = torch.zeros((ring,), dtype=torch.int64, device=dev)
-            self._pbuf = (ring, thg, objg, decg)
-        _, thg, objg, decg = self._pbuf
-        path_t = torch.tensor(self.path, dtype=torch.int32, device=dev)
+                slot_t = torch.tensor([[s.li, s.gid, s.left, s.right] for s in slots], dtype=torch.int32,
+                                      device=dev).reshape(-1)
+                pos_t = torch.tensor(pos, dtype=torch.int32, device=dev)
+                if fabric is None:
+                    thg = torch.zeros((self.n_total * self.d * 4,), dtype=torch.int32, device=dev)
+                    objg = torch.zeros((ring * self.n_total * 4,), dtype=torch.int32, device=dev)
+                    decg = torch.zeros((ring,), dtype=torch.int64, device=dev)
+                    ptrs = (thg.data_ptr(), objg.data_ptr(), decg.data_ptr())
+                    push = None
+                    dec_push = torch.tensor([decg.data_ptr()], dtype=torch.int64, device=dev)
+                    keep = (thg, objg, decg)
+                else:
+                    owner = self._placement_owner
+                    pl = []
+                    for s in slots:
+                        peers = sorted({int(owner[u]) for u in (s.left, s.right) if u >= 0} - {self.rank})
+                        ps = [fabric.thg_peer[r] for r in peers] + [0, 0]
+                        pl += ps[:2]
+                    push = torch.tensor(pl, dtype=torch.int64, device=dev)
+                    ptrs = (fabric.thg.ptr.value, fabric.objg_mon, fabric.decg.ptr.value)
+                    dec_push = torch.tensor(fabric.dec_all if fabric.dec_all else [0], dtype=torch.int64,
+                                            device=dev)
+                    keep = ()
+            self._pbuf = (key, slot_t, pos_t, ptrs, push, dec_push, keep, [0])
+        _, slot_t, pos_t, ptrs, push, dec_push, keep, epoch_box = self._pbuf
+        if fabric is not None:
+            epoch = fabric.next_epoch()
+        else:
+            epoch_box[0] = epoch_box[0] % 4095 + 1
+            epoch = epoch_box[0]
         pa = native.PersistArgs()
-        pa.d, pa.n, pa.start_iter, pa.max_iter = self.d, self.n_total, int(start_iter), self.max_iter
+        pa.d, pa.n, pa.n_local, pa.start_iter, pa.max_iter = self.d, self.n_total, len(slots), int(start_iter), \
+            self.max_iter
         pa.lag, pa.ring, pa.nvar, pa.obj_mode = int(lag), ring, self.nvar, self._obj_mode()
         for i, v in enumerate(self.deg_to_var):
             pa.deg_to_var[i] = v
         pa.pending_in = int(pending_in)
+        pa.has_monitor = 1 if (fabric is None or self.rank == 0) else 0
+        pa.nranks = 1 if fabric is None else self.nranks
+        pa.sys_scope = 0 if fabric is None else 1
+        pa.epoch = int(epoch)
         pa.rho, pa.obj0, pa.tol = self.rho, self.obj0, self.tol
         pa.timeout_ticks = int(timeout_s * 1e8)
-        pa.path = path_t.data_ptr()
+        pa.slots, pa.pos = slot_t.data_ptr(), pos_t.data_ptr()
         pa.Minv, pa.A, pa.b, pa.yy = self.Minv.data_ptr(), self.A.data_ptr(), self.b.data_ptr(), self.yy.data_ptr()
         pa.theta, pa.mu = self.theta.data_ptr(), self.mu.data_ptr()
-        pa.thg, pa.objg, pa.decg = thg.data_ptr(), objg.data_ptr(), decg.data_ptr()
+        pa.thg, pa.objg, pa.decg = ptrs
+        pa.push = push.data_ptr() if push is not None else None
+        pa.dec_push = dec_push.data_ptr()
         pa.trace, pa.ctl = self.trace.data_ptr(), self.ctl.data_ptr()
         import time as _time
         with torch.cuda.stream(self.stream):
-            thg.zero_()
-            objg.zero_()
-            decg.zero_()
             t0 = _time.perf_counter()
             native.check(self.lib.gadmm_chain_persistent_launch(ctypes.byref(pa), self.stream.cuda_stream),
                          "chain_persistent_launch")

@@ -70,12 +70,14 @@ class RunStats(ctypes.Structure):
 
 class PersistArgs(ctypes.Structure):
     _fields_ = [
-        ("d", c_int), ("n", c_int), ("start_iter", c_int), ("max_iter", c_int), ("lag", c_int), ("ring", c_int),
-        ("nvar", c_int), ("obj_mode", c_int), ("deg_to_var", c_int * 3), ("pending_in", c_int),
+        ("d", c_int), ("n", c_int), ("n_local", c_int), ("start_iter", c_int), ("max_iter", c_int),
+        ("lag", c_int), ("ring", c_int), ("nvar", c_int), ("obj_mode", c_int), ("deg_to_var", c_int * 3),
+        ("pending_in", c_int), ("has_monitor", c_int), ("nranks", c_int), ("sys_scope", c_int),
+        ("epoch", ctypes.c_uint), ("pad_", c_int),
         ("rho", c_double), ("obj0", c_double), ("tol", c_double), ("timeout_ticks", c_longlong),
-        ("path", c_void_p), ("Minv", c_void_p), ("A", c_void_p), ("b", c_void_p), ("yy", c_void_p),
-        ("theta", c_void_p), ("mu", c_void_p), ("thg", c_void_p), ("objg", c_void_p), ("decg", c_void_p),
-        ("trace", c_void_p), ("ctl", c_void_p),
+        ("slots", c_void_p), ("pos", c_void_p), ("Minv", c_void_p), ("A", c_void_p), ("b", c_void_p),
+        ("yy", c_void_p), ("theta", c_void_p), ("mu", c_void_p), ("thg", c_void_p), ("push", c_void_p),
+        ("objg", c_void_p), ("decg", c_void_p), ("dec_push", c_void_p), ("trace", c_void_p), ("ctl", c_void_p),
     ]
 
 
@@ -110,6 +112,11 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
         "gadmm_chain_persistent_lds": (c_long, [c_int, c_int]),
         "gadmm_chain_big_rbuf_stride": (c_long, [c_int]),
+        "gadmm_xgmi_alloc": (c_int, [ctypes.c_size_t, ctypes.POINTER(c_void_p), ctypes.c_char_p]),
+        "gadmm_xgmi_open": (c_int, [ctypes.c_char_p, ctypes.POINTER(c_void_p)]),
+        "gadmm_xgmi_close": (c_int, [c_void_p]),
+        "gadmm_xgmi_free": (c_int, [c_void_p]),
+        "gadmm_device_can_access_peer": (c_int, [c_int, c_int]),
         "gadmm_chain_persistent_launch": (c_int, [ctypes.POINTER(PersistArgs), c_void_p]),
         "gadmm_rccl_unique_id": (c_int, [ctypes.c_char_p]),
         "gadmm_rccl_version": (c_int, []),

@@ -85,6 +85,20 @@ class Comm:
     def _allreduce_max(self, t):
         return t
 
+    def close(self) -> None:
+        pass
+
+
+class RankInfo(Comm):
+    """Rank identity without a data-plane communicator (the xGMI fabric moves the data)."""
+
+    backend = "none"
+
+    def __init__(self, rank: int, nranks: int):
+        super().__init__()
+        self.rank, self.nranks = rank, nranks
+        self.handle = None
+
 
 class LocalComm(Comm):
     backend = "local"

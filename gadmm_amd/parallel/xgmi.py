@@ -1,0 +1,121 @@
+"""xGMI-direct fabric for the persistent chain kernel on several MI355X (one process per GPU).
+
+The RCCL path (``RcclComm`` + graph-replayed phase kernels) pays a collective/p2p launch and a kernel
+boundary per phase. At the reference problem sizes a phase is ~1 us of arithmetic, so on a single
+node the framework can instead keep one persistent kernel per GPU and move the boundary theta
+*device-initiated*: every GPU allocates fine-grained (uncached) granule buffers, exports them by IPC
+(dmabuf; HSA_ENABLE_IPC_MODE_LEGACY=0), and maps its chain neighbours' buffers; a worker's kernel
+writes its fresh theta granules straight into the neighbour GPU's table over xGMI (every pair of
+MI355X in a node is one xGMI hop), objective granules into rank 0's monitor ring, and rank 0's
+monitor writes each stop decision into every rank's ring. The hand-off protocol is the same tagged
+granule protocol as on one GPU (tags salted per solve), so correctness does not depend on timing;
+every spin is bounded, and a stalled peer surfaces as ``done == 4`` (the caller falls back to RCCL).
+
+Handles travel over the gloo control plane (``dist.all_gather_object``).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops import native
+
+
+class _Buf:
+    def __init__(self, lib, nbytes: int):
+        self.lib = lib
+        self.ptr = ctypes.c_void_p()
+        self.handle = ctypes.create_string_buffer(64)
+        native.check(lib.gadmm_xgmi_alloc(nbytes, ctypes.byref(self.ptr), self.handle), "xgmi_alloc")
+        self.nbytes = nbytes
+
+    def free(self):
+        if self.ptr:
+            self.lib.gadmm_xgmi_free(self.ptr)
+            self.ptr = ctypes.c_void_p()
+
+
+class XgmiFabric:
+    """Per-rank granule buffers + the peers' mapped buffers.
+
+    theta table: (N, d) x 16-B granules on every rank; objective ring: (ring, N) x 16 B (read on the
+    monitor rank 0); decision ring: ring x 8 B on every rank."""
+
+    def __init__(self, n_total: int, d: int, ring: int, rank: int, nranks: int, device: torch.device,
+                 group=None, peers_needed: Optional[List[int]] = None):
+        """Collective over ``group``: every rank must call it. Failures on any rank are raised on
+        every rank (so callers can fall back together)."""
+        self.lib = native.require()
+        self.rank, self.nranks, self.device = rank, nranks, device
+        self.n, self.d, self.ring = n_total, d, ring
+        self.opened: Dict[tuple, ctypes.c_void_p] = {}
+        self.thg = self.objg = self.decg = None
+        torch.cuda.set_device(device)
+        mine = None
+        err = ""
+        try:
+            self.thg = _Buf(self.lib, n_total * d * 16)
+            self.objg = _Buf(self.lib, ring * n_total * 16)
+            self.decg = _Buf(self.lib, ring * 8)
+            mine = (bytes(self.thg.handle.raw), bytes(self.objg.handle.raw), bytes(self.decg.handle.raw))
+        except Exception as e:
+            err = "rank %d alloc: %s" % (rank, e)
+        allh = [None] * nranks
+        dist.all_gather_object(allh, (mine, err), group=group)
+        errs = [e for _, e in allh if e]
+        if errs:
+            self.close()
+            raise RuntimeError("xgmi fabric: " + "; ".join(errs))
+        allh = [h for h, _ in allh]
+        ok = True
+        try:
+            need_thg = set(peers_needed if peers_needed is not None else [r for r in range(nranks) if r != rank])
+            self.thg_peer: Dict[int, int] = {}
+            for r in need_thg:
+                self.thg_peer[r] = self._open(allh[r][0], ("thg", r))
+            self.objg_mon = self.objg.ptr.value if rank == 0 else self._open(allh[0][1], ("objg", 0))
+            self.dec_all: List[int] = []
+            if rank == 0:
+                for r in range(nranks):
+                    self.dec_all.append(self.decg.ptr.value if r == 0 else self._open(allh[r][2], ("decg", r)))
+        except Exception as e:
+            ok = False
+            err = str(e)
+        flag = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64)
+        dist.all_reduce(flag, group=group)
+        if float(flag.item()) != 0.0:
+            self.close()
+            raise RuntimeError("xgmi fabric: peer mapping failed on some rank (%s)" % (err or "remote"))
+        self.epoch = 0
+
+    def _open(self, h: bytes, key) -> int:
+        p = ctypes.c_void_p()
+        native.check(self.lib.gadmm_xgmi_open(ctypes.create_string_buffer(h, 64), ctypes.byref(p)),
+                     "xgmi_open %s" % (key,))
+        self.opened[key] = p
+        return p.value
+
+    def next_epoch(self) -> int:
+        self.epoch = (self.epoch + 1) % 4095 + 1
+        return self.epoch
+
+    def close(self):
+        for p in self.opened.values():
+            self.lib.gadmm_xgmi_close(p)
+        self.opened = {}
+        for b in (self.thg, self.objg, self.decg):
+            if b is not None:
+                b.free()
+        self.thg = self.objg = self.decg = None
+
+
+def peer_access_ok(nranks: int) -> bool:
+    lib = native.require()
+    n = torch.cuda.device_count()
+    if n < 2:
+        return True
+    return all(lib.gadmm_device_can_access_peer(i, j) == 1 for i in range(min(n, nranks)) for j in range(min(n, nranks))
+               if i != j)
