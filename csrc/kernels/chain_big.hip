@@ -157,12 +157,12 @@ __global__ void __launch_bounds__(1024) chain_big_post(PhaseArgs a) {
   if (a.obj_mode != 0) {
     f = block_sum_f64(part, scratch);
   } else {
-    // fixed-order sum of the per-workgroup partials of chain_big_obj
+    // fixed-order sum of the per-workgroup partials of chain_big_obj: strided per thread, then the
+    // deterministic block reduction (same order every call)
     const int nblk = (a.d + ROWS_PER_WG - 1) / ROWS_PER_WG;
     double t = 0.0;
-    if (threadIdx.x == 0)
-      for (int k = 0; k < nblk; ++k) t += r[d + k];
-    f = t;
+    for (int k = threadIdx.x; k < nblk; k += blockDim.x) t += r[d + k];
+    f = block_sum_f64(t, scratch);
   }
   if (threadIdx.x == 0) a.objw[s.li] = f + 0.5 * a.yy[s.li];
   if (a.flags & PH_FINISH) {

@@ -16,6 +16,7 @@
 //
 // f64 MFMA fragment maps (cdna_hip_programming.md §3): A/B one f64 per lane, A[i=l&15][k=l>>4],
 // B[k=l>>4][j=l&15]; C/D col = l&15, row = (l>>4) + 4*reg.
+#include <stdlib.h>
 #include "gadmm_common.h"
 
 namespace {
@@ -31,15 +32,7 @@ struct GramTile {
   static constexpr int PER_THREAD = BK * BT / 256;
 };
 
-__device__ __forceinline__ double aug_load(const double* __restrict__ H, const double* __restrict__ y,
-                                           long k, int c, int d, long kend) {
-  if (k >= kend) return 0.0;
-  if (c < d) return H[k * (long)d + c];
-  if (c == d) return y[k];
-  return 0.0;
-}
-
-template <int BT>
+template <int BT, bool EVEN>
 __global__ void __launch_bounds__(256)
 gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int m, int d,
                 int ntiles, int ksplit, long rows_per_split,
@@ -81,24 +74,70 @@ gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int 
 #pragma unroll
     for (int b = 0; b < T::TM; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
 
-  // staging: thread t loads slab element e = t + 256*p  (row = e / BT, col = e % BT)
+  // staging: thread t loads slab element e = t + 256*p  (row = e / BT, col = e % BT).
+  // Interior tiles (every column < d, every row < kend, d even) take branch-free 16-byte loads;
+  // boundary tiles take branch-free clamped loads + selects. A per-element branch around each load
+  // would make hipcc drain vmcnt(0) per element (cdna_hip_programming.md §5, trap (c)).
   double ri[T::PER_THREAD], rj[T::PER_THREAD];
+  const bool cols_in = (row0 + BT <= d) && (diag || col0 + BT <= d);
   auto fetch = [&](long k0) {
+    const bool interior = cols_in && (k0 + BK <= kend);
+    if (!EVEN && interior) {  // odd d: rows are not 16-B aligned -> branch-free 8-B loads
 #pragma unroll
-    for (int p = 0; p < T::PER_THREAD; ++p) {
-      const int e = tid + 256 * p;
-      const int r = e / BT, c = e % BT;
-      ri[p] = (row0 + c < D) ? aug_load(H, yv, k0 + r, row0 + c, d, kend) : 0.0;
-      if (!diag) rj[p] = (col0 + c < D) ? aug_load(H, yv, k0 + r, col0 + c, d, kend) : 0.0;
+      for (int p = 0; p < T::PER_THREAD / 2; ++p) {
+        const int e2 = tid + 256 * p;
+        const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
+        const double* src = H + (k0 + r) * (long)d;
+        ri[2 * p] = src[row0 + c];
+        ri[2 * p + 1] = src[row0 + c + 1];
+        if (!diag) {
+          rj[2 * p] = src[col0 + c];
+          rj[2 * p + 1] = src[col0 + c + 1];
+        }
+      }
+    } else if (EVEN && interior) {
+#pragma unroll
+      for (int p = 0; p < T::PER_THREAD / 2; ++p) {
+        const int e2 = tid + 256 * p;
+        const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
+        const double2 a = *reinterpret_cast<const double2*>(H + (k0 + r) * (long)d + row0 + c);
+        ri[2 * p] = a.x;
+        ri[2 * p + 1] = a.y;
+        if (!diag) {
+          const double2 b = *reinterpret_cast<const double2*>(H + (k0 + r) * (long)d + col0 + c);
+          rj[2 * p] = b.x;
+          rj[2 * p + 1] = b.y;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int p = 0; p < T::PER_THREAD / 2; ++p) {
+        const int e2 = tid + 256 * p;
+        const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
+        const long k = k0 + r;
+        const long kk = k < kend ? k : (kend - 1);
+        const double yk = yv[kk];
+        const bool kin = k < kend;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          const int ca = row0 + c + q, cb = col0 + c + q;
+          const double va = H[kk * d + (ca < d ? ca : d - 1)];
+          ri[2 * p + q] = kin ? (ca < d ? va : (ca == d ? yk : 0.0)) : 0.0;
+          if (!diag) {
+            const double vb = H[kk * d + (cb < d ? cb : d - 1)];
+            rj[2 * p + q] = kin ? (cb < d ? vb : (cb == d ? yk : 0.0)) : 0.0;
+          }
+        }
+      }
     }
   };
   auto stash = [&]() {
 #pragma unroll
-    for (int p = 0; p < T::PER_THREAD; ++p) {
-      const int e = tid + 256 * p;
-      const int r = e / BT, c = e % BT;
-      Li[r * T::LDSROW + c] = ri[p];
-      if (!diag) Lj[r * T::LDSROW + c] = rj[p];
+    for (int p = 0; p < T::PER_THREAD / 2; ++p) {
+      const int e2 = tid + 256 * p;
+      const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
+      *reinterpret_cast<double2*>(Li + r * T::LDSROW + c) = make_double2(ri[2 * p], ri[2 * p + 1]);
+      if (!diag) *reinterpret_cast<double2*>(Lj + r * T::LDSROW + c) = make_double2(rj[2 * p], rj[2 * p + 1]);
     }
   };
 
@@ -196,8 +235,13 @@ int launch_gram(const double* X, const double* Y, int N, int m, int d, int kspli
   ksplit = (int)(((long)m + rows - 1) / rows);
   if (ksplit < 1) ksplit = 1;
   const long nwg = (long)ntiles * ksplit * N;
-  hipLaunchKernelGGL(gram_aug_kernel<BT>, dim3((unsigned)nwg), dim3(256), 0, st, X, Y, m, d, ntiles,
-                     ksplit, rows, A, B, YY, slab);
+  static const bool novec = getenv("GADMM_GRAM_NOVEC") != nullptr;  // A/B switch (tools/gram_bench.py)
+  if ((d & 1) == 0 && !novec)
+    hipLaunchKernelGGL((gram_aug_kernel<BT, true>), dim3((unsigned)nwg), dim3(256), 0, st, X, Y, m, d, ntiles,
+                       ksplit, rows, A, B, YY, slab);
+  else
+    hipLaunchKernelGGL((gram_aug_kernel<BT, false>), dim3((unsigned)nwg), dim3(256), 0, st, X, Y, m, d, ntiles,
+                       ksplit, rows, A, B, YY, slab);
   if (ksplit > 1) {
     hipLaunchKernelGGL(gram_reduce_kernel<BT>, dim3(ntiles, N), dim3(256), 0, st, slab, d, ntiles,
                        ksplit, A, B, YY);
