@@ -26,112 +26,13 @@
 // done = 4 and every workgroup exits.
 #include "gadmm_common.h"
 #include "gadmm_chain.h"
+#include "persist_device.h"
 #include <string.h>
 
 namespace {
 
 constexpr int NT = 256;
 constexpr int NW = 4;
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
-}
-
-template <bool SYS>
-__device__ __forceinline__ void store_granule(__amdgpu_buffer_rsrc_t rs, int byte_off, unsigned tag, double v) {
-  const unsigned long long bits = __double_as_longlong(v);
-  u32x4 g = {tag, (unsigned)(bits & 0xffffffffull), tag, (unsigned)(bits >> 32)};
-  if (SYS) __builtin_amdgcn_raw_buffer_store_b128(g, rs, byte_off, 0, 17 /* sc0 sc1 */);
-  else __builtin_amdgcn_raw_buffer_store_b128(g, rs, byte_off, 0, 16 /* sc1 */);
-}
-
-template <bool SYS>
-__device__ __forceinline__ bool load_granule(__amdgpu_buffer_rsrc_t rs, int byte_off, unsigned tag, double* v) {
-  const u32x4 g = SYS ? __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 17)
-                      : __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16);
-  *v = __longlong_as_double((long long)(((unsigned long long)g.w << 32) | g.y));
-  return g.x == tag && g.z == tag;
-}
-
-template <bool SYS>
-__device__ __forceinline__ void store_dec(unsigned long long* p, unsigned long long v) {
-  if (SYS) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <bool SYS>
-__device__ __forceinline__ unsigned long long load_dec(unsigned long long* p) {
-  if (SYS) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ unsigned long long now_ticks() { return __builtin_amdgcn_s_memrealtime(); }
-
-__device__ __forceinline__ unsigned make_tag(unsigned epoch, int it) { return (epoch << 20) | ((unsigned)it & 0xfffffu); }
-
-// Every lane of wave 0 polls the granules of its elements of table row `row` until all carry `tag`.
-template <int NC, bool SYS>
-__device__ __forceinline__ bool wait_row(__amdgpu_buffer_rsrc_t rs, int row, int d, unsigned tag, double (&out)[NC],
-                                         unsigned long long deadline) {
-  const int lane = threadIdx.x & 63;
-  for (;;) {
-    bool ok = true;
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int i = lane + 64 * c;
-      if (i < d) ok &= load_granule<SYS>(rs, (row * d + i) * 16, tag, &out[c]);
-    }
-    if (__all(ok)) return true;
-    if (now_ticks() > deadline) return false;
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// y[i] = sum_j M[j][i] x[j] with M (symmetric) and x in LDS; lanes own i, waves split j.
-template <int NC>
-__device__ __forceinline__ void symv_lds(const double* M, const double* x, double (&y)[NC], double* red, int d) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  double acc[NC];
-#pragma unroll
-  for (int c = 0; c < NC; ++c) acc[c] = 0.0;
-  // 4 rows of M per batch per wave: the 4 (x NC) LDS loads issue together, one wait per batch
-  int j = w;
-  for (; j + 3 * NW < d; j += 4 * NW) {
-    double mv[4][NC], xv[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      xv[q] = x[j + q * NW];
-#pragma unroll
-      for (int c = 0; c < NC; ++c) {
-        const int i = lane + 64 * c;
-        mv[q][c] = i < d ? M[(j + q * NW) * d + i] : 0.0;
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-#pragma unroll
-      for (int c = 0; c < NC; ++c) acc[c] = fma(mv[q][c], xv[q], acc[c]);
-  }
-  for (; j < d; j += NW) {
-    const double xj = x[j];
-#pragma unroll
-    for (int c = 0; c < NC; ++c) {
-      const int i = lane + 64 * c;
-      if (i < d) acc[c] = fma(M[j * d + i], xj, acc[c]);
-    }
-  }
-#pragma unroll
-  for (int c = 0; c < NC; ++c) red[(w * NC + c) * 64 + lane] = acc[c];
-  __syncthreads();
-#pragma unroll
-  for (int c = 0; c < NC; ++c) {
-    double s = 0.0;
-#pragma unroll
-    for (int ww = 0; ww < NW; ++ww) s += red[(ww * NC + c) * 64 + lane];
-    y[c] = s;  // every wave holds the full result for its lanes' rows
-  }
-  __syncthreads();
-}
 
 }  // namespace
 

@@ -13,6 +13,10 @@ Realisation on the fabric:
 * cIAG / RIAG: one worker refreshes per iteration and uploads its row to the server. RIAG's draw
   uses an RNG seeded identically on every rank (no message).
 
+Single GPU: when every worker lives on one CUDA device (one rank) and d <= 128, each algorithm
+runs as ONE persistent kernel launch (``engine/first_order.py``, ``csrc/kernels/first_order.hip``);
+``backend="torch"`` forces the implementation below (the multi-rank path and the test oracle).
+
 Faithful quirks (SURVEY.md §5, ``faithful=True``): gradients start as ``ones`` (GD_DGD_LAG.m:44-67);
 LAG-PS refreshes worker 1 every iteration (timing side effect, :204-209); LAG does nothing before
 ``iter > triggerslot = 10``; a communication unit is still counted every 1000 quiet iterations
@@ -93,6 +97,29 @@ def _gather_hmax(ctx: _Ctx, hmax_local: torch.Tensor) -> torch.Tensor:
     return ctx.allsum(full)
 
 
+def _fo_engine(ctx: _Ctx, backend: str):
+    """The persistent first-order engine when this run can use it (None -> torch path)."""
+    if backend == "torch":
+        return None
+    from ..engine.first_order import FirstOrderEngine
+
+    ok = FirstOrderEngine.eligible(ctx.model, ctx.comm, ctx.n_total)
+    if not ok:
+        if backend == "native":
+            raise RuntimeError("native first-order engine needs one rank on a GPU with d <= 128")
+        return None
+    return FirstOrderEngine.get(ctx.model)
+
+
+def _native_result(name, out, obj0, units, **extra) -> RunResult:
+    obj = out["obj"]
+    n = len(obj)
+    return RunResult(algorithm=name, obj=obj, loss=np.abs(obj - obj0), iters=out["iters"] if out["converged"] else n,
+                     converged=out["converged"], wall_s=float(out["times"][-1]) if n else 0.0,
+                     time_trace=out["times"], comm_units=units, bytes_sent=0, bytes_total=0,
+                     extra=dict(extra, engine="native-persistent"))
+
+
 def _result(name, stop: Stopper, ctx: _Ctx, units: np.ndarray, converged: bool, iters: int, **extra):
     obj, loss, times = stop.arrays()
     return RunResult(algorithm=name, obj=obj, loss=loss, iters=iters, converged=converged,
@@ -103,8 +130,14 @@ def _result(name, stop: Stopper, ctx: _Ctx, units: np.ndarray, converged: bool, 
 
 # ------------------------------------------------------------------------------------------------- GD
 def gradient_descent(model, local_ids, n_total, num_iter, obj0, stepsize, comm=None, placement=None,
-                     faithful=True, tol: Optional[float] = None) -> RunResult:
+                     faithful=True, tol: Optional[float] = None, backend: str = "auto") -> RunResult:
     ctx = _Ctx(model, local_ids, n_total, comm, placement)
+    eng = _fo_engine(ctx, backend)
+    if eng is not None:
+        out = eng.run("GD", num_iter, stepsize, obj0, tol, faithful)
+        n = len(out["obj"])
+        return _native_result("GD", out, obj0, np.arange(1, n + 1, dtype=np.float64) * (n_total + 1),
+                              final_theta=None)
     d = ctx.d
     theta = torch.zeros(d, dtype=torch.float64, device=ctx.dev)
     stop = Stopper(obj0, tol if tol is not None else -1.0, num_iter)
@@ -132,9 +165,14 @@ def gradient_descent(model, local_ids, n_total, num_iter, obj0, stepsize, comm=N
 
 # ------------------------------------------------------------------------------------------------ DGD
 def decentralized_gd(model, local_ids, n_total, num_iter, obj0, stepsize, comm=None, placement=None,
-                     faithful=True, tol: Optional[float] = None) -> RunResult:
+                     faithful=True, tol: Optional[float] = None, backend: str = "auto") -> RunResult:
     """DGD (GD_DGD_LAG.m:124-180): step stepsize/100 on the chain-neighbour average of gradients."""
     ctx = _Ctx(model, local_ids, n_total, comm, placement)
+    eng = _fo_engine(ctx, backend)
+    if eng is not None:
+        out = eng.run("DGD", num_iter, stepsize / 100.0, obj0, tol, faithful)
+        n = len(out["obj"])
+        return _native_result("DGD", out, obj0, np.arange(1, n + 1, dtype=np.float64) * n_total)
     d, dev = ctx.d, ctx.dev
     nl = len(ctx.local_ids)
     theta = torch.zeros((nl, d), dtype=torch.float64, device=dev)
@@ -222,13 +260,30 @@ class _Server:
         return new
 
 
+def _lag_units(counts: np.ndarray) -> np.ndarray:
+    """Reference communication units of LAG from the per-iteration upload counts (GD_DGD_LAG.m:246-251)."""
+    comm_iter, out = 1.0, []
+    for it, c in enumerate(counts, start=1):
+        if c > 0:
+            comm_iter += c
+        elif it % 1000 == 0:
+            comm_iter += 1
+        out.append(comm_iter)
+    return np.asarray(out) + np.arange(1, len(out) + 1)
+
+
 def lag(model, local_ids, n_total, num_iter, obj0, stepsize, hmax_full: torch.Tensor, variant: str = "PS",
-        comm=None, placement=None, faithful=True, tol: Optional[float] = None) -> RunResult:
+        comm=None, placement=None, faithful=True, tol: Optional[float] = None, backend: str = "auto") -> RunResult:
     """LAG-PS (server-side trigger) / LAG-WK (worker-side trigger), GD_DGD_LAG.m:184-327."""
     ctx = _Ctx(model, local_ids, n_total, comm, placement)
     d, dev = ctx.d, ctx.dev
     N = n_total
     thrd = (10.0 if variant == "PS" else 1.0) / (stepsize ** 2 * N ** 2) / TRIGGERSLOT
+    eng = _fo_engine(ctx, backend)
+    if eng is not None:
+        out = eng.run("LAG-" + variant, num_iter, stepsize, obj0, tol, faithful, thrd=thrd,
+                      hsq=hmax_full.to(dev, torch.float64) ** 2)
+        return _native_result("LAG-" + variant, out, obj0, _lag_units(out["cnt"]), uploads=int(round(out["uploads"])))
     ids = torch.tensor(ctx.local_ids, dtype=torch.long, device=dev)
     nl = len(ctx.local_ids)
     server = _Server(ctx, torch.ones((N, d), dtype=torch.float64, device=dev))
@@ -238,6 +293,7 @@ def lag(model, local_ids, n_total, num_iter, obj0, stepsize, hmax_full: torch.Te
     hist = [torch.zeros(d, dtype=torch.float64, device=dev)]        # theta^{iter-11..iter}
     comm_iter = 1.0
     comm_final = []
+    counts_trace = []
     uploads = 0
     stop = Stopper(obj0, tol if tol is not None else -1.0, num_iter)
     converged, iters = False, num_iter
@@ -276,6 +332,7 @@ def lag(model, local_ids, n_total, num_iter, obj0, stepsize, hmax_full: torch.Te
             ctx.comm.allreduce_sum(t)
             c_all = int(t.item())
         uploads += c_all
+        counts_trace.append(c_all)
         hit = stop.record(ctx.obj(theta))
         if c_all > 0:
             comm_iter += c_all
@@ -290,33 +347,46 @@ def lag(model, local_ids, n_total, num_iter, obj0, stepsize, hmax_full: torch.Te
             break
     n = len(stop.obj)
     units = np.asarray(comm_final) + np.arange(1, n + 1)
+    assert np.array_equal(units, _lag_units(np.asarray(counts_trace)))
     return _result("LAG-" + variant, stop, ctx, units, converged, iters if converged else n, uploads=uploads)
 
 
 # ------------------------------------------------------------------------------------------------ IAG
+def iag_schedule(n_total: int, num_iter: int, mode: str, hmax_full=None, seed: int = 7) -> np.ndarray:
+    """Refreshing worker of every iteration (index it-1): ``it mod N`` or a draw proportional to
+    Hmax_i from a generator seeded identically on every rank."""
+    its = np.arange(1, num_iter + 1)
+    if mode == "cyclic":
+        return (its % n_total).astype(np.int64)
+    rng = np.random.default_rng(seed)
+    prob = np.asarray(hmax_full.cpu().numpy(), dtype=np.float64)
+    cum = np.cumsum(prob / prob.sum())
+    return np.minimum(np.searchsorted(cum, rng.random(num_iter), side="left"), n_total - 1).astype(np.int64)
+
+
 def iag(model, local_ids, n_total, num_iter, obj0, stepsize, mode: str = "cyclic", hmax_full=None, seed: int = 7,
-        comm=None, placement=None, faithful=True, tol: Optional[float] = None) -> RunResult:
+        comm=None, placement=None, faithful=True, tol: Optional[float] = None, backend: str = "auto") -> RunResult:
     """Cyclic IAG (worker ``iter mod N`` refreshes) and non-uniform randomized IAG (worker drawn
     with probability proportional to Hmax_i); step alpha/N (GD_DGD_LAG.m:330-371)."""
     ctx = _Ctx(model, local_ids, n_total, comm, placement)
+    name = "cIAG" if mode == "cyclic" else "R-IAG"
+    sched = iag_schedule(n_total, num_iter, mode, hmax_full, seed)
+    eng = _fo_engine(ctx, backend)
+    if eng is not None:
+        out = eng.run("IAG", num_iter, stepsize / n_total, obj0, tol, faithful, sched=sched)
+        n = len(out["obj"])
+        return _native_result(name, out, obj0, np.arange(1, n + 1, dtype=np.float64) * 2)
     d, dev = ctx.d, ctx.dev
     N = n_total
     step = stepsize / N
     server = _Server(ctx, torch.ones((N, d), dtype=torch.float64, device=dev))
     theta = torch.zeros(d, dtype=torch.float64, device=dev)
-    rng = np.random.default_rng(seed)
-    if mode != "cyclic":
-        prob = np.asarray(hmax_full.cpu().numpy(), dtype=np.float64)
-        cum = np.cumsum(prob / prob.sum())
     stop = Stopper(obj0, tol if tol is not None else -1.0, num_iter)
     converged, iters = False, num_iter
     empty_r = torch.zeros(0, dtype=torch.long, device=dev)
     empty_v = torch.zeros((0, d), dtype=torch.float64, device=dev)
     for it in range(1, num_iter + 1):
-        if mode == "cyclic":
-            w = it % N
-        else:
-            w = min(int(np.searchsorted(cum, rng.random(), side="left")), N - 1)
+        w = int(sched[it - 1])
         if it > 1:
             if int(ctx.placement.owner[w]) == ctx.comm.rank:
                 g = ctx.worker_grad(w, theta)
@@ -329,14 +399,14 @@ def iag(model, local_ids, n_total, num_iter, obj0, stepsize, mode: str = "cyclic
             converged, iters = True, it
             break
     n = len(stop.obj)
-    return _result("cIAG" if mode == "cyclic" else "R-IAG", stop, ctx, np.arange(1, n + 1, dtype=np.float64) * 2,
+    return _result(name, stop, ctx, np.arange(1, n + 1, dtype=np.float64) * 2,
                    converged, iters if converged else n)
 
 
 # ------------------------------------------------------------------------------------------- bundle
 def gd_dgd_lag(model, local_ids, n_total, num_iter, obj0: Optional[float], comm=None, placement=None,
                faithful=True, accuracy: Optional[float] = None, which=("GD", "DGD", "LAG-PS", "LAG-WK", "cIAG", "R-IAG"),
-               seed: int = 7) -> Dict[str, object]:
+               seed: int = 7, backend: str = "auto") -> Dict[str, object]:
     """The reference bundle: ``GD_DGD_LAG`` (linear, obj0 given) or ``GD_DGD_LAG_logistic`` (obj0 =
     final GD objective, returned as ``obj1``; LAG/IAG stop at ``accuracy``)."""
     comm = comm if comm is not None else LocalComm()
@@ -348,7 +418,7 @@ def gd_dgd_lag(model, local_ids, n_total, num_iter, obj0: Optional[float], comm=
     logistic = model.kind == "logistic"
     if "GD" in which or logistic:
         gd = gradient_descent(model, local_ids, n_total, num_iter, obj0 if obj0 is not None else 0.0, step, comm,
-                              placement, faithful)
+                              placement, faithful, backend=backend)
         if logistic and obj0 is None:
             obj0 = float(gd.obj[-1])  # GD_DGD_LAG_logistic.m:131-133
             gd.loss = np.abs(gd.obj - obj0)
@@ -356,17 +426,18 @@ def gd_dgd_lag(model, local_ids, n_total, num_iter, obj0: Optional[float], comm=
     out["obj0"] = obj0
     tol_ = accuracy if logistic else None
     if "DGD" in which:
-        out["DGD"] = decentralized_gd(model, local_ids, n_total, num_iter, obj0, step, comm, placement, faithful)
+        out["DGD"] = decentralized_gd(model, local_ids, n_total, num_iter, obj0, step, comm, placement, faithful,
+                                       backend=backend)
     if "LAG-PS" in which:
         out["LAG-PS"] = lag(model, local_ids, n_total, num_iter, obj0, step, hmax_full, "PS", comm, placement,
-                            faithful, tol_)
+                            faithful, tol_, backend=backend)
     if "LAG-WK" in which:
         out["LAG-WK"] = lag(model, local_ids, n_total, num_iter, obj0, step, hmax_full, "WK", comm, placement,
-                            faithful, tol_)
+                            faithful, tol_, backend=backend)
     if "cIAG" in which:
         out["cIAG"] = iag(model, local_ids, n_total, num_iter, obj0, step, "cyclic", None, seed, comm, placement,
-                          faithful, tol_)
+                          faithful, tol_, backend=backend)
     if "R-IAG" in which:
         out["R-IAG"] = iag(model, local_ids, n_total, num_iter, obj0, step, "random", hmax_full, seed, comm,
-                           placement, faithful, tol_)
+                           placement, faithful, tol_, backend=backend)
     return out

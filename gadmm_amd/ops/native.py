@@ -62,6 +62,26 @@ class EngineDesc(ctypes.Structure):
                 ("stream", c_void_p), ("nranks", c_int)]
 
 
+class FoCtl(ctypes.Structure):
+    _fields_ = [("monitored", c_int), ("stop_iter", c_int), ("status", c_int), ("iters", c_int),
+                ("uploads", c_double), ("pad_", c_double)]
+
+
+class FoArgs(ctypes.Structure):
+    """Mirror of csrc/include/gadmm_fo.h (persistent first-order baseline engine)."""
+    _fields_ = [
+        ("alg", c_int), ("model", c_int), ("n", c_int), ("d", c_int), ("m", c_int), ("max_iter", c_int),
+        ("faithful", c_int), ("jacobi", c_int), ("has_tol", c_int), ("ring", c_int),
+        ("epoch", ctypes.c_uint), ("pad_", c_int),
+        ("step", c_double), ("lam", c_double), ("obj0", c_double), ("tol", c_double), ("thrd", c_double),
+        ("timeout_ticks", c_longlong),
+        ("A", c_void_p), ("b", c_void_p), ("yy", c_void_p), ("X", c_void_p), ("Y", c_void_p),
+        ("hsq", c_void_p), ("sched", c_void_p), ("tab", c_void_p), ("part", c_void_p),
+        ("obj_trace", c_void_p), ("cnt_trace", c_void_p), ("time_trace", c_void_p), ("theta_out", c_void_p),
+        ("ctl", c_void_p),
+    ]
+
+
 class RunStats(ctypes.Structure):
     _fields_ = [("iters", c_int), ("done", c_int), ("iterations_launched", c_int), ("replays", c_int),
                 ("wall_ms", c_double), ("p2p_bytes", c_longlong), ("p2p_msgs", c_longlong),
@@ -118,6 +138,9 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_xgmi_free": (c_int, [c_void_p]),
         "gadmm_device_can_access_peer": (c_int, [c_int, c_int]),
         "gadmm_chain_persistent_launch": (c_int, [ctypes.POINTER(PersistArgs), c_void_p]),
+        "gadmm_fo_lds": (c_long, [c_int, c_int, c_int]),
+        "gadmm_fo_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
+        "gadmm_fo_launch": (c_int, [ctypes.POINTER(FoArgs), c_void_p]),
         "gadmm_rccl_unique_id": (c_int, [ctypes.c_char_p]),
         "gadmm_rccl_version": (c_int, []),
         "gadmm_rccl_init": (c_void_p, [ctypes.c_char_p, c_int, c_int, c_int]),

@@ -155,6 +155,53 @@ def test_baselines_run_on_device(lin24, lin_obj0):
     assert dual_averaging(m, list(range(24)), 24, c["stepsize"], lin_obj0, 1e-4, 50).iters == 50
 
 
+@pytest.mark.parametrize("kind", ["linear", "logistic"])
+def test_first_order_engine_matches_torch(kind, lin24, log24, lin_obj0, log_obj0):
+    """Persistent first-order kernel (one launch per run) vs the torch implementations on the same
+    device: objective traces, LAG upload counts, dual averaging (Gauss-Seidel and Jacobi)."""
+    from gadmm_amd.models import LinearRegression, LogisticRegression
+    from gadmm_amd.algorithms import gd_dgd_lag, dual_averaging, global_constants
+
+    ds, obj0 = (lin24, lin_obj0) if kind == "linear" else (log24, log_obj0)
+    m = (LinearRegression if kind == "linear" else LogisticRegression)(ds.X.to(DEV), ds.y.to(DEV),
+                                                                      **({} if kind == "linear" else {"lam": 1e-5}))
+    ids = list(range(24))
+    iters = 1500
+    nat = gd_dgd_lag(m, ids, 24, iters, obj0 if kind == "linear" else None, accuracy=1e-4, backend="native")
+    ref = gd_dgd_lag(m, ids, 24, iters, obj0 if kind == "linear" else None, accuracy=1e-4, backend="torch")
+    for k in ("GD", "DGD", "LAG-PS", "LAG-WK", "cIAG", "R-IAG"):
+        assert nat[k].extra.get("engine") == "native-persistent", k
+        assert len(nat[k].obj) == len(ref[k].obj), k
+        assert np.allclose(nat[k].obj, ref[k].obj, rtol=1e-9, atol=1e-12), k
+        assert np.array_equal(nat[k].comm_units, ref[k].comm_units), k
+    for k in ("LAG-PS", "LAG-WK"):
+        assert nat[k].extra["uploads"] == ref[k].extra["uploads"], k
+    step = global_constants(m)["stepsize"]
+    for jac in (False, True):
+        a = dual_averaging(m, ids, 24, step, obj0, 1e-4, 800, jacobi=jac, backend="native")
+        b = dual_averaging(m, ids, 24, step, obj0, 1e-4, 800, jacobi=jac, backend="torch")
+        assert a.extra["engine"] == "native-persistent"
+        assert len(a.obj) == len(b.obj) and np.allclose(a.obj, b.obj, rtol=1e-9, atol=1e-12), jac
+
+
+def test_first_order_engine_golden(lin24, lin_obj0):
+    """BASELINE.md golden numbers at the reference budget (60,000 iterations), on the native engine:
+    GD 53,891; LAG-PS 52,890 (342,113 uploads); LAG-WK 44,368 (58,186 uploads)."""
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import gradient_descent, lag, global_constants
+
+    m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
+    s = global_constants(m)["stepsize"]
+    ids = list(range(24))
+    gd = gradient_descent(m, ids, 24, 60000, lin_obj0, s, backend="native")
+    assert gd.first_below(1e-4) == 53891
+    ps = lag(m, ids, 24, 60000, lin_obj0, s, m.hmax(), "PS", backend="native")
+    assert ps.first_below(1e-4) == 52890 and ps.extra["uploads"] == 342113
+    wk = lag(m, ids, 24, 60000, lin_obj0, s, m.hmax(), "WK", backend="native")
+    assert wk.first_below(1e-4) == 44368 and wk.extra["uploads"] == 58186
+    assert gd.wall_s < 5.0  # one launch, microseconds per iteration
+
+
 def test_bench_json_contract():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "3", "--warmup", "1"],

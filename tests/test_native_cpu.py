@@ -31,6 +31,15 @@ def test_abi_layout_matches_ctypes():
     assert got == exp
 
 
+def test_fo_abi_layout_matches_ctypes():
+    lib = native.require()
+    buf = (ctypes.c_longlong * 16)()
+    k = lib.gadmm_fo_abi_layout(buf, 16)
+    exp = [ctypes.sizeof(native.FoCtl), ctypes.sizeof(native.FoArgs), native.FoArgs.step.offset,
+           native.FoArgs.timeout_ticks.offset, native.FoArgs.A.offset, native.FoArgs.ctl.offset]
+    assert list(buf[:k]) == exp
+
+
 def test_code_objects_target_gfx950():
     import subprocess
     lib = native.library_path()
