@@ -46,9 +46,10 @@ __device__ __forceinline__ bool should_stop(int s, int it) { return s < 0 || (s 
 // LDS layout (doubles) shared by host sizing (gadmm_fo_lds) and the kernel.
 struct FoLds {
   int mat, xs, aux, red, wred, dl, total;
-  __host__ __device__ FoLds(int model, int d, int m, int nc) {
+  __host__ __device__ FoLds(int model, int d, int m, int nc, int mc) {
     mat = 0;
-    const int msz = model == FO_LINEAR ? d * d : m * d + 2 * m;  // X | y | s
+    // linear: A | logistic: X (m x d) | X^T (d x m, when mc > 0) | y | s
+    const int msz = model == FO_LINEAR ? d * d : m * d * (mc > 0 ? 2 : 1) + 2 * m;
     xs = (msz + 1) & ~1;
     aux = xs + 64 * nc;
     red = aux + 64 * nc;
@@ -60,7 +61,7 @@ struct FoLds {
 
 // f_n and grad f_n at the point held in LDS `xs` (and in registers `th`, lane element i = lane + 64c,
 // identical in every wave). Results are identical in every wave. Contains __syncthreads.
-template <int NC>
+template <int NC, int MC>
 __device__ __forceinline__ double local_eval(const FoArgs& a, double* lds, const FoLds& L, const double (&th)[NC],
                                              const double (&bb)[NC], double half_yy, double (&g)[NC]) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -79,13 +80,40 @@ __device__ __forceinline__ double local_eval(const FoArgs& a, double* lds, const
     }
     return wave_sum_f64(p) + half_yy;
   }
-  // logistic: z_j = x_j . theta (wave per row), s_j = y_j / (1 + exp(y_j z_j)), softplus(-y_j z_j)
+  // logistic: z = X theta, s_j = y_j / (1 + exp(y_j z_j)), f = sum softplus(-y_j z_j), g = -X^T s
   const int m = a.m;
   const double* X = lds + L.mat;
-  const double* Yl = X + (long)m * d;
+  const double* Yl = X + (long)m * d * (MC > 0 ? 2 : 1);
   double* sv = const_cast<double*>(Yl) + m;
+  if constexpr (MC > 0) {
+    // z from the transposed copy: lanes own rows j, every wave holds z; no serial wave reductions
+    double z[MC];
+    gemv_t_lds<MC>(X + (long)m * d, lds + L.xs, z, red, d, m);
+    double sp = 0.0;
+#pragma unroll
+    for (int c = 0; c < MC; ++c) {
+      const int j = lane + 64 * c;
+      if (j < m) {
+        const double yj = Yl[j];
+        sp += softplus_f64(-yj * z[c]);
+        if (wv == 0) sv[j] = yj / (1.0 + exp(yj * z[c]));
+      }
+    }
+    sp = wave_sum_f64(sp);
+    __syncthreads();
+    double Xs[NC];
+    gemv_t_lds<NC>(X, sv, Xs, red, m, d);
+    double q = 0.0;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int i = lane + 64 * c;
+      g[c] = i < d ? -Xs[c] + a.lam * th[c] : 0.0;
+      if (i < d) q += th[c] * th[c];
+    }
+    return 0.5 * a.lam * wave_sum_f64(q) + sp;
+  }
   double sp = 0.0;
-  for (int j = wv; j < m; j += NWV) {
+  for (int j = wv; j < m; j += NWV) {  // m > 128: one wave per row
     double p = 0.0;
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -151,14 +179,14 @@ __device__ void fo_abort(FoCtl* ctl) {
 
 }  // namespace
 
-template <int NC>
+template <int NC, int MC>
 __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int flag_lds;
   const int n = a.n, d = a.d;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
-  const FoLds L(a.model, d, a.m, NC);
+  const FoLds L(a.model, d, a.m, NC, MC);
   const __amdgpu_buffer_rsrc_t rtab = rsrc_of(a.tab);
   const __amdgpu_buffer_rsrc_t rpart = rsrc_of(a.part);
   FoCtl* ctl = a.ctl;
@@ -234,7 +262,13 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
     const int m = a.m;
     const double* Xg = a.X + (long)w * m * d;
     for (int e = threadIdx.x; e < m * d; e += NT) lds[L.mat + e] = Xg[e];
-    for (int e = threadIdx.x; e < m; e += NT) lds[L.mat + m * d + e] = a.Y[(long)w * m + e];
+    const int yoff = m * d * (MC > 0 ? 2 : 1);
+    for (int e = threadIdx.x; e < m; e += NT) lds[L.mat + yoff + e] = a.Y[(long)w * m + e];
+    if (MC > 0)
+      for (int e = threadIdx.x; e < m * d; e += NT) {  // X^T[i][j] = X[j][i]
+        const int i = e / m, j = e % m;
+        lds[L.mat + m * d + e] = Xg[(long)j * d + i];
+      }
   }
   if (threadIdx.x < 16) dl[threadIdx.x] = 0.0;
   double bb[NC], th[NC], G[NC], aux[NC], g[NC];
@@ -255,7 +289,7 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
   const double hsq = a.alg == FO_LAG_PS ? a.hsq[w] : 0.0;
   __syncthreads();
   double f = 0.0;
-  if (a.alg == FO_DUALAVG) f = local_eval<NC>(a, lds, L, th, bb, half_yy, g);  // grad at theta^0 = 0
+  if (a.alg == FO_DUALAVG) f = local_eval<NC, MC>(a, lds, L, th, bb, half_yy, g);  // grad at theta^0 = 0
 
   int mon_seen = 0;
   for (int it = 1; it <= a.max_iter; ++it) {
@@ -268,7 +302,7 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
     double cnt = 0.0;
     double pub[NC];
     if (a.alg != FO_DUALAVG) {
-      f = local_eval<NC>(a, lds, L, th, bb, half_yy, g);
+      f = local_eval<NC, MC>(a, lds, L, th, bb, half_yy, g);
       if (a.alg == FO_GD) {
         if (it == 1 && a.faithful) {  // linear: ones; logistic: worker 1's gradient (GD_DGD_LAG_logistic.m:97)
 #pragma unroll
@@ -361,7 +395,7 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
         const int i = lane + 64 * c;
         th[c] = i < d ? xs[i] : 0.0;
       }
-      f = local_eval<NC>(a, lds, L, th, bb, half_yy, g);
+      f = local_eval<NC, MC>(a, lds, L, th, bb, half_yy, g);
     }
 
     // ---- publish the upload row (replicated / DGD) and (f_n, count) to the monitor
@@ -489,9 +523,11 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
 
 extern "C" {
 
+static int fo_mc(int model, int m) { return model == FO_LINEAR ? 0 : (m <= 64 ? 1 : (m <= 128 ? 2 : 0)); }
+
 long gadmm_fo_lds(int model, int d, int m) {
   const int nc = d <= 64 ? 1 : 2;
-  const FoLds L(model, d, m, nc);
+  const FoLds L(model, d, m, nc, fo_mc(model, m));
   return (long)L.total * 8;
 }
 
@@ -515,14 +551,17 @@ int gadmm_fo_launch(const FoArgs* a, void* stream) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return -4;
   int per_cu = 0;
-  const void* fn = a->d <= 64 ? (const void*)fo_persistent_kernel<1> : (const void*)fo_persistent_kernel<2>;
+  const int mc = fo_mc(a->model, a->m);
+  const void* fns[2][3] = {{(const void*)fo_persistent_kernel<1, 0>, (const void*)fo_persistent_kernel<1, 1>,
+                            (const void*)fo_persistent_kernel<1, 2>},
+                           {(const void*)fo_persistent_kernel<2, 0>, (const void*)fo_persistent_kernel<2, 1>,
+                            (const void*)fo_persistent_kernel<2, 2>}};
+  const int nci = a->d <= 64 ? 0 : 1;
+  const void* fn = fns[nci][mc];
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, (size_t)lds) != hipSuccess) return -4;
   if ((long)per_cu * prop.multiProcessorCount < a->n + 1) return -5;  // persistent: all must be resident
-  hipStream_t st = (hipStream_t)stream;
-  if (a->d <= 64)
-    hipLaunchKernelGGL(fo_persistent_kernel<1>, dim3(a->n + 1), dim3(NT), (size_t)lds, st, *a);
-  else
-    hipLaunchKernelGGL(fo_persistent_kernel<2>, dim3(a->n + 1), dim3(NT), (size_t)lds, st, *a);
+  void* args[] = {const_cast<FoArgs*>(a)};
+  if (hipLaunchKernel(fn, dim3(a->n + 1), dim3(NT), args, (size_t)lds, (hipStream_t)stream) != hipSuccess) return -1;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
