@@ -124,4 +124,7 @@ struct PersistArgs {
   unsigned long long* const* dec_push;  // [nranks] every rank's decision ring (monitor only)
   double* trace;            // [max_iter] (monitor rank)
   ChainCtl* ctl;
+  long long* timeline;      // optional [n_local + 1][timeline_iters][8] s_memrealtime stamps (debug profiling)
+  int timeline_iters;
+  int pad2_;
 };

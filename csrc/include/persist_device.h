@@ -28,6 +28,16 @@ __device__ __forceinline__ bool load_granule(__amdgpu_buffer_rsrc_t rs, int byte
 }
 
 template <bool SYS>
+__device__ __forceinline__ u32x4 load_raw(__amdgpu_buffer_rsrc_t rs, int byte_off) {
+  return SYS ? __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 17)
+             : __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 16);
+}
+__device__ __forceinline__ bool granule_ok(const u32x4& g, unsigned tag) { return g.x == tag && g.z == tag; }
+__device__ __forceinline__ double granule_val(const u32x4& g) {
+  return __longlong_as_double((long long)(((unsigned long long)g.w << 32) | g.y));
+}
+
+template <bool SYS>
 __device__ __forceinline__ void store_dec(unsigned long long* p, unsigned long long v) {
   if (SYS) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   else __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -57,6 +67,37 @@ __device__ __forceinline__ bool wait_row(__amdgpu_buffer_rsrc_t rs, int row, int
     }
     if (__all(ok)) return true;
     if (now_ticks() > deadline) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// Poll up to two rows (row < 0: skipped) in ONE loop, so a worker waiting on both chain neighbours
+// pays one round trip, not two. Rows may carry different tags. `stopw` (nullable) is a run-wide stop
+// word: -1 abort, k > 0 stopped after iteration k (the wait is abandoned once it > k).
+// Returns 1 ok, 0 deadline passed, -1 stopped. Wave-uniform.
+template <int NC, bool SYS>
+__device__ __forceinline__ int wait_pair(__amdgpu_buffer_rsrc_t rs, int d, int ra, unsigned ta, double (&va)[NC],
+                                         int rb, unsigned tb, double (&vb)[NC], unsigned long long deadline,
+                                         const int* stopw = nullptr, int it = 0) {
+  const int lane = threadIdx.x & 63;
+  for (int spin = 0;; ++spin) {
+    bool ok = true;
+#pragma unroll
+    for (int c = 0; c < NC; ++c) {
+      const int i = lane + 64 * c;
+      if (i < d) {
+        if (ra >= 0) ok &= load_granule<SYS>(rs, (ra * d + i) * 16, ta, &va[c]);
+        if (rb >= 0) ok &= load_granule<SYS>(rs, (rb * d + i) * 16, tb, &vb[c]);
+      }
+    }
+    if (__all(ok)) return 1;
+    if ((spin & 7) == 7) {
+      if (stopw) {
+        const int s = __hip_atomic_load(stopw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (s < 0 || (s > 0 && it > s)) return -1;
+      }
+      if (now_ticks() > deadline) return 0;
+    }
     __builtin_amdgcn_s_sleep(1);
   }
 }

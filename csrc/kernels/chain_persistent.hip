@@ -27,17 +27,42 @@
 #include "gadmm_common.h"
 #include "gadmm_chain.h"
 #include "persist_device.h"
+#include <stdlib.h>
 #include <string.h>
 
 namespace {
 
 constexpr int NT = 256;
 constexpr int NW = 4;
+constexpr int DREG = 64;  // register-resident variant: d <= 64, one wave per worker
+
+// y_i = sum_j M[i][j] x_j with lane i holding row i of M in registers and x broadcast from LDS
+// (zero-padded to DREG); four independent accumulators over j = k mod 4, combined ((a0 + a1) + a2) + a3:
+// exactly the summation order of symv_lds / symv_cols (wave k of 4 sums rows j = k mod 4, partials
+// added in wave order), so every engine produces bit-identical iterates (M is exactly symmetric).
+__device__ __forceinline__ double reg_gemv(const double (&Mr)[DREG], const double* xv) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll
+  for (int j = 0; j < DREG; j += 4) {
+    const double2 x01 = *reinterpret_cast<const double2*>(xv + j);
+    const double2 x23 = *reinterpret_cast<const double2*>(xv + j + 2);
+    a0 = fma(Mr[j], x01.x, a0);
+    a1 = fma(Mr[j + 1], x01.y, a1);
+    a2 = fma(Mr[j + 2], x23.x, a2);
+    a3 = fma(Mr[j + 3], x23.y, a3);
+  }
+  return ((a0 + a1) + a2) + a3;
+}
 
 }  // namespace
 
-template <int NC, bool SYS>
-__global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
+// REG = true: d <= 64, ONE wave per worker that keeps its rows of (A + deg rho I)^{-1} and A in
+// VGPRs (lane i holds row i): a phase's GEMV is 64 FMAs per lane with x broadcast from LDS, and no
+// cross-wave reduction or barrier sits on the critical path (tools/persist_timeline.py measured
+// ~0.9 us of LDS-GEMV + barriers per phase in the 4-wave LDS variant at d = 50).
+// REG = false: 4 waves, matrices in LDS (64 < d <= 128).
+template <int NC, bool SYS, bool REG>
+__global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(PersistArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int abort_lds;
   __shared__ int stop_lds;
@@ -89,6 +114,8 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
         const unsigned long long dv = ((unsigned long long)tag << 32) | code;
         for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
         if (code) stop_lds = 1;
+        const int k = it - a.start_iter;
+        if (a.timeline && k < a.timeline_iters) a.timeline[((long)blockIdx.x * a.timeline_iters + k) * 8] = (long long)now_ticks();
       }
       __syncthreads();
       if (stop_lds) return;
@@ -108,16 +135,26 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
   const __amdgpu_buffer_rsrc_t rp0 = rsrc_of(p0 ? (const void*)p0 : (const void*)a.thg);
   const __amdgpu_buffer_rsrc_t rp1 = rsrc_of(p1 ? (const void*)p1 : (const void*)a.thg);
 
+  const long msz = REG ? 0 : (long)d * d;
   double* Ml = lds;                                            // d*d
-  double* Al = lds + (long)d * d;                              // d*d (obj_mode 0)
-  double* xv = lds + (long)(a.obj_mode == 0 ? 2 : 1) * d * d;  // [64*NC] rhs / theta staging
+  double* Al = lds + msz;                                      // d*d (obj_mode 0)
+  double* xv = lds + (a.obj_mode == 0 ? 2 : 1) * msz;          // [64*NC] rhs / theta staging
   double* red = xv + 64 * NC;                                  // [NW*NC*64]
 
   const double* Mg = a.Minv + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)d * d;
-  for (int e = threadIdx.x; e < d * d; e += NT) Ml[e] = Mg[e];
-  if (a.obj_mode == 0) {
-    const double* Ag = a.A + (long)li * d * d;
-    for (int e = threadIdx.x; e < d * d; e += NT) Al[e] = Ag[e];
+  const double* Ag = a.A + (long)li * d * d;
+  double Mr[REG ? DREG : 1], Ar[REG ? DREG : 1];
+  if constexpr (REG) {
+#pragma unroll
+    for (int j = 0; j < DREG; ++j) {
+      Mr[j] = (lane < d && j < d) ? Mg[lane * d + j] : 0.0;
+      Ar[j] = (a.obj_mode == 0 && lane < d && j < d) ? Ag[lane * d + j] : 0.0;
+    }
+    xv[lane] = 0.0;  // zero padding beyond d stays untouched
+  } else {
+    for (int e = threadIdx.x; e < d * d; e += NT) Ml[e] = Mg[e];
+    if (a.obj_mode == 0)
+      for (int e = threadIdx.x; e < d * d; e += NT) Al[e] = Ag[e];
   }
   // worker state, meaningful in wave 0 (lane owns elements i = lane + 64c)
   double th[NC], mu[NC], bb[NC], tl[NC], tr[NC];
@@ -138,73 +175,92 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
 
   int it = a.start_iter;
   for (;; ++it) {
-    // -- stop rule: decision of iteration it - lag (all workers leave at the same boundary)
-    if (it - a.start_iter >= a.lag) {
-      const int j = it - a.lag;
-      if (threadIdx.x == 0) {
-        const unsigned tj = make_tag(a.epoch, j);
-        unsigned long long v;
-        for (;;) {
-          v = load_dec<SYS>(&a.decg[j % a.ring]);
-          if ((unsigned)(v >> 32) == tj) break;
-          if (now_ticks() > deadline) {
-            v = 4;
-            abort_lds = 1;
-            break;
+    if (it > a.max_iter + a.lag) break;
+    const long long t_start = a.timeline ? (long long)now_ticks() : 0;
+    long long t_ready = 0, t_pub = 0, t_bar = 0, t_gemv = 0;
+    // -- stop rule: decision of iteration it - lag (all workers leave at the same boundary). Its
+    // load is issued here and resolved after the neighbour wait, so its latency overlaps the wait;
+    // nothing is committed before the barrier that publishes the decision.
+    const bool check = it - a.start_iter >= a.lag;
+    const int jdec = it - a.lag;
+
+    // -- neighbours' theta, the stop decision, and the rhs (wave 0). The decision of iteration
+    // it - lag is polled in the same loop as the neighbours' granules (one round trip for both);
+    // a stop decision abandons the wait, since a neighbour that already saw it publishes no more.
+    // Nothing is committed before the barrier that publishes the outcome.
+    double mun[NC];
+    if (w0) {
+      const bool need_nb = head ? it > a.start_iter : true;
+      const unsigned tnb = make_tag(a.epoch, head ? it - 1 : it);
+      const int ra = need_nb ? left : -1, rb = need_nb ? right : -1;
+      const unsigned tj = make_tag(a.epoch, jdec);
+      bool decided = !check;
+      unsigned long long dv = 0;
+      int outcome = 0;  // 1 go, 2 stop, 3 timeout
+      for (int spin = 0;; ++spin) {
+        bool nb = true;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          const int i = lane + 64 * c;
+          if (i < d) {
+            if (ra >= 0) nb &= load_granule<SYS>(rth, (ra * d + i) * 16, tnb, &tl[c]);
+            if (rb >= 0) nb &= load_granule<SYS>(rth, (rb * d + i) * 16, tnb, &tr[c]);
           }
-          __builtin_amdgcn_s_sleep(2);
         }
-        const unsigned code = (unsigned)(v & 0xffffffffu);
-        stop_lds = code != 0u;
-        if (code) {
-          stop_code = (int)code;
-          stop_iter = j;
+        if (!decided) {
+          dv = __shfl(load_dec<SYS>(&a.decg[jdec % a.ring]), 0, 64);
+          decided = (unsigned)(dv >> 32) == tj;
+        }
+        if (decided && (unsigned)(dv & 0xffffffffu) != 0u) { outcome = 2; break; }
+        if (decided && __all(nb)) { outcome = 1; break; }
+        if ((spin & 7) == 7 && now_ticks() > deadline) { outcome = 3; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (lane == 0) {
+        if (a.timeline) t_ready = (long long)now_ticks();
+        if (outcome == 3) abort_lds = 1;
+        if (outcome == 2) {
+          stop_lds = 1;
+          stop_code = (int)(unsigned)(dv & 0xffffffffu);
+          stop_iter = jdec;
         }
       }
-      __syncthreads();
-      if (stop_lds) break;
-    }
-    if (it > a.max_iter + a.lag) break;
-
-    // -- neighbours' theta and the rhs (wave 0)
-    if (w0) {
-      bool ok = true;
       if (head) {
-        if (it > a.start_iter) {
-          const unsigned tp = make_tag(a.epoch, it - 1);
-          if (left >= 0) ok &= wait_row<NC, SYS>(rth, left, d, tp, tl, deadline);
-          if (ok && right >= 0) ok &= wait_row<NC, SYS>(rth, right, d, tp, tr, deadline);
-        }
-        if (pending) {  // lazy end-of-iteration dual (reference order: -rho(th_l - th) then +rho(th - th_r))
 #pragma unroll
-          for (int c = 0; c < NC; ++c) {
-            double m = mu[c];
+        for (int c = 0; c < NC; ++c) {  // lazy end-of-iteration dual (reference order: -rho(th_l - th) then +rho(th - th_r))
+          double m = mu[c];
+          if (pending) {
             if (left >= 0) m = m - rho * (tl[c] - th[c]);
             if (right >= 0) m = m + rho * (th[c] - tr[c]);
-            mu[c] = m;
           }
+          mun[c] = m;
         }
       } else {
-        const unsigned tc = make_tag(a.epoch, it);
-        if (left >= 0) ok &= wait_row<NC, SYS>(rth, left, d, tc, tl, deadline);
-        if (ok && right >= 0) ok &= wait_row<NC, SYS>(rth, right, d, tc, tr, deadline);
+#pragma unroll
+        for (int c = 0; c < NC; ++c) mun[c] = mu[c];
       }
-      if (!ok && lane == 0) abort_lds = 1;
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         const int i = lane + 64 * c;
-        double r = bb[c] - mu[c];
+        double r = bb[c] - mun[c];
         if (left >= 0) r = r + rho * tl[c];
         if (right >= 0) r = r + rho * tr[c];
         if (i < d) xv[i] = r;
       }
     }
     __syncthreads();
-    if (abort_lds) break;
+    if (abort_lds || stop_lds) break;
+    if (a.timeline) t_bar = (long long)now_ticks();
+    if (w0) {
+#pragma unroll
+      for (int c = 0; c < NC; ++c) mu[c] = mun[c];
+    }
 
     // -- solve theta = (A + deg rho I)^{-1} r
     double tn[NC];
-    symv_lds<NC>(Ml, xv, tn, red, d);
+    if constexpr (REG) tn[0] = reg_gemv(Mr, xv);
+    else symv_lds<NC>(Ml, xv, tn, red, d);
+    if (a.timeline) t_gemv = (long long)now_ticks();
     double part = 0.0;
     if (w0) {
       const unsigned tag = make_tag(a.epoch, it);
@@ -217,6 +273,7 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
           if (p1) store_granule<SYS>(rp1, (w * d + i) * 16, tag, tn[c]);
         }
       }
+      if (a.timeline) t_pub = (long long)now_ticks();
       if (!head) {  // tails: both neighbours are this iteration's heads -> dual update now
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
@@ -247,7 +304,8 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
       }
       __syncthreads();
       double q[NC];
-      symv_lds<NC>(Al, xv, q, red, d);
+      if constexpr (REG) q[0] = reg_gemv(Ar, xv);
+      else symv_lds<NC>(Al, xv, q, red, d);
       if (w0) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
@@ -261,6 +319,16 @@ __global__ void __launch_bounds__(NT) chain_persistent_kernel(PersistArgs a) {
       if (lane == 0) store_granule<SYS>(rob, ((it % a.ring) * n + w) * 16, make_tag(a.epoch, it), f);
 #pragma unroll
       for (int c = 0; c < NC; ++c) th[c] = tn[c];
+      const int k = it - a.start_iter;
+      if (lane == 0 && a.timeline && k < a.timeline_iters) {
+        long long* tl = a.timeline + ((long)blockIdx.x * a.timeline_iters + k) * 8;
+        tl[0] = t_start;
+        tl[1] = t_ready;
+        tl[2] = t_pub;
+        tl[3] = (long long)now_ticks();
+        tl[4] = t_bar;
+        tl[5] = t_gemv;
+      }
     }
     __syncthreads();
   }
@@ -323,20 +391,25 @@ int gadmm_chain_persistent_launch(const PersistArgs* args, hipStream_t st) {
   }
   const long monitor_lds = (long)a.n * 8;
   const size_t shm = (size_t)(lds > monitor_lds ? lds : monitor_lds);
-#define GADMM_P_LAUNCH(NCv, SYSv)                                                                  \
+#define GADMM_P_LAUNCH(NCv, SYSv, REGv)                                                            \
   do {                                                                                             \
-    auto kfn = chain_persistent_kernel<NCv, SYSv>;                                                 \
-    if (shm > 65536)                                                                               \
+    auto kfn = chain_persistent_kernel<NCv, SYSv, REGv>;                                           \
+    const size_t sh = REGv ? (size_t)(monitor_lds > 1024 ? monitor_lds : 1024) : shm;             \
+    if (sh > 65536)                                                                                \
       GADMM_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                      (int)shm));                                                  \
-    hipLaunchKernelGGL(kfn, dim3(blocks), dim3(NT), shm, st, a);                                   \
+                                      (int)sh));                                                   \
+    hipLaunchKernelGGL(kfn, dim3(blocks), dim3(REGv ? 64 : NT), sh, st, a);                        \
   } while (0)
-  if (a.d <= 64) {
-    if (a.sys_scope) GADMM_P_LAUNCH(1, true);
-    else GADMM_P_LAUNCH(1, false);
+  static const bool force_lds = getenv("GADMM_PERSIST_LDS") != nullptr;  // A/B switch
+  if (a.d <= DREG && !force_lds) {
+    if (a.sys_scope) GADMM_P_LAUNCH(1, true, true);
+    else GADMM_P_LAUNCH(1, false, true);
+  } else if (a.d <= 64) {
+    if (a.sys_scope) GADMM_P_LAUNCH(1, true, false);
+    else GADMM_P_LAUNCH(1, false, false);
   } else {
-    if (a.sys_scope) GADMM_P_LAUNCH(2, true);
-    else GADMM_P_LAUNCH(2, false);
+    if (a.sys_scope) GADMM_P_LAUNCH(2, true, false);
+    else GADMM_P_LAUNCH(2, false, false);
   }
 #undef GADMM_P_LAUNCH
   GADMM_CHECK(hipGetLastError());

@@ -356,13 +356,11 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
       if (w0) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) zl[0][c] = zr[0][c] = 0.0;
-        if (has_l && (!a.jacobi || it > 1)) {
-          const int lit = a.jacobi ? it - 1 : it;
-          ok = wait_rows<NC, 1>(rtab, ((lit & 1) * n) + w - 1, 1, 1, d, make_tag(a.epoch, lit), zl, deadline, ctl, it);
-        }
-        if (ok == 1 && has_r && it > 1)
-          ok = wait_rows<NC, 1>(rtab, (((it - 1) & 1) * n) + w + 1, 1, 1, d, make_tag(a.epoch, it - 1), zr, deadline,
-                                ctl, it);
+        const int lit = a.jacobi ? it - 1 : it;
+        const int rl = (has_l && (!a.jacobi || it > 1)) ? ((lit & 1) * n) + w - 1 : -1;
+        const int rr = (has_r && it > 1) ? (((it - 1) & 1) * n) + w + 1 : -1;
+        ok = wait_pair<NC, false>(rtab, d, rl, make_tag(a.epoch, lit), zl[0], rr, make_tag(a.epoch, it - 1), zr[0],
+                                  deadline, &ctl->stop_iter, it);
         if (lane == 0) flag_lds = ok;
       }
       __syncthreads();
@@ -469,8 +467,8 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
       double gl[1][NC], gr[1][NC];
 #pragma unroll
       for (int c = 0; c < NC; ++c) gl[0][c] = gr[0][c] = 0.0;
-      if (w > 0) ok = wait_rows<NC, 1>(rtab, slot * n + w - 1, 1, 1, d, tag, gl, deadline, ctl, it);
-      if (ok == 1 && w < n - 1) ok = wait_rows<NC, 1>(rtab, slot * n + w + 1, 1, 1, d, tag, gr, deadline, ctl, it);
+      ok = wait_pair<NC, false>(rtab, d, w > 0 ? slot * n + w - 1 : -1, tag, gl[0], w < n - 1 ? slot * n + w + 1 : -1, tag,
+                                gr[0], deadline, &ctl->stop_iter, it);
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         if (n == 1) S[c] = G[c];

@@ -273,9 +273,13 @@ class NativeChainEngine:
         return 0 if int(self.lib.gadmm_chain_persistent_lds(self.d, 0)) > 0 else 1
 
     def run_persistent(self, lag: int = 4, timeout_s: float = 20.0, start_iter: int = 1,
-                       pending_in: int = 0, fabric=None) -> EngineRun:
+                       pending_in: int = 0, fabric=None, timeline_iters: int = 0) -> EngineRun:
         """Whole solve in one launch per GPU. State must be reset (``reset()``) or resumed by the
-        caller. ``fabric``: an ``XgmiFabric`` for the multi-GPU device-initiated transport."""
+        caller. ``fabric``: an ``XgmiFabric`` for the multi-GPU device-initiated transport.
+        ``timeline_iters > 0`` records s_memrealtime stamps (10 ns) of the first iterations into
+        ``self.last_timeline``: (workgroup, iteration, [start, ready, published, end, after the
+        barrier, after the solve GEMV, -, -]); the last
+        workgroup row is the monitor (column 0 = decision posted)."""
         if not self.persistent_eligible(fabric):
             raise RuntimeError("persistent kernel not eligible for this engine/config")
         ring = lag + 4
@@ -335,6 +339,10 @@ class NativeChainEngine:
         pa.push = push.data_ptr() if push is not None else None
         pa.dec_push = dec_push.data_ptr()
         pa.trace, pa.ctl = self.trace.data_ptr(), self.ctl.data_ptr()
+        tl = None
+        if timeline_iters > 0:
+            tl = torch.zeros((len(slots) + 1, int(timeline_iters), 8), dtype=torch.int64, device=dev)
+            pa.timeline, pa.timeline_iters = tl.data_ptr(), int(timeline_iters)
         import time as _time
         with torch.cuda.stream(self.stream):
             t0 = _time.perf_counter()
@@ -342,6 +350,8 @@ class NativeChainEngine:
                          "chain_persistent_launch")
             self.stream.synchronize()
             t1 = _time.perf_counter()
+        self.last_timeline = tl.cpu().numpy() if tl is not None else None
+        self.last_timeline_slots = [(s.gid, p) for s, p in zip(slots, pos)] if tl is not None else None
         c = self.ctl.cpu().tolist()
         done, conv, nxt = c[1], c[2], c[0]
         if done == 4:

@@ -98,6 +98,7 @@ class PersistArgs(ctypes.Structure):
         ("slots", c_void_p), ("pos", c_void_p), ("Minv", c_void_p), ("A", c_void_p), ("b", c_void_p),
         ("yy", c_void_p), ("theta", c_void_p), ("mu", c_void_p), ("thg", c_void_p), ("push", c_void_p),
         ("objg", c_void_p), ("decg", c_void_p), ("dec_push", c_void_p), ("trace", c_void_p), ("ctl", c_void_p),
+        ("timeline", c_void_p), ("timeline_iters", c_int), ("pad2_", c_int),
     ]
 
 
