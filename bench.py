@@ -205,6 +205,7 @@ def main():
             "p2p_messages_per_iteration": chain_message_count(path, placement),
             "us_per_iteration": round(ms * 1e3 / max(iters, 1), 3),
             "engine": "persistent" if persistent else ("graph" if eng.graph_ok() and not args.no_graph else "eager"),
+            "kernel": getattr(eng, "last_kernel", None) if persistent else None,
             "fabric": fabric_kind,
             "baseline_s": BASELINE_S,
         }

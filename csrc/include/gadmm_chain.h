@@ -126,5 +126,8 @@ struct PersistArgs {
   ChainCtl* ctl;
   long long* timeline;      // optional [n_local + 1][timeline_iters][8] s_memrealtime stamps (debug profiling)
   int timeline_iters;
-  int pad2_;
+  int blk_k;                // temporal blocking: iterations between halo exchanges (0: auto, -1: off)
+  int blk_len;              // temporal blocking: chain positions owned per workgroup (0: auto)
+  int pad3_;
+  u32x4* blk_tab;           // [2][n][2][d] (theta, mu) granules of the halo exchange
 };

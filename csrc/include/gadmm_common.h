@@ -36,6 +36,16 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
+// Workgroup barrier that orders LDS only. __syncthreads() also waits for every outstanding global
+// store (s_waitcnt vmcnt(0)) - a write-through granule store takes ~1 us to complete, which a
+// persistent kernel would then pay at every barrier. Global hand-offs in this code base are
+// data-is-flag granules (self-validating), so the workgroup barrier only has to cover LDS.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Block-level f64 sum; `scratch` must hold >= blockDim.x/64 doubles. Result valid on all threads.
 __device__ __forceinline__ double block_sum_f64(double v, double* scratch) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;

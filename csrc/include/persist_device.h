@@ -142,7 +142,7 @@ __device__ __forceinline__ void gemv_t_lds(const double* M, const double* x, dou
   }
 #pragma unroll
   for (int c = 0; c < NC; ++c) red[(w * NC + c) * 64 + lane] = acc[c];
-  __syncthreads();
+  lds_barrier();
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     double s = 0.0;
@@ -150,13 +150,35 @@ __device__ __forceinline__ void gemv_t_lds(const double* M, const double* x, dou
     for (int ww = 0; ww < NW; ++ww) s += red[(ww * NC + c) * 64 + lane];
     y[c] = s;  // every wave holds the full result for its lanes' rows
   }
-  __syncthreads();
+  lds_barrier();
 }
 
 // y = M x for symmetric M (d x d) in LDS.
 template <int NC>
 __device__ __forceinline__ void symv_lds(const double* M, const double* x, double (&y)[NC], double* red, int d) {
   gemv_t_lds<NC>(M, x, y, red, d, d);
+}
+
+constexpr int DREG = 64;  // register-resident variant: d <= 64, one wave per worker
+
+// y_i = sum_j M[i][j] x_j with lane i holding row i of M in registers and x broadcast from LDS
+// (zero-padded to DREG); four independent accumulators over j = k mod 4, combined ((a0 + a1) + a2) + a3:
+// exactly the summation order of symv_lds / symv_cols (wave k of 4 sums rows j = k mod 4, partials
+// added in wave order), so every engine produces bit-identical iterates (M is exactly symmetric).
+template <int DB>
+__device__ __forceinline__ double reg_gemv(const double (&Mr)[DB], const double* xv) {
+  static_assert(DB % 4 == 0, "row length must be a multiple of 4");
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+#pragma unroll
+  for (int j = 0; j < DB; j += 4) {
+    const double2 x01 = *reinterpret_cast<const double2*>(xv + j);
+    const double2 x23 = *reinterpret_cast<const double2*>(xv + j + 2);
+    a0 = fma(Mr[j], x01.x, a0);
+    a1 = fma(Mr[j + 1], x01.y, a1);
+    a2 = fma(Mr[j + 2], x23.x, a2);
+    a3 = fma(Mr[j + 3], x23.y, a3);
+  }
+  return ((a0 + a1) + a2) + a3;
 }
 
 }  // namespace persist

@@ -1,0 +1,398 @@
+// Temporally blocked persistent GADMM (linear, closed form, one GPU, d <= 64).
+//
+// Why: in the one-workgroup-per-worker kernel (chain_persistent.hip) an iteration is two dependent
+// cross-CU hand-offs of ~0.8 us each plus two phases of compute (profiles/r01_persistent_timeline).
+// Here a workgroup owns a contiguous chain segment of L positions and ALSO computes a halo of
+// H = 2k positions on each side, one wave per computed worker, with every worker's row of
+// (A + deg rho I)^{-1} in VGPRs. Head -> tail -> head dependencies inside the computed range are
+// LDS + workgroup-barrier hand-offs (tens of ns). Each phase invalidates one more position at each
+// edge of the computed range (a worker needs both neighbours' fresh theta), so after k iterations
+// exactly the owned segment is still exact. Then the workgroups exchange the (theta, mu) of their
+// owned workers through data-is-flag granules and refresh their halos: ONE cross-CU hand-off per k
+// iterations instead of 2k. The halo recomputation costs idle waves, not latency.
+//
+// Arithmetic is identical to the other engines (reg_gemv order == symv_lds == symv_cols, the exact
+// objective 1/2 th^T A th - b^T th + 1/2 y^T y with A from LDS in the same order, the monitor sums
+// f_n in worker order), so iterates and objective traces are bit-identical to the multi-kernel
+// and per-worker persistent paths.
+//
+// Schedule per iteration it (reference semantics, group_ADMM_closedForm.m / A4 with a static chain):
+//   [every k iterations] publish owned (theta, mu), refresh halo (theta, mu)      -- 1 hand-off
+//   [stop rule] decision of iteration it - lag (prefetched one iteration ahead)
+//   head phase: heads apply the lazy dual with the tails' theta^{it-1}, solve, write theta^it to LDS
+//   barrier
+//   tail phase: tails solve with the heads' theta^it, dual update
+//   barrier
+// Owned workers also post theta^it into a ring; OBJECTIVE workgroups (one wave per worker, A_n in
+// VGPRs) evaluate f_n(theta^it) off the critical path and feed the monitor, which sums in worker
+// order and posts the stop decision (monitor as in chain_persistent.hip). Grid: W worker
+// workgroups, Wo objective workgroups, 1 monitor.
+#include "gadmm_common.h"
+#include "gadmm_chain.h"
+#include "persist_device.h"
+#include <stdlib.h>
+
+namespace {
+
+constexpr int MAXW = 12;  // computed workers (waves) per workgroup: 3 waves per SIMD -> <= 170 VGPRs
+
+// q_i = sum_j A[j][i] th_j with A (symmetric, row-major d x d) in LDS and th broadcast from LDS;
+// the summation order of reg_gemv (accumulator j mod 4, ((a0 + a1) + a2) + a3).
+__device__ __forceinline__ double lds_gemv_cols(const double* A, int d, const double* xv, int i) {
+  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+  if (i < d) {
+    int j = 0;
+    for (; j + 3 < d; j += 4) {
+      a0 = fma(A[j * d + i], xv[j], a0);
+      a1 = fma(A[(j + 1) * d + i], xv[j + 1], a1);
+      a2 = fma(A[(j + 2) * d + i], xv[j + 2], a2);
+      a3 = fma(A[(j + 3) * d + i], xv[j + 3], a3);
+    }
+    if (j < d) a0 = fma(A[j * d + i], xv[j], a0);
+    if (j + 1 < d) a1 = fma(A[(j + 1) * d + i], xv[j + 1], a1);
+    if (j + 2 < d) a2 = fma(A[(j + 2) * d + i], xv[j + 2], a2);
+  }
+  return ((a0 + a1) + a2) + a3;
+}
+
+}  // namespace
+
+// DB: register row length (multiple of 4, >= d); 52 keeps d = 50 within the 3-waves-per-SIMD budget.
+template <int DB>
+__global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ int abort_lds, stop_lds;
+    const int d = a.d, n = a.n;
+  const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
+  const int k = a.blk_k, L = a.blk_len, H = 2 * a.blk_k;
+  const int W = (n + L - 1) / L;
+  const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
+  const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
+  const __amdgpu_buffer_rsrc_t rtab = rsrc_of(a.blk_tab);
+  if (threadIdx.x == 0) {
+    abort_lds = 0;
+    stop_lds = 0;
+  }
+  lds_barrier();
+
+  if ((int)blockIdx.x == W) {
+    // ------------------------------------------------------------- monitor (same as chain_persistent)
+    if (v != 0) return;
+    double* vals = lds;  // [n]
+    for (int it = a.start_iter;; ++it) {
+      const unsigned tag = make_tag(a.epoch, it);
+      const int slot = it % a.ring;
+      bool okall = true;
+      for (int w = lane; w < n; w += 64) {
+        double val = 0.0;
+        for (int spin = 0;; ++spin) {
+          if (load_granule<false>(rob, (slot * n + w) * 16, tag, &val)) break;
+          if ((spin & 7) == 7 && now_ticks() > deadline) {
+            okall = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        vals[w] = val;
+      }
+      const bool ok = __all(okall);
+      unsigned code = 0;
+      if (lane == 0) {
+        if (!ok) {
+          code = 4;
+        } else {
+          double s = 0.0;
+          for (int w = 0; w < n; ++w) s += vals[w];  // worker order: == the other engines
+          if (it - 1 < a.max_iter) a.trace[it - 1] = s;
+          if (!(s == s) || isinf(s)) code = 3;
+          else if (fabs(s - a.obj0) < a.tol) code = 1;
+          else if (it >= a.max_iter) code = 2;
+        }
+        store_dec<false>(a.decg + slot, ((unsigned long long)tag << 32) | code);
+        const int kk = it - a.start_iter;
+        if (a.timeline && kk < a.timeline_iters) a.timeline[((long)blockIdx.x * a.timeline_iters + kk) * 8] = (long long)now_ticks();
+      }
+      if (__shfl((int)code, 0, 64)) {
+        if (lane == 0)  // epoch-tagged stop word for the objective workgroups
+          __hip_atomic_store(&a.ctl->ticket, (a.epoch << 1) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+    }
+  }
+
+  const int Wo = (n + MAXW - 1) / MAXW;
+  const long ring_base = 2L * n * 2 * d;  // theta ring [ring][n][d] after the exchange table
+  if ((int)blockIdx.x >= W) {
+    // ----------------------------------------------------------------- objective workgroup
+    const int q = ((int)blockIdx.x - W - 1) * MAXW + v;  // chain position (block W is the monitor)
+    if (q >= n) return;
+    const PhaseSlot so = a.slots[q];
+    const bool in = lane < d;
+    double Ar[DB];
+    const double* Ag = a.A + (long)so.li * d * d;
+#pragma unroll
+    for (int j = 0; j < DB; ++j) Ar[j] = (in && j < d) ? Ag[lane * d + j] : 0.0;
+    const double bo = in ? a.b[(long)so.li * d + lane] : 0.0;
+    const double hy = 0.5 * a.yy[so.li];
+    double* xo = lds + v * 64;
+    xo[lane] = 0.0;
+    const unsigned stopw = (a.epoch << 1) | 1u;
+    for (int it = a.start_iter;; ++it) {
+      const unsigned tag = make_tag(a.epoch, it);
+      const long off = (ring_base + ((long)(it % a.ring) * n + q) * d + lane) * 16;
+      double x = 0.0;
+      for (int spin = 0;; ++spin) {
+        const bool ok = !in || load_granule<false>(rtab, (int)off, tag, &x);
+        if (__all(ok)) break;
+        if ((spin & 7) == 7) {
+          if (__hip_atomic_load(&a.ctl->ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == stopw) return;
+          if (now_ticks() > deadline) return;  // the monitor times out and reports it
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      xo[lane] = in ? x : 0.0;
+      const double qv = reg_gemv(Ar, xo);  // (A th)_i in the order of every other engine
+      const double part = in ? (0.5 * qv - bo) * x : 0.0;
+      const double f = wave_sum_f64(part) + hy;
+      if (lane == 0) store_granule<false>(rob, ((it % a.ring) * n + so.gid) * 16, tag, f);
+    }
+  }
+
+  // ---------------------------------------------------------------------- worker workgroup
+  const int g = blockIdx.x;
+  const int s0 = g * L, e0 = min(n, s0 + L) - 1;  // owned chain positions [s0, e0]
+  const int ra = max(0, s0 - H), rb = min(n - 1, e0 + H);
+  const int nv = rb - ra + 1;
+  const int p = ra + v;  // this wave's chain position
+  const bool active = v < nv;
+  const bool owned = active && p >= s0 && p <= e0;
+  const PhaseSlot sl = a.slots[active ? p : 0];  // slots are sorted by chain position
+  const int li = sl.li, w = sl.gid;
+  const bool has_l = active && sl.left >= 0, has_r = active && sl.right >= 0;
+  const bool head = (p % 2) == 0;
+  const int deg = (int)has_l + (int)has_r;
+  const double rho = a.rho;
+  const bool in = lane < d;
+
+  double* thS = lds;                       // [MAXW][64] theta of every computed worker
+  double* xs = thS + MAXW * 64;            // [MAXW][64] per-wave rhs / broadcast staging
+  double* myx = xs + v * 64;
+  // the wave's neighbours inside the computed range (outside it the halo worker is already stale)
+  const double* thL = thS + (v > 0 ? v - 1 : v) * 64;
+  const double* thR = thS + (v + 1 < nv ? v + 1 : v) * 64;
+  const bool nbl = has_l && v > 0, nbr = has_r && v + 1 < nv;
+
+  double Mr[DB];
+  const double* Mg = a.Minv + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)d * d;
+#pragma unroll
+  for (int j = 0; j < DB; ++j) Mr[j] = (active && in && j < d) ? Mg[lane * d + j] : 0.0;
+  double th = (active && in) ? a.theta[(long)w * d + lane] : 0.0;
+  double mu = (active && in) ? a.mu[(long)li * d + lane] : 0.0;
+  const double bb = (active && in) ? a.b[(long)li * d + lane] : 0.0;
+  const double half_yy = active ? 0.5 * a.yy[li] : 0.0;
+  thS[v * 64 + lane] = th;
+  myx[lane] = 0.0;
+  int pending = a.pending_in;
+  int stop_code = 0, stop_iter = 0;
+  unsigned long long dv_next = 0;
+  lds_barrier();
+
+  int it = a.start_iter;
+  long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (;; ++it) {
+    if (it > a.max_iter + a.lag) break;
+    const bool stamp = a.timeline && threadIdx.x == 0 && it - a.start_iter < a.timeline_iters;
+    if (stamp) ts[0] = (long long)now_ticks();
+    // ---- halo exchange every k iterations (state after iteration it - 1)
+    if (it > a.start_iter && (it - a.start_iter) % k == 0) {
+      const unsigned tag = make_tag(a.epoch, it);
+      const int slot = ((it - a.start_iter) / k) & 1;
+      const int base = ((slot * n + p) * 2) * d;
+      if (owned && in) {
+        store_granule<false>(rtab, (base + lane) * 16, tag, th);
+        store_granule<false>(rtab, (base + d + lane) * 16, tag, mu);
+      } else if (active) {
+        double t0 = 0.0, t1 = 0.0;
+        bool ok = true;
+        for (int spin = 0;; ++spin) {
+          bool g0 = true;
+          if (in) {
+            g0 &= load_granule<false>(rtab, (base + lane) * 16, tag, &t0);
+            g0 &= load_granule<false>(rtab, (base + d + lane) * 16, tag, &t1);
+          }
+          if (__all(g0)) break;
+          if ((spin & 7) == 7 && now_ticks() > deadline) {
+            ok = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (!ok && lane == 0) abort_lds = 1;
+        th = in ? t0 : 0.0;
+        mu = in ? t1 : 0.0;
+        thS[v * 64 + lane] = th;
+      }
+    }
+    if (stamp) ts[1] = (long long)now_ticks();
+    // ---- stop rule: decision of it - lag (loaded one iteration ahead; normally already there)
+    if (threadIdx.x == 0 && it - a.start_iter >= a.lag) {
+      const int jdec = it - a.lag;
+      const unsigned tj = make_tag(a.epoch, jdec);
+      unsigned long long dv = dv_next;
+      for (int spin = 0; (unsigned)(dv >> 32) != tj; ++spin) {
+        if ((spin & 7) == 7 && now_ticks() > deadline) {
+          abort_lds = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        dv = load_dec<false>(&a.decg[jdec % a.ring]);
+      }
+      const unsigned code = (unsigned)(dv & 0xffffffffu);
+      if (code && !abort_lds) {
+        stop_lds = 1;
+        stop_code = (int)code;
+        stop_iter = jdec;
+      }
+    }
+    if (threadIdx.x == 0 && it + 1 - a.start_iter >= a.lag)
+      dv_next = load_dec<false>(&a.decg[(it + 1 - a.lag) % a.ring]);
+    if (stamp) ts[2] = (long long)now_ticks();
+    lds_barrier();
+    if (abort_lds || stop_lds) break;
+    if (stamp) ts[3] = (long long)now_ticks();
+
+    // ---- head phase (owned tails meanwhile report f(theta^{it-1}))
+    if (active && head) {
+      const double tl = nbl ? thL[lane] : 0.0, tr = nbr ? thR[lane] : 0.0;
+      double m = mu;
+      if (pending) {  // lazy end-of-iteration dual (reference order)
+        if (has_l) m = m - rho * (tl - th);
+        if (has_r) m = m + rho * (th - tr);
+      }
+      mu = m;
+      double r = bb - m;
+      if (has_l) r = r + rho * tl;
+      if (has_r) r = r + rho * tr;
+      myx[lane] = in ? r : 0.0;
+      if (stamp) ts[6] = (long long)now_ticks();
+      th = in ? reg_gemv(Mr, myx) : 0.0;
+      if (stamp) {
+        asm volatile("" ::"v"(th));
+        ts[7] = (long long)now_ticks();
+      }
+      thS[v * 64 + lane] = th;
+      if (owned && in)
+        store_granule<false>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
+                             make_tag(a.epoch, it), th);
+    }
+    pending = 1;
+    lds_barrier();
+    if (stamp) ts[4] = (long long)now_ticks();
+
+    // ---- tail phase (owned heads meanwhile report f(theta^it))
+    if (active && !head) {
+      const double tl = nbl ? thL[lane] : 0.0, tr = nbr ? thR[lane] : 0.0;
+      double r = bb - mu;
+      if (has_l) r = r + rho * tl;
+      if (has_r) r = r + rho * tr;
+      myx[lane] = in ? r : 0.0;
+      const double tn = in ? reg_gemv(Mr, myx) : 0.0;
+      double m = mu;
+      if (has_l) m = m - rho * (tl - tn);
+      if (has_r) m = m + rho * (tn - tr);
+      mu = m;
+      th = tn;
+      thS[v * 64 + lane] = th;
+      if (owned && in)
+        store_granule<false>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
+                             make_tag(a.epoch, it), th);
+    }
+    lds_barrier();
+    if (stamp) {
+      long long* tl = a.timeline + ((long)g * a.timeline_iters + (it - a.start_iter)) * 8;
+      for (int q = 0; q < 5; ++q) tl[q] = ts[q];
+      tl[5] = (long long)now_ticks();
+      tl[6] = ts[6];
+      tl[7] = ts[7];
+    }
+  }
+
+  if (owned && in) {
+    a.theta[(long)w * d + lane] = th;
+    a.mu[(long)li * d + lane] = mu;
+  }
+  if (threadIdx.x == 0) {
+    if (abort_lds) {
+      a.ctl->done = 4;
+    } else if (g == 0 && stop_code) {
+      a.ctl->done = stop_code;
+      a.ctl->conv_iter = stop_iter;
+      a.ctl->iter = it;
+      a.ctl->pending = 1;
+      a.ctl->monitored = stop_iter;
+    }
+  }
+}
+
+extern "C" {
+
+// Pick (k, L) for n workers; returns the number of worker workgroups, 0 if not applicable.
+int gadmm_chain_blocked_plan(int n, int d, int want_k, int* k_out, int* len_out) {
+  if (d > 52 || n < 2) return 0;  // DB = 64 rows spill at 3 waves per SIMD: the per-worker kernel covers d <= 64
+  int k = want_k > 0 ? want_k : 2;
+  int len = MAXW - 4 * k;
+  while (len < 1 && k > 1) {
+    --k;
+    len = MAXW - 4 * k;
+  }
+  if (len < 1) return 0;
+  if (len > n) len = n;
+  const int W = (n + len - 1) / len;
+  if (W + (n + MAXW - 1) / MAXW + 1 > 256) return 0;
+  *k_out = k;
+  *len_out = len;
+  return W;
+}
+
+long gadmm_chain_blocked_lds(int d, int len) {
+  (void)d;
+  (void)len;
+  return (long)(2 * MAXW * 64) * 8;
+}
+
+// Granules of the blk_tab buffer: exchange table [2][n][2][d] + theta ring [ring][n][d].
+long gadmm_chain_blocked_tab_granules(int n, int d, int ring) { return 2L * n * 2 * d + (long)ring * n * d; }
+
+int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
+  const PersistArgs& a = *args;
+  if (a.blk_k < 1 || a.blk_len < 1 || a.blk_len + 4 * a.blk_k > MAXW || a.d > DREG || !a.blk_tab ||
+      a.nranks != 1 || !a.has_monitor || a.n != a.n_local) {
+    gadmm_set_error("blocked chain kernel: unsupported configuration");
+    return -1;
+  }
+  if (a.lag < 1 || a.ring <= a.lag + 1 || a.start_iter + a.max_iter + a.lag >= (1 << 20)) {
+    gadmm_set_error("blocked chain kernel: ring/lag/tag range");
+    return -1;
+  }
+  const int W = (a.n + a.blk_len - 1) / a.blk_len;
+  long lds = gadmm_chain_blocked_lds(a.d, a.blk_len);
+  if (lds < (long)a.n * 8) lds = (long)a.n * 8;
+  if (lds > 160 * 1024) {
+    gadmm_set_error("blocked chain kernel: %ld B of LDS", lds);
+    return -1;
+  }
+  const void* fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32>
+                   : a.d <= 52 ? (const void*)chain_blocked_kernel<52> : (const void*)chain_blocked_kernel<64>;
+  if (lds > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  void* kargs[] = {const_cast<PersistArgs*>(&a)};
+  const int Wo = (a.n + MAXW - 1) / MAXW;
+  if (W + Wo + 1 > 256) {
+    gadmm_set_error("blocked chain kernel: %d workgroups exceed one per CU", W + Wo + 1);
+    return -1;
+  }
+  GADMM_CHECK(hipLaunchKernel(fn, dim3(W + Wo + 1), dim3(64 * MAXW), kargs, (size_t)lds, st));
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"

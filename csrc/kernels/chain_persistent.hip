@@ -34,25 +34,6 @@ namespace {
 
 constexpr int NT = 256;
 constexpr int NW = 4;
-constexpr int DREG = 64;  // register-resident variant: d <= 64, one wave per worker
-
-// y_i = sum_j M[i][j] x_j with lane i holding row i of M in registers and x broadcast from LDS
-// (zero-padded to DREG); four independent accumulators over j = k mod 4, combined ((a0 + a1) + a2) + a3:
-// exactly the summation order of symv_lds / symv_cols (wave k of 4 sums rows j = k mod 4, partials
-// added in wave order), so every engine produces bit-identical iterates (M is exactly symmetric).
-__device__ __forceinline__ double reg_gemv(const double (&Mr)[DREG], const double* xv) {
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-#pragma unroll
-  for (int j = 0; j < DREG; j += 4) {
-    const double2 x01 = *reinterpret_cast<const double2*>(xv + j);
-    const double2 x23 = *reinterpret_cast<const double2*>(xv + j + 2);
-    a0 = fma(Mr[j], x01.x, a0);
-    a1 = fma(Mr[j + 1], x01.y, a1);
-    a2 = fma(Mr[j + 2], x23.x, a2);
-    a3 = fma(Mr[j + 3], x23.y, a3);
-  }
-  return ((a0 + a1) + a2) + a3;
-}
 
 }  // namespace
 
@@ -76,7 +57,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
     abort_lds = 0;
     stop_lds = 0;
   }
-  __syncthreads();
+  lds_barrier();
 
   if (a.has_monitor && (int)blockIdx.x == a.n_local) {
     // ---------------------------------------------------------------- monitor workgroup
@@ -98,7 +79,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
           vals[w] = v;
         }
       }
-      __syncthreads();
+      lds_barrier();
       if (threadIdx.x == 0) {
         unsigned code = 0;
         if (abort_lds) {
@@ -117,7 +98,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
         const int k = it - a.start_iter;
         if (a.timeline && k < a.timeline_iters) a.timeline[((long)blockIdx.x * a.timeline_iters + k) * 8] = (long long)now_ticks();
       }
-      __syncthreads();
+      lds_barrier();
       if (stop_lds) return;
     }
   }
@@ -171,7 +152,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
   const double half_yy = 0.5 * a.yy[li];
   int pending = a.pending_in;
   int stop_code = 0, stop_iter = 0;
-  __syncthreads();
+  lds_barrier();
 
   int it = a.start_iter;
   for (;; ++it) {
@@ -248,7 +229,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
         if (i < d) xv[i] = r;
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (abort_lds || stop_lds) break;
     if (a.timeline) t_bar = (long long)now_ticks();
     if (w0) {
@@ -294,7 +275,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       }
     }
     if (a.obj_mode == 0) {  // exact: 1/2 th^T A th - b^T th + 1/2 y^T y
-      __syncthreads();
+      lds_barrier();
       if (w0) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
@@ -302,7 +283,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
           if (i < d) xv[i] = tn[c];
         }
       }
-      __syncthreads();
+      lds_barrier();
       double q[NC];
       if constexpr (REG) q[0] = reg_gemv(Ar, xv);
       else symv_lds<NC>(Al, xv, q, red, d);
@@ -330,7 +311,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
         tl[5] = t_gemv;
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
 
   // write back the final state (plain stores; visible to the host after the kernel)

@@ -100,7 +100,7 @@ __device__ __forceinline__ double local_eval(const FoArgs& a, double* lds, const
       }
     }
     sp = wave_sum_f64(sp);
-    __syncthreads();
+    lds_barrier();
     double Xs[NC];
     gemv_t_lds<NC>(X, sv, Xs, red, m, d);
     double q = 0.0;
@@ -126,7 +126,7 @@ __device__ __forceinline__ double local_eval(const FoArgs& a, double* lds, const
     if (lane == 0) sv[j] = yj / (1.0 + exp(yj * z));
   }
   if (lane == 0) wred[wv] = sp;
-  __syncthreads();
+  lds_barrier();
   double Xs[NC];
   gemv_t_lds<NC>(X, sv, Xs, red, m, d);
   double q = 0.0;
@@ -287,7 +287,7 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
   }
   const double half_yy = linear ? 0.5 * a.yy[w] : 0.0;
   const double hsq = a.alg == FO_LAG_PS ? a.hsq[w] : 0.0;
-  __syncthreads();
+  lds_barrier();
   double f = 0.0;
   if (a.alg == FO_DUALAVG) f = local_eval<NC, MC>(a, lds, L, th, bb, half_yy, g);  // grad at theta^0 = 0
 
@@ -363,7 +363,7 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
                                   deadline, &ctl->stop_iter, it);
         if (lane == 0) flag_lds = ok;
       }
-      __syncthreads();
+      lds_barrier();
       ok = flag_lds;
       if (ok != 1) {
         if (ok == 0 && threadIdx.x == 0) fo_abort(ctl);
@@ -386,7 +386,7 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
           }
         }
       }
-      __syncthreads();
+      lds_barrier();
       // every wave needs theta in registers for local_eval
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
@@ -424,7 +424,7 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
       }
       if (lane == 0) flag_lds = ok;
     }
-    __syncthreads();
+    lds_barrier();
     if (flag_lds != 1) {
       if (flag_lds == 0 && threadIdx.x == 0) fo_abort(ctl);
       break;
@@ -453,7 +453,7 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
 #pragma unroll
       for (int c = 0; c < NC; ++c) red[(wv * NC + c) * 64 + lane] = acc[c];
       if (lane == 0) lds[L.wred + wv] = (double)ok;
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
       for (int c = 0; c < NC; ++c) {
         double s = 0.0;
@@ -462,7 +462,7 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
         S[c] = s;
       }
       for (int q = 0; q < NWV; ++q) ok = min(ok, (int)lds[L.wred + q]);
-      __syncthreads();
+      lds_barrier();
     } else {  // DGD: average with the chain neighbours' gradients (GD_DGD_LAG.m:155-171)
       double gl[1][NC], gr[1][NC];
 #pragma unroll
@@ -477,9 +477,9 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
         else S[c] = G[c] + gr[0][c] + gl[0][c];
       }
       if (lane == 0) lds[L.wred + wv] = (double)ok;
-      __syncthreads();
+      lds_barrier();
       for (int q = 0; q < NWV; ++q) ok = min(ok, (int)lds[L.wred + q]);
-      __syncthreads();
+      lds_barrier();
     }
     if (ok != 1) {
       if (ok == 0 && threadIdx.x == 0) fo_abort(ctl);
@@ -508,7 +508,7 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
       }
     }  // consume
     if (threadIdx.x == 0) flag_lds = should_stop(sw, it + 1);
-    __syncthreads();
+    lds_barrier();
     if (flag_lds) break;
   }
   if (w0)

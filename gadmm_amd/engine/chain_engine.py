@@ -272,6 +272,18 @@ class NativeChainEngine:
         # exact objective (second GEMV with the Gram in LDS) whenever both matrices fit in LDS
         return 0 if int(self.lib.gadmm_chain_persistent_lds(self.d, 0)) > 0 else 1
 
+    def blocked_plan(self, fabric=None):
+        """(k, L, W) of the temporally blocked kernel for this engine, or None (multi-GPU, d > 64,
+        GADMM_BLOCKED=0)."""
+        import os
+
+        if fabric is not None or self.nranks > 1 or self.d > 64 or os.environ.get("GADMM_BLOCKED", "1") == "0":
+            return None
+        kk, ll = ctypes.c_int(0), ctypes.c_int(0)
+        want = int(os.environ.get("GADMM_BLOCK_K", "0"))
+        W = int(self.lib.gadmm_chain_blocked_plan(self.n_total, self.d, want, ctypes.byref(kk), ctypes.byref(ll)))
+        return (kk.value, ll.value, W) if W > 0 else None
+
     def run_persistent(self, lag: int = 4, timeout_s: float = 20.0, start_iter: int = 1,
                        pending_in: int = 0, fabric=None, timeline_iters: int = 0) -> EngineRun:
         """Whole solve in one launch per GPU. State must be reset (``reset()``) or resumed by the
@@ -282,6 +294,9 @@ class NativeChainEngine:
         workgroup row is the monitor (column 0 = decision posted)."""
         if not self.persistent_eligible(fabric):
             raise RuntimeError("persistent kernel not eligible for this engine/config")
+        plan = self.blocked_plan(fabric)
+        if plan is not None:
+            lag = max(lag, 8)  # the objective takes one more hop (worker -> objective wave -> monitor)
         ring = lag + 4
         dev = self.device
         slots = sorted(self.plan.head + self.plan.tail, key=lambda s: self.path.index(s.gid))
@@ -341,13 +356,24 @@ class NativeChainEngine:
         pa.trace, pa.ctl = self.trace.data_ptr(), self.ctl.data_ptr()
         tl = None
         if timeline_iters > 0:
-            tl = torch.zeros((len(slots) + 1, int(timeline_iters), 8), dtype=torch.int64, device=dev)
+            tl = torch.zeros((max(len(slots), 256) + 1, int(timeline_iters), 8), dtype=torch.int64, device=dev)
             pa.timeline, pa.timeline_iters = tl.data_ptr(), int(timeline_iters)
         import time as _time
+        if plan is not None:  # temporally blocked kernel: one halo hand-off per k iterations
+            ng = int(self.lib.gadmm_chain_blocked_tab_granules(self.n_total, self.d, ring))
+            if getattr(self, "_blk_tab", None) is None or self._blk_tab.numel() != ng * 4:
+                self._blk_tab = torch.zeros((ng * 4,), dtype=torch.int32, device=dev)
+            pa.blk_k, pa.blk_len = plan[0], plan[1]
+            pa.blk_tab = self._blk_tab.data_ptr()
+        self.last_kernel = "blocked(k=%d,L=%d,W=%d)" % plan if plan is not None else "per-worker"
         with torch.cuda.stream(self.stream):
             t0 = _time.perf_counter()
-            native.check(self.lib.gadmm_chain_persistent_launch(ctypes.byref(pa), self.stream.cuda_stream),
-                         "chain_persistent_launch")
+            if plan is not None:
+                native.check(self.lib.gadmm_chain_blocked_launch(ctypes.byref(pa), self.stream.cuda_stream),
+                             "chain_blocked_launch")
+            else:
+                native.check(self.lib.gadmm_chain_persistent_launch(ctypes.byref(pa), self.stream.cuda_stream),
+                             "chain_persistent_launch")
             self.stream.synchronize()
             t1 = _time.perf_counter()
         self.last_timeline = tl.cpu().numpy() if tl is not None else None

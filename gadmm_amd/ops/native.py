@@ -98,7 +98,8 @@ class PersistArgs(ctypes.Structure):
         ("slots", c_void_p), ("pos", c_void_p), ("Minv", c_void_p), ("A", c_void_p), ("b", c_void_p),
         ("yy", c_void_p), ("theta", c_void_p), ("mu", c_void_p), ("thg", c_void_p), ("push", c_void_p),
         ("objg", c_void_p), ("decg", c_void_p), ("dec_push", c_void_p), ("trace", c_void_p), ("ctl", c_void_p),
-        ("timeline", c_void_p), ("timeline_iters", c_int), ("pad2_", c_int),
+        ("timeline", c_void_p), ("timeline_iters", c_int), ("blk_k", c_int), ("blk_len", c_int), ("pad3_", c_int),
+        ("blk_tab", c_void_p),
     ]
 
 
@@ -139,6 +140,10 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_xgmi_free": (c_int, [c_void_p]),
         "gadmm_device_can_access_peer": (c_int, [c_int, c_int]),
         "gadmm_chain_persistent_launch": (c_int, [ctypes.POINTER(PersistArgs), c_void_p]),
+        "gadmm_chain_blocked_plan": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+        "gadmm_chain_blocked_lds": (c_long, [c_int, c_int]),
+        "gadmm_chain_blocked_tab_granules": (c_long, [c_int, c_int, c_int]),
+        "gadmm_chain_blocked_launch": (c_int, [ctypes.POINTER(PersistArgs), c_void_p]),
         "gadmm_fo_lds": (c_long, [c_int, c_int, c_int]),
         "gadmm_fo_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
         "gadmm_fo_launch": (c_int, [ctypes.POINTER(FoArgs), c_void_p]),
