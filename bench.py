@@ -16,6 +16,10 @@ of the same loop ([measured-here] row).
 
     python bench.py                      # 1 GPU
     torchrun --nproc-per-node 8 bench.py --gpus 8
+
+The other BASELINE.json configs (same JSON contract, own metric): ``--config logistic`` (configs[2]),
+``--config dgadmm`` (configs[3]), ``--config real10m`` (configs[4]: 1.25M x 10k f64 per GPU);
+see gadmm_amd/benchmarks.py.
 """
 from __future__ import annotations
 
@@ -49,6 +53,10 @@ def main():
     ap.add_argument("--fabric", choices=["auto", "xgmi", "rccl"], default="auto",
                     help="multi-GPU transport: xgmi = device-initiated granule pushes between persistent kernels "
                          "(IPC fine-grained buffers), rccl = RCCL send/recv between graph-replayed phases")
+    ap.add_argument("--config", choices=["e1", "logistic", "dgadmm", "real10m"], default="e1",
+                    help="e1 = the headline (default); the others are BASELINE.json configs[2..4]")
+    ap.add_argument("--rows", type=int, default=1_250_000, help="real10m: rows per GPU")
+    ap.add_argument("--dim", type=int, default=10_000, help="real10m: features")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -77,6 +85,9 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from gadmm_amd.parallel.comm import RcclComm, RankInfo
         comm = RankInfo(rank, world) if share else RcclComm(device)
+
+    if args.config != "e1":
+        return run_other(args, rank, world, device, comm)
 
     def all_ok(flag: bool) -> bool:
         if world == 1:
@@ -214,6 +225,32 @@ def main():
     if fabric is not None:
         fabric.close()
     if comm is not None:
+        comm.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def run_other(args, rank, world, device, comm):
+    from gadmm_amd.benchmarks import CONFIGS
+
+    if comm is None:
+        from gadmm_amd.parallel.comm import LocalComm
+        comm = LocalComm()
+    r = CONFIGS[args.config](args, rank, world, device, comm)
+    if rank == 0:
+        value = r["ms"] / 1e3
+        out = {"metric": r["metric"], "value": round(value, 6), "unit": "s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": round(r["ms"], 4), "higher_is_better": False,
+               "scaling": "weak" if args.config == "real10m" else "strong", "vs_baseline": None, "dtype": "fp64",
+               "data": "synthetic (random-init / reference-shaped, generated on device)", "config": r["config"],
+               "iterations_to_tol": r["iters"], "expected_iterations": r["expected"],
+               "iterations_match_reference": (r["iters"] == r["expected"]) if r["expected"] else None,
+               "backend": r.get("backend")}
+        for k in ("setup_s", "gram_tflops", "star_admm_s", "star_admm_iters"):
+            if k in r:
+                out[k] = r[k]
+        print(json.dumps(out), flush=True)
+    if hasattr(comm, "close"):
         comm.close()
     if world > 1:
         dist.destroy_process_group()

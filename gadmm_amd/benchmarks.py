@@ -1,0 +1,161 @@
+"""Benchmark bodies for the BASELINE.json configs other than the headline (``bench.py --config``).
+
+Each body builds this rank's problem, runs ``warmup`` untimed solves, times ``steps`` solves between a
+barrier + device synchronisation on both sides, and returns the fields of the JSON line (rank 0
+prints it; the time is the max over ranks).
+
+* ``logistic`` (configs[2]): LogisticRegression_Synthetic (the reference's inputData.mat, N = 24,
+  lambda = 1e-5), GADMM with the inexact inner-GD local solver (``chain_phase_logistic_wave`` HIP
+  kernel), rho = 2e-4, step 2.2, to the reference's 1e-4 gap (53 iterations in the reference
+  semantics; 1e-8 is not reachable with the faithful linearised inner GD).
+* ``dgadmm`` (configs[3]): D-GADMM on LinearRegression_Synthetic (N = 24), rho = 1, findPath2
+  re-chaining every 10 iterations (seeded identically on every rank), to 1e-4.
+* ``real10m`` (configs[4]): the real-shaped linear regression, 1.25M x 10k f64 per GPU as two
+  chain workers of 625K rows (100 GB of HBM each; 8 GPUs = 10M x 10k), generated on device; run it
+  with ``--steps 1 --warmup 0`` (a step is ~10 s). A step is the whole solve: Gram
+  on f64 MFMA, cached inverses, GADMM to a 1e-8 relative gap. The star ADMM of the reference on
+  the same fabric is timed once for comparison.
+"""
+from __future__ import annotations
+
+import time
+from typing import Callable, Dict
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def _timed(solve: Callable, steps: int, warmup: int, device, world: int):
+    last = None
+    for _ in range(warmup):
+        last = solve()
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        last = solve()
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    ms = (t1 - t0) * 1e3 / max(steps, 1)
+    if world > 1:
+        t = torch.tensor([ms], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+    return ms, last
+
+
+def run_logistic(args, rank, world, device, comm) -> Dict:
+    from .data import logistic_synthetic
+    from .models import LogisticRegression
+    from .algorithms import chain_admm
+    from .parallel.topology import Placement
+
+    n = args.workers
+    ds = logistic_synthetic(n)
+    pl = Placement.contiguous(n, world)
+    local = pl.local_workers(rank)
+    m = LogisticRegression(ds.X[local].to(device).contiguous(), ds.y[local].to(device).contiguous(), lam=1e-5)
+    obj0 = m.optimum(comm if world > 1 else None, n_total=n)
+    rho, tol = 2e-4, 1e-4
+
+    def solve():
+        return chain_admm(m, local, n, rho, obj0, tol, 400, comm=comm, placement=pl, local_solver="gd", step=2.2)
+
+    ms, r = _timed(solve, args.steps, args.warmup, device, world)
+    return {"metric": "wall-clock to 1e-4 objective gap, GADMM logistic regression, inner-GD HIP kernel "
+                      "(LogisticRegression_Synthetic)",
+            "ms": ms, "iters": r.iters, "expected": 53 if n == 24 else None, "backend": r.extra.get("backend"),
+            "config": {"model": "LogisticRegression_Synthetic GADMM inner-GD", "workers": n, "features": ds.dim,
+                       "samples_per_worker": ds.rows_per_worker, "rho": rho, "gd_step": 2.2, "lam": 1e-5,
+                       "tol": tol, "global_batch": n * ds.rows_per_worker, "seq_len": 1,
+                       "parallelism": "chain%d-over-%dgpu" % (n, world)}}
+
+
+def run_dgadmm(args, rank, world, device, comm) -> Dict:
+    from .data import linear_synthetic
+    from .models import LinearRegression
+    from .algorithms import dynamic_group_admm
+    from .parallel import topology as T
+    from .oracle.reference import opt_linear
+
+    n = args.workers
+    ds = linear_synthetic(n)
+    Xf, yf = ds.stacked()
+    obj0 = opt_linear(Xf.numpy(), yf.numpy())
+    pl = T.Placement.contiguous(n, world)
+    local = pl.local_workers(rank)
+    m = LinearRegression(ds.X[local].to(device).contiguous(), ds.y[local].to(device).contiguous())
+    p0, c0, _ = T.find_path(n, np.random.default_rng(5))
+    rho, tol, coh = 1.0, 1e-4, 10
+
+    def solve():
+        return dynamic_group_admm(m, rho, obj0, tol, 3000, p0, c0, coh, seed=99, n_total=n, local_ids=local,
+                                  comm=comm, placement=pl)
+
+    ms, r = _timed(solve, args.steps, args.warmup, device, world)
+    return {"metric": "wall-clock to 1e-4 objective gap, D-GADMM (findPath2 re-chaining every 10 iterations), "
+                      "linear regression (LinearRegression_Synthetic)",
+            "ms": ms, "iters": r.iters, "expected": None, "backend": r.extra.get("backend"),
+            "config": {"model": "LinearRegression_Synthetic D-GADMM closed-form", "workers": n,
+                       "features": ds.dim, "samples_per_worker": ds.rows_per_worker, "rho": rho, "coherence": coh,
+                       "tol": tol, "global_batch": n * ds.rows_per_worker, "seq_len": 1,
+                       "parallelism": "dynamic-chain%d-over-%dgpu" % (n, world)}}
+
+
+def run_real10m(args, rank, world, device, comm) -> Dict:
+    from .data import gaussian_regression
+    from .models import LinearRegression
+    from .algorithms import chain_admm, standard_admm
+    from .parallel.topology import Placement
+
+    rows, dim = args.rows, args.dim
+    wpg = 2  # two chain workers per GPU (rows / 2 each), so even one GPU runs a real chain
+    n = wpg * world
+    ids = list(range(rank * wpg, (rank + 1) * wpg))
+    pl = Placement.contiguous(n, world)
+    ds = gaussian_regression(n, rows // wpg, dim, seed=0, labels="linear", device=device, worker_ids=ids)
+    X, y = ds.X, ds.y
+    rho = 0.5 * (rows // wpg)
+    state = {}
+
+    def setup():
+        m = LinearRegression(X, y)  # f64-MFMA Gram (K1)
+        obj0 = m.optimum(comm if world > 1 else None, n_total=n)
+        return m, obj0
+
+    def solve():
+        t0 = time.perf_counter()
+        m, obj0 = setup()
+        torch.cuda.synchronize(device)
+        state["t_setup"] = time.perf_counter() - t0
+        r = chain_admm(m, ids, n, rho, obj0, 1e-8 * abs(obj0), 2000, comm=comm, placement=pl)
+        state["m"], state["obj0"] = m, obj0
+        return r
+
+    ms, r = _timed(solve, args.steps, args.warmup, device, world)
+    out = {"metric": "wall-clock to 1e-8 relative objective gap incl. Gram set-up, GADMM linear regression, "
+                     "real-shaped %d x %d per GPU" % (rows, dim),
+           "ms": ms, "iters": r.iters, "expected": None, "backend": r.extra.get("backend"),
+           "setup_s": state.get("t_setup"),
+           "gram_tflops": 2.0 * rows * (dim + 1) * (dim + 2) / 2 / max(state.get("t_setup", 1.0), 1e-9) / 1e12,
+           "config": {"model": "LinearRegression_Real-shaped", "rows_per_gpu": rows, "workers": n, "features": dim,
+                      "rho": rho, "tol_rel": 1e-8, "global_batch": rows * world, "seq_len": 1,
+                      "parallelism": "chain%d-over-%dgpu" % (n, world)}}
+    if world > 1:  # the reference's star ADMM on the same fabric (timed once, set-up excluded)
+        torch.cuda.synchronize(device)
+        dist.barrier()
+        t0 = time.perf_counter()
+        s = standard_admm(state["m"], ids, n, rho, state["obj0"], 1e-8 * abs(state["obj0"]), 500, comm=comm,
+                          placement=pl)
+        torch.cuda.synchronize(device)
+        dist.barrier()
+        out["star_admm_s"] = time.perf_counter() - t0
+        out["star_admm_iters"] = s.iters
+    return out
+
+
+CONFIGS = {"logistic": run_logistic, "dgadmm": run_dgadmm, "real10m": run_real10m}
