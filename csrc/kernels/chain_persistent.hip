@@ -374,12 +374,11 @@ int gadmm_chain_persistent_launch(const PersistArgs* args, hipStream_t st) {
   const size_t shm = (size_t)(lds > monitor_lds ? lds : monitor_lds);
 #define GADMM_P_LAUNCH(NCv, SYSv, REGv)                                                            \
   do {                                                                                             \
-    auto kfn = chain_persistent_kernel<NCv, SYSv, REGv>;                                           \
+    const void* kfn = (const void*)chain_persistent_kernel<NCv, SYSv, REGv>;                       \
     const size_t sh = REGv ? (size_t)(monitor_lds > 1024 ? monitor_lds : 1024) : shm;             \
-    if (sh > 65536)                                                                                \
-      GADMM_CHECK(hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                      (int)sh));                                                   \
-    hipLaunchKernelGGL(kfn, dim3(blocks), dim3(REGv ? 64 : NT), sh, st, a);                        \
+    if (sh > 65536) GADMM_CHECK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh)); \
+    void* kargs[] = {const_cast<PersistArgs*>(&a)};                                                \
+    GADMM_CHECK(hipLaunchKernel(kfn, dim3(blocks), dim3(REGv ? 64 : NT), kargs, sh, st));          \
   } while (0)
   static const bool force_lds = getenv("GADMM_PERSIST_LDS") != nullptr;  // A/B switch
   if (a.d <= DREG && !force_lds) {
