@@ -45,12 +45,18 @@ def chain_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: 
                local_solver: Optional[str] = None, step: float = 1.0, max_inner: int = 100,
                inner_tol: float = 1e-4, cost_quirk: bool = True, backend: str = "auto",
                name: str = "GADMM", record_theta: bool = False, engine_opts: Optional[dict] = None,
-               state=None) -> RunResult:
+               state=None, check_exchange: Optional[bool] = None) -> RunResult:
     """Run one chain-ADMM solve on this rank. ``model`` holds this rank's shards (local order =
     ``local_ids``). ``schedule`` (D-GADMM) overrides ``path``; ``cost_quirk`` reproduces the
     reference's per-head-worker accumulation of ``sum(pathCost)`` (dynamic_group_ADMM_closedForm.m:51-55).
-    ``state``: optional ``(theta_table, mu, start_iter)`` to resume from a checkpoint."""
+    ``state``: optional ``(theta_table, mu, start_iter)`` to resume from a checkpoint.
+    ``check_exchange`` (or ``GADMM_CHECK_EXCHANGE=1``): verify every ghost row against its owner after
+    every exchange (debug/race.py; forces the torch path)."""
+    import os
+
     comm = comm if comm is not None else LocalComm()
+    if check_exchange is None:
+        check_exchange = os.environ.get("GADMM_CHECK_EXCHANGE", "0") == "1"
     placement = placement if placement is not None else Placement.contiguous(n_total, comm.nranks)
     if schedule is None:
         p0 = list(path) if path is not None else list(range(n_total))
@@ -59,7 +65,8 @@ def chain_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: 
         local_solver = "closed" if model.kind == "linear" else "gd"
     dev = model.device
     use_native = False
-    if backend in ("auto", "native") and dev.type == "cuda" and local_solver in ("closed", "gd") and state is None:
+    if backend in ("auto", "native") and dev.type == "cuda" and local_solver in ("closed", "gd") and state is None \
+            and not check_exchange:
         from ..ops import native
 
         if native.available() and (comm.nranks == 1 or getattr(comm, "backend", "") == "rccl"):
@@ -70,12 +77,20 @@ def chain_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: 
         return _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, schedule,
                                   local_solver, step, max_inner, inner_tol, cost_quirk, name, engine_opts or {})
     return _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, schedule,
-                             local_solver, step, max_inner, inner_tol, cost_quirk, name, record_theta, state)
+                             local_solver, step, max_inner, inner_tol, cost_quirk, name, record_theta, state,
+                             check_exchange)
 
 
 def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, schedule,
-                      local_solver, step, max_inner, inner_tol, cost_quirk, name, record_theta, state):
+                      local_solver, step, max_inner, inner_tol, cost_quirk, name, record_theta, state,
+                      check_exchange=False):
     rank = comm.rank
+    checker = None
+    if check_exchange:
+        from ..debug.race import ExchangeChecker
+
+        checker = ExchangeChecker(comm, local_ids, n_total)
+        owner = [int(o) for o in placement.owner]
     d = model.d
     dev = model.device
     local_ids = [int(w) for w in local_ids]
@@ -100,6 +115,8 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
             plan = chain_plan(schedule.path, placement, rank)
             # new cross-rank neighbours: heads need their (new) tails' current theta first
             comm.exchange_rows(theta, plan.xchg_tail)
+            if checker is not None:
+                checker.verify(theta, [r for _, r, s in plan.xchg_tail if not s], it, "re-chain", owner)
         n_heads = (n_total + 1) // 2
         cc += float(np.sum(schedule.cost)) * (n_heads if cost_quirk else 1)
         com_cost.append(cc)
@@ -128,6 +145,9 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
                     raise ValueError("unknown local solver %r" % local_solver)
                 theta[torch.tensor(gid, dtype=torch.long, device=dev)] = new
             comm.exchange_rows(theta, xchg)
+            if checker is not None:
+                checker.verify(theta, [r for _, r, s in xchg if not s], it,
+                               "head" if xchg is plan.xchg_head else "tail", owner)
         # dual update, reference order: mu - rho (th_l - th) + rho (th - th_r)
         for slots in (plan.head, plan.tail):
             if not slots:
