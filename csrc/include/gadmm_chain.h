@@ -128,6 +128,9 @@ struct PersistArgs {
   int timeline_iters;
   int blk_k;                // temporal blocking: iterations between halo exchanges (0: auto, -1: off)
   int blk_len;              // temporal blocking: chain positions owned per workgroup (0: auto)
-  int pad3_;
+  int n_epochs;             // D-GADMM in one launch: > 0 = number of chain epochs in this launch
   u32x4* blk_tab;           // [2][n][2][d] (theta, mu) granules of the halo exchange
+  const int* epoch_start;   // [n_epochs] first iteration of each epoch (epoch_start[0] == start_iter)
+  const PhaseSlot* ep_slots;  // [n_epochs][n_local] slot of local worker b (li == b) in each epoch
+  const int* ep_pos;        // [n_epochs][n_local] chain position of local worker b in each epoch
 };

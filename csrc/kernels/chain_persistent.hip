@@ -104,23 +104,32 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
   }
 
   // ------------------------------------------------------------------ worker workgroup
-  const PhaseSlot sl = a.slots[blockIdx.x];
-  const int pos = a.pos[blockIdx.x];
-  const int li = sl.li, w = sl.gid, left = sl.left, right = sl.right;
-  const bool head = (pos % 2) == 0;
-  const int deg = (left >= 0) + (right >= 0);
+  // Static chain: workgroup b runs slot b of the position-sorted plan. D-GADMM (n_epochs > 0, LDS
+  // variant only): workgroup b is local worker b for the whole launch and takes its slot / position
+  // of each epoch from ep_slots / ep_pos (chains pre-drawn by the seeded schedule on the host).
+  const bool dyn = !REG && a.n_epochs > 0;
+  PhaseSlot sl = dyn ? a.ep_slots[blockIdx.x] : a.slots[blockIdx.x];
+  int pos = dyn ? a.ep_pos[blockIdx.x] : a.pos[blockIdx.x];
+  const int li = sl.li, w = sl.gid;
+  int left = sl.left, right = sl.right;
+  bool head = (pos % 2) == 0;
+  int deg = (left >= 0) + (right >= 0);
   const double rho = a.rho;
-  const double crho = deg * rho;
+  double crho = deg * rho;
+  int ep = 0;
+  int next_start = (dyn && a.n_epochs > 1) ? a.epoch_start[1] : 0x7fffffff;
   u32x4* const p0 = a.push ? a.push[2 * blockIdx.x] : nullptr;
   u32x4* const p1 = a.push ? a.push[2 * blockIdx.x + 1] : nullptr;
   const __amdgpu_buffer_rsrc_t rp0 = rsrc_of(p0 ? (const void*)p0 : (const void*)a.thg);
   const __amdgpu_buffer_rsrc_t rp1 = rsrc_of(p1 ? (const void*)p1 : (const void*)a.thg);
 
   const long msz = REG ? 0 : (long)d * d;
-  double* Ml = lds;                                            // d*d
-  double* Al = lds + msz;                                      // d*d (obj_mode 0)
-  double* xv = lds + (a.obj_mode == 0 ? 2 : 1) * msz;          // [64*NC] rhs / theta staging
+  const int nM = dyn ? a.nvar : 1;                             // inverses kept in LDS
+  double* Mall = lds;                                          // [nM][d*d]
+  double* Al = lds + nM * msz;                                 // d*d (obj_mode 0)
+  double* xv = Al + (a.obj_mode == 0 ? msz : 0);               // [64*NC] rhs / theta staging
   double* red = xv + 64 * NC;                                  // [NW*NC*64]
+  double* Ml = Mall + (dyn ? (long)a.deg_to_var[deg] * msz : 0);
 
   const double* Mg = a.Minv + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)d * d;
   const double* Ag = a.A + (long)li * d * d;
@@ -133,7 +142,12 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
     }
     xv[lane] = 0.0;  // zero padding beyond d stays untouched
   } else {
-    for (int e = threadIdx.x; e < d * d; e += NT) Ml[e] = Mg[e];
+    if (dyn) {
+      const double* Mw = a.Minv + (long)li * a.nvar * d * d;
+      for (long e = threadIdx.x; e < (long)a.nvar * d * d; e += NT) Mall[e] = Mw[e];
+    } else {
+      for (int e = threadIdx.x; e < d * d; e += NT) Ml[e] = Mg[e];
+    }
     if (a.obj_mode == 0)
       for (int e = threadIdx.x; e < d * d; e += NT) Al[e] = Ag[e];
   }
@@ -158,6 +172,34 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
   for (;; ++it) {
     if (it > a.max_iter + a.lag) break;
     const long long t_start = a.timeline ? (long long)now_ticks() : 0;
+    if (dyn && it == next_start) {
+      // re-chain (dynamic_group_ADMM_closedForm.m:18-21): a worker that was a head still owes the
+      // previous iteration's dual, computed with its OLD neighbours' theta^{it-1} (every worker that
+      // reached this iteration has published theta^{it-1}); then it takes its new slot.
+      if (w0 && pending && it > a.start_iter) {
+        const unsigned tp = make_tag(a.epoch, it - 1);
+        const int ok = wait_pair<NC, SYS>(rth, d, left, tp, tl, right, tp, tr, deadline);
+        if (ok != 1 && lane == 0) abort_lds = 1;
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+          double m = mu[c];
+          if (left >= 0) m = m - rho * (tl[c] - th[c]);
+          if (right >= 0) m = m + rho * (th[c] - tr[c]);
+          mu[c] = m;
+        }
+      }
+      pending = 0;
+      ++ep;
+      sl = a.ep_slots[(long)ep * a.n_local + blockIdx.x];
+      pos = a.ep_pos[(long)ep * a.n_local + blockIdx.x];
+      left = sl.left;
+      right = sl.right;
+      head = (pos % 2) == 0;
+      deg = (left >= 0) + (right >= 0);
+      crho = deg * rho;
+      Ml = Mall + (long)a.deg_to_var[deg] * msz;
+      next_start = ep + 1 < a.n_epochs ? a.epoch_start[ep + 1] : 0x7fffffff;
+    }
     long long t_ready = 0, t_pub = 0, t_bar = 0, t_gemv = 0;
     // -- stop rule: decision of iteration it - lag (all workers leave at the same boundary). Its
     // load is issued here and resolved after the neighbour wait, so its latency overlaps the wait;
@@ -341,6 +383,15 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
 extern "C" {
 
 // LDS bytes the persistent kernel needs; 0 if the shape is not eligible.
+long gadmm_chain_persistent_lds_dyn(int d, int obj_mode, int n_inv) {
+  if (d > 128) return 0;
+  const int nc = (d + 63) / 64;
+  long doubles = (long)(n_inv + (obj_mode == 0 ? 1 : 0)) * d * d + 64 * nc + NW * nc * 64 + NW + 16;
+  long bytes = doubles * 8;
+  if (bytes > 160 * 1024 - 64) return 0;
+  return bytes;
+}
+
 long gadmm_chain_persistent_lds(int d, int obj_mode) {
   if (d > 128) return 0;
   const int nc = (d + 63) / 64;
@@ -352,7 +403,13 @@ long gadmm_chain_persistent_lds(int d, int obj_mode) {
 
 int gadmm_chain_persistent_launch(const PersistArgs* args, hipStream_t st) {
   const PersistArgs& a = *args;
-  const long lds = gadmm_chain_persistent_lds(a.d, a.obj_mode);
+  const bool dyn = a.n_epochs > 0;
+  if (dyn && (a.nranks != 1 || a.push || !a.epoch_start || !a.ep_slots || !a.ep_pos)) {
+    gadmm_set_error("persistent chain kernel: dynamic epochs need one rank (epoch_start[0] must be start_iter)");
+    return -1;
+  }
+  const long lds = dyn ? gadmm_chain_persistent_lds_dyn(a.d, a.obj_mode, a.nvar)
+                       : gadmm_chain_persistent_lds(a.d, a.obj_mode);
   if (lds == 0) {
     gadmm_set_error("persistent chain kernel: d=%d not eligible", a.d);
     return -1;
@@ -381,7 +438,7 @@ int gadmm_chain_persistent_launch(const PersistArgs* args, hipStream_t st) {
     GADMM_CHECK(hipLaunchKernel(kfn, dim3(blocks), dim3(REGv ? 64 : NT), kargs, sh, st));          \
   } while (0)
   static const bool force_lds = getenv("GADMM_PERSIST_LDS") != nullptr;  // A/B switch
-  if (a.d <= DREG && !force_lds) {
+  if (a.d <= DREG && !force_lds && !dyn) {
     if (a.sys_scope) GADMM_P_LAUNCH(1, true, true);
     else GADMM_P_LAUNCH(1, false, true);
   } else if (a.d <= 64) {

@@ -268,9 +268,18 @@ class NativeChainEngine:
             return False
         return int(self.lib.gadmm_chain_persistent_lds(self.d, self._obj_mode())) > 0
 
-    def _obj_mode(self) -> int:
+    def _obj_mode(self, dynamic: bool = False) -> int:
         # exact objective (second GEMV with the Gram in LDS) whenever both matrices fit in LDS
+        if dynamic:
+            return 0 if int(self.lib.gadmm_chain_persistent_lds_dyn(self.d, 0, self.nvar)) > 0 else 1
         return 0 if int(self.lib.gadmm_chain_persistent_lds(self.d, 0)) > 0 else 1
+
+    def dynamic_eligible(self) -> bool:
+        """One-launch D-GADMM (per-epoch chains in device tables): one rank, linear, every degree's
+        inverse in LDS."""
+        if self.model != "linear" or self.nranks != 1 or self.n_local != self.n_total or self.n_local + 1 > 256:
+            return False
+        return int(self.lib.gadmm_chain_persistent_lds_dyn(self.d, self._obj_mode(True), self.nvar)) > 0
 
     def blocked_plan(self, fabric=None):
         """(k, L, W) of the temporally blocked kernel for this engine, or None (multi-GPU, d > 64,
@@ -285,16 +294,23 @@ class NativeChainEngine:
         return (kk.value, ll.value, W) if W > 0 else None
 
     def run_persistent(self, lag: int = 4, timeout_s: float = 20.0, start_iter: int = 1,
-                       pending_in: int = 0, fabric=None, timeline_iters: int = 0) -> EngineRun:
+                       pending_in: int = 0, fabric=None, timeline_iters: int = 0,
+                       epochs: Optional[Sequence] = None) -> EngineRun:
         """Whole solve in one launch per GPU. State must be reset (``reset()``) or resumed by the
         caller. ``fabric``: an ``XgmiFabric`` for the multi-GPU device-initiated transport.
         ``timeline_iters > 0`` records s_memrealtime stamps (10 ns) of the first iterations into
         ``self.last_timeline``: (workgroup, iteration, [start, ready, published, end, after the
         barrier, after the solve GEMV, -, -]); the last
-        workgroup row is the monitor (column 0 = decision posted)."""
-        if not self.persistent_eligible(fabric):
+        workgroup row is the monitor (column 0 = decision posted).
+        ``epochs``: D-GADMM in one launch, a list of ``(first_iteration, path)`` (the first entry at
+        ``start_iter``); every worker switches neighbours / role at each epoch start and flushes its
+        pending head dual with the old chain first (single rank only)."""
+        if epochs is not None:
+            if not self.dynamic_eligible():
+                raise RuntimeError("dynamic persistent kernel not eligible for this engine/config")
+        elif not self.persistent_eligible(fabric):
             raise RuntimeError("persistent kernel not eligible for this engine/config")
-        plan = self.blocked_plan(fabric)
+        plan = self.blocked_plan(fabric) if epochs is None else None
         if plan is not None:
             lag = max(lag, 8)  # the objective takes one more hop (worker -> objective wave -> monitor)
         ring = lag + 4
@@ -337,7 +353,7 @@ class NativeChainEngine:
         pa = native.PersistArgs()
         pa.d, pa.n, pa.n_local, pa.start_iter, pa.max_iter = self.d, self.n_total, len(slots), int(start_iter), \
             self.max_iter
-        pa.lag, pa.ring, pa.nvar, pa.obj_mode = int(lag), ring, self.nvar, self._obj_mode()
+        pa.lag, pa.ring, pa.nvar, pa.obj_mode = int(lag), ring, self.nvar, self._obj_mode(epochs is not None)
         for i, v in enumerate(self.deg_to_var):
             pa.deg_to_var[i] = v
         pa.pending_in = int(pending_in)
@@ -354,6 +370,29 @@ class NativeChainEngine:
         pa.push = push.data_ptr() if push is not None else None
         pa.dec_push = dec_push.data_ptr()
         pa.trace, pa.ctl = self.trace.data_ptr(), self.ctl.data_ptr()
+        ep_keep = None
+        if epochs is not None:
+            starts = [int(e[0]) for e in epochs]
+            if starts[0] != int(start_iter) or any(b <= a for a, b in zip(starts, starts[1:])):
+                raise ValueError("epochs must start at start_iter and be increasing")
+            P = np.asarray([list(e[1]) for e in epochs], dtype=np.int64)           # (E, n) position -> worker
+            E, n = P.shape
+            pos_of = np.argsort(P, axis=1)                                          # worker -> position
+            loc = np.asarray([int(w) for w in self.local_ids], dtype=np.int64)
+            k = pos_of[:, loc]                                                      # (E, n_local)
+            rows = np.arange(E)[:, None]
+            left = np.where(k > 0, P[rows, np.maximum(k - 1, 0)], -1)
+            right = np.where(k + 1 < n, P[rows, np.minimum(k + 1, n - 1)], -1)
+            li = np.broadcast_to(np.arange(len(loc)), k.shape)
+            es = np.stack([li, np.broadcast_to(loc, k.shape), left, right], axis=-1).astype(np.int32).reshape(-1)
+            pp = k.astype(np.int32).reshape(-1)
+            with torch.cuda.stream(self.stream):
+                st_t = torch.tensor(starts, dtype=torch.int32, device=dev)
+                es_t = torch.from_numpy(np.ascontiguousarray(es)).to(dev)
+                pp_t = torch.from_numpy(np.ascontiguousarray(pp)).to(dev)
+            ep_keep = (st_t, es_t, pp_t)
+            pa.n_epochs = len(starts)
+            pa.epoch_start, pa.ep_slots, pa.ep_pos = st_t.data_ptr(), es_t.data_ptr(), pp_t.data_ptr()
         tl = None
         if timeline_iters > 0:
             tl = torch.zeros((max(len(slots), 256) + 1, int(timeline_iters), 8), dtype=torch.int64, device=dev)

@@ -98,8 +98,8 @@ class PersistArgs(ctypes.Structure):
         ("slots", c_void_p), ("pos", c_void_p), ("Minv", c_void_p), ("A", c_void_p), ("b", c_void_p),
         ("yy", c_void_p), ("theta", c_void_p), ("mu", c_void_p), ("thg", c_void_p), ("push", c_void_p),
         ("objg", c_void_p), ("decg", c_void_p), ("dec_push", c_void_p), ("trace", c_void_p), ("ctl", c_void_p),
-        ("timeline", c_void_p), ("timeline_iters", c_int), ("blk_k", c_int), ("blk_len", c_int), ("pad3_", c_int),
-        ("blk_tab", c_void_p),
+        ("timeline", c_void_p), ("timeline_iters", c_int), ("blk_k", c_int), ("blk_len", c_int), ("n_epochs", c_int),
+        ("blk_tab", c_void_p), ("epoch_start", c_void_p), ("ep_slots", c_void_p), ("ep_pos", c_void_p),
     ]
 
 
@@ -133,6 +133,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_chain_engine_exchange": (c_int, [c_void_p, c_int]),
         "gadmm_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
         "gadmm_chain_persistent_lds": (c_long, [c_int, c_int]),
+        "gadmm_chain_persistent_lds_dyn": (c_long, [c_int, c_int, c_int]),
         "gadmm_chain_big_rbuf_stride": (c_long, [c_int]),
         "gadmm_xgmi_alloc": (c_int, [ctypes.c_size_t, ctypes.POINTER(c_void_p), ctypes.c_char_p]),
         "gadmm_xgmi_open": (c_int, [ctypes.c_char_p, ctypes.POINTER(c_void_p)]),

@@ -63,6 +63,25 @@ def greedy_chain(d_square: np.ndarray, start: int = 0) -> List[int]:
     return path
 
 
+def greedy_chains(d_square: np.ndarray, start: int = 0) -> np.ndarray:
+    """``greedy_chain`` for a batch of geometries (E, N, N) at once; same tie rule (lowest index)."""
+    E, n, _ = d_square.shape
+    paths = np.zeros((E, n), dtype=np.int64)
+    paths[:, 0] = start
+    visited = np.zeros((E, n), dtype=bool)
+    visited[:, start] = True
+    cur = np.full(E, start)
+    ar = np.arange(E)
+    for k in range(1, n):
+        row = np.where(visited, np.inf, d_square[ar, cur])
+        row[ar, cur] = np.inf
+        nxt = np.argmin(row, axis=1)
+        paths[:, k] = nxt
+        visited[ar, nxt] = True
+        cur = nxt
+    return paths
+
+
 def find_path(n: int, rng: np.random.Generator) -> Tuple[List[int], np.ndarray, np.ndarray]:
     """``[path, pathCost, d_square] = findPath(N)``: squared-distance hop costs, 50x50 area."""
     g = random_geometry(n, 50.0, rng)
@@ -109,6 +128,15 @@ def rechain_iteration(it: int, coherence: float) -> bool:
     return it > 1 and c > 0 and it % c == 0
 
 
+def rechain_iterations(max_iter: int, coherence: float) -> np.ndarray:
+    """All iterations in [2, max_iter] at which ``rechain_iteration`` fires."""
+    if coherence is None or coherence <= 0 or not np.isfinite(coherence) or int(coherence) <= 0:
+        return np.zeros(0, dtype=np.int64)
+    c = int(coherence)
+    its = np.arange(c, max_iter + 1, c, dtype=np.int64)
+    return its[its > 1]
+
+
 class PathSchedule:
     """Deterministic sequence of chains for D-GADMM.
 
@@ -128,6 +156,43 @@ class PathSchedule:
         self.path_matrix = path_matrix
         self.cost_matrix = cost_matrix
         self.k = 1  # next row of the matrices
+
+    def save(self):
+        return (self.rng.bit_generator.state, list(self.path), self.cost.copy(), self.k)
+
+    def restore(self, st) -> None:
+        self.rng.bit_generator.state = st[0]
+        self.path, self.cost, self.k = list(st[1]), st[2].copy(), st[3]
+
+    def prefetch(self, count: int):
+        """The next ``count`` chains, exactly as ``count`` successive re-chains would draw them
+        (same RNG stream: the geometries of all epochs come from one batched draw), vectorised over
+        epochs. Advances the schedule past them. Returns ``[(path, cost), ...]``."""
+        out = []
+        if count <= 0:
+            return out
+        if self.kind == "matrix":
+            for _ in range(count):
+                out.append((list(self.path_matrix[self.k]), np.asarray(self.cost_matrix[self.k])))
+                self.k += 1
+        else:
+            n = self.n
+            side = 50.0 if self.kind == "findPath" else 250.0
+            xy = self.rng.random((count, n, 2)) * side   # == count sequential rng.random((n, 2))
+            x, y = xy[..., 0], xy[..., 1]
+            d2 = (x[:, :, None] - x[:, None, :]) ** 2 + (y[:, :, None] - y[:, None, :]) ** 2
+            idx = np.arange(n)
+            d2[:, idx, idx] = 0.0
+            paths = greedy_chains(d2)
+            if self.kind == "findPath":
+                hop = d2
+            else:
+                hop = link_energy(d2)
+            for e in range(count):
+                p = paths[e]
+                out.append(([int(v) for v in p], hop[e, p[:-1], p[1:]].copy()))
+        self.path, self.cost = out[-1][0], np.asarray(out[-1][1], dtype=np.float64)
+        return out
 
     def step(self, it: int) -> bool:
         """Advance to iteration ``it``; returns True if the chain changed."""
