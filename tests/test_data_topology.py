@@ -125,3 +125,20 @@ def test_path_schedule_deterministic():
     for it in range(1, 20):
         assert a.step(it) == b.step(it)
         assert a.path == b.path
+
+
+def test_optimal_sol_fixture_loads_and_is_dominated_by_certified_optimum():
+    """D5 optimalSol.mat (shipped, only ``%load``-ed at GD_DGD_LAG_logistic.m:79, provenance unknown):
+    read with the plain MAT v5 reader (nothing executed). Its obj0 = 0.72487849 is not produced by any
+    reference script on inputData.mat - parity unpinned; it lies above the certified optimum with the
+    N*lambda ridge (0.71772698), which 100k-iteration GD also reaches, so it is not a
+    lower bound we could be missing."""
+    import os
+    import numpy as np
+    from gadmm_amd.data.matfile import load_optimal_sol
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    obj0, trace = load_optimal_sol(os.path.join(root, "fixtures", "optimalSol.mat"))
+    assert abs(obj0 - 0.7248784913764398) < 1e-15
+    assert trace.shape == (40000,) and np.all(trace == obj0)
+    assert 0.7177269844827422 < obj0
