@@ -117,7 +117,26 @@ def main():
 
     fabric = None
     fabric_kind = "local" if world == 1 else "rccl"
-    if world > 1 and args.fabric in ("auto", "xgmi") and args.engine != "graph":
+    blk = None  # temporally blocked kernel across GPUs (one xGMI exchange per k iterations)
+    if world > 1 and args.fabric in ("auto", "xgmi") and args.engine != "graph" and ds.dim <= 52 \
+            and os.environ.get("GADMM_BLOCKED", "1") != "0":
+        ok, err = False, ""
+        try:
+            from gadmm_amd.engine.blocked_xgmi import BlockedXgmiEngine
+            blk = BlockedXgmiEngine(ds.X, ds.y, args.workers, placement, rank, args.rho, obj0, args.tol, max_iter,
+                                    device)
+            ok = True
+        except Exception as e:
+            err = str(e)
+        if not all_ok(ok):
+            if rank == 0:
+                print("bench.py: blocked xgmi engine unavailable (%s)" % (err or "remote"), file=sys.stderr)
+            if blk is not None:
+                blk.close()
+            blk = None
+        else:
+            fabric_kind = "xgmi"
+    if world > 1 and blk is None and args.fabric in ("auto", "xgmi") and args.engine != "graph":
         ok = False
         err = ""
         try:
@@ -137,9 +156,16 @@ def main():
         else:
             fabric_kind = "xgmi"
     persistent = (args.engine in ("auto", "persistent")) and (
-        eng.persistent_eligible() if world == 1 else fabric is not None)
+        eng.persistent_eligible() if world == 1 else (fabric is not None or blk is not None))
+
+    from collections import namedtuple
+    BlkRun = namedtuple("BlkRun", "iters done wall_ms p2p_bytes monitor_bytes")
 
     def solve():
+        if blk is not None and persistent:
+            blk.refresh()
+            it_, done_, ms_ = blk.run()
+            return BlkRun(it_, done_, ms_, blk.exchange_bytes_per_solve(it_), 0)
         eng.refresh(X_loc, y_loc)
         eng.reset()
         if persistent:
@@ -155,10 +181,17 @@ def main():
             good = False
             print("bench.py[rank %d]: %s" % (rank, e), file=sys.stderr)
         if persistent and world > 1 and not all_ok(good):
-            # a stalled device-initiated hand-off (done == 4) on any rank: every rank drops to RCCL
-            persistent, fabric_kind = False, "rccl(fallback)"
+            # a stalled device-initiated hand-off (done == 4) on any rank: every rank drops to the
+            # per-worker xgmi kernel (if the blocked one failed) or to RCCL
+            if blk is not None:
+                blk.close()
+                blk = None
+                persistent = fabric is not None
+                fabric_kind = "xgmi(per-worker fallback)" if persistent else "rccl(fallback)"
+            else:
+                persistent, fabric_kind = False, "rccl(fallback)"
             if rank == 0:
-                print("bench.py: xgmi solve failed; falling back to RCCL", file=sys.stderr)
+                print("bench.py: xgmi solve failed; falling back (%s)" % fabric_kind, file=sys.stderr)
         runs.append(None)
     barrier()
     t0 = time.perf_counter()
@@ -172,7 +205,9 @@ def main():
     iters = last.iters if last is not None else 0
     p2p = last.p2p_bytes if last is not None else 0
     mon = last.monitor_bytes if last is not None else 0
-    if persistent and world > 1:
+    if persistent and world > 1 and blk is not None:
+        mon = 0
+    elif persistent and world > 1:
         # device-initiated pushes: one d-vector per cross-GPU neighbour relation per phase
         p2p = chain_message_count(path, placement) * ds.dim * 8 * iters // world  # per-rank share, summed below
         n_remote = sum(1 for w in range(args.workers) if int(placement.owner[w]) != 0)
@@ -185,7 +220,7 @@ def main():
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         ms = float(mx[0])
         p2p, mon = int(sm[1]), int(sm[2])
-    tr = eng.objective_trace(iters)
+    tr = blk.objective_trace(iters) if (blk is not None and persistent) else eng.objective_trace(iters)
     gap = abs(float(tr[iters - 1]) - obj0) if iters > 0 else float("nan")
     expect = EXPECTED_ITERS.get(float(args.rho)) if args.workers == 24 and args.tol == 1e-8 else None
     if rank == 0:
@@ -216,12 +251,14 @@ def main():
             "p2p_messages_per_iteration": chain_message_count(path, placement),
             "us_per_iteration": round(ms * 1e3 / max(iters, 1), 3),
             "engine": "persistent" if persistent else ("graph" if eng.graph_ok() and not args.no_graph else "eager"),
-            "kernel": getattr(eng, "last_kernel", None) if persistent else None,
+            "kernel": (blk.last_kernel if blk is not None else getattr(eng, "last_kernel", None)) if persistent else None,
             "fabric": fabric_kind,
             "baseline_s": BASELINE_S,
         }
         print(json.dumps(out), flush=True)
     eng.close()
+    if blk is not None:
+        blk.close()
     if fabric is not None:
         fabric.close()
     if comm is not None:

@@ -133,4 +133,11 @@ struct PersistArgs {
   const int* epoch_start;   // [n_epochs] first iteration of each epoch (epoch_start[0] == start_iter)
   const PhaseSlot* ep_slots;  // [n_epochs][n_local] slot of local worker b (li == b) in each epoch
   const int* ep_pos;        // [n_epochs][n_local] chain position of local worker b in each epoch
+  // temporal blocking across GPUs (xGMI): this rank owns chain positions [seg_lo, seg_hi]; its
+  // workgroups compute [seg_lo - 2k, seg_hi + 2k]; owned (theta, mu) are also pushed into the
+  // exchange tables of the peers whose computed range [peer_lo, peer_hi] contains them.
+  int seg_lo, seg_hi;       // seg_hi < 0: the whole chain (one GPU)
+  int blk_npeer, pad5_;
+  int blk_peer_lo[8], blk_peer_hi[8];
+  u32x4* const* blk_peer_tab;  // [blk_npeer] peers' exchange tables (IPC-mapped)
 };

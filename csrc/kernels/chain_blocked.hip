@@ -58,14 +58,22 @@ __device__ __forceinline__ double lds_gemv_cols(const double* A, int d, const do
 }  // namespace
 
 // DB: register row length (multiple of 4, >= d); 52 keeps d = 50 within the 3-waves-per-SIMD budget.
-template <int DB>
+// SYS: multi-GPU (xGMI fabric): system-scope granules in IPC fine-grained memory; this rank owns
+// chain positions [seg_lo, seg_hi] and pushes owned (theta, mu) into its peers' exchange tables.
+// Block layout: [0, W) worker workgroups, [W, W + Wo) objective workgroups, W + Wo the monitor
+// (rank 0 only).
+template <int DB, bool SYS>
 __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int abort_lds, stop_lds;
-    const int d = a.d, n = a.n;
+  const int d = a.d, n = a.n;
   const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
   const int k = a.blk_k, L = a.blk_len, H = 2 * a.blk_k;
-  const int W = (n + L - 1) / L;
+  const bool multi = a.nranks > 1;
+  const int seg_lo = multi ? a.seg_lo : 0, seg_hi = multi ? a.seg_hi : n - 1;
+  const int nseg = seg_hi - seg_lo + 1;
+  const int W = (nseg + L - 1) / L;
+  const int Wo = (nseg + MAXW - 1) / MAXW;
   const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
   const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
   const __amdgpu_buffer_rsrc_t rtab = rsrc_of(a.blk_tab);
@@ -75,7 +83,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   }
   lds_barrier();
 
-  if ((int)blockIdx.x == W) {
+  if ((int)blockIdx.x == W + Wo) {
     // ------------------------------------------------------------- monitor (same as chain_persistent)
     if (v != 0) return;
     double* vals = lds;  // [n]
@@ -86,7 +94,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       for (int w = lane; w < n; w += 64) {
         double val = 0.0;
         for (int spin = 0;; ++spin) {
-          if (load_granule<false>(rob, (slot * n + w) * 16, tag, &val)) break;
+          if (load_granule<SYS>(rob, (slot * n + w) * 16, tag, &val)) break;
           if ((spin & 7) == 7 && now_ticks() > deadline) {
             okall = false;
             break;
@@ -108,24 +116,20 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
           else if (fabs(s - a.obj0) < a.tol) code = 1;
           else if (it >= a.max_iter) code = 2;
         }
-        store_dec<false>(a.decg + slot, ((unsigned long long)tag << 32) | code);
+        const unsigned long long dv = ((unsigned long long)tag << 32) | code;
+        for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
         const int kk = it - a.start_iter;
         if (a.timeline && kk < a.timeline_iters) a.timeline[((long)blockIdx.x * a.timeline_iters + kk) * 8] = (long long)now_ticks();
       }
-      if (__shfl((int)code, 0, 64)) {
-        if (lane == 0)  // epoch-tagged stop word for the objective workgroups
-          __hip_atomic_store(&a.ctl->ticket, (a.epoch << 1) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-      }
+      if (__shfl((int)code, 0, 64)) return;
     }
   }
 
-  const int Wo = (n + MAXW - 1) / MAXW;
   const long ring_base = 2L * n * 2 * d;  // theta ring [ring][n][d] after the exchange table
   if ((int)blockIdx.x >= W) {
     // ----------------------------------------------------------------- objective workgroup
-    const int q = ((int)blockIdx.x - W - 1) * MAXW + v;  // chain position (block W is the monitor)
-    if (q >= n) return;
+    const int q = seg_lo + ((int)blockIdx.x - W) * MAXW + v;  // an owned chain position
+    if (q > seg_hi) return;
     const PhaseSlot so = a.slots[q];
     const bool in = lane < d;
     double Ar[DB];
@@ -136,16 +140,20 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     const double hy = 0.5 * a.yy[so.li];
     double* xo = lds + v * 64;
     xo[lane] = 0.0;
-    const unsigned stopw = (a.epoch << 1) | 1u;
     for (int it = a.start_iter;; ++it) {
       const unsigned tag = make_tag(a.epoch, it);
       const long off = (ring_base + ((long)(it % a.ring) * n + q) * d + lane) * 16;
       double x = 0.0;
       for (int spin = 0;; ++spin) {
-        const bool ok = !in || load_granule<false>(rtab, (int)off, tag, &x);
+        const bool ok = !in || load_granule<SYS>(rtab, (int)off, tag, &x);
         if (__all(ok)) break;
         if ((spin & 7) == 7) {
-          if (__hip_atomic_load(&a.ctl->ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == stopw) return;
+          // the run ended: the workers stop at iteration j + lag after a stop decision for j, so
+          // theta^it never comes once decision[it - lag] says stop (on every rank's own ring)
+          if (it - a.start_iter >= a.lag) {
+            const unsigned long long dv = load_dec<SYS>(&a.decg[(it - a.lag) % a.ring]);
+            if ((unsigned)(dv >> 32) == make_tag(a.epoch, it - a.lag) && (unsigned)(dv & 0xffffffffu) != 0u) return;
+          }
           if (now_ticks() > deadline) return;  // the monitor times out and reports it
         }
         __builtin_amdgcn_s_sleep(1);
@@ -154,13 +162,13 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       const double qv = reg_gemv(Ar, xo);  // (A th)_i in the order of every other engine
       const double part = in ? (0.5 * qv - bo) * x : 0.0;
       const double f = wave_sum_f64(part) + hy;
-      if (lane == 0) store_granule<false>(rob, ((it % a.ring) * n + so.gid) * 16, tag, f);
+      if (lane == 0) store_granule<SYS>(rob, ((it % a.ring) * n + so.gid) * 16, tag, f);
     }
   }
 
   // ---------------------------------------------------------------------- worker workgroup
   const int g = blockIdx.x;
-  const int s0 = g * L, e0 = min(n, s0 + L) - 1;  // owned chain positions [s0, e0]
+  const int s0 = seg_lo + g * L, e0 = min(seg_hi + 1, s0 + L) - 1;  // owned chain positions [s0, e0]
   const int ra = max(0, s0 - H), rb = min(n - 1, e0 + H);
   const int nv = rb - ra + 1;
   const int p = ra + v;  // this wave's chain position
@@ -209,16 +217,22 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       const int slot = ((it - a.start_iter) / k) & 1;
       const int base = ((slot * n + p) * 2) * d;
       if (owned && in) {
-        store_granule<false>(rtab, (base + lane) * 16, tag, th);
-        store_granule<false>(rtab, (base + d + lane) * 16, tag, mu);
+        store_granule<SYS>(rtab, (base + lane) * 16, tag, th);
+        store_granule<SYS>(rtab, (base + d + lane) * 16, tag, mu);
+        for (int q = 0; q < a.blk_npeer; ++q)
+          if (p >= a.blk_peer_lo[q] && p <= a.blk_peer_hi[q]) {  // a peer GPU computes this position too
+            const __amdgpu_buffer_rsrc_t rpe = rsrc_of(a.blk_peer_tab[q]);
+            store_granule<SYS>(rpe, (base + lane) * 16, tag, th);
+            store_granule<SYS>(rpe, (base + d + lane) * 16, tag, mu);
+          }
       } else if (active) {
         double t0 = 0.0, t1 = 0.0;
         bool ok = true;
         for (int spin = 0;; ++spin) {
           bool g0 = true;
           if (in) {
-            g0 &= load_granule<false>(rtab, (base + lane) * 16, tag, &t0);
-            g0 &= load_granule<false>(rtab, (base + d + lane) * 16, tag, &t1);
+            g0 &= load_granule<SYS>(rtab, (base + lane) * 16, tag, &t0);
+            g0 &= load_granule<SYS>(rtab, (base + d + lane) * 16, tag, &t1);
           }
           if (__all(g0)) break;
           if ((spin & 7) == 7 && now_ticks() > deadline) {
@@ -245,7 +259,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
           break;
         }
         __builtin_amdgcn_s_sleep(1);
-        dv = load_dec<false>(&a.decg[jdec % a.ring]);
+        dv = load_dec<SYS>(&a.decg[jdec % a.ring]);
       }
       const unsigned code = (unsigned)(dv & 0xffffffffu);
       if (code && !abort_lds) {
@@ -255,7 +269,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       }
     }
     if (threadIdx.x == 0 && it + 1 - a.start_iter >= a.lag)
-      dv_next = load_dec<false>(&a.decg[(it + 1 - a.lag) % a.ring]);
+      dv_next = load_dec<SYS>(&a.decg[(it + 1 - a.lag) % a.ring]);
     if (stamp) ts[2] = (long long)now_ticks();
     lds_barrier();
     if (abort_lds || stop_lds) break;
@@ -282,7 +296,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       }
       thS[v * 64 + lane] = th;
       if (owned && in)
-        store_granule<false>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
+        store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
                              make_tag(a.epoch, it), th);
     }
     pending = 1;
@@ -304,7 +318,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       th = tn;
       thS[v * 64 + lane] = th;
       if (owned && in)
-        store_granule<false>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
+        store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
                              make_tag(a.epoch, it), th);
     }
     lds_barrier();
@@ -365,8 +379,11 @@ long gadmm_chain_blocked_tab_granules(int n, int d, int ring) { return 2L * n * 
 
 int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   const PersistArgs& a = *args;
-  if (a.blk_k < 1 || a.blk_len < 1 || a.blk_len + 4 * a.blk_k > MAXW || a.d > DREG || !a.blk_tab ||
-      a.nranks != 1 || !a.has_monitor || a.n != a.n_local) {
+  const bool multi = a.nranks > 1;
+  if (a.blk_k < 1 || a.blk_len < 1 || a.blk_len + 4 * a.blk_k > MAXW || a.d > 52 || !a.blk_tab || !a.dec_push ||
+      (!multi && (!a.has_monitor || a.n != a.n_local)) ||
+      (multi && (a.seg_lo < 0 || a.seg_hi < a.seg_lo || a.seg_hi >= a.n || a.blk_npeer < 0 || a.blk_npeer > 8 ||
+                 (a.blk_npeer > 0 && !a.blk_peer_tab) || a.start_iter != 1 || a.pending_in != 0 || !a.sys_scope))) {
     gadmm_set_error("blocked chain kernel: unsupported configuration");
     return -1;
   }
@@ -374,23 +391,26 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
     gadmm_set_error("blocked chain kernel: ring/lag/tag range");
     return -1;
   }
-  const int W = (a.n + a.blk_len - 1) / a.blk_len;
+  const int nseg = multi ? a.seg_hi - a.seg_lo + 1 : a.n;
+  const int W = (nseg + a.blk_len - 1) / a.blk_len;
+  const int Wo = (nseg + MAXW - 1) / MAXW;
+  const int blocks = W + Wo + (a.has_monitor ? 1 : 0);
+  if (blocks > 256) {
+    gadmm_set_error("blocked chain kernel: %d workgroups exceed one per CU", blocks);
+    return -1;
+  }
   long lds = gadmm_chain_blocked_lds(a.d, a.blk_len);
   if (lds < (long)a.n * 8) lds = (long)a.n * 8;
   if (lds > 160 * 1024) {
     gadmm_set_error("blocked chain kernel: %ld B of LDS", lds);
     return -1;
   }
-  const void* fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32>
-                   : a.d <= 52 ? (const void*)chain_blocked_kernel<52> : (const void*)chain_blocked_kernel<64>;
+  const void* fn;
+  if (a.sys_scope) fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, true> : (const void*)chain_blocked_kernel<52, true>;
+  else fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, false> : (const void*)chain_blocked_kernel<52, false>;
   if (lds > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   void* kargs[] = {const_cast<PersistArgs*>(&a)};
-  const int Wo = (a.n + MAXW - 1) / MAXW;
-  if (W + Wo + 1 > 256) {
-    gadmm_set_error("blocked chain kernel: %d workgroups exceed one per CU", W + Wo + 1);
-    return -1;
-  }
-  GADMM_CHECK(hipLaunchKernel(fn, dim3(W + Wo + 1), dim3(64 * MAXW), kargs, (size_t)lds, st));
+  GADMM_CHECK(hipLaunchKernel(fn, dim3(blocks), dim3(64 * MAXW), kargs, (size_t)lds, st));
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

@@ -1,0 +1,204 @@
+"""Temporally blocked GADMM across GPUs (one process per GPU, xGMI fabric).
+
+Each rank owns a contiguous chain segment [seg_lo, seg_hi] and runs ``chain_blocked_kernel<SYS>``:
+its workgroups compute the segment plus a halo of H = 2k positions on each side (the halo workers'
+Gram / inverse are computed locally from their shards), and every k iterations each rank pushes the
+(theta, mu) of its owned workers straight into the exchange tables of the peer GPUs whose computed
+range contains them (IPC-mapped fine-grained memory, system-scope granule stores over xGMI). A
+cross-GPU hand-off therefore happens once per k iterations instead of twice per iteration.
+Objective waves on every rank evaluate f_n of the owned workers and push them to rank 0's monitor
+ring; rank 0's monitor pushes the stop decision into every rank's ring (as in the per-worker fabric,
+parallel/xgmi.py). Hand-offs are tagged granules salted per solve, so correctness never depends on
+timing; every spin has a deadline and a stalled peer surfaces as ``done == 4`` (callers fall back).
+
+Identity chain (the static GADMM of the headline benchmark); the halo workers' data must be
+available on the rank (the benchmark generates the full synthetic dataset on every rank).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops import native
+from ..ops.linalg import gram, spd_inverse
+from ..parallel.topology import Placement
+from ..parallel.xgmi import _Buf
+
+
+class BlockedXgmiEngine:
+    LAG = 8
+
+    def __init__(self, X_all: torch.Tensor, y_all: torch.Tensor, n_total: int, placement: Placement, rank: int,
+                 rho: float, obj0: float, tol: float, max_iter: int, device: torch.device, group=None,
+                 want_k: int = 0):
+        """Collective over ``group``. ``X_all`` / ``y_all``: the shards of at least this rank's
+        computed range (indexable by global worker id); only those rows are read."""
+        self.lib = native.require()
+        self.rank, self.nranks, self.device = rank, placement.nranks, device
+        self.n, self.d = int(n_total), int(X_all.shape[2])
+        self.rho, self.obj0, self.tol, self.max_iter = float(rho), float(obj0), float(tol), int(max_iter)
+        mine = placement.local_workers(rank)
+        self.seg_lo, self.seg_hi = min(mine), max(mine)
+        if mine != list(range(self.seg_lo, self.seg_hi + 1)):
+            raise ValueError("blocked xgmi engine needs contiguous segments")
+        segs = [(min(placement.local_workers(r)), max(placement.local_workers(r))) for r in range(self.nranks)]
+        nseg = max(hi - lo + 1 for lo, hi in segs)
+        kk, ll = ctypes.c_int(0), ctypes.c_int(0)
+        if int(self.lib.gadmm_chain_blocked_plan(nseg, self.d, int(want_k), ctypes.byref(kk), ctypes.byref(ll))) <= 0:
+            raise RuntimeError("blocked xgmi engine: no blocking plan for d=%d" % self.d)
+        self.k, self.L = kk.value, ll.value
+        H = 2 * self.k
+        self.H = H
+        comp = [(max(0, lo - H), min(self.n - 1, hi + H)) for lo, hi in segs]
+        self.ext_lo, self.ext_hi = comp[rank]
+        self.ring = self.LAG + 4
+        torch.cuda.set_device(device)
+        f64 = torch.float64
+        ext = list(range(self.ext_lo, self.ext_hi + 1))
+        self.X = X_all[ext].to(device).contiguous()
+        self.y = y_all[ext].to(device).contiguous()
+        self.stream = torch.cuda.Stream(device)
+        with torch.cuda.stream(self.stream):
+            self.A, self.b, self.yy = gram(self.X, self.y)
+            self._inverses()
+            self.theta = torch.zeros((self.n, self.d), dtype=f64, device=device)
+            self.mu = torch.zeros((len(ext), self.d), dtype=f64, device=device)
+            self.trace = torch.full((self.max_iter,), float("nan"), dtype=f64, device=device)
+            self.ctl = torch.zeros((8,), dtype=torch.int32, device=device)
+            slots = []
+            for p in range(self.n):  # position == worker id (identity chain); li indexes the ext arrays
+                li = p - self.ext_lo if self.ext_lo <= p <= self.ext_hi else -1
+                slots += [li, p, p - 1 if p > 0 else -1, p + 1 if p + 1 < self.n else -1]
+            self.slots = torch.tensor(slots, dtype=torch.int32, device=device)
+            self.pos = torch.arange(self.n, dtype=torch.int32, device=device)
+        self.stream.synchronize()
+        # ---- fabric: exchange table + theta ring (every rank), objective ring (rank 0), decision rings
+        ng = int(self.lib.gadmm_chain_blocked_tab_granules(self.n, self.d, self.ring))
+        self.tab = self.objg = self.decg = None
+        self.opened = {}
+        err = ""
+        h = None
+        try:
+            self.tab = _Buf(self.lib, ng * 16)
+            self.objg = _Buf(self.lib, self.ring * self.n * 16)
+            self.decg = _Buf(self.lib, self.ring * 8)
+            h = (bytes(self.tab.handle.raw), bytes(self.objg.handle.raw), bytes(self.decg.handle.raw))
+        except Exception as e:  # pragma: no cover - box dependent
+            err = "rank %d alloc: %s" % (rank, e)
+        allh = [None] * self.nranks
+        dist.all_gather_object(allh, (h, err), group=group)
+        errs = [e for _, e in allh if e]
+        ok = not errs
+        self.peers: List[int] = []
+        self.peer_ranges = []
+        self.peer_ptrs: List[int] = []
+        if ok:
+            try:
+                for q in range(self.nranks):
+                    if q == rank:
+                        continue
+                    lo, hi = comp[q]
+                    if hi >= self.seg_lo and lo <= self.seg_hi:  # q computes some of my positions
+                        self.peers.append(q)
+                        self.peer_ranges.append((lo, hi))
+                        self.peer_ptrs.append(self._open(allh[q][0][0], ("tab", q)))
+                self.objg_mon = self.objg.ptr.value if rank == 0 else self._open(allh[0][0][1], ("objg", 0))
+                self.dec_all = [self.decg.ptr.value if q == rank else self._open(allh[q][0][2], ("decg", q))
+                                for q in range(self.nranks)] if rank == 0 else [self.decg.ptr.value]
+            except Exception as e:  # pragma: no cover
+                ok, err = False, str(e)
+        flag = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64)
+        dist.all_reduce(flag, group=group)
+        if float(flag.item()) != 0.0:
+            self.close()
+            raise RuntimeError("blocked xgmi fabric failed on some rank (%s)" % ("; ".join(errs) or err or "remote"))
+        if len(self.peers) > 8:
+            self.close()
+            raise RuntimeError("blocked xgmi engine: more than 8 peers")
+        self.peer_tab_t = torch.tensor(self.peer_ptrs + [0], dtype=torch.int64, device=device)
+        self.dec_push_t = torch.tensor(self.dec_all, dtype=torch.int64, device=device)
+        self.epoch = 0
+        self.last_kernel = "blocked-xgmi(k=%d,L=%d,H=%d,peers=%s)" % (self.k, self.L, H, self.peers)
+
+    def _open(self, hbytes: bytes, key) -> int:
+        p = ctypes.c_void_p()
+        native.check(self.lib.gadmm_xgmi_open(ctypes.create_string_buffer(hbytes, 64), ctypes.byref(p)),
+                     "xgmi_open %s" % (key,))
+        self.opened[key] = p
+        return p.value
+
+    def _inverses(self, out: Optional[torch.Tensor] = None):
+        sh = torch.tensor([self.rho, 2.0 * self.rho], dtype=torch.float64, device=self.device)
+        if out is None:
+            self.Minv = spd_inverse(self.A, sh)
+        else:
+            spd_inverse(self.A, sh, out=out, check_status=False)
+
+    def refresh(self):
+        """Recompute the Gram and cached inverses (the set-up of every solve)."""
+        with torch.cuda.stream(self.stream):
+            gram(self.X, self.y, out=(self.A, self.b, self.yy))
+            self._inverses(out=self.Minv)
+
+    def run(self, timeout_s: float = 20.0):
+        """Reset the state and solve; returns (iters, done, wall_ms). Collective in effect (every rank
+        must run it; the kernels hand off to each other)."""
+        import time
+
+        self.epoch = self.epoch % 4095 + 1
+        pa = native.PersistArgs()
+        pa.d, pa.n, pa.n_local, pa.start_iter, pa.max_iter = self.d, self.n, self.ext_hi - self.ext_lo + 1, 1, \
+            self.max_iter
+        pa.lag, pa.ring, pa.nvar, pa.obj_mode = self.LAG, self.ring, 2, 0
+        pa.deg_to_var[0], pa.deg_to_var[1], pa.deg_to_var[2] = 0, 0, 1
+        pa.pending_in, pa.has_monitor, pa.nranks, pa.sys_scope = 0, 1 if self.rank == 0 else 0, self.nranks, 1
+        pa.epoch = self.epoch
+        pa.rho, pa.obj0, pa.tol = self.rho, self.obj0, self.tol
+        pa.timeout_ticks = int(timeout_s * 1e8)
+        pa.slots, pa.pos = self.slots.data_ptr(), self.pos.data_ptr()
+        pa.Minv, pa.A, pa.b, pa.yy = self.Minv.data_ptr(), self.A.data_ptr(), self.b.data_ptr(), self.yy.data_ptr()
+        pa.theta, pa.mu = self.theta.data_ptr(), self.mu.data_ptr()
+        pa.objg, pa.decg = self.objg_mon, self.decg.ptr.value
+        pa.dec_push = self.dec_push_t.data_ptr()
+        pa.trace, pa.ctl = self.trace.data_ptr(), self.ctl.data_ptr()
+        pa.blk_k, pa.blk_len = self.k, self.L
+        pa.blk_tab = self.tab.ptr.value
+        pa.seg_lo, pa.seg_hi = self.seg_lo, self.seg_hi
+        pa.blk_npeer = len(self.peers)
+        for i, (lo, hi) in enumerate(self.peer_ranges):
+            pa.blk_peer_lo[i], pa.blk_peer_hi[i] = lo, hi
+        pa.blk_peer_tab = self.peer_tab_t.data_ptr()
+        with torch.cuda.stream(self.stream):
+            self.theta.zero_()
+            self.mu.zero_()
+            self.ctl.zero_()
+            t0 = time.perf_counter()
+            native.check(self.lib.gadmm_chain_blocked_launch(ctypes.byref(pa), self.stream.cuda_stream),
+                         "chain_blocked_launch")
+            self.stream.synchronize()
+            t1 = time.perf_counter()
+        c = self.ctl.cpu().tolist()
+        if c[1] == 4:
+            raise RuntimeError("blocked xgmi kernel timed out (hand-off never completed)")
+        return c[2], c[1], (t1 - t0) * 1e3
+
+    def exchange_bytes_per_solve(self, iters: int) -> int:
+        """Bytes this rank pushes over xGMI per solve: every k iterations, (theta, mu) of each owned
+        worker that a peer computes, to that peer."""
+        pushes = sum(1 for lo, hi in self.peer_ranges for p in range(self.seg_lo, self.seg_hi + 1) if lo <= p <= hi)
+        return pushes * 2 * self.d * 8 * (iters // self.k)
+
+    def objective_trace(self, upto: int):
+        return self.trace.cpu().numpy()[:upto]
+
+    def close(self):
+        for p in self.opened.values():
+            self.lib.gadmm_xgmi_close(p)
+        self.opened = {}
+        for b in (self.tab, self.objg, self.decg):
+            if b is not None:
+                b.free()
+        self.tab = self.objg = self.decg = None
