@@ -352,3 +352,19 @@ def test_blocked_xgmi_processes_one_gpu(world, lin24, lin_obj0):
     m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
     single = chain_admm(m, list(range(24)), 24, 3.0, lin_obj0, 1e-8, 3000)
     assert np.array_equal(np.asarray(res[0]["trace"]), single.obj)
+
+
+@pytest.mark.parametrize("name", ["LinearRegression_Synthetic", "LogisticRegression_Synthetic",
+                                  "Dynamic_LinearRegression_Synthetic", "LinearRegression_gadmm_vs_admm"])
+def test_entry_points_on_gpu(name, tmp_path):
+    """The reference entry scripts end to end on the MI355X (reduced budgets): native engines for
+    GADMM / D-GADMM and the persistent first-order engine for the baselines."""
+    from gadmm_amd import entry
+    argv = ["--quick", "--device", "cuda", "--out", str(tmp_path), "--no-plot"]
+    if name.startswith("Dynamic"):
+        argv += ["--set", "gadmm_iters=400", "coherences=1,10", "n_pregen_paths=60"]
+    out = entry.get(name).main(argv)
+    assert out["runs"], out
+    for k, r in out["runs"].items():
+        assert r["iters"] > 0, (k, r)
+    assert os.path.exists(out["summary_path"])
