@@ -24,24 +24,32 @@ namespace {
 constexpr int BK = 16;
 constexpr int PAD = 16;
 
-template <int BT>
+// NT threads = NT/64 waves arranged WR x 2; a wave owns a (BT/WR) x (BT/2) sub-tile of MFMA tiles.
+template <int BT, int NT>
 struct GramTile {
-  static constexpr int WT = BT / 2;        // wave tile edge
-  static constexpr int TM = WT / 16;       // MFMA tiles per wave edge
-  static constexpr int LDSROW = BT + PAD;  // doubles per LDS row
-  static constexpr int PER_THREAD = BK * BT / 256;
+  static constexpr int NWAVE = NT / 64;
+  static constexpr int WR = NWAVE / 2;      // wave rows
+  static constexpr int WTR = BT / WR;       // wave tile rows
+  static constexpr int WTC = BT / 2;        // wave tile cols
+  static constexpr int TMR = WTR / 16;      // MFMA tiles per wave (rows)
+  static constexpr int TMC = WTC / 16;      // MFMA tiles per wave (cols)
+  static constexpr int LDSROW = BT + PAD;   // doubles per LDS row
+  static constexpr int PER_THREAD = BK * BT / NT;
 };
 
-template <int BT, bool EVEN>
-__global__ void __launch_bounds__(256)
+template <int BT, int NT>
+__global__ void __launch_bounds__(NT)
 gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int m, int d,
                 int ntiles, int ksplit, long rows_per_split,
                 double* __restrict__ A, double* __restrict__ B, double* __restrict__ YY,
                 double* __restrict__ slab) {
-  using T = GramTile<BT>;
-  __shared__ __attribute__((aligned(16))) double lds[2 * BK * T::LDSROW];
-  double* Li = lds;
-  double* Lj = lds + BK * T::LDSROW;
+  using T = GramTile<BT, NT>;
+  // two LDS buffers (double buffering): slab s is read from buffer s&1 while slab s+1 is written
+  // into the other one, so each K step needs ONE LDS-only barrier and the staging stores issue
+  // behind the MFMAs instead of between two barriers
+  __shared__ __attribute__((aligned(16))) double lds[2][2 * BK * T::LDSROW];
+  double* Li = lds[0];
+  double* Lj = lds[0] + BK * T::LDSROW;
 
   const int nwg = gridDim.x;
   const int gid = xcd_remap(blockIdx.x, nwg);
@@ -65,27 +73,27 @@ gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int 
   if (kend > m) kend = m;
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
+  const int wr = wid >> 1, wc = wid & 1;  // T::WR x 2 waves
   const int D = d + 1;
 
-  f64x4 acc[T::TM][T::TM];
+  f64x4 acc[T::TMR][T::TMC];
 #pragma unroll
-  for (int a = 0; a < T::TM; ++a)
+  for (int a = 0; a < T::TMR; ++a)
 #pragma unroll
-    for (int b = 0; b < T::TM; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int b = 0; b < T::TMC; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
 
-  // staging: thread t loads slab element e = t + 256*p  (row = e / BT, col = e % BT).
-  // Interior tiles (every column < d, every row < kend, d even) take branch-free 16-byte loads;
+  // staging: thread t loads slab element pair e2 = t + NT*p  (row = e2 / (BT/2), col = 2 (e2 % (BT/2))).
+  // Interior tiles (every column < d, every row < kend) take branch-free 8-byte loads;
   // boundary tiles take branch-free clamped loads + selects. A per-element branch around each load
   // would make hipcc drain vmcnt(0) per element (cdna_hip_programming.md §5, trap (c)).
   double ri[T::PER_THREAD], rj[T::PER_THREAD];
   const bool cols_in = (row0 + BT <= d) && (diag || col0 + BT <= d);
   auto fetch = [&](long k0) {
     const bool interior = cols_in && (k0 + BK <= kend);
-    if (!EVEN && interior) {  // odd d: rows are not 16-B aligned -> branch-free 8-B loads
+    if (interior) {  // branch-free 8-B loads (measured faster than 16-B loads for every d: tools/gram_ab.py)
 #pragma unroll
       for (int p = 0; p < T::PER_THREAD / 2; ++p) {
-        const int e2 = tid + 256 * p;
+        const int e2 = tid + NT * p;
         const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
         const double* src = H + (k0 + r) * (long)d;
         ri[2 * p] = src[row0 + c];
@@ -95,24 +103,10 @@ gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int 
           rj[2 * p + 1] = src[col0 + c + 1];
         }
       }
-    } else if (EVEN && interior) {
-#pragma unroll
-      for (int p = 0; p < T::PER_THREAD / 2; ++p) {
-        const int e2 = tid + 256 * p;
-        const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
-        const double2 a = *reinterpret_cast<const double2*>(H + (k0 + r) * (long)d + row0 + c);
-        ri[2 * p] = a.x;
-        ri[2 * p + 1] = a.y;
-        if (!diag) {
-          const double2 b = *reinterpret_cast<const double2*>(H + (k0 + r) * (long)d + col0 + c);
-          rj[2 * p] = b.x;
-          rj[2 * p + 1] = b.y;
-        }
-      }
     } else {
 #pragma unroll
       for (int p = 0; p < T::PER_THREAD / 2; ++p) {
-        const int e2 = tid + 256 * p;
+        const int e2 = tid + NT * p;
         const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
         const long k = k0 + r;
         const long kk = k < kend ? k : (kend - 1);
@@ -131,49 +125,57 @@ gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int 
       }
     }
   };
-  auto stash = [&]() {
+  auto stash = [&](int buf) {
+    double* Si = lds[buf];
+    double* Sj = lds[buf] + BK * T::LDSROW;
 #pragma unroll
     for (int p = 0; p < T::PER_THREAD / 2; ++p) {
-      const int e2 = tid + 256 * p;
+      const int e2 = tid + NT * p;
       const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
-      *reinterpret_cast<double2*>(Li + r * T::LDSROW + c) = make_double2(ri[2 * p], ri[2 * p + 1]);
-      if (!diag) *reinterpret_cast<double2*>(Lj + r * T::LDSROW + c) = make_double2(rj[2 * p], rj[2 * p + 1]);
+      *reinterpret_cast<double2*>(Si + r * T::LDSROW + c) = make_double2(ri[2 * p], ri[2 * p + 1]);
+      if (!diag) *reinterpret_cast<double2*>(Sj + r * T::LDSROW + c) = make_double2(rj[2 * p], rj[2 * p + 1]);
     }
   };
 
-  const double* Lb = diag ? Li : Lj;
-  if (kbeg < kend) fetch(kbeg);
+  if (kbeg < kend) {
+    fetch(kbeg);
+    stash(0);
+  }
+  lds_barrier();
+  int cur = 0;
   for (long k0 = kbeg; k0 < kend; k0 += BK) {
-    __syncthreads();  // previous slab fully consumed
-    stash();
-    __syncthreads();
-    if (k0 + BK < kend) fetch(k0 + BK);  // prefetch next slab into registers (overlaps MFMAs)
+    const bool more = k0 + BK < kend;
+    if (more) fetch(k0 + BK);  // next slab into registers (lands during this slab's MFMAs)
+    const double* Ci = lds[cur];
+    const double* Cb = diag ? Ci : lds[cur] + BK * T::LDSROW;
 #pragma unroll
     for (int ks = 0; ks < BK / 4; ++ks) {
       const int kr = ks * 4 + (lane >> 4);
-      double a[T::TM], b[T::TM];
+      double a[T::TMR], b[T::TMC];
 #pragma unroll
-      for (int t = 0; t < T::TM; ++t) {
-        a[t] = Li[kr * T::LDSROW + wr * T::WT + t * 16 + (lane & 15)];
-        b[t] = Lb[kr * T::LDSROW + wc * T::WT + t * 16 + (lane & 15)];
-      }
+      for (int t = 0; t < T::TMR; ++t) a[t] = Ci[kr * T::LDSROW + wr * T::WTR + t * 16 + (lane & 15)];
 #pragma unroll
-      for (int x = 0; x < T::TM; ++x)
+      for (int t = 0; t < T::TMC; ++t) b[t] = Cb[kr * T::LDSROW + wc * T::WTC + t * 16 + (lane & 15)];
 #pragma unroll
-        for (int yq = 0; yq < T::TM; ++yq)
+      for (int x = 0; x < T::TMR; ++x)
+#pragma unroll
+        for (int yq = 0; yq < T::TMC; ++yq)
           acc[x][yq] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[x], b[yq], acc[x][yq], 0, 0, 0);
     }
+    if (more) stash(cur ^ 1);  // the other buffer: nobody reads it during this slab
+    lds_barrier();             // slab s+1 visible, and every wave is done reading slab s
+    cur ^= 1;
   }
 
   // epilogue
 #pragma unroll
-  for (int x = 0; x < T::TM; ++x)
+  for (int x = 0; x < T::TMR; ++x)
 #pragma unroll
-    for (int yq = 0; yq < T::TM; ++yq)
+    for (int yq = 0; yq < T::TMC; ++yq)
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) {
-        const int lr = wr * T::WT + x * 16 + (lane >> 4) + 4 * reg;  // row within tile
-        const int lc = wc * T::WT + yq * 16 + (lane & 15);          // col within tile
+        const int lr = wr * T::WTR + x * 16 + (lane >> 4) + 4 * reg;  // row within tile
+        const int lc = wc * T::WTC + yq * 16 + (lane & 15);          // col within tile
         const double v = acc[x][yq][reg];
         if (ksplit > 1) {
           slab[(((long)n * ntiles + tile) * ksplit + split) * (BT * BT) + lr * BT + lc] = v;
@@ -235,13 +237,14 @@ int launch_gram(const double* X, const double* Y, int N, int m, int d, int kspli
   ksplit = (int)(((long)m + rows - 1) / rows);
   if (ksplit < 1) ksplit = 1;
   const long nwg = (long)ntiles * ksplit * N;
-  static const bool novec = getenv("GADMM_GRAM_NOVEC") != nullptr;  // A/B switch (tools/gram_bench.py)
-  if ((d & 1) == 0 && !novec)
-    hipLaunchKernelGGL((gram_aug_kernel<BT, true>), dim3((unsigned)nwg), dim3(256), 0, st, X, Y, m, d, ntiles,
-                       ksplit, rows, A, B, YY, slab);
+  static const int nt_env = getenv("GADMM_GRAM_NT") ? atoi(getenv("GADMM_GRAM_NT")) : 0;  // A/B switch
+  const int nthr = nt_env == 256 || nt_env == 512 ? nt_env : (BT == 128 ? 512 : 256);
+  if (nthr == 512)
+    hipLaunchKernelGGL((gram_aug_kernel<BT, 512>), dim3((unsigned)nwg), dim3(512), 0, st, X, Y, m, d, ntiles, ksplit,
+                       rows, A, B, YY, slab);
   else
-    hipLaunchKernelGGL((gram_aug_kernel<BT, false>), dim3((unsigned)nwg), dim3(256), 0, st, X, Y, m, d, ntiles,
-                       ksplit, rows, A, B, YY, slab);
+    hipLaunchKernelGGL((gram_aug_kernel<BT, 256>), dim3((unsigned)nwg), dim3(256), 0, st, X, Y, m, d, ntiles, ksplit,
+                       rows, A, B, YY, slab);
   if (ksplit > 1) {
     hipLaunchKernelGGL(gram_reduce_kernel<BT>, dim3(ntiles, N), dim3(256), 0, st, slab, d, ntiles,
                        ksplit, A, B, YY);
@@ -264,15 +267,39 @@ long gadmm_gram_workspace(int N, int m, int d, int ksplit) {
 
 // Heuristic split so that the grid covers the chip (>= ~2 workgroups per CU) for tall shards.
 int gadmm_gram_pick_ksplit(int N, int m, int d) {
+  // Split K so the grid fills whole "waves" of resident workgroups: with W workgroups and S
+  // resident slots the run takes ceil(W / S) rounds, efficiency W / (rounds * S). Pick the
+  // smallest split reaching 90 % (the split-K reduce pass is cheap next to the SYRK itself).
   const int BT = (d + 1 <= 64) ? 64 : 128;
   const int nt = (d + 1 + BT - 1) / BT;
   const long tiles = (long)N * (nt * (nt + 1) / 2);
-  long want = (512 + tiles - 1) / tiles;
-  long maxk = (m + 255) / 256;  // keep >= 256 rows per split
-  if (want > maxk) want = maxk;
-  if (want < 1) want = 1;
-  if (want > 1024) want = 1024;
-  return (int)want;
+  static int cus = 0;
+  if (cus == 0) {
+    hipDeviceProp_t prop;
+    int dev = 0;
+    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
+              ? prop.multiProcessorCount : 256;
+  }
+  const long slots = (long)cus * 2;  // 2 resident workgroups per CU (LDS / VGPR bound)
+  long maxk = (m + 255) / 256;       // keep >= 256 rows per split
+  if (maxk > 64) maxk = 64;
+  if (maxk < 1) maxk = 1;
+  long best = 1;
+  double best_eff = 0.0;
+  for (long k = 1; k <= maxk; ++k) {
+    const long W = tiles * k;
+    const long rounds = (W + slots - 1) / slots;
+    const double eff = (double)W / (double)(rounds * slots);
+    if (eff > best_eff + 1e-9) {
+      best_eff = eff;
+      best = k;
+    }
+    if (eff >= 0.9 && W >= slots) {
+      best = k;
+      break;
+    }
+  }
+  return (int)best;
 }
 
 int gadmm_gram_f64(const double* X, const double* Y, int N, int m, int d, int ksplit, double* A,

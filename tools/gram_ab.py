@@ -1,4 +1,6 @@
-"""A/B of the two Gram staging paths in ONE process (interleaved rounds; cdna_hip_programming.md §5.4 rule 24)."""
+"""A/B of Gram kernel variants (env-selected) in interleaved child processes on one GPU.
+
+    python tools/gram_ab.py [M D]"""
 import os, sys, time, subprocess, json
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 if len(sys.argv) > 1 and sys.argv[1] == "child":
@@ -24,9 +26,10 @@ if len(sys.argv) > 1 and sys.argv[1] == "child":
         out["rocblas_dgemm_syrk_equiv_tflops"] = fl / min(tl) / 1e12
     print(json.dumps(out))
     sys.exit(0)
-M, D = 262144, 8192
+M = int(sys.argv[1]) if len(sys.argv) > 1 else 262144
+D = int(sys.argv[2]) if len(sys.argv) > 2 else 8192
 for rnd in range(2):
-    for name, env in (("vec16", {"GRAM_AB_LIB": "1"} if rnd == 0 else {}), ("scalar8", {"GADMM_GRAM_NOVEC": "1"})):
+    for name, env in (("nt256", {"GADMM_GRAM_NT": "256"}), ("nt512", {"GADMM_GRAM_NT": "512"})):
         out = subprocess.run([sys.executable, __file__, "child", str(M), str(D)], capture_output=True, text=True,
                              env=dict(os.environ, **env))
         line = [l for l in out.stdout.splitlines() if l.startswith("{")]
