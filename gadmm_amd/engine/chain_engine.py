@@ -151,6 +151,8 @@ class NativeChainEngine:
         rho = self.rho
         if self.n_total == 1:
             shifts, self.deg_to_var = [0.0], (0, 0, 0)
+        elif self.n_total == 2:  # both workers are chain ends in every chain: degree 1 only
+            shifts, self.deg_to_var = [rho], (0, 0, 0)
         else:
             shifts, self.deg_to_var = [rho, 2.0 * rho], (0, 0, 1)
         self.nvar = len(shifts)

@@ -14,6 +14,15 @@ import torch
 from ..ops.linalg import gram, spd_inverse
 
 
+def _spd_solve(M: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
+    """Solve the SPD normal equations by Cholesky (half the flops of LU, no pivoting); LU only if
+    the factorisation reports the matrix is not positive definite."""
+    L, info = torch.linalg.cholesky_ex(M)
+    if int(info.item()) != 0:
+        return torch.linalg.solve(M, r)
+    return torch.cholesky_solve(r.unsqueeze(-1), L).squeeze(-1)
+
+
 class LinearRegression:
     kind = "linear"
 
@@ -112,7 +121,7 @@ class LinearRegression:
             yy = buf[-1]
         eye = torch.eye(self.d, dtype=As.dtype, device=As.device)
         lam_tot = self.lam * (n_total if n_total is not None else self.n_local)
-        x = torch.linalg.solve(As + lam_tot * eye, bs)
+        x = _spd_solve(As + lam_tot * eye, bs)
         return float(0.5 * x @ (As @ x) - bs @ x + 0.5 * yy + 0.5 * lam_tot * (x @ x))
 
     def optimum_point(self, comm=None) -> torch.Tensor:
@@ -122,4 +131,4 @@ class LinearRegression:
             comm.allreduce_sum(buf)
             As = buf[: self.d * self.d].reshape(self.d, self.d)
             bs = buf[self.d * self.d:]
-        return torch.linalg.solve(As, bs)
+        return _spd_solve(As, bs)
