@@ -45,13 +45,18 @@ def chain_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: 
                local_solver: Optional[str] = None, step: float = 1.0, max_inner: int = 100,
                inner_tol: float = 1e-4, cost_quirk: bool = True, backend: str = "auto",
                name: str = "GADMM", record_theta: bool = False, engine_opts: Optional[dict] = None,
-               state=None, check_exchange: Optional[bool] = None) -> RunResult:
+               state=None, check_exchange: Optional[bool] = None,
+               failures: Optional[dict] = None) -> RunResult:
     """Run one chain-ADMM solve on this rank. ``model`` holds this rank's shards (local order =
     ``local_ids``). ``schedule`` (D-GADMM) overrides ``path``; ``cost_quirk`` reproduces the
     reference's per-head-worker accumulation of ``sum(pathCost)`` (dynamic_group_ADMM_closedForm.m:51-55).
     ``state``: optional ``(theta_table, mu, start_iter)`` to resume from a checkpoint.
     ``check_exchange`` (or ``GADMM_CHECK_EXCHANGE=1``): verify every ghost row against its owner after
-    every exchange (debug/race.py; forces the torch path)."""
+    every exchange (debug/race.py; forces the torch path).
+    ``failures``: ``{iteration: [worker ids]}`` - elastic recovery: at that iteration
+    the workers drop out, the chain re-forms over the survivors, each failed worker's aggregated
+    dual is handed to a surviving chain neighbour (keeping sum(mu) = 0, the consensus-dual
+    invariant) and the stopping target becomes the survivors' optimum (linear, torch path)."""
     import os
 
     comm = comm if comm is not None else LocalComm()
@@ -66,7 +71,7 @@ def chain_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: 
     dev = model.device
     use_native = False
     if backend in ("auto", "native") and dev.type == "cuda" and local_solver in ("closed", "gd") and state is None \
-            and not check_exchange:
+            and not check_exchange and not failures:
         from ..ops import native
 
         if native.available() and (comm.nranks == 1 or getattr(comm, "backend", "") == "rccl"):
@@ -78,12 +83,12 @@ def chain_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: 
                                   local_solver, step, max_inner, inner_tol, cost_quirk, name, engine_opts or {})
     return _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, schedule,
                              local_solver, step, max_inner, inner_tol, cost_quirk, name, record_theta, state,
-                             check_exchange)
+                             check_exchange, failures)
 
 
 def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, schedule,
                       local_solver, step, max_inner, inner_tol, cost_quirk, name, record_theta, state,
-                      check_exchange=False):
+                      check_exchange=False, failures=None):
     rank = comm.rank
     checker = None
     if check_exchange:
@@ -104,6 +109,11 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
         start = 1
     stop = Stopper(obj0, tol, max_iter)
     snap = comm.stats.snapshot()
+    alive = np.ones(n_total, dtype=bool)
+    failures = {int(k): [int(w) for w in v] for k, v in (failures or {}).items()}
+    if failures and model.kind != "linear":
+        raise NotImplementedError("elastic failures: linear models (the survivors' optimum is closed form)")
+    lidx_of = {w: i for i, w in enumerate(local_ids)}
     plan = chain_plan(schedule.path, placement, rank)
     cc = 0.0
     com_cost: List[float] = []
@@ -111,8 +121,13 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
     iters = max_iter
     converged = False
     for it in range(start, max_iter + 1):
+        if it in failures:
+            obj0 = _drop_workers(failures[it], alive, schedule, theta, mu, lidx_of, model, comm, n_total, dev)
+            stop.obj0 = obj0
+            plan = chain_plan([w for w in schedule.path if alive[w]], placement, rank)
+            comm.exchange_rows(theta, plan.xchg_tail)  # new cross-rank neighbours
         if schedule.step(it):
-            plan = chain_plan(schedule.path, placement, rank)
+            plan = chain_plan([w for w in schedule.path if alive[w]], placement, rank)
             # new cross-rank neighbours: heads need their (new) tails' current theta first
             comm.exchange_rows(theta, plan.xchg_tail)
             if checker is not None:
@@ -162,6 +177,8 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
             mu[li] = m
         th_loc = theta.index_select(0, torch.tensor(local_ids, dtype=torch.long, device=dev))
         f = model.objective(th_loc)
+        if not alive.all():
+            f = f * torch.as_tensor(alive[local_ids], dtype=f.dtype, device=dev)
         if stop.record(global_objective(comm, f, local_ids, n_total)):
             iters = it
             converged = True
@@ -300,6 +317,48 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
                            "solver": local_solver, "monitor_bytes": int(mon)})
     res.extra["engine_obj"] = eng
     return res
+
+
+def _drop_workers(dead, alive, schedule, theta, mu, lidx_of, model, comm, n_total, dev) -> float:
+    """Remove ``dead`` workers (elastic recovery): hand each one's aggregated dual to its nearest
+    surviving neighbour on the current chain (sum(mu) = 0 is the dual-feasibility invariant of the
+    consensus problem; ADMM's dual steps preserve it, a lost dual would break it), mark it dead, and
+    return the survivors' optimal objective. Collective: every rank calls it with the same list."""
+    d = theta.shape[1]
+    path = [w for w in schedule.path if alive[w]]
+    lost = torch.zeros((n_total, d), dtype=torch.float64, device=dev)
+    for w in dead:
+        if w in lidx_of:
+            lost[w] = mu[lidx_of[w]]
+    if comm.nranks > 1:
+        comm.allreduce_sum(lost)
+    for w in dead:
+        if not alive[w]:
+            continue
+        pos = path.index(w)
+        heir = None
+        for q in list(range(pos - 1, -1, -1)) + list(range(pos + 1, len(path))):  # nearest survivor, left first
+            if alive[path[q]] and path[q] not in dead:
+                heir = path[q]
+                break
+        if heir is not None and heir in lidx_of:
+            mu[lidx_of[heir]] += lost[w]
+        if w in lidx_of:
+            mu[lidx_of[w]].zero_()
+    for w in dead:
+        alive[w] = False
+    # the survivors' optimum: all-reduced Gram of the alive workers (one-time, like SURVEY.md C10)
+    keep = torch.as_tensor([alive[w] for w in lidx_of], dtype=torch.float64, device=dev)
+    As = (model.A * keep.view(-1, 1, 1)).sum(0)
+    bs = (model.b * keep.view(-1, 1)).sum(0)
+    yy = (model.yy * keep).sum()
+    buf = torch.cat([As.reshape(-1), bs, yy.reshape(1)]).contiguous()
+    if comm.nranks > 1:
+        comm.allreduce_sum(buf)
+    As, bs, yy = buf[: d * d].reshape(d, d), buf[d * d: d * d + d], buf[-1]
+    lam_tot = model.lam * int(alive.sum())
+    x = torch.linalg.solve(As + lam_tot * torch.eye(d, dtype=torch.float64, device=dev), bs)
+    return float(0.5 * x @ (As @ x) - bs @ x + 0.5 * yy + 0.5 * lam_tot * (x @ x))
 
 
 def _is_rechain(it: int, coherence) -> bool:
