@@ -20,7 +20,9 @@ class RunResult:
       LinearRegression_Synthetic.m:100-142);
     * ``com_cost``: cumulative energy/distance cost where the reference tracks one (D-GADMM, E7);
     * ``wall_s``/``time_trace``: real wall clock (cumulative per iteration);
-    * ``bytes_sent``: actual bytes this rank put on the fabric; ``bytes_total`` summed over ranks.
+    * ``bytes_sent``: actual bytes this rank put on the fabric; ``bytes_total`` summed over ranks;
+    * ``primal_res``: per-iteration consensus violation sum over chain edges ||th_n - th_right||^2
+      (kernel K4's residual; chain algorithms).
     """
 
     algorithm: str
@@ -36,6 +38,7 @@ class RunResult:
     bytes_total: int = 0
     extra: Dict[str, Any] = field(default_factory=dict)
     theta: Optional[np.ndarray] = None
+    primal_res: Optional[np.ndarray] = None
 
     def summary(self) -> Dict[str, Any]:
         return {
@@ -102,6 +105,24 @@ def total_bytes(comm, snap=None) -> int:
 
         dist.all_reduce(t, group=getattr(comm, "control_group", None))
     return int(t.item())
+
+
+def global_objective_and_residual(comm, f_local, r_local, local_ids, n_total: int):
+    """``global_objective`` plus the summed primal residual in the same all-reduce (2N entries,
+    one contributor each, summed in worker order)."""
+    import torch
+
+    full = torch.zeros((2, n_total), dtype=torch.float64, device=f_local.device)
+    ids = torch.as_tensor(list(local_ids), dtype=torch.long, device=f_local.device)
+    full[0, ids] = f_local
+    full[1, ids] = r_local
+    if comm is not None and comm.nranks > 1:
+        comm.allreduce_sum(full)
+        nb = full.numel() * full.element_size()
+        comm.stats.coll_bytes -= nb
+        comm.stats.monitor_bytes += nb
+    s = full.sum(-1)
+    return float(s[0].item()), float(s[1].item())
 
 
 def global_objective(comm, f_local, local_ids, n_total: int) -> float:

@@ -29,7 +29,7 @@ import torch
 
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.topology import rechain_iterations, PathSchedule, Placement, chain_plan
-from .base import RunResult, Stopper, total_bytes, global_objective, run_bytes
+from .base import global_objective_and_residual, RunResult, Stopper, total_bytes, global_objective, run_bytes
 
 
 def _gather_rows(theta: torch.Tensor, ids: List[int]) -> torch.Tensor:
@@ -118,6 +118,7 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
     cc = 0.0
     com_cost: List[float] = []
     inner_used: List[float] = []
+    primal: List[float] = []
     iters = max_iter
     converged = False
     for it in range(start, max_iter + 1):
@@ -179,7 +180,15 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
         f = model.objective(th_loc)
         if not alive.all():
             f = f * torch.as_tensor(alive[local_ids], dtype=f.dtype, device=dev)
-        if stop.record(global_objective(comm, f, local_ids, n_total)):
+        # consensus residual of the edges this rank's workers start (edge n -> right neighbour)
+        res_loc = torch.zeros(len(local_ids), dtype=torch.float64, device=dev)
+        for s_ in plan.head + plan.tail:
+            if s_.right >= 0:
+                dlt = theta[s_.gid] - theta[s_.right]
+                res_loc[s_.li] = dlt @ dlt
+        f_all, r_all = global_objective_and_residual(comm, f, res_loc, local_ids, n_total)
+        primal.append(r_all)
+        if stop.record(f_all):
             iters = it
             converged = True
             break
@@ -192,7 +201,8 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
                     bytes_total=total_bytes(comm, snap),
                     extra={"backend": "torch", "rank": rank, "nranks": comm.nranks, "solver": local_solver,
                            "inner_steps_mean": float(np.mean(inner_used)) if inner_used else 0.0,
-                           "monitor_bytes": int(comm.stats.delta(snap)["monitor_bytes"])})
+                           "monitor_bytes": int(comm.stats.delta(snap)["monitor_bytes"])},
+                    primal_res=np.asarray(primal))
     res.extra["state"] = (theta, mu, (iters if converged else start - 1 + n_it) + 1)
     if record_theta:
         res.theta = theta.cpu().numpy()

@@ -49,6 +49,9 @@ class RunWriter:
                 row["wall_s"] = float(result.time_trace[i])
             if result.com_cost is not None and len(result.com_cost) > i:
                 row["com_cost"] = float(result.com_cost[i])
+            pr = getattr(result, "primal_res", None)
+            if pr is not None and len(pr) > i:
+                row["primal_res"] = float(pr[i])
             rows.append(row)
         base = os.path.join(self.outdir, _safe(key))
         with open(base + ".jsonl", "w") as f:
