@@ -326,6 +326,12 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
                     extra={"backend": "native", "engine": engine_kind, "rank": rank, "nranks": comm.nranks,
                            "solver": local_solver, "monitor_bytes": int(mon)})
     res.extra["engine_obj"] = eng
+    if opts.get("state", True):
+        # resumable state for checkpoints: apply the heads' pending (lazy) duals with the current
+        # chain, so (theta, mu) is the reference state after iteration next-1
+        eng.flush_duals()
+        nxt = int(eng.ctl_state()["iter"])
+        res.extra["state"] = (eng.theta.clone(), eng.mu.clone(), nxt)
     return res
 
 
