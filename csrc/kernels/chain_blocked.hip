@@ -65,7 +65,7 @@ __device__ __forceinline__ double lds_gemv_cols(const double* A, int d, const do
 template <int DB, bool SYS>
 __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  __shared__ int abort_lds, stop_lds;
+  __shared__ int abort_lds, stop_lds, stop_iter_lds;
   const int d = a.d, n = a.n;
   const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
   const int k = a.blk_k, L = a.blk_len, H = 2 * a.blk_k;
@@ -181,6 +181,14 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   const int deg = (int)has_l + (int)has_r;
   const double rho = a.rho;
   const bool in = lane < d;
+  // Decision wave: polls the stop decision during the tail phase, when heads are idle. A halo head
+  // is preferred: it never stores to global memory, so its decision load does not queue behind
+  // write-through granule stores (vmcnt counts stores on gfx9).
+  int vdec = -1;
+  for (int u = 0; u < nv && vdec < 0; ++u)
+    if (((ra + u) % 2) == 0 && (ra + u < s0 || ra + u > e0)) vdec = u;
+  if (vdec < 0) vdec = (ra % 2 == 0 || nv < 2) ? 0 : 1;
+  const bool dec_wave = v == vdec;
 
   double* thS = lds;                       // [MAXW][64] theta of every computed worker
   double* xs = thS + MAXW * 64;            // [MAXW][64] per-wave rhs / broadcast staging
@@ -197,35 +205,40 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   double th = (active && in) ? a.theta[(long)w * d + lane] : 0.0;
   double mu = (active && in) ? a.mu[(long)li * d + lane] : 0.0;
   const double bb = (active && in) ? a.b[(long)li * d + lane] : 0.0;
-  const double half_yy = active ? 0.5 * a.yy[li] : 0.0;
   thS[v * 64 + lane] = th;
   myx[lane] = 0.0;
   int pending = a.pending_in;
-  int stop_code = 0, stop_iter = 0;
-  unsigned long long dv_next = 0;
+  if (threadIdx.x == 0) stop_iter_lds = 0;
   lds_barrier();
 
+  // a stop decision for iteration j arrives before iteration j + lag runs: polled during the tail
+  // phase of iteration j + lag - 1 and published by that phase's closing barrier
+  // owned (theta, mu) after iteration j, for the exchange at the start of iteration j + 1: into
+  // this GPU's table and into every peer GPU that computes position p too
+  auto publish = [&](int j) {
+    const unsigned tag = make_tag(a.epoch, j + 1);
+    const int base = (((((j + 1 - a.start_iter) / k) & 1) * n + p) * 2) * d;
+    store_granule<SYS>(rtab, (base + lane) * 16, tag, th);
+    store_granule<SYS>(rtab, (base + d + lane) * 16, tag, mu);
+    for (int q = 0; q < a.blk_npeer; ++q)
+      if (p >= a.blk_peer_lo[q] && p <= a.blk_peer_hi[q]) {
+        const __amdgpu_buffer_rsrc_t rpe = rsrc_of(a.blk_peer_tab[q]);
+        store_granule<SYS>(rpe, (base + lane) * 16, tag, th);
+        store_granule<SYS>(rpe, (base + d + lane) * 16, tag, mu);
+      }
+  };
   int it = a.start_iter;
   long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (;; ++it) {
     if (it > a.max_iter + a.lag) break;
     const bool stamp = a.timeline && threadIdx.x == 0 && it - a.start_iter < a.timeline_iters;
     if (stamp) ts[0] = (long long)now_ticks();
-    // ---- halo exchange every k iterations (state after iteration it - 1)
+    // ---- halo exchange every k iterations (state after iteration it - 1); the owned workers
+    // published theirs during the tail phase of it - 1 (publish() below)
     if (it > a.start_iter && (it - a.start_iter) % k == 0) {
-      const unsigned tag = make_tag(a.epoch, it);
-      const int slot = ((it - a.start_iter) / k) & 1;
-      const int base = ((slot * n + p) * 2) * d;
-      if (owned && in) {
-        store_granule<SYS>(rtab, (base + lane) * 16, tag, th);
-        store_granule<SYS>(rtab, (base + d + lane) * 16, tag, mu);
-        for (int q = 0; q < a.blk_npeer; ++q)
-          if (p >= a.blk_peer_lo[q] && p <= a.blk_peer_hi[q]) {  // a peer GPU computes this position too
-            const __amdgpu_buffer_rsrc_t rpe = rsrc_of(a.blk_peer_tab[q]);
-            store_granule<SYS>(rpe, (base + lane) * 16, tag, th);
-            store_granule<SYS>(rpe, (base + d + lane) * 16, tag, mu);
-          }
-      } else if (active) {
+      if (active && !owned) {
+        const unsigned tag = make_tag(a.epoch, it);
+        const int base = (((((it - a.start_iter) / k) & 1) * n + p) * 2) * d;
         double t0 = 0.0, t1 = 0.0;
         bool ok = true;
         for (int spin = 0;; ++spin) {
@@ -246,36 +259,12 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         mu = in ? t1 : 0.0;
         thS[v * 64 + lane] = th;
       }
+      lds_barrier();  // refreshed halo theta visible to the neighbouring waves
+      if (abort_lds) break;
     }
-    if (stamp) ts[1] = (long long)now_ticks();
-    // ---- stop rule: decision of it - lag (loaded one iteration ahead; normally already there)
-    if (threadIdx.x == 0 && it - a.start_iter >= a.lag) {
-      const int jdec = it - a.lag;
-      const unsigned tj = make_tag(a.epoch, jdec);
-      unsigned long long dv = dv_next;
-      for (int spin = 0; (unsigned)(dv >> 32) != tj; ++spin) {
-        if ((spin & 7) == 7 && now_ticks() > deadline) {
-          abort_lds = 1;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        dv = load_dec<SYS>(&a.decg[jdec % a.ring]);
-      }
-      const unsigned code = (unsigned)(dv & 0xffffffffu);
-      if (code && !abort_lds) {
-        stop_lds = 1;
-        stop_code = (int)code;
-        stop_iter = jdec;
-      }
-    }
-    if (threadIdx.x == 0 && it + 1 - a.start_iter >= a.lag)
-      dv_next = load_dec<SYS>(&a.decg[(it + 1 - a.lag) % a.ring]);
-    if (stamp) ts[2] = (long long)now_ticks();
-    lds_barrier();
-    if (abort_lds || stop_lds) break;
-    if (stamp) ts[3] = (long long)now_ticks();
+    if (stamp) ts[1] = ts[2] = ts[3] = (long long)now_ticks();
 
-    // ---- head phase (owned tails meanwhile report f(theta^{it-1}))
+    // ---- head phase
     if (active && head) {
       const double tl = nbl ? thL[lane] : 0.0, tr = nbr ? thR[lane] : 0.0;
       double m = mu;
@@ -287,8 +276,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       double r = bb - m;
       if (has_l) r = r + rho * tl;
       if (has_r) r = r + rho * tr;
-      myx[lane] = in ? r : 0.0;
       if (stamp) ts[6] = (long long)now_ticks();
+      myx[lane] = in ? r : 0.0;
       th = in ? reg_gemv(Mr, myx) : 0.0;
       if (stamp) {
         asm volatile("" ::"v"(th));
@@ -303,7 +292,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     lds_barrier();
     if (stamp) ts[4] = (long long)now_ticks();
 
-    // ---- tail phase (owned heads meanwhile report f(theta^it))
+    // ---- tail phase; the (idle head) decision wave fetches decision[it + 1 - lag]
+    const bool xnext = (it + 1 - a.start_iter) % k == 0;  // the next iteration starts with an exchange
     if (active && !head) {
       const double tl = nbl ? thL[lane] : 0.0, tr = nbr ? thR[lane] : 0.0;
       double r = bb - mu;
@@ -317,9 +307,31 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       mu = m;
       th = tn;
       thS[v * 64 + lane] = th;
-      if (owned && in)
+      if (owned && in) {
         store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
                              make_tag(a.epoch, it), th);
+        if (xnext) publish(it);
+      }
+    } else if (active && owned && xnext) {  // heads: theta^it and the (still pending) mu are final
+      if (in) publish(it);
+    }
+    if (dec_wave && !(active && !head) && lane == 0 && it + 1 - a.start_iter >= a.lag) {
+      const int jdec = it + 1 - a.lag;
+      const unsigned tj = make_tag(a.epoch, jdec);
+      unsigned long long dv = load_dec<SYS>(&a.decg[jdec % a.ring]);
+      for (int spin = 0; (unsigned)(dv >> 32) != tj; ++spin) {
+        if ((spin & 7) == 7 && now_ticks() > deadline) {
+          abort_lds = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        dv = load_dec<SYS>(&a.decg[jdec % a.ring]);
+      }
+      const unsigned code = (unsigned)(dv & 0xffffffffu);
+      if (code && (unsigned)(dv >> 32) == tj) {
+        stop_lds = (int)code;
+        stop_iter_lds = jdec;
+      }
     }
     lds_barrier();
     if (stamp) {
@@ -328,6 +340,10 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       tl[5] = (long long)now_ticks();
       tl[6] = ts[6];
       tl[7] = ts[7];
+    }
+    if (abort_lds || stop_lds) {
+      ++it;  // the next iteration to run
+      break;
     }
   }
 
@@ -338,12 +354,12 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   if (threadIdx.x == 0) {
     if (abort_lds) {
       a.ctl->done = 4;
-    } else if (g == 0 && stop_code) {
-      a.ctl->done = stop_code;
-      a.ctl->conv_iter = stop_iter;
+    } else if (g == 0 && stop_lds) {
+      a.ctl->done = stop_lds;
+      a.ctl->conv_iter = stop_iter_lds;
       a.ctl->iter = it;
       a.ctl->pending = 1;
-      a.ctl->monitored = stop_iter;
+      a.ctl->monitored = stop_iter_lds;
     }
   }
 }
