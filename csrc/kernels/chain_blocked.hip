@@ -62,12 +62,14 @@ __device__ __forceinline__ double lds_gemv_cols(const double* A, int d, const do
 // chain positions [seg_lo, seg_hi] and pushes owned (theta, mu) into its peers' exchange tables.
 // Block layout: [0, W) worker workgroups, [W, W + Wo) objective workgroups, W + Wo the monitor
 // (rank 0 only).
-template <int DB, bool SYS>
+template <int DB, bool SYS, bool QUAD>
 __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a) {
+  constexpr int QT = DB / 4;  // quad layout: columns per lane
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int abort_lds, stop_lds, stop_iter_lds;
   const int d = a.d, n = a.n;
-  const int lane = threadIdx.x & 63, v = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int v = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: per-wave state in SGPRs
   const int k = a.blk_k, L = a.blk_len, H = 2 * a.blk_k;
   const bool multi = a.nranks > 1;
   const int seg_lo = multi ? a.seg_lo : 0, seg_hi = multi ? a.seg_hi : n - 1;
@@ -132,14 +134,18 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     if (q > seg_hi) return;
     const PhaseSlot so = a.slots[q];
     const bool in = lane < d;
-    double Ar[DB];
+    double Ar[QUAD ? 1 : DB], Aq[QUAD ? 4 : 1][QUAD ? QT : 1];
     const double* Ag = a.A + (long)so.li * d * d;
+    if constexpr (QUAD) {
+      quad_load<QT>(Aq, Ag, d, true);
+    } else {
 #pragma unroll
-    for (int j = 0; j < DB; ++j) Ar[j] = (in && j < d) ? Ag[lane * d + j] : 0.0;
+      for (int j = 0; j < DB; ++j) Ar[j] = (in && j < d) ? Ag[lane * d + j] : 0.0;
+    }
     const double bo = in ? a.b[(long)so.li * d + lane] : 0.0;
     const double hy = 0.5 * a.yy[so.li];
-    double* xo = lds + v * 64;
-    xo[lane] = 0.0;
+    double* xo = lds + v * (QUAD ? QSTAGE : 64);
+    if constexpr (!QUAD) xo[lane] = 0.0;
     for (int it = a.start_iter;; ++it) {
       const unsigned tag = make_tag(a.epoch, it);
       const long off = (ring_base + ((long)(it % a.ring) * n + q) * d + lane) * 16;
@@ -158,8 +164,13 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      xo[lane] = in ? x : 0.0;
-      const double qv = reg_gemv(Ar, xo);  // (A th)_i in the order of every other engine
+      double qv;  // (A th)_i in the order of every other engine
+      if constexpr (QUAD) {
+        qv = quad_gemv<QT>(Aq, in ? x : 0.0, xo);
+      } else {
+        xo[lane] = in ? x : 0.0;
+        qv = reg_gemv(Ar, xo);
+      }
       const double part = in ? (0.5 * qv - bo) * x : 0.0;
       const double f = wave_sum_f64(part) + hy;
       if (lane == 0) store_granule<SYS>(rob, ((it % a.ring) * n + so.gid) * 16, tag, f);
@@ -171,8 +182,14 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   const int s0 = seg_lo + g * L, e0 = min(seg_hi + 1, s0 + L) - 1;  // owned chain positions [s0, e0]
   const int ra = max(0, s0 - H), rb = min(n - 1, e0 + H);
   const int nv = rb - ra + 1;
-  const int p = ra + v;  // this wave's chain position
-  const bool active = v < nv;
+  // Wave v computes local position u. Waves are dealt to the 4 SIMDs round-robin (v mod 4), so
+  // v < MAXW/2 take the heads and the rest the tails: each phase keeps every SIMD busy with
+  // MAXW/8 GEMV waves instead of piling a phase's 6 GEMVs onto two SIMDs (identity map: heads
+  // are every other wave -> SIMDs 0 and 2 only).
+  const int h0 = ra & 1;  // parity offset: position ra + u is a head iff u has parity h0
+  const int u = v < MAXW / 2 ? 2 * v + h0 : 2 * (v - MAXW / 2) + (1 - h0);
+  const int p = ra + u;  // this wave's chain position
+  const bool active = u < nv;
   const bool owned = active && p >= s0 && p <= e0;
   const PhaseSlot sl = a.slots[active ? p : 0];  // slots are sorted by chain position
   const int li = sl.li, w = sl.gid;
@@ -188,25 +205,39 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   for (int u = 0; u < nv && vdec < 0; ++u)
     if (((ra + u) % 2) == 0 && (ra + u < s0 || ra + u > e0)) vdec = u;
   if (vdec < 0) vdec = (ra % 2 == 0 || nv < 2) ? 0 : 1;
-  const bool dec_wave = v == vdec;
+  const bool dec_wave = u == vdec;
 
   double* thS = lds;                       // [MAXW][64] theta of every computed worker
-  double* xs = thS + MAXW * 64;            // [MAXW][64] per-wave rhs / broadcast staging
-  double* myx = xs + v * 64;
+  double* xs = thS + MAXW * 64;            // [MAXW][64 | QSTAGE] per-wave rhs / broadcast staging
+  double* myx = xs + v * (QUAD ? QSTAGE : 64);
   // the wave's neighbours inside the computed range (outside it the halo worker is already stale)
-  const double* thL = thS + (v > 0 ? v - 1 : v) * 64;
-  const double* thR = thS + (v + 1 < nv ? v + 1 : v) * 64;
-  const bool nbl = has_l && v > 0, nbr = has_r && v + 1 < nv;
+  const double* thL = thS + (u > 0 ? u - 1 : u) * 64;
+  const double* thR = thS + (u + 1 < nv ? u + 1 : u) * 64;
+  const bool nbl = has_l && u > 0, nbr = has_r && u + 1 < nv;
 
-  double Mr[DB];
+  double Mr[QUAD ? 1 : DB], Mq[QUAD ? 4 : 1][QUAD ? QT : 1];
   const double* Mg = a.Minv + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)d * d;
+  if constexpr (QUAD) {
+    quad_load<QT>(Mq, Mg, d, active);
+  } else {
 #pragma unroll
-  for (int j = 0; j < DB; ++j) Mr[j] = (active && in && j < d) ? Mg[lane * d + j] : 0.0;
+    for (int j = 0; j < DB; ++j) Mr[j] = (active && in && j < d) ? Mg[lane * d + j] : 0.0;
+  }
+  // y = (A + deg rho I)^{-1} r for this wave's worker (r: this lane's element)
+  auto solve = [&](double r) -> double {
+    if constexpr (QUAD) {
+      const double y = quad_gemv<QT>(Mq, in ? r : 0.0, myx);
+      return in ? y : 0.0;
+    } else {
+      myx[lane] = in ? r : 0.0;
+      return in ? reg_gemv(Mr, myx) : 0.0;
+    }
+  };
   double th = (active && in) ? a.theta[(long)w * d + lane] : 0.0;
   double mu = (active && in) ? a.mu[(long)li * d + lane] : 0.0;
   const double bb = (active && in) ? a.b[(long)li * d + lane] : 0.0;
-  thS[v * 64 + lane] = th;
-  myx[lane] = 0.0;
+  thS[u * 64 + lane] = th;
+  if constexpr (!QUAD) myx[lane] = 0.0;
   int pending = a.pending_in;
   if (threadIdx.x == 0) stop_iter_lds = 0;
   lds_barrier();
@@ -231,7 +262,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (;; ++it) {
     if (it > a.max_iter + a.lag) break;
-    const bool stamp = a.timeline && threadIdx.x == 0 && it - a.start_iter < a.timeline_iters;
+    const bool stamp = a.timeline && v == 0 && it - a.start_iter < a.timeline_iters;  // wave-uniform (SGPR stamps)
     if (stamp) ts[0] = (long long)now_ticks();
     // ---- halo exchange every k iterations (state after iteration it - 1); the owned workers
     // published theirs during the tail phase of it - 1 (publish() below)
@@ -257,7 +288,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         if (!ok && lane == 0) abort_lds = 1;
         th = in ? t0 : 0.0;
         mu = in ? t1 : 0.0;
-        thS[v * 64 + lane] = th;
+        thS[u * 64 + lane] = th;
       }
       lds_barrier();  // refreshed halo theta visible to the neighbouring waves
       if (abort_lds) break;
@@ -277,13 +308,12 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       if (has_l) r = r + rho * tl;
       if (has_r) r = r + rho * tr;
       if (stamp) ts[6] = (long long)now_ticks();
-      myx[lane] = in ? r : 0.0;
-      th = in ? reg_gemv(Mr, myx) : 0.0;
+      th = solve(r);
       if (stamp) {
         asm volatile("" ::"v"(th));
         ts[7] = (long long)now_ticks();
       }
-      thS[v * 64 + lane] = th;
+      thS[u * 64 + lane] = th;
       if (owned && in)
         store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
                              make_tag(a.epoch, it), th);
@@ -299,14 +329,13 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       double r = bb - mu;
       if (has_l) r = r + rho * tl;
       if (has_r) r = r + rho * tr;
-      myx[lane] = in ? r : 0.0;
-      const double tn = in ? reg_gemv(Mr, myx) : 0.0;
+      const double tn = solve(r);
       double m = mu;
       if (has_l) m = m - rho * (tl - tn);
       if (has_r) m = m + rho * (tn - tr);
       mu = m;
       th = tn;
-      thS[v * 64 + lane] = th;
+      thS[u * 64 + lane] = th;
       if (owned && in) {
         store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
                              make_tag(a.epoch, it), th);
@@ -334,7 +363,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       }
     }
     lds_barrier();
-    if (stamp) {
+    if (stamp && lane == 0) {
       long long* tl = a.timeline + ((long)g * a.timeline_iters + (it - a.start_iter)) * 8;
       for (int q = 0; q < 5; ++q) tl[q] = ts[q];
       tl[5] = (long long)now_ticks();
@@ -384,10 +413,15 @@ int gadmm_chain_blocked_plan(int n, int d, int want_k, int* k_out, int* len_out)
   return W;
 }
 
+static bool blocked_quad() {  // GADMM_QUAD=0: the row-per-lane reg_gemv variant (A/B measurements)
+  const char* e = getenv("GADMM_QUAD");
+  return !(e && e[0] == '0');
+}
+
 long gadmm_chain_blocked_lds(int d, int len) {
   (void)d;
   (void)len;
-  return (long)(2 * MAXW * 64) * 8;
+  return (long)(MAXW * 64 + MAXW * (blocked_quad() ? QSTAGE : 64)) * 8;
 }
 
 // Granules of the blk_tab buffer: exchange table [2][n][2][d] + theta ring [ring][n][d].
@@ -422,8 +456,14 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
     return -1;
   }
   const void* fn;
-  if (a.sys_scope) fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, true> : (const void*)chain_blocked_kernel<52, true>;
-  else fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, false> : (const void*)chain_blocked_kernel<52, false>;
+  const bool q = blocked_quad();
+  if (a.sys_scope) {
+    if (q) fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, true, true> : (const void*)chain_blocked_kernel<52, true, true>;
+    else fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, true, false> : (const void*)chain_blocked_kernel<52, true, false>;
+  } else {
+    if (q) fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, false, true> : (const void*)chain_blocked_kernel<52, false, true>;
+    else fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, false, false> : (const void*)chain_blocked_kernel<52, false, false>;
+  }
   if (lds > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   void* kargs[] = {const_cast<PersistArgs*>(&a)};
   GADMM_CHECK(hipLaunchKernel(fn, dim3(blocks), dim3(64 * MAXW), kargs, (size_t)lds, st));
