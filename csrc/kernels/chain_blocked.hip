@@ -258,6 +258,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         store_granule<SYS>(rpe, (base + d + lane) * 16, tag, mu);
       }
   };
+  unsigned long long dv_pref = 0;  // decision wave, lane 0: decision[it + 1 - lag] prefetched
   int it = a.start_iter;
   long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (;; ++it) {
@@ -324,12 +325,24 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
 
     // ---- tail phase; the (idle head) decision wave fetches decision[it + 1 - lag]
     const bool xnext = (it + 1 - a.start_iter) % k == 0;  // the next iteration starts with an exchange
+    // tail-wave stamps (wave MAXW/2), timeline row 128 + g: [start, rhs, gemv, stores, barrier]
+    const bool tstamp = a.timeline && v == MAXW / 2 && it - a.start_iter < a.timeline_iters && g < 128;
+    long long tt[4] = {0, 0, 0, 0};
     if (active && !head) {
+      if (tstamp) tt[0] = (long long)now_ticks();
       const double tl = nbl ? thL[lane] : 0.0, tr = nbr ? thR[lane] : 0.0;
       double r = bb - mu;
       if (has_l) r = r + rho * tl;
       if (has_r) r = r + rho * tr;
+      if (tstamp) {
+        asm volatile("" ::"v"(r));
+        tt[1] = (long long)now_ticks();
+      }
       const double tn = solve(r);
+      if (tstamp) {
+        asm volatile("" ::"v"(tn));
+        tt[2] = (long long)now_ticks();
+      }
       double m = mu;
       if (has_l) m = m - rho * (tl - tn);
       if (has_r) m = m + rho * (tn - tr);
@@ -341,13 +354,17 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
                              make_tag(a.epoch, it), th);
         if (xnext) publish(it);
       }
+      if (tstamp) tt[3] = (long long)now_ticks();
     } else if (active && owned && xnext) {  // heads: theta^it and the (still pending) mu are final
       if (in) publish(it);
     }
     if (dec_wave && !(active && !head) && lane == 0 && it + 1 - a.start_iter >= a.lag) {
       const int jdec = it + 1 - a.lag;
       const unsigned tj = make_tag(a.epoch, jdec);
-      unsigned long long dv = load_dec<SYS>(&a.decg[jdec % a.ring]);
+      // loaded during the previous iteration's tail phase: its L2 round trip (~0.7 us) is off the
+      // critical path; a decision that was not yet published then is re-polled here
+      unsigned long long dv = dv_pref;
+      if ((unsigned)(dv >> 32) != tj) dv = load_dec<SYS>(&a.decg[jdec % a.ring]);
       for (int spin = 0; (unsigned)(dv >> 32) != tj; ++spin) {
         if ((spin & 7) == 7 && now_ticks() > deadline) {
           abort_lds = 1;
@@ -361,8 +378,14 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         stop_lds = (int)code;
         stop_iter_lds = jdec;
       }
+      dv_pref = load_dec<SYS>(&a.decg[(jdec + 1) % a.ring]);
     }
     lds_barrier();
+    if (tstamp && lane == 0) {
+      long long* tl = a.timeline + ((long)(128 + g) * a.timeline_iters + (it - a.start_iter)) * 8;
+      for (int q = 0; q < 4; ++q) tl[q] = tt[q];
+      tl[4] = (long long)now_ticks();
+    }
     if (stamp && lane == 0) {
       long long* tl = a.timeline + ((long)g * a.timeline_iters + (it - a.start_iter)) * 8;
       for (int q = 0; q < 5; ++q) tl[q] = ts[q];

@@ -37,4 +37,10 @@ res["wave0_head_gemv_us_median"] = float(np.median(T[0, ks, 7] - T[0, ks, 6]))
 res["wave0_head_after_gemv_to_barrier_us_median"] = float(np.median(T[0, ks, 4] - T[0, ks, 7]))
 res["exchange_us_mean_per_iter"] = float(np.mean(exch))
 res["exchange_us_max"] = float(np.max(exch))
+Tt = eng.last_timeline[128: 128 + W].astype(np.float64) * 10e-3
+for q, nm in enumerate(["tail_rhs", "tail_gemv", "tail_dual_stores", "tail_to_barrier_end"]):
+    dd = np.concatenate([Tt[g, ks, q + 1] - Tt[g, ks, q] for g in range(W)])
+    res["tailwave_" + nm + "_us_median"] = float(np.median(dd))
+dd = np.concatenate([Tt[g, ks, 0] - T[g, ks, 4] for g in range(W)])
+res["tailwave_start_after_head_barrier_us_median"] = float(np.median(dd))
 print(json.dumps(res, indent=1))
