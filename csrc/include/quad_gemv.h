@@ -1,0 +1,56 @@
+// Split-column ("quad") register GEMV for matrices with <= 64 rows, shared by the persistent
+// linear kernels (chain_blocked.hip) and the logistic inner-GD phase (chain_small.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+// Split-column register GEMV for d <= 64 ("quad" layout). Lane l = i + 16c (i < 16, c < 4) holds
+// the rows i, i+16, i+32, i+48 of M restricted to the columns j = c + 4t (t < T), so each lane
+// needs only T broadcast x values instead of 4T: the LDS data return of a GEMV drops from 4T
+// ds_read_b128 per wave (reg_gemv, the phase bottleneck at several GEMV waves per CU,
+// profiles/r01_persistent_timeline) to T/2 + 4 reads. Lane (i, c) accumulates exactly reg_gemv's
+// accumulator a_c (columns j = c mod 4, ascending) for its four rows; the four partials of row l
+// meet in lane l through wave-private LDS and are added ((a0 + a1) + a2) + a3, so the result is
+// bit-identical to reg_gemv / symv_lds / symv_cols. x: this lane's element x_l (zero beyond d).
+// st: QSTAGE doubles of LDS private to the calling wave. Returns y_l in lane l.
+constexpr int QX = 18;  // permuted-x class stride: 2*18 mod 32 banks = 4 -> disjoint 4-bank windows
+constexpr int QR = 68;  // partial class stride: 2*68 mod 32 = 8
+constexpr int QSTAGE = 4 * QX + 4 * QR;
+
+template <int T>
+__device__ __forceinline__ void quad_load(double (&m)[4][T], const double* M, int d, bool on) {
+  const int lane = threadIdx.x & 63, i = lane & 15, c = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int row = i + 16 * r, col = c + 4 * t;
+      m[r][t] = (on && row < d && col < d) ? M[(long)row * d + col] : 0.0;
+    }
+}
+
+template <int T>
+__device__ __forceinline__ double quad_gemv(const double (&m)[4][T], double x, double* st) {
+  static_assert(T >= 1 && T <= 16, "quad layout covers d <= 64");
+  const int lane = threadIdx.x & 63, c = lane >> 4;
+  st[(lane & 3) * QX + (lane >> 2)] = x;
+  asm volatile("" ::: "memory");  // LDS is in order within a wave; keep the compiler from hoisting
+  const double* xs = st + c * QX;
+  double p[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int t = 0; t < T; t += 2) {  // x pairs consumed as they arrive (VGPR budget at 3 waves/SIMD)
+    const double2 xp = *reinterpret_cast<const double2*>(xs + t);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p[r] = fma(m[r][t], xp.x, p[r]);
+    if (t + 1 < T) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p[r] = fma(m[r][t + 1], xp.y, p[r]);
+    }
+  }
+  double* red = st + 4 * QX;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[c * QR + (lane & 15) + 16 * r] = p[r];
+  asm volatile("" ::: "memory");
+  const double q0 = red[lane], q1 = red[QR + lane], q2 = red[2 * QR + lane], q3 = red[3 * QR + lane];
+  asm volatile("" ::: "memory");  // the next call's writes stay behind these reads
+  return ((q0 + q1) + q2) + q3;
+}

@@ -30,6 +30,7 @@
 #include "gadmm_common.h"
 #include "gadmm_chain.h"
 #include "chain_device.h"
+#include "quad_gemv.h"
 
 
 namespace {
@@ -464,6 +465,96 @@ __global__ void __launch_bounds__(64) chain_phase_logistic_wave(PhaseArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// Logistic phase, one wave per worker, shard in REGISTERS (d, m <= 4T <= 64; default for E3/E4).
+// Both inner-GD GEMVs run in the split-column quad layout (quad_gemv.h): lane (i, c) holds
+// X[i + 16r][c + 4t] (margins z = X x) and X[c + 4t][i + 16r] (gradient X^T s), so a step is two
+// register GEMVs with 7 LDS broadcast reads each plus the elementwise sigmoid, instead of ~150 LDS
+// reads through the staged shard (chain_phase_logistic_wave, 1.8 us per inner step). Same
+// semantics as logReg_GD.m:3-25 (frozen proximal shift, all-coordinate |dx| < tol break).
+template <int T>
+__global__ void __launch_bounds__(64) chain_phase_logistic_quad(PhaseArgs a) {
+  __shared__ __attribute__((aligned(16))) double st[QSTAGE];
+  __shared__ int flag_lds;
+  ChainCtl* ctl = a.ctl;
+  if (ctl->done) return;
+  const int it = ctl->iter;
+  const int pending = ctl->pending;
+  const PhaseSlot sl = a.slots[blockIdx.x];
+  const int d = a.d, m = a.m;
+  const double rho = a.rho, lam = a.lam, step = a.step;
+  const int lane = threadIdx.x, qi = lane & 15, qc = lane >> 4;
+  double* th = a.theta;
+  const double* thw = th + (long)sl.gid * d;
+  const double* thl = sl.left >= 0 ? th + (long)sl.left * d : nullptr;
+  const double* thr = sl.right >= 0 ? th + (long)sl.right * d : nullptr;
+  double* mu = a.mu + (long)sl.li * d;
+  const double* Xg = a.X + (long)sl.li * m * d;
+  const double* Yg = a.Y + (long)sl.li * m;
+  double Xq[4][T], XTq[4][T];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int row = qi + 16 * r, col = qc + 4 * t;
+      Xq[r][t] = (row < m && col < d) ? Xg[(long)row * d + col] : 0.0;   // X[row][col]
+      XTq[r][t] = (col < m && row < d) ? Xg[(long)col * d + row] : 0.0;  // X^T[row][col]
+    }
+  const bool inj = lane < d, ini = lane < m;
+  double x = 0.0, sh = 0.0, yv = 0.0;
+  if (inj) {
+    double mm = mu[lane];
+    if ((a.flags & PH_PRE_DUAL) && pending) {
+      if (thl) mm = mm - rho * (thl[lane] - thw[lane]);
+      if (thr) mm = mm + rho * (thw[lane] - thr[lane]);
+      mu[lane] = mm;
+    }
+    const double x0 = thw[lane];
+    double s = mm;  // -C1 + C2 (edge form) == mu
+    if (thl) s = s + rho * (x0 - thl[lane]);
+    if (thr) s = s + rho * (x0 - thr[lane]);
+    sh = s;
+    x = x0;
+  }
+  if (ini) yv = Yg[lane];
+  int used = 0;
+  for (int k = 0; k < a.max_inner; ++k) {
+    const double z = quad_gemv<T>(Xq, x, st);                   // margins z_i = X[i,:] x
+    const double sv = ini ? yv / (1.0 + exp(yv * z)) : 0.0;    // y_i / (1 + e^{y_i z_i})
+    const double gx = quad_gemv<T>(XTq, sv, st);               // (X^T s)_j
+    bool conv = true;
+    if (inj) {
+      const double g = -gx + lam * x + sh;
+      const double xn = x - step * g;
+      conv = fabs(xn - x) < a.inner_tol;
+      x = xn;
+    }
+    used = k + 1;
+    if (__all(conv)) break;
+  }
+  // local objective lam/2 |x|^2 + sum softplus(-y z) at the new iterate
+  const double z = quad_gemv<T>(Xq, x, st);
+  const double part = wave_sum_f64(ini ? softplus(-yv * z) : 0.0);
+  const double xx = wave_sum_f64(inj ? x * x : 0.0);
+  double* thw_out = th + (long)sl.gid * d;
+  if (inj) {
+    thw_out[lane] = x;
+    if (a.flags & PH_POST_DUAL) {
+      double mm = mu[lane];
+      if (thl) mm = mm - rho * (thl[lane] - x);
+      if (thr) mm = mm + rho * (x - thr[lane]);
+      mu[lane] = mm;
+    }
+  }
+  if (lane == 0) {
+    a.objw[sl.li] = lam * 0.5 * xx + part;
+    if (a.inner_iters) a.inner_iters[sl.li] = used;
+  }
+  if (a.flags & PH_FINISH) {
+    if (phase_arrive(ctl, a.n_slots, &flag_lds)) finish_iteration(a, it);
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
 // Apply the pending heads' dual updates with the chain they were computed on (used before a
 // re-chain and before checkpointing). One workgroup per slot of the OLD head plan.
 __global__ void __launch_bounds__(NT) chain_dual_flush_kernel(const PhaseSlot* slots, int n_slots, int d,
@@ -564,7 +655,14 @@ int gadmm_chain_phase(const PhaseArgs* args, hipStream_t st) {
     if (ldsx) {
       // one wave per worker (default); GADMM_LOGISTIC_BLOCK=1 selects the 4-wave variant
       static const bool block4 = getenv("GADMM_LOGISTIC_BLOCK") != nullptr;
-      if (!block4) {
+      // GADMM_LOGISTIC_QUAD=0: the LDS-staged one-wave kernel (A/B measurements)
+      static const bool quad = !(getenv("GADMM_LOGISTIC_QUAD") && getenv("GADMM_LOGISTIC_QUAD")[0] == '0');
+      const int dm = a.d > a.m ? a.d : a.m;
+      if (!block4 && quad && dm <= 64) {
+        if (dm <= 32) hipLaunchKernelGGL(chain_phase_logistic_quad<8>, dim3(a.n_slots), dim3(64), 0, st, a);
+        else if (dm <= 52) hipLaunchKernelGGL(chain_phase_logistic_quad<13>, dim3(a.n_slots), dim3(64), 0, st, a);
+        else hipLaunchKernelGGL(chain_phase_logistic_quad<16>, dim3(a.n_slots), dim3(64), 0, st, a);
+      } else if (!block4) {
         const int cmax = nc > mc ? nc : mc;
         const size_t lw = lds + (size_t)2 * 64 * cmax * sizeof(double);
 #define GADMM_LOGW_LAUNCH(CV)                                                                           \
