@@ -263,22 +263,23 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         # D-GADMM in ONE persistent launch: the seeded chain sequence is drawn up front (batched,
         # identical RNG stream), every worker switches neighbours/role at each epoch on the device.
         engine_kind = "persistent-dynamic"
-        rechains = [int(v) for v in rechain_iterations(max_iter, schedule.coherence)]
+        rechains = rechain_iterations(max_iter, schedule.coherence)
         saved = schedule.save()
-        pre = schedule.prefetch(len(rechains))
-        epochs = [(1, list(saved[1]))] + [(it, pc[0]) for it, pc in zip(rechains, pre)]
-        costs = [np.asarray(saved[2])] + [np.asarray(pc[1]) for pc in pre]
-        r = eng.run_persistent(epochs=epochs)
+        Pn, Cn = schedule.prefetch_arrays(len(rechains))
+        P = np.concatenate([np.asarray(saved[1], dtype=np.int64)[None], Pn])
+        starts = np.concatenate([[1], rechains]).astype(np.int64)
+        r = eng.run_persistent(epochs=(starts, P))
         iters, done = r.iters, r.done
-        starts = np.asarray([e[0] for e in epochs])
-        per_it = np.asarray([float(np.sum(c)) * (n_heads if cost_quirk else 1) for c in costs])
+        # per-epoch cost; the initial cost vector may be ragged (the v0 column-slice quirk)
+        csum = Cn.sum(axis=1) if Cn.dtype != object else np.asarray([float(np.sum(c)) for c in Cn])
+        per_it = np.concatenate([[float(np.sum(saved[2]))], csum]) * (n_heads if cost_quirk else 1)
         which = np.searchsorted(starts, np.arange(1, iters + 1), side="right") - 1
         com_cost = list(np.cumsum(per_it[which]))
         # leave the schedule (and the engine's plan) where the epoch-by-epoch run would have left them
-        schedule.restore(saved)
-        schedule.prefetch(int(np.sum(np.asarray(rechains) <= iters)))
+        schedule.skip(saved, Pn, Cn, int(np.sum(rechains <= iters)))
         last = int(eng.ctl_state()["iter"]) - 1
-        eng.set_path(epochs[int(np.searchsorted(starts, max(last, 1), side="right") - 1)][1], placement, rank)
+        eng.set_path([int(v) for v in P[int(np.searchsorted(starts, max(last, 1), side="right") - 1)]], placement,
+                     rank)
     else:
         # D-GADMM: run epoch by epoch; at a re-chain iteration flush the heads' pending duals with the
         # old chain, install the new chain, continue. Every rank draws the same chain sequence.

@@ -304,8 +304,8 @@ class NativeChainEngine:
         ``self.last_timeline``: (workgroup, iteration, [start, ready, published, end, after the
         barrier, after the solve GEMV, -, -]); the last
         workgroup row is the monitor (column 0 = decision posted).
-        ``epochs``: D-GADMM in one launch, a list of ``(first_iteration, path)`` (the first entry at
-        ``start_iter``); every worker switches neighbours / role at each epoch start and flushes its
+        ``epochs``: D-GADMM in one launch, a list of ``(first_iteration, path)`` or a pair of arrays
+        ``(first_iterations (E,), paths (E, n))`` (the first epoch starts at ``start_iter``); every worker switches neighbours / role at each epoch start and flushes its
         pending head dual with the old chain first (single rank only)."""
         if epochs is not None:
             if not self.dynamic_eligible():
@@ -374,10 +374,14 @@ class NativeChainEngine:
         pa.trace, pa.ctl = self.trace.data_ptr(), self.ctl.data_ptr()
         ep_keep = None
         if epochs is not None:
-            starts = [int(e[0]) for e in epochs]
+            if isinstance(epochs, tuple) and len(epochs) == 2 and isinstance(epochs[1], np.ndarray):
+                starts = [int(v) for v in epochs[0]]                                # (starts, paths) arrays
+                P = np.asarray(epochs[1], dtype=np.int64)
+            else:
+                starts = [int(e[0]) for e in epochs]
+                P = np.asarray([list(e[1]) for e in epochs], dtype=np.int64)       # (E, n) position -> worker
             if starts[0] != int(start_iter) or any(b <= a for a, b in zip(starts, starts[1:])):
                 raise ValueError("epochs must start at start_iter and be increasing")
-            P = np.asarray([list(e[1]) for e in epochs], dtype=np.int64)           # (E, n) position -> worker
             E, n = P.shape
             pos_of = np.argsort(P, axis=1)                                          # worker -> position
             loc = np.asarray([int(w) for w in self.local_ids], dtype=np.int64)

@@ -17,6 +17,7 @@ Indices are 0-based throughout (reference worker ``ii`` == our worker ``ii-1``).
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -137,6 +138,36 @@ def rechain_iterations(max_iter: int, coherence: float) -> np.ndarray:
     return its[its > 1]
 
 
+def native_greedy_chains(uv: np.ndarray, side: float, energy: bool) -> Tuple[np.ndarray, np.ndarray]:
+    """Greedy chains + hop costs for a batch of node-position draws ``uv`` (E, N, 2) in [0, 1) by the
+    native C++ routine (csrc/runtime/topology.cpp), bit-identical to the numpy path."""
+    from ..ops import native
+
+    lib = native.load(build_if_missing=False)
+    uv = np.ascontiguousarray(uv, dtype=np.float64)
+    E, n, _ = uv.shape
+    paths = np.empty((E, n), dtype=np.int64)
+    costs = np.empty((E, max(n - 1, 0)), dtype=np.float64)
+    rc = lib.gadmm_greedy_chains(uv.ctypes.data, E, n, float(side), int(energy), ETA, BANDWIDTH,
+                                 2.0 ** (RATE / BANDWIDTH), paths.ctypes.data, costs.ctypes.data)
+    if rc != 0:
+        raise RuntimeError("gadmm_greedy_chains failed")
+    return paths, costs
+
+
+def _native_chains_ok() -> bool:
+    """The native chain builder is used when the library is already built (never builds it)."""
+    if os.environ.get("GADMM_NATIVE_TOPOLOGY", "1") == "0":
+        return False
+    try:
+        from ..ops import native
+
+        lib = native.load(build_if_missing=False)
+        return lib is not None and getattr(lib, "gadmm_greedy_chains", None) is not None
+    except Exception:
+        return False
+
+
 class PathSchedule:
     """Deterministic sequence of chains for D-GADMM.
 
@@ -164,19 +195,29 @@ class PathSchedule:
         self.rng.bit_generator.state = st[0]
         self.path, self.cost, self.k = list(st[1]), st[2].copy(), st[3]
 
-    def prefetch(self, count: int):
-        """The next ``count`` chains, exactly as ``count`` successive re-chains would draw them
-        (same RNG stream: the geometries of all epochs come from one batched draw), vectorised over
-        epochs. Advances the schedule past them. Returns ``[(path, cost), ...]``."""
-        out = []
+    def prefetch_arrays(self, count: int) -> Tuple[np.ndarray, np.ndarray]:
+        """The next ``count`` chains as arrays ``(paths (count, N) int64, costs (count, N-1))``,
+        exactly as ``count`` successive re-chains would draw them (same RNG stream: the geometries
+        of all epochs come from one batched draw), vectorised over epochs. Advances the schedule
+        past them."""
+        n = self.n
         if count <= 0:
-            return out
+            return np.zeros((0, n), dtype=np.int64), np.zeros((0, max(n - 1, 0)))
         if self.kind == "matrix":
-            for _ in range(count):
-                out.append((list(self.path_matrix[self.k]), np.asarray(self.cost_matrix[self.k])))
-                self.k += 1
+            rows = range(self.k, self.k + count)
+            paths = np.asarray([list(self.path_matrix[k]) for k in rows], dtype=np.int64)
+            cl = [np.asarray(self.cost_matrix[k], dtype=np.float64) for k in rows]
+            if len({len(c) for c in cl}) == 1:
+                costs = np.asarray(cl)
+            else:  # ragged rows (the v0 quirk): a 1-D object array of cost vectors
+                costs = np.empty(len(cl), dtype=object)
+                costs[:] = cl
+            self.k += count
+        elif native_greedy_chains is not None and _native_chains_ok():
+            side = 50.0 if self.kind == "findPath" else 250.0
+            uv = self.rng.random((count, n, 2))   # == count sequential rng.random((n, 2))
+            paths, costs = native_greedy_chains(uv, side, self.kind != "findPath")
         else:
-            n = self.n
             side = 50.0 if self.kind == "findPath" else 250.0
             xy = self.rng.random((count, n, 2)) * side   # == count sequential rng.random((n, 2))
             x, y = xy[..., 0], xy[..., 1]
@@ -184,15 +225,28 @@ class PathSchedule:
             idx = np.arange(n)
             d2[:, idx, idx] = 0.0
             paths = greedy_chains(d2)
-            if self.kind == "findPath":
-                hop = d2
-            else:
-                hop = link_energy(d2)
-            for e in range(count):
-                p = paths[e]
-                out.append(([int(v) for v in p], hop[e, p[:-1], p[1:]].copy()))
-        self.path, self.cost = out[-1][0], np.asarray(out[-1][1], dtype=np.float64)
-        return out
+            hop = d2 if self.kind == "findPath" else link_energy(d2)
+            costs = hop[np.arange(count)[:, None], paths[:, :-1], paths[:, 1:]]   # hop[e, p_k, p_{k+1}]
+        self.path, self.cost = [int(v) for v in paths[-1]], np.asarray(costs[-1], dtype=np.float64)
+        return paths, costs
+
+    def prefetch(self, count: int):
+        """``prefetch_arrays`` as a list ``[(path, cost), ...]``."""
+        paths, costs = self.prefetch_arrays(count)
+        return [([int(v) for v in p], c.copy()) for p, c in zip(paths, costs)]
+
+    def skip(self, saved, paths: np.ndarray, costs: np.ndarray, count: int) -> None:
+        """Put the schedule where ``count`` re-chains after the ``save()`` point ``saved`` leave
+        it, given the chains ``prefetch_arrays`` drew from there (the RNG is advanced, not
+        re-drawn: every findPath/findPath2 geometry consumes 2N doubles)."""
+        self.restore(saved)
+        if count <= 0:
+            return
+        if self.kind == "matrix":
+            self.k += count
+        else:
+            self.rng.bit_generator.advance(2 * self.n * count)
+        self.path, self.cost = [int(v) for v in paths[count - 1]], np.asarray(costs[count - 1], dtype=np.float64)
 
     def step(self, it: int) -> bool:
         """Advance to iteration ``it``; returns True if the chain changed."""

@@ -47,3 +47,31 @@ def test_code_objects_target_gfx950():
                          text=True)
     txt = out.stdout + out.stderr
     assert "gfx950" in txt
+
+
+def test_native_greedy_chains_match_numpy(monkeypatch):
+    """csrc/runtime/topology.cpp == PathSchedule's numpy path (findPath / findPath2), bit for bit,
+    and == successive step() draws (the reference's one-geometry-per-refresh stream)."""
+    import numpy as np
+    from gadmm_amd.parallel import topology as T
+
+    native.require()
+    for kind in ("findPath2", "findPath"):
+        for n in (5, 24, 50):
+            s1 = T.PathSchedule(n, list(range(n)), np.zeros(n - 1), 10, kind=kind, seed=11)
+            P, C = s1.prefetch_arrays(40)
+            monkeypatch.setenv("GADMM_NATIVE_TOPOLOGY", "0")
+            s2 = T.PathSchedule(n, list(range(n)), np.zeros(n - 1), 10, kind=kind, seed=11)
+            P2, C2 = s2.prefetch_arrays(40)
+            monkeypatch.delenv("GADMM_NATIVE_TOPOLOGY")
+            assert np.array_equal(P, P2) and np.array_equal(C, C2)
+            s3 = T.PathSchedule(n, list(range(n)), np.zeros(n - 1), 10, kind=kind, seed=11)
+            for e in range(3):
+                s3.step(10 * (e + 1))
+                assert s3.path == [int(v) for v in P[e]] and np.array_equal(s3.cost, C[e])
+            # skip() == drawing the chains one by one
+            s4 = T.PathSchedule(n, list(range(n)), np.zeros(n - 1), 10, kind=kind, seed=11)
+            s4.skip(s4.save(), P, C, 7)
+            s5 = T.PathSchedule(n, list(range(n)), np.zeros(n - 1), 10, kind=kind, seed=11)
+            s5.prefetch(7)
+            assert s4.path == s5.path and np.array_equal(s4.rng.random(4), s5.rng.random(4))
