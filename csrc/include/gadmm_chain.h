@@ -137,7 +137,7 @@ struct PersistArgs {
   // workgroups compute [seg_lo - 2k, seg_hi + 2k]; owned (theta, mu) are also pushed into the
   // exchange tables of the peers whose computed range [peer_lo, peer_hi] contains them.
   int seg_lo, seg_hi;       // seg_hi < 0: the whole chain (one GPU)
-  int blk_npeer, pad5_;
+  int blk_npeer, dbg;       // dbg: experiment bits (0 in production; see chain_blocked.hip)
   int blk_peer_lo[8], blk_peer_hi[8];
   u32x4* const* blk_peer_tab;  // [blk_npeer] peers' exchange tables (IPC-mapped)
 };

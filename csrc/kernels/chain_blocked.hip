@@ -315,7 +315,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         ts[7] = (long long)now_ticks();
       }
       thS[u * 64 + lane] = th;
-      if (owned && in)
+      if (owned && in && !(a.dbg & 2))
         store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
                              make_tag(a.epoch, it), th);
     }
@@ -350,7 +350,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       th = tn;
       thS[u * 64 + lane] = th;
       if (owned && in) {
-        store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
+        if (!(a.dbg & 2)) store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
                              make_tag(a.epoch, it), th);
         if (xnext) publish(it);
       }
@@ -358,7 +358,11 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     } else if (active && owned && xnext) {  // heads: theta^it and the (still pending) mu are final
       if (in) publish(it);
     }
-    if (dec_wave && !(active && !head) && lane == 0 && it + 1 - a.start_iter >= a.lag) {
+    if (a.timeline && g < 8 && it - a.start_iter < a.timeline_iters && lane == 0) {
+      const long long t_end = (long long)now_ticks();  // this wave's tail-phase work done
+      a.timeline[((long)(160 + g * MAXW + v) * a.timeline_iters + (it - a.start_iter)) * 8] = t_end;
+    }
+    if (!(a.dbg & 1) && dec_wave && !(active && !head) && lane == 0 && it + 1 - a.start_iter >= a.lag) {
       const int jdec = it + 1 - a.lag;
       const unsigned tj = make_tag(a.epoch, jdec);
       // loaded during the previous iteration's tail phase: its L2 round trip (~0.7 us) is off the
@@ -488,7 +492,12 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
     else fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, false, false> : (const void*)chain_blocked_kernel<52, false, false>;
   }
   if (lds > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  void* kargs[] = {const_cast<PersistArgs*>(&a)};
+  PersistArgs ka = a;
+  {
+    const char* e = getenv("GADMM_BLK_DBG");  // experiment bits: 1 no stop polling, 2 no objective ring stores
+    ka.dbg = e ? atoi(e) : 0;
+  }
+  void* kargs[] = {&ka};
   GADMM_CHECK(hipLaunchKernel(fn, dim3(blocks), dim3(64 * MAXW), kargs, (size_t)lds, st));
   GADMM_CHECK(hipGetLastError());
   return 0;

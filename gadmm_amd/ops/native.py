@@ -100,7 +100,7 @@ class PersistArgs(ctypes.Structure):
         ("objg", c_void_p), ("decg", c_void_p), ("dec_push", c_void_p), ("trace", c_void_p), ("ctl", c_void_p),
         ("timeline", c_void_p), ("timeline_iters", c_int), ("blk_k", c_int), ("blk_len", c_int), ("n_epochs", c_int),
         ("blk_tab", c_void_p), ("epoch_start", c_void_p), ("ep_slots", c_void_p), ("ep_pos", c_void_p),
-        ("seg_lo", c_int), ("seg_hi", c_int), ("blk_npeer", c_int), ("pad5_", c_int),
+        ("seg_lo", c_int), ("seg_hi", c_int), ("blk_npeer", c_int), ("dbg", c_int),
         ("blk_peer_lo", c_int * 8), ("blk_peer_hi", c_int * 8), ("blk_peer_tab", c_void_p),
     ]
 

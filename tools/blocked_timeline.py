@@ -21,11 +21,11 @@ eng = NativeChainEngine(ds.X.to(dev), ds.y.to(dev), list(range(24)), 24, "linear
 eng.set_path(list(range(24)), Placement.contiguous(24, 1), 0)
 for rep in range(3):
     eng.reset()
-    r = eng.run_persistent(timeline_iters=K)
+    r = eng.run_persistent(timeline_iters=K, timeout_s=float(os.environ.get("TL_TIMEOUT", "20")))
 k, L, W = eng.blocked_plan()
 T = eng.last_timeline[: W + 1].astype(np.float64) * 10e-3
 ks = np.arange(20, K - 2)
-res = {"kernel": eng.last_kernel, "iters": r.iters, "us_per_iter_wall": r.wall_ms * 1e3 / r.iters}
+res = {"kernel": eng.last_kernel, "iters": r.iters, "us_per_iter_wall": r.wall_ms * 1e3 / max(r.iters, 1)}
 res["period_us_median"] = float(np.median(np.diff(T[0, :, 0])[ks]))
 names = ["exchange", "decision_wait", "decision_barrier", "head_phase", "tail_phase"]
 for q, nm in enumerate(names):
@@ -43,4 +43,13 @@ for q, nm in enumerate(["tail_rhs", "tail_gemv", "tail_dual_stores", "tail_to_ba
     res["tailwave_" + nm + "_us_median"] = float(np.median(dd))
 dd = np.concatenate([Tt[g, ks, 0] - T[g, ks, 4] for g in range(W)])
 res["tailwave_start_after_head_barrier_us_median"] = float(np.median(dd))
+# per-wave end of tail-phase work (rows 160 + g*12 + v): which wave closes the tail barrier?
+Tw = eng.last_timeline[160: 160 + 12 * min(W, 8)].astype(np.float64).reshape(min(W, 8), 12, K, 8)[..., 0] * 10e-3
+late = []
+for g in range(min(W, 8)):
+    e = Tw[g][:, ks]                       # (12, iters)
+    valid = e.min(axis=1) > 0
+    rel = e - e[valid].min(axis=0, keepdims=True)
+    late.append([round(float(np.median(rel[v])), 2) if valid[v] else None for v in range(12)])
+res["tail_work_end_rel_us_median[g][wave]"] = late
 print(json.dumps(res, indent=1))
