@@ -41,8 +41,11 @@ constexpr int NW = 4;
 // VGPRs (lane i holds row i): a phase's GEMV is 64 FMAs per lane with x broadcast from LDS, and no
 // cross-wave reduction or barrier sits on the critical path (tools/persist_timeline.py measured
 // ~0.9 us of LDS-GEMV + barriers per phase in the 4-wave LDS variant at d = 50).
-// REG = false: 4 waves, matrices in LDS (64 < d <= 128).
-template <int NC, bool SYS, bool REG>
+// The register GEMV uses the split-column quad layout (quad_gemv.h, QT columns per lane, 7 LDS
+// broadcasts per GEMV instead of 26), bit-identical to the LDS variants. NV = 2: D-GADMM in one
+// launch with both degree variants of the inverse in registers (the degree changes on re-chain).
+// REG = false: 4 waves, matrices in LDS (64 < d <= 128, or D-GADMM with three degree variants).
+template <int NC, bool SYS, bool REG, int QT = 1, int NV = 1>
 __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(PersistArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int abort_lds;
@@ -107,7 +110,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
   // Static chain: workgroup b runs slot b of the position-sorted plan. D-GADMM (n_epochs > 0, LDS
   // variant only): workgroup b is local worker b for the whole launch and takes its slot / position
   // of each epoch from ep_slots / ep_pos (chains pre-drawn by the seeded schedule on the host).
-  const bool dyn = !REG && a.n_epochs > 0;
+  const bool dyn = a.n_epochs > 0;
   PhaseSlot sl = dyn ? a.ep_slots[blockIdx.x] : a.slots[blockIdx.x];
   int pos = dyn ? a.ep_pos[blockIdx.x] : a.pos[blockIdx.x];
   const int li = sl.li, w = sl.gid;
@@ -124,23 +127,27 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
   const __amdgpu_buffer_rsrc_t rp1 = rsrc_of(p1 ? (const void*)p1 : (const void*)a.thg);
 
   const long msz = REG ? 0 : (long)d * d;
-  const int nM = dyn ? a.nvar : 1;                             // inverses kept in LDS
+  const int nM = (dyn && !REG) ? a.nvar : 1;                   // inverses kept in LDS
   double* Mall = lds;                                          // [nM][d*d]
   double* Al = lds + nM * msz;                                 // d*d (obj_mode 0)
   double* xv = Al + (a.obj_mode == 0 ? msz : 0);               // [64*NC] rhs / theta staging
   double* red = xv + 64 * NC;                                  // [NW*NC*64]
-  double* Ml = Mall + (dyn ? (long)a.deg_to_var[deg] * msz : 0);
+  double* Ml = Mall + ((dyn && !REG) ? (long)a.deg_to_var[deg] * msz : 0);
+  double* st = lds;                                            // REG: quad GEMV staging (QSTAGE doubles)
+  int vsel = (dyn && REG) ? a.deg_to_var[deg] : 0;             // REG + D-GADMM: register variant in use
 
   const double* Mg = a.Minv + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)d * d;
   const double* Ag = a.A + (long)li * d * d;
-  double Mr[REG ? DREG : 1], Ar[REG ? DREG : 1];
+  double Mq[REG ? NV : 1][REG ? 4 : 1][REG ? QT : 1], Aq[REG ? 4 : 1][REG ? QT : 1];
   if constexpr (REG) {
+    if (dyn) {
 #pragma unroll
-    for (int j = 0; j < DREG; ++j) {
-      Mr[j] = (lane < d && j < d) ? Mg[lane * d + j] : 0.0;
-      Ar[j] = (a.obj_mode == 0 && lane < d && j < d) ? Ag[lane * d + j] : 0.0;
+      for (int v = 0; v < NV; ++v)
+        quad_load<QT>(Mq[v], a.Minv + ((long)li * a.nvar + (v < a.nvar ? v : 0)) * d * d, d, v < a.nvar);
+    } else {
+      quad_load<QT>(Mq[0], Mg, d, true);
     }
-    xv[lane] = 0.0;  // zero padding beyond d stays untouched
+    quad_load<QT>(Aq, Ag, d, a.obj_mode == 0);
   } else {
     if (dyn) {
       const double* Mw = a.Minv + (long)li * a.nvar * d * d;
@@ -197,7 +204,8 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       head = (pos % 2) == 0;
       deg = (left >= 0) + (right >= 0);
       crho = deg * rho;
-      Ml = Mall + (long)a.deg_to_var[deg] * msz;
+      if constexpr (REG) vsel = a.deg_to_var[deg];
+      else Ml = Mall + (long)a.deg_to_var[deg] * msz;
       next_start = ep + 1 < a.n_epochs ? a.epoch_start[ep + 1] : 0x7fffffff;
     }
     long long t_ready = 0, t_pub = 0, t_bar = 0, t_gemv = 0;
@@ -212,6 +220,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
     // a stop decision abandons the wait, since a neighbour that already saw it publishes no more.
     // Nothing is committed before the barrier that publishes the outcome.
     double mun[NC];
+    double rv = 0.0;  // REG: this lane's rhs element (the quad GEMV's input)
     if (w0) {
       const bool need_nb = head ? it > a.start_iter : true;
       const unsigned tnb = make_tag(a.epoch, head ? it - 1 : it);
@@ -268,7 +277,8 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
         double r = bb[c] - mun[c];
         if (left >= 0) r = r + rho * tl[c];
         if (right >= 0) r = r + rho * tr[c];
-        if (i < d) xv[i] = r;
+        if constexpr (REG) rv = i < d ? r : 0.0;
+        else if (i < d) xv[i] = r;
       }
     }
     lds_barrier();
@@ -281,8 +291,12 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
 
     // -- solve theta = (A + deg rho I)^{-1} r
     double tn[NC];
-    if constexpr (REG) tn[0] = reg_gemv(Mr, xv);
-    else symv_lds<NC>(Ml, xv, tn, red, d);
+    if constexpr (REG) {
+      if (NV > 1 && vsel == 1) tn[0] = quad_gemv<QT>(Mq[NV > 1 ? 1 : 0], rv, st);
+      else tn[0] = quad_gemv<QT>(Mq[0], rv, st);
+    } else {
+      symv_lds<NC>(Ml, xv, tn, red, d);
+    }
     if (a.timeline) t_gemv = (long long)now_ticks();
     double part = 0.0;
     if (w0) {
@@ -312,7 +326,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
           const int i = lane + 64 * c;
-          if (i < d) part += (0.5 * (xv[i] - crho * tn[c]) - bb[c]) * tn[c];
+          if (i < d) part += (0.5 * ((REG ? rv : xv[i]) - crho * tn[c]) - bb[c]) * tn[c];
         }
       }
     }
@@ -327,7 +341,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       }
       lds_barrier();
       double q[NC];
-      if constexpr (REG) q[0] = reg_gemv(Ar, xv);
+      if constexpr (REG) q[0] = quad_gemv<QT>(Aq, lane < d ? tn[0] : 0.0, st);
       else symv_lds<NC>(Al, xv, q, red, d);
       if (w0) {
 #pragma unroll
@@ -429,18 +443,27 @@ int gadmm_chain_persistent_launch(const PersistArgs* args, hipStream_t st) {
   }
   const long monitor_lds = (long)a.n * 8;
   const size_t shm = (size_t)(lds > monitor_lds ? lds : monitor_lds);
-#define GADMM_P_LAUNCH(NCv, SYSv, REGv)                                                            \
+#define GADMM_P_LAUNCH(NCv, SYSv, REGv, ...)                                                       \
   do {                                                                                             \
-    const void* kfn = (const void*)chain_persistent_kernel<NCv, SYSv, REGv>;                       \
-    const size_t sh = REGv ? (size_t)(monitor_lds > 1024 ? monitor_lds : 1024) : shm;             \
+    const void* kfn = (const void*)chain_persistent_kernel<NCv, SYSv, REGv, ##__VA_ARGS__>;        \
+    const size_t sh = REGv ? (size_t)(monitor_lds > QSTAGE * 8 ? monitor_lds : QSTAGE * 8) : shm;   \
     if (sh > 65536) GADMM_CHECK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh)); \
     void* kargs[] = {const_cast<PersistArgs*>(&a)};                                                \
     GADMM_CHECK(hipLaunchKernel(kfn, dim3(blocks), dim3(REGv ? 64 : NT), kargs, sh, st));          \
   } while (0)
   static const bool force_lds = getenv("GADMM_PERSIST_LDS") != nullptr;  // A/B switch
-  if (a.d <= DREG && !force_lds && !dyn) {
-    if (a.sys_scope) GADMM_P_LAUNCH(1, true, true);
-    else GADMM_P_LAUNCH(1, false, true);
+  if (a.d <= DREG && !force_lds && (!dyn || a.nvar <= 2)) {
+    // register kernel: QT = 13 covers d <= 52 (E1/E5), 16 covers d <= 64
+    if (dyn) {
+      if (a.d <= 52) GADMM_P_LAUNCH(1, false, true, 13, 2);
+      else GADMM_P_LAUNCH(1, false, true, 16, 2);
+    } else if (a.sys_scope) {
+      if (a.d <= 52) GADMM_P_LAUNCH(1, true, true, 13, 1);
+      else GADMM_P_LAUNCH(1, true, true, 16, 1);
+    } else {
+      if (a.d <= 52) GADMM_P_LAUNCH(1, false, true, 13, 1);
+      else GADMM_P_LAUNCH(1, false, true, 16, 1);
+    }
   } else if (a.d <= 64) {
     if (a.sys_scope) GADMM_P_LAUNCH(1, true, false);
     else GADMM_P_LAUNCH(1, false, false);
