@@ -36,25 +36,6 @@ namespace {
 
 constexpr int MAXW = 12;  // computed workers (waves) per workgroup: 3 waves per SIMD -> <= 170 VGPRs
 
-// q_i = sum_j A[j][i] th_j with A (symmetric, row-major d x d) in LDS and th broadcast from LDS;
-// the summation order of reg_gemv (accumulator j mod 4, ((a0 + a1) + a2) + a3).
-__device__ __forceinline__ double lds_gemv_cols(const double* A, int d, const double* xv, int i) {
-  double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-  if (i < d) {
-    int j = 0;
-    for (; j + 3 < d; j += 4) {
-      a0 = fma(A[j * d + i], xv[j], a0);
-      a1 = fma(A[(j + 1) * d + i], xv[j + 1], a1);
-      a2 = fma(A[(j + 2) * d + i], xv[j + 2], a2);
-      a3 = fma(A[(j + 3) * d + i], xv[j + 3], a3);
-    }
-    if (j < d) a0 = fma(A[j * d + i], xv[j], a0);
-    if (j + 1 < d) a1 = fma(A[(j + 1) * d + i], xv[j + 1], a1);
-    if (j + 2 < d) a2 = fma(A[(j + 2) * d + i], xv[j + 2], a2);
-  }
-  return ((a0 + a1) + a2) + a3;
-}
-
 }  // namespace
 
 // DB: register row length (multiple of 4, >= d); 52 keeps d = 50 within the 3-waves-per-SIMD budget.
@@ -62,7 +43,9 @@ __device__ __forceinline__ double lds_gemv_cols(const double* A, int d, const do
 // chain positions [seg_lo, seg_hi] and pushes owned (theta, mu) into its peers' exchange tables.
 // Block layout: [0, W) worker workgroups, [W, W + Wo) objective workgroups, W + Wo the monitor
 // (rank 0 only).
-template <int DB, bool SYS, bool QUAD>
+// TL: the instrumented instantiation (timeline stamps, experiment bits); the production one has no
+// diagnostics code in its loop.
+template <int DB, bool SYS, bool TL>
 __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a) {
   constexpr int QT = DB / 4;  // quad layout: columns per lane
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -121,7 +104,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         const unsigned long long dv = ((unsigned long long)tag << 32) | code;
         for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
         const int kk = it - a.start_iter;
-        if (a.timeline && kk < a.timeline_iters) a.timeline[((long)blockIdx.x * a.timeline_iters + kk) * 8] = (long long)now_ticks();
+        if (TL && kk < a.timeline_iters) a.timeline[((long)blockIdx.x * a.timeline_iters + kk) * 8] = (long long)now_ticks();
       }
       if (__shfl((int)code, 0, 64)) return;
     }
@@ -134,18 +117,11 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     if (q > seg_hi) return;
     const PhaseSlot so = a.slots[q];
     const bool in = lane < d;
-    double Ar[QUAD ? 1 : DB], Aq[QUAD ? 4 : 1][QUAD ? QT : 1];
-    const double* Ag = a.A + (long)so.li * d * d;
-    if constexpr (QUAD) {
-      quad_load<QT>(Aq, Ag, d, true);
-    } else {
-#pragma unroll
-      for (int j = 0; j < DB; ++j) Ar[j] = (in && j < d) ? Ag[lane * d + j] : 0.0;
-    }
+    double Aq[4][QT];
+    quad_load<QT>(Aq, a.A + (long)so.li * d * d, d, true);
     const double bo = in ? a.b[(long)so.li * d + lane] : 0.0;
     const double hy = 0.5 * a.yy[so.li];
-    double* xo = lds + v * (QUAD ? QSTAGE : 64);
-    if constexpr (!QUAD) xo[lane] = 0.0;
+    double* xo = lds + v * QSTAGE;
     for (int it = a.start_iter;; ++it) {
       const unsigned tag = make_tag(a.epoch, it);
       const long off = (ring_base + ((long)(it % a.ring) * n + q) * d + lane) * 16;
@@ -164,13 +140,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      double qv;  // (A th)_i in the order of every other engine
-      if constexpr (QUAD) {
-        qv = quad_gemv<QT>(Aq, in ? x : 0.0, xo);
-      } else {
-        xo[lane] = in ? x : 0.0;
-        qv = reg_gemv(Ar, xo);
-      }
+      const double qv = quad_gemv<QT>(Aq, in ? x : 0.0, xo);  // (A th)_i in the order of every other engine
       const double part = in ? (0.5 * qv - bo) * x : 0.0;
       const double f = wave_sum_f64(part) + hy;
       if (lane == 0) store_granule<SYS>(rob, ((it % a.ring) * n + so.gid) * 16, tag, f);
@@ -208,36 +178,24 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   const bool dec_wave = u == vdec;
 
   double* thS = lds;                       // [MAXW][64] theta of every computed worker
-  double* xs = thS + MAXW * 64;            // [MAXW][64 | QSTAGE] per-wave rhs / broadcast staging
-  double* myx = xs + v * (QUAD ? QSTAGE : 64);
+  double* xs = thS + MAXW * 64;            // [MAXW][QSTAGE] per-wave quad GEMV staging
+  double* myx = xs + v * QSTAGE;
   // the wave's neighbours inside the computed range (outside it the halo worker is already stale)
   const double* thL = thS + (u > 0 ? u - 1 : u) * 64;
   const double* thR = thS + (u + 1 < nv ? u + 1 : u) * 64;
   const bool nbl = has_l && u > 0, nbr = has_r && u + 1 < nv;
 
-  double Mr[QUAD ? 1 : DB], Mq[QUAD ? 4 : 1][QUAD ? QT : 1];
-  const double* Mg = a.Minv + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)d * d;
-  if constexpr (QUAD) {
-    quad_load<QT>(Mq, Mg, d, active);
-  } else {
-#pragma unroll
-    for (int j = 0; j < DB; ++j) Mr[j] = (active && in && j < d) ? Mg[lane * d + j] : 0.0;
-  }
+  double Mq[4][QT];
+  quad_load<QT>(Mq, a.Minv + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)d * d, d, active);
   // y = (A + deg rho I)^{-1} r for this wave's worker (r: this lane's element)
   auto solve = [&](double r) -> double {
-    if constexpr (QUAD) {
-      const double y = quad_gemv<QT>(Mq, in ? r : 0.0, myx);
-      return in ? y : 0.0;
-    } else {
-      myx[lane] = in ? r : 0.0;
-      return in ? reg_gemv(Mr, myx) : 0.0;
-    }
+    const double y = quad_gemv<QT>(Mq, in ? r : 0.0, myx);
+    return in ? y : 0.0;
   };
   double th = (active && in) ? a.theta[(long)w * d + lane] : 0.0;
   double mu = (active && in) ? a.mu[(long)li * d + lane] : 0.0;
   const double bb = (active && in) ? a.b[(long)li * d + lane] : 0.0;
   thS[u * 64 + lane] = th;
-  if constexpr (!QUAD) myx[lane] = 0.0;
   int pending = a.pending_in;
   if (threadIdx.x == 0) stop_iter_lds = 0;
   lds_barrier();
@@ -263,7 +221,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (;; ++it) {
     if (it > a.max_iter + a.lag) break;
-    const bool stamp = a.timeline && v == 0 && it - a.start_iter < a.timeline_iters;  // wave-uniform (SGPR stamps)
+    const bool stamp = TL && v == 0 && it - a.start_iter < a.timeline_iters;  // wave-uniform (SGPR stamps)
     if (stamp) ts[0] = (long long)now_ticks();
     // ---- halo exchange every k iterations (state after iteration it - 1); the owned workers
     // published theirs during the tail phase of it - 1 (publish() below)
@@ -315,7 +273,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         ts[7] = (long long)now_ticks();
       }
       thS[u * 64 + lane] = th;
-      if (owned && in && !(a.dbg & 2))
+      if (owned && in && !(TL && (a.dbg & 2)))
         store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
                              make_tag(a.epoch, it), th);
     }
@@ -326,7 +284,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     // ---- tail phase; the (idle head) decision wave fetches decision[it + 1 - lag]
     const bool xnext = (it + 1 - a.start_iter) % k == 0;  // the next iteration starts with an exchange
     // tail-wave stamps (wave MAXW/2), timeline row 128 + g: [start, rhs, gemv, stores, barrier]
-    const bool tstamp = a.timeline && v == MAXW / 2 && it - a.start_iter < a.timeline_iters && g < 128;
+    const bool tstamp = TL && v == MAXW / 2 && it - a.start_iter < a.timeline_iters && g < 128;
     long long tt[4] = {0, 0, 0, 0};
     if (active && !head) {
       if (tstamp) tt[0] = (long long)now_ticks();
@@ -350,7 +308,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       th = tn;
       thS[u * 64 + lane] = th;
       if (owned && in) {
-        if (!(a.dbg & 2)) store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
+        if (!(TL && (a.dbg & 2))) store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
                              make_tag(a.epoch, it), th);
         if (xnext) publish(it);
       }
@@ -358,11 +316,11 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     } else if (active && owned && xnext) {  // heads: theta^it and the (still pending) mu are final
       if (in) publish(it);
     }
-    if (a.timeline && g < 8 && it - a.start_iter < a.timeline_iters && lane == 0) {
+    if (TL && g < 8 && it - a.start_iter < a.timeline_iters && lane == 0) {
       const long long t_end = (long long)now_ticks();  // this wave's tail-phase work done
       a.timeline[((long)(160 + g * MAXW + v) * a.timeline_iters + (it - a.start_iter)) * 8] = t_end;
     }
-    if (!(a.dbg & 1) && dec_wave && !(active && !head) && lane == 0 && it + 1 - a.start_iter >= a.lag) {
+    if (!(TL && (a.dbg & 1)) && dec_wave && !(active && !head) && lane == 0 && it + 1 - a.start_iter >= a.lag) {
       const int jdec = it + 1 - a.lag;
       const unsigned tj = make_tag(a.epoch, jdec);
       // loaded during the previous iteration's tail phase: its L2 round trip (~0.7 us) is off the
@@ -440,15 +398,10 @@ int gadmm_chain_blocked_plan(int n, int d, int want_k, int* k_out, int* len_out)
   return W;
 }
 
-static bool blocked_quad() {  // GADMM_QUAD=0: the row-per-lane reg_gemv variant (A/B measurements)
-  const char* e = getenv("GADMM_QUAD");
-  return !(e && e[0] == '0');
-}
-
 long gadmm_chain_blocked_lds(int d, int len) {
   (void)d;
   (void)len;
-  return (long)(MAXW * 64 + MAXW * (blocked_quad() ? QSTAGE : 64)) * 8;
+  return (long)(MAXW * 64 + MAXW * QSTAGE) * 8;
 }
 
 // Granules of the blk_tab buffer: exchange table [2][n][2][d] + theta ring [ring][n][d].
@@ -483,12 +436,12 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
     return -1;
   }
   const void* fn;
-  const bool q = blocked_quad();
+  const bool tl = a.timeline != nullptr;
   if (a.sys_scope) {
-    if (q) fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, true, true> : (const void*)chain_blocked_kernel<52, true, true>;
+    if (tl) fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, true, true> : (const void*)chain_blocked_kernel<52, true, true>;
     else fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, true, false> : (const void*)chain_blocked_kernel<52, true, false>;
   } else {
-    if (q) fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, false, true> : (const void*)chain_blocked_kernel<52, false, true>;
+    if (tl) fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, false, true> : (const void*)chain_blocked_kernel<52, false, true>;
     else fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, false, false> : (const void*)chain_blocked_kernel<52, false, false>;
   }
   if (lds > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));

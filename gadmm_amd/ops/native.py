@@ -16,8 +16,8 @@ from typing import Optional
 
 import torch  # noqa: F401  (must be loaded before the native library)
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native",
-                         "libgadmm_native.so")
+_LIB_PATH = os.environ.get("GADMM_NATIVE_LIB") or os.path.join(  # override: A/B runs of two builds
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "_native", "libgadmm_native.so")
 _lib: Optional[ctypes.CDLL] = None
 _load_error: Optional[str] = None
 

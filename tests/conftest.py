@@ -9,6 +9,13 @@ if ROOT not in sys.path:
 
 
 def pytest_configure(config):
+    # under pytest-xdist every worker would start a full-width torch thread pool: the tiny (50 x 50)
+    # CPU ops then thrash 8 cores (a 14 s test took 30 min at -n 6); give each worker its share
+    n_workers = int(os.environ.get("PYTEST_XDIST_WORKER_COUNT", "1"))
+    if n_workers > 1:
+        import torch
+
+        torch.set_num_threads(max(1, (os.cpu_count() or 8) // n_workers))
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
     config.addinivalue_line("markers", "slow: long CPU run (reference-length baselines)")
 
