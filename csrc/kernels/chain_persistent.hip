@@ -45,7 +45,8 @@ constexpr int NW = 4;
 // broadcasts per GEMV instead of 26), bit-identical to the LDS variants. NV = 2: D-GADMM in one
 // launch with both degree variants of the inverse in registers (the degree changes on re-chain).
 // REG = false: 4 waves, matrices in LDS (64 < d <= 128, or D-GADMM with three degree variants).
-template <int NC, bool SYS, bool REG, int QT = 1, int NV = 1>
+// TL: instrumented instantiation (s_memrealtime timeline); production instantiations have no stamps.
+template <int NC, bool SYS, bool REG, int QT = 1, int NV = 1, bool TL = false>
 __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(PersistArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int abort_lds;
@@ -99,7 +100,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
         for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
         if (code) stop_lds = 1;
         const int k = it - a.start_iter;
-        if (a.timeline && k < a.timeline_iters) a.timeline[((long)blockIdx.x * a.timeline_iters + k) * 8] = (long long)now_ticks();
+        if (TL && k < a.timeline_iters) a.timeline[((long)blockIdx.x * a.timeline_iters + k) * 8] = (long long)now_ticks();
       }
       lds_barrier();
       if (stop_lds) return;
@@ -178,7 +179,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
   int it = a.start_iter;
   for (;; ++it) {
     if (it > a.max_iter + a.lag) break;
-    const long long t_start = a.timeline ? (long long)now_ticks() : 0;
+    const long long t_start = TL ? (long long)now_ticks() : 0;
     if (dyn && it == next_start) {
       // re-chain (dynamic_group_ADMM_closedForm.m:18-21): a worker that was a head still owes the
       // previous iteration's dual, computed with its OLD neighbours' theta^{it-1} (every worker that
@@ -249,7 +250,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
         __builtin_amdgcn_s_sleep(1);
       }
       if (lane == 0) {
-        if (a.timeline) t_ready = (long long)now_ticks();
+        if (TL) t_ready = (long long)now_ticks();
         if (outcome == 3) abort_lds = 1;
         if (outcome == 2) {
           stop_lds = 1;
@@ -283,7 +284,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
     }
     lds_barrier();
     if (abort_lds || stop_lds) break;
-    if (a.timeline) t_bar = (long long)now_ticks();
+    if (TL) t_bar = (long long)now_ticks();
     if (w0) {
 #pragma unroll
       for (int c = 0; c < NC; ++c) mu[c] = mun[c];
@@ -297,7 +298,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
     } else {
       symv_lds<NC>(Ml, xv, tn, red, d);
     }
-    if (a.timeline) t_gemv = (long long)now_ticks();
+    if (TL) t_gemv = (long long)now_ticks();
     double part = 0.0;
     if (w0) {
       const unsigned tag = make_tag(a.epoch, it);
@@ -310,7 +311,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
           if (p1) store_granule<SYS>(rp1, (w * d + i) * 16, tag, tn[c]);
         }
       }
-      if (a.timeline) t_pub = (long long)now_ticks();
+      if (TL) t_pub = (long long)now_ticks();
       if (!head) {  // tails: both neighbours are this iteration's heads -> dual update now
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
@@ -357,7 +358,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
 #pragma unroll
       for (int c = 0; c < NC; ++c) th[c] = tn[c];
       const int k = it - a.start_iter;
-      if (lane == 0 && a.timeline && k < a.timeline_iters) {
+      if (TL && lane == 0 && k < a.timeline_iters) {
         long long* tl = a.timeline + ((long)blockIdx.x * a.timeline_iters + k) * 8;
         tl[0] = t_start;
         tl[1] = t_ready;
@@ -452,9 +453,13 @@ int gadmm_chain_persistent_launch(const PersistArgs* args, hipStream_t st) {
     GADMM_CHECK(hipLaunchKernel(kfn, dim3(blocks), dim3(REGv ? 64 : NT), kargs, sh, st));          \
   } while (0)
   static const bool force_lds = getenv("GADMM_PERSIST_LDS") != nullptr;  // A/B switch
+  const bool tl = a.timeline != nullptr;  // instrumented instantiations (one GPU, register kernel, LDS d <= 64)
   if (a.d <= DREG && !force_lds && (!dyn || a.nvar <= 2)) {
     // register kernel: QT = 13 covers d <= 52 (E1/E5), 16 covers d <= 64
-    if (dyn) {
+    if (tl && !a.sys_scope && a.d <= 52) {
+      if (dyn) GADMM_P_LAUNCH(1, false, true, 13, 2, true);
+      else GADMM_P_LAUNCH(1, false, true, 13, 1, true);
+    } else if (dyn) {
       if (a.d <= 52) GADMM_P_LAUNCH(1, false, true, 13, 2);
       else GADMM_P_LAUNCH(1, false, true, 16, 2);
     } else if (a.sys_scope) {
@@ -466,6 +471,7 @@ int gadmm_chain_persistent_launch(const PersistArgs* args, hipStream_t st) {
     }
   } else if (a.d <= 64) {
     if (a.sys_scope) GADMM_P_LAUNCH(1, true, false);
+    else if (tl) GADMM_P_LAUNCH(1, false, false, 1, 1, true);
     else GADMM_P_LAUNCH(1, false, false);
   } else {
     if (a.sys_scope) GADMM_P_LAUNCH(2, true, false);
