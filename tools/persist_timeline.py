@@ -7,6 +7,7 @@ Per iteration k and worker: start, ready (neighbours' theta + stop decision in h
 (theta granules issued), end (objective granule issued). Reports the iteration period, per-phase
 compute, the hand-off latency (consumer ready - last producer publish) and the monitor's lag."""
 import json, os, sys
+os.environ.setdefault("GADMM_BLOCKED", "0")  # the per-worker kernel (the blocked one: blocked_timeline.py)
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 import torch
