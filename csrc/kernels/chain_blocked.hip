@@ -390,6 +390,10 @@ int gadmm_chain_blocked_plan(int n, int d, int want_k, int* k_out, int* len_out)
     len = MAXW - 4 * k;
   }
   if (len < 1) return 0;
+  if (const char* e = getenv("GADMM_BLOCK_L")) {  // owned positions per workgroup (tuning runs)
+    const int want_len = atoi(e);
+    if (want_len >= 1 && want_len < len) len = want_len;
+  }
   if (len > n) len = n;
   const int W = (n + len - 1) / len;
   if (W + (n + MAXW - 1) / MAXW + 1 > 256) return 0;

@@ -56,6 +56,20 @@ def test_spd_inverse_kernel(d):
     assert _rel(inv, ref) < 1e-11
 
 
+@pytest.mark.parametrize("d", [7, 50, 64])
+def test_spd_inverse_gj64_bit_identical(d, monkeypatch):
+    """The 64-wide Gauss-Jordan (d <= 64) reproduces the general kernel bit for bit."""
+    from gadmm_amd.ops import linalg
+    g = torch.Generator().manual_seed(100 + d)
+    Z = torch.randn(5, 2 * d, d, dtype=torch.float64, generator=g)
+    A = torch.bmm(Z.transpose(1, 2), Z).to(DEV)
+    sh = torch.tensor([0.3, 2.0], dtype=torch.float64, device=DEV)
+    fast = linalg.spd_inverse(A, sh)
+    monkeypatch.setenv("GADMM_GJ64", "0")
+    general = linalg.spd_inverse(A, sh)
+    assert torch.equal(fast, general)
+
+
 def _engine(ds, rho, obj0, tol, **kw):
     from gadmm_amd.engine.chain_engine import NativeChainEngine
     from gadmm_amd.parallel.topology import Placement
