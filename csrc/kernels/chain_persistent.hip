@@ -55,6 +55,13 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
   const int lane = threadIdx.x & 63;
   const bool w0 = threadIdx.x < 64;  // wave 0 owns the worker state; waves 1..3 help in the GEMVs
   const __amdgpu_buffer_rsrc_t rth = rsrc_of(a.thg);
+  // theta table row of worker w's theta^j. D-GADMM: a ring of `ring` iteration slots, because at a
+  // re-chain a head still reads its OLD tails' theta^{it-1} while those tails, no longer its
+  // neighbours, may already run ahead (up to lag iterations: the stop rule bounds the skew) and
+  // would overwrite a single slot. Static chains: one slot (a producer needs the consumer's next
+  // theta before it can overwrite).
+  const bool ring_tab = a.n_epochs > 0;
+  auto trow = [&](int w, int j) -> int { return ring_tab ? (j % a.ring) * n + w : w; };
   const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
   const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
   if (threadIdx.x == 0) {
@@ -186,7 +193,8 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       // reached this iteration has published theta^{it-1}); then it takes its new slot.
       if (w0 && pending && it > a.start_iter) {
         const unsigned tp = make_tag(a.epoch, it - 1);
-        const int ok = wait_pair<NC, SYS>(rth, d, left, tp, tl, right, tp, tr, deadline);
+        const int ok = wait_pair<NC, SYS>(rth, d, left >= 0 ? trow(left, it - 1) : -1, tp, tl,
+                                          right >= 0 ? trow(right, it - 1) : -1, tp, tr, deadline);
         if (ok != 1 && lane == 0) abort_lds = 1;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
@@ -224,7 +232,8 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
     double rv = 0.0;  // REG: this lane's rhs element (the quad GEMV's input)
     if (w0) {
       const bool need_nb = head ? it > a.start_iter : true;
-      const unsigned tnb = make_tag(a.epoch, head ? it - 1 : it);
+      const int jnb = head ? it - 1 : it;
+      const unsigned tnb = make_tag(a.epoch, jnb);
       const int ra = need_nb ? left : -1, rb = need_nb ? right : -1;
       const unsigned tj = make_tag(a.epoch, jdec);
       bool decided = !check;
@@ -236,8 +245,8 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
         for (int c = 0; c < NC; ++c) {
           const int i = lane + 64 * c;
           if (i < d) {
-            if (ra >= 0) nb &= load_granule<SYS>(rth, (ra * d + i) * 16, tnb, &tl[c]);
-            if (rb >= 0) nb &= load_granule<SYS>(rth, (rb * d + i) * 16, tnb, &tr[c]);
+            if (ra >= 0) nb &= load_granule<SYS>(rth, (trow(ra, jnb) * d + i) * 16, tnb, &tl[c]);
+            if (rb >= 0) nb &= load_granule<SYS>(rth, (trow(rb, jnb) * d + i) * 16, tnb, &tr[c]);
           }
         }
         if (!decided) {
@@ -306,7 +315,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       for (int c = 0; c < NC; ++c) {  // publish theta^it: local table + remote neighbours' tables
         const int i = lane + 64 * c;
         if (i < d) {
-          store_granule<SYS>(rth, (w * d + i) * 16, tag, tn[c]);
+          store_granule<SYS>(rth, (trow(w, it) * d + i) * 16, tag, tn[c]);
           if (p0) store_granule<SYS>(rp0, (w * d + i) * 16, tag, tn[c]);
           if (p1) store_granule<SYS>(rp1, (w * d + i) * 16, tag, tn[c]);
         }

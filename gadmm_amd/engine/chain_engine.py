@@ -319,14 +319,16 @@ class NativeChainEngine:
         dev = self.device
         slots = sorted(self.plan.head + self.plan.tail, key=lambda s: self.path.index(s.gid))
         pos = [self.path.index(s.gid) for s in slots]
-        key = (ring, tuple((s.li, s.gid, s.left, s.right) for s in slots), id(fabric))
+        key = (ring, tuple((s.li, s.gid, s.left, s.right) for s in slots), id(fabric), epochs is not None)
         if getattr(self, "_pbuf", None) is None or self._pbuf[0] != key:
             with torch.cuda.stream(self.stream):
                 slot_t = torch.tensor([[s.li, s.gid, s.left, s.right] for s in slots], dtype=torch.int32,
                                       device=dev).reshape(-1)
                 pos_t = torch.tensor(pos, dtype=torch.int32, device=dev)
                 if fabric is None:
-                    thg = torch.zeros((self.n_total * self.d * 4,), dtype=torch.int32, device=dev)
+                    # D-GADMM (epochs): one theta slot per ring iteration (see chain_persistent.hip)
+                    thg = torch.zeros(((ring if epochs is not None else 1) * self.n_total * self.d * 4,),
+                                      dtype=torch.int32, device=dev)
                     objg = torch.zeros((ring * self.n_total * 4,), dtype=torch.int32, device=dev)
                     decg = torch.zeros((ring,), dtype=torch.int64, device=dev)
                     ptrs = (thg.data_ptr(), objg.data_ptr(), decg.data_ptr())

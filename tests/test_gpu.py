@@ -308,10 +308,12 @@ def test_xgmi_fabric_two_processes_one_gpu(lin24, lin_obj0):
     assert np.array_equal(np.asarray(res[0]["trace"]), single.obj)  # bit-identical to the 1-GPU persistent run
 
 
-def test_dgadmm_persistent_dynamic_matches_epoch_path(lin24, lin_obj0):
+@pytest.mark.parametrize("coh", [10, 1])
+def test_dgadmm_persistent_dynamic_matches_epoch_path(lin24, lin_obj0, coh):
     """D-GADMM in one persistent launch (per-epoch chains in device tables) == the epoch-by-epoch
     engine: same iterations, bit-identical objective trace, same communication-energy trace, and the
-    schedule left in the same state."""
+    schedule left in the same state. coh = 1 re-chains every iteration: a head's pending-dual flush
+    reads its OLD tails' theta while they may already run ahead (the ring-slotted theta table)."""
     import numpy as np
     from gadmm_amd.models import LinearRegression
     from gadmm_amd.algorithms import dynamic_group_admm
@@ -319,8 +321,8 @@ def test_dgadmm_persistent_dynamic_matches_epoch_path(lin24, lin_obj0):
 
     m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
     p0, c0, _ = T.find_path(24, np.random.default_rng(5))
-    a = dynamic_group_admm(m, 1.0, lin_obj0, 1e-4, 3000, p0, c0, 10, seed=99)
-    b = dynamic_group_admm(m, 1.0, lin_obj0, 1e-4, 3000, p0, c0, 10, seed=99, engine_opts={"persistent": False})
+    a = dynamic_group_admm(m, 1.0, lin_obj0, 1e-4, 3000, p0, c0, coh, seed=99)
+    b = dynamic_group_admm(m, 1.0, lin_obj0, 1e-4, 3000, p0, c0, coh, seed=99, engine_opts={"persistent": False})
     assert a.extra["engine"] == "persistent-dynamic" and b.extra["engine"] == "epochs"
     assert a.iters == b.iters and a.converged
     assert np.array_equal(a.obj, b.obj)
