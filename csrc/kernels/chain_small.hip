@@ -711,6 +711,39 @@ int gadmm_chain_monitor(ChainCtl* ctl, const double* reduced, int ring, double* 
   return 0;
 }
 
+// Fresh-solve reset in ONE launch (was four torch fills + the control reset): theta, mu, part = 0,
+// trace = NaN, control block as chain_reset_kernel.
+__global__ void chain_reset_state_kernel(ChainCtl* ctl, int start_iter, int pending, double* theta, long n_theta,
+                                         double* mu, long n_mu, double* trace, long n_trace, double* part,
+                                         long n_part) {
+  const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x, step = (long)gridDim.x * blockDim.x;
+  for (long i = i0; i < n_theta; i += step) theta[i] = 0.0;
+  for (long i = i0; i < n_mu; i += step) mu[i] = 0.0;
+  for (long i = i0; i < n_part; i += step) part[i] = 0.0;
+  const double qnan = __longlong_as_double(0x7ff8000000000000ll);
+  for (long i = i0; i < n_trace; i += step) trace[i] = qnan;
+  if (i0 == 0) {
+    ctl->iter = start_iter;
+    ctl->done = 0;
+    ctl->conv_iter = 0;
+    ctl->pending = pending;
+    ctl->ticket = 0u;
+    ctl->monitored = start_iter - 1;
+  }
+}
+
+int gadmm_chain_reset_state(ChainCtl* ctl, int start_iter, int pending, double* theta, long n_theta, double* mu,
+                            long n_mu, double* trace, long n_trace, double* part, long n_part, hipStream_t st) {
+  long mx = n_theta > n_mu ? n_theta : n_mu;
+  mx = mx > n_trace ? mx : n_trace;
+  int blocks = (int)((mx + 255) / 256);
+  blocks = blocks < 1 ? 1 : (blocks > 64 ? 64 : blocks);
+  hipLaunchKernelGGL(chain_reset_state_kernel, dim3(blocks), dim3(256), 0, st, ctl, start_iter, pending, theta,
+                     n_theta, mu, n_mu, trace, n_trace, part, n_part);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
 int gadmm_chain_reset(ChainCtl* ctl, int start_iter, int pending, hipStream_t st) {
   hipLaunchKernelGGL(chain_reset_kernel, dim3(1), dim3(64), 0, st, ctl, start_iter, pending);
   GADMM_CHECK(hipGetLastError());

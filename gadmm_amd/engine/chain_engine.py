@@ -156,11 +156,17 @@ class NativeChainEngine:
         else:
             shifts, self.deg_to_var = [rho, 2.0 * rho], (0, 0, 1)
         self.nvar = len(shifts)
-        sh = torch.tensor(shifts, dtype=torch.float64, device=self.device)
+        key = (tuple(shifts), self.A.shape[0])
+        if getattr(self, "_shift_key", None) != key:  # (N, V) shifts + status word, built once per rho
+            self._shift_key = key
+            self._shifts = torch.tensor(shifts, dtype=torch.float64, device=self.device).unsqueeze(0).expand(
+                self.A.shape[0], -1).contiguous()
+            self._inv_status = torch.zeros((1,), dtype=torch.int32, device=self.device)
+        st = None if check else self._inv_status  # the cached word only where nobody reads it back
         if in_place and self.Minv is not None:
-            spd_inverse(self.A, sh, out=self.Minv, check_status=check)
+            spd_inverse(self.A, self._shifts, out=self.Minv, check_status=check, status=st)
         else:
-            self.Minv = spd_inverse(self.A, sh, check_status=check)
+            self.Minv = spd_inverse(self.A, self._shifts, check_status=check, status=st)
 
     def refresh(self, X_loc: torch.Tensor, y_loc: torch.Tensor):
         """Recompute the loop-invariant set-up (Gram + cached inverses) from the raw shards, in place
@@ -232,13 +238,13 @@ class NativeChainEngine:
         native.check(rc, "set_plan")
 
     def reset(self, start_iter: int = 1, pending: int = 0, zero_state: bool = True):
-        with torch.cuda.stream(self.stream):
-            if zero_state:
-                self.theta.zero_()
-                self.mu.zero_()
-                self.trace.fill_(float("nan"))
-                self.part.zero_()
-        native.check(self.lib.gadmm_chain_engine_reset(self.handle, int(start_iter), int(pending)), "reset")
+        if zero_state:  # theta = mu = part = 0, trace = NaN and the control block: one launch
+            native.check(self.lib.gadmm_chain_reset_state(
+                self.ctl.data_ptr(), int(start_iter), int(pending), self.theta.data_ptr(), self.theta.numel(),
+                self.mu.data_ptr(), self.mu.numel(), self.trace.data_ptr(), self.trace.numel(),
+                self.part.data_ptr(), self.part.numel(), self.stream.cuda_stream), "reset_state")
+        else:
+            native.check(self.lib.gadmm_chain_engine_reset(self.handle, int(start_iter), int(pending)), "reset")
 
     def exchange(self, which: str = "tail"):
         """Eager neighbour exchange with the current plan ('head' or 'tail' messages)."""

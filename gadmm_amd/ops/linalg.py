@@ -71,12 +71,14 @@ def spd_inverse_torch(A: torch.Tensor, shifts: torch.Tensor) -> torch.Tensor:
 
 
 def spd_inverse(A: torch.Tensor, shifts: torch.Tensor, out: Optional[torch.Tensor] = None,
-                check_status: bool = True) -> torch.Tensor:
-    """``(N, V, d, d)`` inverses of ``A_n + shifts[n, v] I`` (all SPD); ``out`` written in place."""
+                check_status: bool = True, status: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``(N, V, d, d)`` inverses of ``A_n + shifts[n, v] I`` (all SPD); ``out`` written in place.
+    ``status``: optional preallocated int32 word (the not-SPD flag; sticky once set)."""
     shifts = torch.as_tensor(shifts, dtype=torch.float64, device=A.device)
     if shifts.dim() == 1:
         shifts = shifts.unsqueeze(0).expand(A.shape[0], -1)
-    shifts = shifts.contiguous()
+    if not shifts.is_contiguous():
+        shifts = shifts.contiguous()
     N, d, _ = A.shape
     V = shifts.shape[1]
     if not A.is_cuda or d > 128:
@@ -88,7 +90,8 @@ def spd_inverse(A: torch.Tensor, shifts: torch.Tensor, out: Optional[torch.Tenso
     lib = native.require()
     if out is None:
         out = torch.empty((N, V, d, d), dtype=torch.float64, device=A.device)
-    status = torch.zeros((1,), dtype=torch.int32, device=A.device)
+    if status is None:
+        status = torch.zeros((1,), dtype=torch.int32, device=A.device)
     rc = lib.gadmm_spd_inverse_small_f64(A.contiguous().data_ptr(), shifts.data_ptr(), N, d, V, out.data_ptr(),
                                          status.data_ptr(), native.stream_handle())
     native.check(rc, "spd_inverse_small_f64")
