@@ -135,3 +135,43 @@ extern "C" int gadmm_spd_inverse_small_f64(const double* A, const double* shift,
   GADMM_CHECK(hipGetLastError());
   return 0;
 }
+
+// ---- test entry: the split-column quad GEMV (quad_gemv.h) on a batch of matrices ----------------
+// y[b] = M[b] x[b] for row-major M[b] (rows x cols, both <= 64), one wave per matrix: lets the test
+// suite check the device function every persistent kernel uses against a torch reference.
+#include "quad_gemv.h"
+
+namespace {
+template <int T>
+__global__ void __launch_bounds__(64) quad_gemv_test_kernel(const double* M, const double* x, double* y, int rows,
+                                                            int cols) {
+  __shared__ __attribute__((aligned(16))) double st[QSTAGE];
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const double* Mb = M + (long)b * rows * cols;
+  double m[4][T];
+  const int i = lane & 15, c = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int row = i + 16 * r, col = c + 4 * t;
+      m[r][t] = (row < rows && col < cols) ? Mb[(long)row * cols + col] : 0.0;
+    }
+  const double xv = lane < cols ? x[(long)b * cols + lane] : 0.0;
+  const double v = quad_gemv<T>(m, xv, st);
+  if (lane < rows) y[(long)b * rows + lane] = v;
+}
+}  // namespace
+
+extern "C" int gadmm_quad_gemv_test(const double* M, const double* x, double* y, int batch, int rows, int cols,
+                                    hipStream_t st) {
+  if (rows < 1 || rows > 64 || cols < 1 || cols > 64 || batch < 1) {
+    gadmm_set_error("quad_gemv_test: rows/cols must be in [1, 64]");
+    return -1;
+  }
+  if (cols <= 32) hipLaunchKernelGGL(quad_gemv_test_kernel<8>, dim3(batch), dim3(64), 0, st, M, x, y, rows, cols);
+  else if (cols <= 52) hipLaunchKernelGGL(quad_gemv_test_kernel<13>, dim3(batch), dim3(64), 0, st, M, x, y, rows, cols);
+  else hipLaunchKernelGGL(quad_gemv_test_kernel<16>, dim3(batch), dim3(64), 0, st, M, x, y, rows, cols);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}

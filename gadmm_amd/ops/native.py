@@ -152,6 +152,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_fo_lds": (c_long, [c_int, c_int, c_int]),
         "gadmm_fo_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
         "gadmm_fo_launch": (c_int, [ctypes.POINTER(FoArgs), c_void_p]),
+        "gadmm_quad_gemv_test": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
         "gadmm_greedy_chains": (c_int, [c_void_p, c_int, c_int, c_double, c_int, c_double, c_double, c_double,
                                         c_void_p, c_void_p]),
         "gadmm_rccl_unique_id": (c_int, [ctypes.c_char_p]),

@@ -56,6 +56,23 @@ def test_spd_inverse_kernel(d):
     assert _rel(inv, ref) < 1e-11
 
 
+@pytest.mark.parametrize("rows,cols", [(50, 50), (14, 14), (34, 36), (64, 64), (5, 61), (63, 3)])
+def test_quad_gemv_matches_torch(rows, cols):
+    """The split-column register GEMV (csrc/include/quad_gemv.h) == the fp64 torch product (its
+    bit-identity with the other engines' summation order is checked through the engine traces)."""
+    from gadmm_amd.ops import native
+    lib = native.require()
+    g = torch.Generator().manual_seed(rows * 100 + cols)
+    M = torch.randn(7, rows, cols, dtype=torch.float64, generator=g)
+    x = torch.randn(7, cols, dtype=torch.float64, generator=g)
+    Md, xd = M.to(DEV), x.to(DEV)
+    y = torch.empty(7, rows, dtype=torch.float64, device=DEV)
+    native.check(lib.gadmm_quad_gemv_test(Md.data_ptr(), xd.data_ptr(), y.data_ptr(), 7, rows, cols,
+                                          torch.cuda.current_stream().cuda_stream), "quad_gemv_test")
+    ref = torch.einsum("brc,bc->br", M, x)
+    assert _rel(y.cpu(), ref) < 1e-14
+
+
 @pytest.mark.parametrize("d", [7, 50, 64])
 def test_spd_inverse_gj64_bit_identical(d, monkeypatch):
     """The 64-wide Gauss-Jordan (d <= 64) reproduces the general kernel bit for bit."""
@@ -135,6 +152,23 @@ def test_engine_logistic(log24, log_obj0):
     eng.reset()
     eng.set_targets(log_obj0, 1e-4)
     assert eng.run(use_graph=False).iters == 53
+
+
+def test_logistic_register_kernel_trace_matches_torch(log24, log_obj0):
+    """chain_phase_logistic_quad (shard + transpose in VGPRs) follows the torch inexact-GD path
+    (logReg_GD.m semantics) iteration by iteration, not only in the final count."""
+    import numpy as np
+    from gadmm_amd.models import LogisticRegression
+    from gadmm_amd.algorithms import chain_admm
+    eng = _engine(log24, 2e-4, log_obj0, 1e-4, model="logistic", lam=1e-5, step=2.2, max_inner=100, inner_tol=1e-4,
+                  max_iter=400, block=8)
+    r = eng.run()
+    tr = eng.objective_trace(r.iters)
+    m = LogisticRegression(log24.X, log24.y, lam=1e-5)
+    t = chain_admm(m, list(range(24)), 24, 2e-4, log_obj0, 1e-4, 400, local_solver="gd", step=2.2, max_inner=100,
+                   inner_tol=1e-4, backend="torch")
+    assert r.iters == t.iters == 53
+    assert np.allclose(tr, t.obj, rtol=1e-11, atol=0)
 
 
 def test_chain_admm_auto_native_matches_torch(lin24, lin_obj0):
