@@ -106,7 +106,7 @@ struct PersistArgs {
   int deg_to_var[3];
   int pending_in, has_monitor, nranks, sys_scope;
   unsigned epoch;           // salts every tag: tag = epoch << 20 | iteration (no re-zeroing between solves)
-  int pad_;
+  int blk_pw;               // temporal blocking: chain positions per wave (1: 12-wave kernel, 2: paired 8-wave)
   double rho, obj0, tol;
   long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
   const PhaseSlot* slots;   // [n_local] (li, gid, left, right) in launch order

@@ -54,3 +54,62 @@ __device__ __forceinline__ double quad_gemv(const double (&m)[4][T], double x, d
   asm volatile("" ::: "memory");  // the next call's writes stay behind these reads
   return ((q0 + q1) + q2) + q3;
 }
+
+// Paired layout for two matrices with <= 52 rows held by one wave (chain_blocked_pair_kernel):
+// each keeps its row groups r = 0..2 (rows i + 16r) as in quad_load, and the two share ONE register
+// block for rows 48..51: lanes with i < 4 hold matrix 0's row 48 + i, lanes with 4 <= i < 8 hold
+// matrix 1's row 48 + (i - 4). 3T + 3T + T doubles per lane instead of 8T (T = 13: 182 VGPRs, so
+// two waves per SIMD fit in the 256-register budget). Same per-row accumulation order as quad_gemv.
+template <int T>
+__device__ __forceinline__ void quad_load_pair(double (&m0)[3][T], double (&m1)[3][T], double (&s3)[T],
+                                               const double* M0, const double* M1, int d, bool on0, bool on1) {
+  const int lane = threadIdx.x & 63, i = lane & 15, c = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 3; ++r)
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int row = i + 16 * r, col = c + 4 * t;
+      m0[r][t] = (on0 && row < d && col < d) ? M0[(long)row * d + col] : 0.0;
+      m1[r][t] = (on1 && row < d && col < d) ? M1[(long)row * d + col] : 0.0;
+    }
+  const int q = i & 3, which = i >> 2;  // which = 0: matrix 0, 1: matrix 1, else unused
+  const double* Ms = which == 0 ? M0 : M1;
+  const bool ons = (which == 0 && on0) || (which == 1 && on1);
+#pragma unroll
+  for (int t = 0; t < T; ++t) {
+    const int row = 48 + q, col = c + 4 * t;
+    s3[t] = (ons && row < d && col < d) ? Ms[(long)row * d + col] : 0.0;
+  }
+}
+
+// y_l = (M_sel x)_l for the paired layout (sel = 0 / 1, wave-uniform), lane l in, lane l out.
+template <int T>
+__device__ __forceinline__ double quad_gemv_pair(const double (&m)[3][T], const double (&s3)[T], int sel, double x,
+                                                 double* st) {
+  static_assert(T >= 1 && T <= 13, "paired layout covers d <= 52");
+  const int lane = threadIdx.x & 63, i = lane & 15, c = lane >> 4;
+  st[(lane & 3) * QX + (lane >> 2)] = x;
+  asm volatile("" ::: "memory");
+  const double* xs = st + c * QX;
+  double p[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int t = 0; t < T; t += 2) {
+    const double2 xp = *reinterpret_cast<const double2*>(xs + t);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) p[r] = fma(m[r][t], xp.x, p[r]);
+    p[3] = fma(s3[t], xp.x, p[3]);
+    if (t + 1 < T) {
+#pragma unroll
+      for (int r = 0; r < 3; ++r) p[r] = fma(m[r][t + 1], xp.y, p[r]);
+      p[3] = fma(s3[t + 1], xp.y, p[3]);
+    }
+  }
+  double* red = st + 4 * QX;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) red[c * QR + i + 16 * r] = p[r];
+  if ((i >> 2) == sel) red[c * QR + 48 + (i & 3)] = p[3];
+  asm volatile("" ::: "memory");
+  const double q0 = red[lane], q1 = red[QR + lane], q2 = red[2 * QR + lane], q3 = red[3 * QR + lane];
+  asm volatile("" ::: "memory");
+  return ((q0 + q1) + q2) + q3;
+}

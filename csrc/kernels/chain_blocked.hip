@@ -38,6 +38,92 @@ constexpr int MAXW = 12;  // computed workers (waves) per workgroup: 3 waves per
 
 }  // namespace
 
+// ---- monitor workgroup (same protocol as chain_persistent): sums f_n in worker order, records the
+// trace and posts the stop decision of every iteration to every rank's decision ring
+template <bool SYS, bool TL>
+__device__ __forceinline__ void blocked_monitor(const PersistArgs& a, double* lds, int v, int lane,
+                                                unsigned long long deadline, __amdgpu_buffer_rsrc_t rob) {
+  const int n = a.n;
+  if (v != 0) return;
+  double* vals = lds;  // [n]
+  for (int it = a.start_iter;; ++it) {
+    const unsigned tag = make_tag(a.epoch, it);
+    const int slot = it % a.ring;
+    bool okall = true;
+    for (int w = lane; w < n; w += 64) {
+      double val = 0.0;
+      for (int spin = 0;; ++spin) {
+        if (load_granule<SYS>(rob, (slot * n + w) * 16, tag, &val)) break;
+        if ((spin & 7) == 7 && now_ticks() > deadline) {
+          okall = false;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      vals[w] = val;
+    }
+    const bool ok = __all(okall);
+    unsigned code = 0;
+    if (lane == 0) {
+      if (!ok) {
+        code = 4;
+      } else {
+        double s = 0.0;
+        for (int w = 0; w < n; ++w) s += vals[w];  // worker order: == the other engines
+        if (it - 1 < a.max_iter) a.trace[it - 1] = s;
+        if (!(s == s) || isinf(s)) code = 3;
+        else if (fabs(s - a.obj0) < a.tol) code = 1;
+        else if (it >= a.max_iter) code = 2;
+      }
+      const unsigned long long dv = ((unsigned long long)tag << 32) | code;
+      for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
+      const int kk = it - a.start_iter;
+      if (TL && kk < a.timeline_iters) a.timeline[((long)blockIdx.x * a.timeline_iters + kk) * 8] = (long long)now_ticks();
+    }
+    if (__shfl((int)code, 0, 64)) return;
+  }
+}
+
+// ---- objective workgroup: wave v evaluates f_q(theta_q^it) of owned chain position q (A_q in VGPRs,
+// quad layout) off the critical path and posts it to the monitor ring
+template <int QT, bool SYS>
+__device__ __forceinline__ void blocked_objective(const PersistArgs& a, double* lds, int v, int lane, int q,
+                                                  unsigned long long deadline, __amdgpu_buffer_rsrc_t rob,
+                                                  __amdgpu_buffer_rsrc_t rtab) {
+  const int d = a.d, n = a.n;
+  const long ring_base = 2L * n * 2 * d;  // theta ring [ring][n][d] after the exchange table
+  const PhaseSlot so = a.slots[q];
+  const bool in = lane < d;
+  double Aq[4][QT];
+  quad_load<QT>(Aq, a.A + (long)so.li * d * d, d, true);
+  const double bo = in ? a.b[(long)so.li * d + lane] : 0.0;
+  const double hy = 0.5 * a.yy[so.li];
+  double* xo = lds + v * QSTAGE;
+  for (int it = a.start_iter;; ++it) {
+    const unsigned tag = make_tag(a.epoch, it);
+    const long off = (ring_base + ((long)(it % a.ring) * n + q) * d + lane) * 16;
+    double x = 0.0;
+    for (int spin = 0;; ++spin) {
+      const bool ok = !in || load_granule<SYS>(rtab, (int)off, tag, &x);
+      if (__all(ok)) break;
+      if ((spin & 7) == 7) {
+        // the run ended: the workers stop at iteration j + lag after a stop decision for j, so
+        // theta^it never comes once decision[it - lag] says stop (on every rank's own ring)
+        if (it - a.start_iter >= a.lag) {
+          const unsigned long long dv = load_dec<SYS>(&a.decg[(it - a.lag) % a.ring]);
+          if ((unsigned)(dv >> 32) == make_tag(a.epoch, it - a.lag) && (unsigned)(dv & 0xffffffffu) != 0u) return;
+        }
+        if (now_ticks() > deadline) return;  // the monitor times out and reports it
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const double qv = quad_gemv<QT>(Aq, in ? x : 0.0, xo);  // (A th)_i in the order of every other engine
+    const double part = in ? (0.5 * qv - bo) * x : 0.0;
+    const double f = wave_sum_f64(part) + hy;
+    if (lane == 0) store_granule<SYS>(rob, ((it % a.ring) * n + so.gid) * 16, tag, f);
+  }
+}
+
 // DB: register row length (multiple of 4, >= d); 52 keeps d = 50 within the 3-waves-per-SIMD budget.
 // SYS: multi-GPU (xGMI fabric): system-scope granules in IPC fine-grained memory; this rank owns
 // chain positions [seg_lo, seg_hi] and pushes owned (theta, mu) into its peers' exchange tables.
@@ -69,82 +155,15 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   lds_barrier();
 
   if ((int)blockIdx.x == W + Wo) {
-    // ------------------------------------------------------------- monitor (same as chain_persistent)
-    if (v != 0) return;
-    double* vals = lds;  // [n]
-    for (int it = a.start_iter;; ++it) {
-      const unsigned tag = make_tag(a.epoch, it);
-      const int slot = it % a.ring;
-      bool okall = true;
-      for (int w = lane; w < n; w += 64) {
-        double val = 0.0;
-        for (int spin = 0;; ++spin) {
-          if (load_granule<SYS>(rob, (slot * n + w) * 16, tag, &val)) break;
-          if ((spin & 7) == 7 && now_ticks() > deadline) {
-            okall = false;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        vals[w] = val;
-      }
-      const bool ok = __all(okall);
-      unsigned code = 0;
-      if (lane == 0) {
-        if (!ok) {
-          code = 4;
-        } else {
-          double s = 0.0;
-          for (int w = 0; w < n; ++w) s += vals[w];  // worker order: == the other engines
-          if (it - 1 < a.max_iter) a.trace[it - 1] = s;
-          if (!(s == s) || isinf(s)) code = 3;
-          else if (fabs(s - a.obj0) < a.tol) code = 1;
-          else if (it >= a.max_iter) code = 2;
-        }
-        const unsigned long long dv = ((unsigned long long)tag << 32) | code;
-        for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
-        const int kk = it - a.start_iter;
-        if (TL && kk < a.timeline_iters) a.timeline[((long)blockIdx.x * a.timeline_iters + kk) * 8] = (long long)now_ticks();
-      }
-      if (__shfl((int)code, 0, 64)) return;
-    }
+    blocked_monitor<SYS, TL>(a, lds, v, lane, deadline, rob);
+    return;
   }
 
   const long ring_base = 2L * n * 2 * d;  // theta ring [ring][n][d] after the exchange table
   if ((int)blockIdx.x >= W) {
-    // ----------------------------------------------------------------- objective workgroup
     const int q = seg_lo + ((int)blockIdx.x - W) * MAXW + v;  // an owned chain position
-    if (q > seg_hi) return;
-    const PhaseSlot so = a.slots[q];
-    const bool in = lane < d;
-    double Aq[4][QT];
-    quad_load<QT>(Aq, a.A + (long)so.li * d * d, d, true);
-    const double bo = in ? a.b[(long)so.li * d + lane] : 0.0;
-    const double hy = 0.5 * a.yy[so.li];
-    double* xo = lds + v * QSTAGE;
-    for (int it = a.start_iter;; ++it) {
-      const unsigned tag = make_tag(a.epoch, it);
-      const long off = (ring_base + ((long)(it % a.ring) * n + q) * d + lane) * 16;
-      double x = 0.0;
-      for (int spin = 0;; ++spin) {
-        const bool ok = !in || load_granule<SYS>(rtab, (int)off, tag, &x);
-        if (__all(ok)) break;
-        if ((spin & 7) == 7) {
-          // the run ended: the workers stop at iteration j + lag after a stop decision for j, so
-          // theta^it never comes once decision[it - lag] says stop (on every rank's own ring)
-          if (it - a.start_iter >= a.lag) {
-            const unsigned long long dv = load_dec<SYS>(&a.decg[(it - a.lag) % a.ring]);
-            if ((unsigned)(dv >> 32) == make_tag(a.epoch, it - a.lag) && (unsigned)(dv & 0xffffffffu) != 0u) return;
-          }
-          if (now_ticks() > deadline) return;  // the monitor times out and reports it
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      const double qv = quad_gemv<QT>(Aq, in ? x : 0.0, xo);  // (A th)_i in the order of every other engine
-      const double part = in ? (0.5 * qv - bo) * x : 0.0;
-      const double f = wave_sum_f64(part) + hy;
-      if (lane == 0) store_granule<SYS>(rob, ((it % a.ring) * n + so.gid) * 16, tag, f);
-    }
+    if (q <= seg_hi) blocked_objective<QT, SYS>(a, lds, v, lane, q, deadline, rob, rtab);
+    return;
   }
 
   // ---------------------------------------------------------------------- worker workgroup
@@ -378,6 +397,251 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Paired-wave variant (PW = 2, opt-in: GADMM_BLOCK_PW=2): a workgroup of PWW = 8 waves computes up to 16 chain positions, wave
+// v the adjacent pair (2v, 2v + 1) = one head + one tail, with BOTH rows of (A + deg rho I)^{-1} in
+// VGPRs (2 x 52 doubles at 2 waves per SIMD). Every phase then runs exactly one GEMV per wave, two
+// per SIMD on all four SIMDs (the 12-wave kernel runs 2,2,1,1), and 16 positions allow k = 3
+// (L = 4 owned + 2 x 6 halo): one cross-CU (or cross-GPU) exchange per 3 iterations instead of 2.
+// Same arithmetic and stop protocol as chain_blocked_kernel (bit-identical traces).
+constexpr int PWW = 8;            // waves per workgroup
+constexpr int PCAP = 2 * PWW;     // computed positions per workgroup
+
+template <int DB, bool SYS>
+__global__ void __launch_bounds__(64 * PWW) chain_blocked_pair_kernel(PersistArgs a) {
+  constexpr int QT = DB / 4;
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ int abort_lds, stop_lds, stop_iter_lds;
+  const int d = a.d, n = a.n;
+  const int lane = threadIdx.x & 63;
+  const int v = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int k = a.blk_k, L = a.blk_len, H = 2 * a.blk_k;
+  const bool multi = a.nranks > 1;
+  const int seg_lo = multi ? a.seg_lo : 0, seg_hi = multi ? a.seg_hi : n - 1;
+  const int nseg = seg_hi - seg_lo + 1;
+  const int W = (nseg + L - 1) / L;
+  const int Wo = (nseg + PWW - 1) / PWW;
+  const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
+  const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
+  const __amdgpu_buffer_rsrc_t rtab = rsrc_of(a.blk_tab);
+  if (threadIdx.x == 0) {
+    abort_lds = 0;
+    stop_lds = 0;
+    stop_iter_lds = 0;
+  }
+  lds_barrier();
+  if ((int)blockIdx.x == W + Wo) {
+    blocked_monitor<SYS, false>(a, lds, v, lane, deadline, rob);
+    return;
+  }
+  const long ring_base = 2L * n * 2 * d;
+  if ((int)blockIdx.x >= W) {
+    const int q = seg_lo + ((int)blockIdx.x - W) * PWW + v;
+    if (q <= seg_hi) blocked_objective<QT, SYS>(a, lds, v, lane, q, deadline, rob, rtab);
+    return;
+  }
+
+  // ---------------------------------------------------------------------- worker workgroup
+  const int g = blockIdx.x;
+  const int s0 = seg_lo + g * L, e0 = min(seg_hi + 1, s0 + L) - 1;  // owned chain positions [s0, e0]
+  const int ra = max(0, s0 - H), rb = min(n - 1, e0 + H);
+  const int nv = rb - ra + 1;
+  // this wave's head / tail local positions (ra + u is a head iff even)
+  const int uA = 2 * v;
+  const bool aHead = ((ra + uA) & 1) == 0;
+  const int uH = aHead ? uA : uA + 1, uT = aHead ? uA + 1 : uA;
+  const bool actH = uH < nv, actT = uT < nv;
+  const int pH = ra + uH, pT = ra + uT;
+  const bool ownH = actH && pH >= s0 && pH <= e0, ownT = actT && pT >= s0 && pT <= e0;
+  const PhaseSlot slH = a.slots[actH ? pH : 0], slT = a.slots[actT ? pT : 0];
+  const bool hlH = actH && slH.left >= 0, hrH = actH && slH.right >= 0;
+  const bool hlT = actT && slT.left >= 0, hrT = actT && slT.right >= 0;
+  const double rho = a.rho;
+  const bool in = lane < d;
+  // decision wave: one whose positions are both halo (no granule stores queue ahead of its load)
+  int vdec = 0;
+  for (int vv = PWW - 1; vv >= 0; --vv) {
+    const int pa = ra + 2 * vv, pb = pa + 1;
+    if (2 * vv + 1 < nv && (pa < s0 || pa > e0) && (pb < s0 || pb > e0)) vdec = vv;
+  }
+  const bool dec_wave = v == vdec;
+
+  double* thS = lds;                        // [PCAP][64] theta of every computed position
+  double* bbS = thS + PCAP * 64;            // [PCAP][64] b of every computed position
+  double* myx = bbS + PCAP * 64 + v * QSTAGE;  // [PWW][QSTAGE] quad GEMV staging
+  const bool nblH = hlH && uH > 0, nbrH = hrH && uH + 1 < nv;
+  const bool nblT = hlT && uT > 0, nbrT = hrT && uT + 1 < nv;
+
+  double MH[3][QT], MT[3][QT], M3[QT];  // paired layout: rows 48..51 of both in one shared block
+  quad_load_pair<QT>(MH, MT, M3,
+                     a.Minv + ((long)slH.li * a.nvar + a.deg_to_var[(int)hlH + (int)hrH]) * (long)d * d,
+                     a.Minv + ((long)slT.li * a.nvar + a.deg_to_var[(int)hlT + (int)hrT]) * (long)d * d, d, actH,
+                     actT);
+  double thH = (actH && in) ? a.theta[(long)slH.gid * d + lane] : 0.0;
+  double muH = (actH && in) ? a.mu[(long)slH.li * d + lane] : 0.0;
+  double thT = (actT && in) ? a.theta[(long)slT.gid * d + lane] : 0.0;
+  double muT = (actT && in) ? a.mu[(long)slT.li * d + lane] : 0.0;
+  if (actH) {
+    thS[uH * 64 + lane] = thH;
+    bbS[uH * 64 + lane] = in ? a.b[(long)slH.li * d + lane] : 0.0;
+  }
+  if (actT) {
+    thS[uT * 64 + lane] = thT;
+    bbS[uT * 64 + lane] = in ? a.b[(long)slT.li * d + lane] : 0.0;
+  }
+  int pending = a.pending_in;
+  lds_barrier();
+
+  auto publish = [&](int j, int p, double th, double mu) {
+    const unsigned tag = make_tag(a.epoch, j + 1);
+    const int base = (((((j + 1 - a.start_iter) / k) & 1) * n + p) * 2) * d;
+    store_granule<SYS>(rtab, (base + lane) * 16, tag, th);
+    store_granule<SYS>(rtab, (base + d + lane) * 16, tag, mu);
+    for (int q = 0; q < a.blk_npeer; ++q)
+      if (p >= a.blk_peer_lo[q] && p <= a.blk_peer_hi[q]) {
+        const __amdgpu_buffer_rsrc_t rpe = rsrc_of(a.blk_peer_tab[q]);
+        store_granule<SYS>(rpe, (base + lane) * 16, tag, th);
+        store_granule<SYS>(rpe, (base + d + lane) * 16, tag, mu);
+      }
+  };
+  unsigned long long dv_pref = 0;
+  int it = a.start_iter;
+  for (;; ++it) {
+    if (it > a.max_iter + a.lag) break;
+    // ---- halo exchange every k iterations: both of the wave's halo positions in one poll loop
+    if (it > a.start_iter && (it - a.start_iter) % k == 0) {
+      const bool needH = actH && !ownH, needT = actT && !ownT;
+      if (needH || needT) {
+        const unsigned tag = make_tag(a.epoch, it);
+        const int bsel = ((it - a.start_iter) / k) & 1;
+        const int baseH = ((bsel * n + pH) * 2) * d, baseT = ((bsel * n + pT) * 2) * d;
+        double h0 = 0.0, h1 = 0.0, t0 = 0.0, t1 = 0.0;
+        bool ok = true;
+        for (int spin = 0;; ++spin) {
+          bool g0 = true;
+          if (in && needH) {
+            g0 &= load_granule<SYS>(rtab, (baseH + lane) * 16, tag, &h0);
+            g0 &= load_granule<SYS>(rtab, (baseH + d + lane) * 16, tag, &h1);
+          }
+          if (in && needT) {
+            g0 &= load_granule<SYS>(rtab, (baseT + lane) * 16, tag, &t0);
+            g0 &= load_granule<SYS>(rtab, (baseT + d + lane) * 16, tag, &t1);
+          }
+          if (__all(g0)) break;
+          if ((spin & 7) == 7 && now_ticks() > deadline) {
+            ok = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (!ok && lane == 0) abort_lds = 1;
+        if (needH) {
+          thH = in ? h0 : 0.0;
+          muH = in ? h1 : 0.0;
+          thS[uH * 64 + lane] = thH;
+        }
+        if (needT) {
+          thT = in ? t0 : 0.0;
+          muT = in ? t1 : 0.0;
+          thS[uT * 64 + lane] = thT;
+        }
+      }
+      lds_barrier();
+      if (abort_lds) break;
+    }
+
+    // ---- head phase: every wave solves its head
+    if (actH) {
+      const double tl = nblH ? thS[(uH - 1) * 64 + lane] : 0.0, tr = nbrH ? thS[(uH + 1) * 64 + lane] : 0.0;
+      double m = muH;
+      if (pending) {  // lazy end-of-iteration dual (reference order)
+        if (hlH) m = m - rho * (tl - thH);
+        if (hrH) m = m + rho * (thH - tr);
+      }
+      muH = m;
+      double r = bbS[uH * 64 + lane] - m;
+      if (hlH) r = r + rho * tl;
+      if (hrH) r = r + rho * tr;
+      const double y = quad_gemv_pair<QT>(MH, M3, 0, in ? r : 0.0, myx);
+      thH = in ? y : 0.0;
+      thS[uH * 64 + lane] = thH;
+      if (ownH && in)
+        store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + pH) * d + lane) * 16),
+                           make_tag(a.epoch, it), thH);
+    }
+    pending = 1;
+    lds_barrier();
+
+    // ---- tail phase: every wave solves its tail; owned heads publish at an exchange boundary
+    const bool xnext = (it + 1 - a.start_iter) % k == 0;
+    if (actT) {
+      const double tl = nblT ? thS[(uT - 1) * 64 + lane] : 0.0, tr = nbrT ? thS[(uT + 1) * 64 + lane] : 0.0;
+      double r = bbS[uT * 64 + lane] - muT;
+      if (hlT) r = r + rho * tl;
+      if (hrT) r = r + rho * tr;
+      const double y = quad_gemv_pair<QT>(MT, M3, 1, in ? r : 0.0, myx);
+      const double tn = in ? y : 0.0;
+      double m = muT;
+      if (hlT) m = m - rho * (tl - tn);
+      if (hrT) m = m + rho * (tn - tr);
+      muT = m;
+      thT = tn;
+      thS[uT * 64 + lane] = thT;
+      if (ownT && in) {
+        store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + pT) * d + lane) * 16),
+                           make_tag(a.epoch, it), thT);
+        if (xnext) publish(it, pT, thT, muT);
+      }
+    }
+    if (ownH && xnext && in) publish(it, pH, thH, muH);  // theta^it and the (still pending) mu are final
+    if (dec_wave && lane == 0 && it + 1 - a.start_iter >= a.lag) {
+      const int jdec = it + 1 - a.lag;
+      const unsigned tj = make_tag(a.epoch, jdec);
+      unsigned long long dvv = dv_pref;  // prefetched one iteration ahead
+      if ((unsigned)(dvv >> 32) != tj) dvv = load_dec<SYS>(&a.decg[jdec % a.ring]);
+      for (int spin = 0; (unsigned)(dvv >> 32) != tj; ++spin) {
+        if ((spin & 7) == 7 && now_ticks() > deadline) {
+          abort_lds = 1;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        dvv = load_dec<SYS>(&a.decg[jdec % a.ring]);
+      }
+      const unsigned code = (unsigned)(dvv & 0xffffffffu);
+      if (code && (unsigned)(dvv >> 32) == tj) {
+        stop_lds = (int)code;
+        stop_iter_lds = jdec;
+      }
+      dv_pref = load_dec<SYS>(&a.decg[(jdec + 1) % a.ring]);
+    }
+    lds_barrier();
+    if (abort_lds || stop_lds) {
+      ++it;
+      break;
+    }
+  }
+
+  if (ownH && in) {
+    a.theta[(long)slH.gid * d + lane] = thH;
+    a.mu[(long)slH.li * d + lane] = muH;
+  }
+  if (ownT && in) {
+    a.theta[(long)slT.gid * d + lane] = thT;
+    a.mu[(long)slT.li * d + lane] = muT;
+  }
+  if (threadIdx.x == 0) {
+    if (abort_lds) {
+      a.ctl->done = 4;
+    } else if (g == 0 && stop_lds) {
+      a.ctl->done = stop_lds;
+      a.ctl->conv_iter = stop_iter_lds;
+      a.ctl->iter = it;
+      a.ctl->pending = 1;
+      a.ctl->monitored = stop_iter_lds;
+    }
+  }
+}
+
 extern "C" {
 
 // Pick (k, L) for n workers; returns the number of worker workgroups, 0 if not applicable.
@@ -402,6 +666,42 @@ int gadmm_chain_blocked_plan(int n, int d, int want_k, int* k_out, int* len_out)
   return W;
 }
 
+// Plan with the wave layout: pw = 1 (default: the 12-wave kernel, up to 12 positions per workgroup,
+// k = 2) or pw = 2 (GADMM_BLOCK_PW=2 or want_pw = 2: the paired 8-wave kernel, up to 16 positions,
+// k = 3). Measured on MI355X (profiles/r01c_pair_layout): pw = 2 exchanges a third less often but
+// its iteration is ~0.3 us longer (255 VGPRs, SGPR spills, the decision poll on a computing wave),
+// 2.80 vs 2.40 ms per E1 solve on one GPU and 3.58 vs 3.02 ms in the 2-rank rehearsal.
+int gadmm_chain_blocked_plan2(int n, int d, int want_k, int want_pw, int* k_out, int* len_out, int* pw_out) {
+  int pw = want_pw;
+  if (pw <= 0) {
+    const char* e = getenv("GADMM_BLOCK_PW");
+    pw = (e && e[0] == '2') ? 2 : 1;
+  }
+  if (pw == 1) {
+    *pw_out = 1;
+    return gadmm_chain_blocked_plan(n, d, want_k, k_out, len_out);
+  }
+  if (d > 52 || n < 2) return 0;
+  int k = want_k > 0 ? want_k : 3;
+  int len = PCAP - 4 * k;
+  while (len < 1 && k > 1) {
+    --k;
+    len = PCAP - 4 * k;
+  }
+  if (len < 1) return 0;
+  if (const char* e = getenv("GADMM_BLOCK_L")) {
+    const int want_len = atoi(e);
+    if (want_len >= 1 && want_len < len) len = want_len;
+  }
+  if (len > n) len = n;
+  const int W = (n + len - 1) / len;
+  if (W + (n + PWW - 1) / PWW + 1 > 256) return 0;
+  *k_out = k;
+  *len_out = len;
+  *pw_out = 2;
+  return W;
+}
+
 long gadmm_chain_blocked_lds(int d, int len) {
   (void)d;
   (void)len;
@@ -414,7 +714,8 @@ long gadmm_chain_blocked_tab_granules(int n, int d, int ring) { return 2L * n * 
 int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   const PersistArgs& a = *args;
   const bool multi = a.nranks > 1;
-  if (a.blk_k < 1 || a.blk_len < 1 || a.blk_len + 4 * a.blk_k > MAXW || a.d > 52 || !a.blk_tab || !a.dec_push ||
+  if (a.blk_k < 1 || a.blk_len < 1 || a.blk_len + 4 * a.blk_k > (a.blk_pw == 2 ? PCAP : MAXW) || a.d > 52 ||
+      !a.blk_tab || !a.dec_push ||
       (!multi && (!a.has_monitor || a.n != a.n_local)) ||
       (multi && (a.seg_lo < 0 || a.seg_hi < a.seg_lo || a.seg_hi >= a.n || a.blk_npeer < 0 || a.blk_npeer > 8 ||
                  (a.blk_npeer > 0 && !a.blk_peer_tab) || a.start_iter != 1 || a.pending_in != 0 || !a.sys_scope))) {
@@ -427,6 +728,29 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   }
   const int nseg = multi ? a.seg_hi - a.seg_lo + 1 : a.n;
   const int W = (nseg + a.blk_len - 1) / a.blk_len;
+  if (a.blk_pw == 2) {  // paired-wave kernel
+    if (a.blk_len + 4 * a.blk_k > PCAP || a.timeline) {
+      gadmm_set_error("blocked chain kernel (pw=2): L + 4k > %d or timeline requested", PCAP);
+      return -1;
+    }
+    const int Wo2 = (nseg + PWW - 1) / PWW;
+    const int blocks2 = W + Wo2 + (a.has_monitor ? 1 : 0);
+    if (blocks2 > 256) {
+      gadmm_set_error("blocked chain kernel: %d workgroups exceed one per CU", blocks2);
+      return -1;
+    }
+    long lds2 = (long)(2 * PCAP * 64 + PWW * QSTAGE) * 8;
+    if (lds2 < (long)a.n * 8) lds2 = (long)a.n * 8;
+    const void* fn2 = a.sys_scope ? (a.d <= 32 ? (const void*)chain_blocked_pair_kernel<32, true>
+                                               : (const void*)chain_blocked_pair_kernel<52, true>)
+                                  : (a.d <= 32 ? (const void*)chain_blocked_pair_kernel<32, false>
+                                               : (const void*)chain_blocked_pair_kernel<52, false>);
+    if (lds2 > 65536) GADMM_CHECK(hipFuncSetAttribute(fn2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
+    void* kargs2[] = {const_cast<PersistArgs*>(&a)};
+    GADMM_CHECK(hipLaunchKernel(fn2, dim3(blocks2), dim3(64 * PWW), kargs2, (size_t)lds2, st));
+    GADMM_CHECK(hipGetLastError());
+    return 0;
+  }
   const int Wo = (nseg + MAXW - 1) / MAXW;
   const int blocks = W + Wo + (a.has_monitor ? 1 : 0);
   if (blocks > 256) {

@@ -46,10 +46,11 @@ class BlockedXgmiEngine:
             raise ValueError("blocked xgmi engine needs contiguous segments")
         segs = [(min(placement.local_workers(r)), max(placement.local_workers(r))) for r in range(self.nranks)]
         nseg = max(hi - lo + 1 for lo, hi in segs)
-        kk, ll = ctypes.c_int(0), ctypes.c_int(0)
-        if int(self.lib.gadmm_chain_blocked_plan(nseg, self.d, int(want_k), ctypes.byref(kk), ctypes.byref(ll))) <= 0:
+        kk, ll, pp = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+        if int(self.lib.gadmm_chain_blocked_plan2(nseg, self.d, int(want_k), 0, ctypes.byref(kk), ctypes.byref(ll),
+                                                  ctypes.byref(pp))) <= 0:
             raise RuntimeError("blocked xgmi engine: no blocking plan for d=%d" % self.d)
-        self.k, self.L = kk.value, ll.value
+        self.k, self.L, self.pw = kk.value, ll.value, pp.value
         H = 2 * self.k
         self.H = H
         comp = [(max(0, lo - H), min(self.n - 1, hi + H)) for lo, hi in segs]
@@ -121,7 +122,7 @@ class BlockedXgmiEngine:
         self.peer_tab_t = torch.tensor(self.peer_ptrs + [0], dtype=torch.int64, device=device)
         self.dec_push_t = torch.tensor(self.dec_all, dtype=torch.int64, device=device)
         self.epoch = 0
-        self.last_kernel = "blocked-xgmi(k=%d,L=%d,H=%d,peers=%s)" % (self.k, self.L, H, self.peers)
+        self.last_kernel = "blocked-xgmi(k=%d,L=%d,H=%d,pw=%d,peers=%s)" % (self.k, self.L, H, self.pw, self.peers)
 
     def _open(self, hbytes: bytes, key) -> int:
         p = ctypes.c_void_p()
@@ -164,7 +165,7 @@ class BlockedXgmiEngine:
         pa.objg, pa.decg = self.objg_mon, self.decg.ptr.value
         pa.dec_push = self.dec_push_t.data_ptr()
         pa.trace, pa.ctl = self.trace.data_ptr(), self.ctl.data_ptr()
-        pa.blk_k, pa.blk_len = self.k, self.L
+        pa.blk_k, pa.blk_len, pa.blk_pw = self.k, self.L, self.pw
         pa.blk_tab = self.tab.ptr.value
         pa.seg_lo, pa.seg_hi = self.seg_lo, self.seg_hi
         pa.blk_npeer = len(self.peers)

@@ -289,17 +289,19 @@ class NativeChainEngine:
             return False
         return int(self.lib.gadmm_chain_persistent_lds_dyn(self.d, self._obj_mode(True), self.nvar)) > 0
 
-    def blocked_plan(self, fabric=None):
-        """(k, L, W) of the temporally blocked kernel for this engine, or None (multi-GPU, d > 64,
-        GADMM_BLOCKED=0)."""
+    def blocked_plan(self, fabric=None, timeline: bool = False):
+        """(k, L, W, pw) of the temporally blocked kernel for this engine, or None (multi-GPU, d > 64,
+        GADMM_BLOCKED=0). pw = positions per wave: 1 = the 12-wave kernel (default, also the only
+        instrumented one, so ``timeline`` selects it), 2 = the paired 8-wave kernel (GADMM_BLOCK_PW=2)."""
         import os
 
         if fabric is not None or self.nranks > 1 or self.d > 64 or os.environ.get("GADMM_BLOCKED", "1") == "0":
             return None
-        kk, ll = ctypes.c_int(0), ctypes.c_int(0)
+        kk, ll, pp = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
         want = int(os.environ.get("GADMM_BLOCK_K", "0"))
-        W = int(self.lib.gadmm_chain_blocked_plan(self.n_total, self.d, want, ctypes.byref(kk), ctypes.byref(ll)))
-        return (kk.value, ll.value, W) if W > 0 else None
+        W = int(self.lib.gadmm_chain_blocked_plan2(self.n_total, self.d, want, 1 if timeline else 0, ctypes.byref(kk),
+                                                   ctypes.byref(ll), ctypes.byref(pp)))
+        return (kk.value, ll.value, W, pp.value) if W > 0 else None
 
     def run_persistent(self, lag: int = 4, timeout_s: float = 20.0, start_iter: int = 1,
                        pending_in: int = 0, fabric=None, timeline_iters: int = 0,
@@ -318,7 +320,7 @@ class NativeChainEngine:
                 raise RuntimeError("dynamic persistent kernel not eligible for this engine/config")
         elif not self.persistent_eligible(fabric):
             raise RuntimeError("persistent kernel not eligible for this engine/config")
-        plan = self.blocked_plan(fabric) if epochs is None else None
+        plan = self.blocked_plan(fabric, timeline=timeline_iters > 0) if epochs is None else None
         if plan is not None:
             lag = max(lag, 8)  # the objective takes one more hop (worker -> objective wave -> monitor)
         ring = lag + 4
@@ -416,9 +418,9 @@ class NativeChainEngine:
             ng = int(self.lib.gadmm_chain_blocked_tab_granules(self.n_total, self.d, ring))
             if getattr(self, "_blk_tab", None) is None or self._blk_tab.numel() != ng * 4:
                 self._blk_tab = torch.zeros((ng * 4,), dtype=torch.int32, device=dev)
-            pa.blk_k, pa.blk_len = plan[0], plan[1]
+            pa.blk_k, pa.blk_len, pa.blk_pw = plan[0], plan[1], plan[3]
             pa.blk_tab = self._blk_tab.data_ptr()
-        self.last_kernel = "blocked(k=%d,L=%d,W=%d)" % plan if plan is not None else "per-worker"
+        self.last_kernel = "blocked(k=%d,L=%d,W=%d,pw=%d)" % plan if plan is not None else "per-worker"
         with torch.cuda.stream(self.stream):
             t0 = _time.perf_counter()
             if plan is not None:

@@ -93,7 +93,7 @@ class PersistArgs(ctypes.Structure):
         ("d", c_int), ("n", c_int), ("n_local", c_int), ("start_iter", c_int), ("max_iter", c_int),
         ("lag", c_int), ("ring", c_int), ("nvar", c_int), ("obj_mode", c_int), ("deg_to_var", c_int * 3),
         ("pending_in", c_int), ("has_monitor", c_int), ("nranks", c_int), ("sys_scope", c_int),
-        ("epoch", ctypes.c_uint), ("pad_", c_int),
+        ("epoch", ctypes.c_uint), ("blk_pw", c_int),
         ("rho", c_double), ("obj0", c_double), ("tol", c_double), ("timeout_ticks", c_longlong),
         ("slots", c_void_p), ("pos", c_void_p), ("Minv", c_void_p), ("A", c_void_p), ("b", c_void_p),
         ("yy", c_void_p), ("theta", c_void_p), ("mu", c_void_p), ("thg", c_void_p), ("push", c_void_p),
@@ -146,6 +146,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_device_can_access_peer": (c_int, [c_int, c_int]),
         "gadmm_chain_persistent_launch": (c_int, [ctypes.POINTER(PersistArgs), c_void_p]),
         "gadmm_chain_blocked_plan": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+        "gadmm_chain_blocked_plan2": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
+                                              ctypes.POINTER(c_int)]),
         "gadmm_chain_blocked_lds": (c_long, [c_int, c_int]),
         "gadmm_chain_blocked_tab_granules": (c_long, [c_int, c_int, c_int]),
         "gadmm_chain_blocked_launch": (c_int, [ctypes.POINTER(PersistArgs), c_void_p]),

@@ -117,6 +117,28 @@ def test_engine_graph_and_persistent_iterations(lin24, lin_obj0, rho, it8):
     assert re.iters == it8
 
 
+@pytest.mark.parametrize("pw,k,L", [(1, 2, 0), (2, 3, 0), (2, 2, 0), (2, 1, 0), (2, 3, 2), (1, 1, 3)])
+def test_blocked_layouts_bit_identical(lin24, lin_obj0, pw, k, L, monkeypatch):
+    """Both wave layouts of the temporally blocked kernel (pw = 1: one position per wave, 12 waves;
+    pw = 2: a head + tail pair per wave, 8 waves) at several (k, L) reproduce the graph path's
+    objective trace bit for bit and stop at the reference iteration."""
+    monkeypatch.setenv("GADMM_BLOCK_PW", str(pw))
+    monkeypatch.setenv("GADMM_BLOCK_K", str(k))
+    if L:
+        monkeypatch.setenv("GADMM_BLOCK_L", str(L))
+    eng = _engine(lin24, 5.0, lin_obj0, 1e-8)
+    r = eng.run()
+    assert r.done == 1 and r.iters == 758
+    tr = eng.objective_trace(758).copy()
+    plan = eng.blocked_plan()
+    assert plan is not None and plan[0] == k and plan[3] == pw and (not L or plan[1] == L)
+    eng.reset()
+    rp = eng.run_persistent()
+    assert eng.last_kernel.startswith("blocked(") and ("pw=%d" % pw) in eng.last_kernel
+    assert rp.done == 1 and rp.iters == 758
+    assert np.array_equal(eng.objective_trace(758), tr)
+
+
 def test_engine_monitor_path_with_rccl_one_rank(lin24, lin_obj0):
     """Multi-rank stop protocol (partial-objective ring, RCCL all-reduce, monitor kernel) on one GPU."""
     import torch.distributed as dist
@@ -387,8 +409,8 @@ def _blocked_xgmi_rank(rank, world, rho, tol):
     return {"runs": out, "trace": tr, "kernel": kern}
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_blocked_xgmi_processes_one_gpu(world, lin24, lin_obj0):
+@pytest.mark.parametrize("world,pw", [(2, 1), (2, 2), (4, 1), (4, 2)])
+def test_blocked_xgmi_processes_one_gpu(world, pw, lin24, lin_obj0, monkeypatch):
     """Temporally blocked kernel across ranks (segments + halos, (theta, mu) pushed into the peers'
     IPC exchange tables once per k iterations, objective waves -> rank 0 monitor -> decision fan-out),
     rehearsed with several processes sharing one MI355X: exact iteration count and an objective trace
@@ -396,9 +418,11 @@ def test_blocked_xgmi_processes_one_gpu(world, lin24, lin_obj0):
     from gadmm_amd.parallel.launch import spawn
     from gadmm_amd.algorithms import chain_admm
     from gadmm_amd.models import LinearRegression
+    monkeypatch.setenv("GADMM_BLOCK_PW", str(pw))  # inherited by the spawned ranks
     res = spawn(_blocked_xgmi_rank, world, 3.0, 1e-8, timeout=300)
     for r in res:
         assert all(it == 1373 and done == 1 for it, done in r["runs"]), r
+        assert ("pw=%d" % pw) in r["kernel"]
     m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
     single = chain_admm(m, list(range(24)), 24, 3.0, lin_obj0, 1e-8, 3000)
     assert np.array_equal(np.asarray(res[0]["trace"]), single.obj)

@@ -22,7 +22,7 @@ eng.set_path(list(range(24)), Placement.contiguous(24, 1), 0)
 for rep in range(3):
     eng.reset()
     r = eng.run_persistent(timeline_iters=K, timeout_s=float(os.environ.get("TL_TIMEOUT", "20")))
-k, L, W = eng.blocked_plan()
+k, L, W, _pw = eng.blocked_plan(timeline=True)
 T = eng.last_timeline[: W + 1].astype(np.float64) * 10e-3
 ks = np.arange(20, K - 2)
 res = {"kernel": eng.last_kernel, "iters": r.iters, "us_per_iter_wall": r.wall_ms * 1e3 / max(r.iters, 1)}

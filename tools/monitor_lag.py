@@ -33,7 +33,7 @@ for lag in (8, 16, 32):
     res["lag%d_iters" % lag] = r.iters
 eng.reset()
 r = eng.run_persistent(lag=8, timeline_iters=K)
-k, L, W = eng.blocked_plan()
+k, L, W, _pw = eng.blocked_plan(timeline=True)
 Wo = (24 + 11) // 12
 T = eng.last_timeline.astype(np.float64) * 10e-3
 work_end = T[0, :, 5]
