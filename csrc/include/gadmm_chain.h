@@ -72,7 +72,7 @@ struct PhaseArgs {
   // large-d (d > 256) row-blocked path
   double* rbuf;        // [n_local][d] right-hand sides of the current phase
   int obj_mode;        // 0: exact (second GEMV with A), 1: A th = r - deg rho th (no second matrix pass)
-  int pad_;
+  int solver;          // logistic local solve: 0 inexact inner GD (logReg_GD.m), 1 exact Newton (chain_newton.hip)
 };
 
 // Engine construction arguments (Python mirrors it in gadmm_amd/ops/native.py).

@@ -623,10 +623,12 @@ __global__ void chain_reset_kernel(ChainCtl* ctl, int start_iter, int pending) {
 extern "C" {
 
 int gadmm_chain_phase_big(const PhaseArgs* args, hipStream_t st);
+int gadmm_chain_phase_newton(const PhaseArgs* args, hipStream_t st);
 
 int gadmm_chain_phase(const PhaseArgs* args, hipStream_t st) {
   const PhaseArgs& a = *args;
   if (a.n_slots <= 0) return 0;
+  if (a.model == MODEL_LOGISTIC && a.solver == 1) return gadmm_chain_phase_newton(args, st);
   if (a.d > 256) {
     if (a.model != MODEL_LINEAR) {
       gadmm_set_error("chain_phase: logistic with d=%d > 256 is not supported by the fused kernels", a.d);

@@ -70,7 +70,9 @@ def chain_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: 
         local_solver = "closed" if model.kind == "linear" else "gd"
     dev = model.device
     use_native = False
-    if backend in ("auto", "native") and dev.type == "cuda" and local_solver in ("closed", "gd") and state is None \
+    native_solver = local_solver in ("closed", "gd") or (
+        local_solver == "newton" and model.kind == "logistic" and model.d <= 64 and model.m <= 64)
+    if backend in ("auto", "native") and dev.type == "cuda" and native_solver and state is None \
             and not check_exchange and not failures:
         from ..ops import native
 
@@ -220,14 +222,15 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     pre = (model.A, model.b, model.yy) if kind == "linear" else None
     # one engine per (model, configuration) on a single rank: repeated solves (rho sweeps, benchmarks,
     # D-GADMM re-runs) reuse its device buffers, cached inverses and captured graph
-    key = (kind, n_total, tuple(int(w) for w in local_ids), float(rho), int(max_iter), block, float(step),
-           int(max_inner), float(inner_tol), float(getattr(model, "lam", 0.0)))
+    key = (kind, local_solver, n_total, tuple(int(w) for w in local_ids), float(rho), int(max_iter), block,
+           float(step), int(max_inner), float(inner_tol), float(getattr(model, "lam", 0.0)))
     cache = getattr(model, "_chain_engines", None) if rcomm is None else None
     eng = cache.get(key) if cache is not None else None
     if eng is None:
         eng = NativeChainEngine(model.X, model.y, local_ids, n_total, kind, rho=rho, obj0=obj0, tol=tol,
                                 max_iter=max_iter, lam=getattr(model, "lam", 0.0), step=step, max_inner=max_inner,
-                                inner_tol=inner_tol, comm=rcomm, block=block, precomputed=pre)
+                                inner_tol=inner_tol, comm=rcomm, block=block, precomputed=pre,
+                                local_solver="newton" if local_solver == "newton" else "gd")
         if rcomm is None and opts.get("cache", True):
             if cache is None:
                 cache = {}

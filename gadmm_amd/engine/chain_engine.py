@@ -47,7 +47,10 @@ class NativeChainEngine:
                  model: str = "linear", rho: float = 1.0, obj0: float = 0.0, tol: float = 1e-4,
                  max_iter: int = 1000, lam: float = 0.0, step: float = 0.0, max_inner: int = 100,
                  inner_tol: float = 1e-4, comm=None, block: int = 16, stream: Optional[torch.cuda.Stream] = None,
-                 precomputed=None, force_monitor: bool = False, obj_mode: str = "exact"):
+                 precomputed=None, force_monitor: bool = False, obj_mode: str = "exact", local_solver: str = "gd"):
+        """``local_solver`` (logistic): "gd" = the reference's inexact inner GD (logReg_GD.m, step /
+        max_inner / inner_tol), "newton" = exact local solves (group_ADMM_logistic.m semantics,
+        csrc/kernels/chain_newton.hip; d, m <= 64)."""
         if not X_loc.is_cuda:
             raise ValueError("NativeChainEngine runs on a HIP device; use the torch algorithms on CPU")
         self.lib = native.require()
@@ -60,6 +63,11 @@ class NativeChainEngine:
         self.m = int(X_loc.shape[1])
         self.comm = comm
         self.nranks = 1 if comm is None else comm.nranks
+        if local_solver not in ("gd", "newton"):
+            raise ValueError("unknown local solver %r" % local_solver)
+        if local_solver == "newton" and (model != "logistic" or self.d > 64 or self.m > 64):
+            raise ValueError("native Newton local solves need the logistic model with d, m <= 64")
+        self.local_solver = local_solver
         if force_monitor:
             # exercise the multi-rank stop path (partial-objective ring + RCCL all-reduce + monitor
             # kernel) with a 1-rank communicator: used by the single-GPU tests
@@ -131,6 +139,7 @@ class NativeChainEngine:
         args.inner_iters = self.inner_iters.data_ptr()
         args.rbuf = native.ptr(self.rbuf)
         args.obj_mode = 0 if obj_mode == "exact" else 1
+        args.solver = 1 if local_solver == "newton" else 0
         desc = native.EngineDesc()
         desc.base = args
         desc.d_slots = self.slots.data_ptr()

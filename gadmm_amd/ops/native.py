@@ -53,7 +53,7 @@ class PhaseArgs(ctypes.Structure):
         ("m", c_int), ("max_inner", c_int),
         ("lam", c_double), ("step", c_double), ("inner_tol", c_double),
         ("inner_iters", c_void_p),
-        ("rbuf", c_void_p), ("obj_mode", c_int), ("pad_", c_int),
+        ("rbuf", c_void_p), ("obj_mode", c_int), ("solver", c_int),
     ]
 
 
