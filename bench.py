@@ -53,7 +53,7 @@ def main():
     ap.add_argument("--fabric", choices=["auto", "xgmi", "rccl"], default="auto",
                     help="multi-GPU transport: xgmi = device-initiated granule pushes between persistent kernels "
                          "(IPC fine-grained buffers), rccl = RCCL send/recv between graph-replayed phases")
-    ap.add_argument("--config", choices=["e1", "logistic", "dgadmm", "real10m"], default="e1",
+    ap.add_argument("--config", choices=["e1", "logistic", "logistic_exact", "dgadmm", "real10m"], default="e1",
                     help="e1 = the headline (default); the others are BASELINE.json configs[2..4]")
     ap.add_argument("--rows", type=int, default=1_250_000, help="real10m: rows per GPU")
     ap.add_argument("--dim", type=int, default=10_000, help="real10m: features")

@@ -14,10 +14,11 @@
 //
 // One 256-thread workgroup per worker (d, m <= 64), everything in LDS:
 //   margins / gradient: 4 threads per row (column) with two xor shuffles;
-//   Hessian: lower-triangular 4x4 register blocks (two 16-B LDS reads per operand per sample);
-//   factorisation: symmetric Gaussian elimination H = L D L^T in place (SPD, no pivoting), wave w
-//     updates the columns j = w (mod 4), lane i row i, one LDS barrier per pivot;
-//   substitution: wave 0, column-oriented, the pivot value broadcast by a lane shuffle.
+//   Hessian: lower-triangular 4x4 register blocks (two 16-B LDS reads per operand per sample), the
+//     samples split over a lane pair;
+//   solve: block Gauss-Jordan on [H | g] with 4 x 4 pivot blocks (SPD, no pivoting); lane i of wave
+//     w keeps row i's columns j = w (mod 4) in registers, each block's 4 columns go through LDS,
+//     one barrier per 4 pivots, no back substitution.
 #include "gadmm_common.h"
 #include "gadmm_chain.h"
 #include "chain_device.h"
@@ -28,6 +29,12 @@ constexpr int NTN = 256;
 constexpr int NEWTON_MAX = 50;
 constexpr double NEWTON_TOL = 1e-13;
 
+__device__ __forceinline__ double readlane_f64(double v, int l) {  // l wave-uniform
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
 __device__ __forceinline__ double wave_max_f64(double v) {
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
@@ -36,6 +43,10 @@ __device__ __forceinline__ double wave_max_f64(double v) {
 
 }  // namespace
 
+// TL: instrumented instantiation (GADMM_NEWTON_TL=1): s_memrealtime stamps of every Newton step of
+// every worker into PhaseArgs.rbuf as long long [n_slots][NEWTON_MAX][5]: step start, sigma terms,
+// gradient + Hessian, Gauss-Jordan, update + test.
+template <bool TL>
 __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
   __shared__ int flag_lds, conv_lds;
@@ -55,6 +66,7 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
   double* wv = sv + 64;         // [64] sigma (1 - sigma)
   double* cv = wv + 64;         // [64] mu - rho (theta_l + theta_r): the x-independent gradient part
   double* yv = cv + 64;         // [64] labels
+  double* colv = yv + 64;       // [2][4][64] pivot-block columns of the solve (double-buffered)
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const double rho = a.rho, lam = a.lam;
   double* th = a.theta;
@@ -87,11 +99,14 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
   lds_barrier();
 
   int used = 0;
+  long long* tl = TL ? reinterpret_cast<long long*>(a.rbuf) + (long)blockIdx.x * NEWTON_MAX * 5 : nullptr;
   for (int k = 0; k < NEWTON_MAX; ++k) {
+    if (TL && t == 0) tl[k * 5] = (long long)__builtin_amdgcn_s_memrealtime();
     {  // margins z_i = X[i,:] x -> sigma terms; thread (i, q) sums columns j = q (mod 4)
       const int i = t >> 2, q = t & 3;
       double z = 0.0;
       if (i < m)
+#pragma unroll 4
         for (int j = q; j < d; j += 4) z = fma(Xs[i * DP + j], xv[j], z);
       z += __shfl_xor(z, 1, 64);
       z += __shfl_xor(z, 2, 64);
@@ -103,24 +118,32 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
       }
     }
     lds_barrier();
+    if (TL && t == 0) tl[k * 5 + 1] = (long long)__builtin_amdgcn_s_memrealtime();
     {  // gradient; thread (j, q) sums samples i = q (mod 4)
       const int j = t >> 2, q = t & 3;
       double s = 0.0;
       if (j < d)
+#pragma unroll 4
         for (int i = q; i < m; i += 4) s = fma(Xs[i * DP + j], sv[i], s);
       s += __shfl_xor(s, 1, 64);
       s += __shfl_xor(s, 2, 64);
       if (q == 0 && j < d) gv[j] = -s + shift * xv[j] + cv[j];
     }
-    {  // Hessian, lower 4x4 blocks (bj >= bk)
-      const int bj = t >> 4, bk = t & 15;
-      if (bj >= bk && 4 * bj < d) {
+    {  // Hessian, lower 4x4 blocks (bj >= bk); the two lanes of a pair split the samples
+      const int nbr = (d + 3) >> 2, nb = nbr * (nbr + 1) / 2, half = t & 1;
+      for (int b = t >> 1; b < nb; b += NTN / 2) {
+        int bj = 0, bk = b;
+        while (bk > bj) {  // block-row bj holds bj + 1 blocks
+          bk -= bj + 1;
+          ++bj;
+        }
         double acc[4][4];
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
           for (int v = 0; v < 4; ++v) acc[u][v] = 0.0;
-        for (int i = 0; i < m; ++i) {
+#pragma unroll 4
+        for (int i = half; i < m; i += 2) {
           const double w = wv[i];
           const double2 a01 = *reinterpret_cast<const double2*>(Xs + i * DP + 4 * bj);
           const double2 a23 = *reinterpret_cast<const double2*>(Xs + i * DP + 4 * bj + 2);
@@ -137,41 +160,116 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
         for (int u = 0; u < 4; ++u)
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
+            const double tot = acc[u][v] + __shfl_xor(acc[u][v], 1, 64);
             const int r = 4 * bj + u, c = 4 * bk + v;
-            if (r < d && c <= r) Hs[r * DH + c] = acc[u][v] + (r == c ? shift : 0.0);
+            if (half == 0 && r < d && c <= r) Hs[r * DH + c] = tot + (r == c ? shift : 0.0);
           }
       }
     }
     lds_barrier();
-    // H = L D L^T in place: after pivot p, Hs[i][p] / Hs[p][p] = L[i][p] and Hs[p][p] = D[p]
-    for (int p = 0; p < d - 1; ++p) {
+    if (TL && t == 0) tl[k * 5 + 2] = (long long)__builtin_amdgcn_s_memrealtime();
+    {  // Block Gauss-Jordan on [H | g] with 4 x 4 pivot blocks (SPD, no pivoting). Lane i of wave w
+       // keeps row i's columns j = w + 4c (c < 16) in registers; wave 0 also carries g_i. Block b
+       // (pivots p = 4b .. 4b + 3) has one column in each wave: every wave publishes its column of
+       // the block into a double-buffered LDS slab, one barrier, then every lane eliminates the
+       // block from its row (rows above the block too, so no back substitution is left):
+       //   l_i = H[i][p:p+4] P^-1,  H[i][:] -= l_i H[p:p+4][:],  g_i -= l_i g[p:p+4]
+       // (P = the 4 x 4 pivot block, factorised redundantly per lane as L D L^T). Indices >= d are
+       // identity padding. A pivot row keeps row (i - p) of P^-1 for the final block solve.
       const int i = lane;
-      if (i > p && i < d) {
-        const double lip = Hs[i * DH + p] / Hs[p * DH + p];
-        for (int j = p + 1 + ((wid - p - 1) & 3); j <= i; j += 4) Hs[i * DH + j] = fma(-lip, Hs[j * DH + p], Hs[i * DH + j]);
+      double h[16];
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const int j = wid + 4 * c;
+        h[c] = (i < d && j < d) ? (j <= i ? Hs[i * DH + j] : Hs[j * DH + i]) : (i == j ? 1.0 : 0.0);
+      }
+      double gi = (wid == 0 && i < d) ? gv[i] : 0.0;
+      double pr0 = 0.0, pr1 = 0.0, pr2 = 0.0, pr3 = 0.0;  // row (i mod 4) of this lane's pivot-block inverse
+      const int nb = (d + 3) >> 2;
+      for (int bb = 0; bb < nb; ++bb) {
+        const int p = 4 * bb;
+        double* slab = colv + (bb & 1) * 256;  // [4][64]: column p + q of the current matrix
+        switch (bb) {  // wave-uniform register select: no per-entry cndmasks
+#define GADMM_PUB(C)            \
+  case C:                       \
+    slab[wid * 64 + i] = h[C];  \
+    break;
+          GADMM_PUB(0) GADMM_PUB(1) GADMM_PUB(2) GADMM_PUB(3) GADMM_PUB(4) GADMM_PUB(5) GADMM_PUB(6) GADMM_PUB(7)
+          GADMM_PUB(8) GADMM_PUB(9) GADMM_PUB(10) GADMM_PUB(11) GADMM_PUB(12) GADMM_PUB(13) GADMM_PUB(14)
+          GADMM_PUB(15)
+#undef GADMM_PUB
+        }
+        lds_barrier();
+        double P[4][4], R[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          R[q] = slab[q * 64 + i];  // H[i][p + q]
+#pragma unroll
+          for (int r = 0; r < 4; ++r) P[q][r] = slab[q * 64 + p + r];  // H[p + r][p + q] (symmetric)
+        }
+        const bool pivrow = (i >> 2) == bb;
+        if (pivrow) {  // solve with e_(i - p): the lane's row of P^-1
+#pragma unroll
+          for (int q = 0; q < 4; ++q) R[q] = (q == (i & 3)) ? 1.0 : 0.0;
+        }
+        // P = L D L^T (4 x 4, the same on every lane), then l = P^-1 R
+        auto rcp = [](double v) {
+          double r = __builtin_amdgcn_rcp(v);
+          r = fma(r, fma(-v, r, 1.0), r);
+          return fma(r, fma(-v, r, 1.0), r);
+        };
+        const double d0 = P[0][0], i0 = rcp(d0);
+        const double L10 = P[1][0] * i0, L20 = P[2][0] * i0, L30 = P[3][0] * i0;
+        const double d1 = P[1][1] - L10 * P[1][0], i1 = rcp(d1);
+        const double L21 = (P[2][1] - L20 * P[1][0]) * i1, L31 = (P[3][1] - L30 * P[1][0]) * i1;
+        const double d2 = P[2][2] - L20 * P[2][0] - L21 * (L21 * d1), i2 = rcp(d2);
+        const double L32 = (P[3][2] - L30 * P[2][0] - L31 * (L21 * d1)) * i2;
+        const double d3 = P[3][3] - L30 * P[3][0] - L31 * (L31 * d1) - L32 * (L32 * d2), i3 = rcp(d3);
+        const double y0 = R[0], y1 = R[1] - L10 * y0, y2 = R[2] - L20 * y0 - L21 * y1,
+                     y3 = R[3] - L30 * y0 - L31 * y1 - L32 * y2;
+        const double l3 = y3 * i3, l2 = y2 * i2 - L32 * l3, l1 = y1 * i1 - L21 * l2 - L31 * l3,
+                     l0 = y0 * i0 - L10 * l1 - L20 * l2 - L30 * l3;
+        double f0 = l0, f1 = l1, f2 = l2, f3 = l3;
+        if (pivrow) {
+          pr0 = l0;
+          pr1 = l1;
+          pr2 = l2;
+          pr3 = l3;
+          f0 = f1 = f2 = f3 = 0.0;  // pivot rows are not eliminated by their own block
+        }
+#pragma unroll
+        for (int c = 0; c < 16; ++c) {
+          const int j = wid + 4 * c;  // H[p + q][j] = H[j][p + q] for the trailing columns j >= p + 4
+          double v = h[c];
+          v = fma(-f0, slab[0 * 64 + j], v);
+          v = fma(-f1, slab[1 * 64 + j], v);
+          v = fma(-f2, slab[2 * 64 + j], v);
+          v = fma(-f3, slab[3 * 64 + j], v);
+          h[c] = v;  // columns j < p + 4 are done: updating them too is harmless and branch-free
+        }
+        if (wid == 0) {
+          const double g0 = readlane_f64(gi, p), g1 = readlane_f64(gi, p + 1), g2 = readlane_f64(gi, p + 2),
+                       g3 = readlane_f64(gi, p + 3);
+          gi = fma(-f0, g0, fma(-f1, g1, fma(-f2, g2, fma(-f3, g3, gi))));
+        }
       }
       lds_barrier();
-    }
-    if (wid == 0) {
-      const bool in = lane < d;
-      const double dinv = in ? 1.0 / Hs[lane * DH + lane] : 0.0;
-      double r = in ? gv[lane] : 0.0;
-      for (int p = 0; p < d - 1; ++p) {  // L y = g (unit lower, column by column)
-        const double rp = __shfl(r, p, 64), dp = __shfl(dinv, p, 64);
-        if (lane > p && in) r = fma(-Hs[lane * DH + p] * dp, rp, r);
+      if (TL && t == 0) tl[k * 5 + 3] = (long long)__builtin_amdgcn_s_memrealtime();
+      if (wid == 0) {
+        const bool in = lane < d;
+        const int q0 = lane & ~3;  // the lane's pivot block: dx = P^-1 g over the block
+        const double g0 = __shfl(gi, q0, 64), g1 = __shfl(gi, q0 + 1, 64), g2 = __shfl(gi, q0 + 2, 64),
+                     g3 = __shfl(gi, q0 + 3, 64);
+        const double r = in ? fma(pr0, g0, fma(pr1, g1, fma(pr2, g2, pr3 * g3))) : 0.0;  // dx
+        const double xo = in ? xv[lane] : 0.0;
+        const double xn = xo - (in ? r : 0.0);
+        if (in) xv[lane] = xn;
+        const double mdx = wave_max_f64(in ? fabs(r) : 0.0), mx = wave_max_f64(in ? fabs(xn) : 0.0);
+        if (lane == 0) conv_lds = (mdx < NEWTON_TOL * fmax(1.0, mx)) ? 1 : 0;
       }
-      r *= dinv;                          // D^{-1}
-      for (int p = d - 1; p > 0; --p) {   // L^T dx = y (row p of L read across the lanes)
-        const double xp = __shfl(r, p, 64);
-        if (lane < p) r = fma(-Hs[p * DH + lane] * dinv, xp, r);
-      }
-      const double xo = in ? xv[lane] : 0.0;
-      const double xn = xo - (in ? r : 0.0);
-      if (in) xv[lane] = xn;
-      const double mdx = wave_max_f64(in ? fabs(r) : 0.0), mx = wave_max_f64(in ? fabs(xn) : 0.0);
-      if (lane == 0) conv_lds = (mdx < NEWTON_TOL * fmax(1.0, mx)) ? 1 : 0;
     }
     lds_barrier();
+    if (TL && t == 0) tl[k * 5 + 4] = (long long)__builtin_amdgcn_s_memrealtime();
     used = k + 1;
     if (conv_lds) break;
   }
@@ -215,7 +313,7 @@ extern "C" {
 
 size_t gadmm_chain_newton_lds(int d, int m) {
   const int DP = (d + 3) & ~3, DH = d | 1;
-  return (size_t)(m * DP + d * DH + 6 * 64) * sizeof(double);
+  return (size_t)(m * DP + d * DH + 14 * 64) * sizeof(double);
 }
 
 // Launch one Newton phase (PhaseArgs.solver == 1, logistic model). d, m <= 64.
@@ -227,15 +325,18 @@ int gadmm_chain_phase_newton(const PhaseArgs* args, hipStream_t st) {
     return -1;
   }
   static const bool attr = [] {  // once, outside any stream capture of the caller's later phases
-    return hipFuncSetAttribute((const void*)chain_phase_logistic_newton, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               96 * 1024) == hipSuccess;
+    return hipFuncSetAttribute((const void*)chain_phase_logistic_newton<false>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess &&
+           hipFuncSetAttribute((const void*)chain_phase_logistic_newton<true>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024) == hipSuccess;
   }();
   const size_t lds = gadmm_chain_newton_lds(a.d, a.m);
   if (!attr && lds > 65536) {
     gadmm_set_error("chain_phase newton: %zu B of LDS needs the dynamic-LDS attribute", lds);
     return -1;
   }
-  hipLaunchKernelGGL(chain_phase_logistic_newton, dim3(a.n_slots), dim3(NTN), lds, st, a);
+  if (a.rbuf) hipLaunchKernelGGL(chain_phase_logistic_newton<true>, dim3(a.n_slots), dim3(NTN), lds, st, a);
+  else hipLaunchKernelGGL(chain_phase_logistic_newton<false>, dim3(a.n_slots), dim3(NTN), lds, st, a);
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

@@ -15,6 +15,7 @@ The iteration loop itself runs in C++ (graph-captured kernels + RCCL), so a solv
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -99,6 +100,9 @@ class NativeChainEngine:
             if d > 256:
                 stride = int(native.require().gadmm_chain_big_rbuf_stride(d))
                 self.rbuf = torch.zeros((max(nl, 1) * stride,), dtype=f64, device=dev)
+            elif local_solver == "newton" and os.environ.get("GADMM_NEWTON_TL") == "1":
+                # instrumented Newton kernel: s_memrealtime stamps [n_local][50 steps][5] (tools/newton_stats.py)
+                self.rbuf = torch.zeros((max(nl, 1) * 50 * 5,), dtype=torch.int64, device=dev)
             if model == "linear":
                 if precomputed is not None:
                     self.A, self.b, self.yy = precomputed
