@@ -27,6 +27,11 @@ class ExperimentConfig:
     gd_step: float = 2.2            # logistic inner GD step (gdStep)
     max_inner: int = 100
     coherences: List[float] = field(default_factory=list)
+    # logistic: extra GADMM runs with EXACT local solves (group_ADMM_logistic.m / SURVEY.md D2, the
+    # Newton HIP kernel), which reach gaps the linearised inner GD cannot (SURVEY.md §7.3 "report both")
+    exact_rhos: List[float] = field(default_factory=list)
+    exact_acc: float = 1e-8
+    exact_iters: int = 2000
     coherence_v0: float = 10.0
     n_pregen_paths: int = 1000
     overhead_inflation: float = 5.0 / 15.0   # Dynamic_LinearRegression_Synthetic.m:123,125
@@ -45,7 +50,8 @@ class ExperimentConfig:
         """Reduced budgets for smoke tests (same structure, fewer iterations)."""
         return self.override(baseline_iters=min(self.baseline_iters, 300),
                              dualavg_iters=min(self.dualavg_iters or self.baseline_iters, 300),
-                             gadmm_iters=min(self.gadmm_iters, 400), n_pregen_paths=min(self.n_pregen_paths, 60))
+                             gadmm_iters=min(self.gadmm_iters, 400), n_pregen_paths=min(self.n_pregen_paths, 60),
+                             exact_iters=min(self.exact_iters, 60))
 
 
 PRESETS = {
@@ -60,11 +66,11 @@ PRESETS = {
     "LogisticRegression_Synthetic": ExperimentConfig(
         name="LogisticRegression_Synthetic", model="logistic", data="logistic_synthetic", num_workers=24,
         baseline_iters=100000, gadmm_iters=400, rhos=[3e-4, 2e-4], acc=1e-4, lam=1e-5, gd_step=2.2,
-        reference="LogisticRegression_Synthetic.m:14-17,40-46,88-100"),
+        exact_rhos=[1e-3], reference="LogisticRegression_Synthetic.m:14-17,40-46,88-100"),
     "LogisticRegression_Real": ExperimentConfig(
         name="LogisticRegression_Real", model="logistic", data="derm", num_workers=10, dim=34, total_rows=358,
         baseline_iters=100000, dualavg_iters=500000, gadmm_iters=1000, rhos=[0.03, 0.02], acc=1e-4, lam=1e-5,
-        gd_step=0.08, reference="LogisticRegression_real.m:17-34,46-47,65-85"),
+        gd_step=0.08, exact_rhos=[0.02], reference="LogisticRegression_real.m:17-34,46-47,65-85"),
     "Dynamic_LinearRegression_Synthetic": ExperimentConfig(
         name="Dynamic_LinearRegression_Synthetic", model="linear", data="linear_synthetic", num_workers=50,
         gadmm_iters=5000, rhos=[3.0], acc=1e-4, coherences=[1e9, 1, 10, 50, 100], coherence_v0=10,

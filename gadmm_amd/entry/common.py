@@ -110,9 +110,10 @@ def parse_args(entry: str, argv=None):
     ap.add_argument("--backend", default="auto", choices=["auto", "torch", "native"])
     ap.add_argument("--checkpoint", default=None, help="write per-worker checkpoints of the last GADMM run here")
     a = ap.parse_args(argv)
-    cfg = parse_overrides(get_preset(entry), a.set)
+    cfg = get_preset(entry)
     if a.quick:
         cfg = cfg.quick()
+    cfg = parse_overrides(cfg, a.set)  # explicit --set values win over the --quick budgets
     if a.no_baselines:
         cfg = cfg.override(run_baselines=False, run_dualavg=False)
     if a.tol is not None:
@@ -203,6 +204,13 @@ def gadmm_sweep(prob: Problem, sess: Session, backend: str = "auto") -> Dict[str
                        max_inner=cfg.max_inner, backend=backend, name="GADMM(rho=%g)" % rho)
         r.extra.pop("engine_obj", None)
         out["GADMM_rho%g" % rho] = r
+    if cfg.model == "logistic":
+        for rho in cfg.exact_rhos:  # exact local solves (D2 semantics), to the tighter exact_acc gap
+            r = chain_admm(prob.model, prob.local_ids, prob.n_total, rho, prob.obj0, cfg.exact_acc, cfg.exact_iters,
+                           comm=sess.comm, placement=prob.placement, local_solver="newton", backend=backend,
+                           name="GADMM-exact(rho=%g)" % rho)
+            r.extra.pop("engine_obj", None)
+            out["GADMM_exact_rho%g" % rho] = r
     return out
 
 

@@ -77,3 +77,12 @@ def test_checkpoint_multi_rank_layout(tmp_path):
     save_checkpoint(str(tmp_path), 0, [0, 1, 2], th, mu[:3], 9, [0, 1, 2, 3, 4, 5], {"algorithm": "GADMM"})
     t, m, nxt, path, man = load_checkpoint(str(tmp_path), [3, 4, 5])
     assert torch.equal(t, th) and torch.equal(m, mu[3:]) and nxt == 9 and man["algorithm"] == "GADMM"
+
+
+def test_logistic_entry_reports_exact_runs(tmp_path):
+    """Logistic entries also run GADMM with exact local solves (SURVEY.md §7.3 "report both")."""
+    out = entry.get("LogisticRegression_Synthetic").main(
+        ["--quick", "--device", "cpu", "--out", str(tmp_path), "--no-plot", "--no-baselines",
+         "--set", "exact_iters=500"])
+    r = out["runs"]["GADMM_exact_rho0.001"]
+    assert r["iters"] == 424 and r["converged"]
