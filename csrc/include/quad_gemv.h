@@ -28,6 +28,34 @@ __device__ __forceinline__ void quad_load(double (&m)[4][T], const double* M, in
     }
 }
 
+// Transpose-reduce of the four per-class partials of a quad GEMV without LDS: lane i + 16c holds
+// p[r] = class c's partial of row i + 16r. Two v_permlane32_swap exchanges (class pairs {0,1} <->
+// {2,3}) then two v_permlane16_swap exchanges (0 <-> 1, 2 <-> 3) leave lane l = i + 16g holding
+// class c's partial of row l in p[c], which are summed ((p0 + p1) + p2) + p3: the same order as
+// the LDS reduction, so the result is bit-identical, with 8 cross-lane VALU moves instead of two
+// dependent LDS round trips.
+__device__ __forceinline__ void swap32_f64(double& a, double& b) {  // lanes 32-63 of a <-> lanes 0-31 of b
+  const long long ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+  a = __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
+  b = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+}
+__device__ __forceinline__ void swap16_f64(double& a, double& b) {  // lanes 16-31 (48-63) of a <-> 0-15 (32-47) of b
+  const long long ua = __double_as_longlong(a), ub = __double_as_longlong(b);
+  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)ua, (unsigned)ub, false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+  a = __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
+  b = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+}
+__device__ __forceinline__ double quad_reduce(double (&p)[4]) {
+  swap32_f64(p[0], p[2]);
+  swap32_f64(p[1], p[3]);
+  swap16_f64(p[0], p[1]);
+  swap16_f64(p[2], p[3]);
+  return ((p[0] + p[1]) + p[2]) + p[3];
+}
+
 template <int T>
 __device__ __forceinline__ double quad_gemv(const double (&m)[4][T], double x, double* st) {
   static_assert(T >= 1 && T <= 16, "quad layout covers d <= 64");
@@ -46,6 +74,7 @@ __device__ __forceinline__ double quad_gemv(const double (&m)[4][T], double x, d
       for (int r = 0; r < 4; ++r) p[r] = fma(m[r][t + 1], xp.y, p[r]);
     }
   }
+#ifdef GADMM_QUAD_LDS_REDUCE  // the LDS transpose-reduce (A/B reference build)
   double* red = st + 4 * QX;
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[c * QR + (lane & 15) + 16 * r] = p[r];
@@ -53,6 +82,10 @@ __device__ __forceinline__ double quad_gemv(const double (&m)[4][T], double x, d
   const double q0 = red[lane], q1 = red[QR + lane], q2 = red[2 * QR + lane], q3 = red[3 * QR + lane];
   asm volatile("" ::: "memory");  // the next call's writes stay behind these reads
   return ((q0 + q1) + q2) + q3;
+#else
+  asm volatile("" ::: "memory");  // the next call's x store stays behind this call's x reads
+  return quad_reduce(p);
+#endif
 }
 
 // Paired layout for two matrices with <= 52 rows held by one wave (chain_blocked_pair_kernel):

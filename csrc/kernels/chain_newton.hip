@@ -44,7 +44,7 @@ __device__ __forceinline__ double wave_max_f64(double v) {
 }  // namespace
 
 // TL: instrumented instantiation (GADMM_NEWTON_TL=1): s_memrealtime stamps of every Newton step of
-// every worker into PhaseArgs.rbuf as long long [n_slots][NEWTON_MAX][5]: step start, sigma terms,
+// every worker into PhaseArgs.rbuf as long long [n_local][NEWTON_MAX][5]: step start, sigma terms,
 // gradient + Hessian, Gauss-Jordan, update + test.
 template <bool TL>
 __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) {
@@ -99,7 +99,7 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
   lds_barrier();
 
   int used = 0;
-  long long* tl = TL ? reinterpret_cast<long long*>(a.rbuf) + (long)blockIdx.x * NEWTON_MAX * 5 : nullptr;
+  long long* tl = TL ? reinterpret_cast<long long*>(a.rbuf) + (long)sl.li * NEWTON_MAX * 5 : nullptr;
   for (int k = 0; k < NEWTON_MAX; ++k) {
     if (TL && t == 0) tl[k * 5] = (long long)__builtin_amdgcn_s_memrealtime();
     {  // margins z_i = X[i,:] x -> sigma terms; thread (i, q) sums columns j = q (mod 4)

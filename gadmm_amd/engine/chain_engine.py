@@ -54,6 +54,10 @@ class NativeChainEngine:
         csrc/kernels/chain_newton.hip; d, m <= 64)."""
         if not X_loc.is_cuda:
             raise ValueError("NativeChainEngine runs on a HIP device; use the torch algorithms on CPU")
+        # the kernels read raw f64 pointers: anything else (e.g. float32 labels from torch.where) would be
+        # reinterpreted bit for bit
+        X_loc = X_loc.to(torch.float64)
+        y_loc = y_loc.to(torch.float64)
         self.lib = native.require()
         self.device = X_loc.device
         self.model = model
