@@ -5,18 +5,22 @@
 // per-hop cost -- so pre-drawing ~300 epochs for a one-launch D-GADMM run costs tens of us instead
 // of milliseconds of numpy dispatch. Bit-identical to PathSchedule.prefetch_arrays' numpy path: no
 // FMA contraction, the same operation order ((dx*dx) + (dy*dy); ((d2*eta)*bw)*f for energies).
+#include <algorithm>
 #include <limits>
+#include <thread>
 #include <vector>
 
 #pragma clang fp contract(off)
 
-extern "C" int gadmm_greedy_chains(const double* uv, int E, int n, double side, int energy, double eta, double bw,
-                                   double f, long long* paths, double* costs) {
-  if (E < 0 || n < 1 || !uv || !paths || (n > 1 && !costs)) return -1;
+namespace {
+
+// Epochs [e0, e1) of the batch: one geometry + greedy chain each (independent of the others).
+void greedy_range(const double* uv, int e0, int e1, int n, double side, int energy, double eta, double bw, double f,
+                  long long* paths, double* costs) {
   std::vector<double> x(n), y(n), d2((size_t)n * n);
   std::vector<char> visited(n);
   const double inf = std::numeric_limits<double>::infinity();
-  for (int e = 0; e < E; ++e) {
+  for (int e = e0; e < e1; ++e) {
     const double* g = uv + (size_t)e * n * 2;
     for (int i = 0; i < n; ++i) {
       x[i] = g[2 * i] * side;
@@ -57,5 +61,34 @@ extern "C" int gadmm_greedy_chains(const double* uv, int E, int n, double side, 
       cur = best;
     }
   }
+}
+
+}  // namespace
+
+// The epochs are independent: large batches are split over up to 8 host threads (the ~300-epoch
+// batch of a one-launch D-GADMM solve took ~0.5-1 ms on one core, a third of the solve).
+extern "C" int gadmm_greedy_chains(const double* uv, int E, int n, double side, int energy, double eta, double bw,
+                                   double f, long long* paths, double* costs) {
+  if (E < 0 || n < 1 || !uv || !paths || (n > 1 && !costs)) return -1;
+  const long work = (long)E * n * n;
+  int nt = 1;
+  if (work > 40000) {
+    const unsigned hw = std::thread::hardware_concurrency();
+    nt = (int)std::min<long>(std::min<unsigned>(hw ? hw : 1, 8u), std::max<long>(1, work / 40000));
+    if (nt > E) nt = E;
+  }
+  if (nt <= 1) {
+    greedy_range(uv, 0, E, n, side, energy, eta, bw, f, paths, costs);
+    return 0;
+  }
+  std::vector<std::thread> pool;
+  pool.reserve(nt - 1);
+  const int per = (E + nt - 1) / nt;
+  for (int t = 1; t < nt; ++t) {
+    const int e0 = t * per, e1 = std::min(E, e0 + per);
+    if (e0 < e1) pool.emplace_back(greedy_range, uv, e0, e1, n, side, energy, eta, bw, f, paths, costs);
+  }
+  greedy_range(uv, 0, std::min(E, per), n, side, energy, eta, bw, f, paths, costs);
+  for (auto& th : pool) th.join();
   return 0;
 }
