@@ -109,6 +109,74 @@ spd_inverse_gj64_kernel(const double* __restrict__ A, const double* __restrict__
     if (inj) o[i * d + j] = 0.5 * (M[i * d + j] + M[j * d + i]);
 }
 
+// d <= 64, register rows: lane i of wave w keeps M[i][j] for j = w + 4c (c < 16) in VGPRs. Per
+// pivot k the owner wave of column k publishes it to LDS (one barrier); every lane reads M[i][k] and
+// M[k][k], takes row k of its own wave's columns from lane k by v_readlane, and updates its 16
+// entries in registers. The per-element arithmetic is exactly spd_inverse_gj_kernel's (p = 1/m_kk,
+// m_kj p, fma(-a_ik, m_kj p, m_ij), -a_ik p), so the result is bit-identical, with no LDS matrix
+// traffic and one barrier per pivot instead of two plus 32 LDS accesses per lane.
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__global__ void __launch_bounds__(256)
+spd_inverse_reg64_kernel(const double* __restrict__ A, const double* __restrict__ shift, int d, int nvar,
+                         double* __restrict__ out, int* __restrict__ status) {
+  __shared__ double Ms[64 * 65];    // the result, for the symmetrised write-out
+  __shared__ double colv[2][64];    // the pivot column, double-buffered
+  const int n = blockIdx.x, v = blockIdx.y;
+  const double s = shift[n * nvar + v];
+  const double* An = A + (long)n * d * d;
+  const int i = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double h[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const int j = w + 4 * c;
+    h[c] = (i < d && j < d) ? An[i * d + j] + (i == j ? s : 0.0) : 0.0;
+  }
+  if (w == 0) colv[0][i] = h[0];
+  __syncthreads();
+  for (int k = 0; k < d; ++k) {
+    const double* cb = colv[k & 1];
+    const double pk = cb[k], aik = cb[i];
+    const double p = 1.0 / pk;
+    if (threadIdx.x == 0 && !(pk > 0.0) && status) atomicExch(status, 1);  // not SPD (or NaN)
+#pragma unroll
+    for (int c = 0; c < 16; ++c) {
+      const int j = w + 4 * c;
+      const double mkj = readlane_f64(h[c], k) * p;  // row k, scaled (lane k of this wave)
+      double val = h[c];
+      if (j == k) val = (i == k) ? p : -aik * p;
+      else if (i == k) val = mkj;
+      else val -= aik * mkj;
+      h[c] = val;
+    }
+    const int kn = k + 1;
+    if (kn < d && w == (kn & 3)) {  // owner of the next pivot column publishes it
+      double* dst = &colv[kn & 1][i];
+      switch (kn >> 2) {  // wave-uniform register select
+#define GADMM_PUB(C) \
+  case C:            \
+    *dst = h[C];     \
+    break;
+        GADMM_PUB(0) GADMM_PUB(1) GADMM_PUB(2) GADMM_PUB(3) GADMM_PUB(4) GADMM_PUB(5) GADMM_PUB(6) GADMM_PUB(7)
+        GADMM_PUB(8) GADMM_PUB(9) GADMM_PUB(10) GADMM_PUB(11) GADMM_PUB(12) GADMM_PUB(13) GADMM_PUB(14)
+        GADMM_PUB(15)
+#undef GADMM_PUB
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int c = 0; c < 16; ++c) Ms[i * 65 + w + 4 * c] = h[c];
+  __syncthreads();
+  double* o = out + ((long)n * nvar + v) * d * d;
+  for (int r = w; r < d; r += 4)
+    if (i < d) o[r * d + i] = 0.5 * (Ms[r * 65 + i] + Ms[i * 65 + r]);
+}
+
 }  // namespace
 
 extern "C" int gadmm_spd_inverse_small_f64(const double* A, const double* shift, int N, int d, int nvar,
@@ -120,6 +188,13 @@ extern "C" int gadmm_spd_inverse_small_f64(const double* A, const double* shift,
   if (N <= 0) return 0;
   const char* gje = getenv("GADMM_GJ64");  // A/B switch (read per call: set-up only)
   const bool gj64 = !(gje && gje[0] == '0');
+  const char* rge = getenv("GADMM_INV_REG");  // A/B switch: 0 = the LDS 64-wide kernel
+  const bool reg = !(rge && rge[0] == '0');
+  if (d <= 64 && gj64 && reg) {
+    hipLaunchKernelGGL(spd_inverse_reg64_kernel, dim3(N, nvar), dim3(256), 0, st, A, shift, d, nvar, out, status);
+    GADMM_CHECK(hipGetLastError());
+    return 0;
+  }
   if (d <= 64 && gj64) {
     hipLaunchKernelGGL(spd_inverse_gj64_kernel, dim3(N, nvar), dim3(256), 0, st, A, shift, d, nvar, out, status);
     GADMM_CHECK(hipGetLastError());

@@ -75,16 +75,19 @@ def test_quad_gemv_matches_torch(rows, cols):
 
 @pytest.mark.parametrize("d", [7, 50, 64])
 def test_spd_inverse_gj64_bit_identical(d, monkeypatch):
-    """The 64-wide Gauss-Jordan (d <= 64) reproduces the general kernel bit for bit."""
+    """The 64-wide Gauss-Jordan kernels (d <= 64: register rows, and the LDS variant) reproduce the
+    general kernel bit for bit."""
     from gadmm_amd.ops import linalg
     g = torch.Generator().manual_seed(100 + d)
     Z = torch.randn(5, 2 * d, d, dtype=torch.float64, generator=g)
     A = torch.bmm(Z.transpose(1, 2), Z).to(DEV)
     sh = torch.tensor([0.3, 2.0], dtype=torch.float64, device=DEV)
-    fast = linalg.spd_inverse(A, sh)
+    fast = linalg.spd_inverse(A, sh)             # register-row kernel (default for d <= 64)
+    monkeypatch.setenv("GADMM_INV_REG", "0")
+    lds64 = linalg.spd_inverse(A, sh)            # the LDS 64-wide kernel
     monkeypatch.setenv("GADMM_GJ64", "0")
     general = linalg.spd_inverse(A, sh)
-    assert torch.equal(fast, general)
+    assert torch.equal(fast, general) and torch.equal(lds64, general)
 
 
 def _engine(ds, rho, obj0, tol, **kw):
