@@ -121,19 +121,21 @@ __device__ __forceinline__ double readlane_f64(double v, int l) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-__global__ void __launch_bounds__(256)
+template <int NW>  // waves; lane i of wave w keeps columns j = w + NW c (c < 64 / NW)
+__global__ void __launch_bounds__(64 * NW)
 spd_inverse_reg64_kernel(const double* __restrict__ A, const double* __restrict__ shift, int d, int nvar,
                          double* __restrict__ out, int* __restrict__ status) {
+  constexpr int NC = 64 / NW;
   __shared__ double Ms[64 * 65];    // the result, for the symmetrised write-out
   __shared__ double colv[2][64];    // the pivot column, double-buffered
   const int n = blockIdx.x, v = blockIdx.y;
   const double s = shift[n * nvar + v];
   const double* An = A + (long)n * d * d;
   const int i = threadIdx.x & 63, w = threadIdx.x >> 6;
-  double h[16];
+  double h[NC];
 #pragma unroll
-  for (int c = 0; c < 16; ++c) {
-    const int j = w + 4 * c;
+  for (int c = 0; c < NC; ++c) {
+    const int j = w + NW * c;
     h[c] = (i < d && j < d) ? An[i * d + j] + (i == j ? s : 0.0) : 0.0;
   }
   if (w == 0) colv[0][i] = h[0];
@@ -144,8 +146,8 @@ spd_inverse_reg64_kernel(const double* __restrict__ A, const double* __restrict_
     const double p = 1.0 / pk;
     if (threadIdx.x == 0 && !(pk > 0.0) && status) atomicExch(status, 1);  // not SPD (or NaN)
 #pragma unroll
-    for (int c = 0; c < 16; ++c) {
-      const int j = w + 4 * c;
+    for (int c = 0; c < NC; ++c) {
+      const int j = w + NW * c;
       const double mkj = readlane_f64(h[c], k) * p;  // row k, scaled (lane k of this wave)
       double val = h[c];
       if (j == k) val = (i == k) ? p : -aik * p;
@@ -154,26 +156,19 @@ spd_inverse_reg64_kernel(const double* __restrict__ A, const double* __restrict_
       h[c] = val;
     }
     const int kn = k + 1;
-    if (kn < d && w == (kn & 3)) {  // owner of the next pivot column publishes it
-      double* dst = &colv[kn & 1][i];
-      switch (kn >> 2) {  // wave-uniform register select
-#define GADMM_PUB(C) \
-  case C:            \
-    *dst = h[C];     \
-    break;
-        GADMM_PUB(0) GADMM_PUB(1) GADMM_PUB(2) GADMM_PUB(3) GADMM_PUB(4) GADMM_PUB(5) GADMM_PUB(6) GADMM_PUB(7)
-        GADMM_PUB(8) GADMM_PUB(9) GADMM_PUB(10) GADMM_PUB(11) GADMM_PUB(12) GADMM_PUB(13) GADMM_PUB(14)
-        GADMM_PUB(15)
-#undef GADMM_PUB
-      }
+    if (kn < d && w == kn % NW) {  // owner of the next pivot column publishes it
+      double nxt = 0.0;
+#pragma unroll
+      for (int c = 0; c < NC; ++c) nxt = (c == kn / NW) ? h[c] : nxt;
+      colv[kn & 1][i] = nxt;
     }
     __syncthreads();
   }
 #pragma unroll
-  for (int c = 0; c < 16; ++c) Ms[i * 65 + w + 4 * c] = h[c];
+  for (int c = 0; c < NC; ++c) Ms[i * 65 + w + NW * c] = h[c];
   __syncthreads();
   double* o = out + ((long)n * nvar + v) * d * d;
-  for (int r = w; r < d; r += 4)
+  for (int r = w; r < d; r += NW)
     if (i < d) o[r * d + i] = 0.5 * (Ms[r * 65 + i] + Ms[i * 65 + r]);
 }
 
@@ -191,7 +186,10 @@ extern "C" int gadmm_spd_inverse_small_f64(const double* A, const double* shift,
   const char* rge = getenv("GADMM_INV_REG");  // A/B switch: 0 = the LDS 64-wide kernel
   const bool reg = !(rge && rge[0] == '0');
   if (d <= 64 && gj64 && reg) {
-    hipLaunchKernelGGL(spd_inverse_reg64_kernel, dim3(N, nvar), dim3(256), 0, st, A, shift, d, nvar, out, status);
+    const int nw = rge ? atoi(rge) : 8;  // waves per matrix (A/B: GADMM_INV_REG=4/8/16)
+    if (nw == 4) hipLaunchKernelGGL(spd_inverse_reg64_kernel<4>, dim3(N, nvar), dim3(256), 0, st, A, shift, d, nvar, out, status);
+    else if (nw == 16) hipLaunchKernelGGL(spd_inverse_reg64_kernel<16>, dim3(N, nvar), dim3(1024), 0, st, A, shift, d, nvar, out, status);
+    else hipLaunchKernelGGL(spd_inverse_reg64_kernel<8>, dim3(N, nvar), dim3(512), 0, st, A, shift, d, nvar, out, status);
     GADMM_CHECK(hipGetLastError());
     return 0;
   }
