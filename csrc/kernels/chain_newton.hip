@@ -12,12 +12,12 @@
 //   H = X^T diag(w) X + (lam + deg rho) I,   w = sigma (1 - sigma)
 // (the same stopping rule and iteration cap as models/logistic.py:newton_prox, the torch path).
 //
-// One 256-thread workgroup per worker (d, m <= 64), everything in LDS:
+// One 512-thread workgroup per worker (d, m <= 64), everything in LDS:
 //   margins / gradient: 4 threads per row (column) with two xor shuffles;
 //   Hessian: lower-triangular 4x4 register blocks (two 16-B LDS reads per operand per sample), the
 //     samples split over a lane pair;
 //   solve: block Gauss-Jordan on [H | g] with 4 x 4 pivot blocks (SPD, no pivoting); lane i of wave
-//     w keeps row i's columns j = w (mod 4) in registers, each block's 4 columns go through LDS,
+//     w keeps row i's columns j = w (mod 8) in registers, each block's 4 columns go through LDS,
 //     one barrier per 4 pivots, no back substitution.
 #include "gadmm_common.h"
 #include "gadmm_chain.h"
@@ -25,7 +25,9 @@
 
 namespace {
 
-constexpr int NTN = 256;
+constexpr int NTN = 512;           // 8 waves: each keeps 8 of a row's 64 columns in the solve
+constexpr int NWV = NTN / 64;
+constexpr int NCW = 64 / NWV;      // columns per lane
 constexpr int NEWTON_MAX = 50;
 constexpr double NEWTON_TOL = 1e-13;
 
@@ -129,9 +131,9 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
       s += __shfl_xor(s, 2, 64);
       if (q == 0 && j < d) gv[j] = -s + shift * xv[j] + cv[j];
     }
-    {  // Hessian, lower 4x4 blocks (bj >= bk); the two lanes of a pair split the samples
-      const int nbr = (d + 3) >> 2, nb = nbr * (nbr + 1) / 2, half = t & 1;
-      for (int b = t >> 1; b < nb; b += NTN / 2) {
+    {  // Hessian, lower 4x4 blocks (bj >= bk); the four lanes of a quad split the samples
+      const int nbr = (d + 3) >> 2, nb = nbr * (nbr + 1) / 2, half = t & 3;
+      for (int b = t >> 2; b < nb; b += NTN / 4) {
         int bj = 0, bk = b;
         while (bk > bj) {  // block-row bj holds bj + 1 blocks
           bk -= bj + 1;
@@ -143,7 +145,7 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
 #pragma unroll
           for (int v = 0; v < 4; ++v) acc[u][v] = 0.0;
 #pragma unroll 4
-        for (int i = half; i < m; i += 2) {
+        for (int i = half; i < m; i += 4) {
           const double w = wv[i];
           const double2 a01 = *reinterpret_cast<const double2*>(Xs + i * DP + 4 * bj);
           const double2 a23 = *reinterpret_cast<const double2*>(Xs + i * DP + 4 * bj + 2);
@@ -160,7 +162,8 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
         for (int u = 0; u < 4; ++u)
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
-            const double tot = acc[u][v] + __shfl_xor(acc[u][v], 1, 64);
+            const double t2 = acc[u][v] + __shfl_xor(acc[u][v], 1, 64);
+            const double tot = t2 + __shfl_xor(t2, 2, 64);
             const int r = 4 * bj + u, c = 4 * bk + v;
             if (half == 0 && r < d && c <= r) Hs[r * DH + c] = tot + (r == c ? shift : 0.0);
           }
@@ -169,18 +172,18 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
     lds_barrier();
     if (TL && t == 0) tl[k * 5 + 2] = (long long)__builtin_amdgcn_s_memrealtime();
     {  // Block Gauss-Jordan on [H | g] with 4 x 4 pivot blocks (SPD, no pivoting). Lane i of wave w
-       // keeps row i's columns j = w + 4c (c < 16) in registers; wave 0 also carries g_i. Block b
-       // (pivots p = 4b .. 4b + 3) has one column in each wave: every wave publishes its column of
-       // the block into a double-buffered LDS slab, one barrier, then every lane eliminates the
+       // keeps row i's columns j = w + 8c (c < 8) in registers; wave 0 also carries g_i. Block b
+       // (pivots p = 4b .. 4b + 3) has one column in each of four waves: they publish them into a
+       // double-buffered LDS slab, one barrier, then every lane eliminates the
        // block from its row (rows above the block too, so no back substitution is left):
        //   l_i = H[i][p:p+4] P^-1,  H[i][:] -= l_i H[p:p+4][:],  g_i -= l_i g[p:p+4]
        // (P = the 4 x 4 pivot block, factorised redundantly per lane as L D L^T). Indices >= d are
        // identity padding. A pivot row keeps row (i - p) of P^-1 for the final block solve.
       const int i = lane;
-      double h[16];
+      double h[NCW];
 #pragma unroll
-      for (int c = 0; c < 16; ++c) {
-        const int j = wid + 4 * c;
+      for (int c = 0; c < NCW; ++c) {
+        const int j = wid + NWV * c;
         h[c] = (i < d && j < d) ? (j <= i ? Hs[i * DH + j] : Hs[j * DH + i]) : (i == j ? 1.0 : 0.0);
       }
       double gi = (wid == 0 && i < d) ? gv[i] : 0.0;
@@ -189,15 +192,14 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
       for (int bb = 0; bb < nb; ++bb) {
         const int p = 4 * bb;
         double* slab = colv + (bb & 1) * 256;  // [4][64]: column p + q of the current matrix
-        switch (bb) {  // wave-uniform register select: no per-entry cndmasks
-#define GADMM_PUB(C)            \
-  case C:                       \
-    slab[wid * 64 + i] = h[C];  \
-    break;
-          GADMM_PUB(0) GADMM_PUB(1) GADMM_PUB(2) GADMM_PUB(3) GADMM_PUB(4) GADMM_PUB(5) GADMM_PUB(6) GADMM_PUB(7)
-          GADMM_PUB(8) GADMM_PUB(9) GADMM_PUB(10) GADMM_PUB(11) GADMM_PUB(12) GADMM_PUB(13) GADMM_PUB(14)
-          GADMM_PUB(15)
-#undef GADMM_PUB
+        {  // the block's 4 columns belong to waves (p mod NWV) .. +3, register p / NWV
+          const int q = wid - (p % NWV);
+          if (q >= 0 && q < 4) {
+            double hv = 0.0;
+#pragma unroll
+            for (int c = 0; c < NCW; ++c) hv = (c == p / NWV) ? h[c] : hv;
+            slab[q * 64 + i] = hv;
+          }
         }
         lds_barrier();
         double P[4][4], R[4];
@@ -237,8 +239,8 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
           f0 = f1 = f2 = f3 = 0.0;  // pivot rows are not eliminated by their own block
         }
 #pragma unroll
-        for (int c = 0; c < 16; ++c) {
-          const int j = wid + 4 * c;  // H[p + q][j] = H[j][p + q] for the trailing columns j >= p + 4
+        for (int c = 0; c < NCW; ++c) {
+          const int j = wid + NWV * c;  // H[p + q][j] = H[j][p + q] for the trailing columns j >= p + 4
           double v = h[c];
           v = fma(-f0, slab[0 * 64 + j], v);
           v = fma(-f1, slab[1 * 64 + j], v);
