@@ -86,20 +86,31 @@ __device__ __forceinline__ void blocked_monitor(const PersistArgs& a, double* ld
 
 // ---- objective workgroup: wave v evaluates f_q(theta_q^it) of owned chain position q (A_q in VGPRs,
 // quad layout) off the critical path and posts it to the monitor ring
-template <int QT, bool SYS>
+template <int QT, bool SYS, bool DYN = false>
 __device__ __forceinline__ void blocked_objective(const PersistArgs& a, double* lds, int v, int lane, int q,
                                                   unsigned long long deadline, __amdgpu_buffer_rsrc_t rob,
                                                   __amdgpu_buffer_rsrc_t rtab) {
   const int d = a.d, n = a.n;
   const long ring_base = 2L * n * 2 * d;  // theta ring [ring][n][d] after the exchange table
-  const PhaseSlot so = a.slots[q];
+  PhaseSlot so = DYN ? a.ep_slots[q] : a.slots[q];
   const bool in = lane < d;
   double Aq[4][QT];
   quad_load<QT>(Aq, a.A + (long)so.li * d * d, d, true);
-  const double bo = in ? a.b[(long)so.li * d + lane] : 0.0;
-  const double hy = 0.5 * a.yy[so.li];
+  double bo = in ? a.b[(long)so.li * d + lane] : 0.0;
+  double hy = 0.5 * a.yy[so.li];
   double* xo = lds + v * QSTAGE;
+  int ep = 0, next_start = (DYN && a.n_epochs > 1) ? a.epoch_start[1] : 0x7fffffff;
   for (int it = a.start_iter;; ++it) {
+    if constexpr (DYN) {
+      if (it == next_start) {  // D-GADMM re-chain: another worker now sits at position q
+        ++ep;
+        next_start = ep + 1 < a.n_epochs ? a.epoch_start[ep + 1] : 0x7fffffff;
+        so = a.ep_slots[(long)ep * n + q];
+        quad_load<QT>(Aq, a.A + (long)so.li * d * d, d, true);
+        bo = in ? a.b[(long)so.li * d + lane] : 0.0;
+        hy = 0.5 * a.yy[so.li];
+      }
+    }
     const unsigned tag = make_tag(a.epoch, it);
     const long off = (ring_base + ((long)(it % a.ring) * n + q) * d + lane) * 16;
     double x = 0.0;
@@ -131,7 +142,14 @@ __device__ __forceinline__ void blocked_objective(const PersistArgs& a, double* 
 // (rank 0 only).
 // TL: the instrumented instantiation (timeline stamps, experiment bits); the production one has no
 // diagnostics code in its loop.
-template <int DB, bool SYS, bool TL>
+// DYN: D-GADMM in one launch (single GPU). Positions stay with their workgroups; at every epoch
+// start (ep_slots [E][n] in chain-position order, ep_pos [E][n] worker -> position) the owned
+// positions publish their worker's (theta, mu) by WORKER id into an epoch table, and every computed
+// position loads the state of the worker that the new chain puts there, with its inverse, b and A.
+// A worker that was a head owes its dual of the last iteration of the old chain: the loader applies
+// it with the worker's OLD neighbours' theta, read from the same table (the reference order,
+// dynamic_group_ADMM_closedForm.m:153-168). The regular halo schedule restarts after the switch.
+template <int DB, bool SYS, bool TL, bool DYN = false>
 __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a) {
   constexpr int QT = DB / 4;  // quad layout: columns per lane
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -162,7 +180,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   const long ring_base = 2L * n * 2 * d;  // theta ring [ring][n][d] after the exchange table
   if ((int)blockIdx.x >= W) {
     const int q = seg_lo + ((int)blockIdx.x - W) * MAXW + v;  // an owned chain position
-    if (q <= seg_hi) blocked_objective<QT, SYS>(a, lds, v, lane, q, deadline, rob, rtab);
+    if (q <= seg_hi) blocked_objective<QT, SYS, DYN>(a, lds, v, lane, q, deadline, rob, rtab);
     return;
   }
 
@@ -180,8 +198,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   const int p = ra + u;  // this wave's chain position
   const bool active = u < nv;
   const bool owned = active && p >= s0 && p <= e0;
-  const PhaseSlot sl = a.slots[active ? p : 0];  // slots are sorted by chain position
-  const int li = sl.li, w = sl.gid;
+  PhaseSlot sl = DYN ? a.ep_slots[active ? p : 0] : a.slots[active ? p : 0];  // sorted by chain position
+  int li = sl.li, w = sl.gid;
   const bool has_l = active && sl.left >= 0, has_r = active && sl.right >= 0;
   const bool head = (p % 2) == 0;
   const int deg = (int)has_l + (int)has_r;
@@ -213,9 +231,14 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   };
   double th = (active && in) ? a.theta[(long)w * d + lane] : 0.0;
   double mu = (active && in) ? a.mu[(long)li * d + lane] : 0.0;
-  const double bb = (active && in) ? a.b[(long)li * d + lane] : 0.0;
+  double bb = (active && in) ? a.b[(long)li * d + lane] : 0.0;
   thS[u * 64 + lane] = th;
   int pending = a.pending_in;
+  // DYN: epoch cursor, regular exchange schedule (restarts after every re-chain) and its slot
+  // counter, and the epoch exchange table [2][n][2][d] after the theta ring
+  int ep = 0, next_start = (DYN && a.n_epochs > 1) ? a.epoch_start[1] : 0x7fffffff;
+  int next_x = a.start_iter + k, xc = 0;
+  const long etab_base = 2L * n * 2 * d + (long)a.ring * n * d;
   if (threadIdx.x == 0) stop_iter_lds = 0;
   lds_barrier();
 
@@ -225,7 +248,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   // this GPU's table and into every peer GPU that computes position p too
   auto publish = [&](int j) {
     const unsigned tag = make_tag(a.epoch, j + 1);
-    const int base = (((((j + 1 - a.start_iter) / k) & 1) * n + p) * 2) * d;
+    const int sel = DYN ? (xc & 1) : (((j + 1 - a.start_iter) / k) & 1);
+    const int base = ((sel * n + p) * 2) * d;
     store_granule<SYS>(rtab, (base + lane) * 16, tag, th);
     store_granule<SYS>(rtab, (base + d + lane) * 16, tag, mu);
     for (int q = 0; q < a.blk_npeer; ++q)
@@ -242,12 +266,66 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     if (it > a.max_iter + a.lag) break;
     const bool stamp = TL && v == 0 && it - a.start_iter < a.timeline_iters;  // wave-uniform (SGPR stamps)
     if (stamp) ts[0] = (long long)now_ticks();
+    if constexpr (DYN) {
+      if (it == next_start) {  // ---- re-chain (dynamic_group_ADMM_closedForm.m:18-21)
+        const unsigned tag = make_tag(a.epoch, it);
+        const long eb = etab_base + (long)((ep + 1) & 1) * n * 2 * d;  // this switch's slot
+        if (owned && in) {  // the worker's state after iteration it - 1 (a head's dual still pending)
+          const long base = eb + (long)w * 2 * d;
+          store_granule<SYS>(rtab, (int)((base + lane) * 16), tag, th);
+          store_granule<SYS>(rtab, (int)((base + d + lane) * 16), tag, mu);
+        }
+        ++ep;
+        next_start = ep + 1 < a.n_epochs ? a.epoch_start[ep + 1] : 0x7fffffff;
+        if (active) {
+          sl = a.ep_slots[(long)ep * n + p];
+          li = sl.li;
+          w = sl.gid;
+          const int po = a.ep_pos[(long)(ep - 1) * n + w];       // the worker's old position
+          const PhaseSlot so = a.ep_slots[(long)(ep - 1) * n + po];
+          const bool flush = pending && (po % 2) == 0;           // it was a head: dual pending
+          const bool fl = flush && so.left >= 0, fr = flush && so.right >= 0;
+          double t0 = 0.0, t1 = 0.0, tl = 0.0, tr = 0.0;
+          bool ok = true;
+          for (int spin = 0;; ++spin) {
+            bool g0 = true;
+            if (in) {
+              const long b0 = eb + (long)w * 2 * d;
+              g0 &= load_granule<SYS>(rtab, (int)((b0 + lane) * 16), tag, &t0);
+              g0 &= load_granule<SYS>(rtab, (int)((b0 + d + lane) * 16), tag, &t1);
+              if (fl) g0 &= load_granule<SYS>(rtab, (int)((eb + (long)so.left * 2 * d + lane) * 16), tag, &tl);
+              if (fr) g0 &= load_granule<SYS>(rtab, (int)((eb + (long)so.right * 2 * d + lane) * 16), tag, &tr);
+            }
+            if (__all(g0)) break;
+            if ((spin & 7) == 7 && now_ticks() > deadline) {
+              ok = false;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (!ok && lane == 0) abort_lds = 1;
+          th = in ? t0 : 0.0;
+          double m = in ? t1 : 0.0;
+          if (fl) m = m - rho * (tl - th);  // the old chain's end-of-iteration dual
+          if (fr) m = m + rho * (th - tr);
+          mu = in ? m : 0.0;
+          bb = in ? a.b[(long)li * d + lane] : 0.0;
+          quad_load<QT>(Mq, a.Minv + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)d * d, d, true);
+          thS[u * 64 + lane] = th;
+        }
+        pending = 0;
+        next_x = it + k;
+        lds_barrier();
+        if (abort_lds) break;
+      }
+    }
     // ---- halo exchange every k iterations (state after iteration it - 1); the owned workers
     // published theirs during the tail phase of it - 1 (publish() below)
-    if (it > a.start_iter && (it - a.start_iter) % k == 0) {
+    if (DYN ? it == next_x : (it > a.start_iter && (it - a.start_iter) % k == 0)) {
       if (active && !owned) {
         const unsigned tag = make_tag(a.epoch, it);
-        const int base = (((((it - a.start_iter) / k) & 1) * n + p) * 2) * d;
+        const int sel = DYN ? (xc & 1) : (((it - a.start_iter) / k) & 1);
+        const int base = ((sel * n + p) * 2) * d;
         double t0 = 0.0, t1 = 0.0;
         bool ok = true;
         for (int spin = 0;; ++spin) {
@@ -270,6 +348,10 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       }
       lds_barrier();  // refreshed halo theta visible to the neighbouring waves
       if (abort_lds) break;
+      if constexpr (DYN) {
+        next_x = it + k;
+        ++xc;
+      }
     }
     if (stamp) ts[1] = ts[2] = ts[3] = (long long)now_ticks();
 
@@ -301,7 +383,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     if (stamp) ts[4] = (long long)now_ticks();
 
     // ---- tail phase; the (idle head) decision wave fetches decision[it + 1 - lag]
-    const bool xnext = (it + 1 - a.start_iter) % k == 0;  // the next iteration starts with an exchange
+    // the next iteration starts with a regular exchange (DYN: unless it starts a new epoch)
+    const bool xnext = DYN ? (it + 1 == next_x && it + 1 != next_start) : (it + 1 - a.start_iter) % k == 0;
     // tail-wave stamps (wave MAXW/2), timeline row 128 + g: [start, rhs, gemv, stores, barrier]
     const bool tstamp = TL && v == MAXW / 2 && it - a.start_iter < a.timeline_iters && g < 128;
     long long tt[4] = {0, 0, 0, 0};
@@ -708,8 +791,10 @@ long gadmm_chain_blocked_lds(int d, int len) {
   return (long)(MAXW * 64 + MAXW * QSTAGE) * 8;
 }
 
-// Granules of the blk_tab buffer: exchange table [2][n][2][d] + theta ring [ring][n][d].
+// Granules of the blk_tab buffer: exchange table [2][n][2][d] + theta ring [ring][n][d]
+// (+ the D-GADMM epoch table [2][n][2][d]: gadmm_chain_blocked_tab_granules_dyn).
 long gadmm_chain_blocked_tab_granules(int n, int d, int ring) { return 2L * n * 2 * d + (long)ring * n * d; }
+long gadmm_chain_blocked_tab_granules_dyn(int n, int d, int ring) { return 4L * n * 2 * d + (long)ring * n * d; }
 
 int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   const PersistArgs& a = *args;
@@ -728,7 +813,7 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   }
   const int nseg = multi ? a.seg_hi - a.seg_lo + 1 : a.n;
   const int W = (nseg + a.blk_len - 1) / a.blk_len;
-  if (a.blk_pw == 2) {  // paired-wave kernel
+  if (a.blk_pw == 2 && a.n_epochs == 0) {  // paired-wave kernel (static chains only)
     if (a.blk_len + 4 * a.blk_k > PCAP || a.timeline) {
       gadmm_set_error("blocked chain kernel (pw=2): L + 4k > %d or timeline requested", PCAP);
       return -1;
@@ -765,7 +850,14 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   }
   const void* fn;
   const bool tl = a.timeline != nullptr;
-  if (a.sys_scope) {
+  if (a.n_epochs > 0) {  // D-GADMM in one launch: one GPU, 12-wave layout, no instrumentation
+    if (multi || tl || a.sys_scope || !a.epoch_start || !a.ep_slots || !a.ep_pos) {
+      gadmm_set_error("blocked chain kernel: dynamic epochs need one GPU, epoch tables, no timeline");
+      return -1;
+    }
+    fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, false, false, true>
+                   : (const void*)chain_blocked_kernel<52, false, false, true>;
+  } else if (a.sys_scope) {
     if (tl) fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, true, true> : (const void*)chain_blocked_kernel<52, true, true>;
     else fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, true, false> : (const void*)chain_blocked_kernel<52, true, false>;
   } else {

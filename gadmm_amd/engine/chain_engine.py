@@ -337,7 +337,14 @@ class NativeChainEngine:
                 raise RuntimeError("dynamic persistent kernel not eligible for this engine/config")
         elif not self.persistent_eligible(fabric):
             raise RuntimeError("persistent kernel not eligible for this engine/config")
-        plan = self.blocked_plan(fabric, timeline=timeline_iters > 0) if epochs is None else None
+        plan = self.blocked_plan(fabric, timeline=timeline_iters > 0)
+        if epochs is not None and (plan is None or plan[3] != 1 or timeline_iters > 0 or self.n_local != self.n_total
+                                   or os.environ.get("GADMM_BLOCKED_DYN", "0") != "1"):
+            # D-GADMM: the blocked kernel's dynamic mode (opt-in GADMM_BLOCKED_DYN=1; one GPU, 12-wave
+            # layout) is bit-identical but not faster: its epoch state pushes the kernel past the
+            # SGPR budget (165 SGPR + 10 VGPR spills in the hot loop), 1.616 vs 1.623 ms per solve
+            # (profiles/r01c_dgadmm_blocked)
+            plan = None
         if plan is not None:
             lag = max(lag, 8)  # the objective takes one more hop (worker -> objective wave -> monitor)
         ring = lag + 4
@@ -412,13 +419,24 @@ class NativeChainEngine:
             E, n = P.shape
             pos_of = np.argsort(P, axis=1)                                          # worker -> position
             loc = np.asarray([int(w) for w in self.local_ids], dtype=np.int64)
-            k = pos_of[:, loc]                                                      # (E, n_local)
-            rows = np.arange(E)[:, None]
-            left = np.where(k > 0, P[rows, np.maximum(k - 1, 0)], -1)
-            right = np.where(k + 1 < n, P[rows, np.minimum(k + 1, n - 1)], -1)
-            li = np.broadcast_to(np.arange(len(loc)), k.shape)
-            es = np.stack([li, np.broadcast_to(loc, k.shape), left, right], axis=-1).astype(np.int32).reshape(-1)
-            pp = k.astype(np.int32).reshape(-1)
+            if plan is not None:
+                # blocked kernel: slots in chain-POSITION order per epoch (li, gid, left, right), and
+                # worker -> position
+                li_of = np.full(self.n_total, -1, dtype=np.int64)
+                li_of[loc] = np.arange(len(loc))
+                lft = np.concatenate([np.full((E, 1), -1, dtype=np.int64), P[:, :-1]], axis=1)
+                rgt = np.concatenate([P[:, 1:], np.full((E, 1), -1, dtype=np.int64)], axis=1)
+                es = np.stack([li_of[P], P, lft, rgt], axis=-1).astype(np.int32).reshape(-1)
+                pp = pos_of.astype(np.int32).reshape(-1)
+            else:
+                # per-worker kernel: the slot / position of every LOCAL worker per epoch
+                k = pos_of[:, loc]                                                  # (E, n_local)
+                rows = np.arange(E)[:, None]
+                left = np.where(k > 0, P[rows, np.maximum(k - 1, 0)], -1)
+                right = np.where(k + 1 < n, P[rows, np.minimum(k + 1, n - 1)], -1)
+                li = np.broadcast_to(np.arange(len(loc)), k.shape)
+                es = np.stack([li, np.broadcast_to(loc, k.shape), left, right], axis=-1).astype(np.int32).reshape(-1)
+                pp = k.astype(np.int32).reshape(-1)
             with torch.cuda.stream(self.stream):
                 st_t = torch.tensor(starts, dtype=torch.int32, device=dev)
                 es_t = torch.from_numpy(np.ascontiguousarray(es)).to(dev)
@@ -432,12 +450,14 @@ class NativeChainEngine:
             pa.timeline, pa.timeline_iters = tl.data_ptr(), int(timeline_iters)
         import time as _time
         if plan is not None:  # temporally blocked kernel: one halo hand-off per k iterations
-            ng = int(self.lib.gadmm_chain_blocked_tab_granules(self.n_total, self.d, ring))
+            ng = int((self.lib.gadmm_chain_blocked_tab_granules_dyn if epochs is not None else
+                      self.lib.gadmm_chain_blocked_tab_granules)(self.n_total, self.d, ring))
             if getattr(self, "_blk_tab", None) is None or self._blk_tab.numel() != ng * 4:
                 self._blk_tab = torch.zeros((ng * 4,), dtype=torch.int32, device=dev)
             pa.blk_k, pa.blk_len, pa.blk_pw = plan[0], plan[1], plan[3]
             pa.blk_tab = self._blk_tab.data_ptr()
-        self.last_kernel = "blocked(k=%d,L=%d,W=%d,pw=%d)" % plan if plan is not None else "per-worker"
+        self.last_kernel = ("blocked%s(k=%d,L=%d,W=%d,pw=%d)" % ((("-dyn" if epochs is not None else ""),) + tuple(plan))
+                            if plan is not None else "per-worker")
         with torch.cuda.stream(self.stream):
             t0 = _time.perf_counter()
             if plan is not None:

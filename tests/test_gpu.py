@@ -409,8 +409,8 @@ def test_xgmi_fabric_two_processes_one_gpu(lin24, lin_obj0):
     assert np.array_equal(np.asarray(res[0]["trace"]), single.obj)  # bit-identical to the 1-GPU persistent run
 
 
-@pytest.mark.parametrize("coh", [10, 1])
-def test_dgadmm_persistent_dynamic_matches_epoch_path(lin24, lin_obj0, coh):
+@pytest.mark.parametrize("coh,blocked", [(10, "1"), (1, "1"), (10, "0"), (1, "0"), (3, "1")])
+def test_dgadmm_persistent_dynamic_matches_epoch_path(lin24, lin_obj0, coh, blocked, monkeypatch):
     """D-GADMM in one persistent launch (per-epoch chains in device tables) == the epoch-by-epoch
     engine: same iterations, bit-identical objective trace, same communication-energy trace, and the
     schedule left in the same state. coh = 1 re-chains every iteration: a head's pending-dual flush
@@ -420,9 +420,12 @@ def test_dgadmm_persistent_dynamic_matches_epoch_path(lin24, lin_obj0, coh):
     from gadmm_amd.algorithms import dynamic_group_admm
     from gadmm_amd.parallel import topology as T
 
+    monkeypatch.setenv("GADMM_BLOCKED_DYN", blocked)  # 1: the blocked kernel's dynamic mode, 0: per-worker
     m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
     p0, c0, _ = T.find_path(24, np.random.default_rng(5))
     a = dynamic_group_admm(m, 1.0, lin_obj0, 1e-4, 3000, p0, c0, coh, seed=99)
+    kern = a.extra["engine_obj"].last_kernel
+    assert kern.startswith("blocked-dyn(") if blocked == "1" else kern == "per-worker", kern
     b = dynamic_group_admm(m, 1.0, lin_obj0, 1e-4, 3000, p0, c0, coh, seed=99, engine_opts={"persistent": False})
     assert a.extra["engine"] == "persistent-dynamic" and b.extra["engine"] == "epochs"
     assert a.iters == b.iters and a.converged
