@@ -92,3 +92,33 @@ extern "C" int gadmm_greedy_chains(const double* uv, int E, int n, double side, 
   for (auto& th : pool) th.join();
   return 0;
 }
+
+// Per-epoch device tables of the one-launch D-GADMM kernel (chain_persistent.hip, dynamic mode),
+// from the chains P [E][n] (position -> worker): for each local worker li (global id loc[li]) its
+// slot (li, gid, left, right) and chain position in every epoch. Replaces ~0.5 ms of numpy per
+// solve (argsort + fancy indexing over ~300 epochs) on the host path of every D-GADMM solve.
+extern "C" int gadmm_epoch_tables(const long long* P, int E, int n, const long long* loc, int nloc, int* slots,
+                                  int* pos) {
+  if (E < 0 || n < 1 || nloc < 0 || !P || (nloc > 0 && (!loc || !slots || !pos))) return -1;
+  std::vector<int> pos_of(n);
+  for (int e = 0; e < E; ++e) {
+    const long long* pe = P + (size_t)e * n;
+    for (int p = 0; p < n; ++p) {
+      const long long w = pe[p];
+      if (w < 0 || w >= n) return -2;
+      pos_of[w] = p;
+    }
+    for (int li = 0; li < nloc; ++li) {
+      const long long w = loc[li];
+      if (w < 0 || w >= n) return -3;
+      const int k = pos_of[w];
+      int* s = slots + ((size_t)e * nloc + li) * 4;
+      s[0] = li;
+      s[1] = (int)w;
+      s[2] = k > 0 ? (int)pe[k - 1] : -1;
+      s[3] = k + 1 < n ? (int)pe[k + 1] : -1;
+      pos[(size_t)e * nloc + li] = k;
+    }
+  }
+  return 0;
+}

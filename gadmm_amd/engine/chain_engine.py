@@ -43,6 +43,21 @@ class EngineRun:
         return self.done == 1
 
 
+def epoch_tables_numpy(P: np.ndarray, loc: np.ndarray):
+    """Per-epoch (slots (E, n_local, 4) = (li, gid, left, right), positions (E, n_local)) of the local
+    workers ``loc`` for chains ``P`` (E, n) position -> worker: the reference for the native
+    ``gadmm_epoch_tables`` the dynamic persistent kernel's tables come from."""
+    E, n = P.shape
+    pos_of = np.argsort(P, axis=1)
+    k = pos_of[:, loc]
+    rows = np.arange(E)[:, None]
+    left = np.where(k > 0, P[rows, np.maximum(k - 1, 0)], -1)
+    right = np.where(k + 1 < n, P[rows, np.minimum(k + 1, n - 1)], -1)
+    li = np.broadcast_to(np.arange(len(loc)), k.shape)
+    slots = np.stack([li, np.broadcast_to(loc, k.shape), left, right], axis=-1).astype(np.int32)
+    return slots, k.astype(np.int32)
+
+
 class NativeChainEngine:
     def __init__(self, X_loc: torch.Tensor, y_loc: torch.Tensor, local_ids: Sequence[int], n_total: int,
                  model: str = "linear", rho: float = 1.0, obj0: float = 0.0, tol: float = 1e-4,
@@ -417,9 +432,9 @@ class NativeChainEngine:
             if starts[0] != int(start_iter) or any(b <= a for a, b in zip(starts, starts[1:])):
                 raise ValueError("epochs must start at start_iter and be increasing")
             E, n = P.shape
-            pos_of = np.argsort(P, axis=1)                                          # worker -> position
             loc = np.asarray([int(w) for w in self.local_ids], dtype=np.int64)
             if plan is not None:
+                pos_of = np.argsort(P, axis=1)                                      # worker -> position
                 # blocked kernel: slots in chain-POSITION order per epoch (li, gid, left, right), and
                 # worker -> position
                 li_of = np.full(self.n_total, -1, dtype=np.int64)
@@ -429,14 +444,13 @@ class NativeChainEngine:
                 es = np.stack([li_of[P], P, lft, rgt], axis=-1).astype(np.int32).reshape(-1)
                 pp = pos_of.astype(np.int32).reshape(-1)
             else:
-                # per-worker kernel: the slot / position of every LOCAL worker per epoch
-                k = pos_of[:, loc]                                                  # (E, n_local)
-                rows = np.arange(E)[:, None]
-                left = np.where(k > 0, P[rows, np.maximum(k - 1, 0)], -1)
-                right = np.where(k + 1 < n, P[rows, np.minimum(k + 1, n - 1)], -1)
-                li = np.broadcast_to(np.arange(len(loc)), k.shape)
-                es = np.stack([li, np.broadcast_to(loc, k.shape), left, right], axis=-1).astype(np.int32).reshape(-1)
-                pp = k.astype(np.int32).reshape(-1)
+                # per-worker kernel: the slot / position of every LOCAL worker per epoch (native C++
+                # builder, csrc/runtime/topology.cpp; the numpy equivalent is epoch_tables_numpy)
+                P = np.ascontiguousarray(P)
+                es = np.empty((E * len(loc) * 4,), dtype=np.int32)
+                pp = np.empty((E * len(loc),), dtype=np.int32)
+                native.check(self.lib.gadmm_epoch_tables(P.ctypes.data, E, n, loc.ctypes.data, len(loc),
+                                                         es.ctypes.data, pp.ctypes.data), "epoch_tables")
             with torch.cuda.stream(self.stream):
                 st_t = torch.tensor(starts, dtype=torch.int32, device=dev)
                 es_t = torch.from_numpy(np.ascontiguousarray(es)).to(dev)

@@ -75,3 +75,21 @@ def test_native_greedy_chains_match_numpy(monkeypatch):
             s5 = T.PathSchedule(n, list(range(n)), np.zeros(n - 1), 10, kind=kind, seed=11)
             s5.prefetch(7)
             assert s4.path == s5.path and np.array_equal(s4.rng.random(4), s5.rng.random(4))
+
+
+def test_native_epoch_tables_match_numpy():
+    """csrc/runtime/topology.cpp:gadmm_epoch_tables == the numpy reference (engine/chain_engine.py)."""
+    import numpy as np
+    from gadmm_amd.ops import native
+    from gadmm_amd.engine.chain_engine import epoch_tables_numpy
+    lib = native.load(build_if_missing=False)
+    rng = np.random.default_rng(3)
+    for E, n, loc in ((7, 24, np.arange(24)), (5, 9, np.array([4, 0, 7])), (1, 2, np.array([1]))):
+        P = np.ascontiguousarray(np.stack([rng.permutation(n) for _ in range(E)]).astype(np.int64))
+        loc = np.ascontiguousarray(loc.astype(np.int64))
+        es = np.empty((E * len(loc) * 4,), dtype=np.int32)
+        pp = np.empty((E * len(loc),), dtype=np.int32)
+        assert lib.gadmm_epoch_tables(P.ctypes.data, E, n, loc.ctypes.data, len(loc), es.ctypes.data,
+                                      pp.ctypes.data) == 0
+        s_ref, p_ref = epoch_tables_numpy(P, loc)
+        assert np.array_equal(es.reshape(E, len(loc), 4), s_ref) and np.array_equal(pp.reshape(E, len(loc)), p_ref)
