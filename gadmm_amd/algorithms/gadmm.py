@@ -260,7 +260,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         iters, done = r.iters, r.done
         p2p, mon = r.p2p_bytes, r.monitor_bytes
         per = float(np.sum(schedule.cost)) * (n_heads if cost_quirk else 1)
-        com_cost = list(np.arange(1, iters + 1) * per)
+        com_cost = np.arange(1, iters + 1) * per
     elif comm.nranks == 1 and opts.get("persistent", "auto") in (True, "auto") and eng.dynamic_eligible() \
             and len(rechain_iterations(max_iter, schedule.coherence)) < 4096:
         # D-GADMM in ONE persistent launch: the seeded chain sequence is drawn up front (batched,
@@ -277,10 +277,10 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         csum = Cn.sum(axis=1) if Cn.dtype != object else np.asarray([float(np.sum(c)) for c in Cn])
         per_it = np.concatenate([[float(np.sum(saved[2]))], csum]) * (n_heads if cost_quirk else 1)
         which = np.searchsorted(starts, np.arange(1, iters + 1), side="right") - 1
-        com_cost = list(np.cumsum(per_it[which]))
+        com_cost = np.cumsum(per_it[which])
         # leave the schedule (and the engine's plan) where the epoch-by-epoch run would have left them
         schedule.skip(saved, Pn, Cn, int(np.sum(rechains <= iters)))
-        last = int(eng.ctl_state()["iter"]) - 1
+        last = int(r.iterations_launched)  # = ctl iter - 1: the run started at iteration 1
         eng.set_path([int(v) for v in P[int(np.searchsorted(starts, max(last, 1), side="right") - 1)]], placement,
                      rank)
     else:

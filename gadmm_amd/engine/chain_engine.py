@@ -451,10 +451,24 @@ class NativeChainEngine:
                 pp = np.empty((E * len(loc),), dtype=np.int32)
                 native.check(self.lib.gadmm_epoch_tables(P.ctypes.data, E, n, loc.ctypes.data, len(loc),
                                                          es.ctypes.data, pp.ctypes.data), "epoch_tables")
+            # the three epoch tables go up in ONE async copy from a reused pinned staging buffer (three
+            # pageable copies cost a blocking round trip each); the stream is synchronised after the
+            # kernel, so the staging buffer is free again by the next solve
+            ns, nes = len(starts), es.size
+            total = ns + nes + pp.size
+            stage = getattr(self, "_ep_stage", None)
+            if stage is None or stage[0].numel() < total:
+                cap = max(total, 4096)
+                stage = (torch.empty((cap,), dtype=torch.int32, pin_memory=True),
+                         torch.empty((cap,), dtype=torch.int32, device=dev))
+                self._ep_stage = stage
+            host = stage[0].numpy()
+            host[:ns] = starts
+            host[ns:ns + nes] = es
+            host[ns + nes:total] = pp
             with torch.cuda.stream(self.stream):
-                st_t = torch.tensor(starts, dtype=torch.int32, device=dev)
-                es_t = torch.from_numpy(np.ascontiguousarray(es)).to(dev)
-                pp_t = torch.from_numpy(np.ascontiguousarray(pp)).to(dev)
+                stage[1][:total].copy_(stage[0][:total], non_blocking=True)
+            st_t, es_t, pp_t = stage[1][:ns], stage[1][ns:ns + nes], stage[1][ns + nes:total]
             ep_keep = (st_t, es_t, pp_t)
             pa.n_epochs = len(starts)
             pa.epoch_start, pa.ep_slots, pa.ep_pos = st_t.data_ptr(), es_t.data_ptr(), pp_t.data_ptr()
@@ -498,8 +512,7 @@ class NativeChainEngine:
         return {"iter": c[0], "done": c[1], "conv_iter": c[2], "pending": c[3], "ticket": c[4], "monitored": c[5]}
 
     def objective_trace(self, upto: Optional[int] = None) -> np.ndarray:
-        t = self.trace.cpu().numpy()
-        return t if upto is None else t[:upto]
+        return (self.trace if upto is None else self.trace[:upto]).cpu().numpy()
 
     def local_theta(self) -> torch.Tensor:
         idx = torch.tensor(self.local_ids, dtype=torch.long, device=self.device)
