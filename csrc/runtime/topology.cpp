@@ -15,10 +15,15 @@
 namespace {
 
 // Epochs [e0, e1) of the batch: one geometry + greedy chain each (independent of the others).
+// Only the distances the greedy walk reads are formed: the row of the current node, restricted to
+// the still-unvisited nodes kept compacted in `left` (N^2/2 pairs instead of N^2). Each pair is
+// computed exactly as the full matrix would hold it, and candidates are scanned in ascending index
+// order, so the chain and costs are unchanged.
 void greedy_range(const double* uv, int e0, int e1, int n, double side, int energy, double eta, double bw, double f,
                   long long* paths, double* costs) {
-  std::vector<double> x(n), y(n), d2((size_t)n * n);
-  std::vector<char> visited(n);
+  std::vector<double> x(n), y(n);
+  std::vector<int> left(n);
+  std::vector<double> v(n);
   const double inf = std::numeric_limits<double>::infinity();
   for (int e = e0; e < e1; ++e) {
     const double* g = uv + (size_t)e * n * 2;
@@ -26,32 +31,37 @@ void greedy_range(const double* uv, int e0, int e1, int n, double side, int ener
       x[i] = g[2 * i] * side;
       y[i] = g[2 * i + 1] * side;
     }
-    for (int i = 0; i < n; ++i)
-      for (int j = 0; j < n; ++j) {
-        const double dx = x[i] - x[j], dy = y[i] - y[j];
-        const double a = dx * dx, b = dy * dy;
-        d2[(size_t)i * n + j] = i == j ? 0.0 : a + b;
-      }
     long long* p = paths + (size_t)e * n;
-    std::fill(visited.begin(), visited.end(), 0);
+    int nleft = 0;
+    for (int j = 1; j < n; ++j) left[nleft++] = j;  // ascending: lowest index wins ties
     int cur = 0;
     p[0] = 0;
-    visited[0] = 1;
     for (int k = 1; k < n; ++k) {
-      int best = -1;
+      // distances first (independent, vectorisable), then the minimum (exact in any order), then the
+      // first candidate holding it: the same choice as a sequential strict-< scan
+      const double xc = x[cur], yc = y[cur];
       double bv = inf;
-      const double* row = d2.data() + (size_t)cur * n;
-      for (int j = 0; j < n; ++j)
-        if (!visited[j] && row[j] < bv) {
-          bv = row[j];
-          best = j;
-        }
-      if (best < 0)  // every candidate at +inf / NaN: numpy argmin takes the first unvisited
-        for (int j = 0; j < n && best < 0; ++j)
-          if (!visited[j]) best = j;
+      for (int q = 0; q < nleft; ++q) {
+        const int j = left[q];
+        const double dx = xc - x[j], dy = yc - y[j];
+        const double a = dx * dx, b = dy * dy;
+        v[q] = a + b;
+      }
+      double m4[4] = {inf, inf, inf, inf};  // four independent running minima (short dependent chain)
+      int q = 0;
+      for (; q + 4 <= nleft; q += 4)
+        for (int u = 0; u < 4; ++u) m4[u] = v[q + u] < m4[u] ? v[q + u] : m4[u];
+      for (; q < nleft; ++q) m4[0] = v[q] < m4[0] ? v[q] : m4[0];
+      for (int u = 0; u < 4; ++u) bv = m4[u] < bv ? m4[u] : bv;
+      int bi = 0;
+      if (bv < inf)
+        while (v[bi] != bv) ++bi;
+      // every candidate at +inf / NaN: numpy argmin takes the first unvisited (bi = 0 above)
+      const int best = left[bi];
+      double c = v[bi];
+      for (int q = bi + 1; q < nleft; ++q) left[q - 1] = left[q];  // keep ascending order
+      --nleft;
       p[k] = best;
-      visited[best] = 1;
-      double c = d2[(size_t)cur * n + best];
       if (energy) {
         c = c * eta;
         c = c * bw;
@@ -65,14 +75,13 @@ void greedy_range(const double* uv, int e0, int e1, int n, double side, int ener
 
 }  // namespace
 
-// The epochs are independent: large batches are split over up to 8 host threads (the ~300-epoch
-// batch of a one-launch D-GADMM solve took ~0.5-1 ms on one core, a third of the solve).
+// The epochs are independent: large batches are split over up to 8 host threads.
 extern "C" int gadmm_greedy_chains(const double* uv, int E, int n, double side, int energy, double eta, double bw,
                                    double f, long long* paths, double* costs) {
   if (E < 0 || n < 1 || !uv || !paths || (n > 1 && !costs)) return -1;
   const long work = (long)E * n * n;
   int nt = 1;
-  if (work > 40000) {
+  if (work > 400000) {  // below this one core beats spawning threads (~300 epochs x 24 nodes: ~40 us)
     const unsigned hw = std::thread::hardware_concurrency();
     nt = (int)std::min<long>(std::min<unsigned>(hw ? hw : 1, 8u), std::max<long>(1, work / 40000));
     if (nt > E) nt = E;
