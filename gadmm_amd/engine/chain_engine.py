@@ -238,11 +238,20 @@ class NativeChainEngine:
     # ---------------------------------------------------------------------------------------------
     def set_path(self, path: Sequence[int], placement: Placement, rank: int):
         """Install the chain ``path`` (position -> global worker id) for this rank."""
-        plan = chain_plan(path, placement, rank)
-        lidx = {w: i for i, w in enumerate(self.local_ids)}
-        for s in plan.head + plan.tail:
-            if self.local_ids[s.li] != s.gid or lidx[s.gid] != s.li:
-                raise ValueError("placement/local_ids mismatch")
+        # validated plans are memoised per (chain, rank, placement): a D-GADMM solve installs the same
+        # initial and final chains on every repeat, and building a plan in Python costs ~50 us
+        key = (tuple(int(w) for w in path), int(rank), tuple(int(o) for o in placement.owner))
+        memo = self.__dict__.setdefault("_plan_memo", {})
+        plan = memo.get(key)
+        if plan is None:
+            plan = chain_plan(path, placement, rank)
+            lidx = {w: i for i, w in enumerate(self.local_ids)}
+            for s in plan.head + plan.tail:
+                if self.local_ids[s.li] != s.gid or lidx[s.gid] != s.li:
+                    raise ValueError("placement/local_ids mismatch")
+            if len(memo) > 4096:
+                memo.clear()
+            memo[key] = plan
         self._install(plan)
         self.plan = plan
         self.path = [int(w) for w in path]
@@ -424,12 +433,12 @@ class NativeChainEngine:
         ep_keep = None
         if epochs is not None:
             if isinstance(epochs, tuple) and len(epochs) == 2 and isinstance(epochs[1], np.ndarray):
-                starts = [int(v) for v in epochs[0]]                                # (starts, paths) arrays
+                starts = np.asarray(epochs[0], dtype=np.int64)                      # (starts, paths) arrays
                 P = np.asarray(epochs[1], dtype=np.int64)
             else:
-                starts = [int(e[0]) for e in epochs]
+                starts = np.asarray([int(e[0]) for e in epochs], dtype=np.int64)
                 P = np.asarray([list(e[1]) for e in epochs], dtype=np.int64)       # (E, n) position -> worker
-            if starts[0] != int(start_iter) or any(b <= a for a, b in zip(starts, starts[1:])):
+            if starts[0] != int(start_iter) or np.any(starts[1:] <= starts[:-1]):
                 raise ValueError("epochs must start at start_iter and be increasing")
             E, n = P.shape
             loc = np.asarray([int(w) for w in self.local_ids], dtype=np.int64)
