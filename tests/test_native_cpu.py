@@ -75,6 +75,19 @@ def test_native_greedy_chains_match_numpy(monkeypatch):
             s5 = T.PathSchedule(n, list(range(n)), np.zeros(n - 1), 10, kind=kind, seed=11)
             s5.prefetch(7)
             assert s4.path == s5.path and np.array_equal(s4.rng.random(4), s5.rng.random(4))
+    # a batch large enough for the multi-threaded split (E * n^2 > 400k), with tied distances
+    uv = np.random.default_rng(2).random((240, 50, 2))
+    uv[:, 7] = uv[:, 3]  # nodes 3 and 7 coincide: the lower index must win every tie
+    Pn, Cn = T.native_greedy_chains(uv, 10.0, False)
+    xy = uv * 10.0
+    dx = xy[:, :, None, 0] - xy[:, None, :, 0]
+    dy = xy[:, :, None, 1] - xy[:, None, :, 1]
+    d2 = dx * dx + dy * dy
+    d2[:, np.arange(50), np.arange(50)] = 0.0
+    P = T.greedy_chains(d2)
+    assert np.array_equal(Pn, P)
+    ar = np.arange(240)[:, None]
+    assert np.array_equal(Cn, d2[ar, P[:, :-1], P[:, 1:]])
 
 
 def test_native_epoch_tables_match_numpy():
