@@ -218,7 +218,10 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     rank = comm.rank
     rcomm = comm if comm.nranks > 1 else None
     kind = "linear" if local_solver == "closed" else "logistic"
-    block = int(opts.get("block", 16 if comm.nranks > 1 else 32))
+    # iterations per replayed graph: a logistic phase is ~37 us, so the replays left over after the stop
+    # decision cost more than the extra host round trips of short blocks (tools/logistic_block_sweep.py:
+    # 6.78 / 6.81 / 6.88 / 7.11 ms for 8 / 16 / 32 / 64)
+    block = int(opts.get("block", 16 if comm.nranks > 1 else (8 if kind == "logistic" else 32)))
     pre = (model.A, model.b, model.yy) if kind == "linear" else None
     # one engine per (model, configuration) on a single rank: repeated solves (rho sweeps, benchmarks,
     # D-GADMM re-runs) reuse its device buffers, cached inverses and captured graph
