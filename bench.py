@@ -1,25 +1,38 @@
 """Headline benchmark: wall-clock and communication bytes to a 1e-8 objective gap (BASELINE.json).
 
 Config (BASELINE.json configs[1], BASELINE.md "GADMM lin-syn iterations to 1e-8"): the
-LinearRegression_Synthetic problem of the reference — N = 24 logical workers, d = 50 features,
-m = 50 samples per worker, X_n = 1.3^(n-1) q_n q_n^T + I (rebuilt from the reference's shipped
-inputData.mat), closed-form local solves, GADMM with rho = 3, stop at |obj - obj0| < 1e-8.
-The 24 workers form one chain laid over the N GPUs in contiguous segments (24/N workers per GPU);
-boundary theta crosses GPUs by RCCL send/recv over xGMI. Total work is fixed as N grows
-(strong scaling).
+LinearRegression_Synthetic problem of the reference -- N = 24 logical workers (``--workers``), d = 50
+features, m = 50 samples per worker, X_n = 1.3^(n-1) q_n q_n^T + I (rebuilt from the reference's
+shipped inputData.mat), closed-form local solves, GADMM with rho = 3, stop at |obj - obj0| < 1e-8.
+``--workers 8`` is configs[1] literally: 8 workers, so on 8 GPUs each MI355X is one worker.
+
+The workers form one chain laid over the GPUs in contiguous segments. **Data-local by default**: a
+rank builds and holds only its own workers' shards (``benchmarks.headline_rank_problem``) and ships
+only theta, to the two chain neighbours (group_ADMM_closedForm.m:18-27, 62-70):
+* 1 GPU: the temporally blocked persistent kernel (one launch per solve);
+* N GPUs (``--fabric auto``/``xgmi``): the per-worker persistent kernel, boundary theta pushed into
+  the neighbour GPU's table over xGMI (device-initiated, IPC-mapped fine-grained memory);
+* fallbacks, taken by every rank together: the graph-replayed phase kernels with RCCL send/recv
+  (``--fabric rccl``), or with the device-copy transport (``--fabric ipc``; also the fallback when
+  ranks share one GPU, where RCCL cannot run).
+``--engine replicated-halo`` is the opt-in temporally blocked kernel across GPUs: each rank ALSO holds
+the shards of a 4-position halo of other ranks' workers and exchanges (theta, mu) once per 2
+iterations; its replicated shard bytes are reported.
 
 One *step* = one complete solve from the raw shards already resident on the GPU: Gram + b + y^T y
-(f64 MFMA), cached inverses (A + c rho I)^{-1}, then GADMM iterations from theta = mu = 0 until the
-device-side stopping rule fires (1373 iterations at rho = 3, checked against the reference count).
-`value` is seconds per solve (lower is better); `vs_baseline` = value / 1.13 s, the CPU wall time
+(f64 MFMA), cached inverses, then GADMM iterations from theta = mu = 0 until the device-side stop
+rule fires. Every timed step must converge in the reference's iteration count (1373 at rho = 3,
+N = 24). Bytes per solve are reported three ways, summed over ranks: theta payload (8 B per double),
+wire (the xGMI / IPC granules carry 16 B per double) and stop-rule monitor traffic.
+``value`` is seconds per solve (lower is better); ``vs_baseline`` = value / 1.13 s, the CPU wall time
 of the same loop ([measured-here] row).
 
     python bench.py                      # 1 GPU
-    torchrun --nproc-per-node 8 bench.py --gpus 8
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
 
 The other BASELINE.json configs (same JSON contract, own metric): ``--config logistic`` (configs[2]),
-``--config dgadmm`` (configs[3]), ``--config real10m`` (configs[4]: 1.25M x 10k f64 per GPU);
-see gadmm_amd/benchmarks.py.
+``--config dgadmm`` (configs[3]), ``--config real10m`` (configs[4]: 1.25M x 10k f64 per GPU), ``--config
+star`` (the star-ADMM comparator of E7); see gadmm_amd/benchmarks.py.
 """
 from __future__ import annotations
 
@@ -35,7 +48,10 @@ import torch.distributed as dist
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 BASELINE_S = 1.13  # CPU wall time of the GADMM loop to 1e-8, rho = 3
-EXPECTED_ITERS = {3.0: 1373, 5.0: 758, 7.0: 428}
+
+
+class BenchFailure(RuntimeError):
+    pass
 
 
 def main():
@@ -48,13 +64,15 @@ def main():
     ap.add_argument("--workers", type=int, default=24)
     ap.add_argument("--block", type=int, default=0, help="iterations per graph replay (0: auto)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--engine", choices=["auto", "persistent", "graph"], default="auto",
-                    help="auto: persistent single-launch kernel when eligible, else graph-replayed phases")
-    ap.add_argument("--fabric", choices=["auto", "xgmi", "rccl"], default="auto",
-                    help="multi-GPU transport: xgmi = device-initiated granule pushes between persistent kernels "
-                         "(IPC fine-grained buffers), rccl = RCCL send/recv between graph-replayed phases")
-    ap.add_argument("--config", choices=["e1", "logistic", "logistic_exact", "dgadmm", "real10m"], default="e1",
-                    help="e1 = the headline (default); the others are BASELINE.json configs[2..4]")
+    ap.add_argument("--engine", choices=["auto", "persistent", "graph", "replicated-halo"], default="auto",
+                    help="auto: persistent single-launch kernel when eligible, else graph-replayed phases; "
+                         "replicated-halo: opt-in blocked kernel across GPUs (ranks hold halo shards)")
+    ap.add_argument("--fabric", choices=["auto", "xgmi", "rccl", "ipc"], default="auto",
+                    help="multi-GPU transport: xgmi = device-initiated theta pushes between persistent kernels, "
+                         "rccl = RCCL send/recv between graph-replayed phases, ipc = the device-copy transport "
+                         "between graph-replayed phases")
+    ap.add_argument("--config", choices=["e1", "logistic", "logistic_exact", "dgadmm", "real10m", "star"],
+                    default="e1", help="e1 = the headline (default); the others are BASELINE.json configs[2..4]")
     ap.add_argument("--rows", type=int, default=1_250_000, help="real10m: rows per GPU")
     ap.add_argument("--dim", type=int, default=10_000, help="real10m: features")
     args = ap.parse_args()
@@ -62,167 +80,82 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print("bench.py: --gpus %d needs a torchrun launch with %d processes" % (args.gpus, args.gpus),
-                  file=sys.stderr)
-            sys.exit(2)
+    if world != args.gpus and world == 1 and args.gpus > 1:
+        print("bench.py: --gpus %d needs a torchrun launch with %d processes" % (args.gpus, args.gpus),
+              file=sys.stderr)
+        sys.exit(2)
     # GADMM_BENCH_SHARE_GPU=1: rehearsal of the multi-rank path with every rank on cuda:0 (one-GPU
-    # development box); RCCL refuses two ranks on one device, so only the xgmi fabric runs there.
+    # development box). RCCL refuses two ranks on one device, so there the fallback is the IPC transport.
     share = os.environ.get("GADMM_BENCH_SHARE_GPU") == "1"
     dev_index = 0 if share else local_rank
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
-
-    from gadmm_amd.data import linear_synthetic
-    from gadmm_amd.oracle.reference import opt_linear
-    from gadmm_amd.engine.chain_engine import NativeChainEngine
-    from gadmm_amd.parallel.topology import Placement, chain_message_count
-
-    comm = None
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
-        from gadmm_amd.parallel.comm import RcclComm, RankInfo
-        comm = RankInfo(rank, world) if share else RcclComm(device)
-
-    if args.config != "e1":
-        return run_other(args, rank, world, device, comm)
-
-    def all_ok(flag: bool) -> bool:
-        if world == 1:
-            return flag
-        t = torch.tensor([0.0 if flag else 1.0], dtype=torch.float64)
-        dist.all_reduce(t)
-        return float(t.item()) == 0.0
-
-    ds = linear_synthetic(args.workers)
-    Xf, yf = ds.stacked()
-    obj0 = opt_linear(Xf.numpy(), yf.numpy())
-    placement = Placement.contiguous(args.workers, world)
-    local = placement.local_workers(rank)
-    X_loc = ds.X[local].to(device).contiguous()
-    y_loc = ds.y[local].to(device).contiguous()
-    block = args.block if args.block > 0 else (32 if world == 1 else 16)
-    max_iter = 20000
-    eng = NativeChainEngine(X_loc, y_loc, local, args.workers, "linear", rho=args.rho, obj0=obj0, tol=args.tol,
-                            max_iter=max_iter, comm=comm, block=block)
-    path = list(range(args.workers))
-    eng.set_path(path, placement, rank)
-
-    def barrier():
-        torch.cuda.synchronize(device)
-        if world > 1:
-            dist.barrier()
-
-    fabric = None
-    fabric_kind = "local" if world == 1 else "rccl"
-    blk = None  # temporally blocked kernel across GPUs (one xGMI exchange per k iterations)
-    if world > 1 and args.fabric in ("auto", "xgmi") and args.engine != "graph" and ds.dim <= 52 \
-            and os.environ.get("GADMM_BLOCKED", "1") != "0":
-        ok, err = False, ""
-        try:
-            from gadmm_amd.engine.blocked_xgmi import BlockedXgmiEngine
-            blk = BlockedXgmiEngine(ds.X, ds.y, args.workers, placement, rank, args.rho, obj0, args.tol, max_iter,
-                                    device)
-            ok = True
-        except Exception as e:
-            err = str(e)
-        if not all_ok(ok):
-            if rank == 0:
-                print("bench.py: blocked xgmi engine unavailable (%s)" % (err or "remote"), file=sys.stderr)
-            if blk is not None:
-                blk.close()
-            blk = None
+    try:
+        if args.config != "e1":
+            run_other(args, rank, world, device, share)
         else:
-            fabric_kind = "xgmi"
-    if world > 1 and blk is None and args.fabric in ("auto", "xgmi") and args.engine != "graph":
-        ok = False
-        err = ""
-        try:
-            from gadmm_amd.parallel.xgmi import XgmiFabric
-            need = sorted({int(placement.owner[u]) for w in local for u in (w - 1, w + 1)
-                           if 0 <= u < args.workers} - {rank})
-            fabric = XgmiFabric(args.workers, ds.dim, 8, rank, world, device, peers_needed=need)
-            ok = eng.persistent_eligible(fabric)
-        except Exception as e:  # fall back to RCCL on every rank together
-            err = str(e)
-        if not all_ok(ok):
-            if rank == 0:
-                print("bench.py: xgmi fabric unavailable (%s); using RCCL" % (err or "not eligible"), file=sys.stderr)
-            if fabric is not None:
-                fabric.close()
-            fabric = None
-        else:
-            fabric_kind = "xgmi"
-    persistent = (args.engine in ("auto", "persistent")) and (
-        eng.persistent_eligible() if world == 1 else (fabric is not None or blk is not None))
+            run_headline(args, rank, world, device, share)
+    except BenchFailure as e:
+        print("bench.py[rank %d]: FAILED: %s" % (rank, e), file=sys.stderr, flush=True)
+        sys.exit(3)
+    if world > 1:
+        dist.destroy_process_group()
 
-    from collections import namedtuple
-    BlkRun = namedtuple("BlkRun", "iters done wall_ms p2p_bytes monitor_bytes")
 
-    def solve():
-        if blk is not None and persistent:
-            blk.refresh()
-            it_, done_, ms_ = blk.run()
-            return BlkRun(it_, done_, ms_, blk.exchange_bytes_per_solve(it_), 0)
-        eng.refresh(X_loc, y_loc)
-        eng.reset()
-        if persistent:
-            return eng.run_persistent(fabric=fabric)
-        return eng.run(use_graph=not args.no_graph)
+def run_headline(args, rank, world, device, share):
+    from gadmm_amd.benchmarks import headline_rank_problem, EXPECTED_ITERS_1E8
+    from gadmm_amd.engine.multigpu import DistributedChainSolver, all_ok
+    from gadmm_amd.parallel.topology import chain_message_count
 
-    runs = []
+    X_cpu, y_cpu, local, placement, obj0 = headline_rank_problem(args.workers, rank, world)
+    d, m = int(X_cpu.shape[2]), int(X_cpu.shape[1])
+    halo = None
+    if args.engine == "replicated-halo" and world > 1:
+        from gadmm_amd.data import linear_synthetic
+        ds_all = linear_synthetic(args.workers)  # opt-in: the halo engine needs other ranks' shards
+        halo = (ds_all.X, ds_all.y)
+    sol = DistributedChainSolver(X_cpu.to(device).contiguous(), y_cpu.to(device).contiguous(), local, args.workers,
+                                 placement, rank, world, device, args.rho, obj0, args.tol, engine=args.engine,
+                                 fabric=args.fabric, share=share, block=args.block, halo_data=halo,
+                                 use_graph=not args.no_graph)
+    expect = EXPECTED_ITERS_1E8.get((args.workers, float(args.rho))) if args.tol == 1e-8 else None
     for _ in range(args.warmup):
-        try:
-            r = solve()
-            good = r.done == 1
-        except RuntimeError as e:
-            good = False
-            print("bench.py[rank %d]: %s" % (rank, e), file=sys.stderr)
-        if persistent and world > 1 and not all_ok(good):
-            # a stalled device-initiated hand-off (done == 4) on any rank: every rank drops to the
-            # per-worker xgmi kernel (if the blocked one failed) or to RCCL
-            if blk is not None:
-                blk.close()
-                blk = None
-                persistent = fabric is not None
-                fabric_kind = "xgmi(per-worker fallback)" if persistent else "rccl(fallback)"
-            else:
-                persistent, fabric_kind = False, "rccl(fallback)"
-            if rank == 0:
-                print("bench.py: xgmi solve failed; falling back (%s)" % fabric_kind, file=sys.stderr)
-        runs.append(None)
-    barrier()
+        if sol.solve_agreed().done != 1:  # collective: a failure anywhere moves every rank to the graph engine
+            raise BenchFailure("a warm-up solve did not converge (fabric %s, fallbacks %s)" % (sol.kind, sol.fallbacks))
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    results = []
     t0 = time.perf_counter()
-    last = None
     for _ in range(args.steps):
-        last = solve()
+        results.append(sol.guarded_solve())
     torch.cuda.synchronize(device)
     t1 = time.perf_counter()
-    barrier()
-    ms = (t1 - t0) * 1e3 / max(args.steps, 1)
-    iters = last.iters if last is not None else 0
-    p2p = last.p2p_bytes if last is not None else 0
-    mon = last.monitor_bytes if last is not None else 0
-    if persistent and world > 1 and blk is not None:
-        mon = 0
-    elif persistent and world > 1:
-        # device-initiated pushes: one d-vector per cross-GPU neighbour relation per phase
-        p2p = chain_message_count(path, placement) * ds.dim * 8 * iters // world  # per-rank share, summed below
-        n_remote = sum(1 for w in range(args.workers) if int(placement.owner[w]) != 0)
-        mon = (n_remote * 8 + world * 8) * iters // world
     if world > 1:
-        t = torch.tensor([ms, float(p2p), float(mon)], dtype=torch.float64)
+        dist.barrier()
+    # every timed solve must have converged in the same (reference) iteration count
+    its = {r.iters for r in results}
+    good = all(r.done == 1 for r in results) and len(its) == 1 and (expect is None or its == {expect})
+    if not all_ok(good, world):
+        raise BenchFailure("timed solves: done=%s iterations=%s (expected %s)"
+                           % (sorted({r.done for r in results}), sorted(its), expect))
+    ms = (t1 - t0) * 1e3 / max(args.steps, 1)
+    last = results[-1]
+    iters, p2p, wire, mon, repl = last.iters, last.theta_bytes, last.wire_bytes, last.monitor_bytes, sol.replicated_bytes
+    if world > 1:
+        t = torch.tensor([ms, float(p2p), float(wire), float(mon), float(repl)], dtype=torch.float64)
         mx = t.clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         sm = t.clone()
         dist.all_reduce(sm, op=dist.ReduceOp.SUM)
         ms = float(mx[0])
-        p2p, mon = int(sm[1]), int(sm[2])
-    tr = blk.objective_trace(iters) if (blk is not None and persistent) else eng.objective_trace(iters)
+        p2p, wire, mon, repl = int(sm[1]), int(sm[2]), int(sm[3]), int(sm[4])
+    tr = sol.objective_trace(iters)
     gap = abs(float(tr[iters - 1]) - obj0) if iters > 0 else float("nan")
-    expect = EXPECTED_ITERS.get(float(args.rho)) if args.workers == 24 and args.tol == 1e-8 else None
+    data_local = sol.blk is None
     if rank == 0:
         value = ms / 1e3
         out = {
@@ -239,38 +172,46 @@ def main():
             "dtype": "fp64",
             "data": "synthetic (reference LinearRegression_Synthetic design rebuilt from shipped inputData.mat)",
             "config": {"model": "LinearRegression_Synthetic GADMM closed-form", "workers": args.workers,
-                       "features": ds.dim, "samples_per_worker": ds.rows_per_worker, "rho": args.rho,
-                       "tol": args.tol, "global_batch": args.workers * ds.rows_per_worker, "seq_len": 1,
+                       "features": d, "samples_per_worker": m, "rho": args.rho,
+                       "tol": args.tol, "global_batch": args.workers * m, "seq_len": 1,
                        "parallelism": "chain%d-over-%dgpu" % (args.workers, world)},
             "iterations_to_tol": iters,
             "expected_iterations": expect,
             "iterations_match_reference": (iters == expect) if expect else None,
             "final_gap": gap,
+            "data_local": data_local,
+            # theta over the fabric per solve, all ranks, iterations 1..iters: a data-local chain sends
+            # 2 messages of d doubles per rank boundary per iteration (group_ADMM_closedForm.m:18-27, 62-70)
             "comm_bytes_per_solve": p2p,
+            "theta_payload_bytes_per_solve": p2p,
+            "theta_payload_bytes_formula": 2 * (world - 1) * d * 8 * iters if data_local else None,
+            "wire_bytes_per_solve": wire,
             "monitor_bytes_per_solve": mon,
-            "p2p_messages_per_iteration": chain_message_count(path, placement),
+            "replicated_shard_bytes": repl,
+            "p2p_messages_per_iteration": chain_message_count(list(range(args.workers)), placement),
             "us_per_iteration": round(ms * 1e3 / max(iters, 1), 3),
-            "engine": "persistent" if persistent else ("graph" if eng.graph_ok() and not args.no_graph else "eager"),
-            "kernel": (blk.last_kernel if blk is not None else getattr(eng, "last_kernel", None)) if persistent else None,
-            "fabric": fabric_kind,
+            "engine": sol.engine_name(),
+            "kernel": sol.kernel,
+            "fabric": sol.kind,
+            "fallbacks": sol.fallbacks,
             "baseline_s": BASELINE_S,
         }
         print(json.dumps(out), flush=True)
-    eng.close()
-    if blk is not None:
-        blk.close()
-    if fabric is not None:
-        fabric.close()
-    if comm is not None:
-        comm.close()
-    if world > 1:
-        dist.destroy_process_group()
+    sol.close()
 
 
-def run_other(args, rank, world, device, comm):
+def run_other(args, rank, world, device, share):
     from gadmm_amd.benchmarks import CONFIGS
 
-    if comm is None:
+    comm = None
+    args.share = share
+    if world > 1:
+        if share:
+            comm = None  # RCCL cannot run with ranks on one GPU: the bodies build an IPC transport
+        else:
+            from gadmm_amd.parallel.comm import RcclComm
+            comm = RcclComm(device)
+    else:
         from gadmm_amd.parallel.comm import LocalComm
         comm = LocalComm()
     r = CONFIGS[args.config](args, rank, world, device, comm)
@@ -283,14 +224,12 @@ def run_other(args, rank, world, device, comm):
                "iterations_to_tol": r["iters"], "expected_iterations": r["expected"],
                "iterations_match_reference": (r["iters"] == r["expected"]) if r["expected"] else None,
                "backend": r.get("backend")}
-        for k in ("setup_s", "gram_tflops", "star_admm_s", "star_admm_iters"):
-            if k in r:
-                out[k] = r[k]
+        for k, v in r.items():
+            if k not in out and k not in ("ms", "iters", "expected", "metric", "config"):
+                out[k] = v
         print(json.dumps(out), flush=True)
-    if hasattr(comm, "close"):
+    if comm is not None and hasattr(comm, "close"):
         comm.close()
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -33,9 +33,10 @@ __device__ __forceinline__ bool phase_arrive(ChainCtl* ctl, int n_slots, int* fl
 __device__ __forceinline__ void finish_iteration(const PhaseArgs& a, int it) {
   if (threadIdx.x != 0) return;
   ChainCtl* ctl = a.ctl;
-  double s = 0.0;
-  for (int i = 0; i < a.n_local; ++i) s += a.objw[i];  // fixed order: deterministic
+  if (a.tstamp && it - 1 < a.max_iter) a.tstamp[it - 1] = (long long)__builtin_amdgcn_s_memrealtime();
   if (a.flags & PH_LOCAL_STOP) {
+    double s = 0.0;
+    for (int i = 0; i < a.n_local; ++i) s += a.objw[i];  // fixed order (local order == worker order)
     if (it - 1 < a.max_iter) a.trace[it - 1] = s;
     const double gap = fabs(s - a.obj0);
     if (!(s == s) || isinf(s)) {
@@ -50,7 +51,8 @@ __device__ __forceinline__ void finish_iteration(const PhaseArgs& a, int it) {
     }
     ctl->monitored = it;
   } else {
-    a.part[(it - 1) % a.ring] = s;
+    double* row = a.part + (long)((it - 1) % a.ring) * a.n_total;
+    for (int i = 0; i < a.n_local; ++i) row[a.lgid[i]] = a.objw[i];
   }
   ctl->pending = 1;
   ctl->ticket = 0u;

@@ -60,7 +60,7 @@ struct PhaseArgs {
   double* objw;        // [n_local]
   ChainCtl* ctl;
   double* trace;       // [max_iter]
-  double* part;        // [ring]
+  double* part;        // [ring][n_total] per-worker objectives (multi-rank; gid-indexed, others stay 0)
   int ring, max_iter;
   double obj0, tol;
   // logistic
@@ -73,16 +73,24 @@ struct PhaseArgs {
   double* rbuf;        // [n_local][d] right-hand sides of the current phase
   int obj_mode;        // 0: exact (second GEMV with A), 1: A th = r - deg rho th (no second matrix pass)
   int solver;          // logistic local solve: 0 inexact inner GD (logReg_GD.m), 1 exact Newton (chain_newton.hip)
+  // multi-rank stop rule: every rank files its workers' f_n into part[slot][gid]; the monitor sums
+  // all n_total entries in worker order, the order of the single-rank finish, so the objective trace
+  // is bit-identical for any rank count
+  int n_total, pad_nt;
+  const int* lgid;     // [n_local] global worker id of each local row
+  long long* tstamp;   // optional [max_iter] s_memrealtime (100 MHz) when each iteration was decided
 };
 
 // Engine construction arguments (Python mirrors it in gadmm_amd/ops/native.py).
 struct EngineDesc {
   PhaseArgs base;          // pointers, model params; slots / n_slots / flags filled per phase
   PhaseSlot* d_slots;      // device buffer, capacity >= 2 * n_local (head plan then tail plan)
-  double* reduced;         // device [ring] (multi-rank)
+  double* reduced;         // device [ring][n_total] (multi-rank)
   void* comm;              // RcclComm* or null (single rank)
   hipStream_t stream;
   int nranks;
+  void* xport;             // IpcXport* (device-copy transport, csrc/kernels/ipc_xport.hip) or null: when set
+                           // it replaces RCCL for the row exchange and the stop-rule reduction
 };
 
 struct RunStats {
@@ -93,7 +101,9 @@ struct RunStats {
   double wall_ms;
   long long p2p_bytes;     // bytes this rank sent over the chain, iterations 1..iters
   long long p2p_msgs;
-  long long monitor_bytes; // all-reduce payload of the stopping monitor
+  long long monitor_bytes; // stop-rule traffic leaving this rank (see gadmm_chain_engine_run)
+  long long wire_bytes;    // p2p bytes on the wire: 16-B granules per double with the IPC transport,
+                           // = p2p_bytes with RCCL (its protocol framing is not visible here)
 };
 
 
@@ -140,4 +150,11 @@ struct PersistArgs {
   int blk_npeer, dbg;       // dbg: experiment bits (0 in production; see chain_blocked.hip)
   int blk_peer_lo[8], blk_peer_hi[8];
   u32x4* const* blk_peer_tab;  // [blk_npeer] peers' exchange tables (IPC-mapped)
+  // real clock: the monitor stamps s_memrealtime (100 MHz) when it decides each iteration
+  long long* tstamp;        // optional [max_iter]
+  // D-GADMM across GPUs (per-worker kernel): theta^j of local worker b goes to every rank in
+  // ep_push[epoch(j)][b], plus ep_push[epoch(j)+1][b] when j + 1 starts the next epoch (its new
+  // neighbours read theta^j as their previous-iteration value); peer_thg[r] is rank r's table
+  const unsigned* ep_push;  // [n_epochs][n_local] rank bitmask (own rank excluded)
+  u32x4* const* peer_thg;   // [nranks]
 };

@@ -74,6 +74,7 @@ __device__ __forceinline__ void blocked_monitor(const PersistArgs& a, double* ld
         if (!(s == s) || isinf(s)) code = 3;
         else if (fabs(s - a.obj0) < a.tol) code = 1;
         else if (it >= a.max_iter) code = 2;
+        if (a.tstamp && it - 1 < a.max_iter) a.tstamp[it - 1] = (long long)now_ticks();
       }
       const unsigned long long dv = ((unsigned long long)tag << 32) | code;
       for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
@@ -796,6 +797,8 @@ long gadmm_chain_blocked_lds(int d, int len) {
 long gadmm_chain_blocked_tab_granules(int n, int d, int ring) { return 2L * n * 2 * d + (long)ring * n * d; }
 long gadmm_chain_blocked_tab_granules_dyn(int n, int d, int ring) { return 4L * n * 2 * d + (long)ring * n * d; }
 
+long gadmm_resident_capacity(const void* fn, int threads, size_t shm);  // chain_persistent.hip
+
 int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   const PersistArgs& a = *args;
   const bool multi = a.nranks > 1;
@@ -820,16 +823,17 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
     }
     const int Wo2 = (nseg + PWW - 1) / PWW;
     const int blocks2 = W + Wo2 + (a.has_monitor ? 1 : 0);
-    if (blocks2 > 256) {
-      gadmm_set_error("blocked chain kernel: %d workgroups exceed one per CU", blocks2);
-      return -1;
-    }
     long lds2 = (long)(2 * PCAP * 64 + PWW * QSTAGE) * 8;
     if (lds2 < (long)a.n * 8) lds2 = (long)a.n * 8;
     const void* fn2 = a.sys_scope ? (a.d <= 32 ? (const void*)chain_blocked_pair_kernel<32, true>
                                                : (const void*)chain_blocked_pair_kernel<52, true>)
                                   : (a.d <= 32 ? (const void*)chain_blocked_pair_kernel<32, false>
                                                : (const void*)chain_blocked_pair_kernel<52, false>);
+    const long cap2 = gadmm_resident_capacity(fn2, 64 * PWW, (size_t)lds2);
+    if (blocks2 > cap2) {  // every workgroup must be resident together (they spin on each other)
+      gadmm_set_error("blocked chain kernel: %d workgroups but only %ld can be resident", blocks2, cap2);
+      return -2;
+    }
     if (lds2 > 65536) GADMM_CHECK(hipFuncSetAttribute(fn2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
     void* kargs2[] = {const_cast<PersistArgs*>(&a)};
     GADMM_CHECK(hipLaunchKernel(fn2, dim3(blocks2), dim3(64 * PWW), kargs2, (size_t)lds2, st));
@@ -838,10 +842,6 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   }
   const int Wo = (nseg + MAXW - 1) / MAXW;
   const int blocks = W + Wo + (a.has_monitor ? 1 : 0);
-  if (blocks > 256) {
-    gadmm_set_error("blocked chain kernel: %d workgroups exceed one per CU", blocks);
-    return -1;
-  }
   long lds = gadmm_chain_blocked_lds(a.d, a.blk_len);
   if (lds < (long)a.n * 8) lds = (long)a.n * 8;
   if (lds > 160 * 1024) {
@@ -863,6 +863,11 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   } else {
     if (tl) fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, false, true> : (const void*)chain_blocked_kernel<52, false, true>;
     else fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, false, false> : (const void*)chain_blocked_kernel<52, false, false>;
+  }
+  const long cap = gadmm_resident_capacity(fn, 64 * MAXW, (size_t)lds);
+  if (blocks > cap) {  // every workgroup must be resident together (they spin on each other)
+    gadmm_set_error("blocked chain kernel: %d workgroups but only %ld can be resident", blocks, cap);
+    return -2;
   }
   if (lds > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   PersistArgs ka = a;

@@ -102,6 +102,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
           if (!(s == s) || isinf(s)) code = 3;
           else if (fabs(s - a.obj0) < a.tol) code = 1;
           else if (it >= a.max_iter) code = 2;
+          if (a.tstamp && it - 1 < a.max_iter) a.tstamp[it - 1] = (long long)now_ticks();
         }
         const unsigned long long dv = ((unsigned long long)tag << 32) | code;
         for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
@@ -320,6 +321,22 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
           if (p1) store_granule<SYS>(rp1, (w * d + i) * 16, tag, tn[c]);
         }
       }
+      if (SYS && dyn && a.ep_push) {
+        // D-GADMM across GPUs: to the ranks of this epoch's neighbours, and of the next epoch's when
+        // it starts at it + 1 (a new neighbour's head reads theta^it as its previous iterate)
+        unsigned mask = a.ep_push[(long)ep * a.n_local + blockIdx.x];
+        if (it + 1 == next_start) mask |= a.ep_push[(long)(ep + 1) * a.n_local + blockIdx.x];
+        while (mask) {
+          const int r = __builtin_ctz(mask);
+          mask &= mask - 1u;
+          const __amdgpu_buffer_rsrc_t rr = rsrc_of(a.peer_thg[r]);
+#pragma unroll
+          for (int c = 0; c < NC; ++c) {
+            const int i = lane + 64 * c;
+            if (i < d) store_granule<SYS>(rr, (trow(w, it) * d + i) * 16, tag, tn[c]);
+          }
+        }
+      }
       if (TL) t_pub = (long long)now_ticks();
       if (!head) {  // tails: both neighbours are this iteration's heads -> dual update now
 #pragma unroll
@@ -425,23 +442,114 @@ long gadmm_chain_persistent_lds(int d, int obj_mode) {
   return bytes;
 }
 
+}  // extern "C"
+
+// The kernel variant the launcher runs for these arguments, its block size and dynamic LDS bytes.
+struct PVariant {
+  const void* fn = nullptr;
+  int threads = 0;
+  size_t shm = 0;
+};
+
+static PVariant pick_variant(const PersistArgs& a) {
+  PVariant v;
+  const bool dyn = a.n_epochs > 0;
+  const long lds = dyn ? gadmm_chain_persistent_lds_dyn(a.d, a.obj_mode, a.nvar)
+                       : gadmm_chain_persistent_lds(a.d, a.obj_mode);
+  if (lds == 0) return v;
+  const long monitor_lds = (long)a.n * 8;
+  const size_t shm = (size_t)(lds > monitor_lds ? lds : monitor_lds);
+#define GADMM_P_PICK(NCv, SYSv, REGv, ...)                                                         \
+  do {                                                                                             \
+    v.fn = (const void*)chain_persistent_kernel<NCv, SYSv, REGv, ##__VA_ARGS__>;                   \
+    v.shm = REGv ? (size_t)(monitor_lds > QSTAGE * 8 ? monitor_lds : QSTAGE * 8) : shm;             \
+    v.threads = REGv ? 64 : NT;                                                                    \
+  } while (0)
+  static const bool force_lds = getenv("GADMM_PERSIST_LDS") != nullptr;  // A/B switch
+  const bool tl = a.timeline != nullptr;  // instrumented instantiations (one GPU, register kernel, LDS d <= 64)
+  if (a.d <= DREG && !force_lds && (!dyn || a.nvar <= 2)) {
+    // register kernel: QT = 13 covers d <= 52 (E1/E5), 16 covers d <= 64
+    if (tl && !a.sys_scope && a.d <= 52) {
+      if (dyn) GADMM_P_PICK(1, false, true, 13, 2, true);
+      else GADMM_P_PICK(1, false, true, 13, 1, true);
+    } else if (dyn) {
+      if (a.sys_scope) {
+        if (a.d <= 52) GADMM_P_PICK(1, true, true, 13, 2);
+        else GADMM_P_PICK(1, true, true, 16, 2);
+      } else {
+        if (a.d <= 52) GADMM_P_PICK(1, false, true, 13, 2);
+        else GADMM_P_PICK(1, false, true, 16, 2);
+      }
+    } else if (a.sys_scope) {
+      if (a.d <= 52) GADMM_P_PICK(1, true, true, 13, 1);
+      else GADMM_P_PICK(1, true, true, 16, 1);
+    } else {
+      if (a.d <= 52) GADMM_P_PICK(1, false, true, 13, 1);
+      else GADMM_P_PICK(1, false, true, 16, 1);
+    }
+  } else if (a.d <= 64) {
+    if (a.sys_scope) GADMM_P_PICK(1, true, false);
+    else if (tl) GADMM_P_PICK(1, false, false, 1, 1, true);
+    else GADMM_P_PICK(1, false, false);
+  } else {
+    if (a.sys_scope) GADMM_P_PICK(2, true, false);
+    else GADMM_P_PICK(2, false, false);
+  }
+#undef GADMM_P_PICK
+  return v;
+}
+
+// Workgroups of `fn` (block size, dynamic LDS) that the device can hold resident at once:
+// occupancy per CU x CUs. GADMM_CU_BUDGET=<n> replaces the CU count (tests of a partitioned or
+// shared device). A persistent launch needs every one of its workgroups resident together: the
+// workers spin on each other, so a workgroup that waits for a CU would stall the rest until the
+// deadline. 0 on error.
+extern "C" long gadmm_resident_capacity(const void* fn, int threads, size_t shm) {
+  int dev = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return 0;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
+  if (shm > 65536 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess)
+    return 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, shm) != hipSuccess) return 0;
+  long cus = prop.multiProcessorCount;
+  if (const char* e = getenv("GADMM_CU_BUDGET")) {
+    const long b = atol(e);
+    if (b > 0 && b < cus) cus = b;
+  }
+  return (long)per_cu * cus;
+}
+
+extern "C" {
+
+// Workgroups the persistent kernel for `args` can keep resident (0: shape not eligible).
+long gadmm_chain_persistent_capacity(const PersistArgs* args) {
+  const PVariant v = pick_variant(*args);
+  return v.fn ? gadmm_resident_capacity(v.fn, v.threads, v.shm) : 0;
+}
+
 int gadmm_chain_persistent_launch(const PersistArgs* args, hipStream_t st) {
   const PersistArgs& a = *args;
   const bool dyn = a.n_epochs > 0;
-  if (dyn && (a.nranks != 1 || a.push || !a.epoch_start || !a.ep_slots || !a.ep_pos)) {
-    gadmm_set_error("persistent chain kernel: dynamic epochs need one rank (epoch_start[0] must be start_iter)");
+  if (dyn && (a.push || !a.epoch_start || !a.ep_slots || !a.ep_pos)) {
+    gadmm_set_error("persistent chain kernel: dynamic epochs need epoch tables (epoch_start[0] == start_iter) "
+                    "and per-epoch push masks instead of static push targets");
     return -1;
   }
-  const long lds = dyn ? gadmm_chain_persistent_lds_dyn(a.d, a.obj_mode, a.nvar)
-                       : gadmm_chain_persistent_lds(a.d, a.obj_mode);
-  if (lds == 0) {
+  if (dyn && a.nranks > 1 && (!a.sys_scope || !a.ep_push || !a.peer_thg || a.nranks > 32)) {
+    gadmm_set_error("persistent chain kernel: multi-rank D-GADMM needs the xGMI fabric (ep_push, peer_thg)");
+    return -1;
+  }
+  const PVariant v = pick_variant(a);
+  if (!v.fn) {
     gadmm_set_error("persistent chain kernel: d=%d not eligible", a.d);
     return -1;
   }
   const int blocks = a.n_local + (a.has_monitor ? 1 : 0);
-  if (blocks > 256) {
-    gadmm_set_error("persistent chain kernel: %d workgroups exceed one per CU", blocks);
-    return -1;
+  const long cap = gadmm_resident_capacity(v.fn, v.threads, v.shm);
+  if (blocks > cap) {
+    gadmm_set_error("persistent chain kernel: %d workgroups but only %ld can be resident", blocks, cap);
+    return -2;
   }
   if (a.ring <= a.lag + 1) {
     gadmm_set_error("persistent chain kernel: ring must exceed lag + 1");
@@ -451,42 +559,9 @@ int gadmm_chain_persistent_launch(const PersistArgs* args, hipStream_t st) {
     gadmm_set_error("persistent chain kernel: iteration tags limited to 2^20");
     return -1;
   }
-  const long monitor_lds = (long)a.n * 8;
-  const size_t shm = (size_t)(lds > monitor_lds ? lds : monitor_lds);
-#define GADMM_P_LAUNCH(NCv, SYSv, REGv, ...)                                                       \
-  do {                                                                                             \
-    const void* kfn = (const void*)chain_persistent_kernel<NCv, SYSv, REGv, ##__VA_ARGS__>;        \
-    const size_t sh = REGv ? (size_t)(monitor_lds > QSTAGE * 8 ? monitor_lds : QSTAGE * 8) : shm;   \
-    if (sh > 65536) GADMM_CHECK(hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh)); \
-    void* kargs[] = {const_cast<PersistArgs*>(&a)};                                                \
-    GADMM_CHECK(hipLaunchKernel(kfn, dim3(blocks), dim3(REGv ? 64 : NT), kargs, sh, st));          \
-  } while (0)
-  static const bool force_lds = getenv("GADMM_PERSIST_LDS") != nullptr;  // A/B switch
-  const bool tl = a.timeline != nullptr;  // instrumented instantiations (one GPU, register kernel, LDS d <= 64)
-  if (a.d <= DREG && !force_lds && (!dyn || a.nvar <= 2)) {
-    // register kernel: QT = 13 covers d <= 52 (E1/E5), 16 covers d <= 64
-    if (tl && !a.sys_scope && a.d <= 52) {
-      if (dyn) GADMM_P_LAUNCH(1, false, true, 13, 2, true);
-      else GADMM_P_LAUNCH(1, false, true, 13, 1, true);
-    } else if (dyn) {
-      if (a.d <= 52) GADMM_P_LAUNCH(1, false, true, 13, 2);
-      else GADMM_P_LAUNCH(1, false, true, 16, 2);
-    } else if (a.sys_scope) {
-      if (a.d <= 52) GADMM_P_LAUNCH(1, true, true, 13, 1);
-      else GADMM_P_LAUNCH(1, true, true, 16, 1);
-    } else {
-      if (a.d <= 52) GADMM_P_LAUNCH(1, false, true, 13, 1);
-      else GADMM_P_LAUNCH(1, false, true, 16, 1);
-    }
-  } else if (a.d <= 64) {
-    if (a.sys_scope) GADMM_P_LAUNCH(1, true, false);
-    else if (tl) GADMM_P_LAUNCH(1, false, false, 1, 1, true);
-    else GADMM_P_LAUNCH(1, false, false);
-  } else {
-    if (a.sys_scope) GADMM_P_LAUNCH(2, true, false);
-    else GADMM_P_LAUNCH(2, false, false);
-  }
-#undef GADMM_P_LAUNCH
+  if (v.shm > 65536) GADMM_CHECK(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v.shm));
+  void* kargs[] = {const_cast<PersistArgs*>(&a)};
+  GADMM_CHECK(hipLaunchKernel(v.fn, dim3(blocks), dim3(v.threads), kargs, v.shm, st));
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

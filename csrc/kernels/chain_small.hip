@@ -728,13 +728,15 @@ __global__ void chain_clear_pending_kernel(ChainCtl* ctl) {
 
 // Multi-rank monitor: `reduced` holds the all-reduced per-iteration objective ring. Checks every
 // iteration finished since the last monitor call, in order, exactly like the reference stop rule.
-__global__ void chain_monitor_kernel(ChainCtl* ctl, const double* reduced, int ring, double* trace, int max_iter,
-                                     double obj0, double tol) {
+__global__ void chain_monitor_kernel(ChainCtl* ctl, const double* reduced, int ring, int n_total, double* trace,
+                                     int max_iter, double obj0, double tol) {
   if (threadIdx.x != 0) return;
   if (ctl->done) return;
   const int last = ctl->iter - 1;
   for (int j = ctl->monitored + 1; j <= last; ++j) {
-    const double s = reduced[(j - 1) % ring];
+    const double* row = reduced + (long)((j - 1) % ring) * n_total;
+    double s = 0.0;
+    for (int g = 0; g < n_total; ++g) s += row[g];  // worker order == the single-rank finish
     if (j - 1 < max_iter) trace[j - 1] = s;
     ctl->monitored = j;
     if (!(s == s) || isinf(s)) {
@@ -860,9 +862,10 @@ int gadmm_chain_dual_flush(const PhaseSlot* slots, int n_slots, int d, double rh
   return 0;
 }
 
-int gadmm_chain_monitor(ChainCtl* ctl, const double* reduced, int ring, double* trace, int max_iter, double obj0,
-                        double tol, hipStream_t st) {
-  hipLaunchKernelGGL(chain_monitor_kernel, dim3(1), dim3(64), 0, st, ctl, reduced, ring, trace, max_iter, obj0, tol);
+int gadmm_chain_monitor(ChainCtl* ctl, const double* reduced, int ring, int n_total, double* trace, int max_iter,
+                        double obj0, double tol, hipStream_t st) {
+  hipLaunchKernelGGL(chain_monitor_kernel, dim3(1), dim3(64), 0, st, ctl, reduced, ring, n_total, trace, max_iter,
+                     obj0, tol);
   GADMM_CHECK(hipGetLastError());
   return 0;
 }
@@ -907,6 +910,18 @@ int gadmm_chain_reset(ChainCtl* ctl, int start_iter, int pending, hipStream_t st
 }
 
 }  // extern "C"
+
+// Real-clock reference: s_memrealtime (100 MHz, the clock every monitor stamps decisions with) at the
+// point of the stream where a solve starts.
+__global__ void stamp_kernel(long long* p) {
+  if (threadIdx.x == 0) *p = (long long)__builtin_amdgcn_s_memrealtime();
+}
+
+extern "C" int gadmm_write_stamp(long long* p, hipStream_t st) {
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, st, p);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
 
 // Close an iteration on a rank that owns no tail worker (multi-rank chains can leave a rank with
 // heads only): sums the local objectives and advances the counter exactly like the tail's FINISH.

@@ -1,0 +1,253 @@
+// Device-copy transport for the graph-replayed chain engine: multi-rank GADMM without RCCL.
+//
+// The chain engine (csrc/runtime/chain_engine.cpp) moves boundary theta rows after every phase and
+// reduces the per-worker objective ring at every block end. With RCCL those are ncclSend/ncclRecv
+// and ncclAllReduce. This transport does the same with two small kernels and IPC-mapped memory, so
+//   * the engine's multi-rank code (plans, ghost rows, objective ring, monitor, D-GADMM re-plans)
+//     runs with several processes on ONE GPU (RCCL refuses two ranks on one device), and
+//   * on a node it is an RCCL-free alternative that stays inside the captured hipGraph.
+//
+// Every rank owns one fine-grained (uncached) mailbox, exported by IPC (parallel/ipc.py):
+//   theta area  [R][n_total][d]   16-B granules; slot = code % R, code = 4 * iteration + phase
+//   obj area    [2][n_total][ring] 16-B granules; parity = all-gather sequence & 1
+// A send op stores its row straight into the peer's mailbox as {tag, lo, tag, hi} write-through
+// granules (the data-is-flag form of chain_persistent.hip; a torn store is caught by the tags); the
+// receiving rank's recv op re-reads its own mailbox row until every granule carries the expected
+// tag, then writes the row into its theta table for the next phase kernel (a kernel boundary).
+// Tags are salted with a per-solve epoch that lives in device memory (incremented by a kernel at
+// every engine reset), so captured graphs stay valid and buffers need no re-zeroing.
+// Overwrite safety: all ranks meet at every block-end all-gather, so no rank runs more than one block
+// (<= ring iterations = 4 * ring codes) ahead of a reader; R = 8 * ring + 8 slots.
+// Every spin has a wall-clock deadline; a stalled peer sets ctl->done = 4 on the waiting rank.
+#include "gadmm_common.h"
+#include "gadmm_chain.h"
+#include "persist_device.h"
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+namespace {
+
+constexpr int MAX_BATCH = 64;
+
+struct XchgBatch {
+  int n, phase, pad0, pad1;
+  XchgOp op[MAX_BATCH];
+};
+
+struct IpcXport {
+  int rank, nranks, d, n_total, ring, R;
+  u32x4* box;               // this rank's mailbox
+  u32x4** d_boxes;          // device [nranks]: every rank's mailbox (own included), IPC-mapped
+  unsigned* d_word;         // device [4]: [0] solve epoch, [1] all-gather sequence
+  long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
+  long long payload_bytes = 0, wire_bytes = 0, msgs = 0, obj_bytes = 0;
+};
+
+__device__ __forceinline__ void give_up(ChainCtl* ctl) {
+  __hip_atomic_store(&ctl->done, 4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One workgroup (one wave) per op of the batch.
+__global__ void __launch_bounds__(64) ipc_xchg_kernel(XchgBatch b, double* table, int d, int n_total, int R,
+                                                      u32x4* const* boxes, u32x4* my_box, const unsigned* word,
+                                                      ChainCtl* ctl, long long timeout_ticks) {
+  // multi-rank: `done` changes only in the block-end monitor, identically on every rank, so every rank
+  // skips the same exchanges
+  if (ctl->done) return;
+  const XchgOp o = b.op[blockIdx.x];
+  const int lane = threadIdx.x;
+  const unsigned code = (unsigned)(4 * ctl->iter + b.phase) & 0xfffffu;
+  const unsigned tag = make_tag(word[0], (int)code);
+  const long base = ((long)(code % (unsigned)R) * n_total + o.row) * d;  // granule index of the row
+  const int cnt = o.count > 0 ? o.count : d;
+  double* row = table + (long)o.row * d;
+  if (o.is_send) {
+    const __amdgpu_buffer_rsrc_t rs = rsrc_of(boxes[o.peer] + base);
+    for (int i = lane; i < cnt; i += 64) store_granule<true>(rs, i * 16, tag, row[i]);
+    return;
+  }
+  const __amdgpu_buffer_rsrc_t rs = rsrc_of(my_box + base);
+  const unsigned long long deadline = now_ticks() + (unsigned long long)timeout_ticks;
+  for (int i0 = 0; i0 < cnt; i0 += 64) {
+    const int i = i0 + lane;
+    double v = 0.0;
+    for (int spin = 0;; ++spin) {
+      const bool ok = i >= cnt || load_granule<true>(rs, i * 16, tag, &v);
+      if (__all(ok)) break;
+      if ((spin & 7) == 7 && now_ticks() > deadline) {
+        if (lane == 0) give_up(ctl);
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (i < cnt) row[i] = v;
+  }
+}
+
+// Block-end reduction of the per-worker objective ring: every rank pushes its workers' entries into
+// every rank's obj area, then reads all n_total x ring entries back into `reduced` (worker-indexed, so
+// the monitor's worker-order sum is the same on every rank and equal to the single-rank sum).
+__global__ void __launch_bounds__(256) ipc_allgather_kernel(const double* part, double* reduced, int ring, int n_total,
+                                                            const int* lgid, int n_local, int nranks, long obj_base,
+                                                            u32x4* const* boxes, u32x4* my_box, unsigned* word,
+                                                            ChainCtl* ctl, long long timeout_ticks) {
+  __shared__ int fail;
+  if (ctl->done) return;
+  if (threadIdx.x == 0) fail = 0;
+  __syncthreads();
+  const unsigned seq = word[1];
+  const long par = seq & 1u;
+  const unsigned tag = make_tag(word[0], (int)((seq + 1u) & 0xfffffu));
+  for (int e = threadIdx.x; e < n_local * ring; e += blockDim.x) {
+    const int li = e / ring, s = e % ring, g = lgid[li];
+    const double v = part[(long)s * n_total + g];
+    const long off = obj_base + (par * n_total + g) * ring + s;
+    for (int r = 0; r < nranks; ++r) store_granule<true>(rsrc_of(boxes[r] + off), 0, tag, v);
+  }
+  const unsigned long long deadline = now_ticks() + (unsigned long long)timeout_ticks;
+  const __amdgpu_buffer_rsrc_t rs = rsrc_of(my_box + obj_base + par * n_total * ring);
+  for (int e = threadIdx.x; e < n_total * ring; e += blockDim.x) {
+    const int g = e / ring, s = e % ring;
+    double v = 0.0;
+    for (int spin = 0;; ++spin) {
+      if (load_granule<true>(rs, e * 16, tag, &v)) break;
+      if ((spin & 7) == 7 && now_ticks() > deadline) {
+        fail = 1;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    reduced[(long)s * n_total + g] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (fail) give_up(ctl);
+    word[1] = seq + 1u;
+  }
+}
+
+__global__ void ipc_new_epoch_kernel(unsigned* word) {
+  if (threadIdx.x == 0) word[0] = word[0] % 4095u + 1u;
+}
+
+}  // namespace
+
+extern "C" {
+
+long gadmm_ipc_box_bytes(int n_total, int d, int ring) {
+  const long R = 8L * ring + 8;
+  return (R * n_total * d + 2L * n_total * ring) * 16;
+}
+
+void* gadmm_ipc_xport_create(int rank, int nranks, int d, int n_total, int ring, void* my_box,
+                             void* const* all_boxes, double timeout_s) {
+  if (nranks < 1 || rank < 0 || rank >= nranks || d < 1 || n_total < 1 || ring < 1) {
+    gadmm_set_error("ipc_xport_create: bad shape");
+    return nullptr;
+  }
+  IpcXport* x = new IpcXport();
+  x->rank = rank;
+  x->nranks = nranks;
+  x->d = d;
+  x->n_total = n_total;
+  x->ring = ring;
+  x->R = 8 * ring + 8;
+  x->box = (u32x4*)my_box;
+  x->timeout_ticks = (long long)(timeout_s * 1e8);
+  if (hipMalloc((void**)&x->d_boxes, sizeof(void*) * nranks) != hipSuccess ||
+      hipMalloc((void**)&x->d_word, 4 * sizeof(unsigned)) != hipSuccess) {
+    gadmm_set_error("ipc_xport_create: hipMalloc failed");
+    delete x;
+    return nullptr;
+  }
+  if (hipMemcpy(x->d_boxes, all_boxes, sizeof(void*) * nranks, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(x->d_word, 0, 4 * sizeof(unsigned)) != hipSuccess) {
+    gadmm_set_error("ipc_xport_create: upload failed");
+    delete x;
+    return nullptr;
+  }
+  return x;
+}
+
+int gadmm_ipc_xport_destroy(void* h) {
+  IpcXport* x = (IpcXport*)h;
+  if (!x) return 0;
+  hipFree(x->d_boxes);
+  hipFree(x->d_word);
+  delete x;
+  return 0;
+}
+
+// Start a new solve: every tag of the previous solve stops matching. Every rank calls it once per reset.
+int gadmm_ipc_new_epoch(void* h, hipStream_t st) {
+  IpcXport* x = (IpcXport*)h;
+  hipLaunchKernelGGL(ipc_new_epoch_kernel, dim3(1), dim3(64), 0, st, x->d_word);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+// The grouped exchange of a phase (phase: 0 after heads, 1 after tails, 2/3 eager re-plan refreshes).
+int gadmm_ipc_exchange_rows(void* h, const XchgOp* ops, int nops, double* table, int d, int phase, ChainCtl* ctl,
+                            hipStream_t st) {
+  IpcXport* x = (IpcXport*)h;
+  if (!x) {
+    gadmm_set_error("ipc_exchange_rows: no transport");
+    return -1;
+  }
+  if (d != x->d) {
+    gadmm_set_error("ipc_exchange_rows: d=%d, transport built for %d", d, x->d);
+    return -1;
+  }
+  for (int i0 = 0; i0 < nops; i0 += MAX_BATCH) {
+    XchgBatch b{};
+    b.n = nops - i0 < MAX_BATCH ? nops - i0 : MAX_BATCH;
+    b.phase = phase;
+    for (int k = 0; k < b.n; ++k) {
+      b.op[k] = ops[i0 + k];
+      if (b.op[k].peer < 0 || b.op[k].peer >= x->nranks || b.op[k].row < 0 || b.op[k].row >= x->n_total ||
+          b.op[k].count > d) {
+        gadmm_set_error("ipc_exchange_rows: bad op (peer %d, row %d)", b.op[k].peer, b.op[k].row);
+        return -1;
+      }
+      if (b.op[k].is_send) {
+        const long long c = b.op[k].count > 0 ? b.op[k].count : d;
+        x->payload_bytes += c * 8;
+        x->wire_bytes += c * 16;
+        x->msgs += 1;
+      }
+    }
+    hipLaunchKernelGGL(ipc_xchg_kernel, dim3(b.n), dim3(64), 0, st, b, table, d, x->n_total, x->R, x->d_boxes,
+                       x->box, x->d_word, ctl, x->timeout_ticks);
+  }
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+int gadmm_ipc_allgather(void* h, const double* part, double* reduced, int ring, const int* lgid, int n_local,
+                        ChainCtl* ctl, hipStream_t st) {
+  IpcXport* x = (IpcXport*)h;
+  if (!x || ring != x->ring) {
+    gadmm_set_error("ipc_allgather: transport missing or built for another ring");
+    return -1;
+  }
+  const long obj_base = (long)x->R * x->n_total * x->d;
+  x->obj_bytes += (long long)n_local * ring * 16 * (x->nranks - 1);
+  hipLaunchKernelGGL(ipc_allgather_kernel, dim3(1), dim3(256), 0, st, part, reduced, ring, x->n_total, lgid, n_local,
+                     x->nranks, obj_base, x->d_boxes, x->box, x->d_word, ctl, x->timeout_ticks);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+// out4: theta payload bytes sent, theta wire bytes (16-B granules), messages, objective-ring wire bytes.
+// Counted at enqueue (a captured graph's replays are counted by the engine, see RunStats).
+int gadmm_ipc_counters(void* h, long long* out4) {
+  IpcXport* x = (IpcXport*)h;
+  out4[0] = x->payload_bytes;
+  out4[1] = x->wire_bytes;
+  out4[2] = x->msgs;
+  out4[3] = x->obj_bytes;
+  return 0;
+}
+
+}  // extern "C"

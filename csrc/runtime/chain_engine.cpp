@@ -22,13 +22,17 @@
 extern "C" {
 int gadmm_chain_phase(const PhaseArgs* args, hipStream_t st);
 int gadmm_chain_close(const PhaseArgs* args, hipStream_t st);
-int gadmm_chain_monitor(ChainCtl* ctl, const double* reduced, int ring, double* trace, int max_iter, double obj0,
-                        double tol, hipStream_t st);
+int gadmm_chain_monitor(ChainCtl* ctl, const double* reduced, int ring, int n_total, double* trace, int max_iter,
+                        double obj0, double tol, hipStream_t st);
 int gadmm_chain_reset(ChainCtl* ctl, int start_iter, int pending, hipStream_t st);
 int gadmm_chain_dual_flush(const PhaseSlot* slots, int n_slots, int d, double rho, const double* theta, double* mu,
                            ChainCtl* ctl, hipStream_t st);
 int gadmm_rccl_exchange_rows(void* h, const XchgOp* ops, int nops, double* table, int d, hipStream_t st);
 int gadmm_rccl_allreduce_sum_f64(void* h, const double* send, double* recv, long count, hipStream_t st);
+int gadmm_ipc_exchange_rows(void* h, const XchgOp* ops, int nops, double* table, int d, int phase, ChainCtl* ctl,
+                            hipStream_t st);
+int gadmm_ipc_allgather(void* h, const double* part, double* reduced, int ring, const int* lgid, int n_local,
+                        ChainCtl* ctl, hipStream_t st);
 }
 
 struct ChainEngine {
@@ -53,6 +57,18 @@ struct ChainEngine {
     return f;
   }
 
+  // Row exchange of one phase through whichever data plane the engine was given. A multi-rank plan
+  // without one is an error (never a null-communicator dereference).
+  int exchange_ops(const std::vector<XchgOp>& ops, int phase) {
+    if (ops.empty()) return 0;
+    const PhaseArgs& a = desc.base;
+    if (desc.xport) return gadmm_ipc_exchange_rows(desc.xport, ops.data(), (int)ops.size(), a.theta, a.d, phase,
+                                                   a.ctl, desc.stream);
+    if (desc.comm) return gadmm_rccl_exchange_rows(desc.comm, ops.data(), (int)ops.size(), a.theta, a.d, desc.stream);
+    gadmm_set_error("chain engine: the plan has cross-rank messages but no communicator or transport");
+    return -1;
+  }
+
   int enqueue_iteration() {
     PhaseArgs a = desc.base;
     hipStream_t st = desc.stream;
@@ -64,26 +80,20 @@ struct ChainEngine {
       int r = gadmm_chain_phase(&a, st);
       if (r) return r;
     }
-    if (desc.comm && !xh.empty()) {
-      int r = gadmm_rccl_exchange_rows(desc.comm, xh.data(), (int)xh.size(), a.theta, a.d, st);
-      if (r) return r;
-    }
+    int r = exchange_ops(xh, 0);
+    if (r) return r;
     // tail phase (also closes the iteration: FINISH needs >= 1 block, see run())
     a.slots = desc.d_slots + head.size();
     a.n_slots = (int)tail.size();
     a.flags = flags_tail();
     if (a.n_slots > 0) {
-      int r = gadmm_chain_phase(&a, st);
+      r = gadmm_chain_phase(&a, st);
       if (r) return r;
     } else {
-      int r = gadmm_chain_close(&a, st);
+      r = gadmm_chain_close(&a, st);
       if (r) return r;
     }
-    if (desc.comm && !xt.empty()) {
-      int r = gadmm_rccl_exchange_rows(desc.comm, xt.data(), (int)xt.size(), a.theta, a.d, st);
-      if (r) return r;
-    }
-    return 0;
+    return exchange_ops(xt, 1);
   }
 
   int enqueue_block(int block) {
@@ -92,10 +102,19 @@ struct ChainEngine {
       if (r) return r;
     }
     if (desc.nranks > 1) {
-      int r = gadmm_rccl_allreduce_sum_f64(desc.comm, desc.base.part, desc.reduced, desc.base.ring, desc.stream);
+      const PhaseArgs& a = desc.base;
+      int r;
+      if (desc.xport) {
+        r = gadmm_ipc_allgather(desc.xport, a.part, desc.reduced, a.ring, a.lgid, a.n_local, a.ctl, desc.stream);
+      } else if (desc.comm) {
+        r = gadmm_rccl_allreduce_sum_f64(desc.comm, a.part, desc.reduced, (long)a.ring * a.n_total, desc.stream);
+      } else {
+        gadmm_set_error("chain engine: %d ranks but no communicator or transport", desc.nranks);
+        r = -1;
+      }
       if (r) return r;
-      r = gadmm_chain_monitor(desc.base.ctl, desc.reduced, desc.base.ring, desc.base.trace, desc.base.max_iter,
-                              desc.base.obj0, desc.base.tol, desc.stream);
+      r = gadmm_chain_monitor(a.ctl, desc.reduced, a.ring, a.n_total, a.trace, a.max_iter, a.obj0, a.tol,
+                              desc.stream);
       if (r) return r;
     }
     return 0;
@@ -186,6 +205,9 @@ int gadmm_chain_engine_set_plan(void* h, int n_head, const PhaseSlot* head, int 
 
 int gadmm_chain_engine_set_scalars(void* h, double rho, double obj0, double tol, int max_iter) {
   ChainEngine* e = (ChainEngine*)h;
+  const PhaseArgs& b = e->desc.base;
+  // captured kernels carry these scalars by value: re-capture only when one of them changes
+  if (b.rho == rho && b.obj0 == obj0 && b.tol == tol && b.max_iter == max_iter) return 0;
   e->desc.base.rho = rho;
   e->desc.base.obj0 = obj0;
   e->desc.base.tol = tol;
@@ -272,8 +294,14 @@ int gadmm_chain_engine_run(void* h, int block, int stop_iter, int use_graph, Run
     if (o.is_send) { per_iter += (long long)(o.count > 0 ? o.count : e->desc.base.d) * 8; msgs++; }
   const int ran = out->iters - start + 1 > 0 ? out->iters - start + 1 : 0;
   out->p2p_bytes = per_iter * ran;
+  out->wire_bytes = e->desc.xport ? 2 * per_iter * ran : per_iter * ran;
   out->p2p_msgs = msgs * ran;
-  out->monitor_bytes = e->desc.nranks > 1 ? (long long)replays * e->desc.base.ring * 8 : 0;
+  // stop-rule traffic leaving this rank per block: RCCL all-reduce of the [ring][n_total] objective ring
+  // (payload), or the transport's objective granules to every other rank (wire bytes, 16 B each)
+  const PhaseArgs& pa = e->desc.base;
+  out->monitor_bytes = e->desc.nranks <= 1 ? 0
+                       : e->desc.xport ? (long long)replays * pa.n_local * pa.ring * 16 * (e->desc.nranks - 1)
+                                       : (long long)replays * pa.ring * pa.n_total * 8;
   return 0;
 }
 
@@ -282,11 +310,9 @@ int gadmm_chain_engine_graph_ok(void* h) { return ((ChainEngine*)h)->graph_ok ? 
 // One eager exchange with the current plan (which = 0: after-head messages, 1: after-tail).
 int gadmm_chain_engine_exchange(void* h, int which) {
   ChainEngine* e = (ChainEngine*)h;
-  if (!e->desc.comm) return 0;
   auto& ops = which == 0 ? e->xh : e->xt;
   if (ops.empty()) return 0;
-  int r = gadmm_rccl_exchange_rows(e->desc.comm, ops.data(), (int)ops.size(), e->desc.base.theta, e->desc.base.d,
-                                   e->desc.stream);
+  int r = e->exchange_ops(ops, 2 + (which != 0));  // phase codes 2/3: never collide with the in-loop 0/1
   if (r) return r;
   GADMM_CHECK(hipStreamSynchronize(e->desc.stream));
   return 0;
@@ -299,7 +325,8 @@ int gadmm_abi_layout(long long* out, int n) {
                    (long long)offsetof(PhaseArgs, inner_iters), (long long)sizeof(EngineDesc),
                    (long long)offsetof(EngineDesc, stream), (long long)sizeof(RunStats),
                    (long long)sizeof(PersistArgs), (long long)offsetof(PersistArgs, rho),
-                   (long long)offsetof(PersistArgs, ctl)};
+                   (long long)offsetof(PersistArgs, ctl), (long long)offsetof(PhaseArgs, lgid),
+                   (long long)offsetof(EngineDesc, xport)};
   const int k = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n && i < k; ++i) out[i] = v[i];
   return k;

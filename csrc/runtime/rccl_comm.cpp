@@ -24,6 +24,16 @@ struct RcclComm {
   std::atomic<long long> bytes_sent{0}, bytes_recv{0}, msgs_sent{0}, coll_bytes{0};
 };
 
+// Every entry point takes the handle from Python / the engine: a null one is an error, not a crash.
+#define RCCL_HANDLE(h)                                         \
+  RcclComm* c = (RcclComm*)(h);                                \
+  do {                                                         \
+    if (!c) {                                                  \
+      gadmm_set_error("%s: null RCCL communicator", __func__); \
+      return -1;                                               \
+    }                                                          \
+  } while (0)
+
 #define NCCL_CHECK(expr)                                                                  \
   do {                                                                                    \
     ncclResult_t _r = (expr);                                                             \
@@ -80,7 +90,7 @@ int gadmm_rccl_destroy(void* h) {
 
 // Grouped point-to-point exchange of rows of a row-major (rows x d) f64 table.
 int gadmm_rccl_exchange_rows(void* h, const XchgOp* ops, int nops, double* table, int d, hipStream_t st) {
-  RcclComm* c = (RcclComm*)h;
+  RCCL_HANDLE(h);
   if (nops == 0) return 0;
   NCCL_CHECK(ncclGroupStart());
   long long s = 0, r = 0, ns = 0;
@@ -107,7 +117,7 @@ int gadmm_rccl_exchange_rows(void* h, const XchgOp* ops, int nops, double* table
 // Raw-buffer send/recv pairs (LAG uploads, star ADMM) — pointers are device addresses.
 int gadmm_rccl_sendrecv_raw(void* h, int nops, const int* peers, const int* is_send, double* const* bufs,
                             const long* counts, hipStream_t st) {
-  RcclComm* c = (RcclComm*)h;
+  RCCL_HANDLE(h);
   if (nops == 0) return 0;
   NCCL_CHECK(ncclGroupStart());
   for (int i = 0; i < nops; ++i) {
@@ -125,28 +135,28 @@ int gadmm_rccl_sendrecv_raw(void* h, int nops, const int* peers, const int* is_s
 }
 
 int gadmm_rccl_allreduce_sum_f64(void* h, const double* send, double* recv, long count, hipStream_t st) {
-  RcclComm* c = (RcclComm*)h;
+  RCCL_HANDLE(h);
   NCCL_CHECK(ncclAllReduce(send, recv, (size_t)count, ncclDouble, ncclSum, c->comm, st));
   c->coll_bytes += count * 8;
   return 0;
 }
 
 int gadmm_rccl_reduce_sum_f64(void* h, const double* send, double* recv, long count, int root, hipStream_t st) {
-  RcclComm* c = (RcclComm*)h;
+  RCCL_HANDLE(h);
   NCCL_CHECK(ncclReduce(send, recv, (size_t)count, ncclDouble, ncclSum, root, c->comm, st));
   c->coll_bytes += count * 8;
   return 0;
 }
 
 int gadmm_rccl_bcast_f64(void* h, double* buf, long count, int root, hipStream_t st) {
-  RcclComm* c = (RcclComm*)h;
+  RCCL_HANDLE(h);
   NCCL_CHECK(ncclBroadcast(buf, buf, (size_t)count, ncclDouble, root, c->comm, st));
   c->coll_bytes += count * 8;
   return 0;
 }
 
 int gadmm_rccl_counters(void* h, long long* out4) {
-  RcclComm* c = (RcclComm*)h;
+  RCCL_HANDLE(h);
   out4[0] = c->bytes_sent.load();
   out4[1] = c->bytes_recv.load();
   out4[2] = c->msgs_sent.load();
@@ -155,7 +165,7 @@ int gadmm_rccl_counters(void* h, long long* out4) {
 }
 
 int gadmm_rccl_reset_counters(void* h) {
-  RcclComm* c = (RcclComm*)h;
+  RCCL_HANDLE(h);
   c->bytes_sent = 0;
   c->bytes_recv = 0;
   c->msgs_sent = 0;

@@ -76,7 +76,8 @@ def chain_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: 
             and not check_exchange and not failures:
         from ..ops import native
 
-        if native.available() and (comm.nranks == 1 or getattr(comm, "backend", "") == "rccl"):
+        if native.available() and (comm.nranks == 1 or getattr(comm, "backend", "") in ("rccl", "ipc")
+                                   or (engine_opts or {}).get("fabric") is not None):
             use_native = True
         elif backend == "native":
             raise RuntimeError("native backend requested but unavailable for this comm/device")
@@ -213,10 +214,14 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
 
 def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, schedule, local_solver,
                        step, max_inner, inner_tol, cost_quirk, name, opts):
-    from ..engine.chain_engine import NativeChainEngine
+    """``opts``: ``block`` (iterations per graph replay), ``persistent`` (auto/True/False), ``graph``,
+    ``cache``, ``state``, ``fabric`` (an ``XgmiFabric``: the device-initiated multi-GPU persistent
+    kernels; with ``table_slots >= lag + 4`` it also runs multi-rank D-GADMM in one launch)."""
+    from ..engine.chain_engine import NativeChainEngine, ResidencyError, HandoffTimeout
 
     rank = comm.rank
     rcomm = comm if comm.nranks > 1 else None
+    fabric = opts.get("fabric")
     kind = "linear" if local_solver == "closed" else "logistic"
     # iterations per replayed graph: a logistic phase is ~37 us, so the replays left over after the stop
     # decision cost more than the extra host round trips of short blocks (tools/logistic_block_sweep.py:
@@ -252,19 +257,32 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         or schedule.coherence >= max_iter + 1
     p2p = 0
     mon = 0
+    wire = 0
+    want_persistent = opts.get("persistent", "auto") in (True, "auto")
     if static:
-        persistent = opts.get("persistent", "auto")
-        if (persistent is True or persistent == "auto") and eng.persistent_eligible():
-            r = eng.run_persistent()
-            engine_kind = "persistent"
-        else:
+        r = None
+        engine_kind = None
+        if want_persistent and eng.persistent_eligible(fabric):
+            try:
+                r = eng.run_persistent(fabric=fabric)
+                engine_kind = "persistent"
+            except (ResidencyError, HandoffTimeout) as e:
+                # the device could not hold every workgroup, or a hand-off stalled: the graph engine
+                # runs the same schedule without co-residency (single rank; several ranks must agree,
+                # see bench.py, so they raise)
+                if comm.nranks > 1:
+                    raise
+                eng.reset()
+                engine_kind = "graph(fallback: %s)" % type(e).__name__
+        if r is None:
             r = eng.run(use_graph=opts.get("graph", True))
-            engine_kind = "graph" if eng.graph_ok() else "eager"
+            if engine_kind is None:
+                engine_kind = "graph" if eng.graph_ok() else "eager"
         iters, done = r.iters, r.done
-        p2p, mon = r.p2p_bytes, r.monitor_bytes
+        p2p, mon, wire = r.p2p_bytes, r.monitor_bytes, r.wire_bytes
         per = float(np.sum(schedule.cost)) * (n_heads if cost_quirk else 1)
         com_cost = np.arange(1, iters + 1) * per
-    elif comm.nranks == 1 and opts.get("persistent", "auto") in (True, "auto") and eng.dynamic_eligible() \
+    elif want_persistent and eng.dynamic_eligible(fabric) \
             and len(rechain_iterations(max_iter, schedule.coherence)) < 4096:
         # D-GADMM in ONE persistent launch: the seeded chain sequence is drawn up front (batched,
         # identical RNG stream), every worker switches neighbours/role at each epoch on the device.
@@ -274,7 +292,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         Pn, Cn = schedule.prefetch_arrays(len(rechains))
         P = np.concatenate([np.asarray(saved[1], dtype=np.int64)[None], Pn])
         starts = np.concatenate([[1], rechains]).astype(np.int64)
-        r = eng.run_persistent(epochs=(starts, P))
+        r = eng.run_persistent(epochs=(starts, P), fabric=fabric)
         iters, done = r.iters, r.done
         # per-epoch cost; the initial cost vector may be ragged (the v0 column-slice quirk)
         csum = Cn.sum(axis=1) if Cn.dtype != object else np.asarray([float(np.sum(c)) for c in Cn])
@@ -301,6 +319,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             r = eng.run(stop_iter=nxt - 1, use_graph=False)
             p2p += r.p2p_bytes
             mon += r.monitor_bytes
+            wire += r.wire_bytes
             ran_to = r.iters
             for _ in range(it, ran_to + 1):
                 cc += per
@@ -327,11 +346,12 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         dist.all_reduce(t, group=getattr(comm, "control_group", None))
         bytes_tot = int(t.item())
     res = RunResult(algorithm=name, obj=tr, loss=loss, iters=iters, converged=(done == 1), wall_s=wall,
-                    time_trace=np.linspace(wall / max(iters, 1), wall, iters),
+                    time_trace=eng.time_trace(iters),  # measured on the device: decision time of each iteration
                     comm_units=np.arange(1, iters + 1, dtype=np.float64) * n_total,
                     com_cost=np.asarray(com_cost[:iters]), bytes_sent=int(p2p), bytes_total=bytes_tot,
                     extra={"backend": "native", "engine": engine_kind, "rank": rank, "nranks": comm.nranks,
-                           "solver": local_solver, "monitor_bytes": int(mon)})
+                           "solver": local_solver, "monitor_bytes": int(mon), "wire_bytes": int(wire),
+                           "transport": getattr(comm, "backend", "local") if fabric is None else "xgmi"})
     res.extra["engine_obj"] = eng
     if opts.get("state", True):
         # resumable state for checkpoints: apply the heads' pending (lazy) duals with the current

@@ -28,6 +28,85 @@ import torch
 import torch.distributed as dist
 
 
+# Iterations to the 1e-8 gap of the reference semantics (gadmm_amd/oracle/reference.py:gadmm_linear on
+# linear_synthetic(N)): the correctness gate of every headline run. N = 24: BASELINE.md; N = 8 / 16:
+# pinned by the same oracle (BASELINE.json configs[1] is "8 workers = 8 x MI355X").
+EXPECTED_ITERS_1E8 = {(24, 3.0): 1373, (24, 5.0): 758, (24, 7.0): 428,
+                      (16, 3.0): 588, (16, 5.0): 254, (16, 7.0): 249,
+                      (8, 3.0): 93, (8, 5.0): 126, (8, 7.0): 131}
+
+
+def headline_rank_problem(workers: int, rank: int, world: int, builder=None):
+    """This rank's part of the headline problem, data-local: only the rank's own workers' shards are
+    built (``linear_synthetic(..., worker_ids=local)``), and obj0 comes from the one-time all-reduce
+    of the local Grams over the control plane, not from anybody else's rows.
+    Returns ``(X_loc, y_loc, local_ids, placement, obj0)`` with X_loc (n_local, m, d) on the CPU."""
+    import numpy as np
+    from .data import linear_synthetic
+    from .parallel.topology import Placement
+
+    builder = builder or linear_synthetic
+    placement = Placement.contiguous(workers, world)
+    local = placement.local_workers(rank)
+    ds = builder(workers, worker_ids=local)
+    if ds.num_workers != len(local):
+        raise RuntimeError("builder returned %d shards for %d local workers" % (ds.num_workers, len(local)))
+    X = ds.X.numpy()
+    y = ds.y.numpy()
+    obj0 = linear_obj0_distributed(X, y, local, workers, world)
+    return ds.X, ds.y, local, placement, obj0
+
+
+def linear_obj0_distributed(X, y, local, workers: int, world: int) -> float:
+    """``opt_sol_closedForm.m`` without moving data: the normal equations from the all-reduced Gram
+    ``sum_n [X_n|y_n]^T [X_n|y_n]`` (accumulated in worker order, like the stacked product), then the
+    objective ``1/2 ||X x - y||^2`` from the gathered per-worker residual vectors (m doubles per
+    worker, one-time): evaluated exactly as the stacked oracle (oracle/reference.py:opt_linear), so the
+    stop target -- and with it the reference iteration count -- is the same for every rank count."""
+    import numpy as np
+
+    X = np.asarray(X, dtype=np.float64)
+    y = np.asarray(y, dtype=np.float64)
+    d, m = X.shape[-1], X.shape[1]
+    if world > 1:
+        Xa = np.zeros((workers, m, d))
+        ya = np.zeros((workers, m))
+        Xa[local], ya[local] = X, y
+        # the Gram pieces per worker (d x (d+1) each), summed in worker order below
+        aug = np.concatenate([np.einsum("nmi,nmj->nij", Xa, Xa), np.einsum("nmi,nm->ni", Xa, ya)[:, :, None]], axis=2)
+        t = torch.from_numpy(aug)
+        dist.all_reduce(t)  # every worker's block is non-zero on exactly one rank: the sum is exact
+        aug = t.numpy()
+    else:
+        aug = np.concatenate([np.einsum("nmi,nmj->nij", X, X), np.einsum("nmi,nm->ni", X, y)[:, :, None]], axis=2)
+    G = np.zeros((d, d))
+    b = np.zeros(d)
+    for n in range(workers):
+        G += aug[n, :, :d]
+        b += aug[n, :, d]
+    x = np.linalg.solve(G, b)
+    r_loc = np.einsum("nmi,i->nm", X, x) - y
+    if world > 1:
+        ra = np.zeros((workers, m))
+        ra[local] = r_loc
+        t = torch.from_numpy(ra)
+        dist.all_reduce(t)
+        r = t.numpy()
+    else:
+        r = r_loc
+    return float(0.5 * np.sum(r.reshape(-1) ** 2))
+
+
+def rank_comm(args, world: int, device, comm, n_total: int, d: int, ring: int = 16):
+    """The data plane of a config body: the given communicator (RCCL on a node, LocalComm on one
+    GPU), or -- ranks sharing one GPU (``GADMM_BENCH_SHARE_GPU=1``), where RCCL cannot run -- an IPC
+    device-copy transport sized for this problem."""
+    if comm is not None or world == 1:
+        return comm
+    from .parallel.ipc import IpcComm
+    return IpcComm(n_total, d, ring, device)
+
+
 def _timed(solve: Callable, steps: int, warmup: int, device, world: int):
     last = None
     for _ in range(warmup):
@@ -57,15 +136,17 @@ def run_logistic(args, rank, world, device, comm) -> Dict:
     from .parallel.topology import Placement
 
     n = args.workers
-    ds = logistic_synthetic(n)
     pl = Placement.contiguous(n, world)
     local = pl.local_workers(rank)
-    m = LogisticRegression(ds.X[local].to(device).contiguous(), ds.y[local].to(device).contiguous(), lam=1e-5)
+    ds = logistic_synthetic(n, worker_ids=local)  # data-local: this rank's shards only
+    comm = rank_comm(args, world, device, comm, n, ds.dim, 8)
+    m = LogisticRegression(ds.X.to(device).contiguous(), ds.y.to(device).contiguous(), lam=1e-5)
     obj0 = m.optimum(comm if world > 1 else None, n_total=n)
     rho, tol = 2e-4, 1e-4
 
     def solve():
-        return chain_admm(m, local, n, rho, obj0, tol, 400, comm=comm, placement=pl, local_solver="gd", step=2.2)
+        return chain_admm(m, local, n, rho, obj0, tol, 400, comm=comm, placement=pl, local_solver="gd", step=2.2,
+                          engine_opts={"state": False})
 
     ms, r = _timed(solve, args.steps, args.warmup, device, world)
     return {"metric": "wall-clock to 1e-4 objective gap, GADMM logistic regression, inner-GD HIP kernel "
@@ -86,15 +167,17 @@ def run_logistic_exact(args, rank, world, device, comm) -> Dict:
     from .parallel.topology import Placement
 
     n = args.workers
-    ds = logistic_synthetic(n)
     pl = Placement.contiguous(n, world)
     local = pl.local_workers(rank)
-    m = LogisticRegression(ds.X[local].to(device).contiguous(), ds.y[local].to(device).contiguous(), lam=1e-5)
+    ds = logistic_synthetic(n, worker_ids=local)  # data-local: this rank's shards only
+    comm = rank_comm(args, world, device, comm, n, ds.dim, 16)
+    m = LogisticRegression(ds.X.to(device).contiguous(), ds.y.to(device).contiguous(), lam=1e-5)
     obj0 = m.optimum(comm if world > 1 else None, n_total=n)
     rho, tol = 1e-3, 1e-8
 
     def solve():
-        return chain_admm(m, local, n, rho, obj0, tol, 2000, comm=comm, placement=pl, local_solver="newton")
+        return chain_admm(m, local, n, rho, obj0, tol, 2000, comm=comm, placement=pl, local_solver="newton",
+                          engine_opts={"state": False})
 
     ms, r = _timed(solve, args.steps, args.warmup, device, world)
     return {"metric": "wall-clock to 1e-8 objective gap, GADMM logistic regression, exact (Newton) local solves "
@@ -107,34 +190,70 @@ def run_logistic_exact(args, rank, world, device, comm) -> Dict:
 
 
 def run_dgadmm(args, rank, world, device, comm) -> Dict:
-    from .data import linear_synthetic
+    """D-GADMM (dynamic_group_ADMM_closedForm.m): findPath2 re-chaining every 10 iterations. One GPU:
+    the whole solve in one persistent launch (per-epoch chain tables on the device). Several GPUs:
+    the same kernel on every rank over the xGMI fabric -- each worker pushes theta to the GPUs of its
+    current and next-epoch neighbours -- falling back (all ranks together) to the epoch-by-epoch graph
+    engine on RCCL / the IPC transport."""
     from .models import LinearRegression
     from .algorithms import dynamic_group_admm
     from .parallel import topology as T
-    from .oracle.reference import opt_linear
 
     n = args.workers
-    ds = linear_synthetic(n)
-    Xf, yf = ds.stacked()
-    obj0 = opt_linear(Xf.numpy(), yf.numpy())
-    pl = T.Placement.contiguous(n, world)
-    local = pl.local_workers(rank)
-    m = LinearRegression(ds.X[local].to(device).contiguous(), ds.y[local].to(device).contiguous())
+    X_cpu, y_cpu, local, pl, obj0 = headline_rank_problem(n, rank, world)
+    d = int(X_cpu.shape[2])
+    m = LinearRegression(X_cpu.to(device).contiguous(), y_cpu.to(device).contiguous())
     p0, c0, _ = T.find_path(n, np.random.default_rng(5))
     rho, tol, coh = 1.0, 1e-4, 10
+    opts = {"state": False}
+    fabric = None
+    if world > 1:
+        from .parallel.xgmi import XgmiFabric
+        from .parallel.comm import RankInfo
+        ok = False
+        try:
+            fabric = XgmiFabric(n, d, 8, rank, world, device, table_slots=8)
+            ok = True
+        except Exception as e:
+            print("run_dgadmm[rank %d]: xgmi fabric unavailable: %s" % (rank, e))
+        t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64)
+        dist.all_reduce(t)
+        if float(t.item()) == 0.0:
+            opts["fabric"] = fabric
+            comm = RankInfo(rank, world)
+        else:
+            if fabric is not None:
+                fabric.close()
+            fabric = None
+            comm = rank_comm(args, world, device, comm, n, d, 16)
 
     def solve():
         return dynamic_group_admm(m, rho, obj0, tol, 3000, p0, c0, coh, seed=99, n_total=n, local_ids=local,
-                                  comm=comm, placement=pl)
+                                  comm=comm, placement=pl, engine_opts=opts)
 
     ms, r = _timed(solve, args.steps, args.warmup, device, world)
-    return {"metric": "wall-clock to 1e-4 objective gap, D-GADMM (findPath2 re-chaining every 10 iterations), "
-                      "linear regression (LinearRegression_Synthetic)",
-            "ms": ms, "iters": r.iters, "expected": None, "backend": r.extra.get("backend"),
-            "config": {"model": "LinearRegression_Synthetic D-GADMM closed-form", "workers": n,
-                       "features": ds.dim, "samples_per_worker": ds.rows_per_worker, "rho": rho, "coherence": coh,
-                       "tol": tol, "global_batch": n * ds.rows_per_worker, "seq_len": 1,
-                       "parallelism": "dynamic-chain%d-over-%dgpu" % (n, world)}}
+    out = {"metric": "wall-clock to 1e-4 objective gap, D-GADMM (findPath2 re-chaining every 10 iterations), "
+                     "linear regression (LinearRegression_Synthetic)",
+           "ms": ms, "iters": r.iters, "expected": None, "backend": r.extra.get("backend"),
+           "engine": r.extra.get("engine"), "transport": r.extra.get("transport"),
+           "theta_payload_bytes_per_solve": _sum_ranks(r.bytes_sent, world),
+           "wire_bytes_per_solve": _sum_ranks(r.extra.get("wire_bytes", 0), world),
+           "monitor_bytes_per_solve": _sum_ranks(r.extra.get("monitor_bytes", 0), world),
+           "config": {"model": "LinearRegression_Synthetic D-GADMM closed-form", "workers": n,
+                      "features": d, "samples_per_worker": int(X_cpu.shape[1]), "rho": rho, "coherence": coh,
+                      "tol": tol, "global_batch": n * int(X_cpu.shape[1]), "seq_len": 1,
+                      "parallelism": "dynamic-chain%d-over-%dgpu" % (n, world)}}
+    if fabric is not None:
+        fabric.close()
+    return out
+
+
+def _sum_ranks(v, world: int) -> int:
+    if world == 1:
+        return int(v)
+    t = torch.tensor([float(v)], dtype=torch.float64)
+    dist.all_reduce(t)
+    return int(t.item())
 
 
 def run_real10m(args, rank, world, device, comm) -> Dict:

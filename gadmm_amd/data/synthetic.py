@@ -96,24 +96,29 @@ def _top_eigvec(P: np.ndarray) -> np.ndarray:
 
 
 def _rank_one_dataset(num_workers: int, growth: float, seed: int, use_fixture: bool,
-                      name: str) -> ShardedDataset:
+                      name: str, worker_ids=None) -> ShardedDataset:
     basis = rank_one_basis(num_workers, 50, seed=seed, use_fixture=use_fixture)
     d = basis.P.shape[-1]
     eye = np.eye(d)
-    X = np.stack([growth ** n * basis.P[n] + eye for n in range(num_workers)])
-    y = np.broadcast_to(basis.y, (num_workers, basis.y.shape[0])).copy()
+    ids = list(range(num_workers)) if worker_ids is None else [int(w) for w in worker_ids]
+    X = np.stack([growth ** n * basis.P[n] + eye for n in ids])
+    y = np.broadcast_to(basis.y, (len(ids), basis.y.shape[0])).copy()
     return ShardedDataset(X=torch.from_numpy(X), y=torch.from_numpy(y), name=name,
-                          meta={"source": basis.source, "growth": growth})
+                          meta={"source": basis.source, "growth": growth, "worker_ids": ids,
+                                "num_workers_total": num_workers})
 
 
-def linear_synthetic(num_workers: int = 24, seed: int = 0, use_fixture: bool = True) -> ShardedDataset:
-    """E1/E5/E7 design: ``X_n = 1.3^(n-1) q_n q_n^T + I`` (LinearRegression_Synthetic.m:32)."""
-    return _rank_one_dataset(num_workers, 1.3, seed, use_fixture, "linear_synthetic")
+def linear_synthetic(num_workers: int = 24, seed: int = 0, use_fixture: bool = True,
+                     worker_ids=None) -> ShardedDataset:
+    """E1/E5/E7 design: ``X_n = 1.3^(n-1) q_n q_n^T + I`` (LinearRegression_Synthetic.m:32).
+    ``worker_ids``: build only these workers' shards (a rank materialises nothing else)."""
+    return _rank_one_dataset(num_workers, 1.3, seed, use_fixture, "linear_synthetic", worker_ids)
 
 
-def logistic_synthetic(num_workers: int = 24, seed: int = 0, use_fixture: bool = True) -> ShardedDataset:
+def logistic_synthetic(num_workers: int = 24, seed: int = 0, use_fixture: bool = True,
+                       worker_ids=None) -> ShardedDataset:
     """E3 design: ``X_n = q_n q_n^T + I`` with +-1 labels (LogisticRegression_Synthetic.m:31-35)."""
-    return _rank_one_dataset(num_workers, 1.0, seed, use_fixture, "logistic_synthetic")
+    return _rank_one_dataset(num_workers, 1.0, seed, use_fixture, "logistic_synthetic", worker_ids)
 
 
 def gaussian_regression(num_workers: int, rows_per_worker: int, dim: int, seed: int = 0,

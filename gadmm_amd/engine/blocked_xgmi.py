@@ -11,8 +11,10 @@ ring; rank 0's monitor pushes the stop decision into every rank's ring (as in th
 parallel/xgmi.py). Hand-offs are tagged granules salted per solve, so correctness never depends on
 timing; every spin has a deadline and a stalled peer surfaces as ``done == 4`` (callers fall back).
 
-Identity chain (the static GADMM of the headline benchmark); the halo workers' data must be
-available on the rank (the benchmark generates the full synthetic dataset on every rank).
+Identity chain (the static GADMM of the headline benchmark). NOT data-local: the halo workers' shards
+must be on the rank too (``replicated_shard_bytes``), and (theta, mu) travel instead of theta alone, so
+``bench.py`` runs it only on request (``--engine replicated-halo``); the data-local default is the
+per-worker persistent kernel on ``parallel/xgmi.py``.
 """
 from __future__ import annotations
 
@@ -187,10 +189,22 @@ class BlockedXgmiEngine:
         return c[2], c[1], (t1 - t0) * 1e3
 
     def exchange_bytes_per_solve(self, iters: int) -> int:
-        """Bytes this rank pushes over xGMI per solve: every k iterations, (theta, mu) of each owned
-        worker that a peer computes, to that peer."""
+        """Payload this rank pushes over xGMI per solve (8 B per double; the granules on the wire carry
+        16 B): every k iterations, (theta, mu) of each owned worker that a peer computes, to that peer."""
         pushes = sum(1 for lo, hi in self.peer_ranges for p in range(self.seg_lo, self.seg_hi + 1) if lo <= p <= hi)
         return pushes * 2 * self.d * 8 * (iters // self.k)
+
+    def monitor_bytes_per_solve(self, iters: int) -> int:
+        """Stop-rule wire bytes leaving this rank: one 16-B objective granule per owned worker per
+        iteration to rank 0's monitor (rank 0's own are local), and rank 0's 8-B decision to every
+        other rank per iteration."""
+        owned = self.seg_hi - self.seg_lo + 1
+        return iters * (owned * 16 if self.rank != 0 else 8 * (self.nranks - 1))
+
+    def replicated_shard_bytes(self) -> int:
+        """Bytes of OTHER ranks' shards this rank holds for its halo (X and y of the halo workers)."""
+        halo = (self.ext_hi - self.ext_lo + 1) - (self.seg_hi - self.seg_lo + 1)
+        return halo * int(self.X.shape[1]) * (self.d + 1) * 8
 
     def objective_trace(self, upto: int):
         return self.trace.cpu().numpy()[:upto]

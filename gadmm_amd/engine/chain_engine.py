@@ -27,6 +27,14 @@ from ..ops.linalg import gram, spd_inverse
 from ..parallel.topology import Placement, chain_plan, RankPlan
 
 
+class ResidencyError(RuntimeError):
+    """A persistent kernel's workgroups cannot all be resident on this device at once."""
+
+
+class HandoffTimeout(RuntimeError):
+    """A persistent kernel's hand-off spin passed its deadline (done == 4) on some workgroup."""
+
+
 @dataclass
 class EngineRun:
     iters: int
@@ -37,6 +45,7 @@ class EngineRun:
     p2p_bytes: int
     p2p_msgs: int
     monitor_bytes: int
+    wire_bytes: int = 0
 
     @property
     def converged(self) -> bool:
@@ -83,6 +92,8 @@ class NativeChainEngine:
         self.m = int(X_loc.shape[1])
         self.comm = comm
         self.nranks = 1 if comm is None else comm.nranks
+        # device-copy transport (parallel/ipc.py): replaces RCCL in the graph engine when present
+        self.xport = getattr(comm, "xport", None) if comm is not None else None
         if local_solver not in ("gd", "newton"):
             raise ValueError("unknown local solver %r" % local_solver)
         if local_solver == "newton" and (model != "logistic" or self.d > 64 or self.m > 64):
@@ -108,8 +119,13 @@ class NativeChainEngine:
             self.mu = torch.zeros((nl, d), dtype=f64, device=dev)
             self.objw = torch.zeros((nl,), dtype=f64, device=dev)
             self.trace = torch.full((self.max_iter,), float("nan"), dtype=f64, device=dev)
-            self.part = torch.zeros((self.ring,), dtype=f64, device=dev)
-            self.reduced = torch.zeros((self.ring,), dtype=f64, device=dev)
+            # multi-rank stop rule: per-worker objectives [ring][n_total] (gid-indexed, see gadmm_chain.h)
+            self.part = torch.zeros((self.ring * self.n_total,), dtype=f64, device=dev)
+            self.reduced = torch.zeros((self.ring * self.n_total,), dtype=f64, device=dev)
+            self.lgid = torch.tensor(self.local_ids, dtype=torch.int32, device=dev)
+            # real clock: s_memrealtime (100 MHz) of each iteration's decision, and of the solve start
+            self.tstamp = torch.zeros((self.max_iter,), dtype=torch.int64, device=dev)
+            self.t0stamp = torch.zeros((1,), dtype=torch.int64, device=dev)
             self.ctl = torch.zeros((8,), dtype=torch.int32, device=dev)
             self.slots = torch.zeros((max(2 * nl, 2) * 4,), dtype=torch.int32, device=dev)
             self.inner_iters = torch.zeros((max(nl, 1),), dtype=torch.int32, device=dev)
@@ -163,6 +179,9 @@ class NativeChainEngine:
         args.rbuf = native.ptr(self.rbuf)
         args.obj_mode = 0 if obj_mode == "exact" else 1
         args.solver = 1 if local_solver == "newton" else 0
+        args.n_total = self.n_total
+        args.lgid = self.lgid.data_ptr()
+        args.tstamp = self.tstamp.data_ptr()
         desc = native.EngineDesc()
         desc.base = args
         desc.d_slots = self.slots.data_ptr()
@@ -170,6 +189,7 @@ class NativeChainEngine:
         desc.comm = comm.handle if comm is not None else None
         desc.stream = self.stream.cuda_stream
         desc.nranks = self.nranks
+        desc.xport = self.xport
         self._desc = desc
         self.handle = self.lib.gadmm_chain_engine_create(ctypes.byref(desc))
         if not self.handle:
@@ -279,6 +299,9 @@ class NativeChainEngine:
         native.check(rc, "set_plan")
 
     def reset(self, start_iter: int = 1, pending: int = 0, zero_state: bool = True):
+        if self.xport:  # new solve: the transport's tags of the previous one stop matching (every rank)
+            native.check(self.lib.gadmm_ipc_new_epoch(self.xport, self.stream.cuda_stream), "ipc_new_epoch")
+        native.check(self.lib.gadmm_write_stamp(self.t0stamp.data_ptr(), self.stream.cuda_stream), "write_stamp")
         if zero_state:  # theta = mu = part = 0, trace = NaN and the control block: one launch
             native.check(self.lib.gadmm_chain_reset_state(
                 self.ctl.data_ptr(), int(start_iter), int(pending), self.theta.data_ptr(), self.theta.numel(),
@@ -304,18 +327,28 @@ class NativeChainEngine:
                                              ctypes.byref(st))
         native.check(rc, "chain_engine_run")
         return EngineRun(st.iters, st.done, st.iterations_launched, st.replays, st.wall_ms, st.p2p_bytes,
-                         st.p2p_msgs, st.monitor_bytes)
+                         st.p2p_msgs, st.monitor_bytes, st.wire_bytes)
 
     # ---------------------------------------------------------------------------------------------
     # Persistent single-launch solve (csrc/kernels/chain_persistent.hip)
+    def resident_capacity(self, dynamic: bool = False, sys_scope: bool = False) -> int:
+        """Workgroups of the per-worker persistent kernel this device can keep resident at once
+        (occupancy x CUs, ``GADMM_CU_BUDGET`` shrinks the CU count): a persistent launch needs all of
+        them together, so eligibility is decided here, up front, not by a spin deadline."""
+        pa = native.PersistArgs()
+        pa.d, pa.n, pa.nvar, pa.obj_mode = self.d, self.n_total, self.nvar, self._obj_mode(dynamic)
+        pa.n_epochs = 1 if dynamic else 0
+        pa.sys_scope = 1 if sys_scope else 0
+        return int(self.lib.gadmm_chain_persistent_capacity(ctypes.byref(pa)))
+
     def persistent_eligible(self, fabric=None) -> bool:
         if self.model != "linear" or self.plan is None or self.path is None:
             return False
         if self.nranks != 1 and fabric is None:
             return False
-        if self.n_local + 1 > 256:
+        if int(self.lib.gadmm_chain_persistent_lds(self.d, self._obj_mode())) <= 0:
             return False
-        return int(self.lib.gadmm_chain_persistent_lds(self.d, self._obj_mode())) > 0
+        return self.n_local + 1 <= self.resident_capacity(sys_scope=fabric is not None)
 
     def _obj_mode(self, dynamic: bool = False) -> int:
         # exact objective (second GEMV with the Gram in LDS) whenever both matrices fit in LDS
@@ -323,12 +356,18 @@ class NativeChainEngine:
             return 0 if int(self.lib.gadmm_chain_persistent_lds_dyn(self.d, 0, self.nvar)) > 0 else 1
         return 0 if int(self.lib.gadmm_chain_persistent_lds(self.d, 0)) > 0 else 1
 
-    def dynamic_eligible(self) -> bool:
-        """One-launch D-GADMM (per-epoch chains in device tables): one rank, linear, every degree's
-        inverse in LDS."""
-        if self.model != "linear" or self.nranks != 1 or self.n_local != self.n_total or self.n_local + 1 > 256:
+    def dynamic_eligible(self, fabric=None) -> bool:
+        """One-launch D-GADMM (per-epoch chains in device tables): linear, every degree's inverse
+        resident; several ranks need an xGMI fabric whose theta tables hold a ring of iteration slots."""
+        if self.model != "linear":
             return False
-        return int(self.lib.gadmm_chain_persistent_lds_dyn(self.d, self._obj_mode(True), self.nvar)) > 0
+        if self.nranks != 1 and (fabric is None or getattr(fabric, "table_slots", 1) < 2):
+            return False
+        if self.nranks == 1 and self.n_local != self.n_total:
+            return False
+        if int(self.lib.gadmm_chain_persistent_lds_dyn(self.d, self._obj_mode(True), self.nvar)) <= 0:
+            return False
+        return self.n_local + 1 <= self.resident_capacity(dynamic=True, sys_scope=fabric is not None)
 
     def blocked_plan(self, fabric=None, timeline: bool = False):
         """(k, L, W, pw) of the temporally blocked kernel for this engine, or None (multi-GPU, d > 64,
@@ -355,9 +394,11 @@ class NativeChainEngine:
         workgroup row is the monitor (column 0 = decision posted).
         ``epochs``: D-GADMM in one launch, a list of ``(first_iteration, path)`` or a pair of arrays
         ``(first_iterations (E,), paths (E, n))`` (the first epoch starts at ``start_iter``); every worker switches neighbours / role at each epoch start and flushes its
-        pending head dual with the old chain first (single rank only)."""
+        pending head dual with the old chain first. With a ``fabric`` (several GPUs) each worker also
+        pushes its theta to the ranks of its current and next-epoch neighbours (the fabric's theta
+        tables must hold ``table_slots >= lag + 4`` iteration slots)."""
         if epochs is not None:
-            if not self.dynamic_eligible():
+            if not self.dynamic_eligible(fabric):
                 raise RuntimeError("dynamic persistent kernel not eligible for this engine/config")
         elif not self.persistent_eligible(fabric):
             raise RuntimeError("persistent kernel not eligible for this engine/config")
@@ -391,6 +432,12 @@ class NativeChainEngine:
                     push = None
                     dec_push = torch.tensor([decg.data_ptr()], dtype=torch.int64, device=dev)
                     keep = (thg, objg, decg)
+                elif epochs is not None:
+                    # D-GADMM across GPUs: push targets change per epoch (ep_push masks below)
+                    if getattr(fabric, "table_slots", 1) < ring:
+                        raise RuntimeError("fabric theta tables hold %d slots, D-GADMM needs %d"
+                                           % (getattr(fabric, "table_slots", 1), ring))
+                    push = None
                 else:
                     owner = self._placement_owner
                     pl = []
@@ -399,10 +446,12 @@ class NativeChainEngine:
                         ps = [fabric.thg_peer[r] for r in peers] + [0, 0]
                         pl += ps[:2]
                     push = torch.tensor(pl, dtype=torch.int64, device=dev)
+                if fabric is not None:
                     ptrs = (fabric.thg.ptr.value, fabric.objg_mon, fabric.decg.ptr.value)
                     dec_push = torch.tensor(fabric.dec_all if fabric.dec_all else [0], dtype=torch.int64,
                                             device=dev)
-                    keep = ()
+                    keep = (torch.tensor(fabric.table_ptrs(), dtype=torch.int64, device=dev),) \
+                        if epochs is not None else ()
             self._pbuf = (key, slot_t, pos_t, ptrs, push, dec_push, keep, [0])
         _, slot_t, pos_t, ptrs, push, dec_push, keep, epoch_box = self._pbuf
         if fabric is not None:
@@ -430,6 +479,7 @@ class NativeChainEngine:
         pa.push = push.data_ptr() if push is not None else None
         pa.dec_push = dec_push.data_ptr()
         pa.trace, pa.ctl = self.trace.data_ptr(), self.ctl.data_ptr()
+        pa.tstamp = self.tstamp.data_ptr()
         ep_keep = None
         if epochs is not None:
             if isinstance(epochs, tuple) and len(epochs) == 2 and isinstance(epochs[1], np.ndarray):
@@ -463,8 +513,20 @@ class NativeChainEngine:
             # the three epoch tables go up in ONE async copy from a reused pinned staging buffer (three
             # pageable copies cost a blocking round trip each); the stream is synchronised after the
             # kernel, so the staging buffer is free again by the next solve
+            if fabric is not None:
+                # ranks each local worker pushes theta to in each epoch: its neighbours' owners
+                owner = np.asarray(self._placement_owner, dtype=np.int64)
+                sl4 = es.reshape(E, len(loc), 4)
+                mask = np.zeros((E, len(loc)), dtype=np.int64)
+                for col in (2, 3):
+                    nb = sl4[:, :, col].astype(np.int64)
+                    ow = np.where(nb >= 0, owner[np.maximum(nb, 0)], self.rank)
+                    mask |= np.where(ow != self.rank, np.left_shift(1, ow), 0)
+                pm = mask.astype(np.int32).reshape(-1)
+            else:
+                pm = np.zeros((0,), dtype=np.int32)
             ns, nes = len(starts), es.size
-            total = ns + nes + pp.size
+            total = ns + nes + pp.size + pm.size
             stage = getattr(self, "_ep_stage", None)
             if stage is None or stage[0].numel() < total:
                 cap = max(total, 4096)
@@ -474,13 +536,17 @@ class NativeChainEngine:
             host = stage[0].numpy()
             host[:ns] = starts
             host[ns:ns + nes] = es
-            host[ns + nes:total] = pp
+            host[ns + nes:ns + nes + pp.size] = pp
+            host[ns + nes + pp.size:total] = pm
             with torch.cuda.stream(self.stream):
                 stage[1][:total].copy_(stage[0][:total], non_blocking=True)
-            st_t, es_t, pp_t = stage[1][:ns], stage[1][ns:ns + nes], stage[1][ns + nes:total]
-            ep_keep = (st_t, es_t, pp_t)
+            st_t, es_t = stage[1][:ns], stage[1][ns:ns + nes]
+            pp_t, pm_t = stage[1][ns + nes:ns + nes + pp.size], stage[1][ns + nes + pp.size:total]
+            ep_keep = (st_t, es_t, pp_t, pm_t)
             pa.n_epochs = len(starts)
             pa.epoch_start, pa.ep_slots, pa.ep_pos = st_t.data_ptr(), es_t.data_ptr(), pp_t.data_ptr()
+            if fabric is not None:
+                pa.ep_push, pa.peer_thg = pm_t.data_ptr(), keep[0].data_ptr()
         tl = None
         if timeline_iters > 0:
             tl = torch.zeros((max(len(slots), 256) + 1, int(timeline_iters), 8), dtype=torch.int64, device=dev)
@@ -497,12 +563,19 @@ class NativeChainEngine:
                             if plan is not None else "per-worker")
         with torch.cuda.stream(self.stream):
             t0 = _time.perf_counter()
+            rc = None
             if plan is not None:
-                native.check(self.lib.gadmm_chain_blocked_launch(ctypes.byref(pa), self.stream.cuda_stream),
-                             "chain_blocked_launch")
-            else:
-                native.check(self.lib.gadmm_chain_persistent_launch(ctypes.byref(pa), self.stream.cuda_stream),
-                             "chain_persistent_launch")
+                rc = int(self.lib.gadmm_chain_blocked_launch(ctypes.byref(pa), self.stream.cuda_stream))
+                if rc == -2 and epochs is None:  # its workgroups cannot all be resident: the per-worker kernel
+                    plan, rc = None, None
+                    self.last_kernel = "per-worker"
+                else:
+                    native.check(rc, "chain_blocked_launch")
+            if plan is None:
+                rc = int(self.lib.gadmm_chain_persistent_launch(ctypes.byref(pa), self.stream.cuda_stream))
+                if rc == -2:
+                    raise ResidencyError(self.lib.gadmm_last_error().decode())
+                native.check(rc, "chain_persistent_launch")
             self.stream.synchronize()
             t1 = _time.perf_counter()
         self.last_timeline = tl.cpu().numpy() if tl is not None else None
@@ -510,8 +583,38 @@ class NativeChainEngine:
         c = self.ctl.cpu().tolist()
         done, conv, nxt = c[1], c[2], c[0]
         if done == 4:
-            raise RuntimeError("persistent chain kernel timed out (hand-off never completed)")
-        return EngineRun(conv, done, nxt - start_iter, 1, (t1 - t0) * 1e3, 0, 0, 0)
+            raise HandoffTimeout("persistent chain kernel timed out (hand-off never completed)")
+        p2p = msgs = mon = 0
+        if fabric is not None and conv >= start_iter:
+            # what this rank puts on xGMI for iterations start..conv (the reference's accounting; the
+            # lag iterations run past the decision are not counted): theta rows to remote owners of the
+            # neighbours, objective granules to the monitor rank, decisions from the monitor rank
+            ran = conv - start_iter + 1
+            if epochs is None:
+                owner = self._placement_owner
+                per_it = sum(len({int(owner[u]) for u in (s.left, s.right) if u >= 0} - {self.rank}) for s in slots)
+                msgs = per_it * ran
+            else:
+                js = np.arange(start_iter, conv + 1)
+                e_of = np.searchsorted(starts, js, side="right") - 1
+                m = mask[e_of]                                                  # (ran, n_local)
+                nxt_e = np.minimum(e_of + 1, E - 1)
+                starts_next = np.where(e_of + 1 < E, starts[nxt_e], -1)
+                m = np.where((js + 1 == starts_next)[:, None], m | mask[nxt_e], m)
+                msgs = int(sum(bin(int(v)).count("1") for v in m.reshape(-1)))
+            p2p = msgs * self.d * 8
+            mon = ran * (len(slots) * 16 if self.rank != 0 else 8 * (self.nranks - 1))
+        return EngineRun(conv, done, nxt - start_iter, 1, (t1 - t0) * 1e3, p2p, msgs, mon, 2 * p2p)
+
+    def time_trace(self, upto: int) -> np.ndarray:
+        """Measured clock of the last solve: seconds from the solve start (``reset``) to the decision
+        of each iteration (s_memrealtime, 100 MHz, stamped by the monitor / the iteration's finish on
+        the device). Zero where this rank recorded no decision (non-monitor ranks of the xGMI fabric)."""
+        if upto <= 0:
+            return np.zeros((0,), dtype=np.float64)
+        t = self.tstamp[:upto].cpu().numpy().astype(np.int64)
+        t0 = int(self.t0stamp.cpu().item())
+        return np.where(t > 0, (t - t0) * 1e-8, 0.0)
 
     def graph_ok(self) -> bool:
         return bool(self.lib.gadmm_chain_engine_graph_ok(self.handle))

@@ -1,0 +1,200 @@
+"""One GADMM chain over several MI355X (one process per GPU): engine choice, byte accounting and the
+collective fallback. Used by ``bench.py`` and the multi-rank tests.
+
+Data-local by construction: the solver is given only this rank's shards (``X_loc``) and ships only
+theta, to the ranks of its chain neighbours (group_ADMM_closedForm.m:18-27, 62-70). Engines, in the
+order ``engine="auto"`` tries them:
+
+1. ``xgmi`` -- the per-worker persistent kernel (chain_persistent.hip, SYS scope): one workgroup per
+   local worker, boundary theta stored straight into the neighbour GPU's table over xGMI, objective
+   granules to rank 0's monitor, decisions fanned back out. One launch per solve.
+2. ``rccl`` / ``ipc`` -- the graph-replayed phase kernels (chain_engine.cpp) with RCCL send/recv, or
+   with the device-copy transport (parallel/ipc.py; the only option when ranks share one GPU).
+
+Every choice is agreed by all ranks (an all-reduce of a success flag), and so is every fallback: a
+solve that fails on ANY rank (a stalled hand-off reaches its deadline: ``done == 4``) makes every
+rank drop the persistent kernel and continue on the graph engine together.
+
+``engine="replicated-halo"`` is the opt-in temporally blocked kernel across GPUs
+(engine/blocked_xgmi.py): it needs the halo workers' shards (``halo_data``) and is reported as such.
+"""
+from __future__ import annotations
+
+import sys
+import time
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class SolveOut:
+    iters: int
+    done: int
+    theta_bytes: int   # payload, 8 B per double
+    wire_bytes: int    # on the fabric (granules: 16 B per double)
+    monitor_bytes: int
+
+
+def all_ok(flag: bool, world: int) -> bool:
+    if world == 1:
+        return flag
+    t = torch.tensor([0.0 if flag else 1.0], dtype=torch.float64)
+    dist.all_reduce(t)
+    return float(t.item()) == 0.0
+
+
+class DistributedChainSolver:
+    def __init__(self, X_loc: torch.Tensor, y_loc: torch.Tensor, local: Sequence[int], n_total: int, placement,
+                 rank: int, world: int, device: torch.device, rho: float, obj0: float, tol: float,
+                 max_iter: int = 20000, engine: str = "auto", fabric: str = "auto", share: bool = False,
+                 block: int = 0, halo_data=None, timeout_s: float = 20.0, use_graph: bool = True):
+        from .chain_engine import NativeChainEngine
+
+        self.X, self.y = X_loc, y_loc
+        self.local = [int(w) for w in local]
+        self.n, self.placement, self.rank, self.world, self.device = n_total, placement, rank, world, device
+        self.rho, self.obj0, self.tol, self.max_iter = rho, obj0, tol, max_iter
+        self.share, self.fabric_req, self.timeout_s, self.use_graph = share, fabric, timeout_s, use_graph
+        self.block = block if block > 0 else (32 if world == 1 else 16)
+        self.d = int(X_loc.shape[2])
+        self.path = list(range(n_total))
+        self.eng = self.comm = self.fab = self.blk = None
+        self.kind, self.persistent, self.replicated_bytes = "local", False, 0
+        self.fallbacks = []
+        self.delay_next_s = 0.0  # test hook: sleep before the next launch (a slow / stalled peer)
+        self._NCE = NativeChainEngine
+        if world == 1:
+            self.eng = self._engine(None)
+            self.persistent = engine in ("auto", "persistent") and self.eng.persistent_eligible()
+        elif engine == "replicated-halo":
+            from .blocked_xgmi import BlockedXgmiEngine
+            if halo_data is None:
+                raise ValueError("replicated-halo needs the halo workers' shards (halo_data=(X_all, y_all))")
+            self.blk = BlockedXgmiEngine(halo_data[0], halo_data[1], n_total, placement, rank, rho, obj0, tol,
+                                         max_iter, device)
+            self.replicated_bytes = self.blk.replicated_shard_bytes()
+            self.persistent, self.kind = True, "xgmi(replicated-halo)"
+        else:
+            if fabric in ("auto", "xgmi") and engine != "graph":
+                self._try_xgmi()
+            if self.eng is None:
+                self._graph_engine()
+
+    # ---------------------------------------------------------------------------------------------
+    def _engine(self, comm):
+        e = self._NCE(self.X, self.y, self.local, self.n, "linear", rho=self.rho, obj0=self.obj0, tol=self.tol,
+                      max_iter=self.max_iter, comm=comm, block=self.block)
+        e.set_path(self.path, self.placement, self.rank)
+        return e
+
+    def _try_xgmi(self):
+        from ..parallel.comm import RankInfo
+        from ..parallel.xgmi import XgmiFabric
+
+        ok, err = False, ""
+        eng = self._engine(RankInfo(self.rank, self.world))
+        try:
+            need = sorted({int(self.placement.owner[u]) for w in self.local for u in (w - 1, w + 1)
+                           if 0 <= u < self.n} - {self.rank})
+            self.fab = XgmiFabric(self.n, self.d, 8, self.rank, self.world, self.device, peers_needed=need)
+            ok = eng.persistent_eligible(self.fab)
+            err = "" if ok else "persistent kernel not eligible (residency)"
+        except Exception as e:
+            err = str(e)
+        if all_ok(ok, self.world):
+            self.eng, self.persistent, self.kind = eng, True, "xgmi"
+            return
+        if self.rank == 0:
+            print("DistributedChainSolver: xgmi fabric unavailable (%s); graph engine" % (err or "another rank"),
+                  file=sys.stderr)
+        if self.fab is not None:
+            self.fab.close()
+        self.fab = None
+        eng.close()
+
+    def _graph_engine(self):
+        if self.fabric_req == "ipc" or self.share:
+            from ..parallel.ipc import IpcComm
+            self.comm = IpcComm(self.n, self.d, self.block, self.device, timeout_s=self.timeout_s)
+            self.kind = "ipc"
+        else:
+            from ..parallel.comm import RcclComm
+            self.comm = RcclComm(self.device)
+            self.kind = "rccl"
+        self.eng = self._engine(self.comm)
+        self.persistent = False
+
+    def fall_back(self, why: str):
+        """Collective: every rank drops the persistent kernel for the graph engine."""
+        self.fallbacks.append(why)
+        if self.blk is not None:
+            self.blk.close()
+            self.blk = None
+        if self.fab is not None:
+            self.fab.close()
+            self.fab = None
+        if self.eng is not None:
+            self.eng.close()
+            self.eng = None
+        self._graph_engine()
+
+    # ---------------------------------------------------------------------------------------------
+    def solve(self) -> SolveOut:
+        """One solve from the raw shards (Gram, inverses, iterations). Raises on a stalled hand-off."""
+        if self.delay_next_s > 0:
+            time.sleep(self.delay_next_s)
+            self.delay_next_s = 0.0
+        if self.blk is not None:
+            self.blk.refresh()
+            it, done, _ = self.blk.run(timeout_s=self.timeout_s)
+            pay = self.blk.exchange_bytes_per_solve(it)
+            return SolveOut(it, done, pay, 2 * pay, self.blk.monitor_bytes_per_solve(it))
+        self.eng.refresh(self.X, self.y)
+        self.eng.reset()
+        if self.persistent:
+            r = self.eng.run_persistent(fabric=self.fab, timeout_s=self.timeout_s)
+        else:
+            r = self.eng.run(use_graph=self.use_graph)
+        return SolveOut(r.iters, r.done, r.p2p_bytes, r.wire_bytes, r.monitor_bytes)
+
+    def guarded_solve(self) -> SolveOut:
+        try:
+            return self.solve()
+        except RuntimeError as e:
+            print("DistributedChainSolver[rank %d]: %s" % (self.rank, e), file=sys.stderr)
+            return SolveOut(0, 4, 0, 0, 0)
+
+    def solve_agreed(self) -> SolveOut:
+        """Solve; if it failed on any rank while a persistent kernel was in use, every rank falls back
+        to the graph engine and solves again. Collective."""
+        out = self.guarded_solve()
+        if all_ok(out.done == 1, self.world):
+            return out
+        if self.world > 1 and self.persistent:
+            self.fall_back("persistent solve failed on some rank (done=%d here)" % out.done)
+            out = self.guarded_solve()
+        return out
+
+    # ---------------------------------------------------------------------------------------------
+    @property
+    def kernel(self) -> Optional[str]:
+        if not self.persistent:
+            return None
+        return self.blk.last_kernel if self.blk is not None else getattr(self.eng, "last_kernel", None)
+
+    def engine_name(self) -> str:
+        if self.persistent:
+            return "persistent"
+        return "graph" if (self.eng is not None and self.eng.graph_ok() and self.use_graph) else "eager"
+
+    def objective_trace(self, iters: int):
+        return self.blk.objective_trace(iters) if self.blk is not None else self.eng.objective_trace(iters)
+
+    def close(self):
+        for o in (self.eng, self.blk, self.fab, self.comm):
+            if o is not None:
+                o.close()
+        self.eng = self.blk = self.fab = self.comm = None

@@ -54,12 +54,13 @@ class PhaseArgs(ctypes.Structure):
         ("lam", c_double), ("step", c_double), ("inner_tol", c_double),
         ("inner_iters", c_void_p),
         ("rbuf", c_void_p), ("obj_mode", c_int), ("solver", c_int),
+        ("n_total", c_int), ("pad_nt", c_int), ("lgid", c_void_p), ("tstamp", c_void_p),
     ]
 
 
 class EngineDesc(ctypes.Structure):
     _fields_ = [("base", PhaseArgs), ("d_slots", c_void_p), ("reduced", c_void_p), ("comm", c_void_p),
-                ("stream", c_void_p), ("nranks", c_int)]
+                ("stream", c_void_p), ("nranks", c_int), ("xport", c_void_p)]
 
 
 class FoCtl(ctypes.Structure):
@@ -85,7 +86,7 @@ class FoArgs(ctypes.Structure):
 class RunStats(ctypes.Structure):
     _fields_ = [("iters", c_int), ("done", c_int), ("iterations_launched", c_int), ("replays", c_int),
                 ("wall_ms", c_double), ("p2p_bytes", c_longlong), ("p2p_msgs", c_longlong),
-                ("monitor_bytes", c_longlong)]
+                ("monitor_bytes", c_longlong), ("wire_bytes", c_longlong)]
 
 
 class PersistArgs(ctypes.Structure):
@@ -102,6 +103,7 @@ class PersistArgs(ctypes.Structure):
         ("blk_tab", c_void_p), ("epoch_start", c_void_p), ("ep_slots", c_void_p), ("ep_pos", c_void_p),
         ("seg_lo", c_int), ("seg_hi", c_int), ("blk_npeer", c_int), ("dbg", c_int),
         ("blk_peer_lo", c_int * 8), ("blk_peer_hi", c_int * 8), ("blk_peer_tab", c_void_p),
+        ("tstamp", c_void_p), ("ep_push", c_void_p), ("peer_thg", c_void_p),
     ]
 
 
@@ -145,6 +147,13 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_xgmi_free": (c_int, [c_void_p]),
         "gadmm_device_can_access_peer": (c_int, [c_int, c_int]),
         "gadmm_chain_persistent_launch": (c_int, [ctypes.POINTER(PersistArgs), c_void_p]),
+        "gadmm_chain_persistent_capacity": (c_long, [ctypes.POINTER(PersistArgs)]),
+        "gadmm_write_stamp": (c_int, [c_void_p, c_void_p]),
+        "gadmm_ipc_box_bytes": (c_long, [c_int, c_int, c_int]),
+        "gadmm_ipc_xport_create": (c_void_p, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_double]),
+        "gadmm_ipc_xport_destroy": (c_int, [c_void_p]),
+        "gadmm_ipc_new_epoch": (c_int, [c_void_p, c_void_p]),
+        "gadmm_ipc_counters": (c_int, [c_void_p, ctypes.POINTER(c_longlong)]),
         "gadmm_chain_blocked_plan": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
         "gadmm_chain_blocked_plan2": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
                                               ctypes.POINTER(c_int)]),

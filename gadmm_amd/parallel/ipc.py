@@ -1,0 +1,130 @@
+"""Device-copy transport for the graph-replayed chain engine (``csrc/kernels/ipc_xport.hip``).
+
+The native chain engine exchanges boundary theta rows after every phase and reduces the per-worker
+objective ring at every block end. ``RcclComm`` does that with ncclSend/ncclRecv/ncclAllReduce;
+``IpcComm`` does it with two small kernels over IPC-mapped fine-grained mailboxes (one per rank):
+a sender stores its row as tagged 16-byte granules straight into the receiver's mailbox, and the
+receiver's kernel polls its own mailbox and copies the row into its theta table. Both are plain
+kernels, so the exchange is captured in the engine's hipGraph like the RCCL calls are.
+
+Why it exists:
+* RCCL refuses two ranks on one device, so the engine's multi-rank code (chain plans, ghost rows,
+  the objective ring and monitor, D-GADMM re-plans, logistic across ranks) could never run on a
+  one-GPU box. With this transport it runs with 2..16 processes sharing one MI355X.
+* On a node it is an RCCL-free data plane between graph-replayed phases (every MI355X pair is one
+  xGMI hop; the stores go straight over the link).
+
+Handles travel over the gloo control plane, like ``parallel/xgmi.py``.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops import native
+from .comm import Comm
+from .xgmi import _Buf
+
+
+class IpcTransport:
+    """This rank's mailbox + every peer's mapped mailbox + the native transport handle.
+    Collective over ``group``; a failure on any rank raises on every rank."""
+
+    def __init__(self, n_total: int, d: int, ring: int, rank: int, nranks: int, device: torch.device,
+                 group=None, timeout_s: float = 20.0):
+        self.lib = native.require()
+        self.rank, self.nranks = rank, nranks
+        self.n_total, self.d, self.ring = int(n_total), int(d), int(ring)
+        self.opened: List[ctypes.c_void_p] = []
+        self.box: Optional[_Buf] = None
+        self.handle = None
+        torch.cuda.set_device(device)
+        err, mine = "", None
+        try:
+            self.box = _Buf(self.lib, int(self.lib.gadmm_ipc_box_bytes(self.n_total, self.d, self.ring)))
+            mine = bytes(self.box.handle.raw)
+        except Exception as e:  # pragma: no cover - box dependent
+            err = "rank %d mailbox: %s" % (rank, e)
+        allh = [None] * nranks
+        dist.all_gather_object(allh, (mine, err), group=group)
+        errs = [e for _, e in allh if e]
+        ptrs: List[int] = []
+        if not errs:
+            try:
+                for r, (h, _) in enumerate(allh):
+                    if r == rank:
+                        ptrs.append(self.box.ptr.value)
+                    else:
+                        p = ctypes.c_void_p()
+                        native.check(self.lib.gadmm_xgmi_open(ctypes.create_string_buffer(h, 64), ctypes.byref(p)),
+                                     "ipc open mailbox of rank %d" % r)
+                        self.opened.append(p)
+                        ptrs.append(p.value)
+                arr = (ctypes.c_void_p * nranks)(*ptrs)
+                self.handle = self.lib.gadmm_ipc_xport_create(rank, nranks, self.d, self.n_total, self.ring,
+                                                              self.box.ptr, arr, float(timeout_s))
+                if not self.handle:
+                    native.check(-1, "ipc_xport_create")
+            except Exception as e:
+                errs.append(str(e))
+        flag = torch.tensor([1.0 if errs else 0.0], dtype=torch.float64)
+        dist.all_reduce(flag, group=group)
+        if float(flag.item()) != 0.0:
+            self.close()
+            raise RuntimeError("ipc transport: %s" % ("; ".join(errs) or "failed on another rank"))
+
+    def counters(self) -> dict:
+        out = (ctypes.c_longlong * 4)()
+        self.lib.gadmm_ipc_counters(self.handle, out)
+        return {"payload_bytes": out[0], "wire_bytes": out[1], "msgs": out[2], "obj_wire_bytes": out[3]}
+
+    def close(self):
+        if self.handle:
+            self.lib.gadmm_ipc_xport_destroy(self.handle)
+            self.handle = None
+        for p in self.opened:
+            self.lib.gadmm_xgmi_close(p)
+        self.opened = []
+        if self.box is not None:
+            self.box.free()
+            self.box = None
+
+
+class IpcComm(Comm):
+    """Rank identity + the device-copy transport, for ``NativeChainEngine(comm=...)`` /
+    ``chain_admm(..., comm=...)``. Control-plane helpers (barrier, max) go over gloo."""
+
+    backend = "ipc"
+
+    def __init__(self, n_total: int, d: int, ring: int, device: torch.device, group=None, timeout_s: float = 20.0):
+        super().__init__()
+        self.group = group
+        self.control_group = group
+        self.rank = dist.get_rank(group)
+        self.nranks = dist.get_world_size(group)
+        self.device = torch.device(device)
+        self.transport = IpcTransport(n_total, d, ring, self.rank, self.nranks, self.device, group, timeout_s)
+        self.handle = None          # no RCCL communicator
+        self.xport = self.transport.handle
+
+    def barrier(self):
+        torch.cuda.synchronize(self.device)
+        dist.barrier(group=self.group)
+
+    def _allreduce_max(self, t):
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+        return t
+
+    def allreduce_sum(self, t):  # one-time set-up only (oracles); the hot path never comes here
+        h = t.detach().cpu()
+        dist.all_reduce(h, group=self.group)
+        t.copy_(h)
+        self.stats.coll_bytes += t.numel() * t.element_size()
+        return t
+
+    def close(self):
+        self.transport.close()
+        self.xport = None

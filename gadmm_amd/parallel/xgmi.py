@@ -41,23 +41,26 @@ class _Buf:
 class XgmiFabric:
     """Per-rank granule buffers + the peers' mapped buffers.
 
-    theta table: (N, d) x 16-B granules on every rank; objective ring: (ring, N) x 16 B (read on the
-    monitor rank 0); decision ring: ring x 8 B on every rank."""
+    theta table: (table_slots, N, d) x 16-B granules on every rank (one slot for static chains; a ring
+    of iteration slots for D-GADMM, whose hand-offs change peers at every re-chain); objective ring:
+    (ring, N) x 16 B (read on the monitor rank 0); decision ring: ring x 8 B on every rank."""
 
     def __init__(self, n_total: int, d: int, ring: int, rank: int, nranks: int, device: torch.device,
-                 group=None, peers_needed: Optional[List[int]] = None):
+                 group=None, peers_needed: Optional[List[int]] = None, table_slots: int = 1):
         """Collective over ``group``: every rank must call it. Failures on any rank are raised on
-        every rank (so callers can fall back together)."""
+        every rank (so callers can fall back together). ``peers_needed``: ranks whose theta table
+        this rank writes into (default: all; D-GADMM needs all, any pair can become neighbours)."""
         self.lib = native.require()
         self.rank, self.nranks, self.device = rank, nranks, device
         self.n, self.d, self.ring = n_total, d, ring
+        self.table_slots = int(table_slots)
         self.opened: Dict[tuple, ctypes.c_void_p] = {}
         self.thg = self.objg = self.decg = None
         torch.cuda.set_device(device)
         mine = None
         err = ""
         try:
-            self.thg = _Buf(self.lib, n_total * d * 16)
+            self.thg = _Buf(self.lib, self.table_slots * n_total * d * 16)
             self.objg = _Buf(self.lib, ring * n_total * 16)
             self.decg = _Buf(self.lib, ring * 8)
             mine = (bytes(self.thg.handle.raw), bytes(self.objg.handle.raw), bytes(self.decg.handle.raw))
@@ -97,6 +100,12 @@ class XgmiFabric:
                      "xgmi_open %s" % (key,))
         self.opened[key] = p
         return p.value
+
+    def table_ptrs(self) -> List[int]:
+        """Every rank's theta table (own included) by rank: the D-GADMM push targets."""
+        if len(self.thg_peer) != self.nranks - 1:
+            raise RuntimeError("fabric was built for a subset of peers; D-GADMM needs peers_needed=None")
+        return [self.thg.ptr.value if r == self.rank else self.thg_peer[r] for r in range(self.nranks)]
 
     def next_epoch(self) -> int:
         self.epoch = (self.epoch + 1) % 4095 + 1

@@ -1,0 +1,250 @@
+"""Multi-rank native paths rehearsed with several processes sharing the single MI355X of the test box.
+
+* the graph-replayed engine (chain_engine.cpp) with the IPC device-copy transport: its multi-rank
+  code -- chain plans, ghost rows, the per-worker objective ring, the block-end monitor, D-GADMM
+  re-plans, logistic across ranks -- bit-identical to one rank (RCCL refuses two ranks per device,
+  so only the ncclSend/ncclRecv/ncclAllReduce calls themselves are not exercised here);
+* the data-local multi-GPU default (per-worker persistent kernel on the xGMI fabric): exact bytes;
+* multi-rank D-GADMM in one persistent launch per GPU;
+* residency checks and the collective fallback after a stalled peer.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _single(lin24, rho, tol, **opts):
+    import torch
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import chain_admm
+    m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
+    return chain_admm(m, list(range(24)), 24, rho, _obj0(24), tol, 3000, engine_opts=dict(cache=False, **opts))
+
+
+def _obj0(n):
+    from gadmm_amd.benchmarks import headline_rank_problem
+    return headline_rank_problem(n, 0, 1)[4]
+
+
+# ------------------------------------------------------------------------------------------------
+def _ipc_linear_rank(rank, world, n, rho, tol):
+    import torch
+    from gadmm_amd.benchmarks import headline_rank_problem
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import chain_admm
+    from gadmm_amd.parallel.ipc import IpcComm
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    X, y, loc, pl, obj0 = headline_rank_problem(n, rank, world)
+    comm = IpcComm(n, 50, 16, dev)
+    m = LinearRegression(X.to(dev), y.to(dev))
+    out = []
+    for _ in range(2):  # repeated solves: epoch-salted tags, no mailbox re-zeroing
+        r = chain_admm(m, loc, n, rho, obj0, tol, 3000, comm=comm, placement=pl,
+                       engine_opts={"persistent": False, "state": False})
+        out.append((r.iters, r.converged, r.extra["engine"], r.bytes_sent, r.extra["wire_bytes"]))
+    res = {"runs": out, "trace": r.obj.tolist(), "times": r.time_trace.tolist(),
+           "theta": r.extra["engine_obj"].local_theta().cpu().numpy(), "local": loc}
+    r.extra["engine_obj"].close()
+    comm.close()
+    return res
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_ipc_transport_graph_engine_bit_identical(world, lin24):
+    """Graph engine + IPC transport on 2 / 4 processes == the one-rank graph engine, bit for bit."""
+    from gadmm_amd.parallel.launch import spawn
+    res = spawn(_ipc_linear_rank, world, 24, 3.0, 1e-8, timeout=300)
+    single = _single(lin24, 3.0, 1e-8, persistent=False)
+    assert single.iters == 1373
+    for r in res:
+        assert all(it == 1373 and conv and eng == "graph" for it, conv, eng, _, _ in r["runs"]), r["runs"]
+        assert np.array_equal(np.asarray(r["trace"]), single.obj)
+        # data-local chain: each boundary rank sends one d-row per phase over each boundary it has
+        nb = (r["local"][0] > 0) + (r["local"][-1] < 23)
+        assert r["runs"][-1][3] == nb * 50 * 8 * 1373
+        assert r["runs"][-1][4] == 2 * r["runs"][-1][3]  # granules: 16 B per double
+    th = np.concatenate([r["theta"] for r in res])
+    ref = single.extra["engine_obj"].local_theta().cpu().numpy()
+    assert np.array_equal(th, ref)
+    times = np.asarray(res[0]["times"])
+    assert times.shape == (1373,) and np.all(np.diff(times) >= 0) and times[-1] > 0  # measured device clock
+
+
+def _ipc_logistic_rank(rank, world, n):
+    import torch
+    from gadmm_amd.data import logistic_synthetic
+    from gadmm_amd.models import LogisticRegression
+    from gadmm_amd.algorithms import chain_admm
+    from gadmm_amd.parallel.ipc import IpcComm
+    from gadmm_amd.parallel.topology import Placement
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    pl = Placement.contiguous(n, world)
+    loc = pl.local_workers(rank)
+    ds = logistic_synthetic(n, worker_ids=loc)
+    comm = IpcComm(n, 50, 8, dev)
+    m = LogisticRegression(ds.X.to(dev), ds.y.to(dev), lam=1e-5)
+    obj0 = m.optimum(comm, n_total=n)
+    r = chain_admm(m, loc, n, 2e-4, obj0, 1e-4, 400, comm=comm, placement=pl, local_solver="gd", step=2.2,
+                   engine_opts={"block": 8, "state": False})
+    out = {"iters": r.iters, "trace": r.obj.tolist(), "obj0": obj0}
+    r.extra["engine_obj"].close()
+    comm.close()
+    return out
+
+
+def test_ipc_transport_logistic_two_ranks(log24):
+    """Logistic GADMM (inner-GD HIP kernel) across two processes == one rank."""
+    from gadmm_amd.parallel.launch import spawn
+    from gadmm_amd.models import LogisticRegression
+    from gadmm_amd.algorithms import chain_admm
+    res = spawn(_ipc_logistic_rank, 2, 24, timeout=300)
+    m = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
+    obj0 = res[0]["obj0"]
+    single = chain_admm(m, list(range(24)), 24, 2e-4, obj0, 1e-4, 400, local_solver="gd", step=2.2,
+                        engine_opts={"block": 8, "cache": False})
+    assert single.iters == 53
+    for r in res:
+        assert r["iters"] == 53
+        assert np.array_equal(np.asarray(r["trace"]), single.obj)
+
+
+def _dgadmm_rank(rank, world, n, mode):
+    import torch
+    from gadmm_amd.benchmarks import headline_rank_problem
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import dynamic_group_admm
+    from gadmm_amd.parallel import topology as T
+    from gadmm_amd.parallel.comm import RankInfo
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    X, y, loc, pl, obj0 = headline_rank_problem(n, rank, world)
+    m = LinearRegression(X.to(dev), y.to(dev))
+    p0, c0, _ = T.find_path(n, np.random.default_rng(5))
+    fab = comm = None
+    if mode == "xgmi":
+        from gadmm_amd.parallel.xgmi import XgmiFabric
+        fab = XgmiFabric(n, 50, 8, rank, world, dev, table_slots=8)
+        comm = RankInfo(rank, world)
+        opts = {"fabric": fab, "state": False}
+    else:
+        from gadmm_amd.parallel.ipc import IpcComm
+        comm = IpcComm(n, 50, 16, dev)
+        opts = {"persistent": False, "state": False}
+    outs = []
+    for _ in range(2):
+        r = dynamic_group_admm(m, 1.0, obj0, 1e-4, 3000, p0, c0, 10, seed=99, n_total=n, local_ids=loc, comm=comm,
+                               placement=pl, engine_opts=opts)
+        outs.append((r.iters, r.converged, r.extra["engine"], r.bytes_sent))
+    res = {"runs": outs, "trace": r.obj.tolist(), "com_cost": np.asarray(r.com_cost).tolist()}
+    r.extra["engine_obj"].close()
+    if fab is not None:
+        fab.close()
+    if hasattr(comm, "transport"):
+        comm.close()
+    return res
+
+
+@pytest.mark.parametrize("world,mode", [(2, "ipc"), (2, "xgmi"), (4, "xgmi")])
+def test_dgadmm_multirank_matches_one_gpu(world, mode, lin24):
+    """D-GADMM across ranks -- epoch-by-epoch graph engine on the IPC transport, or ONE persistent launch
+    per GPU on the xGMI fabric (theta pushed to current and next-epoch neighbours' GPUs) -- equals the
+    one-GPU persistent-dynamic solve: iterations, objective trace (bit for bit) and energy trace."""
+    from gadmm_amd.parallel.launch import spawn
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import dynamic_group_admm
+    from gadmm_amd.parallel import topology as T
+    m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
+    p0, c0, _ = T.find_path(24, np.random.default_rng(5))
+    one = dynamic_group_admm(m, 1.0, _obj0(24), 1e-4, 3000, p0, c0, 10, seed=99)
+    assert one.extra["engine"] == "persistent-dynamic"
+    res = spawn(_dgadmm_rank, world, 24, mode, timeout=300)
+    want = "persistent-dynamic" if mode == "xgmi" else "epochs"
+    for r in res:
+        for it, conv, eng, _ in r["runs"]:
+            assert it == one.iters and conv and eng == want
+        assert np.array_equal(np.asarray(r["trace"]), one.obj)
+        assert np.allclose(np.asarray(r["com_cost"]), one.com_cost, rtol=1e-14)
+    assert sum(r["runs"][-1][3] for r in res) > 0  # theta crossed ranks
+
+
+# ------------------------------------------------------------------------------------------------
+def _solver_rank(rank, world, n, delay_rank, timeout_s):
+    import torch
+    from gadmm_amd.benchmarks import headline_rank_problem
+    from gadmm_amd.engine.multigpu import DistributedChainSolver
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    X, y, loc, pl, obj0 = headline_rank_problem(n, rank, world)
+    sol = DistributedChainSolver(X.to(dev), y.to(dev), loc, n, pl, rank, world, dev, 3.0, obj0, 1e-8, share=True,
+                                 timeout_s=timeout_s)
+    kind0 = sol.kind
+    if rank == delay_rank:
+        sol.delay_next_s = 3.0 * timeout_s  # this rank's kernel starts long after its peers gave up
+    outs = [sol.solve_agreed() for _ in range(2)]
+    res = {"kind0": kind0, "kind": sol.kind, "fallbacks": sol.fallbacks, "local": loc,
+           "outs": [(o.iters, o.done, o.theta_bytes, o.wire_bytes, o.monitor_bytes) for o in outs],
+           "trace": sol.objective_trace(outs[-1].iters).tolist() if rank == 0 else None}
+    sol.close()
+    return res
+
+
+@pytest.mark.parametrize("world,n", [(2, 24), (4, 24), (4, 8), (8, 8)])
+def test_data_local_xgmi_default_exact_bytes(world, n, lin24):
+    """The multi-GPU default: per-worker persistent kernel, each rank holding only its shards and
+    shipping only theta. Payload == 2 (N_ranks - 1) d 8 iters exactly; wire == 2 x payload (16-B
+    granules); iterations and trace == one GPU. n = 8 on 8 ranks: each GPU is one worker."""
+    from gadmm_amd.parallel.launch import spawn
+    from gadmm_amd.benchmarks import EXPECTED_ITERS_1E8
+    res = spawn(_solver_rank, world, n, -1, 20.0, timeout=300)
+    it = EXPECTED_ITERS_1E8[(n, 3.0)]
+    for r in res:
+        assert r["kind0"] == "xgmi" and r["kind"] == "xgmi" and not r["fallbacks"]
+        for o in r["outs"]:
+            assert o[0] == it and o[1] == 1
+    pay = sum(r["outs"][-1][2] for r in res)
+    assert pay == 2 * (world - 1) * 50 * 8 * it
+    assert sum(r["outs"][-1][3] for r in res) == 2 * pay
+    assert sum(r["outs"][-1][4] for r in res) > 0
+    if n == 24:
+        single = _single(lin24, 3.0, 1e-8)
+        assert np.array_equal(np.asarray(res[0]["trace"]), single.obj)
+
+
+def test_stalled_peer_every_rank_falls_back_together():
+    """Rank 1's persistent kernel starts after rank 0's hand-off deadline: both see done == 4, agree,
+    drop the xGMI kernel for the graph engine (IPC transport) together and still converge exactly."""
+    from gadmm_amd.parallel.launch import spawn
+    res = spawn(_solver_rank, 2, 24, 1, 2.0, timeout=300)
+    for r in res:
+        assert r["kind0"] == "xgmi" and r["kind"] == "ipc"
+        assert len(r["fallbacks"]) == 1
+        assert [o[:2] for o in r["outs"]] == [(1373, 1), (1373, 1)]
+
+
+def test_residency_budget_falls_back_to_graph(lin24, monkeypatch):
+    """GADMM_CU_BUDGET shrinks the CU count the residency check uses: the persistent kernels are then
+    refused up front (no 20 s deadline) and chain_admm runs the graph engine, same iterations."""
+    import torch
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import chain_admm
+    from gadmm_amd.engine.chain_engine import NativeChainEngine
+    from gadmm_amd.parallel.topology import Placement
+    m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
+    eng = NativeChainEngine(m.X, m.y, list(range(24)), 24, "linear", rho=3.0, obj0=_obj0(24), tol=1e-8, max_iter=3000)
+    eng.set_path(list(range(24)), Placement.contiguous(24, 1), 0)
+    full = eng.resident_capacity()
+    assert full >= 25 and eng.persistent_eligible()
+    monkeypatch.setenv("GADMM_CU_BUDGET", "1")
+    assert eng.resident_capacity() < 25 and not eng.persistent_eligible()
+    monkeypatch.setenv("GADMM_BLOCKED", "0")
+    eng.reset()
+    with pytest.raises(RuntimeError):
+        eng.run_persistent()
+    eng.close()
+    r = chain_admm(m, list(range(24)), 24, 3.0, _obj0(24), 1e-8, 3000, engine_opts={"cache": False})
+    assert r.iters == 1373 and r.extra["engine"] in ("graph", "eager")
