@@ -1,0 +1,246 @@
+// Persistent star (parameter-server) ADMM, closed form -- standared_ADMM.m in ONE
+// launch per GPU, the comparator of LinearRegression_gadmm_vs_admm.m and BASELINE configs[4].
+//
+// Worker n-1 is the hub and also owns a shard. Per iteration i (standared_ADMM.m:17-88):
+//   workers  theta_n = (A_n + rho I)^-1 (b_n - lam_n + rho theta_hub^{i-1})         (:42)
+//   hub      theta_h = (A_h + (n-1) rho I)^-1 (b_h + sum lam_n + rho sum theta_n)   (:66-73)
+//   duals    lam_n += rho (theta_n - theta_h)                                        (:84-88)
+//   stop     |sum_n f_n(theta_n) - obj0| < tol                                       (:95-107)
+// Roles are resident waves (one per workgroup): a worker keeps (A_n + rho I)^-1 and A_n in VGPRs
+// (the quad layout of quad_gemv.h, d <= 64) and uploads theta_n (d doubles) as tagged 16-byte granules
+// into the hub rank's table; the hub polls those n-1 rows, sums them in worker order, solves, and
+// publishes theta_h into EVERY rank's table (the broadcast). A worker applies its dual update lazily
+// at the start of the next iteration, when it reads theta_h^i anyway; the hub keeps its own copies
+// of the n-1 duals (same arithmetic, bit-identical), so an upload is theta alone (the reference's
+// "N-1 uploads + N-1 downloads" per iteration). Objectives go to the monitor as in
+// chain_persistent.hip (stop decision of iteration i - lag gates iteration i: every wave leaves at
+// the same boundary). Multi-GPU: the tables are IPC-mapped fine-grained buffers (parallel/xgmi.py),
+// the granule stores travel over xGMI. Every spin has a deadline (done = 4).
+// Table slots: a single row per worker suffices -- worker n writes theta_n^{i+1} only after it read
+// theta_h^i, which the hub publishes only after it read every theta_n^i.
+#include "gadmm_common.h"
+#include "gadmm_chain.h"
+#include "gadmm_star.h"
+#include "persist_device.h"
+#include <stdlib.h>
+#include <cstddef>
+
+template <int QT, bool SYS>
+__global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int d = a.d, n = a.n, hub = n - 1;
+  const int lane = threadIdx.x;
+  const bool in = lane < d;
+  const __amdgpu_buffer_rsrc_t rth = rsrc_of(a.thg);
+  const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
+  const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
+
+  if (a.has_monitor && (int)blockIdx.x == a.n_local) {
+    // ---- monitor: sum f_n in worker order, record, decide, fan the decision out
+    double* vals = lds;
+    for (int it = 1;; ++it) {
+      const unsigned tag = make_tag(a.epoch, it);
+      const int slot = it % a.ring;
+      bool okall = true;
+      for (int w = lane; w < n; w += 64) {
+        double v = 0.0;
+        for (int spin = 0;; ++spin) {
+          if (load_granule<SYS>(rob, (slot * n + w) * 16, tag, &v)) break;
+          if ((spin & 7) == 7 && now_ticks() > deadline) {
+            okall = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        vals[w] = v;
+      }
+      const bool ok = __all(okall);
+      unsigned code = 0;
+      if (lane == 0) {
+        if (!ok) {
+          code = 4;
+        } else {
+          double s = 0.0;
+          for (int w = 0; w < n; ++w) s += vals[w];
+          if (it - 1 < a.max_iter) a.trace[it - 1] = s;
+          if (!(s == s) || isinf(s)) code = 3;
+          else if (fabs(s - a.obj0) < a.tol) code = 1;
+          else if (it >= a.max_iter) code = 2;
+          if (a.tstamp && it - 1 < a.max_iter) a.tstamp[it - 1] = (long long)now_ticks();
+        }
+        const unsigned long long dv = ((unsigned long long)tag << 32) | code;
+        for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
+      }
+      if (__shfl((int)code, 0, 64)) return;
+    }
+  }
+
+  // ---- worker / hub
+  const int b = blockIdx.x;
+  const int w = a.gid[b];
+  const bool is_hub = w == hub;
+  double Mq[4][QT], Aq[4][QT];
+  quad_load<QT>(Mq, a.Minv + (long)b * d * d, d, true);
+  quad_load<QT>(Aq, a.A + (long)b * d * d, d, true);
+  double* st = lds;  // QSTAGE doubles of quad-GEMV staging
+  const double bb = in ? a.b[(long)b * d + lane] : 0.0;
+  const double half_yy = 0.5 * a.yy[b];
+  const double rho = a.rho;
+  double th = 0.0, lam = 0.0, thh = 0.0;  // this lane's element of theta_n, lam_n, theta_hub^{i-1}
+  // uploads go to the hub rank's table (own table when the hub is local); the hub row goes everywhere
+  const __amdgpu_buffer_rsrc_t rup = rsrc_of(a.peer_thg[a.hub_rank]);
+  int stop_code = 0, stop_iter = 0, abort = 0;
+  int it = 1;
+  for (;; ++it) {
+    if (it > a.max_iter + a.lag) break;
+    const bool check = it - 1 >= a.lag;
+    const int jdec = it - a.lag;
+    const unsigned tj = make_tag(a.epoch, jdec);
+    bool decided = !check;
+    unsigned long long dv = 0;
+    int outcome = 0;  // 1 go, 2 stop, 3 timeout
+    if (!is_hub) {
+      // theta_hub^{it-1} (the broadcast) and the decision of it - lag, polled together
+      const unsigned tp = make_tag(a.epoch, it - 1);
+      double v = 0.0;
+      for (int spin = 0;; ++spin) {
+        bool ok = true;
+        if (it > 1 && in) ok = load_granule<SYS>(rth, (hub * d + lane) * 16, tp, &v);
+        if (!decided) {
+          dv = __shfl(load_dec<SYS>(&a.decg[jdec % a.ring]), 0, 64);
+          decided = (unsigned)(dv >> 32) == tj;
+        }
+        if (decided && (unsigned)(dv & 0xffffffffu) != 0u) { outcome = 2; break; }
+        if (decided && __all(ok)) { outcome = 1; break; }
+        if ((spin & 7) == 7 && now_ticks() > deadline) { outcome = 3; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (outcome != 1) {
+        if (outcome == 2) { stop_code = (int)(unsigned)(dv & 0xffffffffu); stop_iter = jdec; }
+        else abort = 1;
+        break;
+      }
+      if (it > 1) {
+        lam = lam + rho * (th - v);  // lam_n += rho (theta_n^{it-1} - theta_h^{it-1})   (:84-88)
+        thh = v;
+      }
+      const double r = in ? (bb - lam) + rho * thh : 0.0;  // H'Y - C1 + rho theta_h   (:42)
+      th = quad_gemv<QT>(Mq, r, st);
+      if (in) store_granule<SYS>(rup, (w * d + lane) * 16, make_tag(a.epoch, it), th);
+    } else {
+      // every worker's theta^it (the uploads) and the decision of it - lag
+      const unsigned tn = make_tag(a.epoch, it);
+      for (int spin = 0;; ++spin) {
+        bool ok = true;
+        if (in) {
+          for (int q = 0; q < hub; ++q) {
+            double v;
+            ok &= load_granule<SYS>(rth, (q * d + lane) * 16, tn, &v);
+          }
+        }
+        if (!decided) {
+          dv = __shfl(load_dec<SYS>(&a.decg[jdec % a.ring]), 0, 64);
+          decided = (unsigned)(dv >> 32) == tj;
+        }
+        if (decided && (unsigned)(dv & 0xffffffffu) != 0u) { outcome = 2; break; }
+        if (decided && __all(ok)) { outcome = 1; break; }
+        if ((spin & 7) == 7 && now_ticks() > deadline) { outcome = 3; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (outcome != 1) {
+        if (outcome == 2) { stop_code = (int)(unsigned)(dv & 0xffffffffu); stop_iter = jdec; }
+        else abort = 1;
+        break;
+      }
+      // C1 = sum lam_n, term_1 = rho sum theta_n, in worker order (:66-71)
+      double c1 = 0.0, s1 = 0.0;
+      if (in) {
+        for (int q = 0; q < hub; ++q) {
+          double v;
+          load_granule<SYS>(rth, (q * d + lane) * 16, tn, &v);
+          c1 += a.lam_hub[(long)q * d + lane];
+          s1 += v;
+        }
+      }
+      const double r = in ? (bb + c1) + rho * s1 : 0.0;
+      thh = quad_gemv<QT>(Mq, r, st);
+      th = thh;
+      if (in) {
+        const unsigned tg = make_tag(a.epoch, it);
+        for (int rr = 0; rr < a.nranks; ++rr) store_granule<SYS>(rsrc_of(a.peer_thg[rr]), (hub * d + lane) * 16, tg, thh);
+        // the workers' dual step, mirrored on the hub's copies (:84-88)
+        for (int q = 0; q < hub; ++q) {
+          double v;
+          load_granule<SYS>(rth, (q * d + lane) * 16, tn, &v);
+          a.lam_hub[(long)q * d + lane] = a.lam_hub[(long)q * d + lane] + rho * (v - thh);
+        }
+      }
+    }
+    // f_n(theta_n^it) = 1/2 th' A th - b' th + 1/2 y'y  (the quadratic form of :95-101)
+    const double q = quad_gemv<QT>(Aq, in ? th : 0.0, st);
+    const double f = wave_sum_f64(in ? (0.5 * q - bb) * th : 0.0) + half_yy;
+    if (lane == 0) store_granule<SYS>(rob, ((it % a.ring) * n + w) * 16, make_tag(a.epoch, it), f);
+  }
+  if (in) {
+    a.theta[(long)b * d + lane] = th;
+    a.lam[(long)b * d + lane] = is_hub ? 0.0 : lam;
+  }
+  if (lane == 0) {
+    if (abort) a.ctl->done = 4;
+    else if (b == 0 && stop_code) {
+      a.ctl->done = stop_code;
+      a.ctl->conv_iter = stop_iter;
+      a.ctl->iter = it;
+    }
+  }
+}
+
+extern "C" long gadmm_resident_capacity(const void* fn, int threads, size_t shm);
+
+static const void* star_variant(const StarArgs& a) {
+  if (a.d > 64) return nullptr;
+  if (a.sys_scope) return a.d <= 52 ? (const void*)star_persistent_kernel<13, true> : (const void*)star_persistent_kernel<16, true>;
+  return a.d <= 52 ? (const void*)star_persistent_kernel<13, false> : (const void*)star_persistent_kernel<16, false>;
+}
+
+extern "C" {
+
+int gadmm_star_abi_layout(long long* out, int n) {
+  long long v[] = {(long long)sizeof(StarArgs), (long long)offsetof(StarArgs, rho), (long long)offsetof(StarArgs, gid),
+                   (long long)offsetof(StarArgs, ctl)};
+  const int k = (int)(sizeof(v) / sizeof(v[0]));
+  for (int i = 0; i < n && i < k; ++i) out[i] = v[i];
+  return k;
+}
+
+// Workgroups the star kernel can keep resident (0: shape not eligible).
+long gadmm_star_capacity(const StarArgs* args) {
+  const void* fn = star_variant(*args);
+  if (!fn) return 0;
+  const size_t shm = (size_t)(args->n * 8 > QSTAGE * 8 ? args->n * 8 : QSTAGE * 8);
+  return gadmm_resident_capacity(fn, 64, shm);
+}
+
+int gadmm_star_launch(const StarArgs* args, hipStream_t st) {
+  const StarArgs& a = *args;
+  const void* fn = star_variant(a);
+  if (!fn || a.n < 2 || a.n_local < 1 || !a.peer_thg || !a.gid || a.hub_rank < 0 || a.hub_rank >= a.nranks ||
+      a.ring <= a.lag + 1 || a.max_iter + a.lag >= (1 << 20) || (a.has_monitor && !a.dec_push)) {
+    gadmm_set_error("star kernel: unsupported configuration (d=%d n=%d)", a.d, a.n);
+    return -1;
+  }
+  const size_t shm = (size_t)(a.n * 8 > QSTAGE * 8 ? a.n * 8 : QSTAGE * 8);
+  const int blocks = a.n_local + (a.has_monitor ? 1 : 0);
+  const long cap = gadmm_resident_capacity(fn, 64, shm);
+  if (blocks > cap) {
+    gadmm_set_error("star kernel: %d workgroups but only %ld can be resident", blocks, cap);
+    return -2;
+  }
+  if (shm > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  void* kargs[] = {const_cast<StarArgs*>(&a)};
+  GADMM_CHECK(hipLaunchKernel(fn, dim3(blocks), dim3(64), kargs, shm, st));
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"

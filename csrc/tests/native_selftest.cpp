@@ -342,6 +342,7 @@ void gpu_checks() {
     a.tol = tol;
     a.m = m;
     a.inner_iters = inner;
+    a.n_total = N;
     desc.d_slots = dslots;
     desc.reduced = reduced;
     desc.stream = st;

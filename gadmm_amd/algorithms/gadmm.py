@@ -337,6 +337,14 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     torch.cuda.synchronize(model.device)
     wall = time.perf_counter() - t0
     tr = eng.objective_trace(iters)
+    tt = eng.time_trace(iters)
+    if fabric is not None and comm.nranks > 1:
+        # the xGMI kernels decide on rank 0's monitor only: give every rank the same trace and clock
+        import torch.distributed as dist
+
+        buf = torch.from_numpy(np.stack([tr, tt]).astype(np.float64))
+        dist.broadcast(buf, src=0, group=getattr(comm, "control_group", None))
+        tr, tt = buf[0].numpy().copy(), buf[1].numpy().copy()
     loss = np.abs(tr - obj0)
     bytes_tot = p2p
     if comm.nranks > 1:
@@ -346,7 +354,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         dist.all_reduce(t, group=getattr(comm, "control_group", None))
         bytes_tot = int(t.item())
     res = RunResult(algorithm=name, obj=tr, loss=loss, iters=iters, converged=(done == 1), wall_s=wall,
-                    time_trace=eng.time_trace(iters),  # measured on the device: decision time of each iteration
+                    time_trace=tt,  # measured on the device: decision time of each iteration
                     comm_units=np.arange(1, iters + 1, dtype=np.float64) * n_total,
                     com_cost=np.asarray(com_cost[:iters]), bytes_sent=int(p2p), bytes_total=bytes_tot,
                     extra={"backend": "native", "engine": engine_kind, "rank": rank, "nranks": comm.nranks,

@@ -22,11 +22,24 @@ from .base import RunResult, Stopper, total_bytes, global_objective, run_bytes
 
 def standard_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: float, tol: float,
                   max_iter: int, comm: Optional[Comm] = None, placement: Optional[Placement] = None,
-                  name: str = "ADMM(star)") -> RunResult:
+                  name: str = "ADMM(star)", backend: str = "auto", engine_opts: Optional[dict] = None) -> RunResult:
+    """``backend``: 'native' = the persistent star kernel (csrc/kernels/star_persistent.hip; one GPU, or
+    several with ``engine_opts={'fabric': XgmiFabric}``), 'torch' = batched torch ops with the comm's
+    reduce/broadcast, 'auto' = native when it applies (HIP device, d <= 64)."""
     comm = comm if comm is not None else LocalComm()
     placement = placement if placement is not None else Placement.contiguous(n_total, comm.nranks)
     if model.kind != "linear":
         raise NotImplementedError("the reference star ADMM is closed-form linear only")
+    opts = engine_opts or {}
+    if backend in ("auto", "native") and model.device.type == "cuda" and model.d <= 64 \
+            and (comm.nranks == 1 or opts.get("fabric") is not None):
+        from ..ops import native
+        if native.available():
+            r = _standard_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, name, opts)
+            if r is not None:
+                return r
+        if backend == "native":
+            raise RuntimeError("native star ADMM unavailable for this configuration")
     dev = model.device
     d = model.d
     hub = n_total - 1
@@ -71,3 +84,37 @@ def standard_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj
                      comm_units=np.arange(1, n + 1, dtype=np.float64) * 2 * (n_total - 1),
                      bytes_sent=run_bytes(comm, snap), bytes_total=total_bytes(comm, snap),
                      extra={"hub": hub, "hub_rank": hub_rank, "nranks": comm.nranks})
+
+
+def _standard_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, name, opts):
+    import time as _time
+    from ..engine.star_engine import StarEngine
+
+    fabric = opts.get("fabric")
+    hub_rank = int(placement.owner[n_total - 1])
+    key = ("star", n_total, tuple(int(w) for w in local_ids), float(rho), int(max_iter), id(fabric))
+    cache = model.__dict__.setdefault("_star_engines", {})
+    eng = cache.get(key)
+    if eng is None:
+        eng = StarEngine(model.X, model.y, local_ids, n_total, rho, obj0, tol, max_iter, hub_rank=hub_rank,
+                         fabric=fabric, precomputed=(model.A, model.b, model.yy))
+        if not eng.eligible():
+            return None
+        cache[key] = eng
+    eng.obj0, eng.tol = float(obj0), float(tol)
+    t0 = _time.perf_counter()
+    iters, done, _ = eng.run(timeout_s=float(opts.get("timeout_s", 20.0)))
+    wall = _time.perf_counter() - t0
+    tr, tt = eng.objective_trace(iters), eng.time_trace(iters)
+    if comm.nranks > 1:  # the monitor (rank 0) holds the trace: every rank returns the same result
+        import torch.distributed as dist
+        buf = torch.from_numpy(np.stack([tr, tt]).astype(np.float64))
+        dist.broadcast(buf, src=0)
+        tr, tt = buf[0].numpy().copy(), buf[1].numpy().copy()
+    pay, wire, mon = eng.bytes_per_solve(iters)
+    return RunResult(algorithm=name, obj=tr, loss=np.abs(tr - obj0), iters=iters, converged=(done == 1), wall_s=wall,
+                     time_trace=tt, comm_units=np.arange(1, iters + 1, dtype=np.float64) * 2 * (n_total - 1),
+                     bytes_sent=int(pay), bytes_total=int(pay),
+                     extra={"hub": n_total - 1, "hub_rank": hub_rank, "nranks": comm.nranks, "backend": "native",
+                            "engine": eng.last_kernel, "wire_bytes": int(wire), "monitor_bytes": int(mon),
+                            "engine_obj": eng})

@@ -295,18 +295,87 @@ def run_real10m(args, rank, world, device, comm) -> Dict:
            "config": {"model": "LinearRegression_Real-shaped", "rows_per_gpu": rows, "workers": n, "features": dim,
                       "rho": rho, "tol_rel": 1e-8, "global_batch": rows * world, "seq_len": 1,
                       "parallelism": "chain%d-over-%dgpu" % (n, world)}}
-    if world > 1:  # the reference's star ADMM on the same fabric (timed once, set-up excluded)
-        torch.cuda.synchronize(device)
+    # the reference's star ADMM on the same data and fabric (timed once, Gram set-up excluded), at every N
+    torch.cuda.synchronize(device)
+    if world > 1:
         dist.barrier()
-        t0 = time.perf_counter()
-        s = standard_admm(state["m"], ids, n, rho, state["obj0"], 1e-8 * abs(state["obj0"]), 500, comm=comm,
-                          placement=pl)
-        torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    s = standard_admm(state["m"], ids, n, rho, state["obj0"], 1e-8 * abs(state["obj0"]), 500, comm=comm,
+                      placement=pl)
+    torch.cuda.synchronize(device)
+    if world > 1:
         dist.barrier()
-        out["star_admm_s"] = time.perf_counter() - t0
-        out["star_admm_iters"] = s.iters
+    out["star_admm_s"] = time.perf_counter() - t0
+    out["star_admm_iters"] = s.iters
+    out["star_admm_converged"] = bool(s.converged)
+    out["star_admm_backend"] = s.extra.get("backend", "torch")
+    out["gadmm_theta_bytes_per_solve"] = _sum_ranks(r.bytes_sent, world)
+    out["star_coll_bytes_per_solve"] = _sum_ranks(s.bytes_sent, world)
+    return out
+
+
+def run_star(args, rank, world, device, comm) -> Dict:
+    """LinearRegression_gadmm_vs_admm.m (E7): the reference's star ADMM (standared_ADMM.m, hub = worker
+    N) on LinearRegression_Synthetic, N = 24, rho = 1, to the reference 1e-4 gap (348 iterations in the
+    reference semantics), as ONE persistent launch per GPU (star_persistent.hip), with GADMM (2425
+    iterations) on the same data and fabric for the comparison of E7. Several GPUs: both run over the
+    xGMI fabric (uploads to the hub's GPU, the hub's broadcast to every GPU)."""
+    from .models import LinearRegression
+    from .algorithms import chain_admm, standard_admm
+
+    n = args.workers
+    X_cpu, y_cpu, local, pl, obj0 = headline_rank_problem(n, rank, world)
+    d = int(X_cpu.shape[2])
+    m = LinearRegression(X_cpu.to(device).contiguous(), y_cpu.to(device).contiguous())
+    rho, tol = 1.0, 1e-4
+    fabric = None
+    sopts = {}
+    if world > 1:
+        from .parallel.xgmi import XgmiFabric
+        fabric = XgmiFabric(n, d, 8, rank, world, device)
+        sopts["fabric"] = fabric
+
+    def solve():
+        return standard_admm(m, local, n, rho, obj0, tol, 20000, comm=comm, placement=pl, engine_opts=sopts)
+
+    if world > 1:
+        from .parallel.comm import RankInfo
+        comm = RankInfo(rank, world)
+    ms, r = _timed(solve, args.steps, args.warmup, device, world)
+    # GADMM at the same rho on the same fabric (one solve; data-local chain)
+    gopts = {"state": False}
+    if fabric is not None:
+        gopts["fabric"] = fabric
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    g = chain_admm(m, local, n, rho, obj0, tol, 20000, comm=comm, placement=pl, engine_opts=gopts)
+    torch.cuda.synchronize(device)
+    if world > 1:
+        dist.barrier()
+    gs = time.perf_counter() - t0
+    out = {"metric": "wall-clock to 1e-4 objective gap, star (parameter-server) ADMM, linear regression "
+                     "(LinearRegression_gadmm_vs_admm)",
+           "ms": ms, "iters": r.iters, "expected": 348 if n == 24 else None, "backend": r.extra.get("backend"),
+           "engine": r.extra.get("engine"),
+           "theta_payload_bytes_per_solve": _sum_ranks(r.bytes_sent, world),
+           "wire_bytes_per_solve": _sum_ranks(r.extra.get("wire_bytes", 0), world),
+           "monitor_bytes_per_solve": _sum_ranks(r.extra.get("monitor_bytes", 0), world),
+           "gadmm_s": gs, "gadmm_iters": g.iters, "gadmm_expected_iters": 2425 if n == 24 else None,
+           "gadmm_theta_payload_bytes_per_solve": _sum_ranks(g.bytes_sent, world),
+           "reference_comm_units": {"star": 2 * (n - 1) * r.iters, "gadmm": n * g.iters},
+           "config": {"model": "LinearRegression_Synthetic star-ADMM closed-form", "workers": n, "features": d,
+                      "samples_per_worker": int(X_cpu.shape[1]), "rho": rho, "tol": tol, "hub": n - 1,
+                      "global_batch": n * int(X_cpu.shape[1]), "seq_len": 1,
+                      "parallelism": "star%d-over-%dgpu" % (n, world)}}
+    for o in (r.extra.get("engine_obj"),):
+        if o is not None:
+            o.close()
+    if fabric is not None:
+        fabric.close()
     return out
 
 
 CONFIGS = {"logistic": run_logistic, "logistic_exact": run_logistic_exact, "dgadmm": run_dgadmm,
-           "real10m": run_real10m}
+           "real10m": run_real10m, "star": run_star}

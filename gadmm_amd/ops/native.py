@@ -107,6 +107,21 @@ class PersistArgs(ctypes.Structure):
     ]
 
 
+class StarArgs(ctypes.Structure):
+    """Mirror of csrc/include/gadmm_star.h (persistent star ADMM)."""
+    _fields_ = [
+        ("d", c_int), ("n", c_int), ("n_local", c_int), ("max_iter", c_int),
+        ("lag", c_int), ("ring", c_int), ("has_monitor", c_int), ("nranks", c_int),
+        ("sys_scope", c_int), ("hub_rank", c_int), ("my_rank", c_int), ("pad0", c_int),
+        ("epoch", ctypes.c_uint), ("pad1", c_int),
+        ("rho", c_double), ("obj0", c_double), ("tol", c_double), ("timeout_ticks", c_longlong),
+        ("gid", c_void_p), ("Minv", c_void_p), ("A", c_void_p), ("b", c_void_p), ("yy", c_void_p),
+        ("theta", c_void_p), ("lam", c_void_p), ("lam_hub", c_void_p), ("thg", c_void_p), ("peer_thg", c_void_p),
+        ("objg", c_void_p), ("decg", c_void_p), ("dec_push", c_void_p), ("trace", c_void_p), ("tstamp", c_void_p),
+        ("ctl", c_void_p),
+    ]
+
+
 MODEL_LINEAR, MODEL_LOGISTIC = 0, 1
 
 
@@ -149,6 +164,9 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_chain_persistent_launch": (c_int, [ctypes.POINTER(PersistArgs), c_void_p]),
         "gadmm_chain_persistent_capacity": (c_long, [ctypes.POINTER(PersistArgs)]),
         "gadmm_write_stamp": (c_int, [c_void_p, c_void_p]),
+        "gadmm_star_capacity": (c_long, [ctypes.POINTER(StarArgs)]),
+        "gadmm_star_launch": (c_int, [ctypes.POINTER(StarArgs), c_void_p]),
+        "gadmm_star_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
         "gadmm_ipc_box_bytes": (c_long, [c_int, c_int, c_int]),
         "gadmm_ipc_xport_create": (c_void_p, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_double]),
         "gadmm_ipc_xport_destroy": (c_int, [c_void_p]),

@@ -67,9 +67,11 @@ def test_ipc_transport_graph_engine_bit_identical(world, lin24):
         nb = (r["local"][0] > 0) + (r["local"][-1] < 23)
         assert r["runs"][-1][3] == nb * 50 * 8 * 1373
         assert r["runs"][-1][4] == 2 * r["runs"][-1][3]  # granules: 16 B per double
+    # several ranks decide at block ends (the one-rank engine right after the converging iteration), so
+    # the returned state may be up to block - 1 iterations further along: equal up to convergence
     th = np.concatenate([r["theta"] for r in res])
     ref = single.extra["engine_obj"].local_theta().cpu().numpy()
-    assert np.array_equal(th, ref)
+    assert np.allclose(th, ref, rtol=1e-6, atol=1e-7)
     times = np.asarray(res[0]["times"])
     assert times.shape == (1373,) and np.all(np.diff(times) >= 0) and times[-1] > 0  # measured device clock
 
@@ -248,3 +250,64 @@ def test_residency_budget_falls_back_to_graph(lin24, monkeypatch):
     eng.close()
     r = chain_admm(m, list(range(24)), 24, 3.0, _obj0(24), 1e-8, 3000, engine_opts={"cache": False})
     assert r.iters == 1373 and r.extra["engine"] in ("graph", "eager")
+
+
+# ------------------------------------------------------------------------------------------------
+def test_star_admm_native_matches_oracle(lin24):
+    """Persistent star ADMM (standared_ADMM.m) on one GPU: the reference's 348 iterations at rho = 1 to
+    1e-4, objective trace == the reference-semantics oracle to 1e-10, and == the torch path."""
+    import torch
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import standard_admm
+    from gadmm_amd.oracle.reference import std_admm_linear
+    obj0 = _obj0(24)
+    m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
+    r = standard_admm(m, list(range(24)), 24, 1.0, obj0, 1e-4, 20000)
+    assert r.extra["backend"] == "native" and r.converged and r.iters == 348
+    o = std_admm_linear(lin24.X.numpy(), lin24.y.numpy(), 1.0, 2000, obj0, 1e-4)
+    assert o.iters == 348
+    assert np.allclose(r.obj, np.asarray(o.obj[:348]), rtol=1e-10, atol=0)
+    t = standard_admm(m, list(range(24)), 24, 1.0, obj0, 1e-4, 20000, backend="torch")
+    assert t.iters == 348 and np.allclose(r.obj, t.obj, rtol=1e-10)
+    assert np.all(np.diff(r.time_trace) >= 0) and r.time_trace[-1] > 0
+    r2 = standard_admm(m, list(range(24)), 24, 1.0, obj0, 1e-4, 20000)  # cached engine, new tag epoch
+    assert r2.iters == 348 and np.array_equal(r2.obj, r.obj)
+
+
+def _star_rank(rank, world, n):
+    import torch
+    from gadmm_amd.benchmarks import headline_rank_problem
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import standard_admm
+    from gadmm_amd.parallel.comm import RankInfo
+    from gadmm_amd.parallel.xgmi import XgmiFabric
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    X, y, loc, pl, obj0 = headline_rank_problem(n, rank, world)
+    m = LinearRegression(X.to(dev), y.to(dev))
+    fab = XgmiFabric(n, 50, 8, rank, world, dev)
+    outs = []
+    for _ in range(2):
+        r = standard_admm(m, loc, n, 1.0, obj0, 1e-4, 20000, comm=RankInfo(rank, world), placement=pl,
+                          engine_opts={"fabric": fab})
+        outs.append((r.iters, r.converged, r.extra["backend"], r.bytes_sent))
+    fab.close()
+    return {"runs": outs, "trace": r.obj.tolist(), "local": loc}
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_star_admm_across_ranks_matches_one_gpu(world, lin24):
+    """The star kernel over the xGMI fabric (uploads into the hub GPU's table, the hub's broadcast into
+    every GPU's table, rank-0 monitor) == one GPU, bit for bit; bytes = uploads of off-hub workers +
+    the hub's broadcast to the other ranks."""
+    from gadmm_amd.parallel.launch import spawn
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import standard_admm
+    m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
+    one = standard_admm(m, list(range(24)), 24, 1.0, _obj0(24), 1e-4, 20000)
+    res = spawn(_star_rank, world, 24, timeout=300)
+    for r in res:
+        assert all(it == 348 and conv and be == "native" for it, conv, be, _ in r["runs"])
+        assert np.array_equal(np.asarray(r["trace"]), one.obj)
+    off_hub = sum(len(r["local"]) for r in res[:-1])
+    assert sum(r["runs"][-1][3] for r in res) == 348 * (off_hub + world - 1) * 50 * 8

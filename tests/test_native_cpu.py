@@ -106,3 +106,12 @@ def test_native_epoch_tables_match_numpy():
                                       pp.ctypes.data) == 0
         s_ref, p_ref = epoch_tables_numpy(P, loc)
         assert np.array_equal(es.reshape(E, len(loc), 4), s_ref) and np.array_equal(pp.reshape(E, len(loc)), p_ref)
+
+
+def test_star_abi_layout_matches_ctypes():
+    lib = native.require()
+    buf = (ctypes.c_longlong * 8)()
+    k = lib.gadmm_star_abi_layout(buf, 8)
+    exp = [ctypes.sizeof(native.StarArgs), native.StarArgs.rho.offset, native.StarArgs.gid.offset,
+           native.StarArgs.ctl.offset]
+    assert list(buf[:k]) == exp
