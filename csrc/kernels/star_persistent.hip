@@ -83,6 +83,7 @@ __global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
   quad_load<QT>(Mq, a.Minv + (long)b * d * d, d, true);
   quad_load<QT>(Aq, a.A + (long)b * d * d, d, true);
   double* st = lds;  // QSTAGE doubles of quad-GEMV staging
+  double* snap = lds + QSTAGE;  // hub: [n-1][64] this iteration's uploads, read once from the table
   const double bb = in ? a.b[(long)b * d + lane] : 0.0;
   const double half_yy = 0.5 * a.yy[b];
   const double rho = a.rho;
@@ -136,6 +137,7 @@ __global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
           for (int q = 0; q < hub; ++q) {
             double v;
             ok &= load_granule<SYS>(rth, (q * d + lane) * 16, tn, &v);
+            snap[q * 64 + lane] = v;  // lane-private: no barrier needed
           }
         }
         if (!decided) {
@@ -156,10 +158,8 @@ __global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
       double c1 = 0.0, s1 = 0.0;
       if (in) {
         for (int q = 0; q < hub; ++q) {
-          double v;
-          load_granule<SYS>(rth, (q * d + lane) * 16, tn, &v);
           c1 += a.lam_hub[(long)q * d + lane];
-          s1 += v;
+          s1 += snap[q * 64 + lane];
         }
       }
       const double r = in ? (bb + c1) + rho * s1 : 0.0;
@@ -169,11 +169,10 @@ __global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
         const unsigned tg = make_tag(a.epoch, it);
         for (int rr = 0; rr < a.nranks; ++rr) store_granule<SYS>(rsrc_of(a.peer_thg[rr]), (hub * d + lane) * 16, tg, thh);
         // the workers' dual step, mirrored on the hub's copies (:84-88)
-        for (int q = 0; q < hub; ++q) {
-          double v;
-          load_granule<SYS>(rth, (q * d + lane) * 16, tn, &v);
-          a.lam_hub[(long)q * d + lane] = a.lam_hub[(long)q * d + lane] + rho * (v - thh);
-        }
+        // (from the LDS snapshot: once theta_h^it is out, worker q may already be overwriting its
+        // table row with theta_q^{it+1})
+        for (int q = 0; q < hub; ++q)
+          a.lam_hub[(long)q * d + lane] = a.lam_hub[(long)q * d + lane] + rho * (snap[q * 64 + lane] - thh);
       }
     }
     // f_n(theta_n^it) = 1/2 th' A th - b' th + 1/2 y'y  (the quadratic form of :95-101)
@@ -203,6 +202,12 @@ static const void* star_variant(const StarArgs& a) {
   return a.d <= 52 ? (const void*)star_persistent_kernel<13, false> : (const void*)star_persistent_kernel<16, false>;
 }
 
+// monitor: n doubles; worker/hub: quad-GEMV staging + the hub's [n-1][64] upload snapshot
+static size_t star_shm(const StarArgs& a) {
+  const size_t mon = (size_t)a.n * 8, wk = (size_t)(QSTAGE + (a.n - 1) * 64) * 8;
+  return mon > wk ? mon : wk;
+}
+
 extern "C" {
 
 int gadmm_star_abi_layout(long long* out, int n) {
@@ -217,7 +222,8 @@ int gadmm_star_abi_layout(long long* out, int n) {
 long gadmm_star_capacity(const StarArgs* args) {
   const void* fn = star_variant(*args);
   if (!fn) return 0;
-  const size_t shm = (size_t)(args->n * 8 > QSTAGE * 8 ? args->n * 8 : QSTAGE * 8);
+  const size_t shm = star_shm(*args);
+  if (shm > 160 * 1024) return 0;
   return gadmm_resident_capacity(fn, 64, shm);
 }
 
@@ -229,7 +235,7 @@ int gadmm_star_launch(const StarArgs* args, hipStream_t st) {
     gadmm_set_error("star kernel: unsupported configuration (d=%d n=%d)", a.d, a.n);
     return -1;
   }
-  const size_t shm = (size_t)(a.n * 8 > QSTAGE * 8 ? a.n * 8 : QSTAGE * 8);
+  const size_t shm = star_shm(a);
   const int blocks = a.n_local + (a.has_monitor ? 1 : 0);
   const long cap = gadmm_resident_capacity(fn, 64, shm);
   if (blocks > cap) {

@@ -294,6 +294,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         starts = np.concatenate([[1], rechains]).astype(np.int64)
         r = eng.run_persistent(epochs=(starts, P), fabric=fabric)
         iters, done = r.iters, r.done
+        p2p, mon, wire = r.p2p_bytes, r.monitor_bytes, r.wire_bytes
         # per-epoch cost; the initial cost vector may be ragged (the v0 column-slice quirk)
         csum = Cn.sum(axis=1) if Cn.dtype != object else np.asarray([float(np.sum(c)) for c in Cn])
         per_it = np.concatenate([[float(np.sum(saved[2]))], csum]) * (n_heads if cost_quirk else 1)
