@@ -19,7 +19,10 @@ class RunResult:
       transmission: GADMM ``iter*N``, GD ``iter*N + iter``, LAG ``uploads + iter``;
       LinearRegression_Synthetic.m:100-142);
     * ``com_cost``: cumulative energy/distance cost where the reference tracks one (D-GADMM, E7);
-    * ``wall_s``/``time_trace``: real wall clock (cumulative per iteration);
+    * ``wall_s``/``time_trace``: real wall clock (cumulative per iteration; native engines: the
+      device's s_memrealtime at each iteration's stop decision);
+    * ``model_time``: the reference's modelled clock, ``2 * toc`` of worker 1's local solve per
+      iteration (utils/timing.py; group_ADMM_closedForm.m:39-42,53-55), when the caller sets it;
     * ``bytes_sent``: actual bytes this rank put on the fabric; ``bytes_total`` summed over ranks;
     * ``primal_res``: per-iteration consensus violation sum over chain edges ||th_n - th_right||^2
       (kernel K4's residual; chain algorithms).
@@ -39,6 +42,7 @@ class RunResult:
     extra: Dict[str, Any] = field(default_factory=dict)
     theta: Optional[np.ndarray] = None
     primal_res: Optional[np.ndarray] = None
+    model_time: Optional[np.ndarray] = None
 
     def summary(self) -> Dict[str, Any]:
         return {

@@ -30,6 +30,7 @@ import torch
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.topology import rechain_iterations, PathSchedule, Placement, chain_plan
 from .base import global_objective_and_residual, RunResult, Stopper, total_bytes, global_objective, run_bytes
+from ..utils.timing import roctx_range
 
 
 def _gather_rows(theta: torch.Tensor, ids: List[int]) -> torch.Tensor:
@@ -82,8 +83,11 @@ def chain_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: 
         elif backend == "native":
             raise RuntimeError("native backend requested but unavailable for this comm/device")
     if use_native:
-        return _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, schedule,
-                                  local_solver, step, max_inner, inner_tol, cost_quirk, name, engine_opts or {})
+        # a named range per solve in rocprofv3 --marker-trace timelines (no-op without roctx)
+        with roctx_range("%s native N=%d" % (name, n_total)):
+            return _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement,
+                                      schedule, local_solver, step, max_inner, inner_tol, cost_quirk, name,
+                                      engine_opts or {})
     return _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, schedule,
                              local_solver, step, max_inner, inner_tol, cost_quirk, name, record_theta, state,
                              check_exchange, failures)

@@ -35,7 +35,10 @@ def standard_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj
             and (comm.nranks == 1 or opts.get("fabric") is not None):
         from ..ops import native
         if native.available():
-            r = _standard_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, name, opts)
+            from ..utils.timing import roctx_range
+            with roctx_range("%s native N=%d" % (name, n_total)):
+                r = _standard_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement,
+                                          name, opts)
             if r is not None:
                 return r
         if backend == "native":

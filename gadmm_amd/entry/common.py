@@ -192,25 +192,44 @@ def _fname(s: str) -> str:
 
 
 # ----------------------------------------------------------------------------------- building blocks
+def attach_modelled_clock(result, model, rho: float, sess: Session):
+    """Give ``result`` the reference's modelled clock (``2 * toc`` per iteration, toc = worker 1's
+    local solve measured on this device; utils/timing.py). Worker 1 lives on rank 0: its toc is
+    broadcast so every rank reports the same curve."""
+    from ..utils.timing import modelled_time, reference_local_solve_s
+
+    toc = reference_local_solve_s(model, rho) if sess.rank == 0 else 0.0
+    if sess.world > 1:
+        t = torch.tensor([toc], dtype=torch.float64, device=sess.device if sess.device.type == "cuda" else "cpu")
+        sess.comm.broadcast(t, 0)
+        toc = float(t.item())
+    result.model_time = modelled_time(toc, len(result.obj))
+    result.extra["model_toc_s"] = toc
+    return result
+
+
 def gadmm_sweep(prob: Problem, sess: Session, backend: str = "auto") -> Dict[str, object]:
     from ..algorithms import chain_admm
+    from ..utils.timing import roctx_range
 
     cfg = prob.cfg
     out = {}
     for rho in cfg.rhos:
         solver = "closed" if cfg.model == "linear" else "gd"
-        r = chain_admm(prob.model, prob.local_ids, prob.n_total, rho, prob.obj0, cfg.acc, cfg.gadmm_iters,
-                       comm=sess.comm, placement=prob.placement, local_solver=solver, step=cfg.gd_step,
-                       max_inner=cfg.max_inner, backend=backend, name="GADMM(rho=%g)" % rho)
+        with roctx_range("gadmm_sweep rho=%g" % rho):
+            r = chain_admm(prob.model, prob.local_ids, prob.n_total, rho, prob.obj0, cfg.acc, cfg.gadmm_iters,
+                           comm=sess.comm, placement=prob.placement, local_solver=solver, step=cfg.gd_step,
+                           max_inner=cfg.max_inner, backend=backend, name="GADMM(rho=%g)" % rho)
         r.extra.pop("engine_obj", None)
-        out["GADMM_rho%g" % rho] = r
+        out["GADMM_rho%g" % rho] = attach_modelled_clock(r, prob.model, rho, sess)
     if cfg.model == "logistic":
         for rho in cfg.exact_rhos:  # exact local solves (D2 semantics), to the tighter exact_acc gap
-            r = chain_admm(prob.model, prob.local_ids, prob.n_total, rho, prob.obj0, cfg.exact_acc, cfg.exact_iters,
-                           comm=sess.comm, placement=prob.placement, local_solver="newton", backend=backend,
-                           name="GADMM-exact(rho=%g)" % rho)
+            with roctx_range("gadmm_exact rho=%g" % rho):
+                r = chain_admm(prob.model, prob.local_ids, prob.n_total, rho, prob.obj0, cfg.exact_acc,
+                               cfg.exact_iters, comm=sess.comm, placement=prob.placement, local_solver="newton",
+                               backend=backend, name="GADMM-exact(rho=%g)" % rho)
             r.extra.pop("engine_obj", None)
-            out["GADMM_exact_rho%g" % rho] = r
+            out["GADMM_exact_rho%g" % rho] = attach_modelled_clock(r, prob.model, rho, sess)
     return out
 
 

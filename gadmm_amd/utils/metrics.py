@@ -47,6 +47,9 @@ class RunWriter:
                 row["comm_units"] = float(result.comm_units[i])
             if len(result.time_trace) > i:
                 row["wall_s"] = float(result.time_trace[i])
+            mt = getattr(result, "model_time", None)
+            if mt is not None and len(mt) > i:
+                row["model_clock_s"] = float(mt[i])
             if result.com_cost is not None and len(result.com_cost) > i:
                 row["com_cost"] = float(result.com_cost[i])
             pr = getattr(result, "primal_res", None)
@@ -80,9 +83,10 @@ def _safe(key: str) -> str:
 
 
 def plot_three_panel(results: Dict[str, object], path: str, title: str = "", xmax_iter: Optional[int] = None) -> bool:
-    """Gap vs iteration, vs cumulative communication units, vs wall clock (the reference's
-    semilogy figures, e.g. LinearRegression_Synthetic.m:146-248). Returns False if matplotlib
-    is unavailable."""
+    """Gap vs iteration, vs cumulative communication units, vs measured wall clock (the reference's
+    semilogy figures, e.g. LinearRegression_Synthetic.m:146-248), plus a fourth panel with the
+    reference's modelled ``2 * toc`` clock when any run carries one (``RunResult.model_time``).
+    Returns False if matplotlib is unavailable."""
     try:
         import matplotlib
 
@@ -90,7 +94,8 @@ def plot_three_panel(results: Dict[str, object], path: str, title: str = "", xma
         import matplotlib.pyplot as plt
     except Exception:  # pragma: no cover
         return False
-    fig, ax = plt.subplots(1, 3, figsize=(15, 4.2))
+    modelled = any(getattr(r, "model_time", None) is not None for r in results.values())
+    fig, ax = plt.subplots(1, 4 if modelled else 3, figsize=(20 if modelled else 15, 4.2))
     for name, r in results.items():
         loss = np.maximum(np.asarray(r.loss), 1e-16)
         it = np.arange(1, len(loss) + 1)
@@ -99,9 +104,14 @@ def plot_three_panel(results: Dict[str, object], path: str, title: str = "", xma
             ax[1].semilogy(r.comm_units, loss, label=name)
         if len(r.time_trace) == len(loss):
             ax[2].semilogy(r.time_trace, loss, label=name)
+        mt = getattr(r, "model_time", None)
+        if modelled and mt is not None and len(mt) == len(loss):
+            ax[3].semilogy(mt, loss, label=name)
     ax[0].set_xlabel("iteration")
     ax[1].set_xlabel("cumulative communication (reference units)")
-    ax[2].set_xlabel("wall clock [s]")
+    ax[2].set_xlabel("wall clock, measured [s]")
+    if modelled:
+        ax[3].set_xlabel("modelled clock: 2 x local-solve time per iteration [s]")
     for a in ax:
         a.set_ylabel("|obj - obj*|")
         a.grid(True, which="both", alpha=0.3)

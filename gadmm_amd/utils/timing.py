@@ -58,9 +58,37 @@ class EventTimer:
 
 
 def modelled_time(per_solve_s: float, iters: int) -> np.ndarray:
-    """Reference clock model: cumulative ``2 * t_local_solve`` per iteration (first entry 0)."""
+    """Reference clock model: cumulative ``2 * t_local_solve`` per iteration (first entry 0:
+    ``gadmm_time(i) = gadmm_time(i-1) + 2*toc`` for i > 1, group_ADMM_closedForm.m:39-42,53-55)."""
     t = np.arange(iters, dtype=np.float64) * 2.0 * per_solve_s
     return t
+
+
+def reference_local_solve_s(model, rho: float, reps: int = 20) -> float:
+    """The ``toc`` of the reference's clock model, measured on this device: worker 1's local solve
+    from its raw shard, as the reference times it (tic/toc around one solve of the first worker).
+
+    * linear: ``(H'H + rho I) \\ (H'Y + ...)`` -- Gram of the raw rows + dense solve
+      (group_ADMM_closedForm.m:39-43; the head has one neighbour, so the shift is rho);
+    * logistic: the exact prox (Newton to machine precision), the stand-in for the reference's CVX
+      call (group_ADMM_logistic.m:48-58).
+    Median of ``reps`` solves; device-synchronised around each."""
+    dev = model.X.device
+    idx = torch.zeros(1, dtype=torch.long, device=dev)
+    H, Y = model.X[0], model.y[0]
+    d = H.shape[-1]
+    times = []
+    for _ in range(max(1, reps)):
+        with WallTimer(dev) as t:
+            if getattr(model, "kind", "linear") == "linear":
+                M = H.T @ H + rho * torch.eye(d, dtype=H.dtype, device=dev)
+                x = torch.linalg.solve(M, H.T @ Y)
+            else:
+                z = torch.zeros((1, d), dtype=H.dtype, device=dev)
+                x = model.newton_prox(idx, z, z, torch.full((1,), rho, dtype=H.dtype, device=dev), z)
+            del x
+        times.append(t.elapsed)
+    return float(np.median(times))
 
 
 _roctx = None

@@ -26,6 +26,20 @@ def test_entry_quick(name, tmp_path):
     assert any(f.endswith(".jsonl") for f in os.listdir(tmp_path))
 
 
+def test_entry_clock_panels(tmp_path):
+    """Every GADMM run carries the measured wall clock AND the reference's modelled 2*toc clock
+    (group_ADMM_closedForm.m:39-42,53-55): both in the JSONL trace, four panels in the figure."""
+    entry.get("LinearRegression_Synthetic").main(["--quick", "--device", "cpu", "--out", str(tmp_path),
+                                                  "--no-baselines", "--set", "rhos=7"])
+    rows = [json.loads(l) for l in open(os.path.join(tmp_path, "GADMM_rho7.jsonl"))]
+    assert len(rows) == 248
+    mc = np.asarray([r["model_clock_s"] for r in rows])
+    wall = np.asarray([r["wall_s"] for r in rows])
+    assert mc[0] == 0.0 and np.all(np.diff(mc) > 0) and np.allclose(np.diff(mc), mc[1])  # 2*toc steps
+    assert np.all(np.diff(wall) >= 0) and wall[-1] > 0
+    assert [f for f in os.listdir(tmp_path) if f.endswith(".png")]
+
+
 def test_dynamic_entry_quick(tmp_path):
     out = entry.get("Dynamic_LinearRegression_Synthetic").main(
         ["--quick", "--device", "cpu", "--out", str(tmp_path), "--set", "gadmm_iters=60", "coherences=1,10"])

@@ -492,6 +492,25 @@ def test_entry_points_on_gpu(name, tmp_path):
     assert os.path.exists(out["summary_path"])
 
 
+def test_native_entry_measured_clock(tmp_path):
+    """E1 on the native engine: the JSONL wall clock is the device's per-iteration decision stamp
+    (non-uniform, increasing), next to the reference's modelled 2*toc clock; the figure is written."""
+    import json
+    from gadmm_amd import entry
+    out = entry.get("LinearRegression_Synthetic").main(["--quick", "--device", "cuda", "--out", str(tmp_path),
+                                                        "--no-baselines", "--set", "rhos=3", "acc=1e-8", "gadmm_iters=3000"])
+    assert out["runs"]["GADMM_rho3"]["iters"] == 1373 and out["runs"]["GADMM_rho3"]["backend"] == "native"
+    rows = [json.loads(l) for l in open(os.path.join(tmp_path, "GADMM_rho3.jsonl"))]
+    wall = np.asarray([r["wall_s"] for r in rows])
+    assert len(wall) == 1373 and np.all(np.diff(wall) >= 0) and wall[-1] > 0
+    steps = np.diff(wall)
+    assert steps.std() > 0  # measured, not an interpolated ramp
+    assert wall[-1] < 0.1  # the whole solve is milliseconds on the device
+    mc = np.asarray([r["model_clock_s"] for r in rows])
+    assert mc[0] == 0 and np.all(np.diff(mc) > 0)
+    assert [f for f in os.listdir(tmp_path) if f.endswith(".png")]
+
+
 def test_native_run_checkpoint_resumes_in_torch_path(lin24, lin_obj0, tmp_path):
     """A GPU (native persistent) solve leaves a resumable state: per-worker checkpoint written from
     it, reloaded, and continued in the torch path reproduces a continuous torch run's objective."""
