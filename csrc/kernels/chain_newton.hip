@@ -7,18 +7,22 @@
 //
 // Worker n solves   min_x  f_n(x) + mu_n^T x + rho/2 sum_{nbr} ||x - theta_nbr||^2,
 //   f_n(x) = lam/2 ||x||^2 + sum_i log(1 + exp(-y_i x_i^T x))
-// with Newton steps  H dx = g,  x <- x - dx  until max|dx| < 1e-13 max(1, max|x|) (<= 50 steps),
+// with steps  dx = H^-1 g,  x <- x - dx  until max|dx| < 1e-13 max(1, max|x|) (<= 50 steps),
 //   g = -X^T (y . sigma(-y . Xx)) + (lam + deg rho) x + mu - rho (theta_l + theta_r)
 //   H = X^T diag(w) X + (lam + deg rho) I,   w = sigma (1 - sigma)
 // (the same stopping rule and iteration cap as models/logistic.py:newton_prox, the torch path).
+// Chord-Newton (PhaseArgs.step = contraction threshold c > 0): H^-1 is refreshed only when a step
+// contracts by less than c (|dx_k| > c |dx_{k-1}|) or none is cached; otherwise the last inverse of
+// this worker -- kept in global memory across ADMM iterations, keyed by its shift -- is reused. The
+// fixed point (g = 0) and the stopping rule are those of exact Newton; step = 0 refreshes every step.
 //
 // One 512-thread workgroup per worker (d, m <= 64), everything in LDS:
 //   margins / gradient: 4 threads per row (column) with two xor shuffles;
-//   Hessian: lower-triangular 4x4 register blocks (two 16-B LDS reads per operand per sample), the
-//     samples split over a lane pair;
-//   solve: block Gauss-Jordan on [H | g] with 4 x 4 pivot blocks (SPD, no pivoting); lane i of wave
-//     w keeps row i's columns j = w (mod 8) in registers, each block's 4 columns go through LDS,
-//     one barrier per 4 pivots, no back substitution.
+//   Hessian: v_mfma_f64_16x16x4_f64, a 4 x 4 grid of 16 x 16 tiles, two per wave, K = samples;
+//   inverse: in-place block Gauss-Jordan with 4 x 4 pivot blocks (SPD, no pivoting); lane i of wave
+//     w keeps row i's columns j = w (mod 8) in registers, each block's 4 columns go through LDS, one
+//     barrier per 4 pivots; the inverse stays in registers, so H^-1 g is 8 FMAs per lane + one
+//     cross-wave sum.
 #include "gadmm_common.h"
 #include "gadmm_chain.h"
 #include "chain_device.h"
@@ -30,6 +34,7 @@ constexpr int NWV = NTN / 64;
 constexpr int NCW = 64 / NWV;      // columns per lane
 constexpr int NEWTON_MAX = 50;
 constexpr double NEWTON_TOL = 1e-13;
+constexpr long NEWTON_HSTRIDE = 64 * 64 + 8;  // per-worker inverse store: register image + valid flag + shift
 
 __device__ __forceinline__ double readlane_f64(double v, int l) {  // l wave-uniform
   const long long b = __double_as_longlong(v);
@@ -47,11 +52,12 @@ __device__ __forceinline__ double wave_max_f64(double v) {
 
 // TL: instrumented instantiation (GADMM_NEWTON_TL=1): s_memrealtime stamps of every Newton step of
 // every worker into PhaseArgs.rbuf as long long [n_local][NEWTON_MAX][5]: step start, sigma terms,
-// gradient + Hessian, Gauss-Jordan, update + test.
+// gradient (+ Hessian), inversion (= the previous stamp on chord steps), update + test. The low bit
+// of the last stamp is set on steps that refreshed the inverse.
 template <bool TL>
 __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
-  __shared__ int flag_lds, conv_lds;
+  __shared__ int flag_lds, conv_lds, refresh_lds;
   ChainCtl* ctl = a.ctl;
   if (ctl->done) return;
   const int it = ctl->iter;
@@ -61,14 +67,15 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
   const int DP = (d + 3) & ~3;  // X row stride: 4-column blocks are 16-B aligned, padding is zero
   const int DH = d | 1;         // H row stride (odd: a column walk spreads over the banks)
   double* Xs = lds;             // [m][DP]
-  double* Hs = Xs + m * DP;     // [d][DH] lower triangle, factorised in place
+  double* Hs = Xs + m * DP;     // [d][DH] Hessian (full, symmetric)
   double* xv = Hs + d * DH;     // [64] current iterate
-  double* gv = xv + 64;         // [64] Newton right-hand side (gradient)
+  double* gv = xv + 64;         // [64] gradient
   double* sv = gv + 64;         // [64] y_i sigma(-y_i z_i); at the end the per-sample losses
   double* wv = sv + 64;         // [64] sigma (1 - sigma)
   double* cv = wv + 64;         // [64] mu - rho (theta_l + theta_r): the x-independent gradient part
   double* yv = cv + 64;         // [64] labels
-  double* colv = yv + 64;       // [2][4][64] pivot-block columns of the solve (double-buffered)
+  double* colv = yv + 64;       // [2][4][64] pivot-block columns of the inversion (double-buffered)
+  double* pv = colv + 512;      // [NWV][64] per-wave partial sums of H^-1 g
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   const double rho = a.rho, lam = a.lam;
   double* th = a.theta;
@@ -79,6 +86,10 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
   const double* Xg = a.X + (long)sl.li * m * d;
   const double* Yg = a.Y + (long)sl.li * m;
   const double shift = lam + rho * (double)((thl ? 1 : 0) + (thr ? 1 : 0));  // lam + deg rho
+  // the worker's inverse Hessian of its last refresh, in register-image layout [c][wave][lane]
+  // (+ [4096] valid flag, [4097] the shift it was built with); chord threshold 0: exact Newton
+  const double chord = a.step;
+  double* hg = a.Minv ? const_cast<double*>(a.Minv) + (long)sl.li * NEWTON_HSTRIDE : nullptr;
 
   for (int idx = t; idx < m * DP; idx += NTN) {
     const int r = idx / DP, c = idx - r * DP;
@@ -98,9 +109,17 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
     xv[t] = thw[t];
   }
   if (t < m) yv[t] = Yg[t];
+  double h[NCW];  // lane i of wave w: row i of the inverse, columns j = w + NWV c
+  bool refresh = true;
+  if (hg && chord > 0.0 && hg[4096] == 1.0 && hg[4097] == shift) {
+#pragma unroll
+    for (int c = 0; c < NCW; ++c) h[c] = hg[(c * NWV + wid) * 64 + lane];
+    refresh = false;
+  }
   lds_barrier();
 
-  int used = 0;
+  int used = 0, refreshed = 0;
+  double nd_prev = 0.0;
   long long* tl = TL ? reinterpret_cast<long long*>(a.rbuf) + (long)sl.li * NEWTON_MAX * 5 : nullptr;
   for (int k = 0; k < NEWTON_MAX; ++k) {
     if (TL && t == 0) tl[k * 5] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -131,63 +150,49 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
       s += __shfl_xor(s, 2, 64);
       if (q == 0 && j < d) gv[j] = -s + shift * xv[j] + cv[j];
     }
-    {  // Hessian, lower 4x4 blocks (bj >= bk); the four lanes of a quad split the samples
-      const int nbr = (d + 3) >> 2, nb = nbr * (nbr + 1) / 2, half = t & 3;
-      for (int b = t >> 2; b < nb; b += NTN / 4) {
-        int bj = 0, bk = b;
-        while (bk > bj) {  // block-row bj holds bj + 1 blocks
-          bk -= bj + 1;
-          ++bj;
-        }
-        double acc[4][4];
+    if (refresh) {
+      // Hessian X^T diag(w) X + shift I on f64 MFMA: the 4 x 4 grid of 16 x 16 tiles (d <= 64), two
+      // per wave, K = samples in chunks of 4. v_mfma_f64_16x16x4_f64: A[i][k] = lane (k = l >> 4,
+      // i = l & 15), B[k][j] likewise, D row (l >> 4) + 4 reg, column l & 15.
+      const int k4 = lane >> 4, c16 = lane & 15;
+      const int R0 = wid >> 2, C0 = wid & 3, R1 = R0 + 2;  // tiles (R0, C0) and (R0 + 2, C0)
+      f64x4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+      const int ca = 16 * R0 + c16, cb = 16 * R1 + c16, cc = 16 * C0 + c16;
+      for (int k0 = 0; k0 < m; k0 += 4) {
+        const int kk = k0 + k4;
+        const bool kin = kk < m;
+        const double w = kin ? wv[kk] : 0.0;
+        const double* xr = Xs + (kin ? kk : 0) * DP;
+        const double a0 = ca < DP ? w * xr[ca] : 0.0;
+        const double a1 = cb < DP ? w * xr[cb] : 0.0;
+        const double bv = (kin && cc < DP) ? xr[cc] : 0.0;
+        acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, bv, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, bv, acc1, 0, 0, 0);
+      }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) acc[u][v] = 0.0;
-#pragma unroll 4
-        for (int i = half; i < m; i += 4) {
-          const double w = wv[i];
-          const double2 a01 = *reinterpret_cast<const double2*>(Xs + i * DP + 4 * bj);
-          const double2 a23 = *reinterpret_cast<const double2*>(Xs + i * DP + 4 * bj + 2);
-          const double2 b01 = *reinterpret_cast<const double2*>(Xs + i * DP + 4 * bk);
-          const double2 b23 = *reinterpret_cast<const double2*>(Xs + i * DP + 4 * bk + 2);
-          const double wa[4] = {w * a01.x, w * a01.y, w * a23.x, w * a23.y};
-          const double bb[4] = {b01.x, b01.y, b23.x, b23.y};
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int v = 0; v < 4; ++v) acc[u][v] = fma(wa[u], bb[v], acc[u][v]);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-#pragma unroll
-          for (int v = 0; v < 4; ++v) {
-            const double t2 = acc[u][v] + __shfl_xor(acc[u][v], 1, 64);
-            const double tot = t2 + __shfl_xor(t2, 2, 64);
-            const int r = 4 * bj + u, c = 4 * bk + v;
-            if (half == 0 && r < d && c <= r) Hs[r * DH + c] = tot + (r == c ? shift : 0.0);
-          }
+      for (int reg = 0; reg < 4; ++reg) {
+        const int col = 16 * C0 + c16, r0 = 16 * R0 + k4 + 4 * reg, r1 = 16 * R1 + k4 + 4 * reg;
+        if (col < d && r0 < d) Hs[r0 * DH + col] = acc0[reg] + (r0 == col ? shift : 0.0);
+        if (col < d && r1 < d) Hs[r1 * DH + col] = acc1[reg] + (r1 == col ? shift : 0.0);
       }
     }
     lds_barrier();
     if (TL && t == 0) tl[k * 5 + 2] = (long long)__builtin_amdgcn_s_memrealtime();
-    {  // Block Gauss-Jordan on [H | g] with 4 x 4 pivot blocks (SPD, no pivoting). Lane i of wave w
-       // keeps row i's columns j = w + 8c (c < 8) in registers; wave 0 also carries g_i. Block b
-       // (pivots p = 4b .. 4b + 3) has one column in each of four waves: they publish them into a
-       // double-buffered LDS slab, one barrier, then every lane eliminates the
-       // block from its row (rows above the block too, so no back substitution is left):
-       //   l_i = H[i][p:p+4] P^-1,  H[i][:] -= l_i H[p:p+4][:],  g_i -= l_i g[p:p+4]
-       // (P = the 4 x 4 pivot block, solved redundantly per lane by 2 x 2 blocks). Indices >= d are
-       // identity padding. A pivot row keeps row (i - p) of P^-1 for the final block solve.
+    if (refresh) {
+      // In-place block Gauss-Jordan INVERSION of the SPD Hessian with 4 x 4 pivot blocks, no
+      // pivoting. Lane i of wave w keeps row i's columns j = w + 8c in registers. Block K = p..p+3:
+      //   P = A_KK, Pi = P^-1;  non-pivot rows: L_i = A_iK Pi,  A_ij -= L_i A_Kj (j not in K),
+      //   A_iK = -L_i;  pivot rows: A_Kj = Pi A_Kj (j not in K),  A_KK = Pi.
+      // Only column K is published (slab[q][j] = A_{j, p+q}); the pivot ROWS follow from the
+      // structure of in-place Gauss-Jordan on a symmetric matrix: the processed / unprocessed cross
+      // blocks are antisymmetric (A_UP = -A_PU^T), the rest symmetric, so A_{p+q, j} = -slab[q][j] for
+      // already processed columns j < p and +slab[q][j] otherwise. Indices >= d: identity padding.
       const int i = lane;
-      double h[NCW];
 #pragma unroll
       for (int c = 0; c < NCW; ++c) {
         const int j = wid + NWV * c;
-        h[c] = (i < d && j < d) ? (j <= i ? Hs[i * DH + j] : Hs[j * DH + i]) : (i == j ? 1.0 : 0.0);
+        h[c] = (i < d && j < d) ? Hs[i * DH + j] : (i == j ? 1.0 : 0.0);
       }
-      double gi = (wid == 0 && i < d) ? gv[i] : 0.0;
-      double pr0 = 0.0, pr1 = 0.0, pr2 = 0.0, pr3 = 0.0;  // row (i mod 4) of this lane's pivot-block inverse
       const int nb = (d + 3) >> 2;
       for (int bb = 0; bb < nb; ++bb) {
         const int p = 4 * bb;
@@ -205,24 +210,23 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
         double P[4][4], R[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          R[q] = slab[q * 64 + i];  // H[i][p + q]
+          R[q] = slab[q * 64 + i];  // A[i][p + q]
 #pragma unroll
-          for (int r = 0; r < 4; ++r) P[q][r] = slab[q * 64 + p + r];  // H[p + r][p + q] (symmetric)
+          for (int r = 0; r < 4; ++r) P[q][r] = slab[q * 64 + p + r];  // A[p + r][p + q] (symmetric block)
         }
         const bool pivrow = (i >> 2) == bb;
-        if (pivrow) {  // solve with e_(i - p): the lane's row of P^-1
+        if (pivrow) {  // solve with e_(i - p): the lane's row of Pi
 #pragma unroll
           for (int q = 0; q < 4; ++q) R[q] = (q == (i & 3)) ? 1.0 : 0.0;
         }
-        // l = P^-1 R by 2 x 2 blocks P = [A B; B^T D] (the same on every lane): A^-1 and the Schur
-        // complement S = D - B^T A^-1 B inverted by their determinants. The dependent chain is ~20
-        // f64 operations instead of ~35 for a 4 x 4 L D L^T: this solve sits on the critical path
-        // of every block, between the barrier and the row updates.
+        // l = Pi R by 2 x 2 blocks P = [A B; B^T D] (the same on every lane): A^-1 and the Schur
+        // complement S = D - B^T A^-1 B inverted by their determinants (a short dependent chain on
+        // the critical path of every block, between the barrier and the row updates)
         auto rcp = [](double v) {  // v_rcp_f64 (~2^-29) + one Newton-Raphson step (~2^-58)
           const double r = __builtin_amdgcn_rcp(v);
           return fma(r, fma(-v, r, 1.0), r);
         };
-        const double a00 = P[0][0], a01 = P[1][0], a11 = P[1][1];  // lower entries, as published
+        const double a00 = P[0][0], a01 = P[1][0], a11 = P[1][1];
         const double ia = rcp(fma(a00, a11, -a01 * a01));
         const double A00 = a11 * ia, A01 = -a01 * ia, A11 = a00 * ia;  // A^-1
         const double b00 = P[2][0], b01 = P[3][0], b10 = P[2][1], b11 = P[3][1];  // B[i][j] = P[j + 2][i]
@@ -236,49 +240,65 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
         const double z2 = R[2] - fma(b00, y0, b10 * y1), z3 = R[3] - fma(b01, y0, b11 * y1);
         const double l2 = fma(s11, z2, -s01 * z3) * is, l3 = fma(s00, z3, -s01 * z2) * is;  // S^-1 z
         const double l0 = y0 - fma(w00, l2, w01 * l3), l1 = y1 - fma(w10, l2, w11 * l3);
-        double f0 = l0, f1 = l1, f2 = l2, f3 = l3;
-        if (pivrow) {
-          pr0 = l0;
-          pr1 = l1;
-          pr2 = l2;
-          pr3 = l3;
-          f0 = f1 = f2 = f3 = 0.0;  // pivot rows are not eliminated by their own block
-        }
+        const double l[4] = {l0, l1, l2, l3};
 #pragma unroll
         for (int c = 0; c < NCW; ++c) {
-          const int j = wid + NWV * c;  // H[p + q][j] = H[j][p + q] for the trailing columns j >= p + 4
-          double v = h[c];
-          v = fma(-f0, slab[0 * 64 + j], v);
-          v = fma(-f1, slab[1 * 64 + j], v);
-          v = fma(-f2, slab[2 * 64 + j], v);
-          v = fma(-f3, slab[3 * 64 + j], v);
-          h[c] = v;  // columns j < p + 4 are done: updating them too is harmless and branch-free
-        }
-        if (wid == 0) {
-          const double g0 = readlane_f64(gi, p), g1 = readlane_f64(gi, p + 1), g2 = readlane_f64(gi, p + 2),
-                       g3 = readlane_f64(gi, p + 3);
-          gi = fma(-f0, g0, fma(-f1, g1, fma(-f2, g2, fma(-f3, g3, gi))));
+          const int j = wid + NWV * c;
+          const double sg = j < p ? -1.0 : 1.0;  // A_{p+q, j} = sg * slab[q][j]
+          const double k0 = sg * slab[0 * 64 + j], k1 = sg * slab[1 * 64 + j], k2 = sg * slab[2 * 64 + j],
+                       k3 = sg * slab[3 * 64 + j];
+          const bool inK = (j >> 2) == bb;
+          double lj = l[0];
+#pragma unroll
+          for (int q = 1; q < 4; ++q) lj = ((j & 3) == q) ? l[q] : lj;
+          double v;
+          if (pivrow) {
+            v = inK ? lj : fma(l0, k0, fma(l1, k1, fma(l2, k2, l3 * k3)));  // (Pi A_Kj)_i, or Pi[i-p][j-p]
+          } else {
+            v = inK ? -lj : fma(-l0, k0, fma(-l1, k1, fma(-l2, k2, fma(-l3, k3, h[c]))));
+          }
+          h[c] = v;
         }
       }
-      lds_barrier();
-      if (TL && t == 0) tl[k * 5 + 3] = (long long)__builtin_amdgcn_s_memrealtime();
-      if (wid == 0) {
-        const bool in = lane < d;
-        const int q0 = lane & ~3;  // the lane's pivot block: dx = P^-1 g over the block
-        const double g0 = __shfl(gi, q0, 64), g1 = __shfl(gi, q0 + 1, 64), g2 = __shfl(gi, q0 + 2, 64),
-                     g3 = __shfl(gi, q0 + 3, 64);
-        const double r = in ? fma(pr0, g0, fma(pr1, g1, fma(pr2, g2, pr3 * g3))) : 0.0;  // dx
-        const double xo = in ? xv[lane] : 0.0;
-        const double xn = xo - (in ? r : 0.0);
-        if (in) xv[lane] = xn;
-        const double mdx = wave_max_f64(in ? fabs(r) : 0.0), mx = wave_max_f64(in ? fabs(xn) : 0.0);
-        if (lane == 0) conv_lds = (mdx < NEWTON_TOL * fmax(1.0, mx)) ? 1 : 0;
-      }
+      ++refreshed;
+    }
+    if (TL && t == 0) tl[k * 5 + 3] = (long long)__builtin_amdgcn_s_memrealtime();
+    {  // dx = H^-1 g: per-wave partials over the wave's 8 columns, summed in wave order by wave 0
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < NCW; ++c) s = fma(h[c], gv[wid + NWV * c], s);
+      pv[wid * 64 + lane] = s;
     }
     lds_barrier();
-    if (TL && t == 0) tl[k * 5 + 4] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (wid == 0) {
+      const bool in = lane < d;
+      double r = 0.0;
+#pragma unroll
+      for (int w = 0; w < NWV; ++w) r += pv[w * 64 + lane];
+      const double xo = in ? xv[lane] : 0.0;
+      const double xn = xo - (in ? r : 0.0);
+      if (in) xv[lane] = xn;
+      const double mdx = wave_max_f64(in ? fabs(r) : 0.0), mx = wave_max_f64(in ? fabs(xn) : 0.0);
+      if (lane == 0) {
+        conv_lds = (mdx < NEWTON_TOL * fmax(1.0, mx)) ? 1 : 0;
+        // chord steps reuse the inverse while they contract by at least `chord` per step
+        refresh_lds = (chord <= 0.0 || (!refresh && k > 0 && mdx > chord * nd_prev)) ? 1 : 0;
+      }
+      nd_prev = mdx;
+    }
+    lds_barrier();
+    if (TL && t == 0) tl[k * 5 + 4] = ((long long)__builtin_amdgcn_s_memrealtime() & ~1LL) | (refresh ? 1 : 0);
     used = k + 1;
     if (conv_lds) break;
+    refresh = refresh_lds != 0;
+  }
+  if (hg && refreshed && chord > 0.0) {  // keep the newest inverse for this worker's next solve
+#pragma unroll
+    for (int c = 0; c < NCW; ++c) hg[(c * NWV + wid) * 64 + lane] = h[c];
+    if (t == 0) {  // read by the next phase launch (kernel boundary: no fence needed)
+      hg[4097] = shift;
+      hg[4096] = 1.0;
+    }
   }
 
   {  // local objective lam/2 |x|^2 + sum_i softplus(-y_i z_i) at the new iterate
@@ -320,7 +340,7 @@ extern "C" {
 
 size_t gadmm_chain_newton_lds(int d, int m) {
   const int DP = (d + 3) & ~3, DH = d | 1;
-  return (size_t)(m * DP + d * DH + 14 * 64) * sizeof(double);
+  return (size_t)(m * DP + d * DH + 14 * 64 + NWV * 64) * sizeof(double);
 }
 
 // Launch one Newton phase (PhaseArgs.solver == 1, logistic model). d, m <= 64.

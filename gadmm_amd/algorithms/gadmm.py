@@ -235,14 +235,16 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     # one engine per (model, configuration) on a single rank: repeated solves (rho sweeps, benchmarks,
     # D-GADMM re-runs) reuse its device buffers, cached inverses and captured graph
     key = (kind, local_solver, n_total, tuple(int(w) for w in local_ids), float(rho), int(max_iter), block,
-           float(step), int(max_inner), float(inner_tol), float(getattr(model, "lam", 0.0)))
+           float(step), int(max_inner), float(inner_tol), float(getattr(model, "lam", 0.0)),
+           float(opts.get("chord", 0.02)))
     cache = getattr(model, "_chain_engines", None) if rcomm is None else None
     eng = cache.get(key) if cache is not None else None
     if eng is None:
         eng = NativeChainEngine(model.X, model.y, local_ids, n_total, kind, rho=rho, obj0=obj0, tol=tol,
                                 max_iter=max_iter, lam=getattr(model, "lam", 0.0), step=step, max_inner=max_inner,
                                 inner_tol=inner_tol, comm=rcomm, block=block, precomputed=pre,
-                                local_solver="newton" if local_solver == "newton" else "gd")
+                                local_solver="newton" if local_solver == "newton" else "gd",
+                                chord=float(opts.get("chord", 0.02)))
         if rcomm is None and opts.get("cache", True):
             if cache is None:
                 cache = {}

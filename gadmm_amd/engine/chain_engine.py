@@ -72,10 +72,12 @@ class NativeChainEngine:
                  model: str = "linear", rho: float = 1.0, obj0: float = 0.0, tol: float = 1e-4,
                  max_iter: int = 1000, lam: float = 0.0, step: float = 0.0, max_inner: int = 100,
                  inner_tol: float = 1e-4, comm=None, block: int = 16, stream: Optional[torch.cuda.Stream] = None,
-                 precomputed=None, force_monitor: bool = False, obj_mode: str = "exact", local_solver: str = "gd"):
+                 precomputed=None, force_monitor: bool = False, obj_mode: str = "exact", local_solver: str = "gd",
+                 chord: float = 0.02):
         """``local_solver`` (logistic): "gd" = the reference's inexact inner GD (logReg_GD.m, step /
         max_inner / inner_tol), "newton" = exact local solves (group_ADMM_logistic.m semantics,
-        csrc/kernels/chain_newton.hip; d, m <= 64)."""
+        csrc/kernels/chain_newton.hip; d, m <= 64). ``chord`` (newton): a worker reuses its last
+        inverse Hessian while steps contract by at least this factor (0: refresh every step)."""
         if not X_loc.is_cuda:
             raise ValueError("NativeChainEngine runs on a HIP device; use the torch algorithms on CPU")
         # the kernels read raw f64 pointers: anything else (e.g. float32 labels from torch.where) would be
@@ -132,6 +134,10 @@ class NativeChainEngine:
             self.A = self.b = self.yy = self.Minv = None
             self.X = self.Y = None
             self.rbuf = None
+            # Newton: per-worker inverse Hessian store (register image + valid flag + shift)
+            self.hinv = torch.zeros((nl, 64 * 64 + 8), dtype=f64, device=dev) \
+                if local_solver == "newton" and nl > 0 else None
+            self.chord = float(chord)
             if d > 256:
                 stride = int(native.require().gadmm_chain_big_rbuf_stride(d))
                 self.rbuf = torch.zeros((max(nl, 1) * stride,), dtype=f64, device=dev)
@@ -156,7 +162,7 @@ class NativeChainEngine:
         for i, v in enumerate(self.deg_to_var if model == "linear" else (0, 0, 0)):
             args.deg_to_var[i] = v
         args.model = native.MODEL_LINEAR if model == "linear" else native.MODEL_LOGISTIC
-        args.Minv = native.ptr(self.Minv)
+        args.Minv = native.ptr(self.Minv if self.hinv is None else self.hinv)
         args.A = native.ptr(self.A)
         args.b = native.ptr(self.b)
         args.yy = native.ptr(self.yy)
@@ -175,6 +181,8 @@ class NativeChainEngine:
         args.m = self.m
         args.max_inner = int(max_inner)
         args.lam, args.step, args.inner_tol = float(lam), float(step), float(inner_tol)
+        if local_solver == "newton":
+            args.step = self.chord  # the Newton kernel's chord contraction threshold
         args.inner_iters = self.inner_iters.data_ptr()
         args.rbuf = native.ptr(self.rbuf)
         args.obj_mode = 0 if obj_mode == "exact" else 1
@@ -302,6 +310,9 @@ class NativeChainEngine:
         if self.xport:  # new solve: the transport's tags of the previous one stop matching (every rank)
             native.check(self.lib.gadmm_ipc_new_epoch(self.xport, self.stream.cuda_stream), "ipc_new_epoch")
         native.check(self.lib.gadmm_write_stamp(self.t0stamp.data_ptr(), self.stream.cuda_stream), "write_stamp")
+        if self.hinv is not None and zero_state:  # a new solve starts from fresh Hessians
+            with torch.cuda.stream(self.stream):
+                self.hinv[:, 64 * 64].zero_()
         if zero_state:  # theta = mu = part = 0, trace = NaN and the control block: one launch
             native.check(self.lib.gadmm_chain_reset_state(
                 self.ctl.data_ptr(), int(start_iter), int(pending), self.theta.data_ptr(), self.theta.numel(),

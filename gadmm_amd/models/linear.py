@@ -107,8 +107,10 @@ class LinearRegression:
 
     # ---- global oracle ----------------------------------------------------------------------------
     def optimum(self, comm=None, n_total=None) -> float:
-        """Optimal objective of the stacked problem: ``(sum A_n)^{-1} sum b_n`` (one-time all-reduce
-        of the d x d Gram)."""
+        """Optimal objective of the stacked problem: ``x = (sum A_n)^{-1} sum b_n`` (one-time all-reduce
+        of the d x d Gram), evaluated as ``1/2 ||X x - y||^2`` from the raw rows, as
+        ``opt_sol_closedForm.m:2-3`` does (the quadratic form ``x'Ax/2 - b'x + y'y/2`` cancels badly:
+        ~1e-10 absolute on the E1 problem, more than the margin of its 1e-8 stop)."""
         As = self.A.sum(0)
         bs = self.b.sum(0)
         yy = self.yy.sum()
@@ -122,7 +124,11 @@ class LinearRegression:
         eye = torch.eye(self.d, dtype=As.dtype, device=As.device)
         lam_tot = self.lam * (n_total if n_total is not None else self.n_local)
         x = _spd_solve(As + lam_tot * eye, bs)
-        return float(0.5 * x @ (As @ x) - bs @ x + 0.5 * yy + 0.5 * lam_tot * (x @ x))
+        r = torch.matmul(self.X.to(x.dtype), x) - self.y.to(x.dtype)  # (n_loc, m) residuals
+        f = (0.5 * (r * r).sum()).reshape(1)
+        if comm is not None and comm.nranks > 1:
+            comm.allreduce_sum(f)
+        return float(f.item() + 0.5 * lam_tot * (x @ x).item())
 
     def optimum_point(self, comm=None) -> torch.Tensor:
         As, bs = self.A.sum(0), self.b.sum(0)

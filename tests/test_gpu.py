@@ -179,15 +179,17 @@ def test_engine_logistic(log24, log_obj0):
     assert eng.run(use_graph=False).iters == 53
 
 
-def test_logistic_newton_kernel_matches_torch(log24, log_obj0):
-    """Exact local solves on the device (chain_newton.hip: Newton with an in-LDS L D L^T factorisation,
-    SURVEY.md D2) vs the torch Newton path on the same device: the 1e-8 gap at the same iteration and
-    objective traces equal to ~1e-12."""
+@pytest.mark.parametrize("chord", [0.0, 0.02, 0.1])
+def test_logistic_newton_kernel_matches_torch(log24, log_obj0, chord):
+    """Exact local solves on the device (chain_newton.hip: MFMA Hessian, in-place block Gauss-Jordan
+    inverse; chord = 0: a fresh inverse every Newton step, chord > 0: the worker's cached inverse is
+    reused while steps contract by that factor) vs the torch Newton path on the same device: the
+    1e-8 gap at the same iteration and objective traces equal to ~1e-12."""
     import time
     from gadmm_amd.models import LogisticRegression
     from gadmm_amd.algorithms.gadmm import group_admm_logistic_exact
     m = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
-    a = group_admm_logistic_exact(m, 1e-3, log_obj0, 1e-8, 1000)
+    a = group_admm_logistic_exact(m, 1e-3, log_obj0, 1e-8, 1000, engine_opts={"chord": chord, "cache": False})
     assert a.extra["backend"] == "native" and a.extra["solver"] == "newton"
     eng = a.extra["engine_obj"]
     used = eng.inner_iters.cpu().numpy()
@@ -198,7 +200,8 @@ def test_logistic_newton_kernel_matches_torch(log24, log_obj0):
     assert b.extra["backend"] == "torch"
     assert a.iters == b.iters == 424 and a.converged and b.converged
     np.testing.assert_allclose(a.obj, b.obj, rtol=1e-12, atol=0)
-    print("newton: native %.1f ms, torch %.1f ms, %d iterations" % (a.wall_s * 1e3, t_torch * 1e3, a.iters))
+    print("newton(chord=%g): native %.1f ms, torch %.1f ms, %d iterations"
+          % (chord, a.wall_s * 1e3, t_torch * 1e3, a.iters))
 
 
 @pytest.mark.parametrize("n,m,d", [(5, 36, 34), (4, 25, 14), (3, 64, 64), (6, 7, 3)])
