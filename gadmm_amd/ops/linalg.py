@@ -3,14 +3,16 @@
 * ``gram(X, y)``: per-worker ``A = X^T X``, ``b = X^T y``, ``yy = y^T y`` (kernel K1: one f64-MFMA
   SYRK of the augmented shard ``[X | y]``, csrc/kernels/gram.hip).
 * ``spd_inverse(A, shifts)``: ``(A_n + s_{n,v} I)^{-1}`` for every worker n and shift v
-  (kernel K2: in-LDS Gauss-Jordan for d <= 128, csrc/kernels/spd_inverse.hip; rocSOLVER Cholesky
-  for larger d, which is one-time set-up).
+  (kernel K2: in-LDS Gauss-Jordan for d <= 128, csrc/kernels/spd_inverse.hip; blocked Gauss-Jordan
+  with f64-MFMA rank-128 updates for larger d, csrc/kernels/spd_inverse_blocked.hip. One-time set-up;
+  ``GADMM_BIGINV=rocsolver`` selects torch's Cholesky + cholesky_inverse instead, for A/B runs).
 
 CUDA tensors always take the native path (and raise if the library is missing); CPU tensors use
 torch, which is also the fp64 reference the kernels are tested against.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional, Tuple
 
 import torch
@@ -81,6 +83,8 @@ def spd_inverse(A: torch.Tensor, shifts: torch.Tensor, out: Optional[torch.Tenso
         shifts = shifts.contiguous()
     N, d, _ = A.shape
     V = shifts.shape[1]
+    if A.is_cuda and d > 128 and os.environ.get("GADMM_BIGINV", "native") != "rocsolver":
+        return spd_inverse_blocked(A, shifts, out=out, check_status=check_status, status=status)
     if not A.is_cuda or d > 128:
         res = spd_inverse_torch(A, shifts)
         if out is not None:
@@ -98,3 +102,37 @@ def spd_inverse(A: torch.Tensor, shifts: torch.Tensor, out: Optional[torch.Tenso
     if check_status and int(status.item()) != 0:
         raise FloatingPointError("spd_inverse: matrix is not positive definite")
     return out
+
+
+def spd_inverse_blocked(A: torch.Tensor, shifts: torch.Tensor, out: Optional[torch.Tensor] = None, nb: int = 128,
+                        check_status: bool = True, status: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Large-d ``(N, V, d, d)`` inverses of ``A_n + shifts[n, v] I`` on the device: blocked in-place
+    Gauss-Jordan, f64-MFMA rank-``nb`` updates (csrc/kernels/spd_inverse_blocked.hip)."""
+    lib = native.require()
+    shifts = torch.as_tensor(shifts, dtype=torch.float64)
+    if shifts.dim() == 1:
+        shifts = shifts.unsqueeze(0).expand(A.shape[0], -1)
+    N, d, _ = A.shape
+    V = shifts.shape[1]
+    sh = shifts.detach().to("cpu", torch.float64).contiguous()  # set-up: scalars by value per launch
+    if out is None:
+        out = torch.empty((N, V, d, d), dtype=torch.float64, device=A.device)
+    ws = torch.zeros((int(lib.gadmm_spd_inverse_blocked_workspace(d, nb)),), dtype=torch.float64, device=A.device)
+    if status is None:
+        status = torch.zeros((1,), dtype=torch.int32, device=A.device)
+    rc = lib.gadmm_spd_inverse_blocked_f64(A.contiguous().data_ptr(), sh.data_ptr(), N, d, V, out.data_ptr(),
+                                           ws.data_ptr(), status.data_ptr(), nb, native.stream_handle())
+    native.check(rc, "spd_inverse_blocked_f64")
+    if check_status and int(status.item()) != 0:
+        raise FloatingPointError("spd_inverse: matrix is not positive definite")
+    return out
+
+
+def gemm_f64(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
+    """``A @ B`` (row-major f64) with the MFMA tile kernel of the blocked inverse (tests)."""
+    lib = native.require()
+    A, B = A.contiguous(), B.contiguous()
+    C = torch.empty((A.shape[0], B.shape[1]), dtype=torch.float64, device=A.device)
+    native.check(lib.gadmm_gemm_f64_test(A.shape[0], B.shape[1], A.shape[1], A.data_ptr(), B.data_ptr(),
+                                         C.data_ptr(), native.stream_handle()), "gemm_f64_test")
+    return C

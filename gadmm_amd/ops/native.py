@@ -137,6 +137,10 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_gram_pick_ksplit": (c_int, [c_int, c_int, c_int]),
         "gadmm_spd_inverse_small_f64": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
                                                 c_void_p]),
+        "gadmm_spd_inverse_blocked_workspace": (c_long, [c_int, c_int]),
+        "gadmm_spd_inverse_blocked_f64": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                                  c_void_p, c_int, c_void_p]),
+        "gadmm_gemm_f64_test": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
         "gadmm_chain_phase": (c_int, [ctypes.POINTER(PhaseArgs), c_void_p]),
         "gadmm_chain_reset": (c_int, [c_void_p, c_int, c_int, c_void_p]),
         "gadmm_chain_reset_state": (c_int, [c_void_p, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p,

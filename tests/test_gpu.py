@@ -532,3 +532,35 @@ def test_native_run_checkpoint_resumes_in_torch_path(lin24, lin_obj0, tmp_path):
     ref = chain_admm(m, list(range(24)), 24, 3.0, lin_obj0, 1e-30, nxt + 49, backend="torch")
     assert len(b.obj) == 50
     assert np.allclose(b.obj, ref.obj[nxt - 1:nxt + 49], rtol=1e-10)
+
+
+@pytest.mark.parametrize("M,N,K", [(100, 70, 33), (256, 192, 128), (1, 5, 3), (130, 1, 64)])
+def test_gemm_f64_mfma_matches_torch(M, N, K):
+    """The f64-MFMA tile GEMM of the blocked inverse (spd_inverse_blocked.hip) vs torch fp64."""
+    from gadmm_amd.ops.linalg import gemm_f64
+    g = torch.Generator().manual_seed(M * 1000 + N + K)
+    A = torch.randn(M, K, dtype=torch.float64, generator=g)
+    B = torch.randn(K, N, dtype=torch.float64, generator=g)
+    C = gemm_f64(A.to(DEV), B.to(DEV)).cpu()
+    ref = A @ B
+    assert torch.allclose(C, ref, rtol=1e-13, atol=1e-13 * float(ref.abs().max()))
+
+
+@pytest.mark.parametrize("d", [129, 200, 300, 520])
+def test_spd_inverse_blocked_matches_fp64_reference(d):
+    """K2 for d > 128: blocked Gauss-Jordan with MFMA rank-128 updates (last block partial for d not a
+    multiple of 128) vs the fp64 Cholesky inverse, 2 workers x 2 shifts."""
+    from gadmm_amd.ops.linalg import spd_inverse_blocked, spd_inverse_torch
+    g = torch.Generator().manual_seed(d)
+    X = torch.randn(2, 2 * d, d, dtype=torch.float64, generator=g)
+    A = torch.bmm(X.transpose(1, 2), X) / (2 * d)
+    shifts = torch.tensor([[0.3, 0.6], [0.1, 1.0]], dtype=torch.float64)
+    out = spd_inverse_blocked(A.to(DEV), shifts).cpu()
+    ref = spd_inverse_torch(A, shifts)
+    assert torch.allclose(out, ref, rtol=1e-11, atol=1e-11 * float(ref.abs().max()))
+    assert torch.equal(out, out.transpose(-1, -2))
+    eye = torch.eye(d, dtype=torch.float64)
+    for n in range(2):
+        for v in range(2):
+            M = A[n] + shifts[n, v] * eye
+            assert float((M @ out[n, v] - eye).abs().max()) < 1e-11
