@@ -79,6 +79,9 @@ struct PhaseArgs {
   int n_total, pad_nt;
   const int* lgid;     // [n_local] global worker id of each local row
   long long* tstamp;   // optional [max_iter] s_memrealtime (100 MHz) when each iteration was decided
+  // optional K4 primal residual: every tail writes ||th_l - th||^2 + ||th - th_r||^2 of iteration it
+  // (its two chain edges; each edge has exactly one tail end) into rres[(it - 1) * n_total + gid]
+  double* rres;        // [max_iter][n_total] or null
 };
 
 // Engine construction arguments (Python mirrors it in gadmm_amd/ops/native.py).
@@ -157,4 +160,5 @@ struct PersistArgs {
   // neighbours read theta^j as their previous-iteration value); peer_thg[r] is rank r's table
   const unsigned* ep_push;  // [n_epochs][n_local] rank bitmask (own rank excluded)
   u32x4* const* peer_thg;   // [nranks]
+  double* rres;             // optional K4 primal residual [max_iter][n] (see PhaseArgs::rres; owned tails)
 };

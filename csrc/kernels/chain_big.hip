@@ -142,7 +142,7 @@ __global__ void __launch_bounds__(1024) chain_big_post(PhaseArgs a) {
   const double* th = a.theta;
   const double* r = a.rbuf + s.li * rstride(a.d);
   const double crho = s.deg * a.rho;
-  double part = 0.0;
+  double part = 0.0, rpart = 0.0;
   for (long j = threadIdx.x; j < d; j += blockDim.x) {
     const double t = th[s.gid * d + j];
     if (a.flags & PH_POST_DUAL) {
@@ -150,8 +150,17 @@ __global__ void __launch_bounds__(1024) chain_big_post(PhaseArgs a) {
       if (s.left >= 0) m = m - a.rho * (th[s.left * d + j] - t);
       if (s.right >= 0) m = m + a.rho * (t - th[s.right * d + j]);
       a.mu[s.li * d + j] = m;
+      if (a.rres) {  // K4 primal residual of the tail's two edges
+        if (s.left >= 0) rpart = fma(th[s.left * d + j] - t, th[s.left * d + j] - t, rpart);
+        if (s.right >= 0) rpart = fma(t - th[s.right * d + j], t - th[s.right * d + j], rpart);
+      }
     }
     if (a.obj_mode != 0) part += (0.5 * (r[j] - crho * t) - a.b[s.li * d + j]) * t;
+  }
+  if (a.rres && (a.flags & PH_POST_DUAL)) {
+    const double rs = block_sum_f64(rpart, scratch);
+    if (threadIdx.x == 0 && it - 1 < a.max_iter) a.rres[(long)(it - 1) * a.n_total + s.gid] = rs;
+    __syncthreads();  // scratch is reused below
   }
   double f;
   if (a.obj_mode != 0) {

@@ -415,6 +415,13 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
                              make_tag(a.epoch, it), th);
         if (xnext) publish(it);
       }
+      if (a.rres && owned) {  // K4 primal residual of the tail's two edges (after the publish)
+        double rp = 0.0;
+        if (in && has_l) rp = fma(tl - tn, tl - tn, rp);
+        if (in && has_r) rp = fma(tn - tr, tn - tr, rp);
+        const double rs = wave_sum_f64(rp);
+        if (lane == 0 && it - 1 < a.max_iter) a.rres[(long)(it - 1) * n + w] = rs;
+      }
       if (tstamp) tt[3] = (long long)now_ticks();
     } else if (active && owned && xnext) {  // heads: theta^it and the (still pending) mu are final
       if (in) publish(it);
@@ -675,6 +682,13 @@ __global__ void __launch_bounds__(64 * PWW) chain_blocked_pair_kernel(PersistArg
         store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + pT) * d + lane) * 16),
                            make_tag(a.epoch, it), thT);
         if (xnext) publish(it, pT, thT, muT);
+      }
+      if (a.rres && ownT) {  // K4 primal residual of the tail's two edges
+        double rp = 0.0;
+        if (in && hlT) rp = fma(tl - tn, tl - tn, rp);
+        if (in && hrT) rp = fma(tn - tr, tn - tr, rp);
+        const double rs = wave_sum_f64(rp);
+        if (lane == 0 && it - 1 < a.max_iter) a.rres[(long)(it - 1) * n + slT.gid] = rs;
       }
     }
     if (ownH && xnext && in) publish(it, pH, thH, muH);  // theta^it and the (still pending) mu are final

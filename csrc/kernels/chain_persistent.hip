@@ -339,12 +339,21 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       }
       if (TL) t_pub = (long long)now_ticks();
       if (!head) {  // tails: both neighbours are this iteration's heads -> dual update now
+        double rp = 0.0;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
           double m = mu[c];
           if (left >= 0) m = m - rho * (tl[c] - tn[c]);
           if (right >= 0) m = m + rho * (tn[c] - tr[c]);
           mu[c] = m;
+          if (a.rres && lane + 64 * c < d) {  // K4 primal residual of the tail's two edges
+            if (left >= 0) rp = fma(tl[c] - tn[c], tl[c] - tn[c], rp);
+            if (right >= 0) rp = fma(tn[c] - tr[c], tn[c] - tr[c], rp);
+          }
+        }
+        if (a.rres) {
+          const double rs = wave_sum_f64(rp);
+          if (lane == 0 && it - 1 < a.max_iter) a.rres[(long)(it - 1) * n + w] = rs;
         }
       } else {
         pending = 1;

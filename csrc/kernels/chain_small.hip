@@ -123,6 +123,7 @@ __global__ void __launch_bounds__(NT) chain_phase_linear(PhaseArgs a) {
   const double* Mi = a.Minv + ((long)sl.li * a.nvar + a.deg_to_var[deg]) * (long)d * d;
   symv_cols<NC>(Mi, sh_r, sh_t, red, d);
   double* thw_out = th + (long)sl.gid * d;
+  double rpart = 0.0;
   for (int j = threadIdx.x; j < d; j += NT) {
     const double t = sh_t[j];
     thw_out[j] = t;
@@ -131,7 +132,16 @@ __global__ void __launch_bounds__(NT) chain_phase_linear(PhaseArgs a) {
       if (thl) m = m - rho * (thl[j] - t);
       if (thr) m = m + rho * (t - thr[j]);
       mu[j] = m;
+      if (a.rres) {  // K4 primal residual of the tail's two edges
+        if (thl) rpart = fma(thl[j] - t, thl[j] - t, rpart);
+        if (thr) rpart = fma(t - thr[j], t - thr[j], rpart);
+      }
     }
+  }
+  if (a.rres && (a.flags & PH_POST_DUAL)) {
+    const double rs = block_sum_f64(rpart, scratch);
+    if (threadIdx.x == 0 && it - 1 < a.max_iter) a.rres[(long)(it - 1) * a.n_total + sl.gid] = rs;
+    __syncthreads();  // scratch is reused by the objective's block sum
   }
   if (a.flags & PH_OBJ) {
     symv_cols<NC>(a.A + (long)sl.li * d * d, sh_t, sh_q, red, d);

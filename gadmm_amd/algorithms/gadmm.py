@@ -236,7 +236,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     # D-GADMM re-runs) reuse its device buffers, cached inverses and captured graph
     key = (kind, local_solver, n_total, tuple(int(w) for w in local_ids), float(rho), int(max_iter), block,
            float(step), int(max_inner), float(inner_tol), float(getattr(model, "lam", 0.0)),
-           float(opts.get("chord", 0.02)))
+           float(opts.get("chord", 0.02)), bool(opts.get("residual", True)))
     cache = getattr(model, "_chain_engines", None) if rcomm is None else None
     eng = cache.get(key) if cache is not None else None
     if eng is None:
@@ -244,7 +244,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
                                 max_iter=max_iter, lam=getattr(model, "lam", 0.0), step=step, max_inner=max_inner,
                                 inner_tol=inner_tol, comm=rcomm, block=block, precomputed=pre,
                                 local_solver="newton" if local_solver == "newton" else "gd",
-                                chord=float(opts.get("chord", 0.02)))
+                                chord=float(opts.get("chord", 0.02)), residual=bool(opts.get("residual", True)))
         if rcomm is None and opts.get("cache", True):
             if cache is None:
                 cache = {}
@@ -353,6 +353,13 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         dist.broadcast(buf, src=0, group=getattr(comm, "control_group", None))
         tr, tt = buf[0].numpy().copy(), buf[1].numpy().copy()
     loss = np.abs(tr - obj0)
+    pres = eng.primal_residual(iters)  # K4, emitted by the kernels' tails (this rank's edges)
+    if pres is not None and comm.nranks > 1:
+        import torch.distributed as dist
+
+        buf = torch.from_numpy(pres.astype(np.float64))
+        dist.all_reduce(buf, group=getattr(comm, "control_group", None))
+        pres = buf.numpy()
     bytes_tot = p2p
     if comm.nranks > 1:
         import torch.distributed as dist
@@ -364,6 +371,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
                     time_trace=tt,  # measured on the device: decision time of each iteration
                     comm_units=np.arange(1, iters + 1, dtype=np.float64) * n_total,
                     com_cost=np.asarray(com_cost[:iters]), bytes_sent=int(p2p), bytes_total=bytes_tot,
+                    primal_res=pres,
                     extra={"backend": "native", "engine": engine_kind, "rank": rank, "nranks": comm.nranks,
                            "solver": local_solver, "monitor_bytes": int(mon), "wire_bytes": int(wire),
                            "transport": getattr(comm, "backend", "local") if fabric is None else "xgmi"})

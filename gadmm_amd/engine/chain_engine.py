@@ -73,11 +73,13 @@ class NativeChainEngine:
                  max_iter: int = 1000, lam: float = 0.0, step: float = 0.0, max_inner: int = 100,
                  inner_tol: float = 1e-4, comm=None, block: int = 16, stream: Optional[torch.cuda.Stream] = None,
                  precomputed=None, force_monitor: bool = False, obj_mode: str = "exact", local_solver: str = "gd",
-                 chord: float = 0.02):
+                 chord: float = 0.02, residual: bool = False):
         """``local_solver`` (logistic): "gd" = the reference's inexact inner GD (logReg_GD.m, step /
         max_inner / inner_tol), "newton" = exact local solves (group_ADMM_logistic.m semantics,
         csrc/kernels/chain_newton.hip; d, m <= 64). ``chord`` (newton): a worker reuses its last
-        inverse Hessian while steps contract by at least this factor (0: refresh every step)."""
+        inverse Hessian while steps contract by at least this factor (0: refresh every step).
+        ``residual``: the kernels also emit the K4 primal residual (sum over chain edges of
+        ||theta_n - theta_right||^2) per iteration, read back by ``primal_residual``."""
         if not X_loc.is_cuda:
             raise ValueError("NativeChainEngine runs on a HIP device; use the torch algorithms on CPU")
         # the kernels read raw f64 pointers: anything else (e.g. float32 labels from torch.where) would be
@@ -138,6 +140,8 @@ class NativeChainEngine:
             self.hinv = torch.zeros((nl, 64 * 64 + 8), dtype=f64, device=dev) \
                 if local_solver == "newton" and nl > 0 else None
             self.chord = float(chord)
+            # K4 primal residual: per (iteration, worker) contributions of the tails (owned rows only)
+            self.rres = torch.zeros((self.max_iter * self.n_total,), dtype=f64, device=dev) if residual else None
             if d > 256:
                 stride = int(native.require().gadmm_chain_big_rbuf_stride(d))
                 self.rbuf = torch.zeros((max(nl, 1) * stride,), dtype=f64, device=dev)
@@ -190,6 +194,7 @@ class NativeChainEngine:
         args.n_total = self.n_total
         args.lgid = self.lgid.data_ptr()
         args.tstamp = self.tstamp.data_ptr()
+        args.rres = native.ptr(self.rres)
         desc = native.EngineDesc()
         desc.base = args
         desc.d_slots = self.slots.data_ptr()
@@ -313,6 +318,9 @@ class NativeChainEngine:
         if self.hinv is not None and zero_state:  # a new solve starts from fresh Hessians
             with torch.cuda.stream(self.stream):
                 self.hinv[:, 64 * 64].zero_()
+        if self.rres is not None and zero_state:  # a row's non-tail entries stay 0
+            with torch.cuda.stream(self.stream):
+                self.rres.zero_()
         if zero_state:  # theta = mu = part = 0, trace = NaN and the control block: one launch
             native.check(self.lib.gadmm_chain_reset_state(
                 self.ctl.data_ptr(), int(start_iter), int(pending), self.theta.data_ptr(), self.theta.numel(),
@@ -491,6 +499,7 @@ class NativeChainEngine:
         pa.dec_push = dec_push.data_ptr()
         pa.trace, pa.ctl = self.trace.data_ptr(), self.ctl.data_ptr()
         pa.tstamp = self.tstamp.data_ptr()
+        pa.rres = native.ptr(self.rres)
         ep_keep = None
         if epochs is not None:
             if isinstance(epochs, tuple) and len(epochs) == 2 and isinstance(epochs[1], np.ndarray):
@@ -626,6 +635,14 @@ class NativeChainEngine:
         t = self.tstamp[:upto].cpu().numpy().astype(np.int64)
         t0 = int(self.t0stamp.cpu().item())
         return np.where(t > 0, (t - t0) * 1e-8, 0.0)
+
+    def primal_residual(self, upto: int) -> Optional[np.ndarray]:
+        """This rank's part of the K4 primal residual of iterations 1..upto (sum over the chain edges
+        whose tail end it owns of ||theta_l - theta||^2 + ||theta - theta_r||^2, summed in worker
+        order); None unless the engine was built with ``residual=True``. Ranks' parts add up."""
+        if self.rres is None or upto <= 0:
+            return None
+        return self.rres[: upto * self.n_total].view(upto, self.n_total).cpu().numpy().sum(axis=1)
 
     def graph_ok(self) -> bool:
         return bool(self.lib.gadmm_chain_engine_graph_ok(self.handle))

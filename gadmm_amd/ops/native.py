@@ -55,6 +55,7 @@ class PhaseArgs(ctypes.Structure):
         ("inner_iters", c_void_p),
         ("rbuf", c_void_p), ("obj_mode", c_int), ("solver", c_int),
         ("n_total", c_int), ("pad_nt", c_int), ("lgid", c_void_p), ("tstamp", c_void_p),
+        ("rres", c_void_p),
     ]
 
 
@@ -103,7 +104,7 @@ class PersistArgs(ctypes.Structure):
         ("blk_tab", c_void_p), ("epoch_start", c_void_p), ("ep_slots", c_void_p), ("ep_pos", c_void_p),
         ("seg_lo", c_int), ("seg_hi", c_int), ("blk_npeer", c_int), ("dbg", c_int),
         ("blk_peer_lo", c_int * 8), ("blk_peer_hi", c_int * 8), ("blk_peer_tab", c_void_p),
-        ("tstamp", c_void_p), ("ep_push", c_void_p), ("peer_thg", c_void_p),
+        ("tstamp", c_void_p), ("ep_push", c_void_p), ("peer_thg", c_void_p), ("rres", c_void_p),
     ]
 
 

@@ -564,3 +564,37 @@ def test_spd_inverse_blocked_matches_fp64_reference(d):
         for v in range(2):
             M = A[n] + shifts[n, v] * eye
             assert float((M @ out[n, v] - eye).abs().max()) < 1e-11
+
+
+@pytest.mark.parametrize("mode", ["blocked", "per-worker", "graph"])
+def test_native_primal_residual_matches_torch(lin24, lin_obj0, mode, monkeypatch):
+    """K4 on the device: the tails of every native engine (temporally blocked / per-worker persistent
+    kernel, graph-replayed phases) emit ||th_l - th||^2 + ||th - th_r||^2; the per-iteration sum over
+    chain edges equals the torch path's primal residual trace."""
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import chain_admm
+    if mode == "per-worker":
+        monkeypatch.setenv("GADMM_BLOCKED", "0")
+    m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
+    opts = {"cache": False, "persistent": mode != "graph"}
+    a = chain_admm(m, list(range(24)), 24, 3.0, lin_obj0, 1e-8, 3000, engine_opts=opts)
+    assert a.extra["backend"] == "native" and a.iters == 1373
+    assert (a.extra["engine"] == "graph") == (mode == "graph")
+    b = chain_admm(m, list(range(24)), 24, 3.0, lin_obj0, 1e-8, 3000, backend="torch")
+    assert a.primal_res is not None and len(a.primal_res) == 1373
+    np.testing.assert_allclose(a.primal_res, b.primal_res[:1373], rtol=1e-6, atol=1e-12 * float(b.primal_res.max()))
+
+
+def test_native_primal_residual_large_d():
+    """K4 from chain_big_post (d > 256, row-blocked phases) vs the torch path."""
+    from gadmm_amd.data import gaussian_regression
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import chain_admm
+    ds = gaussian_regression(4, 400, 300, seed=3, labels="linear")
+    m = LinearRegression(ds.X.to(DEV), ds.y.to(DEV))
+    mc = LinearRegression(ds.X, ds.y)
+    obj0 = mc.optimum()
+    a = chain_admm(m, list(range(4)), 4, 50.0, obj0, 1e-300, 40, engine_opts={"cache": False})
+    b = chain_admm(mc, list(range(4)), 4, 50.0, obj0, 1e-300, 40)
+    assert a.extra["backend"] == "native" and a.iters == b.iters == 40
+    np.testing.assert_allclose(a.primal_res, b.primal_res, rtol=1e-8)

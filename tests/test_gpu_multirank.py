@@ -46,7 +46,7 @@ def _ipc_linear_rank(rank, world, n, rho, tol):
         r = chain_admm(m, loc, n, rho, obj0, tol, 3000, comm=comm, placement=pl,
                        engine_opts={"persistent": False, "state": False})
         out.append((r.iters, r.converged, r.extra["engine"], r.bytes_sent, r.extra["wire_bytes"]))
-    res = {"runs": out, "trace": r.obj.tolist(), "times": r.time_trace.tolist(),
+    res = {"runs": out, "trace": r.obj.tolist(), "times": r.time_trace.tolist(), "pres": r.primal_res.tolist(),
            "theta": r.extra["engine_obj"].local_theta().cpu().numpy(), "local": loc}
     r.extra["engine_obj"].close()
     comm.close()
@@ -63,6 +63,8 @@ def test_ipc_transport_graph_engine_bit_identical(world, lin24):
     for r in res:
         assert all(it == 1373 and conv and eng == "graph" for it, conv, eng, _, _ in r["runs"]), r["runs"]
         assert np.array_equal(np.asarray(r["trace"]), single.obj)
+        # K4 residual: every rank's tails' edges, all-reduced == the one-rank engine's
+        np.testing.assert_allclose(np.asarray(r["pres"]), single.primal_res, rtol=1e-12)
         # data-local chain: each boundary rank sends one d-row per phase over each boundary it has
         nb = (r["local"][0] > 0) + (r["local"][-1] < 23)
         assert r["runs"][-1][3] == nb * 50 * 8 * 1373
