@@ -317,6 +317,7 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
     const double part = wave_sum_f64(lane < m ? sv[lane] : 0.0);
     const double xx = wave_sum_f64(x * x);
     double* thw_out = th + (long)sl.gid * d;
+    double rp = 0.0;
     if (in) {
       thw_out[lane] = x;
       if (a.flags & PH_POST_DUAL) {  // tails: both neighbours are fresh heads
@@ -324,7 +325,13 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
         if (thl) mm = mm - rho * (thl[lane] - x);
         if (thr) mm = mm + rho * (x - thr[lane]);
         mu[lane] = mm;
+        if (thl) rp = fma(thl[lane] - x, thl[lane] - x, rp);  // K4 primal residual of the tail's edges
+        if (thr) rp = fma(x - thr[lane], x - thr[lane], rp);
       }
+    }
+    if (a.rres && (a.flags & PH_POST_DUAL)) {
+      const double rs = wave_sum_f64(rp);
+      if (lane == 0 && it - 1 < a.max_iter) a.rres[(long)(it - 1) * a.n_total + sl.gid] = rs;
     }
     if (lane == 0) {
       a.objw[sl.li] = lam * 0.5 * xx + part;

@@ -1,0 +1,293 @@
+// Persistent single-launch logistic GADMM with the reference's inexact local solver (inner GD,
+// logReg_GD.m; group_ADMM_logistic_GD.m): the whole solve in ONE kernel per GPU, BASELINE configs[2].
+//
+// The graph engine runs a logistic iteration as two phase kernels (heads, tails), each one wave per
+// worker that loads its shard into VGPRs, runs <= max_inner GD steps and exits (chain_small.hip:
+// chain_phase_logistic_quad). Here every worker is ONE resident wave for the entire solve: the shard
+// X (margins) and X^T (gradient) stay in VGPRs in the split-column quad layout (quad_gemv.h), and
+// the per-phase costs of the graph path -- a kernel boundary, the shard reload, the phase ticket --
+// become a neighbour wait on tagged theta granules. The hand-off / stop protocol is the linear
+// per-worker kernel's (chain_persistent.hip): data-is-flag 16-byte granules, the monitor workgroup
+// sums f_n in worker order and posts the decision of iteration i; a worker starts iteration i only
+// after the decision of i - lag, so every worker (on every GPU) leaves at the same boundary.
+//
+// Per iteration i (group_ADMM_logistic_GD.m:15-103, logReg_GD.m:3-25), worker n with chain
+// neighbours l, r:
+//   head:  wait tails' theta^{i-1}; lazy dual mu -= rho (th_l - th), mu += rho (th - th_r) (the
+//          reference's end-of-iteration dual, applied once the tails are known); GD from th^{i-1}
+//   tail:  wait heads' theta^i; GD; dual update with the fresh heads
+//   GD:    shift s = mu + rho (x0 - th_l) + rho (x0 - th_r) frozen; x <- x - step (-X^T (y / (1 +
+//          e^{y X x})) + lam x + s) until every |dx| < inner_tol or max_inner steps
+//   f_n = lam/2 |x|^2 + sum_i log(1 + e^{-y_i x_i^T x}) -> monitor
+// Arithmetic identical to chain_phase_logistic_quad (same GEMVs, same order), so the objective trace
+// is bit-identical to the graph engine's.
+// Single GPU: agent-scope granules; several GPUs (xGMI fabric): system scope, boundary theta also
+// pushed into the neighbour GPU's table. Every spin has a deadline (done = 4).
+#include "gadmm_common.h"
+#include "gadmm_chain.h"
+#include "persist_device.h"
+#include "chain_device.h"
+#include <cstddef>
+
+struct LogiArgs {
+  const double* X;  // [n_local][m][d]
+  const double* Y;  // [n_local][m]
+  int m, max_inner;
+  double lam, step, inner_tol;
+  int* inner_iters;  // [n_local] optional: GD steps of the worker's last local solve
+};
+
+template <int T, bool SYS>
+__global__ void __launch_bounds__(64) chain_persistent_logistic_kernel(PersistArgs a, LogiArgs g) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  const int d = a.d, n = a.n, m = g.m;
+  const int lane = threadIdx.x, qi = lane & 15, qc = lane >> 4;
+  const __amdgpu_buffer_rsrc_t rth = rsrc_of(a.thg);
+  const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
+  const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
+
+  if (a.has_monitor && (int)blockIdx.x == a.n_local) {
+    // ---------------------------------------------------------------- monitor (one wave)
+    double* vals = lds;  // [n]
+    for (int it = a.start_iter;; ++it) {
+      const unsigned tag = make_tag(a.epoch, it);
+      const int slot = it % a.ring;
+      bool okall = true;
+      for (int w = lane; w < n; w += 64) {
+        double v = 0.0;
+        for (int spin = 0;; ++spin) {
+          if (load_granule<SYS>(rob, (slot * n + w) * 16, tag, &v)) break;
+          if ((spin & 7) == 7 && now_ticks() > deadline) {
+            okall = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        vals[w] = v;
+      }
+      const bool ok = __all(okall);
+      unsigned code = 0;
+      if (lane == 0) {
+        if (!ok) {
+          code = 4;
+        } else {
+          double s = 0.0;
+          for (int w = 0; w < n; ++w) s += vals[w];  // worker order, == the graph engine's finish
+          if (it - 1 < a.max_iter) a.trace[it - 1] = s;
+          if (!(s == s) || isinf(s)) code = 3;
+          else if (fabs(s - a.obj0) < a.tol) code = 1;
+          else if (it >= a.max_iter) code = 2;
+          if (a.tstamp && it - 1 < a.max_iter) a.tstamp[it - 1] = (long long)now_ticks();
+        }
+        const unsigned long long dv = ((unsigned long long)tag << 32) | code;
+        for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
+      }
+      if (__shfl((int)code, 0, 64)) return;
+    }
+  }
+
+  // ------------------------------------------------------------------ worker (one wave)
+  const PhaseSlot sl = a.slots[blockIdx.x];
+  const int li = sl.li, w = sl.gid, left = sl.left, right = sl.right;
+  const bool head = (a.pos[blockIdx.x] % 2) == 0;
+  const double rho = a.rho, lam = g.lam, step = g.step;
+  double* st = lds;  // QSTAGE doubles: quad GEMV staging
+  u32x4* const p0 = a.push ? a.push[2 * blockIdx.x] : nullptr;
+  u32x4* const p1 = a.push ? a.push[2 * blockIdx.x + 1] : nullptr;
+  const __amdgpu_buffer_rsrc_t rp0 = rsrc_of(p0 ? (const void*)p0 : (const void*)a.thg);
+  const __amdgpu_buffer_rsrc_t rp1 = rsrc_of(p1 ? (const void*)p1 : (const void*)a.thg);
+  const double* Xg = g.X + (long)li * m * d;
+  double Xq[4][T], XTq[4][T];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+      const int row = qi + 16 * r, col = qc + 4 * t;
+      Xq[r][t] = (row < m && col < d) ? Xg[(long)row * d + col] : 0.0;   // X[row][col]
+      XTq[r][t] = (col < m && row < d) ? Xg[(long)col * d + row] : 0.0;  // X^T[row][col]
+    }
+  const bool inj = lane < d, ini = lane < m;
+  const double yv = ini ? g.Y[(long)li * m + lane] : 0.0;
+  double th = inj ? a.theta[(long)w * d + lane] : 0.0;  // theta_n^{i-1}
+  double mu = inj ? a.mu[(long)li * d + lane] : 0.0;
+  double tl = (inj && left >= 0) ? a.theta[(long)left * d + lane] : 0.0;
+  double tr = (inj && right >= 0) ? a.theta[(long)right * d + lane] : 0.0;
+  int pending = a.pending_in;
+  int stop_code = 0, stop_iter = 0, abort = 0, used = 0;
+
+  int it = a.start_iter;
+  for (;; ++it) {
+    if (it > a.max_iter + a.lag) break;
+    // -- neighbours' theta (heads: tails' theta^{it-1}; tails: heads' theta^it) and the decision of
+    // it - lag, polled in one loop
+    const bool check = it - a.start_iter >= a.lag;
+    const int jdec = it - a.lag;
+    const bool need_nb = head ? it > a.start_iter : true;
+    const int jnb = head ? it - 1 : it;
+    const unsigned tnb = make_tag(a.epoch, jnb), tj = make_tag(a.epoch, jdec);
+    const int ra = need_nb ? left : -1, rb = need_nb ? right : -1;
+    bool decided = !check;
+    unsigned long long dv = 0;
+    int outcome = 0;  // 1 go, 2 stop, 3 timeout
+    for (int spin = 0;; ++spin) {
+      bool nb = true;
+      if (inj) {
+        if (ra >= 0) nb &= load_granule<SYS>(rth, (ra * d + lane) * 16, tnb, &tl);
+        if (rb >= 0) nb &= load_granule<SYS>(rth, (rb * d + lane) * 16, tnb, &tr);
+      }
+      if (!decided) {
+        dv = __shfl(load_dec<SYS>(&a.decg[jdec % a.ring]), 0, 64);
+        decided = (unsigned)(dv >> 32) == tj;
+      }
+      if (decided && (unsigned)(dv & 0xffffffffu) != 0u) { outcome = 2; break; }
+      if (decided && __all(nb)) { outcome = 1; break; }
+      if ((spin & 7) == 7 && now_ticks() > deadline) { outcome = 3; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (outcome != 1) {
+      if (outcome == 2) {
+        stop_code = (int)(unsigned)(dv & 0xffffffffu);
+        stop_iter = jdec;
+      } else {
+        abort = 1;
+      }
+      break;
+    }
+    // -- lazy dual (heads), frozen proximal shift, inner GD (logReg_GD.m)
+    double sh = 0.0, x = 0.0;
+    if (inj) {
+      double mm = mu;
+      if (head && pending) {
+        if (left >= 0) mm = mm - rho * (tl - th);
+        if (right >= 0) mm = mm + rho * (th - tr);
+        mu = mm;
+      }
+      double s = mm;  // -C1 + C2 (edge form) == mu
+      if (left >= 0) s = s + rho * (th - tl);
+      if (right >= 0) s = s + rho * (th - tr);
+      sh = s;
+      x = th;
+    }
+    used = 0;
+    for (int k = 0; k < g.max_inner; ++k) {
+      const double z = quad_gemv<T>(Xq, x, st);                 // margins z_i = X[i,:] x
+      const double sv = ini ? yv / (1.0 + exp(yv * z)) : 0.0;  // y_i / (1 + e^{y_i z_i})
+      const double gx = quad_gemv<T>(XTq, sv, st);             // (X^T s)_j
+      bool conv = true;
+      if (inj) {
+        const double gr = -gx + lam * x + sh;
+        const double xn = x - step * gr;
+        conv = fabs(xn - x) < g.inner_tol;
+        x = xn;
+      }
+      used = k + 1;
+      if (__all(conv)) break;
+    }
+    // -- publish theta^it: own table + the remote neighbours' tables
+    const unsigned tag = make_tag(a.epoch, it);
+    if (inj) {
+      store_granule<SYS>(rth, (w * d + lane) * 16, tag, x);
+      if (p0) store_granule<SYS>(rp0, (w * d + lane) * 16, tag, x);
+      if (p1) store_granule<SYS>(rp1, (w * d + lane) * 16, tag, x);
+    }
+    if (!head) {  // tails: both neighbours are this iteration's heads -> dual update now
+      double rp = 0.0;
+      if (inj) {
+        double mm = mu;
+        if (left >= 0) mm = mm - rho * (tl - x);
+        if (right >= 0) mm = mm + rho * (x - tr);
+        mu = mm;
+        if (left >= 0) rp = fma(tl - x, tl - x, rp);  // K4 primal residual of the two edges
+        if (right >= 0) rp = fma(x - tr, x - tr, rp);
+      }
+      if (a.rres) {
+        const double rs = wave_sum_f64(rp);
+        if (lane == 0 && it - 1 < a.max_iter) a.rres[(long)(it - 1) * n + w] = rs;
+      }
+    } else {
+      pending = 1;
+    }
+    th = x;
+    // -- f_n(theta^it) = lam/2 |x|^2 + sum softplus(-y z) at the new iterate -> monitor
+    const double z = quad_gemv<T>(Xq, x, st);
+    const double part = wave_sum_f64(ini ? softplus(-yv * z) : 0.0);
+    const double xx = wave_sum_f64(inj ? x * x : 0.0);
+    if (lane == 0) store_granule<SYS>(rob, ((it % a.ring) * n + w) * 16, tag, lam * 0.5 * xx + part);
+  }
+  // final state (plain stores; visible to the host after the kernel)
+  if (inj) {
+    a.theta[(long)w * d + lane] = th;
+    a.mu[(long)li * d + lane] = mu;
+  }
+  if (lane == 0) {
+    if (g.inner_iters) g.inner_iters[li] = used;
+    if (abort) {
+      a.ctl->done = 4;
+    } else if (blockIdx.x == 0 && stop_code) {
+      a.ctl->done = stop_code;
+      a.ctl->conv_iter = stop_iter;
+      a.ctl->iter = it;
+      a.ctl->pending = 1;
+      a.ctl->monitored = stop_iter;
+    }
+  }
+}
+
+extern "C" long gadmm_resident_capacity(const void* fn, int threads, size_t shm);
+
+static const void* logi_variant(const PersistArgs& a, const LogiArgs& g) {
+  const int mx = a.d > g.m ? a.d : g.m;
+  if (mx > 64 || a.n_epochs > 0) return nullptr;
+  if (a.sys_scope) {
+    if (mx <= 52) return (const void*)chain_persistent_logistic_kernel<13, true>;
+    return (const void*)chain_persistent_logistic_kernel<16, true>;
+  }
+  if (mx <= 52) return (const void*)chain_persistent_logistic_kernel<13, false>;
+  return (const void*)chain_persistent_logistic_kernel<16, false>;
+}
+
+static size_t logi_shm(const PersistArgs& a) {
+  const size_t mon = (size_t)a.n * 8, wk = (size_t)QSTAGE * 8;
+  return mon > wk ? mon : wk;
+}
+
+extern "C" {
+
+int gadmm_logi_abi_layout(long long* out, int n) {
+  long long v[] = {(long long)sizeof(LogiArgs), (long long)offsetof(LogiArgs, lam),
+                   (long long)offsetof(LogiArgs, inner_iters)};
+  const int k = (int)(sizeof(v) / sizeof(v[0]));
+  for (int i = 0; i < n && i < k; ++i) out[i] = v[i];
+  return k;
+}
+
+// Workgroups the logistic persistent kernel can keep resident (0: shape not eligible).
+long gadmm_chain_persistent_logistic_capacity(const PersistArgs* args, const LogiArgs* g) {
+  const void* fn = logi_variant(*args, *g);
+  return fn ? gadmm_resident_capacity(fn, 64, logi_shm(*args)) : 0;
+}
+
+int gadmm_chain_persistent_logistic_launch(const PersistArgs* args, const LogiArgs* gargs, hipStream_t st) {
+  const PersistArgs& a = *args;
+  const LogiArgs& g = *gargs;
+  const void* fn = logi_variant(a, g);
+  if (!fn || !g.X || !g.Y || g.max_inner < 1 || a.ring <= a.lag + 1 || a.start_iter + a.max_iter + a.lag >= (1 << 20) ||
+      (a.has_monitor && !a.dec_push)) {
+    gadmm_set_error("persistent logistic kernel: unsupported configuration (d=%d m=%d)", a.d, g.m);
+    return -1;
+  }
+  const size_t shm = logi_shm(a);
+  const int blocks = a.n_local + (a.has_monitor ? 1 : 0);
+  const long cap = gadmm_resident_capacity(fn, 64, shm);
+  if (blocks > cap) {
+    gadmm_set_error("persistent logistic kernel: %d workgroups but only %ld can be resident", blocks, cap);
+    return -2;
+  }
+  if (shm > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  void* kargs[] = {const_cast<PersistArgs*>(&a), const_cast<LogiArgs*>(&g)};
+  GADMM_CHECK(hipLaunchKernel(fn, dim3(blocks), dim3(64), kargs, shm, st));
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"

@@ -298,6 +298,7 @@ __global__ void __launch_bounds__(NT) chain_phase_logistic(PhaseArgs a) {
   const double lossv = block_sum_f64(part, scratch);
   const double xnorm = block_sum_f64(xx, scratch);
   double* thw_out = th + (long)sl.gid * d;
+  double rp = 0.0;
   for (int j = threadIdx.x; j < d; j += NT) {
     const double t = sh_x[j];
     thw_out[j] = t;
@@ -306,7 +307,13 @@ __global__ void __launch_bounds__(NT) chain_phase_logistic(PhaseArgs a) {
       if (thl) mm = mm - rho * (thl[j] - t);
       if (thr) mm = mm + rho * (t - thr[j]);
       mu[j] = mm;
+      if (thl) rp = fma(thl[j] - t, thl[j] - t, rp);  // K4 primal residual of the tail's edges
+      if (thr) rp = fma(t - thr[j], t - thr[j], rp);
     }
+  }
+  if (a.rres && (a.flags & PH_POST_DUAL)) {
+    const double rs = block_sum_f64(rp, scratch);
+    if (threadIdx.x == 0 && it - 1 < a.max_iter) a.rres[(long)(it - 1) * a.n_total + sl.gid] = rs;
   }
   if (threadIdx.x == 0) {
     a.objw[sl.li] = a.lam * 0.5 * xnorm + lossv;
@@ -450,6 +457,7 @@ __global__ void __launch_bounds__(64) chain_phase_logistic_wave(PhaseArgs a) {
   part = wave_sum_f64(part);
   xx = wave_sum_f64(xx);
   double* thw_out = th + (long)sl.gid * d;
+  double rp = 0.0;
 #pragma unroll
   for (int c = 0; c < C; ++c) {
     const int j = lane + 64 * c;
@@ -461,8 +469,14 @@ __global__ void __launch_bounds__(64) chain_phase_logistic_wave(PhaseArgs a) {
         if (thl) mm = mm - rho * (thl[j] - t);
         if (thr) mm = mm + rho * (t - thr[j]);
         mu[j] = mm;
+        if (thl) rp = fma(thl[j] - t, thl[j] - t, rp);  // K4 primal residual of the tail's edges
+        if (thr) rp = fma(t - thr[j], t - thr[j], rp);
       }
     }
+  }
+  if (a.rres && (a.flags & PH_POST_DUAL)) {
+    const double rs = wave_sum_f64(rp);
+    if (lane == 0 && it - 1 < a.max_iter) a.rres[(long)(it - 1) * a.n_total + sl.gid] = rs;
   }
   if (lane == 0) {
     a.objw[sl.li] = lam * 0.5 * xx + part;
@@ -546,6 +560,7 @@ __global__ void __launch_bounds__(64) chain_phase_logistic_quad(PhaseArgs a) {
   const double part = wave_sum_f64(ini ? softplus(-yv * z) : 0.0);
   const double xx = wave_sum_f64(inj ? x * x : 0.0);
   double* thw_out = th + (long)sl.gid * d;
+  double rp = 0.0;
   if (inj) {
     thw_out[lane] = x;
     if (a.flags & PH_POST_DUAL) {
@@ -553,7 +568,13 @@ __global__ void __launch_bounds__(64) chain_phase_logistic_quad(PhaseArgs a) {
       if (thl) mm = mm - rho * (thl[lane] - x);
       if (thr) mm = mm + rho * (x - thr[lane]);
       mu[lane] = mm;
+      if (thl) rp = fma(thl[lane] - x, thl[lane] - x, rp);  // K4 primal residual of the tail's edges
+      if (thr) rp = fma(x - thr[lane], x - thr[lane], rp);
     }
+  }
+  if (a.rres && (a.flags & PH_POST_DUAL)) {
+    const double rs = wave_sum_f64(rp);
+    if (lane == 0 && it - 1 < a.max_iter) a.rres[(long)(it - 1) * a.n_total + sl.gid] = rs;
   }
   if (lane == 0) {
     a.objw[sl.li] = lam * 0.5 * xx + part;
@@ -592,7 +613,7 @@ __global__ void __launch_bounds__(256) chain_phase_logistic_quad4(PhaseArgs a) {
   __shared__ __attribute__((aligned(16))) double xs[4 * QX];  // x, permuted: x_j at (j & 3) * QX + (j >> 2)
   __shared__ __attribute__((aligned(16))) double ss[4 * QX];  // s, same permutation over samples
   __shared__ int vote[2][4];
-  __shared__ double red[8];
+  __shared__ double red[12];
   __shared__ int flag_lds;
   ChainCtl* ctl = a.ctl;
   if (ctl->done) return;
@@ -690,6 +711,7 @@ __global__ void __launch_bounds__(256) chain_phase_logistic_quad4(PhaseArgs a) {
     red[w] = part;
     red[4 + w] = xx;
   }
+  double rp = 0.0;
   if (inj && qc == 0) {
     th[(long)sl.gid * d + row] = x;
     if (a.flags & PH_POST_DUAL) {
@@ -697,10 +719,18 @@ __global__ void __launch_bounds__(256) chain_phase_logistic_quad4(PhaseArgs a) {
       if (thl) mm = mm - rho * (thl[row] - x);
       if (thr) mm = mm + rho * (x - thr[row]);
       mu[row] = mm;
+      if (thl) rp = fma(thl[row] - x, thl[row] - x, rp);  // K4 primal residual of the tail's edges
+      if (thr) rp = fma(x - thr[row], x - thr[row], rp);
     }
+  }
+  if (a.rres && (a.flags & PH_POST_DUAL)) {
+    const double rs = wave_sum_f64(rp);
+    if (lane == 0) red[8 + w] = rs;
   }
   lds_barrier();
   if (threadIdx.x == 0) {
+    if (a.rres && (a.flags & PH_POST_DUAL) && it - 1 < a.max_iter)
+      a.rres[(long)(it - 1) * a.n_total + sl.gid] = ((red[8] + red[9]) + red[10]) + red[11];
     const double pt = ((red[0] + red[1]) + red[2]) + red[3], x2 = ((red[4] + red[5]) + red[6]) + red[7];
     a.objw[sl.li] = lam * 0.5 * x2 + pt;
     if (a.inner_iters) a.inner_iters[sl.li] = used;

@@ -143,15 +143,30 @@ def run_logistic(args, rank, world, device, comm) -> Dict:
     m = LogisticRegression(ds.X.to(device).contiguous(), ds.y.to(device).contiguous(), lam=1e-5)
     obj0 = m.optimum(comm if world > 1 else None, n_total=n)
     rho, tol = 2e-4, 1e-4
+    opts = {"state": False}
+    fabric, scomm = None, comm
+    if world > 1:
+        # one persistent launch per GPU over the xGMI fabric (chain_persistent_logistic.hip); every
+        # rank falls back together to the graph engine on RCCL / the IPC transport
+        fabric = _try_fabric(n, ds.dim, rank, world, device)
+        if fabric is not None:
+            from .parallel.comm import RankInfo
+            opts["fabric"] = fabric
+            scomm = RankInfo(rank, world)
 
     def solve():
-        return chain_admm(m, local, n, rho, obj0, tol, 400, comm=comm, placement=pl, local_solver="gd", step=2.2,
-                          engine_opts={"state": False})
+        return chain_admm(m, local, n, rho, obj0, tol, 400, comm=scomm, placement=pl, local_solver="gd", step=2.2,
+                          engine_opts=opts)
 
     ms, r = _timed(solve, args.steps, args.warmup, device, world)
+    if fabric is not None:
+        fabric.close()
     return {"metric": "wall-clock to 1e-4 objective gap, GADMM logistic regression, inner-GD HIP kernel "
                       "(LogisticRegression_Synthetic)",
             "ms": ms, "iters": r.iters, "expected": 53 if n == 24 else None, "backend": r.extra.get("backend"),
+            "engine": r.extra.get("engine"), "transport": r.extra.get("transport"),
+            "theta_payload_bytes_per_solve": _sum_ranks(r.bytes_sent, world),
+            "wire_bytes_per_solve": _sum_ranks(r.extra.get("wire_bytes", 0), world),
             "config": {"model": "LogisticRegression_Synthetic GADMM inner-GD", "workers": n, "features": ds.dim,
                        "samples_per_worker": ds.rows_per_worker, "rho": rho, "gd_step": 2.2, "lam": 1e-5,
                        "tol": tol, "global_batch": n * ds.rows_per_worker, "seq_len": 1,
@@ -248,6 +263,24 @@ def run_dgadmm(args, rank, world, device, comm) -> Dict:
     return out
 
 
+def _try_fabric(n: int, d: int, rank: int, world: int, device, table_slots: int = 1):
+    """An xGMI fabric on every rank, or None on every rank (agreed by an all-reduce)."""
+    from .parallel.xgmi import XgmiFabric
+    fabric, ok = None, False
+    try:
+        fabric = XgmiFabric(n, d, 8, rank, world, device, table_slots=table_slots)
+        ok = True
+    except Exception as e:
+        print("benchmarks[rank %d]: xgmi fabric unavailable: %s" % (rank, e))
+    t = torch.tensor([0.0 if ok else 1.0], dtype=torch.float64)
+    dist.all_reduce(t)
+    if float(t.item()) == 0.0:
+        return fabric
+    if fabric is not None:
+        fabric.close()
+    return None
+
+
 def _sum_ranks(v, world: int) -> int:
     if world == 1:
         return int(v)
@@ -272,17 +305,23 @@ def run_real10m(args, rank, world, device, comm) -> Dict:
     rho = 0.5 * (rows // wpg)
     state = {}
 
-    def setup():
-        m = LinearRegression(X, y)  # f64-MFMA Gram (K1)
-        obj0 = m.optimum(comm if world > 1 else None, n_total=n)
-        return m, obj0
-
     def solve():
+        # phases timed between device synchronisations (negligible at these sizes): Gram (K1),
+        # optimum (one all-reduce + a d x d solve + the raw residuals), then chain_admm = engine
+        # set-up (cached inverses, K2) + the GADMM iterations
         t0 = time.perf_counter()
-        m, obj0 = setup()
+        m = LinearRegression(X, y)  # f64-MFMA Gram (K1)
         torch.cuda.synchronize(device)
-        state["t_setup"] = time.perf_counter() - t0
-        r = chain_admm(m, ids, n, rho, obj0, 1e-8 * abs(obj0), 2000, comm=comm, placement=pl)
+        t1 = time.perf_counter()
+        obj0 = m.optimum(comm if world > 1 else None, n_total=n)
+        torch.cuda.synchronize(device)
+        t2 = time.perf_counter()
+        r = chain_admm(m, ids, n, rho, obj0, 1e-8 * abs(obj0), 2000, comm=comm, placement=pl,
+                       engine_opts={"cache": False, "residual": False})
+        torch.cuda.synchronize(device)
+        t3 = time.perf_counter()
+        state.update(t_gram=t1 - t0, t_opt=t2 - t1, t_iters=r.wall_s, t_engine=(t3 - t2) - r.wall_s,
+                     t_setup=t2 - t0)
         state["m"], state["obj0"] = m, obj0
         return r
 
@@ -291,7 +330,10 @@ def run_real10m(args, rank, world, device, comm) -> Dict:
                      "real-shaped %d x %d per GPU" % (rows, dim),
            "ms": ms, "iters": r.iters, "expected": None, "backend": r.extra.get("backend"),
            "setup_s": state.get("t_setup"),
-           "gram_tflops": 2.0 * rows * (dim + 1) * (dim + 2) / 2 / max(state.get("t_setup", 1.0), 1e-9) / 1e12,
+           "breakdown_s": {"gram_K1": state.get("t_gram"), "optimum": state.get("t_opt"),
+                           "engine_setup_inverses_K2": state.get("t_engine"), "iterations": state.get("t_iters")},
+           "us_per_iteration": 1e6 * state.get("t_iters", 0.0) / max(r.iters, 1),
+           "gram_tflops": 2.0 * rows * (dim + 1) * (dim + 2) / 2 / max(state.get("t_gram", 1.0), 1e-9) / 1e12,
            "config": {"model": "LinearRegression_Real-shaped", "rows_per_gpu": rows, "workers": n, "features": dim,
                       "rho": rho, "tol_rel": 1e-8, "global_batch": rows * world, "seq_len": 1,
                       "parallelism": "chain%d-over-%dgpu" % (n, world)}}

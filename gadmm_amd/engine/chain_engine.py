@@ -157,6 +157,7 @@ class NativeChainEngine:
             elif model == "logistic":
                 self.X = X_loc.contiguous()
                 self.Y = y_loc.contiguous()
+                self.nvar, self.deg_to_var = 1, (0, 0, 0)  # no cached inverses
             else:
                 raise ValueError("unknown model %r" % model)
 
@@ -360,10 +361,29 @@ class NativeChainEngine:
         pa.sys_scope = 1 if sys_scope else 0
         return int(self.lib.gadmm_chain_persistent_capacity(ctypes.byref(pa)))
 
+    def _logi_args(self) -> native.LogiArgs:
+        g = native.LogiArgs()
+        b = self._desc.base
+        g.X, g.Y, g.m, g.max_inner = native.ptr(self.X), native.ptr(self.Y), self.m, int(b.max_inner)
+        g.lam, g.step, g.inner_tol = float(b.lam), float(b.step), float(b.inner_tol)
+        g.inner_iters = self.inner_iters.data_ptr()
+        return g
+
     def persistent_eligible(self, fabric=None) -> bool:
-        if self.model != "linear" or self.plan is None or self.path is None:
+        if self.plan is None or self.path is None:
             return False
         if self.nranks != 1 and fabric is None:
+            return False
+        if self.model == "logistic":
+            # inner-GD logistic in one launch (chain_persistent_logistic.hip): one wave per worker
+            if self.local_solver != "gd" or max(self.d, self.m) > 64:
+                return False
+            pa = native.PersistArgs()
+            pa.d, pa.n, pa.sys_scope = self.d, self.n_total, 1 if fabric is not None else 0
+            g = self._logi_args()
+            cap = int(self.lib.gadmm_chain_persistent_logistic_capacity(ctypes.byref(pa), ctypes.byref(g)))
+            return self.n_local + 1 <= cap
+        if self.model != "linear":
             return False
         if int(self.lib.gadmm_chain_persistent_lds(self.d, self._obj_mode())) <= 0:
             return False
@@ -421,7 +441,7 @@ class NativeChainEngine:
                 raise RuntimeError("dynamic persistent kernel not eligible for this engine/config")
         elif not self.persistent_eligible(fabric):
             raise RuntimeError("persistent kernel not eligible for this engine/config")
-        plan = self.blocked_plan(fabric, timeline=timeline_iters > 0)
+        plan = self.blocked_plan(fabric, timeline=timeline_iters > 0) if self.model == "linear" else None
         if epochs is not None and (plan is None or plan[3] != 1 or timeline_iters > 0 or self.n_local != self.n_total
                                    or os.environ.get("GADMM_BLOCKED_DYN", "0") != "1"):
             # D-GADMM: the blocked kernel's dynamic mode (opt-in GADMM_BLOCKED_DYN=1; one GPU, 12-wave
@@ -492,7 +512,7 @@ class NativeChainEngine:
         pa.rho, pa.obj0, pa.tol = self.rho, self.obj0, self.tol
         pa.timeout_ticks = int(timeout_s * 1e8)
         pa.slots, pa.pos = slot_t.data_ptr(), pos_t.data_ptr()
-        pa.Minv, pa.A, pa.b, pa.yy = self.Minv.data_ptr(), self.A.data_ptr(), self.b.data_ptr(), self.yy.data_ptr()
+        pa.Minv, pa.A, pa.b, pa.yy = native.ptr(self.Minv), native.ptr(self.A), native.ptr(self.b), native.ptr(self.yy)
         pa.theta, pa.mu = self.theta.data_ptr(), self.mu.data_ptr()
         pa.thg, pa.objg, pa.decg = ptrs
         pa.push = push.data_ptr() if push is not None else None
@@ -591,7 +611,17 @@ class NativeChainEngine:
                     self.last_kernel = "per-worker"
                 else:
                     native.check(rc, "chain_blocked_launch")
-            if plan is None:
+            if plan is None and self.model == "logistic":
+                if epochs is not None:
+                    raise RuntimeError("persistent logistic kernel: static chains only")
+                self.last_kernel = "per-worker-logistic"
+                self._logi = self._logi_args()
+                rc = int(self.lib.gadmm_chain_persistent_logistic_launch(ctypes.byref(pa), ctypes.byref(self._logi),
+                                                                         self.stream.cuda_stream))
+                if rc == -2:
+                    raise ResidencyError(self.lib.gadmm_last_error().decode())
+                native.check(rc, "chain_persistent_logistic_launch")
+            elif plan is None:
                 rc = int(self.lib.gadmm_chain_persistent_launch(ctypes.byref(pa), self.stream.cuda_stream))
                 if rc == -2:
                     raise ResidencyError(self.lib.gadmm_last_error().decode())

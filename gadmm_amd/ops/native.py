@@ -108,6 +108,12 @@ class PersistArgs(ctypes.Structure):
     ]
 
 
+class LogiArgs(ctypes.Structure):
+    """Mirror of LogiArgs in csrc/kernels/chain_persistent_logistic.hip (persistent logistic GADMM)."""
+    _fields_ = [("X", c_void_p), ("Y", c_void_p), ("m", c_int), ("max_inner", c_int),
+                ("lam", c_double), ("step", c_double), ("inner_tol", c_double), ("inner_iters", c_void_p)]
+
+
 class StarArgs(ctypes.Structure):
     """Mirror of csrc/include/gadmm_star.h (persistent star ADMM)."""
     _fields_ = [
@@ -168,6 +174,10 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_device_can_access_peer": (c_int, [c_int, c_int]),
         "gadmm_chain_persistent_launch": (c_int, [ctypes.POINTER(PersistArgs), c_void_p]),
         "gadmm_chain_persistent_capacity": (c_long, [ctypes.POINTER(PersistArgs)]),
+        "gadmm_chain_persistent_logistic_capacity": (c_long, [ctypes.POINTER(PersistArgs), ctypes.POINTER(LogiArgs)]),
+        "gadmm_chain_persistent_logistic_launch": (c_int, [ctypes.POINTER(PersistArgs), ctypes.POINTER(LogiArgs),
+                                                           c_void_p]),
+        "gadmm_logi_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
         "gadmm_write_stamp": (c_int, [c_void_p, c_void_p]),
         "gadmm_star_capacity": (c_long, [ctypes.POINTER(StarArgs)]),
         "gadmm_star_launch": (c_int, [ctypes.POINTER(StarArgs), c_void_p]),

@@ -101,6 +101,54 @@ def _ipc_logistic_rank(rank, world, n):
     return out
 
 
+def _xgmi_logistic_rank(rank, world, n):
+    import torch
+    from gadmm_amd.data import logistic_synthetic
+    from gadmm_amd.models import LogisticRegression
+    from gadmm_amd.algorithms import chain_admm
+    from gadmm_amd.parallel.comm import RankInfo
+    from gadmm_amd.parallel.topology import Placement
+    from gadmm_amd.parallel.xgmi import XgmiFabric
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    pl = Placement.contiguous(n, world)
+    loc = pl.local_workers(rank)
+    ds = logistic_synthetic(n, worker_ids=loc)
+    fab = XgmiFabric(n, 50, 8, rank, world, dev)
+    m = LogisticRegression(ds.X.to(dev), ds.y.to(dev), lam=1e-5)
+    from gadmm_amd.parallel.ipc import IpcComm
+    ipc = IpcComm(n, 50, 8, dev)
+    obj0 = m.optimum(ipc, n_total=n)
+    ipc.close()
+    outs = []
+    for _ in range(2):
+        r = chain_admm(m, loc, n, 2e-4, obj0, 1e-4, 400, comm=RankInfo(rank, world), placement=pl, local_solver="gd",
+                       step=2.2, engine_opts={"fabric": fab, "state": False})
+        outs.append((r.iters, r.extra["engine"], r.bytes_sent))
+    out = {"runs": outs, "trace": r.obj.tolist(), "obj0": obj0, "local": loc}
+    r.extra["engine_obj"].close()
+    fab.close()
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_logistic_persistent_matches_one_gpu(world, log24):
+    """Logistic GADMM (inner GD) in one persistent launch per GPU over the xGMI fabric == one GPU,
+    bit for bit; theta payload = 2 (ranks - 1) d 8 iterations."""
+    from gadmm_amd.parallel.launch import spawn
+    from gadmm_amd.models import LogisticRegression
+    from gadmm_amd.algorithms import chain_admm
+    res = spawn(_xgmi_logistic_rank, world, 24, timeout=300)
+    m = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
+    single = chain_admm(m, list(range(24)), 24, 2e-4, res[0]["obj0"], 1e-4, 400, local_solver="gd", step=2.2,
+                        engine_opts={"cache": False})
+    assert single.iters == 53
+    for r in res:
+        assert all(it == 53 and eng == "persistent" for it, eng, _ in r["runs"]), r["runs"]
+        assert np.array_equal(np.asarray(r["trace"]), single.obj)
+    assert sum(r["runs"][-1][2] for r in res) == 2 * (world - 1) * 50 * 8 * 53
+
+
 def test_ipc_transport_logistic_two_ranks(log24):
     """Logistic GADMM (inner-GD HIP kernel) across two processes == one rank."""
     from gadmm_amd.parallel.launch import spawn

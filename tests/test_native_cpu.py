@@ -115,3 +115,11 @@ def test_star_abi_layout_matches_ctypes():
     exp = [ctypes.sizeof(native.StarArgs), native.StarArgs.rho.offset, native.StarArgs.gid.offset,
            native.StarArgs.ctl.offset]
     assert list(buf[:k]) == exp
+
+
+def test_logi_abi_layout_matches_ctypes():
+    lib = native.require()
+    buf = (ctypes.c_longlong * 8)()
+    k = lib.gadmm_logi_abi_layout(buf, 8)
+    exp = [ctypes.sizeof(native.LogiArgs), native.LogiArgs.lam.offset, native.LogiArgs.inner_iters.offset]
+    assert list(buf[:k]) == exp
