@@ -78,28 +78,31 @@ class LinearRegression:
             self._chol[key] = torch.linalg.cholesky(self.A + (self.lam + key) * eye)
         return self._chol[key]
 
-    def prox_inverse(self, shift: float) -> torch.Tensor:
-        """Cached ``(A_n + (lam + shift) I)^{-1}`` (HIP Gauss-Jordan for d <= 128, rocSOLVER above)."""
-        key = ("inv", float(shift))
+    def prox_inverse(self, shift: float, worker: int) -> torch.Tensor:
+        """Cached ``(A_n + (lam + shift) I)^{-1}`` of local worker ``worker`` (the blocked MFMA
+        Gauss-Jordan of ops/linalg.py for d > 128), built on first use: a worker only pays for the
+        shifts (chain degrees, star hub) it is actually solved with."""
+        key = ("inv", float(shift), int(worker))
         if key not in self._chol:
-            sh = torch.full((self.n_local, 1), self.lam + float(shift), dtype=torch.float64, device=self.A.device)
-            self._chol[key] = spd_inverse(self.A, sh)[:, 0]
+            sh = torch.full((1, 1), self.lam + float(shift), dtype=torch.float64, device=self.A.device)
+            self._chol[key] = spd_inverse(self.A[int(worker):int(worker) + 1], sh)[0, 0]
         return self._chol[key]
 
     def prox_solve(self, idx: torch.Tensor, rhs: torch.Tensor, shifts: torch.Tensor) -> torch.Tensor:
         """Solve ``(A_n + shift_n I) x = rhs_n`` for local workers ``idx``: batched Cholesky solves on
         the CPU / small d; on a HIP device with large d a GEMV with the cached inverse (two
-        latency-bound 10k triangular solves per call would dominate)."""
+        latency-bound 10k triangular solves per call would dominate), read in place (no gathered
+        copy of the d x d inverse)."""
         out = torch.empty_like(rhs)
         use_inv = self.A.is_cuda and self.d > 256
+        if use_inv:
+            for k, (w, s) in enumerate(zip(idx.tolist(), shifts.tolist())):
+                out[k] = torch.mv(self.prox_inverse(s, w), rhs[k])
+            return out
         for s in torch.unique(shifts).tolist():
             sel = (shifts == s).nonzero().flatten()
-            if use_inv:
-                Minv = self.prox_inverse(s)[idx[sel]]
-                out[sel] = torch.bmm(Minv, rhs[sel].unsqueeze(-1)).squeeze(-1)
-            else:
-                L = self.prox_factor(s)[idx[sel]]
-                out[sel] = torch.cholesky_solve(rhs[sel].unsqueeze(-1), L).squeeze(-1)
+            L = self.prox_factor(s)[idx[sel]]
+            out[sel] = torch.cholesky_solve(rhs[sel].unsqueeze(-1), L).squeeze(-1)
         return out
 
     def inverses(self, shifts) -> torch.Tensor:
