@@ -6,7 +6,8 @@
 struct StarArgs {
   int d, n, n_local, max_iter;   // n: all workers (the hub is worker n - 1)
   int lag, ring, has_monitor, nranks;
-  int sys_scope, hub_rank, my_rank, pad0;
+  int sys_scope, hub_rank, my_rank;
+  int timeline_iters;            // > 0: stamp the first iterations into `timeline` (debug profiling)
   unsigned epoch;                // salts every tag (tag = epoch << 20 | iteration)
   int pad1;
   double rho, obj0, tol;
@@ -27,4 +28,6 @@ struct StarArgs {
   double* trace;                 // [max_iter] (monitor rank)
   long long* tstamp;             // [max_iter] decision clock (monitor rank), may be null
   ChainCtl* ctl;
+  long long* timeline;           // optional [n_local + 1][timeline_iters][4] s_memrealtime: wait start,
+                                 // inputs ready, theta published, objective posted (monitor: decided)
 };

@@ -103,15 +103,21 @@ class StarEngine:
         blocks = len(self.local) + (1 if self.rank == 0 else 0)
         return blocks <= int(self.lib.gadmm_star_capacity(ctypes.byref(self._args(1.0))))
 
-    def run(self, timeout_s: float = 20.0):
+    def run(self, timeout_s: float = 20.0, timeline_iters: int = 0):
         """Reset and solve. Returns (iters, done, wall_ms). Collective across ranks (the kernels hand
-        off to each other)."""
+        off to each other). ``timeline_iters > 0``: s_memrealtime stamps of the first iterations into
+        ``self.last_timeline`` [workgroup][iteration][wait start, inputs ready, published, objective
+        posted] (the last row is the monitor: column 0 = decided)."""
         if self.fabric is not None:
             self._epoch = self.fabric.next_epoch()
         else:
             self._epoch = self._epoch % 4095 + 1
         a = self._args(timeout_s)
         a.epoch = self._epoch
+        tl = None
+        if timeline_iters > 0:
+            tl = torch.zeros((len(self.local) + 1, int(timeline_iters), 4), dtype=torch.int64, device=self.device)
+            a.timeline, a.timeline_iters = tl.data_ptr(), int(timeline_iters)
         with torch.cuda.stream(self.stream):
             self.theta.zero_()
             self.lam.zero_()
@@ -123,6 +129,7 @@ class StarEngine:
             native.check(rc, "star_launch")
             self.stream.synchronize()
             t1 = time.perf_counter()
+        self.last_timeline = tl.cpu().numpy() if tl is not None else None
         c = self.ctl.cpu().tolist()
         if c[1] == 4:
             from .chain_engine import HandoffTimeout

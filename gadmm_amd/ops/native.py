@@ -119,13 +119,13 @@ class StarArgs(ctypes.Structure):
     _fields_ = [
         ("d", c_int), ("n", c_int), ("n_local", c_int), ("max_iter", c_int),
         ("lag", c_int), ("ring", c_int), ("has_monitor", c_int), ("nranks", c_int),
-        ("sys_scope", c_int), ("hub_rank", c_int), ("my_rank", c_int), ("pad0", c_int),
+        ("sys_scope", c_int), ("hub_rank", c_int), ("my_rank", c_int), ("timeline_iters", c_int),
         ("epoch", ctypes.c_uint), ("pad1", c_int),
         ("rho", c_double), ("obj0", c_double), ("tol", c_double), ("timeout_ticks", c_longlong),
         ("gid", c_void_p), ("Minv", c_void_p), ("A", c_void_p), ("b", c_void_p), ("yy", c_void_p),
         ("theta", c_void_p), ("lam", c_void_p), ("lam_hub", c_void_p), ("thg", c_void_p), ("peer_thg", c_void_p),
         ("objg", c_void_p), ("decg", c_void_p), ("dec_push", c_void_p), ("trace", c_void_p), ("tstamp", c_void_p),
-        ("ctl", c_void_p),
+        ("ctl", c_void_p), ("timeline", c_void_p),
     ]
 
 
