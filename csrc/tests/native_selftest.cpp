@@ -20,6 +20,7 @@
 
 #include "gadmm_chain.h"
 #include "gadmm_fo.h"
+#include "gadmm_star.h"
 
 extern "C" {
 const char* gadmm_last_error();
@@ -41,6 +42,11 @@ int gadmm_chain_blocked_plan(int n, int d, int want_k, int* k_out, int* len_out)
 long gadmm_chain_blocked_tab_granules(int n, int d, int ring);
 int gadmm_chain_blocked_launch(const PersistArgs* a, hipStream_t st);
 int gadmm_fo_launch(const FoArgs* a, void* stream);
+long gadmm_spd_inverse_blocked_workspace(int d, int nb);
+int gadmm_spd_inverse_blocked_f64(const double* A, const double* shift_host, int N, int d, int nvar, double* out,
+                                  double* ws, int* status, int nb, hipStream_t st);
+int gadmm_star_launch(const StarArgs* a, hipStream_t st);
+int gadmm_star_abi_layout(long long* out, int n);
 }
 
 namespace {
@@ -172,6 +178,36 @@ double optimum(const Problem& p) {
   return f;
 }
 
+// Star ADMM (standared_ADMM.m): hub = worker N - 1; returns iterations to |obj - obj0| < tol.
+int host_star(const Problem& p, double rho, double obj0, double tol, int max_iter) {
+  const int N = p.N, d = p.d, hub = N - 1;
+  std::vector<double> th((size_t)N * d, 0.0), lam((size_t)N * d, 0.0), thh(d, 0.0), r(d);
+  for (int it = 1; it <= max_iter; ++it) {
+    for (int n = 0; n < hub; ++n) {
+      std::vector<double> M(p.A.begin() + (size_t)n * d * d, p.A.begin() + (size_t)(n + 1) * d * d);
+      for (int i = 0; i < d; ++i) M[i * d + i] += rho;
+      for (int i = 0; i < d; ++i) r[i] = p.b[(size_t)n * d + i] - lam[(size_t)n * d + i] + rho * thh[i];
+      chol_solve(M, r.data(), &th[(size_t)n * d], d);
+    }
+    std::vector<double> M(p.A.begin() + (size_t)hub * d * d, p.A.end());
+    for (int i = 0; i < d; ++i) M[i * d + i] += (N - 1) * rho;
+    for (int i = 0; i < d; ++i) {
+      double c1 = 0.0, s1 = 0.0;
+      for (int n = 0; n < hub; ++n) {
+        c1 += lam[(size_t)n * d + i];
+        s1 += th[(size_t)n * d + i];
+      }
+      r[i] = p.b[(size_t)hub * d + i] + c1 + rho * s1;
+    }
+    chol_solve(M, r.data(), &th[(size_t)hub * d], d);
+    for (int i = 0; i < d; ++i) thh[i] = th[(size_t)hub * d + i];
+    for (int n = 0; n < hub; ++n)
+      for (int i = 0; i < d; ++i) lam[(size_t)n * d + i] += rho * (th[(size_t)n * d + i] - thh[i]);
+    if (std::fabs(objective(p, th) - obj0) < tol) return it;
+  }
+  return -1;
+}
+
 // GADMM on the identity chain, per-worker duals (dynamic_group_ADMM_closedForm.m form).
 int host_gadmm(const Problem& p, double rho, double obj0, double tol, int max_iter, std::vector<double>& th) {
   const int N = p.N, d = p.d;
@@ -253,6 +289,16 @@ void host_only_checks() {
   std::memset(&pa, 0, sizeof(pa));
   pa.d = 50;
   EXPECT(gadmm_chain_blocked_launch(&pa, nullptr) != 0, "blocked launch rejects an empty plan");
+  EXPECT(gadmm_star_abi_layout(buf, 32) >= 2 && buf[0] == (long long)sizeof(StarArgs), "star abi layout");
+  StarArgs sa;
+  std::memset(&sa, 0, sizeof(sa));
+  sa.d = 50;
+  sa.n = 1;
+  EXPECT(gadmm_star_launch(&sa, nullptr) == -1, "star launch rejects n < 2");
+  EXPECT(gadmm_spd_inverse_blocked_f64(nullptr, nullptr, 1, 300, 1, nullptr, nullptr, nullptr, 100, nullptr) == -1,
+         "blocked inverse rejects nb = 100");
+  EXPECT(gadmm_spd_inverse_blocked_workspace(300, 128) > gadmm_spd_inverse_blocked_workspace(300, 64),
+         "blocked inverse workspace grows with the block");
 }
 
 // ------------------------------------------------------------------ GPU checks
@@ -523,6 +569,110 @@ void gpu_checks() {
            max_rel(fetch(ot, iters), obj_ref));
     std::printf("first-order GD: %d iterations, trace rel err %.2e\n", c.iters, max_rel(fetch(ot, iters), obj_ref));
     for (void* q : {(void*)tab, (void*)part, (void*)ot, (void*)ct, (void*)tt, (void*)tho, (void*)fc}) HIPOK(hipFree(q));
+  }
+
+  // ---- star ADMM kernel (one launch) vs the host star ADMM
+  {
+    const double srho = 1.0, stol = 1e-6;
+    const int it_star = host_star(p, srho, obj0, stol, 20000);
+    EXPECT(it_star > 0, "host star ADMM did not converge");
+    std::vector<double> sshift(N);
+    for (int n = 0; n < N; ++n) sshift[n] = n == N - 1 ? (N - 1) * srho : srho;
+    double* ssh = dalloc<double>(N);
+    HIPOK(hipMemcpy(ssh, sshift.data(), N * 8, hipMemcpyHostToDevice));
+    double* SMinv = dalloc<double>((size_t)N * d * d);
+    EXPECT(gadmm_spd_inverse_small_f64(A, ssh, N, d, 1, SMinv, status, st) == 0, "star inverses");
+    const int lag = 4, ring = 8, smax = 20000;
+    std::vector<int> gid(N);
+    for (int n = 0; n < N; ++n) gid[n] = n;
+    int* dgid = dalloc<int>(N);
+    HIPOK(hipMemcpy(dgid, gid.data(), N * sizeof(int), hipMemcpyHostToDevice));
+    double* sth = dalloc<double>((size_t)N * d);
+    double* slam = dalloc<double>((size_t)N * d);
+    double* slamh = dalloc<double>((size_t)N * d);
+    double* strace = dalloc<double>(smax);
+    u32x4* sthg = dalloc<u32x4>((size_t)N * d);
+    u32x4* sobjg = dalloc<u32x4>((size_t)ring * N);
+    unsigned long long* sdecg = dalloc<unsigned long long>(ring);
+    unsigned long long** sdecp = dalloc<unsigned long long*>(1);
+    u32x4** speer = dalloc<u32x4*>(1);
+    HIPOK(hipMemcpy(sdecp, &sdecg, sizeof(void*), hipMemcpyHostToDevice));
+    HIPOK(hipMemcpy(speer, &sthg, sizeof(void*), hipMemcpyHostToDevice));
+    ChainCtl* sctl = dalloc<ChainCtl>(1);
+    StarArgs sa;
+    std::memset(&sa, 0, sizeof(sa));
+    sa.d = d;
+    sa.n = N;
+    sa.n_local = N;
+    sa.max_iter = smax;
+    sa.lag = lag;
+    sa.ring = ring;
+    sa.has_monitor = 1;
+    sa.nranks = 1;
+    sa.epoch = 1;
+    sa.rho = srho;
+    sa.obj0 = obj0;
+    sa.tol = stol;
+    sa.timeout_ticks = 20LL * 100000000LL;
+    sa.gid = dgid;
+    sa.Minv = SMinv;
+    sa.A = A;
+    sa.b = b;
+    sa.yy = yy;
+    sa.theta = sth;
+    sa.lam = slam;
+    sa.lam_hub = slamh;
+    sa.thg = sthg;
+    sa.peer_thg = speer;
+    sa.objg = sobjg;
+    sa.decg = sdecg;
+    sa.dec_push = sdecp;
+    sa.trace = strace;
+    sa.ctl = sctl;
+    EXPECT(gadmm_star_launch(&sa, st) == 0, "star launch: %s", gadmm_last_error());
+    HIPOK(hipStreamSynchronize(st));
+    const ChainCtl c = fetch(sctl, 1)[0];
+    EXPECT(c.done == 1 && std::abs(c.conv_iter - it_star) <= 1, "star kernel: done=%d iters=%d (host %d)", c.done,
+           c.conv_iter, it_star);
+    std::printf("star kernel: %d iterations (host %d)\n", c.conv_iter, it_star);
+    for (void* q : {(void*)ssh, (void*)SMinv, (void*)dgid, (void*)sth, (void*)slam, (void*)slamh, (void*)strace,
+                    (void*)sthg, (void*)sobjg, (void*)sdecg, (void*)sdecp, (void*)speer, (void*)sctl})
+      HIPOK(hipFree(q));
+  }
+
+  // ---- blocked large-d inverse (d = 200: a recursive 72-pivot last block) vs M Minv = I on the host
+  {
+    const int D = 200;
+    std::vector<double> Mh((size_t)D * D);
+    unsigned long long sd = 777;
+    std::vector<double> G((size_t)2 * D * D);
+    for (auto& v : G) v = lcg_normal(sd);
+    for (int i = 0; i < D; ++i)
+      for (int j = 0; j < D; ++j) {
+        double acc = 0.0;
+        for (int k = 0; k < 2 * D; ++k) acc += G[(size_t)k * D + i] * G[(size_t)k * D + j];
+        Mh[(size_t)i * D + j] = acc / (2 * D);
+      }
+    double* dA = dalloc<double>((size_t)D * D);
+    double* dout = dalloc<double>((size_t)D * D);
+    const long nws = gadmm_spd_inverse_blocked_workspace(D, 128);
+    double* ws = dalloc<double>((size_t)nws);
+    HIPOK(hipMemcpy(dA, Mh.data(), Mh.size() * 8, hipMemcpyHostToDevice));
+    const double shift = 0.25;
+    EXPECT(gadmm_spd_inverse_blocked_f64(dA, &shift, 1, D, 1, dout, ws, status, 128, st) == 0, "blocked inverse: %s",
+           gadmm_last_error());
+    HIPOK(hipStreamSynchronize(st));
+    const std::vector<double> inv = fetch(dout, (size_t)D * D);
+    double err = 0.0;
+    for (int i = 0; i < D; ++i)
+      for (int j = 0; j < D; ++j) {
+        double acc = 0.0;
+        for (int k = 0; k < D; ++k) acc += (Mh[(size_t)i * D + k] + (i == k ? shift : 0.0)) * inv[(size_t)k * D + j];
+        err = std::fmax(err, std::fabs(acc - (i == j ? 1.0 : 0.0)));
+      }
+    EXPECT(err < 1e-11 && fetch(status, 1)[0] == 0, "blocked inverse: max |M Minv - I| = %.3e", err);
+    std::printf("blocked inverse d=%d: max |M Minv - I| = %.2e\n", D, err);
+    for (void* q : {(void*)dA, (void*)dout, (void*)ws}) HIPOK(hipFree(q));
   }
 
   for (void* q : {(void*)X, (void*)Y, (void*)A, (void*)b, (void*)yy, (void*)sh, (void*)Minv, (void*)status,
