@@ -240,23 +240,19 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
         const double z2 = R[2] - fma(b00, y0, b10 * y1), z3 = R[3] - fma(b01, y0, b11 * y1);
         const double l2 = fma(s11, z2, -s01 * z3) * is, l3 = fma(s00, z3, -s01 * z2) * is;  // S^-1 z
         const double l0 = y0 - fma(w00, l2, w01 * l3), l1 = y1 - fma(w10, l2, w11 * l3);
-        const double l[4] = {l0, l1, l2, l3};
+        // the block's columns j = p .. p+3 sit in register c = p / NWV of waves p % NWV .. +3, so "j in K"
+        // and the sign of A_{p+q, j} are wave-uniform; only the pivot-row case varies by lane
+        const int cK = p / NWV, wK = wid - p % NWV;
+        const double lw = wK == 0 ? l0 : (wK == 1 ? l1 : (wK == 2 ? l2 : l3));  // l[j - p] for j in K
 #pragma unroll
         for (int c = 0; c < NCW; ++c) {
           const int j = wid + NWV * c;
+          const double tq = fma(l0, slab[j], fma(l1, slab[64 + j], fma(l2, slab[128 + j], l3 * slab[192 + j])));
+          const bool inK = c == cK && wK >= 0 && wK < 4;
           const double sg = j < p ? -1.0 : 1.0;  // A_{p+q, j} = sg * slab[q][j]
-          const double k0 = sg * slab[0 * 64 + j], k1 = sg * slab[1 * 64 + j], k2 = sg * slab[2 * 64 + j],
-                       k3 = sg * slab[3 * 64 + j];
-          const bool inK = (j >> 2) == bb;
-          double lj = l[0];
-#pragma unroll
-          for (int q = 1; q < 4; ++q) lj = ((j & 3) == q) ? l[q] : lj;
           double v;
-          if (pivrow) {
-            v = inK ? lj : fma(l0, k0, fma(l1, k1, fma(l2, k2, l3 * k3)));  // (Pi A_Kj)_i, or Pi[i-p][j-p]
-          } else {
-            v = inK ? -lj : fma(-l0, k0, fma(-l1, k1, fma(-l2, k2, fma(-l3, k3, h[c]))));
-          }
+          if (inK) v = pivrow ? lw : -lw;                  // Pi[i-p][j-p], or -L_i
+          else v = pivrow ? sg * tq : fma(-sg, tq, h[c]);  // (Pi A_Kj)_i, or A_ij - L_i A_Kj
           h[c] = v;
         }
       }
