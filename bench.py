@@ -30,9 +30,10 @@ of the same loop ([measured-here] row).
     python bench.py                      # 1 GPU
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
 
-The other BASELINE.json configs (same JSON contract, own metric): ``--config logistic`` (configs[2]),
-``--config dgadmm`` (configs[3]), ``--config real10m`` (configs[4]: 1.25M x 10k f64 per GPU), ``--config
-star`` (the star-ADMM comparator of E7); see gadmm_amd/benchmarks.py.
+The other BASELINE.json configs (same JSON contract, own metric): ``--config cpu_gloo`` (configs[0]: the
+same GADMM over gloo CPU ranks, no GPU), ``--config logistic`` (configs[2]), ``--config dgadmm``
+(configs[3]), ``--config real10m`` (configs[4]: 1.25M x 10k f64 per GPU), ``--config star`` (the
+star-ADMM comparator of E7); see gadmm_amd/benchmarks.py.
 """
 from __future__ import annotations
 
@@ -71,8 +72,10 @@ def main():
                     help="multi-GPU transport: xgmi = device-initiated theta pushes between persistent kernels, "
                          "rccl = RCCL send/recv between graph-replayed phases, ipc = the device-copy transport "
                          "between graph-replayed phases")
-    ap.add_argument("--config", choices=["e1", "logistic", "logistic_exact", "dgadmm", "real10m", "star"],
-                    default="e1", help="e1 = the headline (default); the others are BASELINE.json configs[2..4]")
+    ap.add_argument("--config", choices=["e1", "logistic", "logistic_exact", "dgadmm", "real10m", "star", "cpu_gloo"],
+                    default="e1", help="e1 = the headline (default); the others are BASELINE.json configs[2..4]; "
+                                       "cpu_gloo = configs[0]: the same GADMM over gloo ranks on the CPU (plumbing, "
+                                       "no GPU; launch with torchrun --nproc-per-node 2)")
     ap.add_argument("--rows", type=int, default=1_250_000, help="real10m: rows per GPU")
     ap.add_argument("--dim", type=int, default=10_000, help="real10m: features")
     args = ap.parse_args()
@@ -80,6 +83,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.config == "cpu_gloo":  # BASELINE configs[0]: no device is touched
+        run_cpu_gloo(args, rank, world)
+        return
     if world != args.gpus and world == 1 and args.gpus > 1:
         print("bench.py: --gpus %d needs a torchrun launch with %d processes" % (args.gpus, args.gpus),
               file=sys.stderr)
@@ -198,6 +204,62 @@ def run_headline(args, rank, world, device, share):
         }
         print(json.dumps(out), flush=True)
     sol.close()
+
+
+def run_cpu_gloo(args, rank, world):
+    """BASELINE.json configs[0]: LinearRegression_Synthetic closed-form GADMM with the workers spread
+    over ``world`` CPU processes on gloo (torch path: batched local solves, neighbour theta by gloo
+    isend/irecv), timed like the headline. A plumbing check of the distributed path, not a GPU
+    number."""
+    from gadmm_amd.algorithms import chain_admm
+    from gadmm_amd.benchmarks import headline_rank_problem, EXPECTED_ITERS_1E8
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.parallel.comm import LocalComm, TorchDistComm
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = TorchDistComm() if world > 1 else LocalComm()
+    X, y, local, placement, obj0 = headline_rank_problem(args.workers, rank, world)
+    m = LinearRegression(X, y)
+    expect = EXPECTED_ITERS_1E8.get((args.workers, float(args.rho))) if args.tol == 1e-8 else None
+
+    def solve():
+        return chain_admm(m, local, args.workers, args.rho, obj0, args.tol, 20000, comm=comm, placement=placement,
+                          backend="torch")
+
+    for _ in range(args.warmup):
+        solve()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    rs = [solve() for _ in range(args.steps)]
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    ms = (t1 - t0) * 1e3 / max(args.steps, 1)
+    its = {r.iters for r in rs}
+    if world > 1:
+        t = torch.tensor([ms], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+    r = rs[-1]
+    if rank == 0:
+        print(json.dumps({
+            "metric": "wall-clock to 1e-8 objective gap, GADMM linear regression (LinearRegression_Synthetic), "
+                      "CPU gloo ranks (BASELINE configs[0] plumbing)",
+            "value": round(ms / 1e3, 6), "unit": "s", "n_gpus": 0, "cpu_ranks": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": False, "scaling": "strong",
+            "vs_baseline": round(ms / 1e3 / BASELINE_S, 6), "dtype": "fp64",
+            "data": "synthetic (reference LinearRegression_Synthetic design rebuilt from shipped inputData.mat)",
+            "config": {"model": "LinearRegression_Synthetic GADMM closed-form", "workers": args.workers,
+                       "rho": args.rho, "tol": args.tol, "global_batch": args.workers * 50, "seq_len": 1,
+                       "parallelism": "chain%d-over-%d-gloo-ranks" % (args.workers, world)},
+            "iterations_to_tol": r.iters, "expected_iterations": expect,
+            "iterations_match_reference": (its == {expect}) if expect else None,
+            "theta_payload_bytes_per_solve": int(r.bytes_total), "backend": "torch+gloo"}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def run_other(args, rank, world, device, share):
