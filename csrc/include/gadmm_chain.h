@@ -161,4 +161,9 @@ struct PersistArgs {
   const unsigned* ep_push;  // [n_epochs][n_local] rank bitmask (own rank excluded)
   u32x4* const* peer_thg;   // [nranks]
   double* rres;             // optional K4 primal residual [max_iter][n] (see PhaseArgs::rres; owned tails)
+  // D-GADMM epoch chunks (per-worker kernel): no iteration beyond hard_stop runs (> 0); the monitor
+  // then reports done = 5 unless it decided a stop first. cont = 1: this launch continues a chunked
+  // solve with the SAME tag salt, so the tables still hold theta^{start_iter - 1} (heads wait for it,
+  // and a head's pending dual is flushed with epoch 0's -- the previous chunk's last -- chain).
+  int hard_stop, cont;
 };

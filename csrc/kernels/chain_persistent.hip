@@ -74,6 +74,10 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
     // ---------------------------------------------------------------- monitor workgroup
     double* vals = lds;  // [n]
     for (int it = a.start_iter;; ++it) {
+      if (a.hard_stop > 0 && it > a.hard_stop) {  // chunk exhausted without a stop decision
+        if (threadIdx.x == 0) a.ctl->done = 5;
+        return;
+      }
       const unsigned tag = make_tag(a.epoch, it);
       const int slot = it % a.ring;
       if (w0) {
@@ -106,7 +110,13 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
         }
         const unsigned long long dv = ((unsigned long long)tag << 32) | code;
         for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
-        if (code) stop_lds = 1;
+        if (code) {
+          stop_lds = 1;
+          if (a.hard_stop > 0) {  // chunked: the workers may stop at hard_stop before seeing this decision
+            a.ctl->done = (int)code;
+            a.ctl->conv_iter = it;
+          }
+        }
         const int k = it - a.start_iter;
         if (TL && k < a.timeline_iters) a.timeline[((long)blockIdx.x * a.timeline_iters + k) * 8] = (long long)now_ticks();
       }
@@ -180,19 +190,26 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
     tr[c] = (in && right >= 0) ? a.theta[(long)right * d + i] : 0.0;
   }
   const double half_yy = 0.5 * a.yy[li];
-  int pending = a.pending_in;
+  // a pending (lazy) dual is owed only by a worker that was a head in the last iteration run: in a
+  // D-GADMM continuation epoch 0 is that iteration's chain, and a tail must not flush twice
+  int pending = (a.pending_in && head) ? 1 : 0;
   int stop_code = 0, stop_iter = 0;
   lds_barrier();
 
   int it = a.start_iter;
+  bool hard_stopped = false;
   for (;; ++it) {
+    if (a.hard_stop > 0 && it > a.hard_stop) {  // end of this chunk's epochs: state = after hard_stop
+      hard_stopped = true;
+      break;
+    }
     if (it > a.max_iter + a.lag) break;
     const long long t_start = TL ? (long long)now_ticks() : 0;
     if (dyn && it == next_start) {
       // re-chain (dynamic_group_ADMM_closedForm.m:18-21): a worker that was a head still owes the
       // previous iteration's dual, computed with its OLD neighbours' theta^{it-1} (every worker that
       // reached this iteration has published theta^{it-1}); then it takes its new slot.
-      if (w0 && pending && it > a.start_iter) {
+      if (w0 && pending && (it > a.start_iter || a.cont)) {
         const unsigned tp = make_tag(a.epoch, it - 1);
         const int ok = wait_pair<NC, SYS>(rth, d, left >= 0 ? trow(left, it - 1) : -1, tp, tl,
                                           right >= 0 ? trow(right, it - 1) : -1, tp, tr, deadline);
@@ -232,7 +249,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
     double mun[NC];
     double rv = 0.0;  // REG: this lane's rhs element (the quad GEMV's input)
     if (w0) {
-      const bool need_nb = head ? it > a.start_iter : true;
+      const bool need_nb = head ? (it > a.start_iter || a.cont) : true;
       const int jnb = head ? it - 1 : it;
       const unsigned tnb = make_tag(a.epoch, jnb);
       const int ra = need_nb ? left : -1, rb = need_nb ? right : -1;
@@ -426,6 +443,9 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       a.ctl->iter = it;
       a.ctl->pending = 1;
       a.ctl->monitored = stop_iter;
+    } else if (blockIdx.x == 0 && hard_stopped) {  // done / conv_iter come from the monitor (rank 0)
+      a.ctl->iter = it;
+      a.ctl->pending = 1;
     }
   }
 }
@@ -552,6 +572,11 @@ int gadmm_chain_persistent_launch(const PersistArgs* args, hipStream_t st) {
   const PVariant v = pick_variant(a);
   if (!v.fn) {
     gadmm_set_error("persistent chain kernel: d=%d not eligible", a.d);
+    return -1;
+  }
+  if ((a.hard_stop > 0 || a.cont) && (!dyn || a.hard_stop < 0 || (a.hard_stop > 0 && a.hard_stop < a.start_iter))) {
+    gadmm_set_error("persistent chain kernel: epoch chunks (hard_stop %d, cont %d) need the dynamic mode and "
+                    "hard_stop >= start_iter", a.hard_stop, a.cont);
     return -1;
   }
   const int blocks = a.n_local + (a.has_monitor ? 1 : 0);

@@ -289,28 +289,82 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         per = float(np.sum(schedule.cost)) * (n_heads if cost_quirk else 1)
         com_cost = np.arange(1, iters + 1) * per
     elif want_persistent and eng.dynamic_eligible(fabric) \
-            and len(rechain_iterations(max_iter, schedule.coherence)) < 4096:
-        # D-GADMM in ONE persistent launch: the seeded chain sequence is drawn up front (batched,
-        # identical RNG stream), every worker switches neighbours/role at each epoch on the device.
+            and len(rechain_iterations(max_iter, schedule.coherence)) < (1 << 20):
+        # D-GADMM in persistent launches of up to `epoch_chunk` epochs each: the seeded chain sequence
+        # is drawn a chunk ahead (batched, the identical RNG stream), every worker switches neighbours /
+        # role at each epoch on the device. A chunk ends at a hard stop just before its last+1 epoch
+        # (whose neighbours already receive theta); unless the monitor decided a stop, the next launch
+        # continues with the same tag salt from there. Only the chains a solve reaches are drawn.
         engine_kind = "persistent-dynamic"
         rechains = rechain_iterations(max_iter, schedule.coherence)
+        chunk = max(1, int(opts.get("epoch_chunk", 64)))
+        if eng.dynamic_uses_blocked(fabric):  # the blocked kernel's dynamic mode runs every epoch in one launch
+            chunk = len(rechains) + 1
         saved = schedule.save()
-        Pn, Cn = schedule.prefetch_arrays(len(rechains))
-        P = np.concatenate([np.asarray(saved[1], dtype=np.int64)[None], Pn])
-        starts = np.concatenate([[1], rechains]).astype(np.int64)
-        r = eng.run_persistent(epochs=(starts, P), fabric=fabric)
-        iters, done = r.iters, r.done
-        p2p, mon, wire = r.p2p_bytes, r.monitor_bytes, r.wire_bytes
+        E_total = 1 + len(rechains)
+        ep_P = [np.asarray(saved[1], dtype=np.int64)]
+        ep_C = [saved[2]]
+        ep_start = [1]
+        drawn_P, drawn_C = [], []
+
+        def ensure(upto):  # epochs 0..upto drawn
+            need = upto + 1 - len(ep_P)
+            if need > 0:
+                Pn_, Cn_ = schedule.prefetch_arrays(need)
+                k0 = len(ep_start) - 1
+                ep_P.extend(list(Pn_))
+                ep_C.extend(list(Cn_))
+                ep_start.extend(int(v) for v in rechains[k0:k0 + need])
+                drawn_P.append(Pn_)
+                drawn_C.append(Cn_)
+
+        e0, start_iter, pending_in, cont = 0, 1, 0, False
+        done = iters = 0
+        last_launched = 0
+        while True:
+            e1 = min(e0 + chunk, E_total)  # this launch executes epochs e0 .. e1 - 1
+            look = e1 if e1 < E_total else e1 - 1  # + the next epoch's chain (push targets of theta^hard_stop)
+            ensure(look)
+            hard_stop = ep_start[e1] - 1 if e1 < E_total else 0
+            st_arr = np.asarray(ep_start[e0:look + 1], dtype=np.int64)
+            P_arr = np.stack(ep_P[e0:look + 1]).astype(np.int64)
+            r = eng.run_persistent(epochs=(st_arr, P_arr), fabric=fabric, start_iter=start_iter, pending_in=pending_in,
+                                   hard_stop=hard_stop, cont=cont)
+            done, iters = int(r.done), int(r.iters)
+            if comm.nranks > 1 and hard_stop > 0:
+                # the monitor rank holds the outcome of a chunk (the workers may stop at the hard stop
+                # before the decision of its last lag iterations reaches them)
+                import torch.distributed as dist
+                t = torch.tensor([float(done), float(iters)], dtype=torch.float64)
+                dist.broadcast(t, src=0, group=getattr(comm, "control_group", None))
+                done, iters = int(t[0].item()), int(t[1].item())
+            p2p, mon, wire = p2p + r.p2p_bytes, mon + r.monitor_bytes, wire + r.wire_bytes
+            last_launched = hard_stop if done == 5 else start_iter - 1 + int(r.iterations_launched)
+            if done != 5:
+                if done == 0:
+                    raise RuntimeError("D-GADMM chunk ended without an outcome (hard stop %d)" % hard_stop)
+                break
+            start_iter, pending_in, cont = hard_stop + 1, 1, True
+            e0 = e1 - 1  # epoch 0 of the next launch: this chunk's last (the flush of pending duals)
+        if done == 5:
+            done = 2
+        Pn = np.concatenate(drawn_P) if drawn_P else np.zeros((0, n_total), dtype=np.int64)
+        if drawn_C and any(c.dtype == object for c in drawn_C):
+            Cn = np.empty(sum(len(c) for c in drawn_C), dtype=object)
+            Cn[:] = [c for cc in drawn_C for c in cc]
+        else:
+            Cn = np.concatenate(drawn_C) if drawn_C else np.zeros((0, max(n_total - 1, 0)))
+        starts = np.asarray(ep_start, dtype=np.int64)
+        P = np.stack(ep_P).astype(np.int64)
         # per-epoch cost; the initial cost vector may be ragged (the v0 column-slice quirk)
-        csum = Cn.sum(axis=1) if Cn.dtype != object else np.asarray([float(np.sum(c)) for c in Cn])
+        csum = Cn.sum(axis=1) if (len(Cn) and Cn.dtype != object) else np.asarray([float(np.sum(c)) for c in Cn])
         per_it = np.concatenate([[float(np.sum(saved[2]))], csum]) * (n_heads if cost_quirk else 1)
         which = np.searchsorted(starts, np.arange(1, iters + 1), side="right") - 1
         com_cost = np.cumsum(per_it[which])
         # leave the schedule (and the engine's plan) where the epoch-by-epoch run would have left them
-        schedule.skip(saved, Pn, Cn, int(np.sum(rechains <= iters)))
-        last = int(r.iterations_launched)  # = ctl iter - 1: the run started at iteration 1
-        eng.set_path([int(v) for v in P[int(np.searchsorted(starts, max(last, 1), side="right") - 1)]], placement,
-                     rank)
+        schedule.skip(saved, Pn, Cn, int(np.sum(np.asarray(rechains) <= iters)))
+        eng.set_path([int(v) for v in P[int(np.searchsorted(starts, max(last_launched, 1), side="right") - 1)]],
+                     placement, rank)
     else:
         # D-GADMM: run epoch by epoch; at a re-chain iteration flush the heads' pending duals with the
         # old chain, install the new chain, continue. Every rank draws the same chain sequence.

@@ -395,6 +395,14 @@ class NativeChainEngine:
             return 0 if int(self.lib.gadmm_chain_persistent_lds_dyn(self.d, 0, self.nvar)) > 0 else 1
         return 0 if int(self.lib.gadmm_chain_persistent_lds(self.d, 0)) > 0 else 1
 
+    def dynamic_uses_blocked(self, fabric=None) -> bool:
+        """Whether a one-launch D-GADMM run takes the blocked kernel's dynamic mode (opt-in
+        GADMM_BLOCKED_DYN=1, one GPU, 12-wave layout) rather than the per-worker kernel. Only the
+        per-worker kernel runs epoch chunks (hard stop + continuation)."""
+        plan = self.blocked_plan(fabric) if self.model == "linear" else None
+        return (plan is not None and plan[3] == 1 and self.n_local == self.n_total
+                and os.environ.get("GADMM_BLOCKED_DYN", "0") == "1")
+
     def dynamic_eligible(self, fabric=None) -> bool:
         """One-launch D-GADMM (per-epoch chains in device tables): linear, every degree's inverse
         resident; several ranks need an xGMI fabric whose theta tables hold a ring of iteration slots."""
@@ -424,7 +432,7 @@ class NativeChainEngine:
 
     def run_persistent(self, lag: int = 4, timeout_s: float = 20.0, start_iter: int = 1,
                        pending_in: int = 0, fabric=None, timeline_iters: int = 0,
-                       epochs: Optional[Sequence] = None) -> EngineRun:
+                       epochs: Optional[Sequence] = None, hard_stop: int = 0, cont: bool = False) -> EngineRun:
         """Whole solve in one launch per GPU. State must be reset (``reset()``) or resumed by the
         caller. ``fabric``: an ``XgmiFabric`` for the multi-GPU device-initiated transport.
         ``timeline_iters > 0`` records s_memrealtime stamps (10 ns) of the first iterations into
@@ -435,15 +443,20 @@ class NativeChainEngine:
         ``(first_iterations (E,), paths (E, n))`` (the first epoch starts at ``start_iter``); every worker switches neighbours / role at each epoch start and flushes its
         pending head dual with the old chain first. With a ``fabric`` (several GPUs) each worker also
         pushes its theta to the ranks of its current and next-epoch neighbours (the fabric's theta
-        tables must hold ``table_slots >= lag + 4`` iteration slots)."""
+        tables must hold ``table_slots >= lag + 4`` iteration slots).
+        Epoch chunks (D-GADMM, per-worker kernel): ``hard_stop > 0`` runs no iteration past it (the
+        monitor rank's ``done`` is then 5 unless it decided a stop; the table should include the epoch
+        starting at ``hard_stop + 1``, whose neighbours receive theta^hard_stop); ``cont=True`` continues
+        the previous chunk from ``start_iter = hard_stop + 1`` with the same tag salt, epoch 0 being the
+        previous chunk's last epoch (its heads' pending duals are flushed with that chain)."""
         if epochs is not None:
             if not self.dynamic_eligible(fabric):
                 raise RuntimeError("dynamic persistent kernel not eligible for this engine/config")
         elif not self.persistent_eligible(fabric):
             raise RuntimeError("persistent kernel not eligible for this engine/config")
         plan = self.blocked_plan(fabric, timeline=timeline_iters > 0) if self.model == "linear" else None
-        if epochs is not None and (plan is None or plan[3] != 1 or timeline_iters > 0 or self.n_local != self.n_total
-                                   or os.environ.get("GADMM_BLOCKED_DYN", "0") != "1"):
+        if epochs is not None and (not self.dynamic_uses_blocked(fabric) or timeline_iters > 0 or hard_stop > 0
+                                   or cont):
             # D-GADMM: the blocked kernel's dynamic mode (opt-in GADMM_BLOCKED_DYN=1; one GPU, 12-wave
             # layout) is bit-identical but not faster: its epoch state pushes the kernel past the
             # SGPR budget (165 SGPR + 10 VGPR spills in the hot loop), 1.616 vs 1.623 ms per solve
@@ -493,11 +506,15 @@ class NativeChainEngine:
                         if epochs is not None else ()
             self._pbuf = (key, slot_t, pos_t, ptrs, push, dec_push, keep, [0])
         _, slot_t, pos_t, ptrs, push, dec_push, keep, epoch_box = self._pbuf
-        if fabric is not None:
+        if cont:  # same salt: the tables still hold theta^{start_iter - 1} of the previous chunk
+            epoch = self._salt
+            native.check(self.lib.gadmm_chain_engine_reset(self.handle, int(start_iter), int(pending_in)), "reset")
+        elif fabric is not None:
             epoch = fabric.next_epoch()
         else:
             epoch_box[0] = epoch_box[0] % 4095 + 1
             epoch = epoch_box[0]
+        self._salt = epoch
         pa = native.PersistArgs()
         pa.d, pa.n, pa.n_local, pa.start_iter, pa.max_iter = self.d, self.n_total, len(slots), int(start_iter), \
             self.max_iter
@@ -520,6 +537,7 @@ class NativeChainEngine:
         pa.trace, pa.ctl = self.trace.data_ptr(), self.ctl.data_ptr()
         pa.tstamp = self.tstamp.data_ptr()
         pa.rres = native.ptr(self.rres)
+        pa.hard_stop, pa.cont = int(hard_stop), 1 if cont else 0
         ep_keep = None
         if epochs is not None:
             if isinstance(epochs, tuple) and len(epochs) == 2 and isinstance(epochs[1], np.ndarray):
@@ -528,8 +546,8 @@ class NativeChainEngine:
             else:
                 starts = np.asarray([int(e[0]) for e in epochs], dtype=np.int64)
                 P = np.asarray([list(e[1]) for e in epochs], dtype=np.int64)       # (E, n) position -> worker
-            if starts[0] != int(start_iter) or np.any(starts[1:] <= starts[:-1]):
-                raise ValueError("epochs must start at start_iter and be increasing")
+            if (starts[0] > int(start_iter) if cont else starts[0] != int(start_iter)) or np.any(starts[1:] <= starts[:-1]):
+                raise ValueError("epochs must start at start_iter (continuations: at or before it) and increase")
             E, n = P.shape
             loc = np.asarray([int(w) for w in self.local_ids], dtype=np.int64)
             if plan is not None:
@@ -634,18 +652,22 @@ class NativeChainEngine:
         done, conv, nxt = c[1], c[2], c[0]
         if done == 4:
             raise HandoffTimeout("persistent chain kernel timed out (hand-off never completed)")
+        # a chunk that ran to its hard stop: count iterations start..hard_stop (only the monitor rank
+        # knows the outcome; callers agree on it across ranks)
+        last = conv if done in (1, 2, 3) else (int(hard_stop) if hard_stop > 0 else conv)
         p2p = msgs = mon = 0
-        if fabric is not None and conv >= start_iter:
+        if fabric is not None and last >= start_iter:
             # what this rank puts on xGMI for iterations start..conv (the reference's accounting; the
             # lag iterations run past the decision are not counted): theta rows to remote owners of the
             # neighbours, objective granules to the monitor rank, decisions from the monitor rank
-            ran = conv - start_iter + 1
+            conv_b = last
+            ran = conv_b - start_iter + 1
             if epochs is None:
                 owner = self._placement_owner
                 per_it = sum(len({int(owner[u]) for u in (s.left, s.right) if u >= 0} - {self.rank}) for s in slots)
                 msgs = per_it * ran
             else:
-                js = np.arange(start_iter, conv + 1)
+                js = np.arange(start_iter, conv_b + 1)
                 e_of = np.searchsorted(starts, js, side="right") - 1
                 m = mask[e_of]                                                  # (ran, n_local)
                 nxt_e = np.minimum(e_of + 1, E - 1)

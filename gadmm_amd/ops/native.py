@@ -105,6 +105,7 @@ class PersistArgs(ctypes.Structure):
         ("seg_lo", c_int), ("seg_hi", c_int), ("blk_npeer", c_int), ("dbg", c_int),
         ("blk_peer_lo", c_int * 8), ("blk_peer_hi", c_int * 8), ("blk_peer_tab", c_void_p),
         ("tstamp", c_void_p), ("ep_push", c_void_p), ("peer_thg", c_void_p), ("rres", c_void_p),
+        ("hard_stop", c_int), ("cont", c_int),
     ]
 
 

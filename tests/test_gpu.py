@@ -618,3 +618,26 @@ def test_logistic_persistent_kernel_matches_graph_engine(log24, log_obj0):
     t = chain_admm(m, list(range(24)), 24, 2e-4, log_obj0, 1e-4, 400, backend="torch", **kw)
     np.testing.assert_allclose(a.obj, t.obj[:53], rtol=1e-12)
     assert np.all(np.diff(a.time_trace) >= 0) and a.time_trace[-1] > 0
+
+
+@pytest.mark.parametrize("coherence,chunk", [(10, 4), (1, 16)])
+def test_dgadmm_epoch_chunks_bit_identical(lin24, lin_obj0, coherence, chunk):
+    """D-GADMM in chunks of persistent launches (hard stop before the chunk's last+1 epoch, then a
+    continuation with the same tag salt that flushes the pending head duals with the old chain) ==
+    one launch holding every epoch == the epoch-by-epoch graph engine: iterations, objective trace and
+    energy trace bit for bit; only the chains the solve reaches are drawn."""
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import dynamic_group_admm
+    from gadmm_amd.parallel import topology as T
+    m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
+    p0, c0, _ = T.find_path(24, np.random.default_rng(5))
+    run = lambda **o: dynamic_group_admm(m, 1.0, lin_obj0, 1e-4, 3000, p0, c0, coherence, seed=99,
+                                         engine_opts=dict(cache=False, **o))
+    a = run(epoch_chunk=chunk)
+    b = run(epoch_chunk=100000)
+    e = run(persistent=False)
+    assert a.extra["engine"] == b.extra["engine"] == "persistent-dynamic" and e.extra["engine"] == "epochs"
+    assert a.iters == b.iters == e.iters and a.converged
+    assert a.iters > chunk * coherence  # several launches were chained
+    assert np.array_equal(a.obj, b.obj) and np.array_equal(a.obj, e.obj)
+    assert np.array_equal(a.com_cost, b.com_cost)

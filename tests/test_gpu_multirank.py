@@ -165,7 +165,7 @@ def test_ipc_transport_logistic_two_ranks(log24):
         assert np.array_equal(np.asarray(r["trace"]), single.obj)
 
 
-def _dgadmm_rank(rank, world, n, mode):
+def _dgadmm_rank(rank, world, n, mode, chunk=64):
     import torch
     from gadmm_amd.benchmarks import headline_rank_problem
     from gadmm_amd.models import LinearRegression
@@ -182,7 +182,7 @@ def _dgadmm_rank(rank, world, n, mode):
         from gadmm_amd.parallel.xgmi import XgmiFabric
         fab = XgmiFabric(n, 50, 8, rank, world, dev, table_slots=8)
         comm = RankInfo(rank, world)
-        opts = {"fabric": fab, "state": False}
+        opts = {"fabric": fab, "state": False, "epoch_chunk": chunk}
     else:
         from gadmm_amd.parallel.ipc import IpcComm
         comm = IpcComm(n, 50, 16, dev)
@@ -201,8 +201,8 @@ def _dgadmm_rank(rank, world, n, mode):
     return res
 
 
-@pytest.mark.parametrize("world,mode", [(2, "ipc"), (2, "xgmi"), (4, "xgmi")])
-def test_dgadmm_multirank_matches_one_gpu(world, mode, lin24):
+@pytest.mark.parametrize("world,mode,chunk", [(2, "ipc", 64), (2, "xgmi", 64), (4, "xgmi", 64), (2, "xgmi", 5)])
+def test_dgadmm_multirank_matches_one_gpu(world, mode, chunk, lin24):
     """D-GADMM across ranks -- epoch-by-epoch graph engine on the IPC transport, or ONE persistent launch
     per GPU on the xGMI fabric (theta pushed to current and next-epoch neighbours' GPUs) -- equals the
     one-GPU persistent-dynamic solve: iterations, objective trace (bit for bit) and energy trace."""
@@ -214,7 +214,7 @@ def test_dgadmm_multirank_matches_one_gpu(world, mode, lin24):
     p0, c0, _ = T.find_path(24, np.random.default_rng(5))
     one = dynamic_group_admm(m, 1.0, _obj0(24), 1e-4, 3000, p0, c0, 10, seed=99)
     assert one.extra["engine"] == "persistent-dynamic"
-    res = spawn(_dgadmm_rank, world, 24, mode, timeout=300)
+    res = spawn(_dgadmm_rank, world, 24, mode, chunk, timeout=300)
     want = "persistent-dynamic" if mode == "xgmi" else "epochs"
     for r in res:
         for it, conv, eng, _ in r["runs"]:

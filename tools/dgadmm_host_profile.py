@@ -22,10 +22,12 @@ Xf, yf = ds.stacked()
 obj0 = opt_linear(Xf.numpy(), yf.numpy())
 m = LinearRegression(ds.X.to(dev).contiguous(), ds.y.to(dev).contiguous())
 p0, c0, _ = T.find_path(24, np.random.default_rng(5))
+COH = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 
 
 def solve():
-    return dynamic_group_admm(m, 1.0, obj0, 1e-4, 3000, p0, c0, 10, seed=99, n_total=24, local_ids=list(range(24)))
+    return dynamic_group_admm(m, 1.0, obj0, 1e-4, 3000, p0, c0, COH, seed=99, n_total=24, local_ids=list(range(24)),
+                              engine_opts={"state": False})
 
 
 for _ in range(3):
