@@ -76,6 +76,8 @@ def main():
                     default="e1", help="e1 = the headline (default); the others are BASELINE.json configs[2..4]; "
                                        "cpu_gloo = configs[0]: the same GADMM over gloo ranks on the CPU (plumbing, "
                                        "no GPU; launch with torchrun --nproc-per-node 2)")
+    ap.add_argument("--coherence", type=int, default=10,
+                    help="dgadmm: iterations between re-chains (1 = BASELINE configs[3]'s 're-chaining each round')")
     ap.add_argument("--rows", type=int, default=1_250_000, help="real10m: rows per GPU")
     ap.add_argument("--dim", type=int, default=10_000, help="real10m: features")
     args = ap.parse_args()

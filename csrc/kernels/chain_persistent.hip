@@ -140,6 +140,15 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
   double crho = deg * rho;
   int ep = 0;
   int next_start = (dyn && a.n_epochs > 1) ? a.epoch_start[1] : 0x7fffffff;
+  // the next epoch's slot / position / start, loaded one epoch ahead: at coherence 1 a re-chain every
+  // iteration would otherwise put three dependent global loads on the critical path
+  PhaseSlot nsl = sl;
+  int npos = pos, nnext = 0x7fffffff;
+  if (dyn && a.n_epochs > 1) {
+    nsl = a.ep_slots[(long)a.n_local + blockIdx.x];
+    npos = a.ep_pos[(long)a.n_local + blockIdx.x];
+    nnext = a.n_epochs > 2 ? a.epoch_start[2] : 0x7fffffff;
+  }
   u32x4* const p0 = a.push ? a.push[2 * blockIdx.x] : nullptr;
   u32x4* const p1 = a.push ? a.push[2 * blockIdx.x + 1] : nullptr;
   const __amdgpu_buffer_rsrc_t rp0 = rsrc_of(p0 ? (const void*)p0 : (const void*)a.thg);
@@ -224,8 +233,8 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       }
       pending = 0;
       ++ep;
-      sl = a.ep_slots[(long)ep * a.n_local + blockIdx.x];
-      pos = a.ep_pos[(long)ep * a.n_local + blockIdx.x];
+      sl = nsl;
+      pos = npos;
       left = sl.left;
       right = sl.right;
       head = (pos % 2) == 0;
@@ -233,7 +242,12 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       crho = deg * rho;
       if constexpr (REG) vsel = a.deg_to_var[deg];
       else Ml = Mall + (long)a.deg_to_var[deg] * msz;
-      next_start = ep + 1 < a.n_epochs ? a.epoch_start[ep + 1] : 0x7fffffff;
+      next_start = nnext;
+      if (ep + 1 < a.n_epochs) {  // prefetch the epoch after (consumed at the next re-chain)
+        nsl = a.ep_slots[(long)(ep + 1) * a.n_local + blockIdx.x];
+        npos = a.ep_pos[(long)(ep + 1) * a.n_local + blockIdx.x];
+        nnext = ep + 2 < a.n_epochs ? a.epoch_start[ep + 2] : 0x7fffffff;
+      }
     }
     long long t_ready = 0, t_pub = 0, t_bar = 0, t_gemv = 0;
     // -- stop rule: decision of iteration it - lag (all workers leave at the same boundary). Its

@@ -297,7 +297,10 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         # continues with the same tag salt from there. Only the chains a solve reaches are drawn.
         engine_kind = "persistent-dynamic"
         rechains = rechain_iterations(max_iter, schedule.coherence)
-        chunk = max(1, int(opts.get("epoch_chunk", 64)))
+        # first launch: `epoch_chunk` epochs, each continuation twice the previous. Drawing a chain
+        # costs ~0.75 us on the host, a launch + read-back ~0.25 ms: 128 keeps coherence-10 solves
+        # (~51 epochs) to one launch with few spare chains, coherence-1 solves (~250) to two
+        chunk = max(1, int(opts.get("epoch_chunk", 128)))
         if eng.dynamic_uses_blocked(fabric):  # the blocked kernel's dynamic mode runs every epoch in one launch
             chunk = len(rechains) + 1
         saved = schedule.save()
@@ -346,6 +349,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
                 break
             start_iter, pending_in, cont = hard_stop + 1, 1, True
             e0 = e1 - 1  # epoch 0 of the next launch: this chunk's last (the flush of pending duals)
+            chunk *= 2
         if done == 5:
             done = 2
         Pn = np.concatenate(drawn_P) if drawn_P else np.zeros((0, n_total), dtype=np.int64)
@@ -397,8 +401,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             it = nxt
     torch.cuda.synchronize(model.device)
     wall = time.perf_counter() - t0
-    tr = eng.objective_trace(iters)
-    tt = eng.time_trace(iters)
+    tr, tt = eng.traces(iters)
     if fabric is not None and comm.nranks > 1:
         # the xGMI kernels decide on rank 0's monitor only: give every rank the same trace and clock
         import torch.distributed as dist

@@ -143,7 +143,7 @@ def run_logistic(args, rank, world, device, comm) -> Dict:
     m = LogisticRegression(ds.X.to(device).contiguous(), ds.y.to(device).contiguous(), lam=1e-5)
     obj0 = m.optimum(comm if world > 1 else None, n_total=n)
     rho, tol = 2e-4, 1e-4
-    opts = {"state": False}
+    opts = {"state": False, "residual": False}  # K4 monitoring off in the timed solves
     fabric, scomm = None, comm
     if world > 1:
         # one persistent launch per GPU over the xGMI fabric (chain_persistent_logistic.hip); every
@@ -192,7 +192,7 @@ def run_logistic_exact(args, rank, world, device, comm) -> Dict:
 
     def solve():
         return chain_admm(m, local, n, rho, obj0, tol, 2000, comm=comm, placement=pl, local_solver="newton",
-                          engine_opts={"state": False})
+                          engine_opts={"state": False, "residual": False})
 
     ms, r = _timed(solve, args.steps, args.warmup, device, world)
     return {"metric": "wall-clock to 1e-8 objective gap, GADMM logistic regression, exact (Newton) local solves "
@@ -219,8 +219,8 @@ def run_dgadmm(args, rank, world, device, comm) -> Dict:
     d = int(X_cpu.shape[2])
     m = LinearRegression(X_cpu.to(device).contiguous(), y_cpu.to(device).contiguous())
     p0, c0, _ = T.find_path(n, np.random.default_rng(5))
-    rho, tol, coh = 1.0, 1e-4, 10
-    opts = {"state": False}
+    rho, tol, coh = 1.0, 1e-4, int(getattr(args, "coherence", 10))
+    opts = {"state": False, "residual": False}  # K4 monitoring off in the timed solves
     fabric = None
     if world > 1:
         from .parallel.xgmi import XgmiFabric
@@ -247,8 +247,8 @@ def run_dgadmm(args, rank, world, device, comm) -> Dict:
                                   comm=comm, placement=pl, engine_opts=opts)
 
     ms, r = _timed(solve, args.steps, args.warmup, device, world)
-    out = {"metric": "wall-clock to 1e-4 objective gap, D-GADMM (findPath2 re-chaining every 10 iterations), "
-                     "linear regression (LinearRegression_Synthetic)",
+    out = {"metric": "wall-clock to 1e-4 objective gap, D-GADMM (findPath2 re-chaining every %d iteration%s), "
+                     "linear regression (LinearRegression_Synthetic)" % (coh, "" if coh == 1 else "s"),
            "ms": ms, "iters": r.iters, "expected": None, "backend": r.extra.get("backend"),
            "engine": r.extra.get("engine"), "transport": r.extra.get("transport"),
            "theta_payload_bytes_per_solve": _sum_ranks(r.bytes_sent, world),
@@ -386,7 +386,7 @@ def run_star(args, rank, world, device, comm) -> Dict:
     ms, r = _timed(solve, args.steps, args.warmup, device, world)
     # GADMM at the same rho on the same fabric (data-local chain): one warm-up solve (engine set-up,
     # cached inverses), then one timed solve
-    gopts = {"state": False}
+    gopts = {"state": False, "residual": False}
     if fabric is not None:
         gopts["fabric"] = fabric
     chain_admm(m, local, n, rho, obj0, tol, 20000, comm=comm, placement=pl, engine_opts=gopts)

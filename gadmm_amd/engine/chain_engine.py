@@ -678,6 +678,18 @@ class NativeChainEngine:
             mon = ran * (len(slots) * 16 if self.rank != 0 else 8 * (self.nranks - 1))
         return EngineRun(conv, done, nxt - start_iter, 1, (t1 - t0) * 1e3, p2p, msgs, mon, 2 * p2p)
 
+    def traces(self, upto: int):
+        """(objective trace, measured clock) of iterations 1..upto in ONE device-to-host copy."""
+        if upto <= 0:
+            return np.zeros((0,), dtype=np.float64), np.zeros((0,), dtype=np.float64)
+        with torch.cuda.stream(self.stream):
+            buf = torch.cat([self.trace[:upto], self.tstamp[:upto].view(torch.float64),
+                             self.t0stamp.view(torch.float64)]).cpu().numpy()
+        tr = buf[:upto].copy()
+        t = buf[upto:2 * upto].view(np.int64)
+        t0 = int(buf[2 * upto:].view(np.int64)[0])
+        return tr, np.where(t > 0, (t - t0) * 1e-8, 0.0)
+
     def time_trace(self, upto: int) -> np.ndarray:
         """Measured clock of the last solve: seconds from the solve start (``reset``) to the decision
         of each iteration (s_memrealtime, 100 MHz, stamped by the monitor / the iteration's finish on

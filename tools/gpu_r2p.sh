@@ -1,0 +1,7 @@
+set -o pipefail
+O=gpurun_out/r2p
+mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu.py -q -k "dgadmm" --timeout 170 --timeout-method thread > $O/g_dg.log 2>&1 && \
+timeout -k 10 400 python -u -m pytest tests/test_gpu_multirank.py -q -k "dgadmm" --timeout 170 --timeout-method thread > $O/mr_dg.log 2>&1 && \
+timeout -k 10 200 python -u bench.py --config dgadmm --coherence 1 --steps 10 --warmup 2 > $O/bc_dg_c1.json 2> $O/bc_dg_c1.err && \
+timeout -k 10 200 python -u bench.py --config dgadmm --steps 10 --warmup 2 > $O/bc_dg.json 2> $O/bc_dg.err
