@@ -166,4 +166,12 @@ struct PersistArgs {
   // solve with the SAME tag salt, so the tables still hold theta^{start_iter - 1} (heads wait for it,
   // and a head's pending dual is flushed with epoch 0's -- the previous chunk's last -- chain).
   int hard_stop, cont;
+  // XCD packing (one GPU, speed only): xcd = 1 launches an 8x wider grid whose blocks b % 8 != 0
+  // exit at once, dealing every working block onto one XCD; xcd = 2 also has the blocks post their
+  // XCC_ID into xchk ([XCHK] granules, zeroed by the launcher) and, if all agree, publish granules
+  // with plain stores that stay in that XCD's L2 (MI355X_MICROARCH.md price list). The env
+  // GADMM_XCD overrides xcd (A/B runs).
+  u32x4* xchk;
+  int xcd, pad_xcd;
 };
+constexpr int XCHK = 256;  // placement-check granules (>= workgroups of any XCD-packed launch)

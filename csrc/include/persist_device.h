@@ -20,6 +20,30 @@ __device__ __forceinline__ void store_granule(__amdgpu_buffer_rsrc_t rs, int byt
   else __builtin_amdgcn_raw_buffer_store_b128(g, rs, byte_off, 0, 16 /* sc1 */);
 }
 
+// Plain (write-back) granule store: the line stays in this XCD's L2, so a same-XCD `sc1` reader is
+// served from L2 instead of re-fetching it across the fabric (MI355X_MICROARCH.md, price list:
+// `sc1` stores DROP the line). Visible ONLY to readers on the same XCD: callers must have verified
+// the placement of every reader (chain_blocked.hip: xcd_verdict).
+__device__ __forceinline__ void store_granule_local(__amdgpu_buffer_rsrc_t rs, int byte_off, unsigned tag, double v) {
+  const unsigned long long bits = __double_as_longlong(v);
+  u32x4 g = {tag, (unsigned)(bits & 0xffffffffull), tag, (unsigned)(bits >> 32)};
+  __builtin_amdgcn_raw_buffer_store_b128(g, rs, byte_off, 0, 0);
+}
+
+// store_granule, or (one GPU, placement verified: `local` wave-uniform) store_granule_local
+template <bool SYS>
+__device__ __forceinline__ void put_granule(bool local, __amdgpu_buffer_rsrc_t rs, int byte_off, unsigned tag, double v) {
+  if (!SYS && local) store_granule_local(rs, byte_off, tag, v);
+  else store_granule<SYS>(rs, byte_off, tag, v);
+}
+
+// This wave's XCD (0-7).
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(x));
+  return x;
+}
+
 template <bool SYS>
 __device__ __forceinline__ bool load_granule(__amdgpu_buffer_rsrc_t rs, int byte_off, unsigned tag, double* v) {
   const u32x4 g = SYS ? __builtin_amdgcn_raw_buffer_load_b128(rs, byte_off, 0, 17)
@@ -180,6 +204,41 @@ __device__ __forceinline__ double reg_gemv(const double (&Mr)[DB], const double*
     a3 = fma(Mr[j + 3], x23.y, a3);
   }
   return ((a0 + a1) + a2) + a3;
+}
+
+constexpr unsigned XTAG = 0x5a5a0001u;  // placement-check granule tag (the launcher zeroes xchk first)
+
+// XCD packing (PersistArgs::xcd): every working block posts its XCC_ID into xchk[bid] and waits for
+// all nb; true iff they are all equal, i.e. every reader of every granule shares this block's L2.
+// The verdict is identical in every block (same inputs); false on a deadline (the run then times
+// out through its normal path, with sc1 stores). lds_flag: one int of LDS.
+__device__ __forceinline__ bool xcd_verdict(u32x4* xchk, int bid, int nb, unsigned long long deadline, int* lds_flag) {
+  const __amdgpu_buffer_rsrc_t rs = rsrc_of(xchk);
+  const int lane = threadIdx.x & 63;
+  if (threadIdx.x < 64) {
+    if (lane == 0) store_granule<false>(rs, bid * 16, XTAG, (double)xcc_id());
+    bool ok = true, same = true;
+    double first = -1.0;
+    for (int i0 = 0; i0 < nb; i0 += 64) {
+      const int i = i0 + lane;
+      double x = 0.0;
+      if (i < nb)
+        for (int spin = 0;; ++spin) {
+          if (load_granule<false>(rs, i * 16, XTAG, &x)) break;
+          if ((spin & 7) == 7 && now_ticks() > deadline) {
+            ok = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      if (i0 == 0) first = __shfl(x, 0, 64);  // block 0's XCD
+      same &= i >= nb || x == first;
+    }
+    same = __all(ok && same);
+    if (lane == 0) *lds_flag = same ? 1 : 0;
+  }
+  lds_barrier();
+  return __builtin_amdgcn_readfirstlane(*lds_flag) != 0;
 }
 
 }  // namespace persist

@@ -35,14 +35,15 @@
 namespace {
 
 constexpr int MAXW = 12;  // computed workers (waves) per workgroup: 3 waves per SIMD -> <= 170 VGPRs
-
 }  // namespace
+
+
 
 // ---- monitor workgroup (same protocol as chain_persistent): sums f_n in worker order, records the
 // trace and posts the stop decision of every iteration to every rank's decision ring
 template <bool SYS, bool TL>
 __device__ __forceinline__ void blocked_monitor(const PersistArgs& a, double* lds, int v, int lane,
-                                                unsigned long long deadline, __amdgpu_buffer_rsrc_t rob) {
+                                                unsigned long long deadline, __amdgpu_buffer_rsrc_t rob, int bid) {
   const int n = a.n;
   if (v != 0) return;
   double* vals = lds;  // [n]
@@ -79,7 +80,7 @@ __device__ __forceinline__ void blocked_monitor(const PersistArgs& a, double* ld
       const unsigned long long dv = ((unsigned long long)tag << 32) | code;
       for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
       const int kk = it - a.start_iter;
-      if (TL && kk < a.timeline_iters) a.timeline[((long)blockIdx.x * a.timeline_iters + kk) * 8] = (long long)now_ticks();
+      if (TL && kk < a.timeline_iters) a.timeline[((long)bid * a.timeline_iters + kk) * 8] = (long long)now_ticks();
     }
     if (__shfl((int)code, 0, 64)) return;
   }
@@ -90,7 +91,7 @@ __device__ __forceinline__ void blocked_monitor(const PersistArgs& a, double* ld
 template <int QT, bool SYS, bool DYN = false>
 __device__ __forceinline__ void blocked_objective(const PersistArgs& a, double* lds, int v, int lane, int q,
                                                   unsigned long long deadline, __amdgpu_buffer_rsrc_t rob,
-                                                  __amdgpu_buffer_rsrc_t rtab) {
+                                                  __amdgpu_buffer_rsrc_t rtab, bool local = false) {
   const int d = a.d, n = a.n;
   const long ring_base = 2L * n * 2 * d;  // theta ring [ring][n][d] after the exchange table
   PhaseSlot so = DYN ? a.ep_slots[q] : a.slots[q];
@@ -132,7 +133,7 @@ __device__ __forceinline__ void blocked_objective(const PersistArgs& a, double* 
     const double qv = quad_gemv<QT>(Aq, in ? x : 0.0, xo);  // (A th)_i in the order of every other engine
     const double part = in ? (0.5 * qv - bo) * x : 0.0;
     const double f = wave_sum_f64(part) + hy;
-    if (lane == 0) store_granule<SYS>(rob, ((it % a.ring) * n + so.gid) * 16, tag, f);
+    if (lane == 0) put_granule<SYS>(local, rob, ((it % a.ring) * n + so.gid) * 16, tag, f);
   }
 }
 
@@ -167,26 +168,32 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
   const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
   const __amdgpu_buffer_rsrc_t rtab = rsrc_of(a.blk_tab);
+  const bool packed = !SYS && a.xcd > 0;  // XCD packing (PersistArgs::xcd)
+  if (packed && (blockIdx.x & 7u)) return;  // a spacer block: only b % 8 == 0 work (one XCD)
+  const int bid = packed ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   if (threadIdx.x == 0) {
     abort_lds = 0;
     stop_lds = 0;
   }
   lds_barrier();
+  const long ring_base = 2L * n * 2 * d;  // theta ring [ring][n][d] after the exchange table
+  const long etab_base = 2L * n * 2 * d + (long)a.ring * n * d;
+  bool local = false;  // publish with plain stores (every block verified on this XCD)
+  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, W + Wo + 1, deadline, &stop_iter_lds);
 
-  if ((int)blockIdx.x == W + Wo) {
-    blocked_monitor<SYS, TL>(a, lds, v, lane, deadline, rob);
+  if (bid == W + Wo) {
+    blocked_monitor<SYS, TL>(a, lds, v, lane, deadline, rob, bid);
     return;
   }
 
-  const long ring_base = 2L * n * 2 * d;  // theta ring [ring][n][d] after the exchange table
-  if ((int)blockIdx.x >= W) {
-    const int q = seg_lo + ((int)blockIdx.x - W) * MAXW + v;  // an owned chain position
-    if (q <= seg_hi) blocked_objective<QT, SYS, DYN>(a, lds, v, lane, q, deadline, rob, rtab);
+  if (bid >= W) {
+    const int q = seg_lo + (bid - W) * MAXW + v;  // an owned chain position
+    if (q <= seg_hi) blocked_objective<QT, SYS, DYN>(a, lds, v, lane, q, deadline, rob, rtab, local);
     return;
   }
 
   // ---------------------------------------------------------------------- worker workgroup
-  const int g = blockIdx.x;
+  const int g = bid;
   const int s0 = seg_lo + g * L, e0 = min(seg_hi + 1, s0 + L) - 1;  // owned chain positions [s0, e0]
   const int ra = max(0, s0 - H), rb = min(n - 1, e0 + H);
   const int nv = rb - ra + 1;
@@ -239,7 +246,6 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   // counter, and the epoch exchange table [2][n][2][d] after the theta ring
   int ep = 0, next_start = (DYN && a.n_epochs > 1) ? a.epoch_start[1] : 0x7fffffff;
   int next_x = a.start_iter + k, xc = 0;
-  const long etab_base = 2L * n * 2 * d + (long)a.ring * n * d;
   if (threadIdx.x == 0) stop_iter_lds = 0;
   lds_barrier();
 
@@ -251,8 +257,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     const unsigned tag = make_tag(a.epoch, j + 1);
     const int sel = DYN ? (xc & 1) : (((j + 1 - a.start_iter) / k) & 1);
     const int base = ((sel * n + p) * 2) * d;
-    store_granule<SYS>(rtab, (base + lane) * 16, tag, th);
-    store_granule<SYS>(rtab, (base + d + lane) * 16, tag, mu);
+    put_granule<SYS>(local, rtab, (base + lane) * 16, tag, th);
+    put_granule<SYS>(local, rtab, (base + d + lane) * 16, tag, mu);
     for (int q = 0; q < a.blk_npeer; ++q)
       if (p >= a.blk_peer_lo[q] && p <= a.blk_peer_hi[q]) {
         const __amdgpu_buffer_rsrc_t rpe = rsrc_of(a.blk_peer_tab[q]);
@@ -273,8 +279,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         const long eb = etab_base + (long)((ep + 1) & 1) * n * 2 * d;  // this switch's slot
         if (owned && in) {  // the worker's state after iteration it - 1 (a head's dual still pending)
           const long base = eb + (long)w * 2 * d;
-          store_granule<SYS>(rtab, (int)((base + lane) * 16), tag, th);
-          store_granule<SYS>(rtab, (int)((base + d + lane) * 16), tag, mu);
+          put_granule<SYS>(local, rtab, (int)((base + lane) * 16), tag, th);
+          put_granule<SYS>(local, rtab, (int)((base + d + lane) * 16), tag, mu);
         }
         ++ep;
         next_start = ep + 1 < a.n_epochs ? a.epoch_start[ep + 1] : 0x7fffffff;
@@ -376,8 +382,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       }
       thS[u * 64 + lane] = th;
       if (owned && in && !(TL && (a.dbg & 2)))
-        store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
-                             make_tag(a.epoch, it), th);
+        put_granule<SYS>(local, rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
+                         make_tag(a.epoch, it), th);
     }
     pending = 1;
     lds_barrier();
@@ -411,8 +417,9 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       th = tn;
       thS[u * 64 + lane] = th;
       if (owned && in) {
-        if (!(TL && (a.dbg & 2))) store_granule<SYS>(rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
-                             make_tag(a.epoch, it), th);
+        if (!(TL && (a.dbg & 2)))
+          put_granule<SYS>(local, rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
+                           make_tag(a.epoch, it), th);
         if (xnext) publish(it);
       }
       if (a.rres && owned) {  // K4 primal residual of the tail's two edges (after the publish)
@@ -522,7 +529,7 @@ __global__ void __launch_bounds__(64 * PWW) chain_blocked_pair_kernel(PersistArg
   }
   lds_barrier();
   if ((int)blockIdx.x == W + Wo) {
-    blocked_monitor<SYS, false>(a, lds, v, lane, deadline, rob);
+    blocked_monitor<SYS, false>(a, lds, v, lane, deadline, rob, (int)blockIdx.x);
     return;
   }
   const long ring_base = 2L * n * 2 * d;
@@ -812,6 +819,7 @@ long gadmm_chain_blocked_tab_granules(int n, int d, int ring) { return 2L * n * 
 long gadmm_chain_blocked_tab_granules_dyn(int n, int d, int ring) { return 4L * n * 2 * d + (long)ring * n * d; }
 
 long gadmm_resident_capacity(const void* fn, int threads, size_t shm);  // chain_persistent.hip
+int gadmm_xcd_mode(const PersistArgs* a, int blocks, long cap_total);  // chain_persistent.hip
 
 int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   const PersistArgs& a = *args;
@@ -883,14 +891,18 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
     gadmm_set_error("blocked chain kernel: %d workgroups but only %ld can be resident", blocks, cap);
     return -2;
   }
+  const int xcd = gadmm_xcd_mode(&a, blocks, cap);
+  const int grid = xcd > 0 ? 8 * blocks : blocks;
   if (lds > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   PersistArgs ka = a;
   {
     const char* e = getenv("GADMM_BLK_DBG");  // experiment bits: 1 no stop polling, 2 no objective ring stores
     ka.dbg = e ? atoi(e) : 0;
   }
+  ka.xcd = xcd;
+  if (xcd > 1) GADMM_CHECK(hipMemsetAsync(a.xchk, 0, (size_t)XCHK * 16, st));
   void* kargs[] = {&ka};
-  GADMM_CHECK(hipLaunchKernel(fn, dim3(blocks), dim3(64 * MAXW), kargs, (size_t)lds, st));
+  GADMM_CHECK(hipLaunchKernel(fn, dim3(grid), dim3(64 * MAXW), kargs, (size_t)lds, st));
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

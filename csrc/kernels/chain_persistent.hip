@@ -64,13 +64,19 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
   auto trow = [&](int w, int j) -> int { return ring_tab ? (j % a.ring) * n + w : w; };
   const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
   const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
+  __shared__ int xcd_lds;
+  const bool packed = !SYS && a.xcd > 0;   // XCD packing (PersistArgs::xcd)
+  if (packed && (blockIdx.x & 7u)) return;  // a spacer block: only b % 8 == 0 work (one XCD)
+  const int bid = packed ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   if (threadIdx.x == 0) {
     abort_lds = 0;
     stop_lds = 0;
   }
   lds_barrier();
+  bool local = false;  // publish with plain stores (every block verified on this XCD)
+  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds);
 
-  if (a.has_monitor && (int)blockIdx.x == a.n_local) {
+  if (a.has_monitor && bid == a.n_local) {
     // ---------------------------------------------------------------- monitor workgroup
     double* vals = lds;  // [n]
     for (int it = a.start_iter;; ++it) {
@@ -118,7 +124,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
           }
         }
         const int k = it - a.start_iter;
-        if (TL && k < a.timeline_iters) a.timeline[((long)blockIdx.x * a.timeline_iters + k) * 8] = (long long)now_ticks();
+        if (TL && k < a.timeline_iters) a.timeline[((long)bid * a.timeline_iters + k) * 8] = (long long)now_ticks();
       }
       lds_barrier();
       if (stop_lds) return;
@@ -130,8 +136,8 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
   // variant only): workgroup b is local worker b for the whole launch and takes its slot / position
   // of each epoch from ep_slots / ep_pos (chains pre-drawn by the seeded schedule on the host).
   const bool dyn = a.n_epochs > 0;
-  PhaseSlot sl = dyn ? a.ep_slots[blockIdx.x] : a.slots[blockIdx.x];
-  int pos = dyn ? a.ep_pos[blockIdx.x] : a.pos[blockIdx.x];
+  PhaseSlot sl = dyn ? a.ep_slots[bid] : a.slots[bid];
+  int pos = dyn ? a.ep_pos[bid] : a.pos[bid];
   const int li = sl.li, w = sl.gid;
   int left = sl.left, right = sl.right;
   bool head = (pos % 2) == 0;
@@ -145,12 +151,12 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
   PhaseSlot nsl = sl;
   int npos = pos, nnext = 0x7fffffff;
   if (dyn && a.n_epochs > 1) {
-    nsl = a.ep_slots[(long)a.n_local + blockIdx.x];
-    npos = a.ep_pos[(long)a.n_local + blockIdx.x];
+    nsl = a.ep_slots[(long)a.n_local + bid];
+    npos = a.ep_pos[(long)a.n_local + bid];
     nnext = a.n_epochs > 2 ? a.epoch_start[2] : 0x7fffffff;
   }
-  u32x4* const p0 = a.push ? a.push[2 * blockIdx.x] : nullptr;
-  u32x4* const p1 = a.push ? a.push[2 * blockIdx.x + 1] : nullptr;
+  u32x4* const p0 = a.push ? a.push[2 * bid] : nullptr;
+  u32x4* const p1 = a.push ? a.push[2 * bid + 1] : nullptr;
   const __amdgpu_buffer_rsrc_t rp0 = rsrc_of(p0 ? (const void*)p0 : (const void*)a.thg);
   const __amdgpu_buffer_rsrc_t rp1 = rsrc_of(p1 ? (const void*)p1 : (const void*)a.thg);
 
@@ -244,8 +250,8 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       else Ml = Mall + (long)a.deg_to_var[deg] * msz;
       next_start = nnext;
       if (ep + 1 < a.n_epochs) {  // prefetch the epoch after (consumed at the next re-chain)
-        nsl = a.ep_slots[(long)(ep + 1) * a.n_local + blockIdx.x];
-        npos = a.ep_pos[(long)(ep + 1) * a.n_local + blockIdx.x];
+        nsl = a.ep_slots[(long)(ep + 1) * a.n_local + bid];
+        npos = a.ep_pos[(long)(ep + 1) * a.n_local + bid];
         nnext = ep + 2 < a.n_epochs ? a.epoch_start[ep + 2] : 0x7fffffff;
       }
     }
@@ -347,7 +353,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       for (int c = 0; c < NC; ++c) {  // publish theta^it: local table + remote neighbours' tables
         const int i = lane + 64 * c;
         if (i < d) {
-          store_granule<SYS>(rth, (trow(w, it) * d + i) * 16, tag, tn[c]);
+          put_granule<SYS>(local, rth, (trow(w, it) * d + i) * 16, tag, tn[c]);
           if (p0) store_granule<SYS>(rp0, (w * d + i) * 16, tag, tn[c]);
           if (p1) store_granule<SYS>(rp1, (w * d + i) * 16, tag, tn[c]);
         }
@@ -355,8 +361,8 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       if (SYS && dyn && a.ep_push) {
         // D-GADMM across GPUs: to the ranks of this epoch's neighbours, and of the next epoch's when
         // it starts at it + 1 (a new neighbour's head reads theta^it as its previous iterate)
-        unsigned mask = a.ep_push[(long)ep * a.n_local + blockIdx.x];
-        if (it + 1 == next_start) mask |= a.ep_push[(long)(ep + 1) * a.n_local + blockIdx.x];
+        unsigned mask = a.ep_push[(long)ep * a.n_local + bid];
+        if (it + 1 == next_start) mask |= a.ep_push[(long)(ep + 1) * a.n_local + bid];
         while (mask) {
           const int r = __builtin_ctz(mask);
           mask &= mask - 1u;
@@ -420,12 +426,12 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
     }
     if (w0) {
       const double f = wave_sum_f64(part) + half_yy;
-      if (lane == 0) store_granule<SYS>(rob, ((it % a.ring) * n + w) * 16, make_tag(a.epoch, it), f);
+      if (lane == 0) put_granule<SYS>(local, rob, ((it % a.ring) * n + w) * 16, make_tag(a.epoch, it), f);
 #pragma unroll
       for (int c = 0; c < NC; ++c) th[c] = tn[c];
       const int k = it - a.start_iter;
       if (TL && lane == 0 && k < a.timeline_iters) {
-        long long* tl = a.timeline + ((long)blockIdx.x * a.timeline_iters + k) * 8;
+        long long* tl = a.timeline + ((long)bid * a.timeline_iters + k) * 8;
         tl[0] = t_start;
         tl[1] = t_ready;
         tl[2] = t_pub;
@@ -451,13 +457,13 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
   if (threadIdx.x == 0) {
     if (abort_lds) {
       a.ctl->done = 4;
-    } else if (blockIdx.x == 0 && stop_code) {
+    } else if (bid == 0 && stop_code) {
       a.ctl->done = stop_code;
       a.ctl->conv_iter = stop_iter;
       a.ctl->iter = it;
       a.ctl->pending = 1;
       a.ctl->monitored = stop_iter;
-    } else if (blockIdx.x == 0 && hard_stopped) {  // done / conv_iter come from the monitor (rank 0)
+    } else if (bid == 0 && hard_stopped) {  // done / conv_iter come from the monitor (rank 0)
       a.ctl->iter = it;
       a.ctl->pending = 1;
     }
@@ -563,6 +569,19 @@ extern "C" long gadmm_resident_capacity(const void* fn, int threads, size_t shm)
   return (long)per_cu * cus;
 }
 
+// Effective XCD packing mode of a launch of `blocks` working workgroups (PersistArgs::xcd; env
+// GADMM_XCD overrides it for A/B runs): one GPU only, and only when all of them fit on one XCD
+// (cap_total / 8 of the `cap_total` resident slots), since packing deals every one of them there.
+extern "C" int gadmm_xcd_mode(const PersistArgs* a, int blocks, long cap_total) {
+  int x = a->xcd;
+  if (const char* e = getenv("GADMM_XCD")) x = atoi(e);
+  if (x < 0) x = 0;
+  if (x > 2) x = 2;
+  if (a->sys_scope || a->nranks > 1 || blocks > XCHK || (long)blocks > cap_total / 8) x = 0;
+  if (x == 2 && !a->xchk) x = 1;
+  return x;
+}
+
 extern "C" {
 
 // Workgroups the persistent kernel for `args` can keep resident (0: shape not eligible).
@@ -608,8 +627,11 @@ int gadmm_chain_persistent_launch(const PersistArgs* args, hipStream_t st) {
     return -1;
   }
   if (v.shm > 65536) GADMM_CHECK(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v.shm));
-  void* kargs[] = {const_cast<PersistArgs*>(&a)};
-  GADMM_CHECK(hipLaunchKernel(v.fn, dim3(blocks), dim3(v.threads), kargs, v.shm, st));
+  PersistArgs ka = a;
+  ka.xcd = gadmm_xcd_mode(&a, blocks, cap);
+  if (ka.xcd > 1) GADMM_CHECK(hipMemsetAsync(a.xchk, 0, (size_t)XCHK * 16, st));
+  void* kargs[] = {&ka};
+  GADMM_CHECK(hipLaunchKernel(v.fn, dim3(ka.xcd > 0 ? 8 * blocks : blocks), dim3(v.threads), kargs, v.shm, st));
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

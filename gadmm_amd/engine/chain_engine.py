@@ -73,13 +73,16 @@ class NativeChainEngine:
                  max_iter: int = 1000, lam: float = 0.0, step: float = 0.0, max_inner: int = 100,
                  inner_tol: float = 1e-4, comm=None, block: int = 16, stream: Optional[torch.cuda.Stream] = None,
                  precomputed=None, force_monitor: bool = False, obj_mode: str = "exact", local_solver: str = "gd",
-                 chord: float = 0.02, residual: bool = False):
+                 chord: float = 0.02, residual: bool = False, xcd: int = 2):
         """``local_solver`` (logistic): "gd" = the reference's inexact inner GD (logReg_GD.m, step /
         max_inner / inner_tol), "newton" = exact local solves (group_ADMM_logistic.m semantics,
         csrc/kernels/chain_newton.hip; d, m <= 64). ``chord`` (newton): a worker reuses its last
         inverse Hessian while steps contract by at least this factor (0: refresh every step).
         ``residual``: the kernels also emit the K4 primal residual (sum over chain edges of
-        ||theta_n - theta_right||^2) per iteration, read back by ``primal_residual``."""
+        ||theta_n - theta_right||^2) per iteration, read back by ``primal_residual``. ``xcd`` (one GPU,
+        persistent kernels): 0 default grid, 1 deal every working workgroup onto one XCD, 2 also
+        publish with L2-resident plain stores once the kernel has verified that placement
+        (PersistArgs::xcd; speed only, results are bit-identical)."""
         if not X_loc.is_cuda:
             raise ValueError("NativeChainEngine runs on a HIP device; use the torch algorithms on CPU")
         # the kernels read raw f64 pointers: anything else (e.g. float32 labels from torch.where) would be
@@ -140,6 +143,7 @@ class NativeChainEngine:
             self.hinv = torch.zeros((nl, 64 * 64 + 8), dtype=f64, device=dev) \
                 if local_solver == "newton" and nl > 0 else None
             self.chord = float(chord)
+            self.xcd = int(xcd)
             # K4 primal residual: per (iteration, worker) contributions of the tails (owned rows only)
             self.rres = torch.zeros((self.max_iter * self.n_total,), dtype=f64, device=dev) if residual else None
             if d > 256:
@@ -537,6 +541,10 @@ class NativeChainEngine:
         pa.trace, pa.ctl = self.trace.data_ptr(), self.ctl.data_ptr()
         pa.tstamp = self.tstamp.data_ptr()
         pa.rres = native.ptr(self.rres)
+        if fabric is None:  # XCD packing (one GPU): see PersistArgs::xcd
+            if getattr(self, "_xchk", None) is None:
+                self._xchk = torch.zeros((256 * 4,), dtype=torch.int32, device=dev)
+            pa.xchk, pa.xcd = self._xchk.data_ptr(), int(self.xcd)
         pa.hard_stop, pa.cont = int(hard_stop), 1 if cont else 0
         ep_keep = None
         if epochs is not None:

@@ -106,6 +106,7 @@ class PersistArgs(ctypes.Structure):
         ("blk_peer_lo", c_int * 8), ("blk_peer_hi", c_int * 8), ("blk_peer_tab", c_void_p),
         ("tstamp", c_void_p), ("ep_push", c_void_p), ("peer_thg", c_void_p), ("rres", c_void_p),
         ("hard_stop", c_int), ("cont", c_int),
+        ("xchk", c_void_p), ("xcd", c_int), ("pad_xcd", c_int),
     ]
 
 

@@ -27,7 +27,8 @@ def test_abi_layout_matches_ctypes():
            ctypes.sizeof(native.PhaseArgs), native.PhaseArgs.rho.offset, native.PhaseArgs.ring.offset,
            native.PhaseArgs.inner_iters.offset, ctypes.sizeof(native.EngineDesc), native.EngineDesc.stream.offset,
            ctypes.sizeof(native.RunStats), ctypes.sizeof(native.PersistArgs), native.PersistArgs.rho.offset,
-           native.PersistArgs.ctl.offset, native.PhaseArgs.lgid.offset, native.EngineDesc.xport.offset]
+           native.PersistArgs.ctl.offset, native.PhaseArgs.lgid.offset, native.EngineDesc.xport.offset,
+           native.PersistArgs.xchk.offset]
     assert got == exp
 
 
