@@ -39,4 +39,6 @@ struct FoArgs {
   long long* time_trace;  // [max_iter] s_memrealtime ticks since the monitor started
   double* theta_out;   // [n][d]
   FoCtl* ctl;
+  u32x4* xchk;         // XCD packing: as PersistArgs::xchk / xcd (gadmm_chain.h)
+  int xcd, pad_x;
 };

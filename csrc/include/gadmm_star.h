@@ -30,4 +30,6 @@ struct StarArgs {
   ChainCtl* ctl;
   long long* timeline;           // optional [n_local + 1][timeline_iters][4] s_memrealtime: wait start,
                                  // inputs ready, theta published, objective posted (monitor: decided)
+  u32x4* xchk;                   // XCD packing (one GPU): as PersistArgs::xchk / xcd
+  int xcd, pad2;
 };

@@ -569,17 +569,22 @@ extern "C" long gadmm_resident_capacity(const void* fn, int threads, size_t shm)
   return (long)per_cu * cus;
 }
 
-// Effective XCD packing mode of a launch of `blocks` working workgroups (PersistArgs::xcd; env
-// GADMM_XCD overrides it for A/B runs): one GPU only, and only when all of them fit on one XCD
-// (cap_total / 8 of the `cap_total` resident slots), since packing deals every one of them there.
-extern "C" int gadmm_xcd_mode(const PersistArgs* a, int blocks, long cap_total) {
-  int x = a->xcd;
+// Effective XCD packing mode (PersistArgs::xcd / StarArgs::xcd `want`; env GADMM_XCD overrides it for
+// A/B runs) of a launch of `blocks` working workgroups: one GPU only (`multi` = 0), and only when all
+// of them fit on one XCD (cap_total / 8 of the `cap_total` resident slots), since packing deals every
+// one of them there. Mode 2 needs the placement-check buffer.
+extern "C" int gadmm_xcd_pick(int want, int multi, int blocks, long cap_total, const void* xchk) {
+  int x = want;
   if (const char* e = getenv("GADMM_XCD")) x = atoi(e);
   if (x < 0) x = 0;
   if (x > 2) x = 2;
-  if (a->sys_scope || a->nranks > 1 || blocks > XCHK || (long)blocks > cap_total / 8) x = 0;
-  if (x == 2 && !a->xchk) x = 1;
+  if (multi || blocks > XCHK || (long)blocks > cap_total / 8) x = 0;
+  if (x == 2 && !xchk) x = 1;
   return x;
+}
+
+extern "C" int gadmm_xcd_mode(const PersistArgs* a, int blocks, long cap_total) {
+  return gadmm_xcd_pick(a->xcd, a->sys_scope || a->nranks > 1, blocks, cap_total, a->xchk);
 }
 
 extern "C" {

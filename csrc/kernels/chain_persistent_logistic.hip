@@ -45,8 +45,14 @@ __global__ void __launch_bounds__(64) chain_persistent_logistic_kernel(PersistAr
   const __amdgpu_buffer_rsrc_t rth = rsrc_of(a.thg);
   const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
   const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
+  __shared__ int xcd_lds;
+  const bool packed = !SYS && a.xcd > 0;   // XCD packing (PersistArgs::xcd)
+  if (packed && (blockIdx.x & 7u)) return;  // a spacer block: only b % 8 == 0 work (one XCD)
+  const int bid = packed ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  bool local = false;  // publish with plain stores (every block verified on this XCD)
+  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds);
 
-  if (a.has_monitor && (int)blockIdx.x == a.n_local) {
+  if (a.has_monitor && bid == a.n_local) {
     // ---------------------------------------------------------------- monitor (one wave)
     double* vals = lds;  // [n]
     for (int it = a.start_iter;; ++it) {
@@ -87,13 +93,13 @@ __global__ void __launch_bounds__(64) chain_persistent_logistic_kernel(PersistAr
   }
 
   // ------------------------------------------------------------------ worker (one wave)
-  const PhaseSlot sl = a.slots[blockIdx.x];
+  const PhaseSlot sl = a.slots[bid];
   const int li = sl.li, w = sl.gid, left = sl.left, right = sl.right;
-  const bool head = (a.pos[blockIdx.x] % 2) == 0;
+  const bool head = (a.pos[bid] % 2) == 0;
   const double rho = a.rho, lam = g.lam, step = g.step;
   double* st = lds;  // QSTAGE doubles: quad GEMV staging
-  u32x4* const p0 = a.push ? a.push[2 * blockIdx.x] : nullptr;
-  u32x4* const p1 = a.push ? a.push[2 * blockIdx.x + 1] : nullptr;
+  u32x4* const p0 = a.push ? a.push[2 * bid] : nullptr;
+  u32x4* const p1 = a.push ? a.push[2 * bid + 1] : nullptr;
   const __amdgpu_buffer_rsrc_t rp0 = rsrc_of(p0 ? (const void*)p0 : (const void*)a.thg);
   const __amdgpu_buffer_rsrc_t rp1 = rsrc_of(p1 ? (const void*)p1 : (const void*)a.thg);
   const double* Xg = g.X + (long)li * m * d;
@@ -186,7 +192,7 @@ __global__ void __launch_bounds__(64) chain_persistent_logistic_kernel(PersistAr
     // -- publish theta^it: own table + the remote neighbours' tables
     const unsigned tag = make_tag(a.epoch, it);
     if (inj) {
-      store_granule<SYS>(rth, (w * d + lane) * 16, tag, x);
+      put_granule<SYS>(local, rth, (w * d + lane) * 16, tag, x);
       if (p0) store_granule<SYS>(rp0, (w * d + lane) * 16, tag, x);
       if (p1) store_granule<SYS>(rp1, (w * d + lane) * 16, tag, x);
     }
@@ -212,7 +218,7 @@ __global__ void __launch_bounds__(64) chain_persistent_logistic_kernel(PersistAr
     const double z = quad_gemv<T>(Xq, x, st);
     const double part = wave_sum_f64(ini ? softplus(-yv * z) : 0.0);
     const double xx = wave_sum_f64(inj ? x * x : 0.0);
-    if (lane == 0) store_granule<SYS>(rob, ((it % a.ring) * n + w) * 16, tag, lam * 0.5 * xx + part);
+    if (lane == 0) put_granule<SYS>(local, rob, ((it % a.ring) * n + w) * 16, tag, lam * 0.5 * xx + part);
   }
   // final state (plain stores; visible to the host after the kernel)
   if (inj) {
@@ -223,7 +229,7 @@ __global__ void __launch_bounds__(64) chain_persistent_logistic_kernel(PersistAr
     if (g.inner_iters) g.inner_iters[li] = used;
     if (abort) {
       a.ctl->done = 4;
-    } else if (blockIdx.x == 0 && stop_code) {
+    } else if (bid == 0 && stop_code) {
       a.ctl->done = stop_code;
       a.ctl->conv_iter = stop_iter;
       a.ctl->iter = it;
@@ -234,6 +240,7 @@ __global__ void __launch_bounds__(64) chain_persistent_logistic_kernel(PersistAr
 }
 
 extern "C" long gadmm_resident_capacity(const void* fn, int threads, size_t shm);
+extern "C" int gadmm_xcd_mode(const PersistArgs* a, int blocks, long cap_total);  // chain_persistent.hip
 
 static const void* logi_variant(const PersistArgs& a, const LogiArgs& g) {
   const int mx = a.d > g.m ? a.d : g.m;
@@ -284,8 +291,11 @@ int gadmm_chain_persistent_logistic_launch(const PersistArgs* args, const LogiAr
     return -2;
   }
   if (shm > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-  void* kargs[] = {const_cast<PersistArgs*>(&a), const_cast<LogiArgs*>(&g)};
-  GADMM_CHECK(hipLaunchKernel(fn, dim3(blocks), dim3(64), kargs, shm, st));
+  PersistArgs ka = a;
+  ka.xcd = gadmm_xcd_mode(&a, blocks, cap);
+  if (ka.xcd > 1) GADMM_CHECK(hipMemsetAsync(a.xchk, 0, (size_t)XCHK * 16, st));
+  void* kargs[] = {&ka, const_cast<LogiArgs*>(&g)};
+  GADMM_CHECK(hipLaunchKernel(fn, dim3(ka.xcd > 0 ? 8 * blocks : blocks), dim3(64), kargs, shm, st));
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

@@ -190,8 +190,13 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
   const __amdgpu_buffer_rsrc_t rtab = rsrc_of(a.tab);
   const __amdgpu_buffer_rsrc_t rpart = rsrc_of(a.part);
   FoCtl* ctl = a.ctl;
+  const bool packed = a.xcd > 0;            // XCD packing (FoArgs::xcd)
+  if (packed && (blockIdx.x & 7u)) return;  // a spacer block: only b % 8 == 0 work (one XCD)
+  const int bid = packed ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  bool local = false;  // publish with plain stores (every block verified on this XCD)
+  if (a.xcd > 1) local = xcd_verdict(a.xchk, bid, n + 1, deadline, &flag_lds);
 
-  if ((int)blockIdx.x == n) {
+  if (bid == n) {
     // ------------------------------------------------------------------ monitor (wave 0 only)
     if (wv != 0) return;
     double* vals = lds;  // [2 n]
@@ -251,7 +256,7 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
   }
 
   // -------------------------------------------------------------------- worker workgroup
-  const int w = blockIdx.x;
+  const int w = bid;
   const bool w0 = wv == 0;
   double* xs = lds + L.xs;
   double* dl = lds + L.dl;
@@ -382,7 +387,7 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
           th[c] = i < d ? -a.step * z : 0.0;
           if (i < d) {
             xs[i] = th[c];
-            store_granule<false>(rtab, ((slot * n + w) * d + i) * 16, tag, z);
+            put_granule<false>(local, rtab, ((slot * n + w) * d + i) * 16, tag, z);
           }
         }
       }
@@ -402,7 +407,7 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
           const int i = lane + 64 * c;
-          if (i < d) store_granule<false>(rtab, ((slot * n + w) * d + i) * 16, tag, pub[c]);
+          if (i < d) put_granule<false>(local, rtab, ((slot * n + w) * d + i) * 16, tag, pub[c]);
         }
       }
       int ok = 1;
@@ -419,8 +424,8 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
       }
       if (ok == 1 && lane == 0) {
         const int ps = it % a.ring;
-        store_granule<false>(rpart, ((ps * n + w) * 2) * 16, tag, f);
-        store_granule<false>(rpart, ((ps * n + w) * 2 + 1) * 16, tag, cnt);
+        put_granule<false>(local, rpart, ((ps * n + w) * 2) * 16, tag, f);
+        put_granule<false>(local, rpart, ((ps * n + w) * 2 + 1) * 16, tag, cnt);
       }
       if (lane == 0) flag_lds = ok;
     }
@@ -519,6 +524,8 @@ __global__ void __launch_bounds__(NT) fo_persistent_kernel(FoArgs a) {
     }
 }
 
+extern "C" int gadmm_xcd_pick(int want, int multi, int blocks, long cap_total, const void* xchk);  // chain_persistent.hip
+
 extern "C" {
 
 static int fo_mc(int model, int m) { return model == FO_LINEAR ? 0 : (m <= 64 ? 1 : (m <= 128 ? 2 : 0)); }
@@ -532,7 +539,7 @@ long gadmm_fo_lds(int model, int d, int m) {
 int gadmm_fo_abi_layout(long long* out, int n) {
   long long v[] = {(long long)sizeof(FoCtl), (long long)sizeof(FoArgs), (long long)offsetof(FoArgs, step),
                    (long long)offsetof(FoArgs, timeout_ticks), (long long)offsetof(FoArgs, A),
-                   (long long)offsetof(FoArgs, ctl)};
+                   (long long)offsetof(FoArgs, ctl), (long long)offsetof(FoArgs, xchk)};
   const int k = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n && i < k; ++i) out[i] = v[i];
   return k;
@@ -558,8 +565,13 @@ int gadmm_fo_launch(const FoArgs* a, void* stream) {
   const void* fn = fns[nci][mc];
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, (size_t)lds) != hipSuccess) return -4;
   if ((long)per_cu * prop.multiProcessorCount < a->n + 1) return -5;  // persistent: all must be resident
-  void* args[] = {const_cast<FoArgs*>(a)};
-  if (hipLaunchKernel(fn, dim3(a->n + 1), dim3(NT), args, (size_t)lds, (hipStream_t)stream) != hipSuccess) return -1;
+  FoArgs ka = *a;
+  ka.xcd = gadmm_xcd_pick(a->xcd, 0, a->n + 1, (long)per_cu * prop.multiProcessorCount, a->xchk);
+  if (ka.xcd > 1 && hipMemsetAsync(a->xchk, 0, (size_t)XCHK * 16, (hipStream_t)stream) != hipSuccess) return -1;
+  void* args[] = {&ka};
+  if (hipLaunchKernel(fn, dim3(ka.xcd > 0 ? 8 * (a->n + 1) : a->n + 1), dim3(NT), args, (size_t)lds, (hipStream_t)stream) !=
+      hipSuccess)
+    return -1;
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -36,8 +36,14 @@ __global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
   const __amdgpu_buffer_rsrc_t rth = rsrc_of(a.thg);
   const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
   const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
+  __shared__ int xcd_lds;
+  const bool packed = !SYS && a.xcd > 0;   // XCD packing (StarArgs::xcd)
+  if (packed && (blockIdx.x & 7u)) return;  // a spacer block: only b % 8 == 0 work (one XCD)
+  const int bid = packed ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  bool local = false;  // publish with plain stores (every block verified on this XCD)
+  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds);
 
-  if (a.has_monitor && (int)blockIdx.x == a.n_local) {
+  if (a.has_monitor && bid == a.n_local) {
     // ---- monitor: sum f_n in worker order, record, decide, fan the decision out
     double* vals = lds;
     for (int it = 1;; ++it) {
@@ -73,14 +79,14 @@ __global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
         const unsigned long long dv = ((unsigned long long)tag << 32) | code;
         for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
         if (a.timeline && it - 1 < a.timeline_iters)
-          a.timeline[((long)blockIdx.x * a.timeline_iters + it - 1) * 4] = (long long)now_ticks();
+          a.timeline[((long)bid * a.timeline_iters + it - 1) * 4] = (long long)now_ticks();
       }
       if (__shfl((int)code, 0, 64)) return;
     }
   }
 
   // ---- worker / hub
-  const int b = blockIdx.x;
+  const int b = bid;
   const int w = a.gid[b];
   const bool is_hub = w == hub;
   double Mq[4][QT], Aq[4][QT];
@@ -138,7 +144,7 @@ __global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
       }
       const double r = in ? (bb - lam) + rho * thh : 0.0;  // H'Y - C1 + rho theta_h   (:42)
       th = quad_gemv<QT>(Mq, r, st);
-      if (in) store_granule<SYS>(rup, (w * d + lane) * 16, make_tag(a.epoch, it), th);
+      if (in) put_granule<SYS>(local, rup, (w * d + lane) * 16, make_tag(a.epoch, it), th);
       if (tlr && lane == 0) tlr[2] = (long long)now_ticks();
     } else {
       // every worker's theta^it (the uploads) and the decision of it - lag
@@ -201,7 +207,7 @@ __global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
       th = thh;
       if (in) {
         const unsigned tg = make_tag(a.epoch, it);
-        for (int rr = 0; rr < a.nranks; ++rr) store_granule<SYS>(rsrc_of(a.peer_thg[rr]), (hub * d + lane) * 16, tg, thh);
+        for (int rr = 0; rr < a.nranks; ++rr) put_granule<SYS>(local, rsrc_of(a.peer_thg[rr]), (hub * d + lane) * 16, tg, thh);
         if (tlr && lane == 0) tlr[2] = (long long)now_ticks();
         // the workers' dual step, mirrored on the hub's copies (:84-88)
         // (from the LDS snapshot: once theta_h^it is out, worker q may already be overwriting its
@@ -213,7 +219,7 @@ __global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
     // f_n(theta_n^it) = 1/2 th' A th - b' th + 1/2 y'y  (the quadratic form of :95-101)
     const double q = quad_gemv<QT>(Aq, in ? th : 0.0, st);
     const double f = wave_sum_f64(in ? (0.5 * q - bb) * th : 0.0) + half_yy;
-    if (lane == 0) store_granule<SYS>(rob, ((it % a.ring) * n + w) * 16, make_tag(a.epoch, it), f);
+    if (lane == 0) put_granule<SYS>(local, rob, ((it % a.ring) * n + w) * 16, make_tag(a.epoch, it), f);
     if (tlr && lane == 0) tlr[3] = (long long)now_ticks();
   }
   if (in) {
@@ -233,6 +239,7 @@ __global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
 }
 
 extern "C" long gadmm_resident_capacity(const void* fn, int threads, size_t shm);
+extern "C" int gadmm_xcd_pick(int want, int multi, int blocks, long cap_total, const void* xchk);  // chain_persistent.hip
 
 static const void* star_variant(const StarArgs& a) {
   if (a.d > 64) return nullptr;
@@ -250,7 +257,7 @@ extern "C" {
 
 int gadmm_star_abi_layout(long long* out, int n) {
   long long v[] = {(long long)sizeof(StarArgs), (long long)offsetof(StarArgs, rho), (long long)offsetof(StarArgs, gid),
-                   (long long)offsetof(StarArgs, ctl)};
+                   (long long)offsetof(StarArgs, ctl), (long long)offsetof(StarArgs, xchk)};
   const int k = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n && i < k; ++i) out[i] = v[i];
   return k;
@@ -281,8 +288,11 @@ int gadmm_star_launch(const StarArgs* args, hipStream_t st) {
     return -2;
   }
   if (shm > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-  void* kargs[] = {const_cast<StarArgs*>(&a)};
-  GADMM_CHECK(hipLaunchKernel(fn, dim3(blocks), dim3(64), kargs, shm, st));
+  StarArgs ka = a;
+  ka.xcd = gadmm_xcd_pick(a.xcd, a.sys_scope || a.nranks > 1, blocks, cap, a.xchk);
+  if (ka.xcd > 1) GADMM_CHECK(hipMemsetAsync(a.xchk, 0, (size_t)XCHK * 16, st));
+  void* kargs[] = {&ka};
+  GADMM_CHECK(hipLaunchKernel(fn, dim3(ka.xcd > 0 ? 8 * blocks : blocks), dim3(64), kargs, shm, st));
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

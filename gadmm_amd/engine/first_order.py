@@ -101,6 +101,9 @@ class FirstOrderEngine:
         a.tab, a.part = self.tab.data_ptr(), self.part.data_ptr()
         a.obj_trace, a.cnt_trace, a.time_trace = obj.data_ptr(), cnt.data_ptr(), tms.data_ptr()
         a.theta_out, a.ctl = self.theta.data_ptr(), self.ctl.data_ptr()
+        if getattr(self, "_xchk", None) is None:  # XCD packing (FoArgs::xcd): placement-check granules
+            self._xchk = torch.zeros((256 * 4,), dtype=torch.int32, device=self.dev)
+        a.xchk, a.xcd = self._xchk.data_ptr(), 2
         cur = torch.cuda.current_stream(self.dev)
         self.stream.wait_stream(cur)
         with torch.cuda.stream(self.stream):

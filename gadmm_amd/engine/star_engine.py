@@ -65,6 +65,8 @@ class StarEngine:
                 self.peer_thg = torch.tensor([self._thg.data_ptr()], dtype=torch.int64, device=dev)
                 self.dec_push = torch.tensor([self._decg.data_ptr()], dtype=torch.int64, device=dev)
                 self._ptrs = (self._thg.data_ptr(), self._objg.data_ptr(), self._decg.data_ptr())
+                # XCD packing (one GPU; StarArgs::xcd): placement-check granules
+                self._xchk = torch.zeros((256 * 4,), dtype=torch.int32, device=dev)
             else:
                 self.peer_thg = torch.tensor(fabric.table_ptrs(), dtype=torch.int64, device=dev)
                 self.dec_push = torch.tensor(fabric.dec_all if fabric.dec_all else [0], dtype=torch.int64,
@@ -95,6 +97,8 @@ class StarEngine:
         a.thg, a.objg, a.decg = self._ptrs
         a.peer_thg, a.dec_push = self.peer_thg.data_ptr(), self.dec_push.data_ptr()
         a.trace, a.tstamp, a.ctl = self.trace.data_ptr(), self.tstamp.data_ptr(), self.ctl.data_ptr()
+        if self.fabric is None:
+            a.xchk, a.xcd = self._xchk.data_ptr(), 2
         return a
 
     def eligible(self) -> bool:

@@ -80,7 +80,7 @@ class FoArgs(ctypes.Structure):
         ("A", c_void_p), ("b", c_void_p), ("yy", c_void_p), ("X", c_void_p), ("Y", c_void_p),
         ("hsq", c_void_p), ("sched", c_void_p), ("tab", c_void_p), ("part", c_void_p),
         ("obj_trace", c_void_p), ("cnt_trace", c_void_p), ("time_trace", c_void_p), ("theta_out", c_void_p),
-        ("ctl", c_void_p),
+        ("ctl", c_void_p), ("xchk", c_void_p), ("xcd", c_int), ("pad_x", c_int),
     ]
 
 
@@ -127,7 +127,7 @@ class StarArgs(ctypes.Structure):
         ("gid", c_void_p), ("Minv", c_void_p), ("A", c_void_p), ("b", c_void_p), ("yy", c_void_p),
         ("theta", c_void_p), ("lam", c_void_p), ("lam_hub", c_void_p), ("thg", c_void_p), ("peer_thg", c_void_p),
         ("objg", c_void_p), ("decg", c_void_p), ("dec_push", c_void_p), ("trace", c_void_p), ("tstamp", c_void_p),
-        ("ctl", c_void_p), ("timeline", c_void_p),
+        ("ctl", c_void_p), ("timeline", c_void_p), ("xchk", c_void_p), ("xcd", c_int), ("pad2", c_int),
     ]
 
 

@@ -641,3 +641,55 @@ def test_dgadmm_epoch_chunks_bit_identical(lin24, lin_obj0, coherence, chunk):
     assert a.iters > chunk * coherence  # several launches were chained
     assert np.array_equal(a.obj, b.obj) and np.array_equal(a.obj, e.obj)
     assert np.array_equal(a.com_cost, b.com_cost)
+
+
+def _xcc_ids(xchk):
+    """XCC_IDs the blocks of the last XCD-packed launch posted (placement-check granules)."""
+    g = xchk.view(-1, 4).cpu().numpy().astype(np.int64) & 0xffffffff
+    ids = []
+    for t, lo, t2, hi in g:
+        if t != 0x5a5a0001 or t2 != t:
+            break
+        ids.append(float(np.array([(int(hi) << 32) | int(lo)], dtype=np.uint64).view(np.float64)[0]))
+    return ids
+
+
+def test_xcd_packing_bit_identical(lin24, lin_obj0, log24, log_obj0, monkeypatch):
+    """XCD packing (PersistArgs::xcd = 2, the default: working workgroups dealt onto one XCD, plain
+    L2-resident granule stores once every block reported the same XCC_ID) == the plain grid
+    (GADMM_XCD=0) bit for bit in every persistent kernel family: blocked chain, per-worker D-GADMM,
+    persistent logistic, star ADMM, first-order engine. The placement check itself must pass (all
+    blocks on one XCD), or the fast path would silently not run."""
+    from gadmm_amd.models import LinearRegression, LogisticRegression
+    from gadmm_amd.algorithms import chain_admm, dynamic_group_admm, standard_admm, gradient_descent, \
+        global_constants
+    from gadmm_amd.engine.chain_engine import NativeChainEngine
+    from gadmm_amd.parallel import topology as T
+    m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
+    ml = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
+    p0, c0, _ = T.find_path(24, np.random.default_rng(5))
+    step = global_constants(m)["stepsize"]
+    runs = {
+        "blocked": lambda: chain_admm(m, list(range(24)), 24, 3.0, lin_obj0, 1e-8, 3000,
+                                      engine_opts={"cache": False}),
+        "dgadmm": lambda: dynamic_group_admm(m, 1.0, lin_obj0, 1e-4, 3000, p0, c0, 1, seed=99,
+                                             engine_opts={"cache": False}),
+        "logistic": lambda: chain_admm(ml, list(range(24)), 24, 2e-4, log_obj0, 1e-4, 400, local_solver="gd",
+                                       step=2.2, engine_opts={"cache": False}),
+        "star": lambda: standard_admm(m, list(range(24)), 24, 1.0, lin_obj0, 1e-4, 1000),
+        "fo": lambda: gradient_descent(m, list(range(24)), 24, 3000, lin_obj0, step, backend="native"),
+    }
+    for name, fn in runs.items():
+        monkeypatch.setenv("GADMM_XCD", "0")
+        a = fn()
+        monkeypatch.setenv("GADMM_XCD", "2")
+        b = fn()
+        assert a.iters == b.iters, name
+        assert np.array_equal(np.asarray(a.obj), np.asarray(b.obj)), name
+    monkeypatch.delenv("GADMM_XCD")
+    eng = NativeChainEngine(lin24.X.to(DEV), lin24.y.to(DEV), list(range(24)), 24, "linear", rho=3.0,
+                            obj0=lin_obj0, tol=1e-8, max_iter=3000)
+    eng.set_path(list(range(24)), T.Placement.contiguous(24, 1), 0)
+    r = eng.run_persistent()
+    ids = _xcc_ids(eng._xchk)
+    assert r.done == 1 and len(ids) == 9 and len(set(ids)) == 1, (r.done, ids)

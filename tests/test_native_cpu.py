@@ -37,7 +37,8 @@ def test_fo_abi_layout_matches_ctypes():
     buf = (ctypes.c_longlong * 16)()
     k = lib.gadmm_fo_abi_layout(buf, 16)
     exp = [ctypes.sizeof(native.FoCtl), ctypes.sizeof(native.FoArgs), native.FoArgs.step.offset,
-           native.FoArgs.timeout_ticks.offset, native.FoArgs.A.offset, native.FoArgs.ctl.offset]
+           native.FoArgs.timeout_ticks.offset, native.FoArgs.A.offset, native.FoArgs.ctl.offset,
+           native.FoArgs.xchk.offset]
     assert list(buf[:k]) == exp
 
 
@@ -114,7 +115,7 @@ def test_star_abi_layout_matches_ctypes():
     buf = (ctypes.c_longlong * 8)()
     k = lib.gadmm_star_abi_layout(buf, 8)
     exp = [ctypes.sizeof(native.StarArgs), native.StarArgs.rho.offset, native.StarArgs.gid.offset,
-           native.StarArgs.ctl.offset]
+           native.StarArgs.ctl.offset, native.StarArgs.xchk.offset]
     assert list(buf[:k]) == exp
 
 
