@@ -392,8 +392,9 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     // ---- tail phase; the (idle head) decision wave fetches decision[it + 1 - lag]
     // the next iteration starts with a regular exchange (DYN: unless it starts a new epoch)
     const bool xnext = DYN ? (it + 1 == next_x && it + 1 != next_start) : (it + 1 - a.start_iter) % k == 0;
-    // tail-wave stamps (wave MAXW/2), timeline row 128 + g: [start, rhs, gemv, stores, barrier]
-    const bool tstamp = TL && v == MAXW / 2 && it - a.start_iter < a.timeline_iters && g < 128;
+    // tail-wave stamps (wave MAXW/2 by default), timeline row 128 + g: [start, rhs, gemv, stores, barrier]
+    // (GADMM_BLK_DBG bits 4-6 pick another tail wave: MAXW/2 + ((dbg >> 4) & 7))
+    const bool tstamp = TL && v == MAXW / 2 + ((a.dbg >> 4) & 7) && it - a.start_iter < a.timeline_iters && g < 128;
     long long tt[4] = {0, 0, 0, 0};
     if (active && !head) {
       if (tstamp) tt[0] = (long long)now_ticks();

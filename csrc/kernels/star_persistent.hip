@@ -6,9 +6,10 @@
 //   hub      theta_h = (A_h + (n-1) rho I)^-1 (b_h + sum lam_n + rho sum theta_n)   (:66-73)
 //   duals    lam_n += rho (theta_n - theta_h)                                        (:84-88)
 //   stop     |sum_n f_n(theta_n) - obj0| < tol                                       (:95-107)
-// Roles are resident waves (one per workgroup): a worker keeps (A_n + rho I)^-1 and A_n in VGPRs
-// (the quad layout of quad_gemv.h, d <= 64) and uploads theta_n (d doubles) as tagged 16-byte granules
-// into the hub rank's table; the hub polls those n-1 rows, sums them in worker order, solves, and
+// Roles are resident workgroups: a worker (one wave) keeps (A_n + rho I)^-1 and A_n in VGPRs (the
+// quad layout of quad_gemv.h, d <= 64) and uploads theta_n (d doubles) as tagged 16-byte granules into
+// the hub rank's table; the hub's helper waves poll those n-1 rows and sum them (fixed order: rows of
+// each helper in row order, then the helpers' partials in wave order); its wave 0 solves and
 // publishes theta_h into EVERY rank's table (the broadcast). A worker applies its dual update lazily
 // at the start of the next iteration, when it reads theta_h^i anyway; the hub keeps its own copies
 // of the n-1 duals (same arithmetic, bit-identical), so an upload is theta alone (the reference's
@@ -25,13 +26,24 @@
 #include <stdlib.h>
 #include <cstddef>
 
-constexpr int SB = 8;  // hub: upload rows polled per batch (a batch of 24 measured no faster: 7.9 vs 7.4 us per iteration)
+constexpr int SB = 8;  // hub: upload rows polled per batch by each hub wave
+// Waves per workgroup. The hub's HW - 1 helper waves poll its n - 1 upload rows (wave v: rows
+// q = v - 1 mod HW - 1), sum their rows' duals and thetas and mirror the workers' dual steps; wave 0
+// polls the stop decision, combines the partials, solves, broadcasts and evaluates the objective. One
+// wave polling 23 rows spent ~2.5 us per spin on issue and serialised batches (hub ready 5.2 us after
+// the last upload, profiles/r02_star). Worker and monitor workgroups use wave 0 only.
+constexpr int HW = 4;
 
 template <int QT, bool SYS>
-__global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
+__global__ void __launch_bounds__(64 * HW) star_persistent_kernel(StarArgs a) {
   extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ int oc_lds[HW];               // hub: each wave's poll outcome
+  __shared__ int stop_flag;                // hub: wave 0 saw a stop decision (helpers stop polling)
+  __shared__ __attribute__((aligned(16))) double thh_lds[64];  // hub: theta_h^it for the helpers' dual steps
+  __shared__ __attribute__((aligned(16))) double part_lds[(HW - 1) * 128];  // hub: helpers' (C1, term_1) partials
   const int d = a.d, n = a.n, hub = n - 1;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const bool in = lane < d;
   const __amdgpu_buffer_rsrc_t rth = rsrc_of(a.thg);
   const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
@@ -40,10 +52,13 @@ __global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
   const bool packed = !SYS && a.xcd > 0;   // XCD packing (StarArgs::xcd)
   if (packed && (blockIdx.x & 7u)) return;  // a spacer block: only b % 8 == 0 work (one XCD)
   const int bid = packed ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  if (threadIdx.x == 0) stop_flag = 0;
   bool local = false;  // publish with plain stores (every block verified on this XCD)
   if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds);
+  lds_barrier();
 
   if (a.has_monitor && bid == a.n_local) {
+    if (wv != 0) return;
     // ---- monitor: sum f_n in worker order, record, decide, fan the decision out
     double* vals = lds;
     for (int it = 1;; ++it) {
@@ -89,14 +104,15 @@ __global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
   const int b = bid;
   const int w = a.gid[b];
   const bool is_hub = w == hub;
+  if (!is_hub && wv != 0) return;
   double Mq[4][QT], Aq[4][QT];
-  quad_load<QT>(Mq, a.Minv + (long)b * d * d, d, true);
-  quad_load<QT>(Aq, a.A + (long)b * d * d, d, true);
+  quad_load<QT>(Mq, a.Minv + (long)b * d * d, d, wv == 0);
+  quad_load<QT>(Aq, a.A + (long)b * d * d, d, wv == 0);
   double* st = lds;  // QSTAGE doubles of quad-GEMV staging
   double* snap = lds + QSTAGE;  // hub: [n-1][64] this iteration's uploads, read once from the table
   double* lamS = snap + (n - 1) * 64;  // hub: [n-1][64] its copies of the workers' duals (LDS-resident)
-  if (is_hub && in)
-    for (int q = 0; q < hub; ++q) lamS[q * 64 + lane] = a.lam_hub[(long)q * d + lane];
+  if (is_hub && in && wv > 0)  // helper wave v owns rows q = v - 1 mod (HW - 1)
+    for (int q = wv - 1; q < hub; q += HW - 1) lamS[q * 64 + lane] = a.lam_hub[(long)q * d + lane];
   const double bb = in ? a.b[(long)b * d + lane] : 0.0;
   const double half_yy = 0.5 * a.yy[b];
   const double rho = a.rho;
@@ -108,7 +124,8 @@ __global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
   long long* tlr = nullptr;  // this workgroup's timeline row of the current iteration (debug)
   for (;; ++it) {
     if (it > a.max_iter + a.lag) break;
-    tlr = (a.timeline && it - 1 < a.timeline_iters) ? a.timeline + ((long)b * a.timeline_iters + it - 1) * 4 : nullptr;
+    tlr = (a.timeline && wv == 0 && it - 1 < a.timeline_iters) ? a.timeline + ((long)b * a.timeline_iters + it - 1) * 4
+                                                               : nullptr;
     if (tlr && lane == 0) tlr[0] = (long long)now_ticks();
     const bool check = it - 1 >= a.lag;
     const int jdec = it - a.lag;
@@ -147,73 +164,108 @@ __global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
       if (in) put_granule<SYS>(local, rup, (w * d + lane) * 16, make_tag(a.epoch, it), th);
       if (tlr && lane == 0) tlr[2] = (long long)now_ticks();
     } else {
-      // every worker's theta^it (the uploads) and the decision of it - lag
+      // every worker's theta^it (the uploads) and the decision of it - lag. Helper wave v >= 1 polls
+      // rows q = v - 1 + (HW - 1) j (bit j of `got`: seen by this lane; a seen row cannot change
+      // before the hub publishes), SB loads in flight before any is consumed, then sums its rows'
+      // duals and thetas in row order; wave 0 polls the decision and raises stop_flag on a stop,
+      // which ends the helpers' polls (the rows of it never come then).
       const unsigned tn = make_tag(a.epoch, it);
-      // rows already seen by this lane are not polled again (they cannot change before the hub
-      // publishes), so the spin that sees the last upload issues one load, not n - 1
-      // Loads go out in batches of SB before any is consumed: a load-then-test loop serialises the n - 1
-      // round trips (~0.35 us each: 8.9 us per iteration at n = 24, tools/star_sweep.py timeline).
-      unsigned long long got = 0ull;
-      for (int spin = 0;; ++spin) {
-        bool ok = true;
-        if (in) {
-          for (int q0 = 0; q0 < hub; q0 += SB) {
-            u32x4 g[SB];
+      if (wv > 0) {
+        unsigned long long got = 0ull;
+        for (int spin = 0;; ++spin) {
+          bool ok = true;
+          if (in) {
+            for (int j0 = 0; wv - 1 + (HW - 1) * j0 < hub; j0 += SB) {
+              u32x4 g[SB];
 #pragma unroll
-            for (int k = 0; k < SB; ++k) {
-              const int q = q0 + k;
-              const bool want = q < hub && !(q < 64 && ((got >> q) & 1ull));
-              g[k] = want ? load_raw<SYS>(rth, (q * d + lane) * 16) : u32x4{0u, 0u, 0u, 0u};
-            }
+              for (int k = 0; k < SB; ++k) {
+                const int j = j0 + k, q = wv - 1 + (HW - 1) * j;
+                const bool want = q < hub && !((got >> j) & 1ull);
+                g[k] = want ? load_raw<SYS>(rth, (q * d + lane) * 16) : u32x4{0u, 0u, 0u, 0u};
+              }
 #pragma unroll
-            for (int k = 0; k < SB; ++k) {
-              const int q = q0 + k;
-              if (q >= hub || (q < 64 && ((got >> q) & 1ull))) continue;
-              if (granule_ok(g[k], tn)) {
-                snap[q * 64 + lane] = granule_val(g[k]);  // lane-private: no barrier needed
-                if (q < 64) got |= 1ull << q;
-              } else {
-                ok = false;
+              for (int k = 0; k < SB; ++k) {
+                const int j = j0 + k, q = wv - 1 + (HW - 1) * j;
+                if (q >= hub || ((got >> j) & 1ull)) continue;
+                if (granule_ok(g[k], tn)) {
+                  snap[q * 64 + lane] = granule_val(g[k]);  // this wave's row: it alone reads it back
+                  got |= 1ull << j;
+                } else {
+                  ok = false;
+                }
               }
             }
           }
+          if (__all(ok)) { outcome = 1; break; }
+          if (__hip_atomic_load(&stop_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;  // outcome 0
+          if ((spin & 7) == 7 && now_ticks() > deadline) { outcome = 3; break; }
+          __builtin_amdgcn_s_sleep(1);
         }
-        if (!decided) {
-          dv = __shfl(load_dec<SYS>(&a.decg[jdec % a.ring]), 0, 64);
-          decided = (unsigned)(dv >> 32) == tj;
+        if (outcome == 1 && in) {  // C1 / term_1 partials over this wave's rows (:66-71)
+          double c1 = 0.0, s1 = 0.0;
+          for (int q = wv - 1; q < hub; q += HW - 1) {
+            c1 += lamS[q * 64 + lane];
+            s1 += snap[q * 64 + lane];
+          }
+          part_lds[(wv - 1) * 128 + lane] = c1;
+          part_lds[(wv - 1) * 128 + 64 + lane] = s1;
         }
-        if (decided && (unsigned)(dv & 0xffffffffu) != 0u) { outcome = 2; break; }
-        if (decided && __all(ok)) { outcome = 1; break; }
-        if ((spin & 7) == 7 && now_ticks() > deadline) { outcome = 3; break; }
-        __builtin_amdgcn_s_sleep(1);
+      } else {
+        for (int spin = 0;; ++spin) {
+          if (!decided) {
+            dv = __shfl(load_dec<SYS>(&a.decg[jdec % a.ring]), 0, 64);
+            decided = (unsigned)(dv >> 32) == tj;
+          }
+          if (decided && (unsigned)(dv & 0xffffffffu) != 0u) {
+            outcome = 2;
+            if (lane == 0) __hip_atomic_store(&stop_flag, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            break;
+          }
+          if (decided) { outcome = 1; break; }
+          if ((spin & 7) == 7 && now_ticks() > deadline) { outcome = 3; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
       }
-      if (outcome != 1) {
-        if (outcome == 2) { stop_code = (int)(unsigned)(dv & 0xffffffffu); stop_iter = jdec; }
+      if (lane == 0) oc_lds[wv] = outcome;
+      lds_barrier();  // the partials are in part_lds
+      int oc = oc_lds[0];
+      if (oc != 2)
+        for (int v = 1; v < HW; ++v)
+          if (oc_lds[v] == 3) oc = 3;
+      if (oc != 1) {
+        if (oc == 2) { stop_code = (int)(unsigned)(dv & 0xffffffffu); stop_iter = jdec; }
         else abort = 1;
         break;
       }
       if (tlr && lane == 0) tlr[1] = (long long)now_ticks();
-      // C1 = sum lam_n, term_1 = rho sum theta_n, in worker order (:66-71)
-      double c1 = 0.0, s1 = 0.0;
-      if (in) {
-#pragma unroll 8
-        for (int q = 0; q < hub; ++q) {
-          c1 += lamS[q * 64 + lane];
-          s1 += snap[q * 64 + lane];
+      if (wv == 0) {
+        double c1 = 0.0, s1 = 0.0;
+        if (in)
+          for (int v = 0; v < HW - 1; ++v) {
+            c1 += part_lds[v * 128 + lane];
+            s1 += part_lds[v * 128 + 64 + lane];
+          }
+        const double r = in ? (bb + c1) + rho * s1 : 0.0;
+        thh = quad_gemv<QT>(Mq, r, st);
+        th = thh;
+        if (in) {
+          const unsigned tg = make_tag(a.epoch, it);
+          for (int rr = 0; rr < a.nranks; ++rr) put_granule<SYS>(local, rsrc_of(a.peer_thg[rr]), (hub * d + lane) * 16, tg, thh);
+          if (tlr && lane == 0) tlr[2] = (long long)now_ticks();
         }
+        thh_lds[lane] = thh;
       }
-      const double r = in ? (bb + c1) + rho * s1 : 0.0;
-      thh = quad_gemv<QT>(Mq, r, st);
-      th = thh;
-      if (in) {
-        const unsigned tg = make_tag(a.epoch, it);
-        for (int rr = 0; rr < a.nranks; ++rr) put_granule<SYS>(local, rsrc_of(a.peer_thg[rr]), (hub * d + lane) * 16, tg, thh);
-        if (tlr && lane == 0) tlr[2] = (long long)now_ticks();
-        // the workers' dual step, mirrored on the hub's copies (:84-88)
+      lds_barrier();
+      if (wv != 0) {
+        // the workers' dual step, mirrored on the hub's copies (:84-88), each helper on its own rows
         // (from the LDS snapshot: once theta_h^it is out, worker q may already be overwriting its
         // table row with theta_q^{it+1})
-#pragma unroll 8
-        for (int q = 0; q < hub; ++q) lamS[q * 64 + lane] = lamS[q * 64 + lane] + rho * (snap[q * 64 + lane] - thh);
+        if (in) {
+          const double th_h = thh_lds[lane];
+          for (int q = wv - 1; q < hub; q += HW - 1)
+            lamS[q * 64 + lane] = lamS[q * 64 + lane] + rho * (snap[q * 64 + lane] - th_h);
+        }
+        continue;  // helpers: next iteration (their loop state matches wave 0's)
       }
     }
     // f_n(theta_n^it) = 1/2 th' A th - b' th + 1/2 y'y  (the quadratic form of :95-101)
@@ -222,13 +274,13 @@ __global__ void __launch_bounds__(64) star_persistent_kernel(StarArgs a) {
     if (lane == 0) put_granule<SYS>(local, rob, ((it % a.ring) * n + w) * 16, make_tag(a.epoch, it), f);
     if (tlr && lane == 0) tlr[3] = (long long)now_ticks();
   }
-  if (in) {
+  if (in && wv == 0) {
     a.theta[(long)b * d + lane] = th;
     a.lam[(long)b * d + lane] = is_hub ? 0.0 : lam;
-    if (is_hub)
-      for (int q = 0; q < hub; ++q) a.lam_hub[(long)q * d + lane] = lamS[q * 64 + lane];
   }
-  if (lane == 0) {
+  if (is_hub && in && wv > 0)  // each helper its own rows
+    for (int q = wv - 1; q < hub; q += HW - 1) a.lam_hub[(long)q * d + lane] = lamS[q * 64 + lane];
+  if (lane == 0 && wv == 0) {
     if (abort) a.ctl->done = 4;
     else if (b == 0 && stop_code) {
       a.ctl->done = stop_code;
@@ -269,7 +321,7 @@ long gadmm_star_capacity(const StarArgs* args) {
   if (!fn) return 0;
   const size_t shm = star_shm(*args);
   if (shm > 160 * 1024) return 0;
-  return gadmm_resident_capacity(fn, 64, shm);
+  return gadmm_resident_capacity(fn, 64 * HW, shm);
 }
 
 int gadmm_star_launch(const StarArgs* args, hipStream_t st) {
@@ -282,7 +334,7 @@ int gadmm_star_launch(const StarArgs* args, hipStream_t st) {
   }
   const size_t shm = star_shm(a);
   const int blocks = a.n_local + (a.has_monitor ? 1 : 0);
-  const long cap = gadmm_resident_capacity(fn, 64, shm);
+  const long cap = gadmm_resident_capacity(fn, 64 * HW, shm);
   if (blocks > cap) {
     gadmm_set_error("star kernel: %d workgroups but only %ld can be resident", blocks, cap);
     return -2;
@@ -292,7 +344,7 @@ int gadmm_star_launch(const StarArgs* args, hipStream_t st) {
   ka.xcd = gadmm_xcd_pick(a.xcd, a.sys_scope || a.nranks > 1, blocks, cap, a.xchk);
   if (ka.xcd > 1) GADMM_CHECK(hipMemsetAsync(a.xchk, 0, (size_t)XCHK * 16, st));
   void* kargs[] = {&ka};
-  GADMM_CHECK(hipLaunchKernel(fn, dim3(ka.xcd > 0 ? 8 * blocks : blocks), dim3(64), kargs, shm, st));
+  GADMM_CHECK(hipLaunchKernel(fn, dim3(ka.xcd > 0 ? 8 * blocks : blocks), dim3(64 * HW), kargs, shm, st));
   GADMM_CHECK(hipGetLastError());
   return 0;
 }
