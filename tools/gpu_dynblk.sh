@@ -1,0 +1,5 @@
+set -o pipefail
+O=gpurun_out/dynblk
+mkdir -p $O
+GADMM_BLOCKED_DYN=1 timeout -k 10 240 python3 -u tools/xcd_probe.py 1 8 > $O/dyn1_blk.json 2> $O/dyn1_blk.err && \
+GADMM_BLOCKED_DYN=1 timeout -k 10 240 python3 -u tools/xcd_probe.py 10 8 > $O/dyn10_blk.json 2> $O/dyn10_blk.err
