@@ -246,6 +246,12 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   // counter, and the epoch exchange table [2][n][2][d] after the theta ring
   int ep = 0, next_start = (DYN && a.n_epochs > 1) ? a.epoch_start[1] : 0x7fffffff;
   int next_x = a.start_iter + k, xc = 0;
+  // Only the positions whose result still reaches an owned one before the next exchange are solved:
+  // in phase phi of a block (phi = 0, 1 the head / tail phase of its first iteration, ...) that is the
+  // owned range widened by 2k - 1 - phi on each side; the rest of the halo is stale anyway. Fewer GEMV
+  // waves then share the SIMDs (three of the four phases of a k = 2 block run <= 1 per SIMD).
+  const int uo_lo = s0 - ra, uo_hi = e0 - ra;
+  int blk0 = a.start_iter;  // first iteration of the current block (after an exchange / re-chain)
   if (threadIdx.x == 0) stop_iter_lds = 0;
   lds_barrier();
 
@@ -322,6 +328,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         }
         pending = 0;
         next_x = it + k;
+        blk0 = it;
         lds_barrier();
         if (abort_lds) break;
       }
@@ -355,6 +362,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       }
       lds_barrier();  // refreshed halo theta visible to the neighbouring waves
       if (abort_lds) break;
+      blk0 = it;
       if constexpr (DYN) {
         next_x = it + k;
         ++xc;
@@ -363,7 +371,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     if (stamp) ts[1] = ts[2] = ts[3] = (long long)now_ticks();
 
     // ---- head phase
-    if (active && head) {
+    const int slack = 2 * k - 1 - 2 * (it - blk0);  // head phase; the tail phase has slack - 1
+    if (active && head && u >= uo_lo - slack && u <= uo_hi + slack) {
       const double tl = nbl ? thL[lane] : 0.0, tr = nbr ? thR[lane] : 0.0;
       double m = mu;
       if (pending) {  // lazy end-of-iteration dual (reference order)
@@ -396,7 +405,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     // (GADMM_BLK_DBG bits 4-6 pick another tail wave: MAXW/2 + ((dbg >> 4) & 7))
     const bool tstamp = TL && v == MAXW / 2 + ((a.dbg >> 4) & 7) && it - a.start_iter < a.timeline_iters && g < 128;
     long long tt[4] = {0, 0, 0, 0};
-    if (active && !head) {
+    if (active && !head && u >= uo_lo - (slack - 1) && u <= uo_hi + (slack - 1)) {
       if (tstamp) tt[0] = (long long)now_ticks();
       const double tl = nbl ? thL[lane] : 0.0, tr = nbr ? thR[lane] : 0.0;
       double r = bb - mu;
@@ -760,9 +769,22 @@ int gadmm_chain_blocked_plan(int n, int d, int want_k, int* k_out, int* len_out)
     len = MAXW - 4 * k;
   }
   if (len < 1) return 0;
+  // Owned positions per workgroup: the fewest whose launch (W worker + objective + monitor
+  // workgroups, one per CU) still fits on ONE XCD, so it can be packed there (PersistArgs::xcd).
+  // With the halo GEMVs skipped where unused, a shorter segment means lighter phases: at N = 24,
+  // L = 1 / 2 / 4 ran 1.94 / 1.98 / 2.07 ms (profiles/r02_halo_skip).
+  int cus_xcd = 32, dev = 0;
+  hipDeviceProp_t prop;
+  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount >= 8)
+    cus_xcd = prop.multiProcessorCount / 8;
+  for (int l = 1; l < len; ++l)
+    if ((n + l - 1) / l + (n + MAXW - 1) / MAXW + 1 <= cus_xcd) {
+      len = l;
+      break;
+    }
   if (const char* e = getenv("GADMM_BLOCK_L")) {  // owned positions per workgroup (tuning runs)
     const int want_len = atoi(e);
-    if (want_len >= 1 && want_len < len) len = want_len;
+    if (want_len >= 1 && want_len <= MAXW - 4 * k) len = want_len;
   }
   if (len > n) len = n;
   const int W = (n + len - 1) / len;

@@ -692,4 +692,6 @@ def test_xcd_packing_bit_identical(lin24, lin_obj0, log24, log_obj0, monkeypatch
     eng.set_path(list(range(24)), T.Placement.contiguous(24, 1), 0)
     r = eng.run_persistent()
     ids = _xcc_ids(eng._xchk)
-    assert r.done == 1 and len(ids) == 9 and len(set(ids)) == 1, (r.done, ids)
+    k, L, W, _pw = eng.blocked_plan()
+    nblocks = W + (24 + 11) // 12 + 1  # worker + objective workgroups + the monitor
+    assert r.done == 1 and len(ids) == nblocks and len(set(ids)) == 1, (r.done, ids)
