@@ -261,7 +261,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   // this GPU's table and into every peer GPU that computes position p too
   auto publish = [&](int j) {
     const unsigned tag = make_tag(a.epoch, j + 1);
-    const int sel = DYN ? (xc & 1) : (((j + 1 - a.start_iter) / k) & 1);
+    const int sel = xc & 1;  // exchange table slot: alternates per exchange (every rank counts alike)
     const int base = ((sel * n + p) * 2) * d;
     put_granule<SYS>(local, rtab, (base + lane) * 16, tag, th);
     put_granule<SYS>(local, rtab, (base + d + lane) * 16, tag, mu);
@@ -275,7 +275,23 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   unsigned long long dv_pref = 0;  // decision wave, lane 0: decision[it + 1 - lag] prefetched
   int it = a.start_iter;
   long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (;; ++it) {
+  // Objective-ring posts of owned workers go out in the phase their wave idles in: heads post
+  // theta^it during the tail phase, tails post theta^{it-1} at the start of iteration it
+  // (ring_defer), so neither sits on a phase's critical path. Ring and decision slots are counters
+  // (no integer division in the loop).
+  const int ring_p = (int)((ring_base + (long)(active ? p : 0) * d + lane) * 16);  // (slot 0, p, lane)
+  const int ring_slot_bytes = n * d * 16;
+  const bool ring_post = owned && in && !(TL && (a.dbg & 2));
+  bool ring_defer = false;
+  int rslot = a.start_iter % a.ring;                  // == it % ring
+  int dslot = (a.start_iter + 1 - a.lag) % a.ring;     // == (it + 1 - lag) % ring (>= 0 once polled)
+  if (dslot < 0) dslot += a.ring;
+  for (;; ++it, rslot = rslot + 1 == a.ring ? 0 : rslot + 1, dslot = dslot + 1 == a.ring ? 0 : dslot + 1) {
+    if (ring_defer) {  // tails: theta^{it-1}, before a re-chain may replace th
+      put_granule<SYS>(local, rtab, ring_p + (rslot == 0 ? a.ring - 1 : rslot - 1) * ring_slot_bytes,
+                       make_tag(a.epoch, it - 1), th);
+      ring_defer = false;
+    }
     if (it > a.max_iter + a.lag) break;
     const bool stamp = TL && v == 0 && it - a.start_iter < a.timeline_iters;  // wave-uniform (SGPR stamps)
     if (stamp) ts[0] = (long long)now_ticks();
@@ -335,10 +351,10 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     }
     // ---- halo exchange every k iterations (state after iteration it - 1); the owned workers
     // published theirs during the tail phase of it - 1 (publish() below)
-    if (DYN ? it == next_x : (it > a.start_iter && (it - a.start_iter) % k == 0)) {
+    if (it == next_x) {
       if (active && !owned) {
         const unsigned tag = make_tag(a.epoch, it);
-        const int sel = DYN ? (xc & 1) : (((it - a.start_iter) / k) & 1);
+        const int sel = xc & 1;
         const int base = ((sel * n + p) * 2) * d;
         double t0 = 0.0, t1 = 0.0;
         bool ok = true;
@@ -363,10 +379,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       lds_barrier();  // refreshed halo theta visible to the neighbouring waves
       if (abort_lds) break;
       blk0 = it;
-      if constexpr (DYN) {
-        next_x = it + k;
-        ++xc;
-      }
+      next_x = it + k;
+      ++xc;
     }
     if (stamp) ts[1] = ts[2] = ts[3] = (long long)now_ticks();
 
@@ -390,9 +404,6 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         ts[7] = (long long)now_ticks();
       }
       thS[u * 64 + lane] = th;
-      if (owned && in && !(TL && (a.dbg & 2)))
-        put_granule<SYS>(local, rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
-                         make_tag(a.epoch, it), th);
     }
     pending = 1;
     lds_barrier();
@@ -400,7 +411,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
 
     // ---- tail phase; the (idle head) decision wave fetches decision[it + 1 - lag]
     // the next iteration starts with a regular exchange (DYN: unless it starts a new epoch)
-    const bool xnext = DYN ? (it + 1 == next_x && it + 1 != next_start) : (it + 1 - a.start_iter) % k == 0;
+    const bool xnext = it + 1 == next_x && !(DYN && it + 1 == next_start);
     // tail-wave stamps (wave MAXW/2 by default), timeline row 128 + g: [start, rhs, gemv, stores, barrier]
     // (GADMM_BLK_DBG bits 4-6 pick another tail wave: MAXW/2 + ((dbg >> 4) & 7))
     const bool tstamp = TL && v == MAXW / 2 + ((a.dbg >> 4) & 7) && it - a.start_iter < a.timeline_iters && g < 128;
@@ -426,12 +437,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       mu = m;
       th = tn;
       thS[u * 64 + lane] = th;
-      if (owned && in) {
-        if (!(TL && (a.dbg & 2)))
-          put_granule<SYS>(local, rtab, (int)((ring_base + ((long)(it % a.ring) * n + p) * d + lane) * 16),
-                           make_tag(a.epoch, it), th);
-        if (xnext) publish(it);
-      }
+      if (owned && in && xnext) publish(it);
+      ring_defer = ring_post;
       if (a.rres && owned) {  // K4 primal residual of the tail's two edges (after the publish)
         double rp = 0.0;
         if (in && has_l) rp = fma(tl - tn, tl - tn, rp);
@@ -440,8 +447,9 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         if (lane == 0 && it - 1 < a.max_iter) a.rres[(long)(it - 1) * n + w] = rs;
       }
       if (tstamp) tt[3] = (long long)now_ticks();
-    } else if (active && owned && xnext) {  // heads: theta^it and the (still pending) mu are final
-      if (in) publish(it);
+    } else if (active && owned && in) {  // heads: theta^it and the (still pending) mu are final
+      if (xnext) publish(it);
+      if (ring_post) put_granule<SYS>(local, rtab, ring_p + rslot * ring_slot_bytes, make_tag(a.epoch, it), th);
     }
     if (TL && g < 8 && it - a.start_iter < a.timeline_iters && lane == 0) {
       const long long t_end = (long long)now_ticks();  // this wave's tail-phase work done
@@ -453,21 +461,21 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       // loaded during the previous iteration's tail phase: its L2 round trip (~0.7 us) is off the
       // critical path; a decision that was not yet published then is re-polled here
       unsigned long long dv = dv_pref;
-      if ((unsigned)(dv >> 32) != tj) dv = load_dec<SYS>(&a.decg[jdec % a.ring]);
+      if ((unsigned)(dv >> 32) != tj) dv = load_dec<SYS>(&a.decg[dslot]);
       for (int spin = 0; (unsigned)(dv >> 32) != tj; ++spin) {
         if ((spin & 7) == 7 && now_ticks() > deadline) {
           abort_lds = 1;
           break;
         }
         __builtin_amdgcn_s_sleep(1);
-        dv = load_dec<SYS>(&a.decg[jdec % a.ring]);
+        dv = load_dec<SYS>(&a.decg[dslot]);
       }
       const unsigned code = (unsigned)(dv & 0xffffffffu);
       if (code && (unsigned)(dv >> 32) == tj) {
         stop_lds = (int)code;
         stop_iter_lds = jdec;
       }
-      dv_pref = load_dec<SYS>(&a.decg[(jdec + 1) % a.ring]);
+      dv_pref = load_dec<SYS>(&a.decg[dslot + 1 == a.ring ? 0 : dslot + 1]);
     }
     lds_barrier();
     if (tstamp && lane == 0) {
@@ -488,6 +496,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     }
   }
 
+  if (ring_defer)  // the last iteration's tails (it was advanced past it on a stop)
+    put_granule<SYS>(local, rtab, ring_p + ((it - 1) % a.ring) * ring_slot_bytes, make_tag(a.epoch, it - 1), th);
   if (owned && in) {
     a.theta[(long)w * d + lane] = th;
     a.mu[(long)li * d + lane] = mu;
