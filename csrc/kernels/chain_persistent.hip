@@ -55,13 +55,12 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
   const int lane = threadIdx.x & 63;
   const bool w0 = threadIdx.x < 64;  // wave 0 owns the worker state; waves 1..3 help in the GEMVs
   const __amdgpu_buffer_rsrc_t rth = rsrc_of(a.thg);
-  // theta table row of worker w's theta^j. D-GADMM: a ring of `ring` iteration slots, because at a
+  // theta table rows (row_it / row_prev in the loop). D-GADMM: a ring of `ring` iteration slots, because at a
   // re-chain a head still reads its OLD tails' theta^{it-1} while those tails, no longer its
   // neighbours, may already run ahead (up to lag iterations: the stop rule bounds the skew) and
   // would overwrite a single slot. Static chains: one slot (a producer needs the consumer's next
   // theta before it can overwrite).
   const bool ring_tab = a.n_epochs > 0;
-  auto trow = [&](int w, int j) -> int { return ring_tab ? (j % a.ring) * n + w : w; };
   const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
   const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
   __shared__ int xcd_lds;
@@ -213,7 +212,12 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
 
   int it = a.start_iter;
   bool hard_stopped = false;
-  for (;; ++it) {
+  // ring slots as counters (no integer division in the loop): rs = it % ring; the theta-table row of
+  // worker x's theta^it is rs * n + x (D-GADMM ring) or x (static chains), theta^{it-1} uses rs_prev
+  int rs = a.start_iter % a.ring;
+  for (;; ++it, rs = rs + 1 == a.ring ? 0 : rs + 1) {
+    const int rs_prev = rs == 0 ? a.ring - 1 : rs - 1;
+    const int row_it = ring_tab ? rs * n : 0, row_prev = ring_tab ? rs_prev * n : 0;
     if (a.hard_stop > 0 && it > a.hard_stop) {  // end of this chunk's epochs: state = after hard_stop
       hard_stopped = true;
       break;
@@ -226,8 +230,8 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       // reached this iteration has published theta^{it-1}); then it takes its new slot.
       if (w0 && pending && (it > a.start_iter || a.cont)) {
         const unsigned tp = make_tag(a.epoch, it - 1);
-        const int ok = wait_pair<NC, SYS>(rth, d, left >= 0 ? trow(left, it - 1) : -1, tp, tl,
-                                          right >= 0 ? trow(right, it - 1) : -1, tp, tr, deadline);
+        const int ok = wait_pair<NC, SYS>(rth, d, left >= 0 ? row_prev + left : -1, tp, tl,
+                                          right >= 0 ? row_prev + right : -1, tp, tr, deadline);
         if (ok != 1 && lane == 0) abort_lds = 1;
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
@@ -273,6 +277,9 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       const int jnb = head ? it - 1 : it;
       const unsigned tnb = make_tag(a.epoch, jnb);
       const int ra = need_nb ? left : -1, rb = need_nb ? right : -1;
+      const int row_nb = head ? row_prev : row_it;  // table rows of theta^jnb
+      int dslot = rs - a.lag;  // == jdec % ring
+      if (dslot < 0) dslot += a.ring;
       const unsigned tj = make_tag(a.epoch, jdec);
       bool decided = !check;
       unsigned long long dv = 0;
@@ -283,12 +290,12 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
         for (int c = 0; c < NC; ++c) {
           const int i = lane + 64 * c;
           if (i < d) {
-            if (ra >= 0) nb &= load_granule<SYS>(rth, (trow(ra, jnb) * d + i) * 16, tnb, &tl[c]);
-            if (rb >= 0) nb &= load_granule<SYS>(rth, (trow(rb, jnb) * d + i) * 16, tnb, &tr[c]);
+            if (ra >= 0) nb &= load_granule<SYS>(rth, ((row_nb + ra) * d + i) * 16, tnb, &tl[c]);
+            if (rb >= 0) nb &= load_granule<SYS>(rth, ((row_nb + rb) * d + i) * 16, tnb, &tr[c]);
           }
         }
         if (!decided) {
-          dv = __shfl(load_dec<SYS>(&a.decg[jdec % a.ring]), 0, 64);
+          dv = __shfl(load_dec<SYS>(&a.decg[dslot]), 0, 64);
           decided = (unsigned)(dv >> 32) == tj;
         }
         if (decided && (unsigned)(dv & 0xffffffffu) != 0u) { outcome = 2; break; }
@@ -353,7 +360,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       for (int c = 0; c < NC; ++c) {  // publish theta^it: local table + remote neighbours' tables
         const int i = lane + 64 * c;
         if (i < d) {
-          put_granule<SYS>(local, rth, (trow(w, it) * d + i) * 16, tag, tn[c]);
+          put_granule<SYS>(local, rth, ((row_it + w) * d + i) * 16, tag, tn[c]);
           if (p0) store_granule<SYS>(rp0, (w * d + i) * 16, tag, tn[c]);
           if (p1) store_granule<SYS>(rp1, (w * d + i) * 16, tag, tn[c]);
         }
@@ -370,7 +377,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
 #pragma unroll
           for (int c = 0; c < NC; ++c) {
             const int i = lane + 64 * c;
-            if (i < d) store_granule<SYS>(rr, (trow(w, it) * d + i) * 16, tag, tn[c]);
+            if (i < d) store_granule<SYS>(rr, ((row_it + w) * d + i) * 16, tag, tn[c]);
           }
         }
       }
@@ -426,7 +433,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
     }
     if (w0) {
       const double f = wave_sum_f64(part) + half_yy;
-      if (lane == 0) put_granule<SYS>(local, rob, ((it % a.ring) * n + w) * 16, make_tag(a.epoch, it), f);
+      if (lane == 0) put_granule<SYS>(local, rob, (rs * n + w) * 16, make_tag(a.epoch, it), f);
 #pragma unroll
       for (int c = 0; c < NC; ++c) th[c] = tn[c];
       const int k = it - a.start_iter;
