@@ -88,6 +88,48 @@ __device__ __forceinline__ double quad_gemv(const double (&m)[4][T], double x, d
 #endif
 }
 
+// Quad layout kept in LDS instead of VGPRs (a matrix used off the critical path, e.g. the exact
+// objective's Gram): element m[r][t] of lane l at Ml[((t >> 1) * 4 + r) * 128 + 2 l + (t & 1)], so a
+// lane reads its (t, t + 1) pair with one 16-byte load. quad_gemv_lds performs quad_gemv's FMAs in
+// the same order (bit-identical). Ml: 4 * 64 * (T + (T & 1)) doubles of LDS private to the wave.
+template <int T>
+__device__ __forceinline__ void quad_store_lds(double* Ml, const double* M, int d, bool on) {
+  const int lane = threadIdx.x & 63, i = lane & 15, c = lane >> 4;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int t = 0; t < T + (T & 1); ++t) {
+      const int row = i + 16 * r, col = c + 4 * t;
+      Ml[((t >> 1) * 4 + r) * 128 + 2 * lane + (t & 1)] =
+          (on && t < T && row < d && col < d) ? M[(long)row * d + col] : 0.0;
+    }
+}
+
+template <int T>
+__device__ __forceinline__ double quad_gemv_lds(const double* Ml, double x, double* st) {
+  static_assert(T >= 1 && T <= 16, "quad layout covers d <= 64");
+  const int lane = threadIdx.x & 63, c = lane >> 4;
+  st[(lane & 3) * QX + (lane >> 2)] = x;
+  asm volatile("" ::: "memory");
+  const double* xs = st + c * QX;
+  double p[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int t = 0; t < T; t += 2) {
+    const double2 xp = *reinterpret_cast<const double2*>(xs + t);
+    double2 mv[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) mv[r] = *reinterpret_cast<const double2*>(Ml + ((t >> 1) * 4 + r) * 128 + 2 * lane);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p[r] = fma(mv[r].x, xp.x, p[r]);
+    if (t + 1 < T) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p[r] = fma(mv[r].y, xp.y, p[r]);
+    }
+  }
+  asm volatile("" ::: "memory");
+  return quad_reduce(p);
+}
+
 // Paired layout for two matrices with <= 52 rows held by one wave (chain_blocked_pair_kernel):
 // each keeps its row groups r = 0..2 (rows i + 16r) as in quad_load, and the two share ONE register
 // block for rows 48..51: lanes with i < 4 hold matrix 0's row 48 + i, lanes with 4 <= i < 8 hold

@@ -171,7 +171,12 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
 
   const double* Mg = a.Minv + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)d * d;
   const double* Ag = a.A + (long)li * d * d;
-  double Mq[REG ? NV : 1][REG ? 4 : 1][REG ? QT : 1], Aq[REG ? 4 : 1][REG ? QT : 1];
+  // REG + D-GADMM (NV = 2): the objective's Gram in LDS (quad order, after the GEMV staging): it is
+  // used off the critical path, and next to the two inverses in VGPRs it pushed them into AGPR moves
+  // (coherence 1: 0.880 -> 0.840 ms; with one inverse, NV = 1, registers stay faster: 3.07 vs 3.14 ms)
+  constexpr bool AQ_LDS = REG && NV > 1;
+  double Mq[REG ? NV : 1][REG ? 4 : 1][REG ? QT : 1], Aq[REG && !AQ_LDS ? 4 : 1][REG && !AQ_LDS ? QT : 1];
+  double* Aql = lds + QSTAGE;
   if constexpr (REG) {
     if (dyn) {
 #pragma unroll
@@ -180,7 +185,8 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
     } else {
       quad_load<QT>(Mq[0], Mg, d, true);
     }
-    quad_load<QT>(Aq, Ag, d, a.obj_mode == 0);
+    if constexpr (AQ_LDS) quad_store_lds<QT>(Aql, Ag, d, a.obj_mode == 0);
+    else quad_load<QT>(Aq, Ag, d, a.obj_mode == 0);
   } else {
     if (dyn) {
       const double* Mw = a.Minv + (long)li * a.nvar * d * d;
@@ -421,7 +427,8 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
       }
       lds_barrier();
       double q[NC];
-      if constexpr (REG) q[0] = quad_gemv<QT>(Aq, lane < d ? tn[0] : 0.0, st);
+      if constexpr (AQ_LDS) q[0] = quad_gemv_lds<QT>(Aql, lane < d ? tn[0] : 0.0, st);
+      else if constexpr (REG) q[0] = quad_gemv<QT>(Aq, lane < d ? tn[0] : 0.0, st);
       else symv_lds<NC>(Al, xv, q, red, d);
       if (w0) {
 #pragma unroll
@@ -514,11 +521,12 @@ static PVariant pick_variant(const PersistArgs& a) {
                        : gadmm_chain_persistent_lds(a.d, a.obj_mode);
   if (lds == 0) return v;
   const long monitor_lds = (long)a.n * 8;
+  const long reg_lds = (long)(QSTAGE + 4 * 64 * 16) * 8;  // REG: GEMV staging + the Gram in quad order (T <= 16)
   const size_t shm = (size_t)(lds > monitor_lds ? lds : monitor_lds);
 #define GADMM_P_PICK(NCv, SYSv, REGv, ...)                                                         \
   do {                                                                                             \
     v.fn = (const void*)chain_persistent_kernel<NCv, SYSv, REGv, ##__VA_ARGS__>;                   \
-    v.shm = REGv ? (size_t)(monitor_lds > QSTAGE * 8 ? monitor_lds : QSTAGE * 8) : shm;             \
+    v.shm = REGv ? (size_t)(monitor_lds > reg_lds ? monitor_lds : reg_lds) : shm;                    \
     v.threads = REGv ? 64 : NT;                                                                    \
   } while (0)
   static const bool force_lds = getenv("GADMM_PERSIST_LDS") != nullptr;  // A/B switch
