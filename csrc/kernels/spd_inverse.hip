@@ -140,11 +140,12 @@ spd_inverse_reg64_kernel(const double* __restrict__ A, const double* __restrict_
   }
   if (w == 0) colv[0][i] = h[0];
   __syncthreads();
+  bool bad = false;  // a non-positive (or NaN) pivot: reported once after the loop
   for (int k = 0; k < d; ++k) {
     const double* cb = colv[k & 1];
     const double pk = cb[k], aik = cb[i];
     const double p = 1.0 / pk;
-    if (threadIdx.x == 0 && !(pk > 0.0) && status) atomicExch(status, 1);  // not SPD (or NaN)
+    bad |= !(pk > 0.0);  // not SPD (or NaN)
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
       const int j = w + NW * c;
@@ -164,6 +165,7 @@ spd_inverse_reg64_kernel(const double* __restrict__ A, const double* __restrict_
     }
     __syncthreads();
   }
+  if (threadIdx.x == 0 && bad && status) atomicExch(status, 1);
 #pragma unroll
   for (int c = 0; c < NC; ++c) Ms[i * 65 + w + NW * c] = h[c];
   __syncthreads();
