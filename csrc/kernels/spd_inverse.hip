@@ -127,7 +127,7 @@ spd_inverse_reg64_kernel(const double* __restrict__ A, const double* __restrict_
                          double* __restrict__ out, int* __restrict__ status) {
   constexpr int NC = 64 / NW;
   __shared__ double Ms[64 * 65];    // the result, for the symmetrised write-out
-  __shared__ double colv[2][64];    // the pivot column, double-buffered
+  __shared__ double colv[2][65];    // the pivot column + [64] its reciprocal pivot, double-buffered
   const int n = blockIdx.x, v = blockIdx.y;
   const double s = shift[n * nvar + v];
   const double* An = A + (long)n * d * d;
@@ -138,13 +138,17 @@ spd_inverse_reg64_kernel(const double* __restrict__ A, const double* __restrict_
     const int j = w + NW * c;
     h[c] = (i < d && j < d) ? An[i * d + j] + (i == j ? s : 0.0) : 0.0;
   }
-  if (w == 0) colv[0][i] = h[0];
+  if (w == 0) {
+    colv[0][i] = h[0];
+    const double p0 = 1.0 / readlane_f64(h[0], 0);
+    if (i == 0) colv[0][64] = p0;
+  }
   __syncthreads();
   bool bad = false;  // a non-positive (or NaN) pivot: reported once after the loop
   for (int k = 0; k < d; ++k) {
     const double* cb = colv[k & 1];
-    const double pk = cb[k], aik = cb[i];
-    const double p = 1.0 / pk;
+    // the reciprocal pivot comes with the column: the owner wave divided while the others updated
+    const double pk = cb[k], aik = cb[i], p = cb[64];
     bad |= !(pk > 0.0);  // not SPD (or NaN)
 #pragma unroll
     for (int c = 0; c < NC; ++c) {
@@ -162,6 +166,8 @@ spd_inverse_reg64_kernel(const double* __restrict__ A, const double* __restrict_
 #pragma unroll
       for (int c = 0; c < NC; ++c) nxt = (c == kn / NW) ? h[c] : nxt;
       colv[kn & 1][i] = nxt;
+      const double pn = 1.0 / readlane_f64(nxt, kn);  // == every lane's old 1.0 / pk (bit-identical)
+      if (i == 0) colv[kn & 1][64] = pn;
     }
     __syncthreads();
   }
