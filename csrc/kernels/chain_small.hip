@@ -914,8 +914,9 @@ int gadmm_chain_monitor(ChainCtl* ctl, const double* reduced, int ring, int n_to
 // trace = NaN, control block as chain_reset_kernel.
 __global__ void chain_reset_state_kernel(ChainCtl* ctl, int start_iter, int pending, double* theta, long n_theta,
                                          double* mu, long n_mu, double* trace, long n_trace, double* part,
-                                         long n_part) {
+                                         long n_part, long long* stamp) {
   const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x, step = (long)gridDim.x * blockDim.x;
+  if (stamp && i0 == 0) *stamp = (long long)__builtin_amdgcn_s_memrealtime();  // the solve's real-clock start
   for (long i = i0; i < n_theta; i += step) theta[i] = 0.0;
   for (long i = i0; i < n_mu; i += step) mu[i] = 0.0;
   for (long i = i0; i < n_part; i += step) part[i] = 0.0;
@@ -931,16 +932,24 @@ __global__ void chain_reset_state_kernel(ChainCtl* ctl, int start_iter, int pend
   }
 }
 
-int gadmm_chain_reset_state(ChainCtl* ctl, int start_iter, int pending, double* theta, long n_theta, double* mu,
-                            long n_mu, double* trace, long n_trace, double* part, long n_part, hipStream_t st) {
+// stamp (nullable): also record the real-clock start (gadmm_write_stamp) in the same launch
+int gadmm_chain_reset_state_stamp(ChainCtl* ctl, int start_iter, int pending, double* theta, long n_theta, double* mu,
+                                  long n_mu, double* trace, long n_trace, double* part, long n_part, long long* stamp,
+                                  hipStream_t st) {
   long mx = n_theta > n_mu ? n_theta : n_mu;
   mx = mx > n_trace ? mx : n_trace;
   int blocks = (int)((mx + 255) / 256);
   blocks = blocks < 1 ? 1 : (blocks > 64 ? 64 : blocks);
   hipLaunchKernelGGL(chain_reset_state_kernel, dim3(blocks), dim3(256), 0, st, ctl, start_iter, pending, theta,
-                     n_theta, mu, n_mu, trace, n_trace, part, n_part);
+                     n_theta, mu, n_mu, trace, n_trace, part, n_part, stamp);
   GADMM_CHECK(hipGetLastError());
   return 0;
+}
+
+int gadmm_chain_reset_state(ChainCtl* ctl, int start_iter, int pending, double* theta, long n_theta, double* mu,
+                            long n_mu, double* trace, long n_trace, double* part, long n_part, hipStream_t st) {
+  return gadmm_chain_reset_state_stamp(ctl, start_iter, pending, theta, n_theta, mu, n_mu, trace, n_trace, part,
+                                       n_part, nullptr, st);
 }
 
 int gadmm_chain_reset(ChainCtl* ctl, int start_iter, int pending, hipStream_t st) {

@@ -264,6 +264,7 @@ class NativeChainEngine:
         self.handle = self.lib.gadmm_chain_engine_create(ctypes.byref(self._desc))
         if self.plan is not None:
             self._install(self.plan)
+            self._plan_dirty = False
 
     def set_targets(self, obj0: float, tol: float, max_iter: Optional[int] = None):
         self.obj0, self.tol = float(obj0), float(tol)
@@ -290,11 +291,20 @@ class NativeChainEngine:
             if len(memo) > 4096:
                 memo.clear()
             memo[key] = plan
-        self._install(plan)
+        # installed into the native engine lazily (_sync_plan): the persistent kernels take their slots
+        # from self.plan, and a D-GADMM solve re-installs its final chain after every launch
+        if plan is not getattr(self, "plan", None):
+            self._plan_dirty = True
         self.plan = plan
         self.path = [int(w) for w in path]
         self.rank = rank
         self._placement_owner = [int(o) for o in placement.owner]
+
+    def _sync_plan(self):
+        """Install self.plan into the native (graph / eager) engine if set_path changed it."""
+        if getattr(self, "_plan_dirty", False) and self.plan is not None:
+            self._install(self.plan)
+            self._plan_dirty = False
 
     def _install(self, plan: RankPlan):
         def slots(lst):
@@ -319,27 +329,31 @@ class NativeChainEngine:
     def reset(self, start_iter: int = 1, pending: int = 0, zero_state: bool = True):
         if self.xport:  # new solve: the transport's tags of the previous one stop matching (every rank)
             native.check(self.lib.gadmm_ipc_new_epoch(self.xport, self.stream.cuda_stream), "ipc_new_epoch")
-        native.check(self.lib.gadmm_write_stamp(self.t0stamp.data_ptr(), self.stream.cuda_stream), "write_stamp")
+        if not zero_state:
+            native.check(self.lib.gadmm_write_stamp(self.t0stamp.data_ptr(), self.stream.cuda_stream), "write_stamp")
         if self.hinv is not None and zero_state:  # a new solve starts from fresh Hessians
             with torch.cuda.stream(self.stream):
                 self.hinv[:, 64 * 64].zero_()
         if self.rres is not None and zero_state:  # a row's non-tail entries stay 0
             with torch.cuda.stream(self.stream):
                 self.rres.zero_()
-        if zero_state:  # theta = mu = part = 0, trace = NaN and the control block: one launch
-            native.check(self.lib.gadmm_chain_reset_state(
+        if zero_state:  # theta = mu = part = 0, trace = NaN, the control block and the clock start: one launch
+            native.check(self.lib.gadmm_chain_reset_state_stamp(
                 self.ctl.data_ptr(), int(start_iter), int(pending), self.theta.data_ptr(), self.theta.numel(),
                 self.mu.data_ptr(), self.mu.numel(), self.trace.data_ptr(), self.trace.numel(),
-                self.part.data_ptr(), self.part.numel(), self.stream.cuda_stream), "reset_state")
+                self.part.data_ptr(), self.part.numel(), self.t0stamp.data_ptr(), self.stream.cuda_stream),
+                "reset_state")
         else:
             native.check(self.lib.gadmm_chain_engine_reset(self.handle, int(start_iter), int(pending)), "reset")
 
     def exchange(self, which: str = "tail"):
         """Eager neighbour exchange with the current plan ('head' or 'tail' messages)."""
+        self._sync_plan()
         native.check(self.lib.gadmm_chain_engine_exchange(self.handle, 0 if which == "head" else 1), "exchange")
 
     def flush_duals(self):
         """Apply pending head duals with the current chain (before re-chain / checkpoint)."""
+        self._sync_plan()
         native.check(self.lib.gadmm_chain_engine_flush(self.handle), "flush")
 
     def run(self, stop_iter: int = 0, use_graph: bool = True, block: Optional[int] = None) -> EngineRun:
@@ -347,6 +361,7 @@ class NativeChainEngine:
         blk = self.block if block is None else int(block)
         if blk > self.ring and self.nranks > 1:
             raise ValueError("block must be <= ring for multi-rank runs")
+        self._sync_plan()
         rc = self.lib.gadmm_chain_engine_run(self.handle, blk, int(stop_iter), 1 if use_graph else 0,
                                              ctypes.byref(st))
         native.check(rc, "chain_engine_run")
@@ -652,11 +667,16 @@ class NativeChainEngine:
                 if rc == -2:
                     raise ResidencyError(self.lib.gadmm_last_error().decode())
                 native.check(rc, "chain_persistent_launch")
+            # the control block comes back with the same stream sync (pinned buffer, async copy queued
+            # behind the kernel): no second blocking round trip per solve
+            if getattr(self, "_ctl_host", None) is None:
+                self._ctl_host = torch.empty(self.ctl.shape, dtype=self.ctl.dtype, pin_memory=True)
+            self._ctl_host.copy_(self.ctl, non_blocking=True)
             self.stream.synchronize()
             t1 = _time.perf_counter()
         self.last_timeline = tl.cpu().numpy() if tl is not None else None
         self.last_timeline_slots = [(s.gid, p) for s, p in zip(slots, pos)] if tl is not None else None
-        c = self.ctl.cpu().tolist()
+        c = self._ctl_host.tolist()
         done, conv, nxt = c[1], c[2], c[0]
         if done == 4:
             raise HandoffTimeout("persistent chain kernel timed out (hand-off never completed)")

@@ -154,6 +154,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_chain_reset": (c_int, [c_void_p, c_int, c_int, c_void_p]),
         "gadmm_chain_reset_state": (c_int, [c_void_p, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p,
                                             c_long, c_void_p, c_long, c_void_p]),
+        "gadmm_chain_reset_state_stamp": (c_int, [c_void_p, c_int, c_int, c_void_p, c_long, c_void_p, c_long, c_void_p,
+                                            c_long, c_void_p, c_long, c_void_p, c_void_p]),
         "gadmm_chain_engine_create": (c_void_p, [ctypes.POINTER(EngineDesc)]),
         "gadmm_chain_engine_destroy": (None, [c_void_p]),
         "gadmm_chain_engine_set_plan": (c_int, [c_void_p, c_int, ctypes.POINTER(PhaseSlot), c_int,

@@ -45,3 +45,4 @@ for _ in range(20):
 torch.cuda.synchronize()
 pr.disable()
 pstats.Stats(pr).sort_stats("tottime").print_stats(22)
+pstats.Stats(pr).sort_stats("cumulative").print_stats(40)
