@@ -300,7 +300,18 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         # first launch: `epoch_chunk` epochs, each continuation twice the previous. Drawing a chain
         # costs ~0.75 us on the host, a launch + read-back ~0.25 ms: 128 keeps coherence-10 solves
         # (~51 epochs) to one launch with few spare chains, coherence-1 solves (~250) to two
-        chunk = max(1, int(opts.get("epoch_chunk", 128)))
+        # Without an explicit chunk, a repeat of a schedule of the same shape (coherence, kind, max_iter,
+        # N) on this engine sizes its first launch from the epochs the previous solve reached (+ margin):
+        # chains beyond them would be drawn for nothing. Only the launch size follows the hint; the
+        # chains and iterates do not (a shortfall costs a continuation launch).
+        hint_key = (float(schedule.coherence), schedule.kind, int(max_iter), int(n_total))
+        hints = eng.__dict__.setdefault("_dyn_epoch_hint", {})
+        if "epoch_chunk" in opts:
+            chunk = max(1, int(opts["epoch_chunk"]))
+        elif hint_key in hints:
+            chunk = max(16, int(hints[hint_key]) + 8)
+        else:
+            chunk = 128
         if eng.dynamic_uses_blocked(fabric):  # the blocked kernel's dynamic mode runs every epoch in one launch
             chunk = len(rechains) + 1
         saved = schedule.save()
@@ -352,6 +363,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             chunk *= 2
         if done == 5:
             done = 2
+        hints[hint_key] = int(np.searchsorted(np.asarray(ep_start), max(last_launched, 1), side="right"))
         Pn = np.concatenate(drawn_P) if drawn_P else np.zeros((0, n_total), dtype=np.int64)
         if drawn_C and any(c.dtype == object for c in drawn_C):
             Cn = np.empty(sum(len(c) for c in drawn_C), dtype=object)
