@@ -125,3 +125,15 @@ def test_logi_abi_layout_matches_ctypes():
     k = lib.gadmm_logi_abi_layout(buf, 8)
     exp = [ctypes.sizeof(native.LogiArgs), native.LogiArgs.lam.offset, native.LogiArgs.inner_iters.offset]
     assert list(buf[:k]) == exp
+
+
+def test_blocked_plan_fits_one_xcd():
+    """gadmm_chain_blocked_plan: k = 2 and the shortest owned segment whose launch (worker +
+    objective + monitor workgroups, one per CU) fits one XCD (32 CUs without a device): N = 24 -> L = 1
+    (27 workgroups), N = 50 -> L = 2 (25 + 5 + 1 = 31), N = 100 -> L = 4 (no length fits, the k = 2 maximum)."""
+    lib = native.require()
+    k, L = ctypes.c_int(0), ctypes.c_int(0)
+    for n, want_L in ((24, 1), (50, 2), (8, 1), (100, 4)):
+        W = lib.gadmm_chain_blocked_plan(n, 50, 0, ctypes.byref(k), ctypes.byref(L))
+        assert (k.value, L.value, W) == (2, want_L, (n + want_L - 1) // want_L), (n, k.value, L.value, W)
+    assert lib.gadmm_chain_blocked_plan(24, 100, 0, ctypes.byref(k), ctypes.byref(L)) == 0  # d > 52
