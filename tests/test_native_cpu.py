@@ -42,11 +42,15 @@ def test_fo_abi_layout_matches_ctypes():
     assert list(buf[:k]) == exp
 
 
-def test_code_objects_target_gfx950():
+def test_code_objects_target_gfx950(tmp_path):
+    import shutil
     import subprocess
-    lib = native.library_path()
+    # llvm-objdump --offloading extracts every embedded code object NEXT TO its input: run it on a
+    # copy in a scratch directory so the in-tree _native/ stays clean
+    lib = str(tmp_path / "lib.so")
+    shutil.copy(native.library_path(), lib)
     out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", lib], capture_output=True,
-                         text=True)
+                         text=True, cwd=str(tmp_path))
     txt = out.stdout + out.stderr
     assert "gfx950" in txt
 
