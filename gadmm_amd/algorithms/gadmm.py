@@ -51,13 +51,15 @@ def chain_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: 
     """Run one chain-ADMM solve on this rank. ``model`` holds this rank's shards (local order =
     ``local_ids``). ``schedule`` (D-GADMM) overrides ``path``; ``cost_quirk`` reproduces the
     reference's per-head-worker accumulation of ``sum(pathCost)`` (dynamic_group_ADMM_closedForm.m:51-55).
-    ``state``: optional ``(theta_table, mu, start_iter)`` to resume from a checkpoint.
+    ``state``: optional ``(theta_table, mu, start_iter)`` to resume from a checkpoint (natively on one
+    rank with a static chain; torch path otherwise).
     ``check_exchange`` (or ``GADMM_CHECK_EXCHANGE=1``): verify every ghost row against its owner after
     every exchange (debug/race.py; forces the torch path).
     ``failures``: ``{iteration: [worker ids]}`` - elastic recovery: at that iteration
     the workers drop out, the chain re-forms over the survivors, each failed worker's aggregated
     dual is handed to a surviving chain neighbour (keeping sum(mu) = 0, the consensus-dual
-    invariant) and the stopping target becomes the survivors' optimum (linear, torch path)."""
+    invariant) and the stopping target becomes the survivors' optimum (linear models; natively on
+    one rank with a static chain, ``_chain_admm_native_elastic``; torch path otherwise)."""
     import os
 
     comm = comm if comm is not None else LocalComm()
@@ -73,8 +75,14 @@ def chain_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: 
     use_native = False
     native_solver = local_solver in ("closed", "gd") or (
         local_solver == "newton" and model.kind == "logistic" and model.d <= 64 and model.m <= 64)
-    if backend in ("auto", "native") and dev.type == "cuda" and native_solver and state is None \
-            and not check_exchange and not failures:
+    # resume (``state``) and elastic recovery (``failures``) run natively on one rank with a static
+    # chain; across ranks, with re-chaining, or under the exchange checker they take the torch path
+    one_static = comm.nranks == 1 and _static_schedule(schedule, max_iter)
+    native_state = state is None or one_static
+    native_fail = not failures or (one_static and model.kind == "linear" and local_solver == "closed"
+                                   and sorted(int(w) for w in local_ids) == list(range(n_total)))
+    if backend in ("auto", "native") and dev.type == "cuda" and native_solver and native_state \
+            and not check_exchange and native_fail:
         from ..ops import native
 
         if native.available() and (comm.nranks == 1 or getattr(comm, "backend", "") in ("rccl", "ipc")
@@ -85,9 +93,12 @@ def chain_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: 
     if use_native:
         # a named range per solve in rocprofv3 --marker-trace timelines (no-op without roctx)
         with roctx_range("%s native N=%d" % (name, n_total)):
+            if failures:
+                return _chain_admm_native_elastic(model, n_total, rho, obj0, tol, max_iter, schedule, cost_quirk,
+                                                  name, engine_opts or {}, failures)
             return _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement,
                                       schedule, local_solver, step, max_inner, inner_tol, cost_quirk, name,
-                                      engine_opts or {})
+                                      engine_opts or {}, state=state)
     return _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, schedule,
                              local_solver, step, max_inner, inner_tol, cost_quirk, name, record_theta, state,
                              check_exchange, failures)
@@ -216,11 +227,22 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
     return res
 
 
+def _static_schedule(schedule, max_iter) -> bool:
+    return not schedule.coherence or not np.isfinite(schedule.coherence) or schedule.coherence <= 0 \
+        or schedule.coherence >= max_iter + 1
+
+
 def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, schedule, local_solver,
-                       step, max_inner, inner_tol, cost_quirk, name, opts):
+                       step, max_inner, inner_tol, cost_quirk, name, opts, state=None):
     """``opts``: ``block`` (iterations per graph replay), ``persistent`` (auto/True/False), ``graph``,
     ``cache``, ``state``, ``fabric`` (an ``XgmiFabric``: the device-initiated multi-GPU persistent
-    kernels; with ``table_slots >= lag + 4`` it also runs multi-rank D-GADMM in one launch)."""
+    kernels; with ``table_slots >= lag + 4`` it also runs multi-rank D-GADMM in one launch),
+    ``stop_iter`` (static chains: run no iteration past it, on the graph engine - the persistent
+    kernels stop only at the decision).
+    ``state``: ``(theta_table (n_total, d), mu (n_local, d), start_iter)`` - resume a static chain
+    from a checkpoint (one rank): the engine's tables are loaded and the kernels start at
+    ``start_iter`` with no pending head duals (a saved state has them applied); the result covers
+    iterations ``start_iter..iters`` like the torch path's."""
     from ..engine.chain_engine import NativeChainEngine, ResidencyError, HandoffTimeout
 
     rank = comm.rank
@@ -253,14 +275,25 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     else:
         eng.set_targets(obj0, tol)
     eng.set_path(schedule.path, placement, rank)
-    eng.reset()
+    start = 1 if state is None else int(state[2])
+    static = _static_schedule(schedule, max_iter)
+    if state is not None and not (static and comm.nranks == 1):
+        raise ValueError("native resume: one rank, static chain")
+
+    def load_state():  # fresh solve state, or the checkpoint's tables at start_iter (no pending duals)
+        eng.reset(start_iter=start)
+        if state is not None:
+            with torch.cuda.stream(eng.stream):
+                eng.theta.copy_(state[0].to(eng.theta.device, torch.float64).reshape(eng.theta.shape))
+                eng.mu.copy_(state[1].to(eng.mu.device, torch.float64).reshape(eng.mu.shape))
+
+    load_state()
+    stop_iter = int(opts.get("stop_iter", 0))
     torch.cuda.synchronize(model.device)
     t0 = time.perf_counter()
     cc = 0.0
     com_cost = []
     n_heads = (n_total + 1) // 2
-    static = not schedule.coherence or not np.isfinite(schedule.coherence) or schedule.coherence <= 0 \
-        or schedule.coherence >= max_iter + 1
     p2p = 0
     mon = 0
     wire = 0
@@ -268,9 +301,9 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     if static:
         r = None
         engine_kind = None
-        if want_persistent and eng.persistent_eligible(fabric):
+        if want_persistent and stop_iter <= 0 and eng.persistent_eligible(fabric):
             try:
-                r = eng.run_persistent(fabric=fabric)
+                r = eng.run_persistent(fabric=fabric, start_iter=start)
                 engine_kind = "persistent"
             except (ResidencyError, HandoffTimeout) as e:
                 # the device could not hold every workgroup, or a hand-off stalled: the graph engine
@@ -278,16 +311,16 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
                 # see bench.py, so they raise)
                 if comm.nranks > 1:
                     raise
-                eng.reset()
+                load_state()
                 engine_kind = "graph(fallback: %s)" % type(e).__name__
         if r is None:
-            r = eng.run(use_graph=opts.get("graph", True))
+            r = eng.run(stop_iter=stop_iter, use_graph=opts.get("graph", True))
             if engine_kind is None:
                 engine_kind = "graph" if eng.graph_ok() else "eager"
         iters, done = r.iters, r.done
         p2p, mon, wire = r.p2p_bytes, r.monitor_bytes, r.wire_bytes
         per = float(np.sum(schedule.cost)) * (n_heads if cost_quirk else 1)
-        com_cost = np.arange(1, iters + 1) * per
+        com_cost = np.arange(1, iters - start + 2) * per
     elif want_persistent and eng.dynamic_eligible(fabric) \
             and len(rechain_iterations(max_iter, schedule.coherence)) < (1 << 20):
         # D-GADMM in persistent launches of up to `epoch_chunk` epochs each: the seeded chain sequence
@@ -414,6 +447,8 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     torch.cuda.synchronize(model.device)
     wall = time.perf_counter() - t0
     tr, tt = eng.traces(iters)
+    if start > 1:  # a resumed solve reports iterations start..iters (as the torch path does)
+        tr, tt = tr[start - 1:], tt[start - 1:]
     if fabric is not None and comm.nranks > 1:
         # the xGMI kernels decide on rank 0's monitor only: give every rank the same trace and clock
         import torch.distributed as dist
@@ -423,6 +458,8 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         tr, tt = buf[0].numpy().copy(), buf[1].numpy().copy()
     loss = np.abs(tr - obj0)
     pres = eng.primal_residual(iters)  # K4, emitted by the kernels' tails (this rank's edges)
+    if pres is not None and start > 1:
+        pres = pres[start - 1:]
     if pres is not None and comm.nranks > 1:
         import torch.distributed as dist
 
@@ -438,8 +475,8 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         bytes_tot = int(t.item())
     res = RunResult(algorithm=name, obj=tr, loss=loss, iters=iters, converged=(done == 1), wall_s=wall,
                     time_trace=tt,  # measured on the device: decision time of each iteration
-                    comm_units=np.arange(1, iters + 1, dtype=np.float64) * n_total,
-                    com_cost=np.asarray(com_cost[:iters]), bytes_sent=int(p2p), bytes_total=bytes_tot,
+                    comm_units=np.arange(start, iters + 1, dtype=np.float64) * n_total,
+                    com_cost=np.asarray(com_cost[:iters - start + 1]), bytes_sent=int(p2p), bytes_total=bytes_tot,
                     primal_res=pres,
                     extra={"backend": "native", "engine": engine_kind, "rank": rank, "nranks": comm.nranks,
                            "solver": local_solver, "monitor_bytes": int(mon), "wire_bytes": int(wire),
@@ -451,6 +488,82 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         eng.flush_duals()
         nxt = int(eng.ctl_state()["iter"])
         res.extra["state"] = (eng.theta.clone(), eng.mu.clone(), nxt)
+    return res
+
+
+def _chain_admm_native_elastic(model, n_total, rho, obj0, tol, max_iter, schedule, cost_quirk, name, opts,
+                               failures) -> RunResult:
+    """Elastic recovery (``failures = {iteration: [worker ids]}``) on the native engine: one rank, a
+    static chain, closed-form local solves. Same semantics as the torch path's ``failures``: at the
+    failure iteration each dead worker's aggregated dual goes to its nearest surviving chain
+    neighbour (``_drop_workers``), the chain re-forms over the survivors and the target becomes the
+    survivors' optimum. The solve runs in segments: the current survivors' chain runs natively up to
+    the iteration before the next failure (graph engine, ``stop_iter``), its state (pending head
+    duals applied) goes back into the full tables, the duals are handed on, and the survivors - a
+    smaller engine over their shards (``LinearRegression.subset``), ids renumbered in worker order -
+    resume natively from the failure iteration (persistent kernel, ``start_iter``)."""
+    dev = model.device
+    d = model.d
+    alive = np.ones(n_total, dtype=bool)
+    theta = torch.zeros((n_total, d), dtype=torch.float64, device=dev)
+    mu = torch.zeros((n_total, d), dtype=torch.float64, device=dev)
+    lidx_of = {w: w for w in range(n_total)}
+    events = sorted((int(k), [int(w) for w in v]) for k, v in failures.items() if 1 <= int(k) <= max_iter)
+    start, cur_obj0 = 1, float(obj0)
+    segs: List[RunResult] = []
+    seg_info = []
+
+    def run_segment(stop: int) -> RunResult:
+        S = [w for w in range(n_total) if alive[w]]
+        if len(S) < 2:
+            raise ValueError("elastic recovery: fewer than two workers survive")
+        new_of = {w: i for i, w in enumerate(S)}
+        sub = model.subset(S)
+        sch = PathSchedule(len(S), [new_of[w] for w in schedule.path if alive[w]], np.zeros(len(S) - 1), coherence=0)
+        ix = torch.as_tensor(S, dtype=torch.long, device=dev)
+        st = None if start == 1 else (theta.index_select(0, ix), mu.index_select(0, ix), start)
+        o = dict(opts, cache=False, state=True)
+        if stop > 0:
+            o["stop_iter"] = stop
+        r = _chain_admm_native(sub, list(range(len(S))), len(S), rho, cur_obj0, tol, max_iter, LocalComm(),
+                               Placement.contiguous(len(S), 1), sch, "closed", 1.0, 1, 0.0, cost_quirk, name, o,
+                               state=st)
+        th_s, mu_s, _ = r.extra["state"]
+        theta[ix] = th_s
+        mu[ix] = mu_s
+        seg_info.append({"first": start, "last": int(r.iters), "workers": len(S), "engine": r.extra.get("engine")})
+        segs.append(r)
+        return r
+
+    finished = False
+    for f, dead in events:
+        if f > start:
+            r = run_segment(f - 1)
+            if r.converged or r.iters >= max_iter:
+                finished = True
+                break
+            start = f
+        cur_obj0 = _drop_workers(dead, alive, schedule, theta, mu, lidx_of, model, LocalComm(), n_total, dev)
+    if not finished:
+        run_segment(0)
+    last = segs[-1]
+    iters = int(last.iters)
+    obj = np.concatenate([s.obj for s in segs])
+    loss = np.concatenate([s.loss for s in segs])
+    offs = np.cumsum([0.0] + [float(s.wall_s) for s in segs[:-1]])
+    tt = np.concatenate([np.asarray(s.time_trace) + o for s, o in zip(segs, offs)])
+    pres = None
+    if all(s.primal_res is not None for s in segs):
+        pres = np.concatenate([np.asarray(s.primal_res) for s in segs])
+    per = float(np.sum(schedule.cost)) * ((n_total + 1) // 2 if cost_quirk else 1)
+    res = RunResult(algorithm=name, obj=obj, loss=loss, iters=iters, converged=bool(last.converged),
+                    wall_s=float(sum(s.wall_s for s in segs)), time_trace=tt,
+                    comm_units=np.arange(1, iters + 1, dtype=np.float64) * n_total,
+                    com_cost=np.arange(1, iters + 1) * per, bytes_sent=0, bytes_total=0, primal_res=pres,
+                    extra={"backend": "native", "engine": "elastic", "segments": seg_info, "rank": 0, "nranks": 1,
+                           "solver": "closed", "obj0_final": cur_obj0,
+                           "state": (theta, mu, int(last.extra["state"][2]))})
+    res.theta = theta.cpu().numpy()
     return res
 
 

@@ -38,6 +38,19 @@ class LinearRegression:
     def device(self):
         return self.X.device
 
+    def subset(self, idx) -> "LinearRegression":
+        """The model of the local workers ``idx`` (in that order), sharing this model's Gram slices
+        (no recomputation; the statistics are per worker). Used by elastic recovery: the survivors
+        of a failure form a smaller chain on the same device."""
+        ix = torch.as_tensor(list(idx), dtype=torch.long, device=self.X.device)
+        sub = LinearRegression.__new__(LinearRegression)
+        sub.X, sub.y = self.X.index_select(0, ix), self.y.index_select(0, ix)
+        sub.lam = self.lam
+        sub.A, sub.b, sub.yy = self.A.index_select(0, ix), self.b.index_select(0, ix), self.yy.index_select(0, ix)
+        sub.n_local, sub.m, sub.d = int(ix.numel()), self.m, self.d
+        sub._chol = {}
+        return sub
+
     # ---- objective / gradient -------------------------------------------------------------------
     def objective(self, theta: torch.Tensor) -> torch.Tensor:
         """Per-worker ``1/2 ||X_n theta_n - y_n||^2 (+ lam/2 ||theta_n||^2)`` via the quadratic form.

@@ -534,6 +534,51 @@ def test_native_run_checkpoint_resumes_in_torch_path(lin24, lin_obj0, tmp_path):
     assert np.allclose(b.obj, ref.obj[nxt - 1:nxt + 49], rtol=1e-10)
 
 
+@pytest.mark.parametrize("persistent", [True, False])
+def test_native_resume_continues_native_run(lin24, lin_obj0, tmp_path, persistent):
+    """Checkpoint -> native resume: a native solve's state (per-worker checkpoint files) reloaded and
+    continued on the native engine (persistent kernel from start_iter, or the graph engine)
+    reproduces the uninterrupted native run's objective trace."""
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import chain_admm
+    from gadmm_amd.utils.checkpoint import save_checkpoint, load_checkpoint
+    m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
+    opts = {"persistent": persistent}
+    a = chain_admm(m, list(range(24)), 24, 3.0, lin_obj0, 1e-4, 3000, engine_opts=opts)
+    assert a.extra["backend"] == "native" and a.iters == 784
+    theta, mu, nxt = a.extra["state"]
+    save_checkpoint(str(tmp_path), 0, list(range(24)), theta, mu, nxt, list(range(24)), {"rho": 3.0})
+    th2, mu2, nxt2, _, _ = load_checkpoint(str(tmp_path), list(range(24)))
+    b = chain_admm(m, list(range(24)), 24, 3.0, lin_obj0, 1e-8, 3000, state=(th2, mu2, nxt2), engine_opts=opts)
+    ref = chain_admm(m, list(range(24)), 24, 3.0, lin_obj0, 1e-8, 3000, engine_opts=opts)
+    assert b.extra["backend"] == "native", b.extra
+    assert b.iters == ref.iters == 1373
+    assert len(b.obj) == 1373 - nxt + 1 and len(b.primal_res) == len(b.obj)
+    assert np.allclose(b.obj, ref.obj[nxt - 1:], rtol=1e-12, atol=0)
+    assert np.allclose(b.primal_res, ref.primal_res[nxt - 1:], rtol=1e-9, atol=1e-20)
+
+
+def test_native_elastic_matches_torch_path(lin24, lin_obj0):
+    """Elastic recovery on the native engine (workers 5 then 17, 18 fail; the survivors' chain
+    resumes natively) follows the torch path's elastic run and reaches the survivors' optimum."""
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import chain_admm
+    fail = {60: [5], 150: [17, 18]}
+    m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
+    nat = chain_admm(m, list(range(24)), 24, 3.0, lin_obj0, 1e-8, 5000, failures=fail)
+    tor = chain_admm(m, list(range(24)), 24, 3.0, lin_obj0, 1e-8, 5000, failures=fail, backend="torch")
+    assert nat.extra["backend"] == "native" and nat.extra["engine"] == "elastic", nat.extra
+    segs = nat.extra["segments"]
+    assert [(s["first"], s["last"], s["workers"]) for s in segs] == [(1, 59, 24), (60, 149, 23), (150, nat.iters, 21)]
+    assert nat.converged and tor.converged and nat.iters == tor.iters
+    assert len(nat.obj) == nat.iters
+    assert np.allclose(nat.obj, tor.obj, rtol=1e-10, atol=0)
+    assert abs(nat.obj[-1] - nat.extra["obj0_final"]) < 1e-8
+    alive = [w for w in range(24) if w not in (5, 17, 18)]
+    assert np.allclose(nat.extra["state"][0].cpu().numpy()[alive], tor.extra["state"][0].cpu().numpy()[alive],
+                       rtol=1e-7, atol=1e-9)
+
+
 @pytest.mark.parametrize("M,N,K", [(100, 70, 33), (256, 192, 128), (1, 5, 3), (130, 1, 64)])
 def test_gemm_f64_mfma_matches_torch(M, N, K):
     """The f64-MFMA tile GEMM of the blocked inverse (spd_inverse_blocked.hip) vs torch fp64."""
