@@ -27,7 +27,7 @@ COH = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 
 def solve():
     return dynamic_group_admm(m, 1.0, obj0, 1e-4, 3000, p0, c0, COH, seed=99, n_total=24, local_ids=list(range(24)),
-                              engine_opts={"state": False})
+                              engine_opts={"state": False, "residual": False})
 
 
 for _ in range(3):
