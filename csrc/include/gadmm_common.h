@@ -24,6 +24,9 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 extern "C" {
 #endif
 void gadmm_set_error(const char* fmt, ...);
+// Compute units of the current device (hipDeviceGetAttribute, cached per device: a full
+// hipGetDeviceProperties costs tens of microseconds and sat on every persistent launch's path).
+int gadmm_cu_count(void);
 const char* gadmm_last_error(void);
 #ifdef __cplusplus
 }

@@ -783,10 +783,9 @@ int gadmm_chain_blocked_plan(int n, int d, int want_k, int* k_out, int* len_out)
   // workgroups, one per CU) still fits on ONE XCD, so it can be packed there (PersistArgs::xcd).
   // With the halo GEMVs skipped where unused, a shorter segment means lighter phases: at N = 24,
   // L = 1 / 2 / 4 ran 1.94 / 1.98 / 2.07 ms (profiles/r02_halo_skip).
-  int cus_xcd = 32, dev = 0;
-  hipDeviceProp_t prop;
-  if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount >= 8)
-    cus_xcd = prop.multiProcessorCount / 8;
+  int cus_xcd = 32;
+  const int cus = gadmm_cu_count();
+  if (cus >= 8) cus_xcd = cus / 8;
   for (int l = 1; l < len; ++l)
     if ((n + l - 1) / l + (n + MAXW - 1) / MAXW + 1 <= cus_xcd) {
       len = l;

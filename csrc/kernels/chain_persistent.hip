@@ -29,6 +29,7 @@
 #include "persist_device.h"
 #include <stdlib.h>
 #include <string.h>
+#include <mutex>
 
 namespace {
 
@@ -568,15 +569,40 @@ static PVariant pick_variant(const PersistArgs& a) {
 // shared device). A persistent launch needs every one of its workgroups resident together: the
 // workers spin on each other, so a workgroup that waits for a CU would stall the rest until the
 // deadline. 0 on error.
+// Occupancy of (kernel, threads, LDS, device), queried once: eligibility checks and launches ask for
+// it several times per solve
+namespace {
+struct OccEntry {
+  const void* fn;
+  int threads, dev, per_cu;
+  size_t shm;
+};
+std::mutex g_occ_mu;
+OccEntry g_occ[128];
+int g_occ_n = 0;
+}  // namespace
+
 extern "C" long gadmm_resident_capacity(const void* fn, int threads, size_t shm) {
-  int dev = 0, per_cu = 0;
+  int dev = 0, per_cu = -1;
   if (hipGetDevice(&dev) != hipSuccess) return 0;
-  hipDeviceProp_t prop;
-  if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return 0;
-  if (shm > 65536 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess)
-    return 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, shm) != hipSuccess) return 0;
-  long cus = prop.multiProcessorCount;
+  {
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    for (int i = 0; i < g_occ_n; ++i)
+      if (g_occ[i].fn == fn && g_occ[i].threads == threads && g_occ[i].shm == shm && g_occ[i].dev == dev) {
+        per_cu = g_occ[i].per_cu;
+        break;
+      }
+  }
+  if (per_cu < 0) {
+    per_cu = 0;
+    if (shm > 65536 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm) != hipSuccess)
+      return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, shm) != hipSuccess) return 0;
+    std::lock_guard<std::mutex> lk(g_occ_mu);
+    if (g_occ_n < 128) g_occ[g_occ_n++] = OccEntry{fn, threads, dev, per_cu, shm};
+  }
+  long cus = gadmm_cu_count();
+  if (cus <= 0) return 0;
   if (const char* e = getenv("GADMM_CU_BUDGET")) {
     const long b = atol(e);
     if (b > 0 && b < cus) cus = b;

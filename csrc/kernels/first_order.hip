@@ -552,9 +552,8 @@ int gadmm_fo_launch(const FoArgs* a, void* stream) {
   long lds = gadmm_fo_lds(a->model, a->d, a->m);
   if (lds < 16L * a->n + 64) lds = 16L * a->n + 64;  // the monitor stages 2 doubles per worker
   if (lds > 160 * 1024 - 1024) return -3;
-  hipDeviceProp_t prop;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return -4;
+  const long ncu = gadmm_cu_count();
+  if (ncu <= 0) return -4;
   int per_cu = 0;
   const int mc = fo_mc(a->model, a->m);
   const void* fns[2][3] = {{(const void*)fo_persistent_kernel<1, 0>, (const void*)fo_persistent_kernel<1, 1>,
@@ -564,9 +563,9 @@ int gadmm_fo_launch(const FoArgs* a, void* stream) {
   const int nci = a->d <= 64 ? 0 : 1;
   const void* fn = fns[nci][mc];
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, (size_t)lds) != hipSuccess) return -4;
-  if ((long)per_cu * prop.multiProcessorCount < a->n + 1) return -5;  // persistent: all must be resident
+  if ((long)per_cu * ncu < a->n + 1) return -5;  // persistent: all must be resident
   FoArgs ka = *a;
-  ka.xcd = gadmm_xcd_pick(a->xcd, 0, a->n + 1, (long)per_cu * prop.multiProcessorCount, a->xchk);
+  ka.xcd = gadmm_xcd_pick(a->xcd, 0, a->n + 1, (long)per_cu * ncu, a->xchk);
   if (ka.xcd > 1 && hipMemsetAsync(a->xchk, 0, (size_t)XCHK * 16, (hipStream_t)stream) != hipSuccess) return -1;
   void* args[] = {&ka};
   if (hipLaunchKernel(fn, dim3(ka.xcd > 0 ? 8 * (a->n + 1) : a->n + 1), dim3(NT), args, (size_t)lds, (hipStream_t)stream) !=

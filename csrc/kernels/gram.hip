@@ -273,13 +273,8 @@ int gadmm_gram_pick_ksplit(int N, int m, int d) {
   const int BT = (d + 1 <= 64) ? 64 : 128;
   const int nt = (d + 1 + BT - 1) / BT;
   const long tiles = (long)N * (nt * (nt + 1) / 2);
-  static int cus = 0;
-  if (cus == 0) {
-    hipDeviceProp_t prop;
-    int dev = 0;
-    cus = (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-              ? prop.multiProcessorCount : 256;
-  }
+  int cus = gadmm_cu_count();
+  if (cus <= 0) cus = 256;
   const long slots = (long)cus * 2;  // 2 resident workgroups per CU (LDS / VGPR bound)
   long maxk = (m + 255) / 256;       // keep >= 256 rows per split
   if (maxk > 64) maxk = 64;

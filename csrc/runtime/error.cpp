@@ -3,7 +3,23 @@
 #include <stdio.h>
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 static thread_local char g_err[1024] = {0};
+static std::atomic<int> g_cus[64];
+
+extern "C" int gadmm_cu_count(void) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 0;
+  if (dev < 64) {
+    const int c = g_cus[dev].load(std::memory_order_relaxed);
+    if (c > 0) return c;
+  }
+  int c = 0;
+  if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0) return 0;
+  if (dev < 64) g_cus[dev].store(c, std::memory_order_relaxed);
+  return c;
+}
 
 extern "C" void gadmm_set_error(const char* fmt, ...) {
   va_list ap;

@@ -227,6 +227,21 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
     return res
 
 
+_RECHAINS: dict = {}
+
+
+def _rechains(max_iter: int, coherence) -> np.ndarray:
+    """``rechain_iterations`` memoised per (max_iter, coherence) (read-only array)."""
+    key = (int(max_iter), float(coherence))
+    r = _RECHAINS.get(key)
+    if r is None:
+        r = rechain_iterations(max_iter, coherence)
+        r.setflags(write=False)
+        if len(_RECHAINS) < 64:
+            _RECHAINS[key] = r
+    return r
+
+
 def _static_schedule(schedule, max_iter) -> bool:
     return not schedule.coherence or not np.isfinite(schedule.coherence) or schedule.coherence <= 0 \
         or schedule.coherence >= max_iter + 1
@@ -322,14 +337,14 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         per = float(np.sum(schedule.cost)) * (n_heads if cost_quirk else 1)
         com_cost = np.arange(1, iters - start + 2) * per
     elif want_persistent and eng.dynamic_eligible(fabric) \
-            and len(rechain_iterations(max_iter, schedule.coherence)) < (1 << 20):
+            and len(_rechains(max_iter, schedule.coherence)) < (1 << 20):
         # D-GADMM in persistent launches of up to `epoch_chunk` epochs each: the seeded chain sequence
         # is drawn a chunk ahead (batched, the identical RNG stream), every worker switches neighbours /
         # role at each epoch on the device. A chunk ends at a hard stop just before its last+1 epoch
         # (whose neighbours already receive theta); unless the monitor decided a stop, the next launch
         # continues with the same tag salt from there. Only the chains a solve reaches are drawn.
         engine_kind = "persistent-dynamic"
-        rechains = rechain_iterations(max_iter, schedule.coherence)
+        rechains = _rechains(max_iter, schedule.coherence)
         # first launch: `epoch_chunk` epochs, each continuation twice the previous. Drawing a chain
         # costs ~0.75 us on the host, a launch + read-back ~0.25 ms: 128 keeps coherence-10 solves
         # (~51 epochs) to one launch with few spare chains, coherence-1 solves (~250) to two
@@ -349,20 +364,20 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             chunk = len(rechains) + 1
         saved = schedule.save()
         E_total = 1 + len(rechains)
-        ep_P = [np.asarray(saved[1], dtype=np.int64)]
-        ep_C = [saved[2]]
-        ep_start = [1]
-        drawn_P, drawn_C = [], []
+        # epoch e's chain is row e of one (E_total, N) table, filled as chains are drawn (epoch 0: the
+        # initial chain); epoch e starts at iteration ep_start[e]
+        Pall = np.empty((E_total, n_total), dtype=np.int64)
+        Pall[0] = saved[1]
+        ep_start = np.concatenate([np.ones(1, dtype=np.int64), rechains])
+        drawn_C = []
+        n_drawn = [1]
 
         def ensure(upto):  # epochs 0..upto drawn
-            need = upto + 1 - len(ep_P)
+            need = upto + 1 - n_drawn[0]
             if need > 0:
                 Pn_, Cn_ = schedule.prefetch_arrays(need)
-                k0 = len(ep_start) - 1
-                ep_P.extend(list(Pn_))
-                ep_C.extend(list(Cn_))
-                ep_start.extend(int(v) for v in rechains[k0:k0 + need])
-                drawn_P.append(Pn_)
+                Pall[n_drawn[0]:n_drawn[0] + need] = Pn_
+                n_drawn[0] += need
                 drawn_C.append(Cn_)
 
         e0, start_iter, pending_in, cont = 0, 1, 0, False
@@ -373,8 +388,8 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             look = e1 if e1 < E_total else e1 - 1  # + the next epoch's chain (push targets of theta^hard_stop)
             ensure(look)
             hard_stop = ep_start[e1] - 1 if e1 < E_total else 0
-            st_arr = np.asarray(ep_start[e0:look + 1], dtype=np.int64)
-            P_arr = np.stack(ep_P[e0:look + 1]).astype(np.int64)
+            st_arr = ep_start[e0:look + 1]
+            P_arr = Pall[e0:look + 1]
             r = eng.run_persistent(epochs=(st_arr, P_arr), fabric=fabric, start_iter=start_iter, pending_in=pending_in,
                                    hard_stop=hard_stop, cont=cont)
             done, iters = int(r.done), int(r.iters)
@@ -396,15 +411,16 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             chunk *= 2
         if done == 5:
             done = 2
-        hints[hint_key] = int(np.searchsorted(np.asarray(ep_start), max(last_launched, 1), side="right"))
-        Pn = np.concatenate(drawn_P) if drawn_P else np.zeros((0, n_total), dtype=np.int64)
+        ep_start = ep_start[:n_drawn[0]]
+        hints[hint_key] = int(np.searchsorted(ep_start, max(last_launched, 1), side="right"))
+        Pn = Pall[1:n_drawn[0]]
         if drawn_C and any(c.dtype == object for c in drawn_C):
             Cn = np.empty(sum(len(c) for c in drawn_C), dtype=object)
             Cn[:] = [c for cc in drawn_C for c in cc]
         else:
             Cn = np.concatenate(drawn_C) if drawn_C else np.zeros((0, max(n_total - 1, 0)))
-        starts = np.asarray(ep_start, dtype=np.int64)
-        P = np.stack(ep_P).astype(np.int64)
+        starts = ep_start
+        P = Pall[:n_drawn[0]]
         # per-epoch cost; the initial cost vector may be ragged (the v0 column-slice quirk)
         csum = Cn.sum(axis=1) if (len(Cn) and Cn.dtype != object) else np.asarray([float(np.sum(c)) for c in Cn])
         per_it = np.concatenate([[float(np.sum(saved[2]))], csum]) * (n_heads if cost_quirk else 1)

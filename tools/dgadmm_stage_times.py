@@ -1,0 +1,69 @@
+"""Where a D-GADMM solve's wall time goes on the host: stamps at the solve start, at the persistent
+kernel launch call, after the launch returns, after the stream sync, and at the solve end (the launch
+entry points are wrapped on the ctypes library). Median over 40 solves of the bench config.
+Usage: python tools/dgadmm_stage_times.py [coherence]"""
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from gadmm_amd.data import linear_synthetic  # noqa: E402
+from gadmm_amd.models import LinearRegression  # noqa: E402
+from gadmm_amd.algorithms import dynamic_group_admm  # noqa: E402
+from gadmm_amd.parallel import topology as T  # noqa: E402
+from gadmm_amd.oracle.reference import opt_linear  # noqa: E402
+from gadmm_amd.ops import native  # noqa: E402
+
+dev = torch.device("cuda", 0)
+ds = linear_synthetic(24)
+Xf, yf = ds.stacked()
+obj0 = opt_linear(Xf.numpy(), yf.numpy())
+m = LinearRegression(ds.X.to(dev).contiguous(), ds.y.to(dev).contiguous())
+p0, c0, _ = T.find_path(24, np.random.default_rng(5))
+COH = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+lib = native.require()
+stamps = {}
+orig = lib.gadmm_chain_persistent_launch
+
+
+def wrapped(*a):
+    stamps["launch"] = time.perf_counter()
+    rc = orig(*a)
+    stamps["launched"] = time.perf_counter()
+    return rc
+
+
+lib.gadmm_chain_persistent_launch = wrapped
+orig_sync = torch.cuda.Stream.synchronize
+
+
+def sync(self):
+    orig_sync(self)
+    stamps["synced"] = time.perf_counter()
+
+
+torch.cuda.Stream.synchronize = sync
+
+
+def solve():
+    return dynamic_group_admm(m, 1.0, obj0, 1e-4, 3000, p0, c0, COH, seed=99, n_total=24, local_ids=list(range(24)),
+                              engine_opts={"state": False, "residual": False})
+
+
+for _ in range(3):
+    solve()
+torch.cuda.synchronize()
+rows = []
+for _ in range(40):
+    t0 = time.perf_counter()
+    r = solve()
+    t1 = time.perf_counter()
+    rows.append([stamps["launch"] - t0, stamps["launched"] - stamps["launch"], stamps["synced"] - stamps["launched"],
+                 t1 - stamps["synced"], t1 - t0])
+a = np.median(np.asarray(rows), axis=0) * 1e6
+print("coherence %d, %d iterations, engine %s" % (COH, r.iters, r.extra.get("engine")))
+print("median us: before launch %.1f | launch call %.1f | kernel + sync %.1f | after sync %.1f | total %.1f"
+      % tuple(a))
