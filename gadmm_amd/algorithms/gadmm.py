@@ -276,6 +276,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
            float(opts.get("chord", 0.02)), bool(opts.get("residual", True)))
     cache = getattr(model, "_chain_engines", None) if rcomm is None else None
     eng = cache.get(key) if cache is not None else None
+    fresh = eng is None
     if eng is None:
         eng = NativeChainEngine(model.X, model.y, local_ids, n_total, kind, rho=rho, obj0=obj0, tol=tol,
                                 max_iter=max_iter, lam=getattr(model, "lam", 0.0), step=step, max_inner=max_inner,
@@ -304,7 +305,10 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
 
     load_state()
     stop_iter = int(opts.get("stop_iter", 0))
-    torch.cuda.synchronize(model.device)
+    if fresh or state is not None:
+        # inputs made on other streams (a new engine's set-up, a loaded state) are complete before the
+        # solve; a cached engine's inputs are, and its own stream orders the reset before the kernel
+        torch.cuda.synchronize(model.device)
     t0 = time.perf_counter()
     cc = 0.0
     com_cost = []
@@ -460,7 +464,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             if comm.nranks > 1:
                 eng.exchange("tail")  # refresh ghost rows of the new cross-rank neighbours
             it = nxt
-    torch.cuda.synchronize(model.device)
+    eng.stream.synchronize()  # every engine path has synchronised its stream already: cheap
     wall = time.perf_counter() - t0
     tr, tt = eng.traces(iters)
     if start > 1:  # a resumed solve reports iterations start..iters (as the torch path does)

@@ -487,9 +487,16 @@ class NativeChainEngine:
             lag = max(lag, 8)  # the objective takes one more hop (worker -> objective wave -> monitor)
         ring = lag + 4
         dev = self.device
-        slots = sorted(self.plan.head + self.plan.tail, key=lambda s: self.path.index(s.gid))
-        pos = [self.path.index(s.gid) for s in slots]
-        key = (ring, tuple((s.li, s.gid, s.left, s.right) for s in slots), id(fabric), epochs is not None)
+        # this rank's slots in chain order, their positions and the buffer key: memoised per plan
+        pk = (id(self.plan), tuple(self.path))
+        memo = getattr(self, "_slot_memo", None)
+        if memo is None or memo[0] != pk:
+            pos_of = {g: i for i, g in enumerate(self.path)}
+            sl = sorted(self.plan.head + self.plan.tail, key=lambda s: pos_of[s.gid])
+            memo = (pk, sl, [pos_of[s.gid] for s in sl], tuple((s.li, s.gid, s.left, s.right) for s in sl), self.plan)
+            self._slot_memo = memo
+        _, slots, pos, slot_key, _ = memo
+        key = (ring, slot_key, id(fabric), epochs is not None)
         if getattr(self, "_pbuf", None) is None or self._pbuf[0] != key:
             with torch.cuda.stream(self.stream):
                 slot_t = torch.tensor([[s.li, s.gid, s.left, s.right] for s in slots], dtype=torch.int32,

@@ -46,6 +46,28 @@ def sync(self):
 
 
 torch.cuda.Stream.synchronize = sync
+acc = {}
+
+
+def timed(name, fn):
+    def w(*a, **k):
+        t = time.perf_counter()
+        r = fn(*a, **k)
+        acc[name] = acc.get(name, 0.0) + time.perf_counter() - t
+        return r
+    return w
+
+
+# pieces of the pre-launch path, summed per solve
+T.PathSchedule.prefetch_arrays = timed("draws", T.PathSchedule.prefetch_arrays)
+T.PathSchedule.__init__ = timed("schedule", T.PathSchedule.__init__)
+lib.gadmm_epoch_tables = timed("epoch_tables", lib.gadmm_epoch_tables)
+torch.cuda.synchronize = timed("device_sync", torch.cuda.synchronize)
+from gadmm_amd.engine import chain_engine as CE  # noqa: E402
+CE.NativeChainEngine.reset = timed("reset", CE.NativeChainEngine.reset)
+CE.NativeChainEngine.set_path = timed("set_path", CE.NativeChainEngine.set_path)
+CE.NativeChainEngine.dynamic_eligible = timed("eligible", CE.NativeChainEngine.dynamic_eligible)
+CE.NativeChainEngine.traces = timed("traces", CE.NativeChainEngine.traces)
 
 
 def solve():
@@ -57,6 +79,7 @@ for _ in range(3):
     solve()
 torch.cuda.synchronize()
 rows = []
+acc.clear()
 for _ in range(40):
     t0 = time.perf_counter()
     r = solve()
@@ -67,3 +90,4 @@ a = np.median(np.asarray(rows), axis=0) * 1e6
 print("coherence %d, %d iterations, engine %s" % (COH, r.iters, r.extra.get("engine")))
 print("median us: before launch %.1f | launch call %.1f | kernel + sync %.1f | after sync %.1f | total %.1f"
       % tuple(a))
+print("per solve, us: " + ", ".join("%s %.1f" % (k, v / 40 * 1e6) for k, v in sorted(acc.items())))
