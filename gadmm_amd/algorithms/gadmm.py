@@ -322,7 +322,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         engine_kind = None
         if want_persistent and stop_iter <= 0 and eng.persistent_eligible(fabric):
             try:
-                r = eng.run_persistent(fabric=fabric, start_iter=start)
+                r = eng.run_persistent(fabric=fabric, start_iter=start, fetch_trace=True)
                 engine_kind = "persistent"
             except (ResidencyError, HandoffTimeout) as e:
                 # the device could not hold every workgroup, or a hand-off stalled: the graph engine
@@ -395,7 +395,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             st_arr = ep_start[e0:look + 1]
             P_arr = Pall[e0:look + 1]
             r = eng.run_persistent(epochs=(st_arr, P_arr), fabric=fabric, start_iter=start_iter, pending_in=pending_in,
-                                   hard_stop=hard_stop, cont=cont)
+                                   hard_stop=hard_stop, cont=cont, fetch_trace=True)
             done, iters = int(r.done), int(r.iters)
             if comm.nranks > 1 and hard_stop > 0:
                 # the monitor rank holds the outcome of a chunk (the workers may stop at the hard stop

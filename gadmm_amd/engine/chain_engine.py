@@ -453,7 +453,8 @@ class NativeChainEngine:
 
     def run_persistent(self, lag: int = 4, timeout_s: float = 20.0, start_iter: int = 1,
                        pending_in: int = 0, fabric=None, timeline_iters: int = 0,
-                       epochs: Optional[Sequence] = None, hard_stop: int = 0, cont: bool = False) -> EngineRun:
+                       epochs: Optional[Sequence] = None, hard_stop: int = 0, cont: bool = False,
+                       fetch_trace: bool = False) -> EngineRun:
         """Whole solve in one launch per GPU. State must be reset (``reset()``) or resumed by the
         caller. ``fabric``: an ``XgmiFabric`` for the multi-GPU device-initiated transport.
         ``timeline_iters > 0`` records s_memrealtime stamps (10 ns) of the first iterations into
@@ -469,7 +470,9 @@ class NativeChainEngine:
         monitor rank's ``done`` is then 5 unless it decided a stop; the table should include the epoch
         starting at ``hard_stop + 1``, whose neighbours receive theta^hard_stop); ``cont=True`` continues
         the previous chunk from ``start_iter = hard_stop + 1`` with the same tag salt, epoch 0 being the
-        previous chunk's last epoch (its heads' pending duals are flushed with that chain)."""
+        previous chunk's last epoch (its heads' pending duals are flushed with that chain).
+        ``fetch_trace``: the objective trace and clock come back behind the same stream sync (for a
+        caller that reads ``traces()`` next; a benchmark loop that does not leaves it off)."""
         if epochs is not None:
             if not self.dynamic_eligible(fabric):
                 raise RuntimeError("dynamic persistent kernel not eligible for this engine/config")
@@ -684,14 +687,15 @@ class NativeChainEngine:
             # the objective trace and the clock come back behind the same sync too (short traces:
             # traces() then reads the pinned copy instead of a second blocking device round trip)
             nt = self.trace.numel()
-            if nt <= 16384:
+            fetch = fetch_trace and nt <= 16384
+            if fetch:
                 if getattr(self, "_tr_host", None) is None or self._tr_host.numel() != 2 * nt + 1:
                     self._tr_host = torch.empty((2 * nt + 1,), dtype=torch.float64, pin_memory=True)
                 self._tr_host[:nt].copy_(self.trace, non_blocking=True)
                 self._tr_host[nt:2 * nt].copy_(self.tstamp[:nt].view(torch.float64), non_blocking=True)
                 self._tr_host[2 * nt:].copy_(self.t0stamp.view(torch.float64), non_blocking=True)
             self.stream.synchronize()
-            self._tr_valid = nt <= 16384
+            self._tr_valid = fetch
             t1 = _time.perf_counter()
         self.last_timeline = tl.cpu().numpy() if tl is not None else None
         self.last_timeline_slots = [(s.gid, p) for s, p in zip(slots, pos)] if tl is not None else None

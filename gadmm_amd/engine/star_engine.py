@@ -50,9 +50,13 @@ class StarEngine:
             self._shifts = torch.tensor([[(self.n - 1) * self.rho if w == self.n - 1 else self.rho]
                                          for w in self.local], dtype=f64, device=dev)
             self.Minv = spd_inverse(self.A, self._shifts)
-            self.theta = torch.zeros((nl, d), dtype=f64, device=dev)
-            self.lam = torch.zeros((nl, d), dtype=f64, device=dev)
-            self.lam_hub = torch.zeros((self.n, d), dtype=f64, device=dev)
+            # theta, lam and the hub's lam table in ONE buffer: a solve's reset is one fill
+            # (each part starts on a 256-byte boundary, as its own allocation would)
+            seg = (nl * d + 31) // 32 * 32
+            self._state = torch.zeros((2 * seg + self.n * d,), dtype=f64, device=dev)
+            self.theta = self._state[: nl * d].view(nl, d)
+            self.lam = self._state[seg: seg + nl * d].view(nl, d)
+            self.lam_hub = self._state[2 * seg: 2 * seg + self.n * d].view(self.n, d)
             self.trace = torch.full((self.max_iter,), float("nan"), dtype=f64, device=dev)
             self.tstamp = torch.zeros((self.max_iter,), dtype=torch.int64, device=dev)
             self.t0stamp = torch.zeros((1,), dtype=torch.int64, device=dev)
@@ -122,19 +126,30 @@ class StarEngine:
         if timeline_iters > 0:
             tl = torch.zeros((len(self.local) + 1, int(timeline_iters), 4), dtype=torch.int64, device=self.device)
             a.timeline, a.timeline_iters = tl.data_ptr(), int(timeline_iters)
+        self._host_n = 0
         with torch.cuda.stream(self.stream):
-            self.theta.zero_()
-            self.lam.zero_()
-            self.lam_hub.zero_()
+            self._state.zero_()
             self.ctl.zero_()
             native.check(self.lib.gadmm_write_stamp(self.t0stamp.data_ptr(), self.stream.cuda_stream), "write_stamp")
             t0 = time.perf_counter()
             rc = int(self.lib.gadmm_star_launch(ctypes.byref(a), self.stream.cuda_stream))
             native.check(rc, "star_launch")
+            # control block, the first K trace / clock entries and the start stamp come back behind the
+            # kernel in one pinned copy batch: one blocking round trip per solve instead of four
+            K = min(self.max_iter, 4096)
+            if getattr(self, "_host", None) is None:
+                self._host = (torch.empty((8,), dtype=torch.int32, pin_memory=True),
+                              torch.empty((2 * K + 1,), dtype=torch.int64, pin_memory=True))
+            hc, ht = self._host
+            hc.copy_(self.ctl, non_blocking=True)
+            ht[:K].copy_(self.trace[:K].view(torch.int64), non_blocking=True)
+            ht[K:2 * K].copy_(self.tstamp[:K], non_blocking=True)
+            ht[2 * K:].copy_(self.t0stamp, non_blocking=True)
             self.stream.synchronize()
             t1 = time.perf_counter()
+            self._host_n = K
         self.last_timeline = tl.cpu().numpy() if tl is not None else None
-        c = self.ctl.cpu().tolist()
+        c = self._host[0].tolist()
         if c[1] == 4:
             from .chain_engine import HandoffTimeout
             raise HandoffTimeout("star kernel timed out (hand-off never completed)")
@@ -154,11 +169,18 @@ class StarEngine:
         return pay, 2 * pay, mon
 
     def objective_trace(self, upto: int) -> np.ndarray:
+        if 0 <= upto <= getattr(self, "_host_n", 0):  # the pinned copy of the last run
+            return self._host[1].numpy()[:upto].view(np.float64).copy()
         return self.trace[:upto].cpu().numpy()
 
     def time_trace(self, upto: int) -> np.ndarray:
-        t = self.tstamp[:upto].cpu().numpy().astype(np.int64)
-        t0 = int(self.t0stamp.cpu().item())
+        K = getattr(self, "_host_n", 0)
+        if 0 <= upto <= K:
+            h = self._host[1].numpy()
+            t, t0 = h[K:K + upto], int(h[2 * K])
+        else:
+            t = self.tstamp[:upto].cpu().numpy().astype(np.int64)
+            t0 = int(self.t0stamp.cpu().item())
         return np.where(t > 0, (t - t0) * 1e-8, 0.0)
 
     def close(self):
