@@ -2,6 +2,15 @@
 // (cdna_hip_programming.md §6 Guideline 16, R2), wall-clock deadlines, LDS-resident GEMV.
 #pragma once
 #include "gadmm_common.h"
+
+// Pause between two polls of a hand-off spin (s_sleep units of 64 clocks; 0 = poll back to back).
+#ifndef GADMM_POLL_SLEEP
+#define GADMM_POLL_SLEEP 1
+#endif
+#define GADMM_POLL_PAUSE()                                              \
+  do {                                                                  \
+    if (GADMM_POLL_SLEEP > 0) __builtin_amdgcn_s_sleep(GADMM_POLL_SLEEP); \
+  } while (0)
 #include "gadmm_chain.h"
 #include "quad_gemv.h"
 
@@ -92,7 +101,7 @@ __device__ __forceinline__ bool wait_row(__amdgpu_buffer_rsrc_t rs, int row, int
     }
     if (__all(ok)) return true;
     if (now_ticks() > deadline) return false;
-    __builtin_amdgcn_s_sleep(1);
+    GADMM_POLL_PAUSE();
   }
 }
 
@@ -123,7 +132,7 @@ __device__ __forceinline__ int wait_pair(__amdgpu_buffer_rsrc_t rs, int d, int r
       }
       if (now_ticks() > deadline) return 0;
     }
-    __builtin_amdgcn_s_sleep(1);
+    GADMM_POLL_PAUSE();
   }
 }
 

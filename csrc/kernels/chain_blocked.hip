@@ -59,7 +59,7 @@ __device__ __forceinline__ void blocked_monitor(const PersistArgs& a, double* ld
           okall = false;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        GADMM_POLL_PAUSE();
       }
       vals[w] = val;
     }
@@ -128,7 +128,7 @@ __device__ __forceinline__ void blocked_objective(const PersistArgs& a, double* 
         }
         if (now_ticks() > deadline) return;  // the monitor times out and reports it
       }
-      __builtin_amdgcn_s_sleep(1);
+      GADMM_POLL_PAUSE();
     }
     const double qv = quad_gemv<QT>(Aq, in ? x : 0.0, xo);  // (A th)_i in the order of every other engine
     const double part = in ? (0.5 * qv - bo) * x : 0.0;
@@ -330,7 +330,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
               ok = false;
               break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            GADMM_POLL_PAUSE();
           }
           if (!ok && lane == 0) abort_lds = 1;
           th = in ? t0 : 0.0;
@@ -369,7 +369,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
             ok = false;
             break;
           }
-          __builtin_amdgcn_s_sleep(1);
+          GADMM_POLL_PAUSE();
         }
         if (!ok && lane == 0) abort_lds = 1;
         th = in ? t0 : 0.0;
@@ -467,7 +467,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
           abort_lds = 1;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        GADMM_POLL_PAUSE();
         dv = load_dec<SYS>(&a.decg[dslot]);
       }
       const unsigned code = (unsigned)(dv & 0xffffffffu);
@@ -650,7 +650,7 @@ __global__ void __launch_bounds__(64 * PWW) chain_blocked_pair_kernel(PersistArg
             ok = false;
             break;
           }
-          __builtin_amdgcn_s_sleep(1);
+          GADMM_POLL_PAUSE();
         }
         if (!ok && lane == 0) abort_lds = 1;
         if (needH) {
@@ -729,7 +729,7 @@ __global__ void __launch_bounds__(64 * PWW) chain_blocked_pair_kernel(PersistArg
           abort_lds = 1;
           break;
         }
-        __builtin_amdgcn_s_sleep(1);
+        GADMM_POLL_PAUSE();
         dvv = load_dec<SYS>(&a.decg[jdec % a.ring]);
       }
       const unsigned code = (unsigned)(dvv & 0xffffffffu);

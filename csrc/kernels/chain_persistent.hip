@@ -24,6 +24,10 @@
 // Tags are salted with a per-solve epoch, so buffers need no re-zeroing between solves.
 // Every spin is bounded by a wall-clock deadline (s_memrealtime); on timeout the kernel records
 // done = 4 and every workgroup exits.
+// One wave per worker, one hand-off wait per phase on the critical path: poll back to back (same-box
+// A/B, profiles/r02_pollab: per-worker E1 3.065 -> 3.016 ms, D-GADMM 1.51 -> 1.48 ms; the blocked and
+// star kernels keep the default pause, where polling back to back measured no gain)
+#define GADMM_POLL_SLEEP 0
 #include "gadmm_common.h"
 #include "gadmm_chain.h"
 #include "persist_device.h"
@@ -95,7 +99,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
               abort_lds = 1;
               break;
             }
-            __builtin_amdgcn_s_sleep(1);
+            GADMM_POLL_PAUSE();
           }
           vals[w] = v;
         }
@@ -308,7 +312,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
         if (decided && (unsigned)(dv & 0xffffffffu) != 0u) { outcome = 2; break; }
         if (decided && __all(nb)) { outcome = 1; break; }
         if ((spin & 7) == 7 && now_ticks() > deadline) { outcome = 3; break; }
-        __builtin_amdgcn_s_sleep(1);
+        GADMM_POLL_PAUSE();
       }
       if (lane == 0) {
         if (TL) t_ready = (long long)now_ticks();
