@@ -506,6 +506,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         # resumable state for checkpoints: apply the heads' pending (lazy) duals with the current
         # chain, so (theta, mu) is the reference state after iteration next-1
         eng.flush_duals()
+        eng.stream.synchronize()  # the flush runs on the engine's stream; the copies below do not
         nxt = int(eng.ctl_state()["iter"])
         res.extra["state"] = (eng.theta.clone(), eng.mu.clone(), nxt)
     return res
