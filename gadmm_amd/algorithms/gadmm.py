@@ -299,6 +299,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     def load_state():  # fresh solve state, or the checkpoint's tables at start_iter (no pending duals)
         eng.reset(start_iter=start)
         if state is not None:
+            eng.stream.wait_stream(torch.cuda.current_stream(model.device))  # the state's producers
             with torch.cuda.stream(eng.stream):
                 eng.theta.copy_(state[0].to(eng.theta.device, torch.float64).reshape(eng.theta.shape))
                 eng.mu.copy_(state[1].to(eng.mu.device, torch.float64).reshape(eng.mu.shape))
