@@ -6,6 +6,7 @@
 // of milliseconds of numpy dispatch. Bit-identical to PathSchedule.prefetch_arrays' numpy path: no
 // FMA contraction, the same operation order ((dx*dx) + (dy*dy); ((d2*eta)*bw)*f for energies).
 #include <algorithm>
+#include <cstdlib>
 #include <limits>
 #include <thread>
 #include <vector>
@@ -84,8 +85,10 @@ extern "C" int gadmm_greedy_chains(const double* uv, int E, int n, double side, 
   if (work > 400000) {  // below this one core beats spawning threads (~300 epochs x 24 nodes: ~40 us)
     const unsigned hw = std::thread::hardware_concurrency();
     nt = (int)std::min<long>(std::min<unsigned>(hw ? hw : 1, 8u), std::max<long>(1, work / 40000));
-    if (nt > E) nt = E;
   }
+  static const int env_nt = getenv("GADMM_CHAIN_THREADS") ? atoi(getenv("GADMM_CHAIN_THREADS")) : 0;  // A/B
+  if (env_nt >= 1) nt = std::min(env_nt, 8);
+  if (nt > E) nt = E;
   if (nt <= 1) {
     greedy_range(uv, 0, E, n, side, energy, eta, bw, f, paths, costs);
     return 0;
