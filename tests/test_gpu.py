@@ -579,6 +579,24 @@ def test_native_elastic_matches_torch_path(lin24, lin_obj0):
                        rtol=1e-7, atol=1e-9)
 
 
+@pytest.mark.parametrize("fail", [{1: [0]}, {3000: [3]}, {40: [23], 41: [22]}])
+def test_native_elastic_edge_cases(lin24, lin_obj0, fail):
+    """Native elastic recovery at the edges: a failure before the first iteration (the survivors
+    start from scratch), one after convergence (never reached: one plain segment) and failures on
+    consecutive iterations at the chain's end (a one-iteration segment in between)."""
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import chain_admm
+    m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
+    nat = chain_admm(m, list(range(24)), 24, 3.0, lin_obj0, 1e-8, 5000, failures=fail)
+    tor = chain_admm(m, list(range(24)), 24, 3.0, lin_obj0, 1e-8, 5000, failures=fail, backend="torch")
+    assert nat.extra["backend"] == "native" and nat.extra["engine"] == "elastic", nat.extra
+    assert nat.converged and tor.converged and nat.iters == tor.iters and len(nat.obj) == nat.iters
+    assert np.allclose(nat.obj, tor.obj, rtol=1e-10, atol=0)
+    segs = nat.extra["segments"]
+    assert segs[0]["first"] == 1 and segs[-1]["last"] == nat.iters
+    assert all(b["first"] == a["last"] + 1 for a, b in zip(segs, segs[1:]))
+
+
 @pytest.mark.parametrize("M,N,K", [(100, 70, 33), (256, 192, 128), (1, 5, 3), (130, 1, 64)])
 def test_gemm_f64_mfma_matches_torch(M, N, K):
     """The f64-MFMA tile GEMM of the blocked inverse (spd_inverse_blocked.hip) vs torch fp64."""
