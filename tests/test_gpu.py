@@ -558,6 +558,24 @@ def test_native_resume_continues_native_run(lin24, lin_obj0, tmp_path, persisten
     assert np.allclose(b.primal_res, ref.primal_res[nxt - 1:], rtol=1e-9, atol=1e-20)
 
 
+def test_native_resume_logistic_inner_gd(log24, log_obj0):
+    """Native resume of the persistent logistic (inner GD) kernel: a solve stopped at a looser gap,
+    continued from its state to the reference 1e-4 gap, follows the uninterrupted native solve
+    (53 iterations, the reference count)."""
+    from gadmm_amd.models import LogisticRegression
+    from gadmm_amd.algorithms import chain_admm
+    m = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
+    kw = dict(local_solver="gd", step=2.2, max_inner=100, inner_tol=1e-4)
+    a = chain_admm(m, list(range(24)), 24, 2e-4, log_obj0, 1e-2, 400, **kw)
+    assert a.extra["backend"] == "native" and a.converged and a.iters < 53
+    th, mu, nxt = a.extra["state"]
+    b = chain_admm(m, list(range(24)), 24, 2e-4, log_obj0, 1e-4, 400, state=(th, mu, nxt), **kw)
+    ref = chain_admm(m, list(range(24)), 24, 2e-4, log_obj0, 1e-4, 400, **kw)
+    assert b.extra["backend"] == "native" and b.extra["engine"] == "persistent", b.extra
+    assert b.iters == ref.iters == 53 and len(b.obj) == 53 - nxt + 1
+    assert np.allclose(b.obj, ref.obj[nxt - 1:], rtol=1e-12, atol=0)
+
+
 def test_native_elastic_matches_torch_path(lin24, lin_obj0):
     """Elastic recovery on the native engine (workers 5 then 17, 18 fail; the survivors' chain
     resumes natively) follows the torch path's elastic run and reaches the survivors' optimum."""
