@@ -173,5 +173,14 @@ struct PersistArgs {
   // GADMM_XCD overrides xcd (A/B runs).
   u32x4* xchk;
   int xcd, pad_xcd;
+  // Data-local temporal blocking across GPUs (chain_blocked_kernel, blk_dl = 1; engine/blocked_xgmi.py
+  // data_local=True): the workgroups of a rank compute ONLY its own segment [seg_lo, seg_hi] (no other
+  // rank's shards), blocked inside it as on one GPU; a position at a rank boundary exchanges theta with
+  // the neighbouring rank's boundary position EVERY phase through the theta ring of blk_tab: the owner
+  // pushes theta^j of position p into the neighbour rank's ring (slot j % ring, row p, tag j), readers
+  // poll their own ring (group_ADMM_closedForm.m:18-27,62-70: only theta crosses, never mu).
+  // dl_tab[0] / [1]: blk_tab of the rank owning seg_lo - 1 / seg_hi + 1 (null at the chain ends).
+  int blk_dl, pad_dl;
+  u32x4* dl_tab[2];
 };
 constexpr int XCHK = 256;  // placement-check granules (>= workgroups of any XCD-packed launch)

@@ -107,8 +107,19 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
     if (thr) c = c - rho * thr[t];
     cv[t] = c;
     xv[t] = thw[t];
+  } else if (t < 64) {
+    // padding slots d..63 are read by the 64-wide loops below (H^-1 g multiplies them by the
+    // identity padding's exact zeros): they must hold finite values, not a previous kernel's LDS
+    cv[t] = 0.0;
+    xv[t] = 0.0;
+    gv[t] = 0.0;
   }
   if (t < m) yv[t] = Yg[t];
+  else if (t < 64) {
+    yv[t] = 0.0;
+    sv[t] = 0.0;
+    wv[t] = 0.0;
+  }
   double h[NCW];  // lane i of wave w: row i of the inverse, columns j = w + NWV c
   bool refresh = true;
   if (hg && chord > 0.0 && hg[4096] == 1.0 && hg[4097] == shift) {

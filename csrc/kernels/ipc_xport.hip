@@ -127,8 +127,15 @@ __global__ void __launch_bounds__(256) ipc_allgather_kernel(const double* part, 
   }
 }
 
+// A new epoch restarts the all-gather sequence too: a rank that returned early (ctl->done) and one
+// whose all-gather timed out have advanced word[1] differently, and the parity / tag derived from
+// it must agree across ranks for every later solve on this transport. The epoch salts the tags, so
+// restarting the sequence at 0 cannot match a granule of an earlier epoch.
 __global__ void ipc_new_epoch_kernel(unsigned* word) {
-  if (threadIdx.x == 0) word[0] = word[0] % 4095u + 1u;
+  if (threadIdx.x == 0) {
+    word[0] = word[0] % 4095u + 1u;
+    word[1] = 0u;
+  }
 }
 
 }  // namespace

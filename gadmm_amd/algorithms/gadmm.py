@@ -395,15 +395,30 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             hard_stop = ep_start[e1] - 1 if e1 < E_total else 0
             st_arr = ep_start[e0:look + 1]
             P_arr = Pall[e0:look + 1]
-            r = eng.run_persistent(epochs=(st_arr, P_arr), fabric=fabric, start_iter=start_iter, pending_in=pending_in,
-                                   hard_stop=hard_stop, cont=cont, fetch_trace=True)
-            done, iters = int(r.done), int(r.iters)
-            if comm.nranks > 1 and hard_stop > 0:
-                # the monitor rank holds the outcome of a chunk (the workers may stop at the hard stop
-                # before the decision of its last lag iterations reaches them)
+            timed_out = None
+            try:
+                r = eng.run_persistent(epochs=(st_arr, P_arr), fabric=fabric, start_iter=start_iter,
+                                       pending_in=pending_in, hard_stop=hard_stop, cont=cont, fetch_trace=True)
+            except HandoffTimeout as e:
+                if comm.nranks == 1:
+                    raise
+                timed_out = e  # agree with the other ranks first: they may be waiting on this chunk's outcome
+                r = None
+            done, iters = (int(r.done), int(r.iters)) if r is not None else (4, 0)
+            if comm.nranks > 1:
+                # every chunk ends in ONE collective on every rank: the monitor rank holds the outcome
+                # (the workers may stop at the hard stop before the decision of its last lag iterations
+                # reaches them), and a timeout on ANY rank is agreed in the same all-reduce, so all ranks
+                # raise together instead of the others waiting in a broadcast until the group's timeout.
+                # MAX over [rank 0's (done, iters) | -1 elsewhere, failed flag].
                 import torch.distributed as dist
-                t = torch.tensor([float(done), float(iters)], dtype=torch.float64)
-                dist.broadcast(t, src=0, group=getattr(comm, "control_group", None))
+                mine = comm.rank == 0
+                t = torch.tensor([float(done) if mine else -1.0, float(iters) if mine else -1.0,
+                                  1.0 if timed_out is not None else 0.0], dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX, group=getattr(comm, "control_group", None))
+                if float(t[2].item()) > 0:
+                    raise HandoffTimeout("D-GADMM chunk: a persistent hand-off timed out on some rank"
+                                         + (" (here: %s)" % timed_out if timed_out is not None else ""))
                 done, iters = int(t[0].item()), int(t[1].item())
             p2p, mon, wire = p2p + r.p2p_bytes, mon + r.monitor_bytes, wire + r.wire_bytes
             last_launched = hard_stop if done == 5 else start_iter - 1 + int(r.iterations_launched)

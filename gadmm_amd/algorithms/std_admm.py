@@ -112,7 +112,8 @@ def _standard_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, c
     if comm.nranks > 1:  # the monitor (rank 0) holds the trace: every rank returns the same result
         import torch.distributed as dist
         buf = torch.from_numpy(np.stack([tr, tt]).astype(np.float64))
-        dist.broadcast(buf, src=0)
+        # a CPU tensor: the comm's gloo control group (the default group may be nccl under launch.py)
+        dist.broadcast(buf, src=0, group=getattr(comm, "control_group", None))
         tr, tt = buf[0].numpy().copy(), buf[1].numpy().copy()
     pay, wire, mon = eng.bytes_per_solve(iters)
     return RunResult(algorithm=name, obj=tr, loss=np.abs(tr - obj0), iters=iters, converged=(done == 1), wall_s=wall,

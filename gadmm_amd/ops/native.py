@@ -107,6 +107,7 @@ class PersistArgs(ctypes.Structure):
         ("tstamp", c_void_p), ("ep_push", c_void_p), ("peer_thg", c_void_p), ("rres", c_void_p),
         ("hard_stop", c_int), ("cont", c_int),
         ("xchk", c_void_p), ("xcd", c_int), ("pad_xcd", c_int),
+        ("blk_dl", c_int), ("pad_dl", c_int), ("dl_tab", c_void_p * 2),
     ]
 
 
@@ -215,6 +216,9 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_rccl_bcast_f64": (c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p]),
         "gadmm_rccl_counters": (c_int, [c_void_p, ctypes.POINTER(c_longlong)]),
         "gadmm_rccl_reset_counters": (c_int, [c_void_p]),
+        "gadmm_poison_lds": (c_int, [c_long, c_int, c_void_p]),
+        "gadmm_poison_buffer": (c_int, [c_void_p, c_long, c_void_p]),
+        "gadmm_lds_probe": (c_int, [c_void_p, c_int, c_int, c_void_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)
@@ -266,6 +270,15 @@ def check(rc: int, what: str = "native call") -> None:
     if rc != 0:
         msg = require().gadmm_last_error()
         raise RuntimeError("%s failed (rc=%d): %s" % (what, rc, msg.decode() if msg else "?"))
+
+
+def poison_lds(per_cu: int = 4, sync: bool = True) -> None:
+    """Fill every CU's LDS with NaN patterns (csrc/kernels/debug_poison.hip). A kernel that reads
+    LDS it did not write then produces NaN deterministically instead of depending on what the
+    previous kernel left behind (the GPU test tier poisons before every test)."""
+    check(require().gadmm_poison_lds(0, per_cu, stream_handle()), "poison_lds")
+    if sync:
+        torch.cuda.synchronize()
 
 
 def ptr(t: Optional[torch.Tensor]) -> Optional[int]:

@@ -28,7 +28,7 @@ def test_abi_layout_matches_ctypes():
            native.PhaseArgs.inner_iters.offset, ctypes.sizeof(native.EngineDesc), native.EngineDesc.stream.offset,
            ctypes.sizeof(native.RunStats), ctypes.sizeof(native.PersistArgs), native.PersistArgs.rho.offset,
            native.PersistArgs.ctl.offset, native.PhaseArgs.lgid.offset, native.EngineDesc.xport.offset,
-           native.PersistArgs.xchk.offset]
+           native.PersistArgs.xchk.offset, native.PersistArgs.dl_tab.offset]
     assert got == exp
 
 
