@@ -10,8 +10,10 @@ The workers form one chain laid over the GPUs in contiguous segments. **Data-loc
 rank builds and holds only its own workers' shards (``benchmarks.headline_rank_problem``) and ships
 only theta, to the two chain neighbours (group_ADMM_closedForm.m:18-27, 62-70):
 * 1 GPU: the temporally blocked persistent kernel (one launch per solve);
-* N GPUs (``--fabric auto``/``xgmi``): the per-worker persistent kernel, boundary theta pushed into
-  the neighbour GPU's table over xGMI (device-initiated, IPC-mapped fine-grained memory);
+* N GPUs (``--fabric auto``/``xgmi``): the temporally blocked kernel run inside every rank's segment
+  (data-local mode: only the segment-edge workers' theta crosses, every phase, pushed into the
+  neighbour GPU's ring over xGMI -- device-initiated, IPC-mapped fine-grained memory); if that is
+  unavailable, the per-worker persistent kernel over the same fabric;
 * fallbacks, taken by every rank together: the graph-replayed phase kernels with RCCL send/recv
   (``--fabric rccl``), or with the device-copy transport (``--fabric ipc``; also the fallback when
   ranks share one GPU, where RCCL cannot run).
@@ -65,9 +67,12 @@ def main():
     ap.add_argument("--workers", type=int, default=24)
     ap.add_argument("--block", type=int, default=0, help="iterations per graph replay (0: auto)")
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--engine", choices=["auto", "persistent", "graph", "replicated-halo"], default="auto",
-                    help="auto: persistent single-launch kernel when eligible, else graph-replayed phases; "
-                         "replicated-halo: opt-in blocked kernel across GPUs (ranks hold halo shards)")
+    ap.add_argument("--engine", choices=["auto", "persistent", "blocked-dl", "per-worker", "graph", "replicated-halo"],
+                    default="auto",
+                    help="auto: persistent single-launch kernel when eligible (N GPUs: the data-local blocked "
+                         "kernel, then the per-worker kernel), else graph-replayed phases; blocked-dl / "
+                         "per-worker: only that persistent kernel; replicated-halo: opt-in blocked kernel "
+                         "across GPUs (ranks hold halo shards)")
     ap.add_argument("--fabric", choices=["auto", "xgmi", "rccl", "ipc"], default="auto",
                     help="multi-GPU transport: xgmi = device-initiated theta pushes between persistent kernels, "
                          "rccl = RCCL send/recv between graph-replayed phases, ipc = the device-copy transport "
@@ -163,7 +168,7 @@ def run_headline(args, rank, world, device, share):
         p2p, wire, mon, repl = int(sm[1]), int(sm[2]), int(sm[3]), int(sm[4])
     tr = sol.objective_trace(iters)
     gap = abs(float(tr[iters - 1]) - obj0) if iters > 0 else float("nan")
-    data_local = sol.blk is None
+    data_local = sol.blk is None or sol.blk.data_local
     if rank == 0:
         value = ms / 1e3
         out = {

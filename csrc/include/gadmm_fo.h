@@ -25,20 +25,34 @@ struct FoArgs {
   double obj0, tol;
   double thrd;    // LAG trigger constant
   long long timeout_ticks;
-  const double* A;     // linear: (n, d, d) Grams
-  const double* b;     // linear: (n, d)
-  const double* yy;    // linear: (n)
-  const double* X;     // logistic: (n, m, d)
-  const double* Y;     // logistic: (n, m) labels +-1
-  const double* hsq;   // LAG-PS: Hmax_n^2
+  const double* A;     // linear: (n_local, d, d) Grams of THIS rank's workers
+  const double* b;     // linear: (n_local, d)
+  const double* yy;    // linear: (n_local)
+  const double* X;     // logistic: (n_local, m, d)
+  const double* Y;     // logistic: (n_local, m) labels +-1
+  const double* hsq;   // LAG-PS: Hmax_n^2 of EVERY worker (n)
   const int* sched;    // IAG: refreshing worker of iteration it at sched[it - 1]
-  u32x4* tab;          // [2][n][d] gradient / dual-variable granules
-  u32x4* part;         // [ring][n][2] (f_n, trigger count) granules
-  double* obj_trace;   // [max_iter]
-  double* cnt_trace;   // [max_iter] LAG uploads per iteration
-  long long* time_trace;  // [max_iter] s_memrealtime ticks since the monitor started
-  double* theta_out;   // [n][d]
+  u32x4* tab;          // this rank's [2][n][d] upload rows + [2][n] LAG upload flags (granules)
+  u32x4* part;         // [ring][n][2] (f_n, trigger count) granules: the MONITOR rank's ring
+  double* obj_trace;   // [max_iter] (monitor rank)
+  double* cnt_trace;   // [max_iter] LAG uploads per iteration (monitor rank)
+  long long* time_trace;  // [max_iter] s_memrealtime ticks since the monitor started (monitor rank)
+  double* theta_out;   // [n_local][d]
   FoCtl* ctl;
   u32x4* xchk;         // XCD packing: as PersistArgs::xchk / xcd (gadmm_chain.h)
   int xcd, pad_x;
+  // ---- several ranks (xGMI fabric; nranks == 1: one GPU, every field below at its one-GPU value).
+  // This rank runs workers w_lo .. w_lo + n_local - 1 (workgroup b = worker w_lo + b); the monitor
+  // workgroup (has_monitor, rank 0) follows them. Upload rows go to the tab of every rank that
+  // reads them (GD / LAG / IAG: every rank replicates the server step; DGD / dual averaging: the
+  // chain neighbours' ranks) with system-scope granule stores; f_n to the monitor's part ring; the
+  // monitor pushes its progress and stop words (wmon, wstop) into every rank.
+  int nranks, my_rank, w_lo, n_local;
+  int has_monitor, pad_m;
+  const int* owner;              // [n] rank of every worker (nranks > 1)
+  u32x4* const* tab_push;        // [nranks] every rank's tab (own included; nranks > 1)
+  int* wmon;                     // this rank's monitor-progress word (one GPU: &ctl->monitored)
+  int* wstop;                    // this rank's stop word (one GPU: &ctl->stop_iter)
+  int* const* wpush;             // [nranks] every rank's {wmon, wstop} pair (monitor, nranks > 1)
+  double* pushc;                 // optional [n_local][2]: rows / flag granules each worker pushed to OTHER ranks
 };

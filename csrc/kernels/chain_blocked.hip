@@ -165,6 +165,9 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   const int nseg = seg_hi - seg_lo + 1;
   const int W = (nseg + L - 1) / L;
   const int Wo = (nseg + MAXW - 1) / MAXW;
+  // data-local mode (PersistArgs::blk_dl): the computed ranges stop at this rank's segment edges, and
+  // a segment-edge position gets its other-rank neighbour's theta every phase through the theta ring
+  const bool dl = SYS && multi && a.blk_dl != 0;
   const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
   const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
   const __amdgpu_buffer_rsrc_t rtab = rsrc_of(a.blk_tab);
@@ -195,7 +198,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   // ---------------------------------------------------------------------- worker workgroup
   const int g = bid;
   const int s0 = seg_lo + g * L, e0 = min(seg_hi + 1, s0 + L) - 1;  // owned chain positions [s0, e0]
-  const int ra = max(0, s0 - H), rb = min(n - 1, e0 + H);
+  const int ra = max(dl ? seg_lo : 0, s0 - H), rb = min(dl ? seg_hi : n - 1, e0 + H);
   const int nv = rb - ra + 1;
   // Wave v computes local position u. Waves are dealt to the 4 SIMDs round-robin (v mod 4), so
   // v < MAXW/2 take the heads and the rest the tails: each phase keeps every SIMD busy with
@@ -216,10 +219,14 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   // Decision wave: polls the stop decision during the tail phase, when heads are idle. A halo head
   // is preferred: it never stores to global memory, so its decision load does not queue behind
   // write-through granule stores (vmcnt counts stores on gfx9).
+  // Next best: an idle wave (u >= nv: no position). A computed tail can never be it (it is busy in
+  // exactly the phase the poll runs in) -- a workgroup whose only position is a tail (one worker per
+  // rank, odd position) polls on an idle wave.
   int vdec = -1;
   for (int u = 0; u < nv && vdec < 0; ++u)
     if (((ra + u) % 2) == 0 && (ra + u < s0 || ra + u > e0)) vdec = u;
-  if (vdec < 0) vdec = (ra % 2 == 0 || nv < 2) ? 0 : 1;
+  if (vdec < 0 && nv < MAXW) vdec = nv;
+  if (vdec < 0) vdec = (ra % 2 == 0) ? 0 : 1;
   const bool dec_wave = u == vdec;
 
   double* thS = lds;                       // [MAXW][64] theta of every computed worker
@@ -229,6 +236,13 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   const double* thL = thS + (u > 0 ? u - 1 : u) * 64;
   const double* thR = thS + (u + 1 < nv ? u + 1 : u) * 64;
   const bool nbl = has_l && u > 0, nbr = has_r && u + 1 < nv;
+  // data-local segment edges: the neighbour beyond seg_lo / seg_hi is another rank's worker. It is
+  // never stale: its theta^j arrives in THIS rank's theta ring (row seg_lo - 1 / seg_hi + 1, slot
+  // j % ring, tag j), pushed there by its owner right after its solve; the owner of an edge position
+  // pushes its own theta^j into the neighbour rank's ring the same way (no mu, no shard crosses).
+  // (p == seg_lo implies u == 0 and p == seg_hi implies u == nv - 1, so nbl / nbr are false there.)
+  const bool rl = dl && has_l && p == seg_lo, rr = dl && has_r && p == seg_hi;
+  const bool rpush = owned && (rl || rr);
 
   double Mq[4][QT];
   quad_load<QT>(Mq, a.Minv + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)d * d, d, active);
@@ -282,6 +296,32 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   const int ring_p = (int)((ring_base + (long)(active ? p : 0) * d + lane) * 16);  // (slot 0, p, lane)
   const int ring_slot_bytes = n * d * 16;
   const bool ring_post = owned && in && !(TL && (a.dbg & 2));
+  const int ring_l = (int)((ring_base + (long)(rl ? p - 1 : 0) * d + lane) * 16);  // slot 0, row p - 1
+  const int ring_r = (int)((ring_base + (long)(rr ? p + 1 : 0) * d + lane) * 16);  // slot 0, row p + 1
+  const __amdgpu_buffer_rsrc_t rdl0 = rsrc_of(rl && a.dl_tab[0] ? (const void*)a.dl_tab[0] : (const void*)a.blk_tab);
+  const __amdgpu_buffer_rsrc_t rdl1 = rsrc_of(rr && a.dl_tab[1] ? (const void*)a.dl_tab[1] : (const void*)a.blk_tab);
+  // other-rank neighbours' theta^j (ring slot `slot`) into tl / tr; false on a deadline
+  auto poll_remote = [&](int slot, int j, double& tl, double& tr) -> bool {
+    const unsigned tag = make_tag(a.epoch, j);
+    const int so = slot * ring_slot_bytes;
+    for (int spin = 0;; ++spin) {
+      bool g0 = true;
+      if (in) {
+        if (rl) g0 &= load_granule<SYS>(rtab, ring_l + so, tag, &tl);
+        if (rr) g0 &= load_granule<SYS>(rtab, ring_r + so, tag, &tr);
+      }
+      if (__all(g0)) return true;
+      if ((spin & 7) == 7 && now_ticks() > deadline) return false;
+      GADMM_POLL_PAUSE();
+    }
+  };
+  // this edge position's theta^j into the neighbour ranks' rings (their row p, slot `slot`)
+  auto push_remote = [&](int slot, int j) {
+    const unsigned tag = make_tag(a.epoch, j);
+    const int off = ring_p + slot * ring_slot_bytes;
+    if (rl) store_granule<SYS>(rdl0, off, tag, th);
+    if (rr) store_granule<SYS>(rdl1, off, tag, th);
+  };
   bool ring_defer = false;
   int rslot = a.start_iter % a.ring;                  // == it % ring
   int dslot = (a.start_iter + 1 - a.lag) % a.ring;     // == (it + 1 - lag) % ring (>= 0 once polled)
@@ -387,7 +427,15 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     // ---- head phase
     const int slack = 2 * k - 1 - 2 * (it - blk0);  // head phase; the tail phase has slack - 1
     if (active && head && u >= uo_lo - slack && u <= uo_hi + slack) {
-      const double tl = nbl ? thL[lane] : 0.0, tr = nbr ? thR[lane] : 0.0;
+      double tl = nbl ? thL[lane] : 0.0, tr = nbr ? thR[lane] : 0.0;
+      if (rl || rr) {  // the other ranks' tails' theta^{it-1} (their initial theta at the first iteration)
+        if (it == a.start_iter) {
+          if (rl && in) tl = a.theta[(long)(p - 1) * d + lane];
+          if (rr && in) tr = a.theta[(long)(p + 1) * d + lane];
+        } else if (!poll_remote(rslot == 0 ? a.ring - 1 : rslot - 1, it - 1, tl, tr) && lane == 0) {
+          abort_lds = 1;
+        }
+      }
       double m = mu;
       if (pending) {  // lazy end-of-iteration dual (reference order)
         if (has_l) m = m - rho * (tl - th);
@@ -403,6 +451,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         asm volatile("" ::"v"(th));
         ts[7] = (long long)now_ticks();
       }
+      if (rpush && in) push_remote(rslot, it);  // first: the other rank's tail waits on it
       thS[u * 64 + lane] = th;
     }
     pending = 1;
@@ -418,7 +467,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     long long tt[4] = {0, 0, 0, 0};
     if (active && !head && u >= uo_lo - (slack - 1) && u <= uo_hi + (slack - 1)) {
       if (tstamp) tt[0] = (long long)now_ticks();
-      const double tl = nbl ? thL[lane] : 0.0, tr = nbr ? thR[lane] : 0.0;
+      double tl = nbl ? thL[lane] : 0.0, tr = nbr ? thR[lane] : 0.0;
+      if ((rl || rr) && !poll_remote(rslot, it, tl, tr) && lane == 0) abort_lds = 1;  // other ranks' heads' theta^it
       double r = bb - mu;
       if (has_l) r = r + rho * tl;
       if (has_r) r = r + rho * tr;
@@ -436,6 +486,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       if (has_r) m = m + rho * (tn - tr);
       mu = m;
       th = tn;
+      if (rpush && in) push_remote(rslot, it);  // first: the other rank's next head phase waits on it
       thS[u * 64 + lane] = th;
       if (owned && in && xnext) publish(it);
       ring_defer = ring_post;
@@ -839,6 +890,19 @@ int gadmm_chain_blocked_plan2(int n, int d, int want_k, int want_pw, int* k_out,
   return W;
 }
 
+// Plan of the data-local multi-GPU mode for a segment of nseg positions: one workgroup computing the
+// whole segment when it fits the 12 waves (no intra-rank exchange at all: k = 2^20 never comes), else
+// the one-GPU plan inside the segment (k = 2, owned runs of L, halos clipped at the segment edges).
+int gadmm_chain_blocked_plan_dl(int nseg, int d, int want_k, int* k_out, int* len_out) {
+  if (d > 52 || nseg < 1) return 0;
+  if (nseg <= MAXW) {
+    *k_out = 1 << 20;
+    *len_out = nseg;
+    return 1;
+  }
+  return gadmm_chain_blocked_plan(nseg, d, want_k, k_out, len_out);
+}
+
 long gadmm_chain_blocked_lds(int d, int len) {
   (void)d;
   (void)len;
@@ -856,7 +920,20 @@ int gadmm_xcd_mode(const PersistArgs* a, int blocks, long cap_total);  // chain_
 int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   const PersistArgs& a = *args;
   const bool multi = a.nranks > 1;
-  if (a.blk_k < 1 || a.blk_len < 1 || a.blk_len + 4 * a.blk_k > (a.blk_pw == 2 ? PCAP : MAXW) || a.d > 52 ||
+  const bool dl = a.blk_dl != 0;
+  if (dl) {  // data-local mode: SYS scope, 12-wave layout, static chain, every computed range within MAXW
+    const int nseg_dl = a.seg_hi - a.seg_lo + 1;
+    const int W_dl = nseg_dl > 0 && a.blk_len > 0 ? (nseg_dl + a.blk_len - 1) / a.blk_len : 0;
+    const long span = W_dl == 1 ? nseg_dl : (long)a.blk_len + 4L * a.blk_k;
+    if (!multi || !a.sys_scope || a.blk_pw != 1 || a.n_epochs != 0 || a.blk_npeer != 0 || a.blk_k < 1 ||
+        a.blk_len < 1 || nseg_dl < 1 || span > MAXW || (W_dl > 1 && a.ring < 2 * a.blk_k + 4) ||
+        (a.seg_lo > 0 && !a.dl_tab[0]) || (a.seg_hi < a.n - 1 && !a.dl_tab[1])) {
+      gadmm_set_error("blocked chain kernel (data-local): unsupported configuration (seg %d..%d, L=%d, k=%d)",
+                      a.seg_lo, a.seg_hi, a.blk_len, a.blk_k);
+      return -1;
+    }
+  }
+  if (a.blk_k < 1 || a.blk_len < 1 || (!dl && a.blk_len + 4 * a.blk_k > (a.blk_pw == 2 ? PCAP : MAXW)) || a.d > 52 ||
       !a.blk_tab || !a.dec_push ||
       (!multi && (!a.has_monitor || a.n != a.n_local)) ||
       (multi && (a.seg_lo < 0 || a.seg_hi < a.seg_lo || a.seg_hi >= a.n || a.blk_npeer < 0 || a.blk_npeer > 8 ||

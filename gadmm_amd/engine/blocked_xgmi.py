@@ -1,20 +1,27 @@
 """Temporally blocked GADMM across GPUs (one process per GPU, xGMI fabric).
 
-Each rank owns a contiguous chain segment [seg_lo, seg_hi] and runs ``chain_blocked_kernel<SYS>``:
-its workgroups compute the segment plus a halo of H = 2k positions on each side (the halo workers'
-Gram / inverse are computed locally from their shards), and every k iterations each rank pushes the
-(theta, mu) of its owned workers straight into the exchange tables of the peer GPUs whose computed
-range contains them (IPC-mapped fine-grained memory, system-scope granule stores over xGMI). A
-cross-GPU hand-off therefore happens once per k iterations instead of twice per iteration.
+Each rank owns a contiguous chain segment [seg_lo, seg_hi] and runs ``chain_blocked_kernel<SYS>``
+(csrc/kernels/chain_blocked.hip). Two modes:
+
+* ``data_local=True`` (the multi-GPU default, ``engine/multigpu.py``): the rank holds ONLY its own
+  workers' shards. Its workgroups compute its segment, temporally blocked inside it exactly as on one
+  GPU (one workgroup for the whole segment when it fits 12 waves, else owned runs + halos clipped at
+  the segment edges, one intra-rank exchange per k iterations). The two positions at the segment
+  edges exchange theta with the neighbouring ranks' edge positions every phase -- the owner pushes
+  theta^j into the neighbour GPU's theta ring right after its solve, the reader polls its own ring --
+  which is the reference's exchange (group_ADMM_closedForm.m:18-27, 62-70): theta only, d doubles per
+  boundary per phase, no mu, no shard. Payload per solve: 2 (ranks - 1) d 8 B per iteration.
+* ``data_local=False`` (opt-in ``--engine replicated-halo``): the workgroups also compute a halo of
+  H = 2k positions of the neighbouring ranks (whose Gram / inverse come from their shards, held
+  here: ``replicated_shard_bytes``) and every k iterations each rank pushes the (theta, mu) of its
+  owned workers into the exchange tables of the peers whose computed range contains them: one
+  cross-GPU hand-off per k iterations instead of two per iteration, at the price of the shards.
+
 Objective waves on every rank evaluate f_n of the owned workers and push them to rank 0's monitor
 ring; rank 0's monitor pushes the stop decision into every rank's ring (as in the per-worker fabric,
 parallel/xgmi.py). Hand-offs are tagged granules salted per solve, so correctness never depends on
 timing; every spin has a deadline and a stalled peer surfaces as ``done == 4`` (callers fall back).
-
-Identity chain (the static GADMM of the headline benchmark). NOT data-local: the halo workers' shards
-must be on the rank too (``replicated_shard_bytes``), and (theta, mu) travel instead of theta alone, so
-``bench.py`` runs it only on request (``--engine replicated-halo``); the data-local default is the
-per-worker persistent kernel on ``parallel/xgmi.py``.
+Identity chain (the static GADMM of the headline benchmark).
 """
 from __future__ import annotations
 
@@ -27,7 +34,7 @@ import torch.distributed as dist
 from ..ops import native
 from ..ops.linalg import gram, spd_inverse
 from ..parallel.topology import Placement
-from ..parallel.xgmi import _Buf
+from ..parallel.xgmi import _Buf, preflight
 
 
 class BlockedXgmiEngine:
@@ -35,25 +42,36 @@ class BlockedXgmiEngine:
 
     def __init__(self, X_all: torch.Tensor, y_all: torch.Tensor, n_total: int, placement: Placement, rank: int,
                  rho: float, obj0: float, tol: float, max_iter: int, device: torch.device, group=None,
-                 want_k: int = 0):
-        """Collective over ``group``. ``X_all`` / ``y_all``: the shards of at least this rank's
-        computed range (indexable by global worker id); only those rows are read."""
+                 want_k: int = 0, data_local: bool = False):
+        """Collective over ``group``. ``data_local=False``: ``X_all`` / ``y_all`` hold the shards of at
+        least this rank's computed range (indexable by global worker id); only those rows are read.
+        ``data_local=True``: ``X_all`` / ``y_all`` are this rank's own shards, in segment order."""
         self.lib = native.require()
         self.rank, self.nranks, self.device = rank, placement.nranks, device
         self.n, self.d = int(n_total), int(X_all.shape[2])
         self.rho, self.obj0, self.tol, self.max_iter = float(rho), float(obj0), float(tol), int(max_iter)
+        self.data_local = bool(data_local)
         mine = placement.local_workers(rank)
         self.seg_lo, self.seg_hi = min(mine), max(mine)
         if mine != list(range(self.seg_lo, self.seg_hi + 1)):
             raise ValueError("blocked xgmi engine needs contiguous segments")
         segs = [(min(placement.local_workers(r)), max(placement.local_workers(r))) for r in range(self.nranks)]
-        nseg = max(hi - lo + 1 for lo, hi in segs)
-        kk, ll, pp = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
-        if int(self.lib.gadmm_chain_blocked_plan2(nseg, self.d, int(want_k), 0, ctypes.byref(kk), ctypes.byref(ll),
-                                                  ctypes.byref(pp))) <= 0:
-            raise RuntimeError("blocked xgmi engine: no blocking plan for d=%d" % self.d)
+        kk, ll, pp = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(1)
+        if self.data_local:
+            nseg = self.seg_hi - self.seg_lo + 1
+            if int(X_all.shape[0]) != nseg:
+                raise ValueError("data-local blocked engine: %d shards for a %d-position segment"
+                                 % (int(X_all.shape[0]), nseg))
+            if int(self.lib.gadmm_chain_blocked_plan_dl(nseg, self.d, int(want_k), ctypes.byref(kk),
+                                                        ctypes.byref(ll))) <= 0:
+                raise RuntimeError("data-local blocked engine: no plan for d=%d, %d positions" % (self.d, nseg))
+        else:
+            nseg = max(hi - lo + 1 for lo, hi in segs)
+            if int(self.lib.gadmm_chain_blocked_plan2(nseg, self.d, int(want_k), 0, ctypes.byref(kk), ctypes.byref(ll),
+                                                      ctypes.byref(pp))) <= 0:
+                raise RuntimeError("blocked xgmi engine: no blocking plan for d=%d" % self.d)
         self.k, self.L, self.pw = kk.value, ll.value, pp.value
-        H = 2 * self.k
+        H = 0 if self.data_local else 2 * self.k
         self.H = H
         comp = [(max(0, lo - H), min(self.n - 1, hi + H)) for lo, hi in segs]
         self.ext_lo, self.ext_hi = comp[rank]
@@ -61,8 +79,12 @@ class BlockedXgmiEngine:
         torch.cuda.set_device(device)
         f64 = torch.float64
         ext = list(range(self.ext_lo, self.ext_hi + 1))
-        self.X = X_all[ext].to(device).contiguous()
-        self.y = y_all[ext].to(device).contiguous()
+        if self.data_local:
+            self.X = X_all.to(device).contiguous()
+            self.y = y_all.to(device).contiguous()
+        else:
+            self.X = X_all[ext].to(device).contiguous()
+            self.y = y_all[ext].to(device).contiguous()
         self.stream = torch.cuda.Stream(device)
         with torch.cuda.stream(self.stream):
             self.A, self.b, self.yy = gram(self.X, self.y)
@@ -92,16 +114,36 @@ class BlockedXgmiEngine:
         except Exception as e:  # pragma: no cover - box dependent
             err = "rank %d alloc: %s" % (rank, e)
         allh = [None] * self.nranks
-        dist.all_gather_object(allh, (h, err), group=group)
-        errs = [e for _, e in allh if e]
+        dist.all_gather_object(allh, (h, err, torch.cuda.current_device()), group=group)
+        errs = [e for _, e, _ in allh if e]
+        devs = [dv for _, _, dv in allh]
         ok = not errs
         self.peers: List[int] = []
         self.peer_ranges = []
         self.peer_ptrs: List[int] = []
+        self.dl_ranks = [-1, -1]  # data-local: the ranks owning seg_lo - 1 / seg_hi + 1
+        self.dl_ptrs = [0, 0]
+        if self.data_local:
+            owner = placement.owner
+            if self.seg_lo > 0:
+                self.dl_ranks[0] = int(owner[self.seg_lo - 1])
+            if self.seg_hi < self.n - 1:
+                self.dl_ranks[1] = int(owner[self.seg_hi + 1])
         if ok:
             try:
+                touch = {q for q in self.dl_ranks if q >= 0} | ({0} if rank != 0 else set(range(self.nranks)))
+                if not self.data_local:
+                    touch |= {q for q in range(self.nranks)
+                              if comp[q][1] >= self.seg_lo and comp[q][0] <= self.seg_hi}
+                why = preflight(torch.cuda.current_device(), {q: devs[q] for q in touch if q != rank})
+                if why:
+                    raise RuntimeError("peer access pre-flight: " + why)
+                for side, q in enumerate(self.dl_ranks):
+                    if q >= 0:
+                        self.dl_ptrs[side] = self._open(allh[q][0][0], ("tab", q)) if ("tab", q) not in self.opened \
+                            else self.opened[("tab", q)].value
                 for q in range(self.nranks):
-                    if q == rank:
+                    if q == rank or self.data_local:
                         continue
                     lo, hi = comp[q]
                     if hi >= self.seg_lo and lo <= self.seg_hi:  # q computes some of my positions
@@ -124,7 +166,13 @@ class BlockedXgmiEngine:
         self.peer_tab_t = torch.tensor(self.peer_ptrs + [0], dtype=torch.int64, device=device)
         self.dec_push_t = torch.tensor(self.dec_all, dtype=torch.int64, device=device)
         self.epoch = 0
-        self.last_kernel = "blocked-xgmi(k=%d,L=%d,H=%d,pw=%d,peers=%s)" % (self.k, self.L, H, self.pw, self.peers)
+        if self.data_local:
+            W = (self.seg_hi - self.seg_lo + self.L) // self.L
+            self.last_kernel = "blocked-dl(k=%s,L=%d,W=%d,nbr=%s)" % ("inf" if W == 1 else self.k, self.L, W,
+                                                                      self.dl_ranks)
+        else:
+            self.last_kernel = "blocked-xgmi(k=%d,L=%d,H=%d,pw=%d,peers=%s)" % (self.k, self.L, H, self.pw,
+                                                                                self.peers)
 
     def _open(self, hbytes: bytes, key) -> int:
         p = ctypes.c_void_p()
@@ -174,6 +222,8 @@ class BlockedXgmiEngine:
         for i, (lo, hi) in enumerate(self.peer_ranges):
             pa.blk_peer_lo[i], pa.blk_peer_hi[i] = lo, hi
         pa.blk_peer_tab = self.peer_tab_t.data_ptr()
+        pa.blk_dl = 1 if self.data_local else 0
+        pa.dl_tab[0], pa.dl_tab[1] = self.dl_ptrs[0] or None, self.dl_ptrs[1] or None
         with torch.cuda.stream(self.stream):
             self.theta.zero_()
             self.mu.zero_()
@@ -190,7 +240,11 @@ class BlockedXgmiEngine:
 
     def exchange_bytes_per_solve(self, iters: int) -> int:
         """Payload this rank pushes over xGMI per solve (8 B per double; the granules on the wire carry
-        16 B): every k iterations, (theta, mu) of each owned worker that a peer computes, to that peer."""
+        16 B). Data-local: theta of each segment-edge worker to its other-rank neighbour, once per
+        iteration (iterations 1..iters). Replicated halo: every k iterations, (theta, mu) of each owned
+        worker that a peer computes, to that peer."""
+        if self.data_local:
+            return sum(1 for q in self.dl_ranks if q >= 0) * self.d * 8 * iters
         pushes = sum(1 for lo, hi in self.peer_ranges for p in range(self.seg_lo, self.seg_hi + 1) if lo <= p <= hi)
         return pushes * 2 * self.d * 8 * (iters // self.k)
 
@@ -203,6 +257,8 @@ class BlockedXgmiEngine:
 
     def replicated_shard_bytes(self) -> int:
         """Bytes of OTHER ranks' shards this rank holds for its halo (X and y of the halo workers)."""
+        if self.data_local:
+            return 0
         halo = (self.ext_hi - self.ext_lo + 1) - (self.seg_hi - self.seg_lo + 1)
         return halo * int(self.X.shape[1]) * (self.d + 1) * 8
 

@@ -5,10 +5,14 @@ Data-local by construction: the solver is given only this rank's shards (``X_loc
 theta, to the ranks of its chain neighbours (group_ADMM_closedForm.m:18-27, 62-70). Engines, in the
 order ``engine="auto"`` tries them:
 
-1. ``xgmi`` -- the per-worker persistent kernel (chain_persistent.hip, SYS scope): one workgroup per
+1. ``xgmi(blocked-dl)`` -- the temporally blocked kernel run inside each rank's segment
+   (chain_blocked.hip, data-local mode, engine/blocked_xgmi.py): the segment's intra-rank hand-offs
+   are LDS barriers (one workgroup when the segment fits 12 waves) as on one GPU, and only the two
+   segment-edge workers exchange theta with the neighbouring ranks, every phase, over xGMI.
+2. ``xgmi`` -- the per-worker persistent kernel (chain_persistent.hip, SYS scope): one workgroup per
    local worker, boundary theta stored straight into the neighbour GPU's table over xGMI, objective
    granules to rank 0's monitor, decisions fanned back out. One launch per solve.
-2. ``rccl`` / ``ipc`` -- the graph-replayed phase kernels (chain_engine.cpp) with RCCL send/recv, or
+3. ``rccl`` / ``ipc`` -- the graph-replayed phase kernels (chain_engine.cpp) with RCCL send/recv, or
    with the device-copy transport (parallel/ipc.py; the only option when ranks share one GPU).
 
 Every choice is agreed by all ranks (an all-reduce of a success flag), and so is every fallback: a
@@ -78,9 +82,11 @@ class DistributedChainSolver:
             self.replicated_bytes = self.blk.replicated_shard_bytes()
             self.persistent, self.kind = True, "xgmi(replicated-halo)"
         else:
-            if fabric in ("auto", "xgmi") and engine != "graph":
+            if fabric in ("auto", "xgmi") and engine in ("auto", "persistent", "blocked-dl"):
+                self._try_blocked_dl()
+            if self.blk is None and fabric in ("auto", "xgmi") and engine in ("auto", "persistent", "per-worker"):
                 self._try_xgmi()
-            if self.eng is None:
+            if self.eng is None and self.blk is None:
                 self._graph_engine()
 
     # ---------------------------------------------------------------------------------------------
@@ -89,6 +95,23 @@ class DistributedChainSolver:
                       max_iter=self.max_iter, comm=comm, block=self.block)
         e.set_path(self.path, self.placement, self.rank)
         return e
+
+    def _try_blocked_dl(self):
+        """Collective: the data-local blocked kernel over the xGMI fabric, if every rank can run it."""
+        from .blocked_xgmi import BlockedXgmiEngine
+
+        lo, hi = min(self.local), max(self.local)
+        eligible = self.local == list(range(lo, hi + 1)) and self.d <= 52 and self.n >= 2
+        if not all_ok(eligible, self.world):
+            return
+        try:
+            blk = BlockedXgmiEngine(self.X, self.y, self.n, self.placement, self.rank, self.rho, self.obj0, self.tol,
+                                    self.max_iter, self.device, data_local=True)
+        except Exception as e:  # collective inside the constructor: every rank raises together
+            if self.rank == 0:
+                print("DistributedChainSolver: data-local blocked fabric unavailable (%s)" % e, file=sys.stderr)
+            return
+        self.blk, self.persistent, self.kind = blk, True, "xgmi(blocked-dl)"
 
     def _try_xgmi(self):
         from ..parallel.comm import RankInfo
@@ -128,7 +151,7 @@ class DistributedChainSolver:
         self.persistent = False
 
     def fall_back(self, why: str):
-        """Collective: every rank drops the persistent kernel for the graph engine."""
+        """Collective: every rank drops the persistent kernels for the graph engine."""
         self.fallbacks.append(why)
         if self.blk is not None:
             self.blk.close()
@@ -150,6 +173,8 @@ class DistributedChainSolver:
         if self.blk is not None:
             self.blk.refresh()
             it, done, _ = self.blk.run(timeout_s=self.timeout_s)
+            if done == 4:
+                raise RuntimeError("blocked kernel: a hand-off timed out")
             pay = self.blk.exchange_bytes_per_solve(it)
             return SolveOut(it, done, pay, 2 * pay, self.blk.monitor_bytes_per_solve(it))
         self.eng.refresh(self.X, self.y)

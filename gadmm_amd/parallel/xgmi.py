@@ -67,15 +67,20 @@ class XgmiFabric:
         except Exception as e:
             err = "rank %d alloc: %s" % (rank, e)
         allh = [None] * nranks
-        dist.all_gather_object(allh, (mine, err), group=group)
-        errs = [e for _, e in allh if e]
+        dist.all_gather_object(allh, (mine, err, torch.cuda.current_device()), group=group)
+        errs = [e for _, e, _ in allh if e]
         if errs:
             self.close()
             raise RuntimeError("xgmi fabric: " + "; ".join(errs))
-        allh = [h for h, _ in allh]
+        devs = [dv for _, _, dv in allh]
+        allh = [h for h, _, _ in allh]
         ok = True
         try:
             need_thg = set(peers_needed if peers_needed is not None else [r for r in range(nranks) if r != rank])
+            touch = set(need_thg) | ({0} if rank != 0 else set(range(nranks)))  # + the monitor's / decision rings
+            why = preflight(torch.cuda.current_device(), {r: devs[r] for r in touch if r != rank})
+            if why:
+                raise RuntimeError("peer access pre-flight: " + why)
             self.thg_peer: Dict[int, int] = {}
             for r in need_thg:
                 self.thg_peer[r] = self._open(allh[r][0], ("thg", r))
@@ -122,9 +127,25 @@ class XgmiFabric:
 
 
 def peer_access_ok(nranks: int) -> bool:
+    """Every pair of the first ``nranks`` devices can access each other (hipDeviceCanAccessPeer)."""
     lib = native.require()
     n = torch.cuda.device_count()
     if n < 2:
         return True
     return all(lib.gadmm_device_can_access_peer(i, j) == 1 for i in range(min(n, nranks)) for j in range(min(n, nranks))
                if i != j)
+
+
+def preflight(my_dev: int, peer_devs: Dict[int, int]) -> str:
+    """Pre-flight of the IPC / xGMI mappings a rank is about to open: every peer rank's device must
+    be reachable from this rank's device (hipDeviceCanAccessPeer) before ``hipIpcOpenMemHandle``
+    (which would otherwise fail -- or worse, map -- on a box without the link). Ranks sharing this
+    rank's device (the one-GPU rehearsal) need no peer access. Returns '' or the reason."""
+    lib = native.require()
+    bad = []
+    for r, dv in sorted(peer_devs.items()):
+        if dv == my_dev:
+            continue
+        if int(lib.gadmm_device_can_access_peer(my_dev, dv)) != 1:
+            bad.append("rank %d (device %d)" % (r, dv))
+    return ("device %d cannot access %s" % (my_dev, ", ".join(bad))) if bad else ""

@@ -4,7 +4,9 @@
   code -- chain plans, ghost rows, the per-worker objective ring, the block-end monitor, D-GADMM
   re-plans, logistic across ranks -- bit-identical to one rank (RCCL refuses two ranks per device,
   so only the ncclSend/ncclRecv/ncclAllReduce calls themselves are not exercised here);
-* the data-local multi-GPU default (per-worker persistent kernel on the xGMI fabric): exact bytes;
+* the data-local multi-GPU engines on the xGMI fabric (the default: the blocked kernel inside each
+  rank's segment with per-phase edge exchanges; the per-worker persistent kernel): exact bytes,
+  bit-identical traces;
 * multi-rank D-GADMM in one persistent launch per GPU;
 * residency checks and the collective fallback after a stalled peer.
 """
@@ -225,7 +227,7 @@ def test_dgadmm_multirank_matches_one_gpu(world, mode, chunk, lin24):
 
 
 # ------------------------------------------------------------------------------------------------
-def _solver_rank(rank, world, n, delay_rank, timeout_s):
+def _solver_rank(rank, world, n, delay_rank, timeout_s, engine="auto"):
     import torch
     from gadmm_amd.benchmarks import headline_rank_problem
     from gadmm_amd.engine.multigpu import DistributedChainSolver
@@ -233,29 +235,37 @@ def _solver_rank(rank, world, n, delay_rank, timeout_s):
     torch.cuda.set_device(dev)
     X, y, loc, pl, obj0 = headline_rank_problem(n, rank, world)
     sol = DistributedChainSolver(X.to(dev), y.to(dev), loc, n, pl, rank, world, dev, 3.0, obj0, 1e-8, share=True,
-                                 timeout_s=timeout_s)
+                                 timeout_s=timeout_s, engine=engine)
     kind0 = sol.kind
     if rank == delay_rank:
         sol.delay_next_s = 3.0 * timeout_s  # this rank's kernel starts long after its peers gave up
     outs = [sol.solve_agreed() for _ in range(2)]
-    res = {"kind0": kind0, "kind": sol.kind, "fallbacks": sol.fallbacks, "local": loc,
+    res = {"kind0": kind0, "kind": sol.kind, "fallbacks": sol.fallbacks, "local": loc, "kernel": sol.kernel,
+           "replicated": sol.replicated_bytes,
            "outs": [(o.iters, o.done, o.theta_bytes, o.wire_bytes, o.monitor_bytes) for o in outs],
            "trace": sol.objective_trace(outs[-1].iters).tolist() if rank == 0 else None}
     sol.close()
     return res
 
 
-@pytest.mark.parametrize("world,n", [(2, 24), (4, 24), (4, 8), (8, 8)])
-def test_data_local_xgmi_default_exact_bytes(world, n, lin24):
-    """The multi-GPU default: per-worker persistent kernel, each rank holding only its shards and
-    shipping only theta. Payload == 2 (N_ranks - 1) d 8 iters exactly; wire == 2 x payload (16-B
-    granules); iterations and trace == one GPU. n = 8 on 8 ranks: each GPU is one worker."""
+@pytest.mark.parametrize("world,n,engine", [(2, 24, "auto"), (4, 24, "auto"), (8, 24, "auto"), (4, 8, "auto"),
+                                             (8, 8, "auto"), (2, 24, "per-worker"), (4, 8, "per-worker")])
+def test_data_local_xgmi_default_exact_bytes(world, n, engine, lin24):
+    """The multi-GPU engines, each rank holding only its shards and shipping only theta: the default
+    (auto) = the temporally blocked kernel inside every rank's segment, edge workers exchanging theta
+    every phase; per-worker = the one-workgroup-per-worker kernel. Payload == 2 (N_ranks - 1) d 8
+    iters exactly; wire == 2 x payload (16-B granules); iterations and trace == one GPU, bit for bit.
+    n = 8 on 8 ranks: each GPU is one worker (both of its neighbours on other GPUs)."""
     from gadmm_amd.parallel.launch import spawn
     from gadmm_amd.benchmarks import EXPECTED_ITERS_1E8
-    res = spawn(_solver_rank, world, n, -1, 20.0, timeout=300)
+    res = spawn(_solver_rank, world, n, -1, 20.0, engine, timeout=300)
     it = EXPECTED_ITERS_1E8[(n, 3.0)]
+    want = "xgmi(blocked-dl)" if engine == "auto" else "xgmi"
     for r in res:
-        assert r["kind0"] == "xgmi" and r["kind"] == "xgmi" and not r["fallbacks"]
+        assert r["kind0"] == want and r["kind"] == want and not r["fallbacks"], (r["kind0"], r["fallbacks"])
+        assert r["replicated"] == 0
+        if engine == "auto":
+            assert r["kernel"].startswith("blocked-dl(")
         for o in r["outs"]:
             assert o[0] == it and o[1] == 1
     pay = sum(r["outs"][-1][2] for r in res)
@@ -273,7 +283,7 @@ def test_stalled_peer_every_rank_falls_back_together():
     from gadmm_amd.parallel.launch import spawn
     res = spawn(_solver_rank, 2, 24, 1, 2.0, timeout=300)
     for r in res:
-        assert r["kind0"] == "xgmi" and r["kind"] == "ipc"
+        assert r["kind0"] == "xgmi(blocked-dl)" and r["kind"] == "ipc"
         assert len(r["fallbacks"]) == 1
         assert [o[:2] for o in r["outs"]] == [(1373, 1), (1373, 1)]
 
