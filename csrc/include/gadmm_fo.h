@@ -19,7 +19,10 @@ struct FoCtl {
 struct FoArgs {
   int alg, model, n, d, m, max_iter, faithful, jacobi, has_tol, ring;
   unsigned epoch;
-  int pad_;
+  int slots;      // upload-row slots of the table (row of iteration j in slot j % slots): 2 for the
+                  // algorithms whose readers move in lock-step (every iteration reads every worker's
+                  // row or flag, or the chain neighbours'), ring + 3 for IAG (one upload per iteration:
+                  // a fast worker may lead a slow reader by up to `ring` + 1 iterations)
   double step;    // GD/LAG: 1/Hmax_all; DGD: step/100; IAG: step/N; dual averaging: alpha
   double lam;     // ridge inside f_n and grad f_n (logistic lambda; 0 for the linear reference)
   double obj0, tol;
@@ -32,7 +35,7 @@ struct FoArgs {
   const double* Y;     // logistic: (n_local, m) labels +-1
   const double* hsq;   // LAG-PS: Hmax_n^2 of EVERY worker (n)
   const int* sched;    // IAG: refreshing worker of iteration it at sched[it - 1]
-  u32x4* tab;          // this rank's [2][n][d] upload rows + [2][n] LAG upload flags (granules)
+  u32x4* tab;          // this rank's [slots][n][d] upload rows + [2][n] LAG upload flags (granules)
   u32x4* part;         // [ring][n][2] (f_n, trigger count) granules: the MONITOR rank's ring
   double* obj_trace;   // [max_iter] (monitor rank)
   double* cnt_trace;   // [max_iter] LAG uploads per iteration (monitor rank)

@@ -12,14 +12,11 @@
 #include "gadmm_common.h"
 #include "gadmm_chain.h"
 #include "chain_device.h"
+#include "big_gemv.h"
 
 namespace {
 
-constexpr int NT = 256;
-constexpr int RPW = 2;               // rows per wave
-constexpr int ROWS_PER_WG = RPW * (NT / 64);
-
-__device__ __forceinline__ long rstride(int d) { return (long)d + (d + ROWS_PER_WG - 1) / ROWS_PER_WG + 1; }
+using namespace biggemv;
 
 struct SlotView {
   int li, gid, left, right, deg;
@@ -29,38 +26,6 @@ __device__ __forceinline__ SlotView slot_view(const PhaseArgs& a, int s) {
   const PhaseSlot sl = a.slots[s];
   SlotView v{sl.li, sl.gid, sl.left, sl.right, (sl.left >= 0) + (sl.right >= 0)};
   return v;
-}
-
-// y[row] = sum_j M[row][j] x[j] for RPW consecutive rows per wave; returns sums on lane 0.
-__device__ __forceinline__ void wave_rows_dot(const double* __restrict__ M, const double* __restrict__ x, int d,
-                                              int row0, double (&out)[RPW]) {
-  const int lane = threadIdx.x & 63;
-  double acc[RPW];
-#pragma unroll
-  for (int r = 0; r < RPW; ++r) acc[r] = 0.0;
-  if ((d & 1) == 0) {
-    const double2* x2 = reinterpret_cast<const double2*>(x);
-    const int d2 = d >> 1;
-    for (int j = lane; j < d2; j += 64) {
-      const double2 xv = x2[j];
-#pragma unroll
-      for (int r = 0; r < RPW; ++r) {
-        if (row0 + r < d) {
-          const double2 mv = reinterpret_cast<const double2*>(M + (long)(row0 + r) * d)[j];
-          acc[r] = fma(mv.x, xv.x, fma(mv.y, xv.y, acc[r]));
-        }
-      }
-    }
-  } else {
-    for (int j = lane; j < d; j += 64) {
-      const double xv = x[j];
-#pragma unroll
-      for (int r = 0; r < RPW; ++r)
-        if (row0 + r < d) acc[r] = fma(M[(long)(row0 + r) * d + j], xv, acc[r]);
-    }
-  }
-#pragma unroll
-  for (int r = 0; r < RPW; ++r) out[r] = wave_sum_f64(acc[r]);
 }
 
 }  // namespace

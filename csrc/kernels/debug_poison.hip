@@ -88,3 +88,9 @@ int gadmm_poison_buffer(void* p, long bytes, hipStream_t st) {
 }
 
 }  // extern "C"
+
+extern "C" int gadmm_memset_async(void* p, int v, long bytes, hipStream_t st) {
+  if (!p || bytes <= 0) return 0;
+  GADMM_CHECK(hipMemsetAsync(p, v, (size_t)bytes, st));
+  return 0;
+}

@@ -13,9 +13,13 @@ Realisation on the fabric:
 * cIAG / RIAG: one worker refreshes per iteration and uploads its row to the server. RIAG's draw
   uses an RNG seeded identically on every rank (no message).
 
-Single GPU: when every worker lives on one CUDA device (one rank) and d <= 128, each algorithm
-runs as ONE persistent kernel launch (``engine/first_order.py``, ``csrc/kernels/first_order.hip``);
-``backend="torch"`` forces the implementation below (the multi-rank path and the test oracle).
+Native: when the workers live on GPUs and d <= 128, each algorithm runs as ONE persistent kernel
+launch per GPU (``engine/first_order.py``, ``csrc/kernels/first_order.hip``): one rank, or several
+ranks (contiguous segments) over the xGMI fabric, where every upload is a device-initiated push into
+the reading GPUs (the replicated server's table on every rank; LAG's conditional uploads announced by
+a one-granule flag; DGD rows to the chain neighbours' ranks) and the returned ``bytes_sent`` is the
+exact payload that crossed between GPUs. ``backend="torch"`` forces the implementation below (the
+test oracle, and the path for CPU ranks / non-contiguous placements).
 
 Faithful quirks (SURVEY.md §5, ``faithful=True``): gradients start as ``ones`` (GD_DGD_LAG.m:44-67);
 LAG-PS refreshes worker 1 every iteration (timing side effect, :204-209); LAG does nothing before
@@ -97,18 +101,19 @@ def _gather_hmax(ctx: _Ctx, hmax_local: torch.Tensor) -> torch.Tensor:
     return ctx.allsum(full)
 
 
-def _fo_engine(ctx: _Ctx, backend: str):
-    """The persistent first-order engine when this run can use it (None -> torch path)."""
+def _fo_engine(ctx: _Ctx, backend: str, alg: str = "GD"):
+    """The persistent first-order engine when this run can use it (None -> torch path). Collective
+    on several ranks (the eligibility is agreed)."""
     if backend == "torch":
         return None
     from ..engine.first_order import FirstOrderEngine
 
-    ok = FirstOrderEngine.eligible(ctx.model, ctx.comm, ctx.n_total)
+    ok = FirstOrderEngine.eligible(ctx.model, ctx.comm, ctx.n_total, ctx.local_ids, ctx.placement, alg)
     if not ok:
         if backend == "native":
-            raise RuntimeError("native first-order engine needs one rank on a GPU with d <= 128")
+            raise RuntimeError("native first-order engine needs GPU ranks with contiguous segments and d <= 128")
         return None
-    return FirstOrderEngine.get(ctx.model)
+    return FirstOrderEngine.get(ctx.model, ctx.comm, ctx.placement, ctx.n_total)
 
 
 def _native_result(name, out, obj0, units, **extra) -> RunResult:
@@ -116,8 +121,10 @@ def _native_result(name, out, obj0, units, **extra) -> RunResult:
     n = len(obj)
     return RunResult(algorithm=name, obj=obj, loss=np.abs(obj - obj0), iters=out["iters"] if out["converged"] else n,
                      converged=out["converged"], wall_s=float(out["times"][-1]) if n else 0.0,
-                     time_trace=out["times"], comm_units=units, bytes_sent=0, bytes_total=0,
-                     extra=dict(extra, engine="native-persistent"))
+                     time_trace=out["times"], comm_units=units, bytes_sent=int(out.get("payload_bytes", 0)),
+                     bytes_total=int(out.get("payload_bytes", 0)),
+                     extra=dict(extra, engine="native-persistent", rows_pushed=out.get("rows_pushed", 0),
+                                flags_pushed=out.get("flags_pushed", 0), wire_bytes=out.get("wire_bytes", 0)))
 
 
 def _result(name, stop: Stopper, ctx: _Ctx, units: np.ndarray, converged: bool, iters: int, **extra):
@@ -132,7 +139,7 @@ def _result(name, stop: Stopper, ctx: _Ctx, units: np.ndarray, converged: bool, 
 def gradient_descent(model, local_ids, n_total, num_iter, obj0, stepsize, comm=None, placement=None,
                      faithful=True, tol: Optional[float] = None, backend: str = "auto") -> RunResult:
     ctx = _Ctx(model, local_ids, n_total, comm, placement)
-    eng = _fo_engine(ctx, backend)
+    eng = _fo_engine(ctx, backend, "GD")
     if eng is not None:
         out = eng.run("GD", num_iter, stepsize, obj0, tol, faithful)
         n = len(out["obj"])
@@ -168,7 +175,7 @@ def decentralized_gd(model, local_ids, n_total, num_iter, obj0, stepsize, comm=N
                      faithful=True, tol: Optional[float] = None, backend: str = "auto") -> RunResult:
     """DGD (GD_DGD_LAG.m:124-180): step stepsize/100 on the chain-neighbour average of gradients."""
     ctx = _Ctx(model, local_ids, n_total, comm, placement)
-    eng = _fo_engine(ctx, backend)
+    eng = _fo_engine(ctx, backend, "DGD")
     if eng is not None:
         out = eng.run("DGD", num_iter, stepsize / 100.0, obj0, tol, faithful)
         n = len(out["obj"])
@@ -279,7 +286,7 @@ def lag(model, local_ids, n_total, num_iter, obj0, stepsize, hmax_full: torch.Te
     d, dev = ctx.d, ctx.dev
     N = n_total
     thrd = (10.0 if variant == "PS" else 1.0) / (stepsize ** 2 * N ** 2) / TRIGGERSLOT
-    eng = _fo_engine(ctx, backend)
+    eng = _fo_engine(ctx, backend, "LAG-" + variant)
     if eng is not None:
         out = eng.run("LAG-" + variant, num_iter, stepsize, obj0, tol, faithful, thrd=thrd,
                       hsq=hmax_full.to(dev, torch.float64) ** 2)
@@ -371,7 +378,7 @@ def iag(model, local_ids, n_total, num_iter, obj0, stepsize, mode: str = "cyclic
     ctx = _Ctx(model, local_ids, n_total, comm, placement)
     name = "cIAG" if mode == "cyclic" else "R-IAG"
     sched = iag_schedule(n_total, num_iter, mode, hmax_full, seed)
-    eng = _fo_engine(ctx, backend)
+    eng = _fo_engine(ctx, backend, "IAG")
     if eng is not None:
         out = eng.run("IAG", num_iter, stepsize / n_total, obj0, tol, faithful, sched=sched)
         n = len(out["obj"])

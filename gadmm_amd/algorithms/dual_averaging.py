@@ -9,8 +9,9 @@ sees the left neighbour's *current* Z and the right neighbour's *previous* Z —
 wavefront. On several ranks this becomes a pipeline: rank r waits for Z of the last worker of rank
 r-1 from the current sweep and uses Z of the first worker of rank r+1 from the previous sweep
 (SURVEY.md C8). ``jacobi=True`` offers the documented parallel variant (all neighbours' previous Z).
-One rank on a GPU: the whole run is one persistent kernel (``engine/first_order.py``), where the
-wavefront is realised directly between worker workgroups.
+On GPUs the whole run is one persistent kernel per GPU (``engine/first_order.py``), where the
+wavefront is realised directly between worker workgroups (across GPUs: device-initiated Z pushes
+into the neighbour rank's table over xGMI).
 """
 from __future__ import annotations
 
@@ -28,21 +29,24 @@ def dual_averaging(model, local_ids: Sequence[int], n_total: int, alpha: float, 
                    max_iter: int, comm: Optional[Comm] = None, placement: Optional[Placement] = None,
                    jacobi: bool = False, name: str = "DualAvg", backend: str = "auto") -> RunResult:
     comm = comm if comm is not None else LocalComm()
+    placement = placement if placement is not None else Placement.contiguous(n_total, comm.nranks)
     if backend != "torch":
         from ..engine.first_order import FirstOrderEngine
 
-        if FirstOrderEngine.eligible(model, comm, n_total) and list(local_ids) == list(range(n_total)):
-            out = FirstOrderEngine.get(model).run("DualAvg", max_iter, alpha, obj0, tol, jacobi=jacobi)
+        if FirstOrderEngine.eligible(model, comm, n_total, local_ids, placement, "DualAvg"):
+            out = FirstOrderEngine.get(model, comm, placement, n_total).run("DualAvg", max_iter, alpha, obj0, tol,
+                                                                              jacobi=jacobi)
             obj = out["obj"]
             n = len(obj)
             return RunResult(algorithm=name, obj=obj, loss=np.abs(obj - obj0),
                              iters=out["iters"] if out["converged"] else n, converged=out["converged"],
                              wall_s=float(out["times"][-1]) if n else 0.0, time_trace=out["times"],
-                             comm_units=np.arange(1, n + 1, dtype=np.float64) * n_total, bytes_sent=0,
-                             bytes_total=0, extra={"jacobi": jacobi, "nranks": 1, "engine": "native-persistent"})
+                             comm_units=np.arange(1, n + 1, dtype=np.float64) * n_total,
+                             bytes_sent=int(out["payload_bytes"]), bytes_total=int(out["payload_bytes"]),
+                             extra={"jacobi": jacobi, "nranks": comm.nranks, "engine": "native-persistent",
+                                    "rows_pushed": out["rows_pushed"], "wire_bytes": out["wire_bytes"]})
         if backend == "native":
-            raise RuntimeError("native dual averaging needs one rank on a GPU with d <= 128")
-    placement = placement if placement is not None else Placement.contiguous(n_total, comm.nranks)
+            raise RuntimeError("native dual averaging needs GPU ranks with contiguous segments and d <= 128")
     dev, d = model.device, model.d
     local_ids = [int(w) for w in local_ids]
     if local_ids != sorted(local_ids) or (local_ids and local_ids[-1] - local_ids[0] + 1 != len(local_ids)):

@@ -23,14 +23,24 @@ from .base import RunResult, Stopper, total_bytes, global_objective, run_bytes
 def standard_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: float, tol: float,
                   max_iter: int, comm: Optional[Comm] = None, placement: Optional[Placement] = None,
                   name: str = "ADMM(star)", backend: str = "auto", engine_opts: Optional[dict] = None) -> RunResult:
-    """``backend``: 'native' = the persistent star kernel (csrc/kernels/star_persistent.hip; one GPU, or
-    several with ``engine_opts={'fabric': XgmiFabric}``), 'torch' = batched torch ops with the comm's
-    reduce/broadcast, 'auto' = native when it applies (HIP device, d <= 64)."""
+    """``backend``: 'native' = the persistent star kernel (csrc/kernels/star_persistent.hip, d <= 64; one
+    GPU, or several with ``engine_opts={'fabric': XgmiFabric}``) or, for d > 64, the streaming large-d
+    engine (csrc/kernels/star_big.hip: cached-inverse GEMVs, RCCL reduce / broadcast across GPUs, the
+    stop rule on the device); 'torch' = batched torch ops with the comm's reduce/broadcast; 'auto' =
+    native when it applies."""
     comm = comm if comm is not None else LocalComm()
     placement = placement if placement is not None else Placement.contiguous(n_total, comm.nranks)
     if model.kind != "linear":
         raise NotImplementedError("the reference star ADMM is closed-form linear only")
     opts = engine_opts or {}
+    if backend in ("auto", "native") and model.device.type == "cuda" and model.d > 64:
+        from ..engine.star_big import comm_ok
+        from ..ops import native
+        if comm_ok(comm) and native.available():
+            return _standard_admm_big(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, name,
+                                      opts)
+        if backend == "native":
+            raise RuntimeError("native large-d star ADMM needs one rank or an RCCL communicator")
     if backend in ("auto", "native") and model.device.type == "cuda" and model.d <= 64 \
             and (comm.nranks == 1 or opts.get("fabric") is not None):
         from ..ops import native
@@ -122,3 +132,29 @@ def _standard_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, c
                      extra={"hub": n_total - 1, "hub_rank": hub_rank, "nranks": comm.nranks, "backend": "native",
                             "engine": eng.last_kernel, "wire_bytes": int(wire), "monitor_bytes": int(mon),
                             "engine_obj": eng})
+
+
+def _standard_admm_big(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, name, opts):
+    """d > 64: the streaming star engine (engine/star_big.py), cached per (model, rho, N, ranks)."""
+    from ..engine.star_big import StarBigEngine
+    from ..utils.timing import roctx_range
+
+    hub_rank = int(placement.owner[n_total - 1])
+    exact = bool(opts.get("exact_objective", False))
+    key = ("star_big", n_total, tuple(int(w) for w in local_ids), float(rho), comm.nranks, exact)
+    cache = model.__dict__.setdefault("_star_engines", {})
+    eng = cache.get(key)
+    if eng is None:
+        eng = StarBigEngine(model, local_ids, n_total, rho, comm, hub_rank=hub_rank, exact_objective=exact)
+        cache[key] = eng
+    snap = comm.stats.snapshot()
+    with roctx_range("%s native-big N=%d" % (name, n_total)):
+        iters, done, wall = eng.run(obj0, tol, max_iter, block=int(opts.get("block", 8)))
+    tr, tt = eng.objective_trace(iters), eng.time_trace(iters)
+    coll = int(comm.stats.delta(snap).get("coll_bytes", 0)) if comm.nranks > 1 else 0
+    return RunResult(algorithm=name, obj=tr, loss=np.abs(tr - obj0), iters=iters, converged=(done == 1), wall_s=wall,
+                     time_trace=tt,
+                     comm_units=np.arange(1, iters + 1, dtype=np.float64) * 2 * (n_total - 1),
+                     bytes_sent=eng.coll_bytes_per_iteration() * iters, bytes_total=coll,
+                     extra={"hub": n_total - 1, "hub_rank": hub_rank, "nranks": comm.nranks, "backend": "native",
+                            "engine": eng.last_kernel, "inverse_setup_s": eng.setup_s, "engine_obj": eng})

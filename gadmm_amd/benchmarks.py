@@ -373,16 +373,19 @@ def run_star(args, rank, world, device, comm) -> Dict:
     fabric = None
     sopts = {}
     if world > 1:
-        from .parallel.xgmi import XgmiFabric
-        fabric = XgmiFabric(n, d, 8, rank, world, device)
-        sopts["fabric"] = fabric
+        # the xGMI fabric on every rank or on none (agreed); without it the star runs its collective
+        # path over the RCCL communicator (reduce to the hub + broadcast, standared_ADMM.m:66-71,86)
+        fabric = _try_fabric(n, d, rank, world, device)
+        if fabric is not None:
+            from .parallel.comm import RankInfo
+            sopts["fabric"] = fabric
+            comm = RankInfo(rank, world)
+        elif comm is None:
+            raise RuntimeError("run_star: no xGMI fabric and no RCCL communicator (ranks sharing one GPU)")
 
     def solve():
         return standard_admm(m, local, n, rho, obj0, tol, 20000, comm=comm, placement=pl, engine_opts=sopts)
 
-    if world > 1:
-        from .parallel.comm import RankInfo
-        comm = RankInfo(rank, world)
     ms, r = _timed(solve, args.steps, args.warmup, device, world)
     # GADMM at the same rho on the same fabric (data-local chain): one warm-up solve (engine set-up,
     # cached inverses), then one timed solve

@@ -74,13 +74,17 @@ class FoArgs(ctypes.Structure):
     _fields_ = [
         ("alg", c_int), ("model", c_int), ("n", c_int), ("d", c_int), ("m", c_int), ("max_iter", c_int),
         ("faithful", c_int), ("jacobi", c_int), ("has_tol", c_int), ("ring", c_int),
-        ("epoch", ctypes.c_uint), ("pad_", c_int),
+        ("epoch", ctypes.c_uint), ("slots", c_int),
         ("step", c_double), ("lam", c_double), ("obj0", c_double), ("tol", c_double), ("thrd", c_double),
         ("timeout_ticks", c_longlong),
         ("A", c_void_p), ("b", c_void_p), ("yy", c_void_p), ("X", c_void_p), ("Y", c_void_p),
         ("hsq", c_void_p), ("sched", c_void_p), ("tab", c_void_p), ("part", c_void_p),
         ("obj_trace", c_void_p), ("cnt_trace", c_void_p), ("time_trace", c_void_p), ("theta_out", c_void_p),
         ("ctl", c_void_p), ("xchk", c_void_p), ("xcd", c_int), ("pad_x", c_int),
+        ("nranks", c_int), ("my_rank", c_int), ("w_lo", c_int), ("n_local", c_int),
+        ("has_monitor", c_int), ("pad_m", c_int),
+        ("owner", c_void_p), ("tab_push", c_void_p), ("wmon", c_void_p), ("wstop", c_void_p),
+        ("wpush", c_void_p), ("pushc", c_void_p),
     ]
 
 
@@ -201,7 +205,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_chain_blocked_tab_granules_dyn": (c_long, [c_int, c_int, c_int]),
         "gadmm_epoch_tables": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
         "gadmm_chain_blocked_launch": (c_int, [ctypes.POINTER(PersistArgs), c_void_p]),
-        "gadmm_fo_lds": (c_long, [c_int, c_int, c_int]),
+        "gadmm_fo_lds": (c_long, [c_int, c_int, c_int, c_int, c_int]),
+        "gadmm_fo_tab_granules": (c_long, [c_int, c_int, c_int]),
         "gadmm_fo_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
         "gadmm_fo_launch": (c_int, [ctypes.POINTER(FoArgs), c_void_p]),
         "gadmm_quad_gemv_test": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
@@ -220,6 +225,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_poison_lds": (c_int, [c_long, c_int, c_void_p]),
         "gadmm_poison_buffer": (c_int, [c_void_p, c_long, c_void_p]),
         "gadmm_lds_probe": (c_int, [c_void_p, c_int, c_int, c_void_p]),
+        "gadmm_memset_async": (c_int, [c_void_p, c_int, c_long, c_void_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name, None)

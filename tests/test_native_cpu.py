@@ -38,7 +38,8 @@ def test_fo_abi_layout_matches_ctypes():
     k = lib.gadmm_fo_abi_layout(buf, 16)
     exp = [ctypes.sizeof(native.FoCtl), ctypes.sizeof(native.FoArgs), native.FoArgs.step.offset,
            native.FoArgs.timeout_ticks.offset, native.FoArgs.A.offset, native.FoArgs.ctl.offset,
-           native.FoArgs.xchk.offset]
+           native.FoArgs.xchk.offset, native.FoArgs.nranks.offset, native.FoArgs.owner.offset,
+           native.FoArgs.pushc.offset]
     assert list(buf[:k]) == exp
 
 
