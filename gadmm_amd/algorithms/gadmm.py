@@ -282,7 +282,8 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
                                 max_iter=max_iter, lam=getattr(model, "lam", 0.0), step=step, max_inner=max_inner,
                                 inner_tol=inner_tol, comm=rcomm, block=block, precomputed=pre,
                                 local_solver="newton" if local_solver == "newton" else "gd",
-                                chord=float(opts.get("chord", 0.02)), residual=bool(opts.get("residual", True)))
+                                chord=float(opts.get("chord", 0.02)), residual=bool(opts.get("residual", True)),
+                                obj_mode=str(opts.get("obj_mode", "auto")))
         if rcomm is None and opts.get("cache", True):
             if cache is None:
                 cache = {}

@@ -72,12 +72,16 @@ class NativeChainEngine:
                  model: str = "linear", rho: float = 1.0, obj0: float = 0.0, tol: float = 1e-4,
                  max_iter: int = 1000, lam: float = 0.0, step: float = 0.0, max_inner: int = 100,
                  inner_tol: float = 1e-4, comm=None, block: int = 16, stream: Optional[torch.cuda.Stream] = None,
-                 precomputed=None, force_monitor: bool = False, obj_mode: str = "exact", local_solver: str = "gd",
+                 precomputed=None, force_monitor: bool = False, obj_mode: str = "auto", local_solver: str = "gd",
                  chord: float = 0.02, residual: bool = False, xcd: int = 2):
         """``local_solver`` (logistic): "gd" = the reference's inexact inner GD (logReg_GD.m, step /
         max_inner / inner_tol), "newton" = exact local solves (group_ADMM_logistic.m semantics,
         csrc/kernels/chain_newton.hip; d, m <= 64). ``chord`` (newton): a worker reuses its last
         inverse Hessian while steps contract by at least this factor (0: refresh every step).
+        ``obj_mode`` (graph / large-d phases): "exact" evaluates f_n = 1/2 th'A th - b'th + 1/2 y'y with a
+        second GEMV by the Gram, "identity" uses A th = r - deg rho th from the solve itself (no second
+        pass; at d > 256 that pass re-streams an 800 MB Gram per worker-phase), "auto" = identity at
+        d > 256, exact otherwise (the verification path stays available as "exact").
         ``residual``: the kernels also emit the K4 primal residual (sum over chain edges of
         ||theta_n - theta_right||^2) per iteration, read back by ``primal_residual``. ``xcd`` (one GPU,
         persistent kernels): 0 default grid, 1 deal every working workgroup onto one XCD, 2 also
@@ -194,7 +198,10 @@ class NativeChainEngine:
             args.step = self.chord  # the Newton kernel's chord contraction threshold
         args.inner_iters = self.inner_iters.data_ptr()
         args.rbuf = native.ptr(self.rbuf)
-        args.obj_mode = 0 if obj_mode == "exact" else 1
+        if obj_mode not in ("auto", "exact", "identity"):
+            raise ValueError("unknown obj_mode %r" % obj_mode)
+        args.obj_mode = 0 if (obj_mode == "exact" or (obj_mode == "auto" and d <= 256)) else 1
+        self.obj_mode_name = "exact" if args.obj_mode == 0 else "identity"
         args.solver = 1 if local_solver == "newton" else 0
         args.n_total = self.n_total
         args.lgid = self.lgid.data_ptr()

@@ -388,7 +388,7 @@ def test_graft_smoke():
     ge.smoke()
 
 
-@pytest.mark.parametrize("d,obj_mode", [(512, "exact"), (1001, "exact"), (640, "identity")])
+@pytest.mark.parametrize("d,obj_mode", [(512, "exact"), (1001, "exact"), (640, "identity"), (384, "auto")])
 def test_large_d_engine_matches_torch(d, obj_mode):
     """Row-blocked large-d phase kernels (d > 256) vs the batched torch path on the same device."""
     from gadmm_amd.data import gaussian_regression
@@ -406,6 +406,7 @@ def test_large_d_engine_matches_torch(d, obj_mode):
     eng.set_path(list(range(4)), Placement.contiguous(4, 1), 0)
     eng.reset()
     r = eng.run()
+    assert eng.obj_mode_name == ("identity" if obj_mode == "auto" else obj_mode)  # auto: identity at d > 256
     assert r.done == 1 and abs(r.iters - ref.iters) <= 1, (r.iters, ref.iters)
     n = min(r.iters, ref.iters) - 1
     tr = eng.objective_trace(n)
@@ -824,3 +825,30 @@ def test_xcd_packing_bit_identical(lin24, lin_obj0, log24, log_obj0, monkeypatch
     k, L, W, _pw = eng.blocked_plan()
     nblocks = W + (24 + 11) // 12 + 1  # worker + objective workgroups + the monitor
     assert r.done == 1 and len(ids) == nblocks and len(set(ids)) == 1, (r.done, ids)
+
+
+@pytest.mark.parametrize("n,m,d", [(4, 400, 200), (3, 700, 300), (2, 300, 70)])
+def test_star_big_native_matches_torch(n, m, d):
+    """Large-d star ADMM (csrc/kernels/star_big.hip: cached-inverse streaming GEMVs, device stop rule,
+    blocks of iterations without a host sync) == the torch star path (standared_ADMM.m semantics): the
+    same stop iteration and objective traces to ~1e-10; identity and exact objective modes agree."""
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import standard_admm
+    g = torch.Generator().manual_seed(n * 1000 + d)
+    X = torch.randn(n, m, d, dtype=torch.float64, generator=g)
+    y = torch.randn(n, m, dtype=torch.float64, generator=g)
+    mod = LinearRegression(X.to(DEV), y.to(DEV))
+    obj0 = mod.optimum()
+    rho = 0.5 * m
+    a = standard_admm(mod, list(range(n)), n, rho, obj0, 1e-8 * abs(obj0), 400)
+    assert a.extra["backend"] == "native" and a.extra["engine"].startswith("star-big")
+    b = standard_admm(mod, list(range(n)), n, rho, obj0, 1e-8 * abs(obj0), 400, backend="torch")
+    assert a.iters == b.iters and a.converged == b.converged
+    np.testing.assert_allclose(a.obj, b.obj, rtol=1e-10, atol=0)
+    c = standard_admm(mod, list(range(n)), n, rho, obj0, 1e-8 * abs(obj0), 400,
+                      engine_opts={"exact_objective": True})
+    assert c.iters == a.iters and c.extra["engine"] == "star-big(exact objective)"
+    np.testing.assert_allclose(c.obj, a.obj, rtol=1e-9, atol=0)
+    assert np.all(np.diff(a.time_trace) >= 0) and a.time_trace[-1] > 0  # measured device clock
+    a2 = standard_admm(mod, list(range(n)), n, rho, obj0, 1e-8 * abs(obj0), 400)  # cached engine
+    assert a2.iters == a.iters and np.array_equal(a2.obj, a.obj)
