@@ -1,0 +1,589 @@
+// Persistent single-launch GADMM with EXACT logistic local solves (the dead CVX variant
+// group_ADMM_logistic.m:26-49): one kernel per GPU for the whole solve.
+//
+// The graph engine runs the exact solve as replayed phase kernels (chain_newton.hip: 512 threads per
+// worker, an in-place Gauss-Jordan inverse of the Hessian on the critical path whenever a chord step
+// contracts too slowly; ~864 launches per solve). Here every worker is ONE resident workgroup for the
+// whole solve, and the two costs of that path leave the critical path:
+//
+//   wave 0 ("solver") keeps the shard X and X^T in VGPRs (split-column quad layout, quad_gemv.h) and
+//   runs the chord-Newton steps of its active phase with no barrier at all:
+//       z = X x,  s_i = y_i sigma(-y_i z_i),  g = -X^T s + (lam + deg rho) x + mu - rho (th_l + th_r),
+//       dx = Hinv g,  x <- x - dx           until max|dx| < 1e-13 max(1, max|x|) (<= 50 steps)
+//   waves 1-4 ("crew") build the inverse Hessian H(x_r)^{-1}, H = X^T diag(w) X + (lam + deg rho) I
+//   (f64 MFMA Hessian, 4-wave in-place block Gauss-Jordan in registers, synchronised among themselves
+//   through an LDS counter, never with wave 0) at the worker's own final iterate of its last active
+//   phase, DURING the idle phase in which the other group solves. The next active phase starts from
+//   that inverse (its own previous iterate: the chord Newton preconditioner is one iteration old).
+//   A step that contracts by less than `chord` (|dx_k| > chord |dx_{k-1}|) asks the crew for an
+//   urgent inverse at the current x, exactly like the graph kernel's chord rule.
+// Which inverse each step uses is fixed by the iterates alone (the solver waits for the inverse it
+// asked for), so the run is deterministic. The fixed point and the stopping rule are exact Newton's.
+//
+// Cross-worker protocol (heads / tails, lazy head dual, tagged theta granules, a monitor workgroup
+// that sums f_n in worker order and posts the lagged stop decision into every rank's ring, deadlines
+// on every spin, the xGMI fabric across GPUs): as chain_persistent_logistic.hip.
+#include "gadmm_common.h"
+#include "gadmm_chain.h"
+#include "persist_device.h"
+#include "chain_device.h"
+#include <cstddef>
+
+struct LogiArgs {  // == chain_persistent_logistic.hip (one ABI for both persistent logistic kernels)
+  const double* X;  // [n_local][m][d]
+  const double* Y;  // [n_local][m]
+  int m, max_inner;
+  double lam, step, inner_tol;  // Newton: step = chord threshold (<= 0: a fresh inverse every step)
+  int* inner_iters;             // [n_local] optional: Newton steps of the worker's last local solve
+};
+
+namespace {
+
+constexpr int NT = 320;       // wave 0 solver + 4 crew waves
+constexpr int CREW = 4;
+constexpr int NCW = 64 / CREW;  // Gauss-Jordan: columns per crew lane (j = cw + CREW c)
+constexpr int NMAX = 50;      // Newton step cap (== models/logistic.py:newton_prox)
+constexpr double NTOL = 1e-13;
+constexpr int QT = 13;        // quad layout: d, m <= 52
+constexpr int QB = 4 * 64 * (QT + (QT & 1));  // doubles of one quad-LDS inverse buffer
+constexpr int HS = 65;        // LDS Hessian row stride
+
+// LDS layout (doubles)
+struct NLds {
+  int xs, hs, qb0, qb1, wq, slab, stage, total;
+  __host__ __device__ NLds(int m, int d) {
+    const int dp = (d + 3) & ~3;
+    xs = 0;                        // X [m][dp] (crew: Hessian operands)
+    hs = xs + ((m * dp + 1) & ~1); // Hessian [64][HS]
+    qb0 = ((hs + 64 * HS + 1) & ~1);
+    qb1 = qb0 + QB;                // two inverse buffers (quad-LDS layout: quad_gemv_lds)
+    wq = qb1 + QB;                 // [64] w_i = sigma (1 - sigma) at the refresh point
+    slab = wq + 64;                // [2][4][64] Gauss-Jordan pivot-column slabs
+    stage = slab + 512;            // [QSTAGE] solver quad GEMV staging
+    total = stage + QSTAGE;
+  }
+};
+
+struct NCtl {        // LDS words of the solver <-> crew protocol
+  int req;           // last refresh requested (solver; -1: quit)
+  int ready;         // last refresh completed (crew)
+  int cnt;           // crew barrier counter
+  int pad;
+  double shift;      // lam + deg rho of the requested refresh
+};
+
+// LDS-only ordering: the fences name the "local" address space, so they wait for LDS operations only
+// (lgkmcnt). A plain workgroup fence would also wait for this wave's outstanding GLOBAL stores
+// (vmcnt) -- for the solver, the write-through theta granules it has just published (~1 us each).
+__device__ __forceinline__ int lds_load_acq(const int* p) {
+  const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+  return v;
+}
+__device__ __forceinline__ void lds_store_rel(int* p, int v) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// barrier among the 4 crew waves only (the solver wave never joins): an LDS arrival counter
+__device__ __forceinline__ void crew_sync(int* cnt, int& gen) {
+  gen += CREW;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < gen) __builtin_amdgcn_s_sleep(1);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__device__ __forceinline__ double wave_max_abs(double v) {
+  v = fabs(v);
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  return v;
+}
+
+__device__ __forceinline__ double rcp_nr(double v) {  // v_rcp_f64 + one Newton-Raphson step
+  const double r = __builtin_amdgcn_rcp(v);
+  return fma(r, fma(-v, r, 1.0), r);
+}
+
+// One refresh by the crew (waves 1-4, cw = 0..3): Hs = X^T diag(wq) X + shift I (MFMA), in-place block
+// Gauss-Jordan inverse in registers, written to the quad-LDS buffer `qb`. Every LDS word read here is
+// written first (padding included): the result never depends on stale LDS.
+__device__ void crew_refresh(double* lds, const NLds& L, int m, int d, double shift, int cw, int* cnt, int& gen,
+                             double* qb, long long* tl) {
+  const int lane = threadIdx.x & 63;
+  const int dp = (d + 3) & ~3;
+  const double* Xs = lds + L.xs;
+  double* Hs = lds + L.hs;
+  const double* wq = lds + L.wq;
+  {  // Hessian tiles (R, C = cw), R = 0..3: v_mfma_f64_16x16x4f64, K = samples in chunks of 4
+    const int k4 = lane >> 4, c16 = lane & 15;
+    f64x4 acc[4];
+#pragma unroll
+    for (int R = 0; R < 4; ++R) acc[R] = f64x4{0.0, 0.0, 0.0, 0.0};
+    const int cc = 16 * cw + c16;
+    for (int k0 = 0; k0 < m; k0 += 4) {
+      const int kk = k0 + k4;
+      const bool kin = kk < m;
+      const double w = kin ? wq[kk] : 0.0;
+      const double* xr = Xs + (kin ? kk : 0) * dp;
+      const double bv = (kin && cc < dp) ? xr[cc] : 0.0;
+#pragma unroll
+      for (int R = 0; R < 4; ++R) {
+        const int ca = 16 * R + c16;
+        const double av = ca < dp ? w * xr[ca] : 0.0;
+        acc[R] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[R], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int R = 0; R < 4; ++R)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int row = 16 * R + k4 + 4 * reg, col = 16 * cw + c16;
+        double v;
+        if (row < d && col < d) v = acc[R][reg] + (row == col ? shift : 0.0);
+        else v = row == col ? 1.0 : 0.0;  // identity padding
+        Hs[row * HS + col] = v;
+      }
+  }
+  crew_sync(cnt, gen);
+  if (tl && cw == 0 && lane == 0) tl[1] = (long long)__builtin_amdgcn_s_memrealtime();
+  // in-place block Gauss-Jordan (SPD, no pivoting), 4 x 4 pivot blocks; lane i of crew wave cw keeps row
+  // i's columns j = cw + 4c. Block K = p..p+3: P = A_KK, non-pivot rows L_i = A_iK P^-1, A_ij -= L_i A_Kj,
+  // A_iK = -L_i; pivot rows A_Kj = P^-1 A_Kj, A_KK = P^-1. Only column K is published; the pivot rows
+  // follow from the symmetric structure (processed / unprocessed cross blocks are antisymmetric), as in
+  // chain_newton.hip.
+  const int i = lane;
+  double h[NCW];
+#pragma unroll
+  for (int c = 0; c < NCW; ++c) h[c] = Hs[i * HS + cw + CREW * c];
+  const int nb = (d + 3) >> 2;
+  double* slabs = lds + L.slab;
+  for (int bb = 0; bb < nb; ++bb) {
+    const int p = 4 * bb;
+    double* slab = slabs + (bb & 1) * 256;  // [4][64]: column p + q of the current matrix
+    {  // the block's column p + q is register c = p / 4 of crew wave q
+      double hv = 0.0;
+#pragma unroll
+      for (int c = 0; c < NCW; ++c) hv = (c == bb) ? h[c] : hv;
+      slab[cw * 64 + i] = hv;
+    }
+    crew_sync(cnt, gen);
+    double P[4][4], Rr[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      Rr[q] = slab[q * 64 + i];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) P[q][r] = slab[q * 64 + p + r];
+    }
+    const bool pivrow = (i >> 2) == bb;
+    if (pivrow) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) Rr[q] = (q == (i & 3)) ? 1.0 : 0.0;
+    }
+    const double a00 = P[0][0], a01 = P[1][0], a11 = P[1][1];
+    const double ia = rcp_nr(fma(a00, a11, -a01 * a01));
+    const double A00 = a11 * ia, A01 = -a01 * ia, A11 = a00 * ia;
+    const double b00 = P[2][0], b01 = P[3][0], b10 = P[2][1], b11 = P[3][1];
+    const double w00 = fma(A00, b00, A01 * b10), w01 = fma(A00, b01, A01 * b11);
+    const double w10 = fma(A01, b00, A11 * b10), w11 = fma(A01, b01, A11 * b11);
+    const double s00 = P[2][2] - fma(b00, w00, b10 * w10);
+    const double s01 = P[3][2] - fma(b00, w01, b10 * w11);
+    const double s11 = P[3][3] - fma(b01, w01, b11 * w11);
+    const double is = rcp_nr(fma(s00, s11, -s01 * s01));
+    const double y0 = fma(A00, Rr[0], A01 * Rr[1]), y1 = fma(A01, Rr[0], A11 * Rr[1]);
+    const double z2 = Rr[2] - fma(b00, y0, b10 * y1), z3 = Rr[3] - fma(b01, y0, b11 * y1);
+    const double l2 = fma(s11, z2, -s01 * z3) * is, l3 = fma(s00, z3, -s01 * z2) * is;
+    const double l0 = y0 - fma(w00, l2, w01 * l3), l1 = y1 - fma(w10, l2, w11 * l3);
+    const double lw = cw == 0 ? l0 : (cw == 1 ? l1 : (cw == 2 ? l2 : l3));  // l[j - p] for j = p + cw
+#pragma unroll
+    for (int c = 0; c < NCW; ++c) {
+      const int j = cw + CREW * c;
+      const double tq = fma(l0, slab[j], fma(l1, slab[64 + j], fma(l2, slab[128 + j], l3 * slab[192 + j])));
+      const bool inK = c == bb;
+      const double sg = j < p ? -1.0 : 1.0;
+      double v;
+      if (inK) v = pivrow ? lw : -lw;
+      else v = pivrow ? sg * tq : fma(-sg, tq, h[c]);
+      h[c] = v;
+    }
+  }
+  if (tl && cw == 0 && lane == 0) tl[2] = (long long)__builtin_amdgcn_s_memrealtime();
+  // the inverse into the quad-LDS layout of quad_gemv_lds<QT>: element (row, col) at
+  // ((t >> 1) * 4 + r) * 128 + 2 lq + (t & 1), row = iq + 16 r, col = c4 + 4 t, lq = iq + 16 c4; padding 0
+  {
+    const int r = i >> 4, iq = i & 15;
+#pragma unroll
+    for (int c = 0; c < NCW; ++c) {
+      const int col = cw + CREW * c;
+      const int t = col >> 2, c4 = col & 3;
+      if (t < QT + (QT & 1)) {
+        const double v = (i < d && col < d && t < QT) ? h[c] : 0.0;
+        qb[((t >> 1) * 4 + r) * 128 + 2 * (iq + 16 * c4) + (t & 1)] = v;
+      }
+    }
+  }
+  crew_sync(cnt, gen);
+}
+
+}  // namespace
+
+template <bool SYS>
+__global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs a, LogiArgs g) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ NCtl nc;
+  const int d = a.d, n = a.n, m = g.m;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const __amdgpu_buffer_rsrc_t rth = rsrc_of(a.thg);
+  const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
+  const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
+  const int bid = (int)blockIdx.x;
+  const NLds L(m, d);
+
+  if (a.has_monitor && bid == a.n_local) {
+    // ---------------------------------------------------------------- monitor (wave 0)
+    if (wid != 0) return;
+    double* vals = lds;  // [n]
+    for (int it = a.start_iter;; ++it) {
+      const unsigned tag = make_tag(a.epoch, it);
+      const int slot = it % a.ring;
+      bool okall = true;
+      for (int w = lane; w < n; w += 64) {
+        double v = 0.0;
+        for (int spin = 0;; ++spin) {
+          if (load_granule<SYS>(rob, (slot * n + w) * 16, tag, &v)) break;
+          if ((spin & 7) == 7 && now_ticks() > deadline) {
+            okall = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        vals[w] = v;
+      }
+      const bool ok = __all(okall);
+      unsigned code = 0;
+      if (lane == 0) {
+        if (!ok) {
+          code = 4;
+        } else {
+          double s = 0.0;
+          for (int w = 0; w < n; ++w) s += vals[w];  // worker order
+          if (it - 1 < a.max_iter) a.trace[it - 1] = s;
+          if (!(s == s) || isinf(s)) code = 3;
+          else if (fabs(s - a.obj0) < a.tol) code = 1;
+          else if (it >= a.max_iter) code = 2;
+          if (a.tstamp && it - 1 < a.max_iter) a.tstamp[it - 1] = (long long)now_ticks();
+        }
+        const unsigned long long dv = ((unsigned long long)tag << 32) | code;
+        for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
+      }
+      if (__shfl((int)code, 0, 64)) return;
+    }
+  }
+  if (bid >= a.n_local) return;
+
+  // ------------------------------------------------------------------ worker workgroup
+  const PhaseSlot sl = a.slots[bid];
+  const int li = sl.li, w = sl.gid, left = sl.left, right = sl.right;
+  const bool head = (a.pos[bid] % 2) == 0;
+  const double rho = a.rho, lam = g.lam, chord = g.step;
+  const double shift = lam + rho * (double)((left >= 0 ? 1 : 0) + (right >= 0 ? 1 : 0));
+  const double* Xg = g.X + (long)li * m * d;
+  const int dp = (d + 3) & ~3;
+  // shared set-up: X into LDS (crew Hessian operands), protocol words
+  for (int e = threadIdx.x; e < m * dp; e += NT) {
+    const int r = e / dp, c = e - r * dp;
+    lds[L.xs + e] = c < d ? Xg[(long)r * d + c] : 0.0;
+  }
+  if (threadIdx.x == 0) {
+    nc.req = 0;
+    nc.ready = -1;
+    nc.cnt = 0;
+    nc.shift = shift;
+  }
+  // refresh 0 is built at the worker's start point theta^{start - 1}: w_i = sigma(z_i)(1 - sigma(z_i)),
+  // z_i = X_i theta (zeros on a fresh solve: w = 1/4)
+  if (threadIdx.x < 64) {
+    const int i = threadIdx.x;
+    double wi = 0.0;
+    if (i < m) {
+      double z = 0.0;
+      for (int j = 0; j < d; ++j) z = fma(Xg[(long)i * d + j], a.theta[(long)w * d + j], z);
+      const double pz = 1.0 / (1.0 + exp(g.Y[(long)li * m + i] * z));
+      wi = pz * (1.0 - pz);
+    }
+    lds[L.wq + i] = wi;
+  }
+  lds_barrier();  // the only workgroup-wide barrier: solver and crew run decoupled from here on
+
+  if (wid > 0) {
+    // ---------------------------------------------------------------- crew (waves 1-4)
+    const int cw = wid - 1;
+    const int li_ = sl.li;
+    int gen = 0, done_req = -1;
+    for (;;) {
+      int r;
+      for (int spin = 0;; ++spin) {
+        r = lds_load_acq(&nc.req);
+        if (r != done_req) break;
+        if ((spin & 63) == 63 && now_ticks() > deadline + 100000000ull) return;  // solver gone (abort path)
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (r < 0) return;  // the solver quit
+      // instrumented runs (PersistArgs::timeline, [n_local][128][8] stamps): refreshes 0..63 in rows 0..63
+      long long* tl = (a.timeline && r < 64) ? a.timeline + ((long)li_ * 128 + r) * 8 : nullptr;
+      if (tl && cw == 0 && lane == 0) tl[0] = (long long)__builtin_amdgcn_s_memrealtime();
+      crew_refresh(lds, L, m, d, nc.shift, cw, &nc.cnt, gen, lds + ((r & 1) ? L.qb1 : L.qb0), tl);
+      if (tl && cw == 0 && lane == 0) tl[3] = (long long)__builtin_amdgcn_s_memrealtime();
+      if (cw == 0 && lane == 0) lds_store_rel(&nc.ready, r);
+      done_req = r;
+    }
+  }
+
+  // ------------------------------------------------------------------ solver (wave 0)
+  double* st = lds + L.stage;
+  double Xq[4][QT], XTq[4][QT];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int t = 0; t < QT; ++t) {
+      const int qi = lane & 15, qc = lane >> 4;
+      const int row = qi + 16 * r, col = qc + 4 * t;
+      Xq[r][t] = (row < m && col < d) ? Xg[(long)row * d + col] : 0.0;
+      XTq[r][t] = (col < m && row < d) ? Xg[(long)col * d + row] : 0.0;
+    }
+  u32x4* const p0 = a.push ? a.push[2 * bid] : nullptr;
+  u32x4* const p1 = a.push ? a.push[2 * bid + 1] : nullptr;
+  const __amdgpu_buffer_rsrc_t rp0 = rsrc_of(p0 ? (const void*)p0 : (const void*)a.thg);
+  const __amdgpu_buffer_rsrc_t rp1 = rsrc_of(p1 ? (const void*)p1 : (const void*)a.thg);
+  const bool inj = lane < d, ini = lane < m;
+  const double yv = ini ? g.Y[(long)li * m + lane] : 0.0;
+  double th = inj ? a.theta[(long)w * d + lane] : 0.0;
+  double mu = inj ? a.mu[(long)li * d + lane] : 0.0;
+  double tl = (inj && left >= 0) ? a.theta[(long)left * d + lane] : 0.0;
+  double tr = (inj && right >= 0) ? a.theta[(long)right * d + lane] : 0.0;
+  int pending = a.pending_in;
+  int stop_code = 0, stop_iter = 0, abort = 0, used = 0;
+  // the refresh this worker's next solve starts from; request 0 (at the start point) is live from the
+  // set-up on: the crew waits for nc.req to differ from its last finished request (-1 at first)
+  int req = 0;
+  bool req_fresh = true;  // refresh `req` was requested at the start point of the next solve
+  const int bg_steps = (g.max_inner >= 1 && g.max_inner < NMAX) ? g.max_inner : 4;
+  auto wait_ready = [&](int r) -> bool {
+    for (int spin = 0;; ++spin) {
+      if (lds_load_acq(&nc.ready) >= r) return true;
+      if ((spin & 63) == 63 && now_ticks() > deadline) return false;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  auto post = [&](int r) { lds_store_rel(&nc.req, r); };
+
+  int it = a.start_iter;
+  for (;; ++it) {
+    if (it > a.max_iter + a.lag) break;
+    const bool check = it - a.start_iter >= a.lag;
+    const int jdec = it - a.lag;
+    const bool need_nb = head ? it > a.start_iter : true;
+    const int jnb = head ? it - 1 : it;
+    const unsigned tnb = make_tag(a.epoch, jnb), tj = make_tag(a.epoch, jdec);
+    const int ra = need_nb ? left : -1, rb = need_nb ? right : -1;
+    bool decided = !check;
+    unsigned long long dv = 0;
+    int outcome = 0;  // 1 go, 2 stop, 3 timeout
+    for (int spin = 0;; ++spin) {
+      bool nb = true;
+      if (inj) {
+        if (ra >= 0) nb &= load_granule<SYS>(rth, (ra * d + lane) * 16, tnb, &tl);
+        if (rb >= 0) nb &= load_granule<SYS>(rth, (rb * d + lane) * 16, tnb, &tr);
+      }
+      if (!decided) {
+        dv = __shfl(load_dec<SYS>(&a.decg[jdec % a.ring]), 0, 64);
+        decided = (unsigned)(dv >> 32) == tj;
+      }
+      if (decided && (unsigned)(dv & 0xffffffffu) != 0u) { outcome = 2; break; }
+      if (decided && __all(nb)) { outcome = 1; break; }
+      if ((spin & 7) == 7 && now_ticks() > deadline) { outcome = 3; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (outcome != 1) {
+      if (outcome == 2) {
+        stop_code = (int)(unsigned)(dv & 0xffffffffu);
+        stop_iter = jdec;
+      } else {
+        abort = 1;
+      }
+      break;
+    }
+    // -- lazy dual (heads); x-independent gradient part cv = mu - rho (th_l + th_r)
+    double cv = 0.0, x = 0.0;
+    if (inj) {
+      double mm = mu;
+      if (head && pending) {
+        if (left >= 0) mm = mm - rho * (tl - th);
+        if (right >= 0) mm = mm + rho * (th - tr);
+        mu = mm;
+      }
+      cv = mm;
+      if (left >= 0) cv = cv - rho * tl;
+      if (right >= 0) cv = cv - rho * tr;
+      x = th;
+    }
+    // -- chord Newton from the inverse at the previous own iterate
+    const int kk_tl = it - a.start_iter;
+    long long* tls = (a.timeline && kk_tl < 64) ? a.timeline + ((long)li * 128 + 64 + kk_tl) * 8 : nullptr;
+    if (tls && lane == 0) tls[0] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (!wait_ready(req)) { abort = 1; break; }
+    if (tls && lane == 0) tls[1] = (long long)__builtin_amdgcn_s_memrealtime();
+    const double* hq = lds + ((req & 1) ? L.qb1 : L.qb0);
+    double nd_prev = 0.0;
+    used = 0;
+    bool urgent = false;
+    bool fresh = req_fresh;  // the inverse in use was built at this solve's start point
+    for (int k = 0; k < NMAX; ++k) {
+      const double z = quad_gemv<QT>(Xq, x, st);                     // margins
+      const double ps = ini ? 1.0 / (1.0 + exp(yv * z)) : 0.0;        // sigma(-y z)
+      const double gx = quad_gemv<QT>(XTq, ini ? yv * ps : 0.0, st);  // (X^T (y . sigma))_j
+      const double gr = inj ? -gx + shift * x + cv : 0.0;
+      const double dx = quad_gemv_lds<QT>(hq, gr, st);
+      const double dxl = inj ? dx : 0.0;
+      x = inj ? x - dxl : 0.0;
+      const double mdx = wave_max_abs(dxl), mx = wave_max_abs(x);
+      used = k + 1;
+      if (mdx < NTOL * fmax(1.0, mx)) break;
+      if (chord <= 0.0 || (!fresh && k > 0 && mdx > chord * nd_prev)) {
+        // contraction too slow: an inverse at the current x, from the crew (idle in this phase)
+        const double z2 = quad_gemv<QT>(Xq, x, st);
+        const double p2 = ini ? 1.0 / (1.0 + exp(yv * z2)) : 0.5;
+        lds[L.wq + lane] = ini ? p2 * (1.0 - p2) : 0.0;
+        ++req;
+        post(req);
+        urgent = true;
+        if (!wait_ready(req)) { abort = 1; break; }
+        hq = lds + ((req & 1) ? L.qb1 : L.qb0);
+        fresh = true;
+        nd_prev = 0.0;
+        continue;
+      }
+      fresh = false;
+      nd_prev = mdx;
+    }
+    if (abort) break;
+    if (tls && lane == 0) {
+      tls[2] = (long long)__builtin_amdgcn_s_memrealtime();
+      tls[3] = used;
+      tls[4] = req;
+    }
+    // -- publish theta^it: own table + the remote neighbours' tables (first: the neighbours wait)
+    const unsigned tag = make_tag(a.epoch, it);
+    if (inj) {
+      store_granule<SYS>(rth, (w * d + lane) * 16, tag, x);
+      if (p0) store_granule<SYS>(rp0, (w * d + lane) * 16, tag, x);
+      if (p1) store_granule<SYS>(rp1, (w * d + lane) * 16, tag, x);
+    }
+    if (!head) {  // tails: both neighbours are this iteration's heads -> dual update now
+      double rp = 0.0;
+      if (inj) {
+        double mm = mu;
+        if (left >= 0) mm = mm - rho * (tl - x);
+        if (right >= 0) mm = mm + rho * (x - tr);
+        mu = mm;
+        if (left >= 0) rp = fma(tl - x, tl - x, rp);
+        if (right >= 0) rp = fma(x - tr, x - tr, rp);
+      }
+      if (a.rres) {
+        const double rs = wave_sum_f64(rp);
+        if (lane == 0 && it - 1 < a.max_iter) a.rres[(long)(it - 1) * n + w] = rs;
+      }
+    } else {
+      pending = 1;
+    }
+    th = x;
+    // -- f_n(theta^it) -> monitor; the same margins give the crew its next refresh point (this worker's
+    // new iterate), built while the other group solves
+    const double z = quad_gemv<QT>(Xq, x, st);
+    const double pz = ini ? 1.0 / (1.0 + exp(yv * z)) : 0.5;
+    const double part = wave_sum_f64(ini ? softplus(-yv * z) : 0.0);
+    const double xx = wave_sum_f64(inj ? x * x : 0.0);
+    if (lane == 0) store_granule<SYS>(rob, ((it % a.ring) * n + w) * 16, tag, lam * 0.5 * xx + part);
+    // background refresh at the new iterate only when this solve says the inverse is ageing (more
+    // than bg_steps chord steps, or an urgent refresh): the crew then works while the other group
+    // solves, and otherwise stays idle -- a busy crew shares this CU's SIMDs and LDS with the solver
+    req_fresh = false;
+    if (used > bg_steps || urgent) {
+      if (!wait_ready(req)) { abort = 1; break; }  // the crew is idle again (it always is here)
+      lds[L.wq + lane] = ini ? pz * (1.0 - pz) : 0.0;
+      ++req;
+      post(req);
+      req_fresh = true;
+    }
+  }
+  lds_store_rel(&nc.req, -1);  // crew: quit (after its current refresh, if any)
+  if (inj) {
+    a.theta[(long)w * d + lane] = th;
+    a.mu[(long)li * d + lane] = mu;
+  }
+  if (lane == 0) {
+    if (g.inner_iters) g.inner_iters[li] = used;
+    if (abort) {
+      a.ctl->done = 4;
+    } else if (bid == 0 && stop_code) {
+      a.ctl->done = stop_code;
+      a.ctl->conv_iter = stop_iter;
+      a.ctl->iter = it;
+      a.ctl->pending = 1;
+      a.ctl->monitored = stop_iter;
+    }
+  }
+}
+
+extern "C" long gadmm_resident_capacity(const void* fn, int threads, size_t shm);
+
+static const void* newton_variant(const PersistArgs& a, const LogiArgs& g) {
+  if (a.d > 4 * QT || g.m > 4 * QT || a.d < 1 || g.m < 1 || a.n_epochs > 0) return nullptr;
+  return a.sys_scope ? (const void*)chain_persistent_newton_kernel<true>
+                     : (const void*)chain_persistent_newton_kernel<false>;
+}
+
+static size_t newton_shm(const PersistArgs& a, const LogiArgs& g) {
+  const NLds L(g.m, a.d);
+  size_t b = (size_t)L.total * 8;
+  if (b < (size_t)a.n * 8) b = (size_t)a.n * 8;  // the monitor stages one double per worker
+  return b;
+}
+
+extern "C" {
+
+long gadmm_chain_persistent_newton_capacity(const PersistArgs* args, const LogiArgs* g) {
+  const void* fn = newton_variant(*args, *g);
+  return fn ? gadmm_resident_capacity(fn, NT, newton_shm(*args, *g)) : 0;
+}
+
+int gadmm_chain_persistent_newton_launch(const PersistArgs* args, const LogiArgs* gargs, hipStream_t st) {
+  const PersistArgs& a = *args;
+  const LogiArgs& g = *gargs;
+  const void* fn = newton_variant(a, g);
+  if (!fn || !g.X || !g.Y || a.ring <= a.lag + 1 || a.start_iter + a.max_iter + a.lag >= (1 << 20) ||
+      (a.has_monitor && !a.dec_push)) {
+    gadmm_set_error("persistent Newton kernel: unsupported configuration (d=%d m=%d)", a.d, g.m);
+    return -1;
+  }
+  const size_t shm = newton_shm(a, g);
+  if (shm > 160 * 1024) {
+    gadmm_set_error("persistent Newton kernel: %zu B of LDS", shm);
+    return -1;
+  }
+  const int blocks = a.n_local + (a.has_monitor ? 1 : 0);
+  const long cap = gadmm_resident_capacity(fn, NT, shm);
+  if (blocks > cap) {
+    gadmm_set_error("persistent Newton kernel: %d workgroups but only %ld can be resident", blocks, cap);
+    return -2;
+  }
+  if (shm > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+  PersistArgs ka = a;
+  void* kargs[] = {&ka, const_cast<LogiArgs*>(&g)};
+  GADMM_CHECK(hipLaunchKernel(fn, dim3(blocks), dim3(NT), kargs, shm, st));
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"

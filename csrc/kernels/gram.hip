@@ -24,6 +24,54 @@ namespace {
 constexpr int BK = 16;
 constexpr int PAD = 16;
 
+// Lower-triangular tile id -> (ti, tj), ti >= tj, in SUPERTILE order: the tiles of an ST x ST block of
+// the triangle (rows [ST I, ST I + ST), columns [ST J, ST J + ST), J <= I) get consecutive ids, blocks
+// in row-major order over the triangle. With the XCD remap, the workgroups one XCD runs together are
+// then a square-ish block of tiles that share 2 ST column panels of the shard (ST^2 tiles from 2 ST
+// panels) instead of a strip of one tile row (~64 tiles from ~65 panels): 3-4x fewer distinct shard
+// bytes per K row through that XCD's L2 (the d = 10k Gram was operand-bandwidth bound at ~52 TF/s).
+// ST = 0: the plain row-major triangle order.
+__device__ __forceinline__ void tri_of(int t, int& ti, int& tj) {
+  ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
+  while (ti * (ti + 1) / 2 > t) --ti;
+  tj = t - ti * (ti + 1) / 2;
+}
+
+__device__ __forceinline__ void tile_of(int tile, int nt, int ST, int& ti, int& tj) {
+  if (ST <= 1 || nt <= ST) {
+    tri_of(tile, ti, tj);
+    return;
+  }
+  // walk the supertile rows: block row I holds I full ST x ST blocks (J < I) and one diagonal block
+  const int nbr = (nt + ST - 1) / ST;
+  int base = 0;
+  for (int I = 0; I < nbr; ++I) {
+    const int rows = (I + 1) * ST <= nt ? ST : nt - I * ST;  // tile rows in this block row
+    const int rlo = I * ST;
+    // tiles of block row I: sum over its rows r of (r + 1) = the rows' triangle widths
+    const int in_row = rows * rlo + rows * (rows + 1) / 2;
+    if (tile >= base + in_row) {
+      base += in_row;
+      continue;
+    }
+    const int off = tile - base;
+    const int full = I * ST * rows;  // the I full blocks (J < I), each rows x ST tiles
+    if (off < full) {
+      const int J = off / (rows * ST), o = off % (rows * ST);
+      ti = rlo + o / ST;
+      tj = J * ST + o % ST;
+    } else {
+      int a, b;
+      tri_of(off - full, a, b);  // the diagonal block: a lower triangle of rows x rows tiles
+      ti = rlo + a;
+      tj = rlo + b;
+    }
+    return;
+  }
+  ti = tj = 0;  // unreachable for tile < ntiles
+}
+
 // NT threads = NT/64 waves arranged WR x 2; a wave owns a (BT/WR) x (BT/2) sub-tile of MFMA tiles.
 template <int BT, int NT>
 struct GramTile {
@@ -42,7 +90,7 @@ __global__ void __launch_bounds__(NT)
 gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int m, int d,
                 int ntiles, int ksplit, long rows_per_split,
                 double* __restrict__ A, double* __restrict__ B, double* __restrict__ YY,
-                double* __restrict__ slab) {
+                double* __restrict__ slab, int nt, int ST) {
   using T = GramTile<BT, NT>;
   // two LDS buffers (double buffering): slab s is read from buffer s&1 while slab s+1 is written
   // into the other one, so each K step needs ONE LDS-only barrier and the staging stores issue
@@ -58,11 +106,8 @@ gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int 
   const int split = rest % ksplit;
   const int n = rest / ksplit;
 
-  // lower-triangular tile id -> (ti, tj), ti >= tj
-  int ti = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
-  while ((ti + 1) * (ti + 2) / 2 <= tile) ++ti;
-  while (ti * (ti + 1) / 2 > tile) --ti;
-  const int tj = tile - ti * (ti + 1) / 2;
+  int ti, tj;
+  tile_of(tile, nt, ST, ti, tj);
   const bool diag = (ti == tj);
   const int row0 = ti * BT, col0 = tj * BT;
 
@@ -199,12 +244,10 @@ gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int 
 template <int BT>
 __global__ void __launch_bounds__(256)
 gram_reduce_kernel(const double* __restrict__ slab, int d, int ntiles, int ksplit,
-                   double* __restrict__ A, double* __restrict__ B, double* __restrict__ YY) {
+                   double* __restrict__ A, double* __restrict__ B, double* __restrict__ YY, int nt, int ST) {
   const int tile = blockIdx.x, n = blockIdx.y;
-  int ti = (int)((sqrt(8.0 * tile + 1.0) - 1.0) * 0.5);
-  while ((ti + 1) * (ti + 2) / 2 <= tile) ++ti;
-  while (ti * (ti + 1) / 2 > tile) --ti;
-  const int tj = tile - ti * (ti + 1) / 2;
+  int ti, tj;
+  tile_of(tile, nt, ST, ti, tj);
   const int D = d + 1;
   const double* s = slab + ((long)n * ntiles + tile) * ksplit * (BT * BT);
   for (int e = threadIdx.x; e < BT * BT; e += blockDim.x) {
@@ -239,15 +282,19 @@ int launch_gram(const double* X, const double* Y, int N, int m, int d, int kspli
   const long nwg = (long)ntiles * ksplit * N;
   static const int nt_env = getenv("GADMM_GRAM_NT") ? atoi(getenv("GADMM_GRAM_NT")) : 0;  // A/B switch
   const int nthr = nt_env == 256 || nt_env == 512 ? nt_env : (BT == 128 ? 512 : 256);
+  // supertile order (tile_of): 8 x 8 blocks of tiles, 64 tiles = one XCD's resident workgroups (2 per
+  // CU x 32 CUs); GADMM_GRAM_ST overrides (0: row-major triangle order, the round-2 schedule)
+  static const int st_env = getenv("GADMM_GRAM_ST") ? atoi(getenv("GADMM_GRAM_ST")) : -1;
+  const int ST = st_env >= 0 ? st_env : 8;
   if (nthr == 512)
     hipLaunchKernelGGL((gram_aug_kernel<BT, 512>), dim3((unsigned)nwg), dim3(512), 0, st, X, Y, m, d, ntiles, ksplit,
-                       rows, A, B, YY, slab);
+                       rows, A, B, YY, slab, nt, ST);
   else
     hipLaunchKernelGGL((gram_aug_kernel<BT, 256>), dim3((unsigned)nwg), dim3(256), 0, st, X, Y, m, d, ntiles, ksplit,
-                       rows, A, B, YY, slab);
+                       rows, A, B, YY, slab, nt, ST);
   if (ksplit > 1) {
     hipLaunchKernelGGL(gram_reduce_kernel<BT>, dim3(ntiles, N), dim3(256), 0, st, slab, d, ntiles,
-                       ksplit, A, B, YY);
+                       ksplit, A, B, YY, nt, ST);
   }
   GADMM_CHECK(hipGetLastError());
   return 0;

@@ -394,6 +394,8 @@ class NativeChainEngine:
         b = self._desc.base
         g.X, g.Y, g.m, g.max_inner = native.ptr(self.X), native.ptr(self.Y), self.m, int(b.max_inner)
         g.lam, g.step, g.inner_tol = float(b.lam), float(b.step), float(b.inner_tol)
+        if self.local_solver == "newton":
+            g.step = self.chord  # the persistent Newton kernel's chord contraction threshold
         g.inner_iters = self.inner_iters.data_ptr()
         return g
 
@@ -403,13 +405,20 @@ class NativeChainEngine:
         if self.nranks != 1 and fabric is None:
             return False
         if self.model == "logistic":
-            # inner-GD logistic in one launch (chain_persistent_logistic.hip): one wave per worker
-            if self.local_solver != "gd" or max(self.d, self.m) > 64:
+            # logistic in one launch: inner GD (chain_persistent_logistic.hip, one wave per worker) or
+            # exact Newton (chain_persistent_newton.hip: a solver wave + a 4-wave crew that rebuilds the
+            # inverse Hessian off the critical path; d, m <= 52; GADMM_NEWTON_PERSISTENT=0: graph engine)
+            if max(self.d, self.m) > 64:
                 return False
             pa = native.PersistArgs()
             pa.d, pa.n, pa.sys_scope = self.d, self.n_total, 1 if fabric is not None else 0
             g = self._logi_args()
-            cap = int(self.lib.gadmm_chain_persistent_logistic_capacity(ctypes.byref(pa), ctypes.byref(g)))
+            if self.local_solver == "newton":
+                if os.environ.get("GADMM_NEWTON_PERSISTENT", "1") == "0":
+                    return False
+                cap = int(self.lib.gadmm_chain_persistent_newton_capacity(ctypes.byref(pa), ctypes.byref(g)))
+            else:
+                cap = int(self.lib.gadmm_chain_persistent_logistic_capacity(ctypes.byref(pa), ctypes.byref(g)))
             return self.n_local + 1 <= cap
         if self.model != "linear":
             return False
@@ -674,10 +683,14 @@ class NativeChainEngine:
             if plan is None and self.model == "logistic":
                 if epochs is not None:
                     raise RuntimeError("persistent logistic kernel: static chains only")
-                self.last_kernel = "per-worker-logistic"
                 self._logi = self._logi_args()
-                rc = int(self.lib.gadmm_chain_persistent_logistic_launch(ctypes.byref(pa), ctypes.byref(self._logi),
-                                                                         self.stream.cuda_stream))
+                if self.local_solver == "newton":
+                    self.last_kernel = "per-worker-newton"
+                    launch = self.lib.gadmm_chain_persistent_newton_launch
+                else:
+                    self.last_kernel = "per-worker-logistic"
+                    launch = self.lib.gadmm_chain_persistent_logistic_launch
+                rc = int(launch(ctypes.byref(pa), ctypes.byref(self._logi), self.stream.cuda_stream))
                 if rc == -2:
                     raise ResidencyError(self.lib.gadmm_last_error().decode())
                 native.check(rc, "chain_persistent_logistic_launch")

@@ -187,6 +187,9 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_chain_persistent_logistic_launch": (c_int, [ctypes.POINTER(PersistArgs), ctypes.POINTER(LogiArgs),
                                                            c_void_p]),
         "gadmm_logi_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
+        "gadmm_chain_persistent_newton_capacity": (c_long, [ctypes.POINTER(PersistArgs), ctypes.POINTER(LogiArgs)]),
+        "gadmm_chain_persistent_newton_launch": (c_int, [ctypes.POINTER(PersistArgs), ctypes.POINTER(LogiArgs),
+                                                         c_void_p]),
         "gadmm_write_stamp": (c_int, [c_void_p, c_void_p]),
         "gadmm_star_capacity": (c_long, [ctypes.POINTER(StarArgs)]),
         "gadmm_star_launch": (c_int, [ctypes.POINTER(StarArgs), c_void_p]),

@@ -30,7 +30,7 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize("N,m,d", [(24, 50, 50), (5, 25, 14), (3, 36, 34), (2, 5000, 70), (2, 300, 200),
-                                   (1, 40000, 20)])
+                                   (1, 40000, 20), (1, 1500, 1100), (2, 700, 2100)])
 def test_gram_kernel_matches_torch(N, m, d):
     from gadmm_amd.ops import linalg
     g = torch.Generator().manual_seed(N * 1000 + d)
@@ -190,18 +190,24 @@ def test_engine_logistic(log24, log_obj0):
     assert eng.run(use_graph=False).iters == 53
 
 
-@pytest.mark.parametrize("chord", [0.0, 0.02, 0.1])
-def test_logistic_newton_kernel_matches_torch(log24, log_obj0, chord):
-    """Exact local solves on the device (chain_newton.hip: MFMA Hessian, in-place block Gauss-Jordan
-    inverse; chord = 0: a fresh inverse every Newton step, chord > 0: the worker's cached inverse is
-    reused while steps contract by that factor) vs the torch Newton path on the same device: the
-    1e-8 gap at the same iteration and objective traces equal to ~1e-12."""
+@pytest.mark.parametrize("chord,persistent", [(0.0, False), (0.02, False), (0.1, False), (0.0, True), (0.02, True),
+                                              (0.1, True)])
+def test_logistic_newton_kernel_matches_torch(log24, log_obj0, chord, persistent):
+    """Exact local solves on the device vs the torch Newton path on the same device: the
+    1e-8 gap at the same iteration and objective traces equal to ~1e-12. persistent = False: the graph
+    engine's phase kernels (chain_newton.hip: MFMA Hessian, in-place block Gauss-Jordan inverse);
+    persistent = True: ONE launch (chain_persistent_newton.hip: a solver wave runs the chord steps, a
+    4-wave crew rebuilds the inverse Hessian at the worker's previous iterate off the critical path).
+    chord = 0: a fresh inverse every Newton step; chord > 0: the inverse is reused while steps contract
+    by that factor."""
     import time
     from gadmm_amd.models import LogisticRegression
     from gadmm_amd.algorithms.gadmm import group_admm_logistic_exact
     m = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
-    a = group_admm_logistic_exact(m, 1e-3, log_obj0, 1e-8, 1000, engine_opts={"chord": chord, "cache": False})
+    a = group_admm_logistic_exact(m, 1e-3, log_obj0, 1e-8, 1000,
+                                  engine_opts={"chord": chord, "cache": False, "persistent": persistent})
     assert a.extra["backend"] == "native" and a.extra["solver"] == "newton"
+    assert (a.extra["engine"] == "persistent") == persistent, a.extra["engine"]
     eng = a.extra["engine_obj"]
     used = eng.inner_iters.cpu().numpy()
     assert 1 <= used.min() and used.max() < 50  # Newton converged inside its cap on every worker
@@ -211,8 +217,8 @@ def test_logistic_newton_kernel_matches_torch(log24, log_obj0, chord):
     assert b.extra["backend"] == "torch"
     assert a.iters == b.iters == 424 and a.converged and b.converged
     np.testing.assert_allclose(a.obj, b.obj, rtol=1e-12, atol=0)
-    print("newton(chord=%g): native %.1f ms, torch %.1f ms, %d iterations"
-          % (chord, a.wall_s * 1e3, t_torch * 1e3, a.iters))
+    print("newton(chord=%g, persistent=%s): native %.1f ms, torch %.1f ms, %d iterations"
+          % (chord, persistent, a.wall_s * 1e3, t_torch * 1e3, a.iters))
 
 
 def test_lds_poison_lands():
