@@ -296,6 +296,9 @@ def run_other(args, rank, world, device, share):
         for k, v in r.items():
             if k not in out and k not in ("ms", "iters", "expected", "metric", "config"):
                 out[k] = v
+        from gadmm_amd.benchmarks import LAST_STEPS
+        for k, v in LAST_STEPS.items():
+            out.setdefault(k, v)
         print(json.dumps(out), flush=True)
     if comm is not None and hasattr(comm, "close"):
         comm.close()

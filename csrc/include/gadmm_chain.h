@@ -15,7 +15,9 @@ struct ChainCtl {
   int pending;     // heads' end-of-iteration dual update still to apply (lazy dual, see phase kernel)
   unsigned ticket; // arrival counter of the current phase kernel
   int monitored;   // last iteration whose global objective has been checked
-  int pad[2];
+  int placed;      // persistent kernels' XCD placement (PersistArgs::xcd): 0 not packed, 1 packed
+                  // (blocks b % 8 dealt) but not verified on one XCD (system-scope stores), 2 verified
+  int pad;
 };
 
 // One slot of a phase plan: the local worker that updates in this phase and its chain neighbours.

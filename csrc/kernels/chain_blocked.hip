@@ -183,6 +183,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   const long etab_base = 2L * n * 2 * d + (long)a.ring * n * d;
   bool local = false;  // publish with plain stores (every block verified on this XCD)
   if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, W + Wo + 1, deadline, &stop_iter_lds);
+  if (!SYS && bid == 0 && threadIdx.x == 0) a.ctl->placed = a.xcd > 0 ? (local ? 2 : 1) : 0;
 
   if (bid == W + Wo) {
     blocked_monitor<SYS, TL>(a, lds, v, lane, deadline, rob, bid);

@@ -79,6 +79,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
   lds_barrier();
   bool local = false;  // publish with plain stores (every block verified on this XCD)
   if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds);
+  if (!SYS && bid == 0 && threadIdx.x == 0) a.ctl->placed = a.xcd > 0 ? (local ? 2 : 1) : 0;
 
   if (a.has_monitor && bid == a.n_local) {
     // ---------------------------------------------------------------- monitor workgroup

@@ -51,6 +51,7 @@ __global__ void __launch_bounds__(64) chain_persistent_logistic_kernel(PersistAr
   const int bid = packed ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   bool local = false;  // publish with plain stores (every block verified on this XCD)
   if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds);
+  if (!SYS && bid == 0 && threadIdx.x == 0) a.ctl->placed = a.xcd > 0 ? (local ? 2 : 1) : 0;
 
   if (a.has_monitor && bid == a.n_local) {
     // ---------------------------------------------------------------- monitor (one wave)

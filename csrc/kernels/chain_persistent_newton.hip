@@ -39,7 +39,12 @@ struct LogiArgs {  // == chain_persistent_logistic.hip (one ABI for both persist
 
 namespace {
 
-constexpr int NT = 320;       // wave 0 solver + 4 crew waves
+// Wave layout: 6 waves, dealt round-robin to the CU's 4 SIMDs (wave w -> SIMD w % 4): wave 0 is the
+// solver, wave 4 (its SIMD mate) leaves right after the set-up, so the solver's SIMD runs nothing
+// else; waves 1, 2, 3, 5 are the crew (crew index 0..3). A crew wave on the solver's SIMD would take
+// its f64 issue slots during every refresh (measured: 3.3 us per chord step with a 5-wave layout).
+constexpr int NT = 384;
+__device__ __forceinline__ int crew_index(int wid) { return wid == 5 ? 3 : wid - 1; }  // wid in {1,2,3,5}
 constexpr int CREW = 4;
 constexpr int NCW = 64 / CREW;  // Gauss-Jordan: columns per crew lane (j = cw + CREW c)
 constexpr int NMAX = 50;      // Newton step cap (== models/logistic.py:newton_prox)
@@ -50,14 +55,18 @@ constexpr int HS = 65;        // LDS Hessian row stride
 
 // LDS layout (doubles)
 struct NLds {
-  int xs, hs, qb0, qb1, wq, slab, stage, total;
+  int xt, hs, qb0, qb1, qb2, wq, slab, stage, total;
+  __host__ __device__ int buf(int r) const { return qb0 + (r % 3) * QB; }
   __host__ __device__ NLds(int m, int d) {
-    const int dp = (d + 3) & ~3;
-    xs = 0;                        // X [m][dp] (crew: Hessian operands)
-    hs = xs + ((m * dp + 1) & ~1); // Hessian [64][HS]
+    (void)m;
+    (void)d;
+    xt = 0;                        // X^T in the quad-LDS layout: the solver's gradient GEMV and the
+                                   // crew's Hessian operands (X itself stays in the solver's VGPRs)
+    hs = xt + QB;                  // Hessian [64][HS]
     qb0 = ((hs + 64 * HS + 1) & ~1);
-    qb1 = qb0 + QB;                // two inverse buffers (quad-LDS layout: quad_gemv_lds)
-    wq = qb1 + QB;                 // [64] w_i = sigma (1 - sigma) at the refresh point
+    qb1 = qb0 + QB;                // three inverse buffers (quad-LDS layout: quad_gemv_lds): the one in
+    qb2 = qb1 + QB;                // use, a background refresh in progress, an urgent refresh
+    wq = qb2 + QB;                 // [64] w_i = sigma (1 - sigma) at the refresh point
     slab = wq + 64;                // [2][4][64] Gauss-Jordan pivot-column slabs
     stage = slab + 512;            // [QSTAGE] solver quad GEMV staging
     total = stage + QSTAGE;
@@ -68,7 +77,7 @@ struct NCtl {        // LDS words of the solver <-> crew protocol
   int req;           // last refresh requested (solver; -1: quit)
   int ready;         // last refresh completed (crew)
   int cnt;           // crew barrier counter
-  int pad;
+  int src;           // refresh mode: -1 Gauss-Jordan; r >= 0: one Newton-Schulz step from refresh r's inverse
   double shift;      // lam + deg rho of the requested refresh
 };
 
@@ -106,14 +115,26 @@ __device__ __forceinline__ double rcp_nr(double v) {  // v_rcp_f64 + one Newton-
   return fma(r, fma(-v, r, 1.0), r);
 }
 
-// One refresh by the crew (waves 1-4, cw = 0..3): Hs = X^T diag(wq) X + shift I (MFMA), in-place block
-// Gauss-Jordan inverse in registers, written to the quad-LDS buffer `qb`. Every LDS word read here is
-// written first (padding included): the result never depends on stale LDS.
+// element (row, col) of a quad-LDS inverse buffer (quad_gemv_lds<QT> layout; columns >= 4 (QT + 1) are 0)
+__device__ __forceinline__ int qidx(int row, int col) {
+  const int r = row >> 4, iq = row & 15, c4 = col & 3, t = col >> 2;
+  return ((t >> 1) * 4 + r) * 128 + 2 * (iq + 16 * c4) + (t & 1);
+}
+constexpr int QCOLS = 4 * (QT + (QT & 1));
+
+// One refresh by the crew (crew index cw = 0..3): Hs = X^T diag(wq) X + shift I (MFMA), then the inverse
+// into the quad-LDS buffer `qb`, either
+//   src == nullptr: in-place block Gauss-Jordan in registers (exact), or
+//   src != nullptr: ONE Newton-Schulz step from the inverse X0 in `src` (the one the solver uses):
+//       X1 = X0 (2 I - H X0) = 2 X0 - X0 (H X0),   I - H X1 = (I - H X0)^2
+//   two 64 x 64 x 64 f64 MFMA products, no pivot chain. X0 was exact for a nearby Hessian (the
+//   worker's previous point), so its residual is small and squaring it gives a chord preconditioner
+//   far better than the stale inverse, at a fraction of the Gauss-Jordan cost.
+// Every LDS word read here is written first (padding included): the result never depends on stale LDS.
 __device__ void crew_refresh(double* lds, const NLds& L, int m, int d, double shift, int cw, int* cnt, int& gen,
-                             double* qb, long long* tl) {
+                             double* qb, long long* tl, const double* src) {
   const int lane = threadIdx.x & 63;
-  const int dp = (d + 3) & ~3;
-  const double* Xs = lds + L.xs;
+  const double* XT = lds + L.xt;  // X^T, quad-LDS layout: X[k][j] = XT[qidx(j, k)] (0 beyond d / m)
   double* Hs = lds + L.hs;
   const double* wq = lds + L.wq;
   {  // Hessian tiles (R, C = cw), R = 0..3: v_mfma_f64_16x16x4f64, K = samples in chunks of 4
@@ -126,12 +147,10 @@ __device__ void crew_refresh(double* lds, const NLds& L, int m, int d, double sh
       const int kk = k0 + k4;
       const bool kin = kk < m;
       const double w = kin ? wq[kk] : 0.0;
-      const double* xr = Xs + (kin ? kk : 0) * dp;
-      const double bv = (kin && cc < dp) ? xr[cc] : 0.0;
+      const double bv = kin ? XT[qidx(cc, kk)] : 0.0;
 #pragma unroll
       for (int R = 0; R < 4; ++R) {
-        const int ca = 16 * R + c16;
-        const double av = ca < dp ? w * xr[ca] : 0.0;
+        const double av = kin ? w * XT[qidx(16 * R + c16, kk)] : 0.0;
         acc[R] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[R], 0, 0, 0);
       }
     }
@@ -148,6 +167,52 @@ __device__ void crew_refresh(double* lds, const NLds& L, int m, int d, double sh
   }
   crew_sync(cnt, gen);
   if (tl && cw == 0 && lane == 0) tl[1] = (long long)__builtin_amdgcn_s_memrealtime();
+  if (src) {
+    const int k4 = lane >> 4, c16 = lane & 15;
+    const int cc = 16 * cw + c16;
+    f64x4 acc[4];
+    // T = H X0: tiles (R, C = cw); A[i][k] = H[16R + i][k], B[k][j] = X0[k][16 cw + j]
+#pragma unroll
+    for (int R = 0; R < 4; ++R) acc[R] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0; k0 < 64; k0 += 4) {
+      const int kk = k0 + k4;
+      const double bv = cc < QCOLS ? src[qidx(kk, cc)] : 0.0;
+#pragma unroll
+      for (int R = 0; R < 4; ++R) acc[R] = __builtin_amdgcn_mfma_f64_16x16x4f64(Hs[(16 * R + c16) * HS + kk], bv,
+                                                                               acc[R], 0, 0, 0);
+    }
+    crew_sync(cnt, gen);  // every crew wave is done reading H: T goes where H was
+#pragma unroll
+    for (int R = 0; R < 4; ++R)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) Hs[(16 * R + k4 + 4 * reg) * HS + cc] = acc[R][reg];
+    crew_sync(cnt, gen);
+    // U = X0 T: A[i][k] = X0[16R + i][k], B[k][j] = T[k][16 cw + j]; X1 = 2 X0 - U
+#pragma unroll
+    for (int R = 0; R < 4; ++R) acc[R] = f64x4{0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0; k0 < 64; k0 += 4) {
+      const int kk = k0 + k4;
+      const double bv = Hs[kk * HS + cc];
+#pragma unroll
+      for (int R = 0; R < 4; ++R) {
+        const double av = kk < QCOLS ? src[qidx(16 * R + c16, kk)] : 0.0;
+        acc[R] = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc[R], 0, 0, 0);
+      }
+    }
+    if (tl && cw == 0 && lane == 0) tl[2] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (cc < QCOLS) {
+#pragma unroll
+      for (int R = 0; R < 4; ++R)
+#pragma unroll
+        for (int reg = 0; reg < 4; ++reg) {
+          const int row = 16 * R + k4 + 4 * reg;
+          const int q = qidx(row, cc);
+          qb[q] = (row < d && cc < d) ? 2.0 * src[q] - acc[R][reg] : 0.0;
+        }
+    }
+    crew_sync(cnt, gen);
+    return;
+  }
   // in-place block Gauss-Jordan (SPD, no pivoting), 4 x 4 pivot blocks; lane i of crew wave cw keeps row
   // i's columns j = cw + 4c. Block K = p..p+3: P = A_KK, non-pivot rows L_i = A_iK P^-1, A_ij -= L_i A_Kj,
   // A_iK = -L_i; pivot rows A_Kj = P^-1 A_Kj, A_KK = P^-1. Only column K is published; the pivot rows
@@ -289,16 +354,18 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
   const double rho = a.rho, lam = g.lam, chord = g.step;
   const double shift = lam + rho * (double)((left >= 0 ? 1 : 0) + (right >= 0 ? 1 : 0));
   const double* Xg = g.X + (long)li * m * d;
-  const int dp = (d + 3) & ~3;
-  // shared set-up: X into LDS (crew Hessian operands), protocol words
-  for (int e = threadIdx.x; e < m * dp; e += NT) {
-    const int r = e / dp, c = e - r * dp;
-    lds[L.xs + e] = c < d ? Xg[(long)r * d + c] : 0.0;
+  // shared set-up: X^T into LDS in the quad-LDS layout (element (row j, col i) = X[i][j]), protocol words
+  for (int e = threadIdx.x; e < QB; e += NT) {
+    const int blk = e >> 7, within = e & 127;
+    const int r = blk & 3, th = blk >> 2, lq = within >> 1, t = 2 * th + (within & 1);
+    const int row = (lq & 15) + 16 * r, col = (lq >> 4) + 4 * t;  // row: feature j, col: sample i
+    lds[L.xt + e] = (row < d && col < m && t < QT) ? Xg[(long)col * d + row] : 0.0;
   }
   if (threadIdx.x == 0) {
     nc.req = 0;
     nc.ready = -1;
     nc.cnt = 0;
+    nc.src = -1;  // refresh 0: Gauss-Jordan
     nc.shift = shift;
   }
   // refresh 0 is built at the worker's start point theta^{start - 1}: w_i = sigma(z_i)(1 - sigma(z_i)),
@@ -316,9 +383,10 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
   }
   lds_barrier();  // the only workgroup-wide barrier: solver and crew run decoupled from here on
 
+  if (wid == 4) return;  // keeps the solver's SIMD free
   if (wid > 0) {
-    // ---------------------------------------------------------------- crew (waves 1-4)
-    const int cw = wid - 1;
+    // ---------------------------------------------------------------- crew (waves 1, 2, 3, 5)
+    const int cw = crew_index(wid);
     const int li_ = sl.li;
     int gen = 0, done_req = -1;
     for (;;) {
@@ -333,7 +401,9 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
       // instrumented runs (PersistArgs::timeline, [n_local][128][8] stamps): refreshes 0..63 in rows 0..63
       long long* tl = (a.timeline && r < 64) ? a.timeline + ((long)li_ * 128 + r) * 8 : nullptr;
       if (tl && cw == 0 && lane == 0) tl[0] = (long long)__builtin_amdgcn_s_memrealtime();
-      crew_refresh(lds, L, m, d, nc.shift, cw, &nc.cnt, gen, lds + ((r & 1) ? L.qb1 : L.qb0), tl);
+      const int srcr = nc.src;  // written before the request (release / acquire on nc.req)
+      crew_refresh(lds, L, m, d, nc.shift, cw, &nc.cnt, gen, lds + L.buf(r), tl,
+                   srcr >= 0 ? lds + L.buf(srcr) : nullptr);
       if (tl && cw == 0 && lane == 0) tl[3] = (long long)__builtin_amdgcn_s_memrealtime();
       if (cw == 0 && lane == 0) lds_store_rel(&nc.ready, r);
       done_req = r;
@@ -342,7 +412,9 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
 
   // ------------------------------------------------------------------ solver (wave 0)
   double* st = lds + L.stage;
-  double Xq[4][QT], XTq[4][QT];
+  // X in VGPRs (margins), X^T from LDS (gradient): both in registers would be 208 VGPRs and spill
+  double Xq[4][QT];
+  const double* XTl = lds + L.xt;
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
@@ -350,7 +422,6 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
       const int qi = lane & 15, qc = lane >> 4;
       const int row = qi + 16 * r, col = qc + 4 * t;
       Xq[r][t] = (row < m && col < d) ? Xg[(long)row * d + col] : 0.0;
-      XTq[r][t] = (col < m && row < d) ? Xg[(long)col * d + row] : 0.0;
     }
   u32x4* const p0 = a.push ? a.push[2 * bid] : nullptr;
   u32x4* const p1 = a.push ? a.push[2 * bid + 1] : nullptr;
@@ -364,11 +435,18 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
   double tr = (inj && right >= 0) ? a.theta[(long)right * d + lane] : 0.0;
   int pending = a.pending_in;
   int stop_code = 0, stop_iter = 0, abort = 0, used = 0;
-  // the refresh this worker's next solve starts from; request 0 (at the start point) is live from the
-  // set-up on: the crew waits for nc.req to differ from its last finished request (-1 at first)
-  int req = 0;
-  bool req_fresh = true;  // refresh `req` was requested at the start point of the next solve
-  const int bg_steps = (g.max_inner >= 1 && g.max_inner < NMAX) ? g.max_inner : 4;
+  // Inverse bookkeeping (refresh ids are consecutive; refresh r lives in buffer r % 3):
+  //   cur   the inverse the chord steps use (refresh 0, at the start point, requested in the set-up)
+  //   pend  a background refresh in progress (-1: none), requested at iteration pend_it at the
+  //         worker's final iterate; adopted at the active phase of iteration pend_it + RLAG (waiting
+  //         for it if the crew is not done), so the crew gets RLAG - 1 whole iterations of slack
+  //   urgent refreshes (a step that contracts by less than `chord`) are waited for at once
+  // Every choice depends on the iterates only: deterministic.
+  constexpr int RLAG = 2;
+  int cur = 0, pend = -1, pend_it = 0, next_id = 0;
+  bool cur_fresh = true;  // `cur` was built at the start point of the next solve
+  const int bg_steps = (g.max_inner >= 1 && g.max_inner < NMAX) ? g.max_inner : 1;
+  const bool ns_bg = g.inner_tol >= 0.0;  // LogiArgs::inner_tol < 0: background refreshes by Gauss-Jordan
   auto wait_ready = [&](int r) -> bool {
     for (int spin = 0;; ++spin) {
       if (lds_load_acq(&nc.ready) >= r) return true;
@@ -432,17 +510,24 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
     const int kk_tl = it - a.start_iter;
     long long* tls = (a.timeline && kk_tl < 64) ? a.timeline + ((long)li * 128 + 64 + kk_tl) * 8 : nullptr;
     if (tls && lane == 0) tls[0] = (long long)__builtin_amdgcn_s_memrealtime();
-    if (!wait_ready(req)) { abort = 1; break; }
+    if (pend >= 0 && it - pend_it >= RLAG) {  // adopt the background refresh
+      if (!wait_ready(pend)) { abort = 1; break; }
+      cur = pend;
+      pend = -1;
+      cur_fresh = false;
+    }
+    if (!wait_ready(cur)) { abort = 1; break; }
     if (tls && lane == 0) tls[1] = (long long)__builtin_amdgcn_s_memrealtime();
-    const double* hq = lds + ((req & 1) ? L.qb1 : L.qb0);
+    const double* hq = lds + L.buf(cur);
     double nd_prev = 0.0;
     used = 0;
     bool urgent = false;
-    bool fresh = req_fresh;  // the inverse in use was built at this solve's start point
+    bool fresh = cur_fresh;  // the inverse in use was built at this solve's start point
+    cur_fresh = false;
     for (int k = 0; k < NMAX; ++k) {
       const double z = quad_gemv<QT>(Xq, x, st);                     // margins
       const double ps = ini ? 1.0 / (1.0 + exp(yv * z)) : 0.0;        // sigma(-y z)
-      const double gx = quad_gemv<QT>(XTq, ini ? yv * ps : 0.0, st);  // (X^T (y . sigma))_j
+      const double gx = quad_gemv_lds<QT>(XTl, ini ? yv * ps : 0.0, st);  // (X^T (y . sigma))_j
       const double gr = inj ? -gx + shift * x + cv : 0.0;
       const double dx = quad_gemv_lds<QT>(hq, gr, st);
       const double dxl = inj ? dx : 0.0;
@@ -455,11 +540,17 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
         const double z2 = quad_gemv<QT>(Xq, x, st);
         const double p2 = ini ? 1.0 / (1.0 + exp(yv * z2)) : 0.5;
         lds[L.wq + lane] = ini ? p2 * (1.0 - p2) : 0.0;
-        ++req;
-        post(req);
+        if (pend >= 0) {  // the crew first finishes the background refresh (adopted: it is newer)
+          if (!wait_ready(pend)) { abort = 1; break; }
+          cur = pend;
+          pend = -1;
+        }
+        cur = ++next_id;
+        nc.src = -1;  // exact: Gauss-Jordan at the current x
+        post(cur);
         urgent = true;
-        if (!wait_ready(req)) { abort = 1; break; }
-        hq = lds + ((req & 1) ? L.qb1 : L.qb0);
+        if (!wait_ready(cur)) { abort = 1; break; }
+        hq = lds + L.buf(cur);
         fresh = true;
         nd_prev = 0.0;
         continue;
@@ -471,7 +562,7 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
     if (tls && lane == 0) {
       tls[2] = (long long)__builtin_amdgcn_s_memrealtime();
       tls[3] = used;
-      tls[4] = req;
+      tls[4] = next_id;
     }
     // -- publish theta^it: own table + the remote neighbours' tables (first: the neighbours wait)
     const unsigned tag = make_tag(a.epoch, it);
@@ -508,13 +599,12 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
     // background refresh at the new iterate only when this solve says the inverse is ageing (more
     // than bg_steps chord steps, or an urgent refresh): the crew then works while the other group
     // solves, and otherwise stays idle -- a busy crew shares this CU's SIMDs and LDS with the solver
-    req_fresh = false;
-    if (used > bg_steps || urgent) {
-      if (!wait_ready(req)) { abort = 1; break; }  // the crew is idle again (it always is here)
+    if ((used > bg_steps || urgent) && pend < 0) {  // the crew is idle (no refresh outstanding)
       lds[L.wq + lane] = ini ? pz * (1.0 - pz) : 0.0;
-      ++req;
-      post(req);
-      req_fresh = true;
+      pend = ++next_id;
+      pend_it = it;
+      nc.src = ns_bg ? cur : -1;  // background: one Newton-Schulz step from the inverse in use
+      post(pend);
     }
   }
   lds_store_rel(&nc.req, -1);  // crew: quit (after its current refresh, if any)

@@ -114,9 +114,13 @@ def _timed(solve: Callable, steps: int, warmup: int, device, world: int):
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
+    stamps, placed = [], []
     t0 = time.perf_counter()
     for _ in range(steps):
         last = solve()
+        stamps.append(time.perf_counter())
+        eng = getattr(last, "extra", {}).get("engine_obj") if hasattr(last, "extra") else None
+        placed.append(getattr(eng, "last_placed", None))
     torch.cuda.synchronize(device)
     t1 = time.perf_counter()
     if world > 1:
@@ -126,7 +130,20 @@ def _timed(solve: Callable, steps: int, warmup: int, device, world: int):
         t = torch.tensor([ms], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         ms = float(t.item())
+    # per-step wall times (this rank; the persistent engines synchronise inside every solve) and the
+    # XCD placement each launch got (ChainCtl::placed): an outlier mean is attributable from the record
+    per = np.diff(np.asarray([t0] + stamps)) * 1e3
+    LAST_STEPS.clear()
+    if len(per):
+        LAST_STEPS.update({"step_ms_min": round(float(per.min()), 4), "step_ms_median": round(float(np.median(per)), 4),
+                           "step_ms_max": round(float(per.max()), 4)})
+        if any(p is not None for p in placed):
+            LAST_STEPS["xcd_placement_counts"] = {str(k): int(sum(1 for p in placed if p == k))
+                                                  for k in sorted({p for p in placed if p is not None})}
     return ms, last
+
+
+LAST_STEPS: Dict = {}  # per-step statistics of the last _timed run (bench.py adds them to its JSON line)
 
 
 def run_logistic(args, rank, world, device, comm) -> Dict:

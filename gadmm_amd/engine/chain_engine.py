@@ -721,6 +721,7 @@ class NativeChainEngine:
         self.last_timeline_slots = [(s.gid, p) for s, p in zip(slots, pos)] if tl is not None else None
         c = self._ctl_host.tolist()
         done, conv, nxt = c[1], c[2], c[0]
+        self.last_placed = c[6]  # ChainCtl::placed: the XCD packing this launch got (0 / 1 / 2)
         if done == 4:
             raise HandoffTimeout("persistent chain kernel timed out (hand-off never completed)")
         # a chunk that ran to its hard stop: count iterations start..hard_stop (only the monitor rank

@@ -18,6 +18,17 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
+@pytest.fixture(autouse=True)
+def _poison_lds():
+    """NaN-filled LDS on every CU before each test (as tests/test_gpu.py): a kernel reading LDS it did
+    not write fails deterministically."""
+    import torch
+    if torch.cuda.is_available():
+        from gadmm_amd.ops import native
+        native.poison_lds()
+    yield
+
+
 def _single(lin24, rho, tol, **opts):
     import torch
     from gadmm_amd.models import LinearRegression
@@ -474,3 +485,34 @@ def test_first_order_chain_and_iag_across_ranks(world, lin24):
     R = world - 1
     assert res[0]["DGD"]["rows"] == 2 * R * iters
     assert res[0]["cIAG"]["rows"] == (iters - 1) * R  # one scheduled upload per iteration from the 2nd
+
+
+def _ipc_delay_rank(rank, world, timeout_s):
+    import torch
+    import torch.distributed as dist
+    from gadmm_amd.benchmarks import headline_rank_problem
+    from gadmm_amd.engine.multigpu import DistributedChainSolver
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    X, y, loc, pl, obj0 = headline_rank_problem(24, rank, world)
+    sol = DistributedChainSolver(X.to(dev), y.to(dev), loc, 24, pl, rank, world, dev, 3.0, obj0, 1e-8, share=True,
+                                 timeout_s=timeout_s, engine="graph")
+    if rank == 1:
+        sol.delay_next_s = 3.0 * timeout_s  # rank 0's exchanges give up on this solve
+    first = sol.guarded_solve()
+    dist.barrier()
+    second = sol.guarded_solve()
+    res = {"kind": sol.kind, "first": first.done, "second": (second.iters, second.done)}
+    sol.close()
+    return res
+
+
+def test_ipc_graph_engine_recovers_after_a_stalled_solve():
+    """after one IPC-transport solve that timed out (a rank arrived late), the next solve on
+    the same transport must work. The all-gather sequence word diverged across ranks on a timeout and
+    every later solve timed out too; a new epoch now restarts it on every rank (ipc_xport.hip)."""
+    from gadmm_amd.parallel.launch import spawn
+    res = spawn(_ipc_delay_rank, 2, 2.0, timeout=300)
+    assert all(r["kind"] == "ipc" for r in res)
+    assert any(r["first"] == 4 for r in res)  # the stalled solve did time out somewhere
+    assert all(r["second"] == (1373, 1) for r in res), res

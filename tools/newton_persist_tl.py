@@ -18,20 +18,24 @@ def main():
     ap.add_argument("--rho", type=float, default=1e-3)
     ap.add_argument("--bg", type=int, default=0, help="background-refresh step threshold (0: kernel default)")
     ap.add_argument("--sweep", action="store_true")
+    ap.add_argument("--gj", action="store_true", help="background refreshes by Gauss-Jordan (not Newton-Schulz)")
     args = ap.parse_args()
     if args.sweep:
-        for chord in (0.02, 0.1, 0.3):
-            for bg in (2, 4, 8):
-                run(chord, bg, args.rho, brief=True)
+        for gj in (False, True):
+            for chord in (0.02, 0.1, 0.3):
+                for bg in (1, 2):
+                    run(chord, bg, args.rho, gj, brief=True)
         return
-    run(args.chord, args.bg, args.rho)
+    run(args.chord, args.bg, args.rho, args.gj)
 
 
-def run(chord, bg, rho, brief=False):
+def run(chord, bg, rho, gj=False, brief=False):
     class A:
         pass
     args = A()
     args.chord, args.bg, args.rho = chord, bg, rho
+    if brief:
+        print("[%s] " % ("gj" if gj else "ns"), end="")
     from gadmm_amd.data import logistic_synthetic
     from gadmm_amd.engine.chain_engine import NativeChainEngine
     from gadmm_amd.models import LogisticRegression
@@ -43,19 +47,23 @@ def run(chord, bg, rho, brief=False):
     obj0 = logistic_optimum(Xf.numpy(), yf.numpy(), 24 * 1e-5)
     eng = NativeChainEngine(ds.X.to(dev), ds.y.to(dev), list(range(24)), 24, "logistic", rho=args.rho, obj0=obj0,
                             tol=1e-8, max_iter=2000, lam=1e-5, local_solver="newton", chord=args.chord,
-                            max_inner=args.bg if args.bg > 0 else 100)
+                            max_inner=args.bg if args.bg > 0 else 100, inner_tol=-1.0 if gj else 1e-4)
     eng.set_path(list(range(24)), Placement.contiguous(24, 1), 0)
-    ms = []
-    for rep in range(3):
-        eng.reset()
-        r = eng.run_persistent(timeline_iters=0 if (brief and rep < 2) else 128)
-        ms.append(r.wall_ms)
-        if not brief:
-            print("solve %d: %d iterations, done %d, %.2f ms" % (rep, r.iters, r.done, r.wall_ms))
     if brief:
+        ms = []
+        for rep in range(3):
+            eng.reset()
+            r = eng.run_persistent()
+            ms.append(r.wall_ms)
+        print("chord %.2f bg %d: %d iterations, %.2f ms (median of 3, timeline off), " % (chord, bg, r.iters,
+                                                                                         float(np.median(ms))), end="")
         eng.reset()
-        r = eng.run_persistent()
-        print("chord %.2f bg %d: %d iterations, %.2f ms (timeline off), " % (chord, bg, r.iters, r.wall_ms), end="")
+        eng.run_persistent(timeline_iters=128)
+    else:
+        for rep in range(3):
+            eng.reset()
+            r = eng.run_persistent(timeline_iters=128)
+            print("solve %d: %d iterations, done %d, %.2f ms" % (rep, r.iters, r.done, r.wall_ms))
     tl = eng.last_timeline[:24, :128, :].astype(np.float64)
     cr = tl[:, :64, :]
     ok = cr[:, :, 3] > 0
