@@ -273,7 +273,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     # D-GADMM re-runs) reuse its device buffers, cached inverses and captured graph
     key = (kind, local_solver, n_total, tuple(int(w) for w in local_ids), float(rho), int(max_iter), block,
            float(step), int(max_inner), float(inner_tol), float(getattr(model, "lam", 0.0)),
-           float(opts.get("chord", 0.02)), bool(opts.get("residual", True)))
+           opts.get("chord"), bool(opts.get("residual", True)))
     cache = getattr(model, "_chain_engines", None) if rcomm is None else None
     eng = cache.get(key) if cache is not None else None
     fresh = eng is None
@@ -282,7 +282,8 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
                                 max_iter=max_iter, lam=getattr(model, "lam", 0.0), step=step, max_inner=max_inner,
                                 inner_tol=inner_tol, comm=rcomm, block=block, precomputed=pre,
                                 local_solver="newton" if local_solver == "newton" else "gd",
-                                chord=float(opts.get("chord", 0.02)), residual=bool(opts.get("residual", True)),
+                                chord=None if opts.get("chord") is None else float(opts["chord"]),
+                                residual=bool(opts.get("residual", True)),
                                 obj_mode=str(opts.get("obj_mode", "auto")))
         if rcomm is None and opts.get("cache", True):
             if cache is None:

@@ -73,11 +73,14 @@ class NativeChainEngine:
                  max_iter: int = 1000, lam: float = 0.0, step: float = 0.0, max_inner: int = 100,
                  inner_tol: float = 1e-4, comm=None, block: int = 16, stream: Optional[torch.cuda.Stream] = None,
                  precomputed=None, force_monitor: bool = False, obj_mode: str = "auto", local_solver: str = "gd",
-                 chord: float = 0.02, residual: bool = False, xcd: int = 2):
+                 chord: Optional[float] = None, residual: bool = False, xcd: int = 2):
         """``local_solver`` (logistic): "gd" = the reference's inexact inner GD (logReg_GD.m, step /
         max_inner / inner_tol), "newton" = exact local solves (group_ADMM_logistic.m semantics,
         csrc/kernels/chain_newton.hip; d, m <= 64). ``chord`` (newton): a worker reuses its last
-        inverse Hessian while steps contract by at least this factor (0: refresh every step).
+        inverse Hessian while steps contract by at least this factor (0: refresh every step); None = the
+        engine's default: 0.02 for the graph engine's phase kernels, 0.3 for the persistent kernel, whose
+        crew refreshes the inverse in the background anyway (tools/newton_persist_tl.py --sweep: 424
+        iterations at every setting, 9.31 / 8.00 / 7.87 ms at 0.02 / 0.1 / 0.3, profiles/r03_newton).
         ``obj_mode`` (graph / large-d phases): "exact" evaluates f_n = 1/2 th'A th - b'th + 1/2 y'y with a
         second GEMV by the Gram, "identity" uses A th = r - deg rho th from the solve itself (no second
         pass; at d > 256 that pass re-streams an 800 MB Gram per worker-phase), "auto" = identity at
@@ -146,7 +149,8 @@ class NativeChainEngine:
             # Newton: per-worker inverse Hessian store (register image + valid flag + shift)
             self.hinv = torch.zeros((nl, 64 * 64 + 8), dtype=f64, device=dev) \
                 if local_solver == "newton" and nl > 0 else None
-            self.chord = float(chord)
+            self.chord = 0.02 if chord is None else float(chord)
+            self.chord_persistent = 0.3 if chord is None else float(chord)
             self.xcd = int(xcd)
             # K4 primal residual: per (iteration, worker) contributions of the tails (owned rows only)
             self.rres = torch.zeros((self.max_iter * self.n_total,), dtype=f64, device=dev) if residual else None
@@ -395,7 +399,7 @@ class NativeChainEngine:
         g.X, g.Y, g.m, g.max_inner = native.ptr(self.X), native.ptr(self.Y), self.m, int(b.max_inner)
         g.lam, g.step, g.inner_tol = float(b.lam), float(b.step), float(b.inner_tol)
         if self.local_solver == "newton":
-            g.step = self.chord  # the persistent Newton kernel's chord contraction threshold
+            g.step = self.chord_persistent  # the persistent Newton kernel's chord contraction threshold
         g.inner_iters = self.inner_iters.data_ptr()
         return g
 

@@ -191,7 +191,7 @@ def test_engine_logistic(log24, log_obj0):
 
 
 @pytest.mark.parametrize("chord,persistent", [(0.0, False), (0.02, False), (0.1, False), (0.0, True), (0.02, True),
-                                              (0.1, True)])
+                                              (0.1, True), (0.3, True), (None, True)])
 def test_logistic_newton_kernel_matches_torch(log24, log_obj0, chord, persistent):
     """Exact local solves on the device vs the torch Newton path on the same device: the
     1e-8 gap at the same iteration and objective traces equal to ~1e-12. persistent = False: the graph
@@ -205,7 +205,8 @@ def test_logistic_newton_kernel_matches_torch(log24, log_obj0, chord, persistent
     from gadmm_amd.algorithms.gadmm import group_admm_logistic_exact
     m = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
     a = group_admm_logistic_exact(m, 1e-3, log_obj0, 1e-8, 1000,
-                                  engine_opts={"chord": chord, "cache": False, "persistent": persistent})
+                                  engine_opts={"chord": chord, "cache": False, "persistent": persistent}
+                                  if chord is not None else {"cache": False, "persistent": persistent})
     assert a.extra["backend"] == "native" and a.extra["solver"] == "newton"
     assert (a.extra["engine"] == "persistent") == persistent, a.extra["engine"]
     eng = a.extra["engine_obj"]
@@ -217,7 +218,7 @@ def test_logistic_newton_kernel_matches_torch(log24, log_obj0, chord, persistent
     assert b.extra["backend"] == "torch"
     assert a.iters == b.iters == 424 and a.converged and b.converged
     np.testing.assert_allclose(a.obj, b.obj, rtol=1e-12, atol=0)
-    print("newton(chord=%g, persistent=%s): native %.1f ms, torch %.1f ms, %d iterations"
+    print("newton(chord=%s, persistent=%s): native %.1f ms, torch %.1f ms, %d iterations"
           % (chord, persistent, a.wall_s * 1e3, t_torch * 1e3, a.iters))
 
 

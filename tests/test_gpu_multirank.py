@@ -114,7 +114,11 @@ def _ipc_logistic_rank(rank, world, n):
     return out
 
 
-def _xgmi_logistic_rank(rank, world, n):
+# (local solver, rho, tol, max_iter, iterations of the reference config)
+_LOGI = {"gd": (2e-4, 1e-4, 400, 53), "newton": (1e-3, 1e-8, 2000, 424)}
+
+
+def _xgmi_logistic_rank(rank, world, n, solver="gd"):
     import torch
     from gadmm_amd.data import logistic_synthetic
     from gadmm_amd.models import LogisticRegression
@@ -133,9 +137,10 @@ def _xgmi_logistic_rank(rank, world, n):
     ipc = IpcComm(n, 50, 8, dev)
     obj0 = m.optimum(ipc, n_total=n)
     ipc.close()
+    rho, tol, mx, _ = _LOGI[solver]
     outs = []
     for _ in range(2):
-        r = chain_admm(m, loc, n, 2e-4, obj0, 1e-4, 400, comm=RankInfo(rank, world), placement=pl, local_solver="gd",
+        r = chain_admm(m, loc, n, rho, obj0, tol, mx, comm=RankInfo(rank, world), placement=pl, local_solver=solver,
                        step=2.2, engine_opts={"fabric": fab, "state": False})
         outs.append((r.iters, r.extra["engine"], r.bytes_sent))
     out = {"runs": outs, "trace": r.obj.tolist(), "obj0": obj0, "local": loc}
@@ -144,22 +149,25 @@ def _xgmi_logistic_rank(rank, world, n):
     return out
 
 
-@pytest.mark.parametrize("world", [2, 4])
-def test_xgmi_logistic_persistent_matches_one_gpu(world, log24):
-    """Logistic GADMM (inner GD) in one persistent launch per GPU over the xGMI fabric == one GPU,
-    bit for bit; theta payload = 2 (ranks - 1) d 8 iterations."""
+@pytest.mark.parametrize("world,solver", [(2, "gd"), (4, "gd"), (2, "newton"), (4, "newton")])
+def test_xgmi_logistic_persistent_matches_one_gpu(world, solver, log24):
+    """Logistic GADMM in one persistent launch per GPU over the xGMI fabric == one GPU, bit for bit;
+    theta payload = 2 (ranks - 1) d 8 iterations. ``gd``: the inner-GD kernel
+    (chain_persistent_logistic.hip); ``newton``: exact local solves, the solver-wave + inverse-crew
+    kernel (chain_persistent_newton.hip) to the 1e-8 gap in the reference's 424 iterations."""
     from gadmm_amd.parallel.launch import spawn
     from gadmm_amd.models import LogisticRegression
     from gadmm_amd.algorithms import chain_admm
-    res = spawn(_xgmi_logistic_rank, world, 24, timeout=300)
+    rho, tol, mx, its = _LOGI[solver]
+    res = spawn(_xgmi_logistic_rank, world, 24, solver, timeout=300)
     m = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
-    single = chain_admm(m, list(range(24)), 24, 2e-4, res[0]["obj0"], 1e-4, 400, local_solver="gd", step=2.2,
+    single = chain_admm(m, list(range(24)), 24, rho, res[0]["obj0"], tol, mx, local_solver=solver, step=2.2,
                         engine_opts={"cache": False})
-    assert single.iters == 53
+    assert single.iters == its and single.extra["engine"] == "persistent"
     for r in res:
-        assert all(it == 53 and eng == "persistent" for it, eng, _ in r["runs"]), r["runs"]
+        assert all(it == its and eng == "persistent" for it, eng, _ in r["runs"]), r["runs"]
         assert np.array_equal(np.asarray(r["trace"]), single.obj)
-    assert sum(r["runs"][-1][2] for r in res) == 2 * (world - 1) * 50 * 8 * 53
+    assert sum(r["runs"][-1][2] for r in res) == 2 * (world - 1) * 50 * 8 * its
 
 
 def test_ipc_transport_logistic_two_ranks(log24):

@@ -2,6 +2,7 @@ set -o pipefail
 O=gpurun_out/r3_n2
 mkdir -p $O
 . tools/gpu_step.sh
+step pingpong 60 build/pingpong
 step newton_sweep 300 python3 -u tools/newton_persist_tl.py --sweep
 step newton_tests 200 python3 -u -m pytest tests/test_gpu.py -v -k "newton" --timeout 120 --timeout-method thread
 step bench_lx 200 python3 -u bench.py --config logistic_exact --steps 10 --warmup 2
