@@ -17,7 +17,6 @@
 // f64 MFMA fragment maps (cdna_hip_programming.md §3): A/B one f64 per lane, A[i=l&15][k=l>>4],
 // B[k=l>>4][j=l&15]; C/D col = l&15, row = (l>>4) + 4*reg.
 #include <stdlib.h>
-#include <string.h>
 #include "gadmm_common.h"
 
 namespace {
@@ -241,130 +240,6 @@ gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int 
       }
 }
 
-// Barrier-free variant (GADMM_GRAM_KERNEL=stream, A/B): no LDS staging. Every wave streams its own
-// MFMA fragments straight from global memory (L1/L2 serve the rows its workgroup's other waves
-// also read) through a P-deep register ring: the operands of K4 step s + P are loaded while step s's
-// MFMAs issue, and the compiler's counted `vmcnt` waits only for the step it consumes. The LDS
-// kernel above spends ~39 % of its wave cycles parked in waits (barrier per 16-row slab + staging
-// drain; profiles/r03_gram, SQ_WAIT_ANY) with the MFMA pipe ~71 % busy. Same tiles, wave layout and
-// epilogue; rows past the split's end are clamped loads selected to 0 (the ring runs to a multiple
-// of P steps, the extra steps add zeros).
-template <int BT, int NT, int P, bool INTERIOR>
-__device__ __forceinline__ void gram_stream_loop(const double* __restrict__ H, const double* __restrict__ yv, int d,
-                                                 long kbeg, long kend, int ca0, int cb0,
-                                                 f64x4 (&acc)[GramTile<BT, NT>::TMR][GramTile<BT, NT>::TMC]) {
-  using T = GramTile<BT, NT>;
-  const int lane = threadIdx.x & 63, k4 = lane >> 4;
-  double sa[P][T::TMR], sb[P][T::TMC];
-  auto load = [&](int s, long k) {
-    const long kr = k + k4;
-    const bool kin = kr < kend;
-    const long kc = kin ? kr : kend - 1;
-    const double* src = H + kc * (long)d;
-#pragma unroll
-    for (int t = 0; t < T::TMR; ++t) {
-      const int c = ca0 + t * 16;
-      double v;
-      if (INTERIOR) {
-        v = src[c];
-      } else {
-        const double h = src[c < d ? c : d - 1];
-        v = c < d ? h : (c == d ? yv[kc] : 0.0);
-      }
-      sa[s][t] = kin ? v : 0.0;
-    }
-#pragma unroll
-    for (int t = 0; t < T::TMC; ++t) {
-      const int c = cb0 + t * 16;
-      double v;
-      if (INTERIOR) {
-        v = src[c];
-      } else {
-        const double h = src[c < d ? c : d - 1];
-        v = c < d ? h : (c == d ? yv[kc] : 0.0);
-      }
-      sb[s][t] = kin ? v : 0.0;
-    }
-  };
-#pragma unroll
-  for (int s = 0; s < P; ++s) load(s, kbeg + 4 * s);
-  const long steps = (kend - kbeg + 3) / 4;
-  for (long st = 0; st < steps; st += P) {
-#pragma unroll
-    for (int s = 0; s < P; ++s) {
-#pragma unroll
-      for (int x = 0; x < T::TMR; ++x)
-#pragma unroll
-        for (int y = 0; y < T::TMC; ++y)
-          acc[x][y] = __builtin_amdgcn_mfma_f64_16x16x4f64(sa[s][x], sb[s][y], acc[x][y], 0, 0, 0);
-      load(s, kbeg + 4 * (st + s + P));
-    }
-  }
-}
-
-template <int BT, int NT, int P>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4)))  // 2 workgroups per CU: <= 128 VGPRs
-gram_stream_kernel(const double* __restrict__ X, const double* __restrict__ Y, int m, int d,
-                   int ntiles, int ksplit, long rows_per_split,
-                   double* __restrict__ A, double* __restrict__ B, double* __restrict__ YY,
-                   double* __restrict__ slab, int nt, int ST) {
-  using T = GramTile<BT, NT>;
-  const int nwg = gridDim.x;
-  const int gid = xcd_remap(blockIdx.x, nwg);
-  const int tile = gid % ntiles;
-  const int rest = gid / ntiles;
-  const int split = rest % ksplit;
-  const int n = rest / ksplit;
-  int ti, tj;
-  tile_of(tile, nt, ST, ti, tj);
-  const bool diag = (ti == tj);
-  const int row0 = ti * BT, col0 = tj * BT;
-  const double* H = X + (long)n * m * d;
-  const double* yv = Y + (long)n * m;
-  const long kbeg = (long)split * rows_per_split;
-  long kend = kbeg + rows_per_split;
-  if (kend > m) kend = m;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-  const int D = d + 1;
-  f64x4 acc[T::TMR][T::TMC];
-#pragma unroll
-  for (int a = 0; a < T::TMR; ++a)
-#pragma unroll
-    for (int b = 0; b < T::TMC; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
-  const int ca0 = row0 + wr * T::WTR + (lane & 15), cb0 = col0 + wc * T::WTC + (lane & 15);
-  const bool cols_in = (row0 + BT <= d) && (diag || col0 + BT <= d);
-  if (kbeg < kend) {
-    if (cols_in) gram_stream_loop<BT, NT, P, true>(H, yv, d, kbeg, kend, ca0, cb0, acc);
-    else gram_stream_loop<BT, NT, P, false>(H, yv, d, kbeg, kend, ca0, cb0, acc);
-  }
-#pragma unroll
-  for (int x = 0; x < T::TMR; ++x)
-#pragma unroll
-    for (int yq = 0; yq < T::TMC; ++yq)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int lr = wr * T::WTR + x * 16 + (lane >> 4) + 4 * reg;
-        const int lc = wc * T::WTC + yq * 16 + (lane & 15);
-        const double v = acc[x][yq][reg];
-        if (ksplit > 1) {
-          slab[(((long)n * ntiles + tile) * ksplit + split) * (BT * BT) + lr * BT + lc] = v;
-          continue;
-        }
-        const int r = row0 + lr, c = col0 + lc;
-        if (r >= D || c >= D || c > r) continue;
-        if (r < d && c < d) {
-          double* An = A + (long)n * d * d;
-          An[(long)r * d + c] = v;
-          An[(long)c * d + r] = v;
-        } else if (r == d && c < d) {
-          B[(long)n * d + c] = v;
-        } else if (r == d && c == d) {
-          YY[n] = v;
-        }
-      }
-}
-
 // Fixed-order reduction of the split-K slabs + symmetric scatter into (A, b, yy).
 template <int BT>
 __global__ void __launch_bounds__(256)
@@ -411,25 +286,7 @@ int launch_gram(const double* X, const double* Y, int N, int m, int d, int kspli
   // (tile_of: 8 x 8 blocks of tiles), measured 0.5 % slower at 2 x 625000 x 10000 (profiles/r03_gram)
   static const int st_env = getenv("GADMM_GRAM_ST") ? atoi(getenv("GADMM_GRAM_ST")) : -1;
   const int ST = st_env >= 0 ? st_env : 0;
-  // GADMM_GRAM_KERNEL = stream2 / stream3 / stream4: the barrier-free kernel with that ring depth
-  static const int stream_p = [] {
-    const char* e = getenv("GADMM_GRAM_KERNEL");
-    if (!e || strncmp(e, "stream", 6) != 0) return 0;
-    const int p = e[6] ? atoi(e + 6) : 3;
-    return p >= 2 && p <= 4 ? p : 3;
-  }();
-  bool streamed = false;
-  if constexpr (BT == 128) {
-    if (stream_p > 0) {
-      auto fn = stream_p == 2 ? gram_stream_kernel<BT, 512, 2> : stream_p == 4 ? gram_stream_kernel<BT, 512, 4>
-                                                                               : gram_stream_kernel<BT, 512, 3>;
-      hipLaunchKernelGGL(fn, dim3((unsigned)nwg), dim3(512), 0, st, X, Y, m, d, ntiles, ksplit, rows, A, B, YY, slab, nt,
-                         ST);
-      streamed = true;
-    }
-  }
-  if (streamed) {
-  } else if (nthr == 512)
+  if (nthr == 512)
     hipLaunchKernelGGL((gram_aug_kernel<BT, 512>), dim3((unsigned)nwg), dim3(512), 0, st, X, Y, m, d, ntiles, ksplit,
                        rows, A, B, YY, slab, nt, ST);
   else
