@@ -42,6 +42,7 @@ int gadmm_chain_blocked_plan(int n, int d, int want_k, int* k_out, int* len_out)
 long gadmm_chain_blocked_tab_granules(int n, int d, int ring);
 int gadmm_chain_blocked_launch(const PersistArgs* a, hipStream_t st);
 int gadmm_fo_launch(const FoArgs* a, void* stream);
+long gadmm_fo_tab_granules(int n, int d, int slots);
 long gadmm_spd_inverse_blocked_workspace(int d, int nb);
 int gadmm_spd_inverse_blocked_f64(const double* A, const double* shift_host, int N, int d, int nvar, double* out,
                                   double* ws, int* status, int nb, hipStream_t st);
@@ -549,7 +550,11 @@ void gpu_checks() {
     fa.A = A;
     fa.b = b;
     fa.yy = yy;
-    u32x4* tab = dalloc<u32x4>((size_t)2 * N * d);
+    fa.slots = 2;  // one GPU: every worker's row per iteration, lock-step readers
+    fa.nranks = 1;
+    fa.n_local = N;
+    fa.has_monitor = 1;
+    u32x4* tab = dalloc<u32x4>((size_t)gadmm_fo_tab_granules(N, d, fa.slots));
     u32x4* part = dalloc<u32x4>((size_t)64 * N * 2);
     double* ot = dalloc<double>(iters);
     double* ct = dalloc<double>(iters);
@@ -563,6 +568,8 @@ void gpu_checks() {
     fa.time_trace = tt;
     fa.theta_out = tho;
     fa.ctl = fc;
+    fa.wmon = &fc->monitored;  // one GPU: the run-wide words are the control block's
+    fa.wstop = &fc->stop_iter;
     EXPECT(gadmm_fo_launch(&fa, st) == 0, "fo launch");
     HIPOK(hipStreamSynchronize(st));
     const FoCtl c = fetch(fc, 1)[0];
