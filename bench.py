@@ -45,6 +45,7 @@ import os
 import sys
 import time
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -141,10 +142,11 @@ def run_headline(args, rank, world, device, share):
     torch.cuda.synchronize(device)
     if world > 1:
         dist.barrier()
-    results = []
+    results, stamps = [], []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         results.append(sol.guarded_solve())
+        stamps.append(time.perf_counter())  # every solve ends in its own stream sync (per-step record)
     torch.cuda.synchronize(device)
     t1 = time.perf_counter()
     if world > 1:
@@ -169,6 +171,7 @@ def run_headline(args, rank, world, device, share):
     tr = sol.objective_trace(iters)
     gap = abs(float(tr[iters - 1]) - obj0) if iters > 0 else float("nan")
     data_local = sol.blk is None or sol.blk.data_local
+    per = np.diff(np.asarray([t0] + stamps)) * 1e3  # this rank's per-step wall times
     if rank == 0:
         value = ms / 1e3
         out = {
@@ -203,6 +206,9 @@ def run_headline(args, rank, world, device, share):
             "replicated_shard_bytes": repl,
             "p2p_messages_per_iteration": chain_message_count(list(range(args.workers)), placement),
             "us_per_iteration": round(ms * 1e3 / max(iters, 1), 3),
+            "step_ms_min": round(float(np.min(per)), 4) if len(per) else None,
+            "step_ms_median": round(float(np.median(per)), 4) if len(per) else None,
+            "step_ms_max": round(float(np.max(per)), 4) if len(per) else None,
             "engine": sol.engine_name(),
             "kernel": sol.kernel,
             "fabric": sol.kind,
