@@ -184,5 +184,16 @@ struct PersistArgs {
   // dl_tab[0] / [1]: blk_tab of the rank owning seg_lo - 1 / seg_hi + 1 (null at the chain ends).
   int blk_dl, pad_dl;
   u32x4* dl_tab[2];
+  // D-GADMM in the blocked kernel (DYN): the cached inverses zero-padded to [n_local][nvar][64][52]
+  // (rows >= d and columns >= d zero), so a re-chain reloads a position's inverse with 52 unmasked
+  // loads: the bounds masks of a d x d reload are loop-invariant, and hoisted out of the main loop
+  // they held ~100 SGPRs for the whole solve (spilled into VGPR lanes, which spilled the inverse
+  // itself to scratch in every GEMV). Null outside DYN.
+  const double* minv_pad;
+  // DYN: per (epoch, chain position) the OLD chain neighbours (worker ids, -1: none) of the worker
+  // the epoch puts there, when that worker was a head of the old chain (its pending dual is flushed
+  // with them at the re-chain), as int pairs [n_epochs][n][2]. Built on the host, so a re-chain
+  // issues two independent table loads instead of a chain of three dependent ones.
+  const int* ep_flush;
 };
 constexpr int XCHK = 256;  // placement-check granules (>= workgroups of any XCD-packed launch)

@@ -48,6 +48,10 @@ __device__ __forceinline__ void blocked_monitor(const PersistArgs& a, double* ld
   if (v != 0) return;
   double* vals = lds;  // [n]
   for (int it = a.start_iter;; ++it) {
+    if (a.hard_stop > 0 && it > a.hard_stop) {  // D-GADMM chunk exhausted without a stop decision
+      if (lane == 0) a.ctl->done = 5;
+      return;
+    }
     const unsigned tag = make_tag(a.epoch, it);
     const int slot = it % a.ring;
     bool okall = true;
@@ -79,6 +83,10 @@ __device__ __forceinline__ void blocked_monitor(const PersistArgs& a, double* ld
       }
       const unsigned long long dv = ((unsigned long long)tag << 32) | code;
       for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
+      if (code && a.hard_stop > 0) {  // chunked: the workers may reach the hard stop before seeing it
+        a.ctl->done = (int)code;
+        a.ctl->conv_iter = it;
+      }
       const int kk = it - a.start_iter;
       if (TL && kk < a.timeline_iters) a.timeline[((long)bid * a.timeline_iters + kk) * 8] = (long long)now_ticks();
     }
@@ -103,12 +111,15 @@ __device__ __forceinline__ void blocked_objective(const PersistArgs& a, double* 
   double* xo = lds + v * QSTAGE;
   int ep = 0, next_start = (DYN && a.n_epochs > 1) ? a.epoch_start[1] : 0x7fffffff;
   for (int it = a.start_iter;; ++it) {
+    if (a.hard_stop > 0 && it > a.hard_stop) return;  // D-GADMM chunk end: no theta^it comes
     if constexpr (DYN) {
       if (it == next_start) {  // D-GADMM re-chain: another worker now sits at position q
         ++ep;
         next_start = ep + 1 < a.n_epochs ? a.epoch_start[ep + 1] : 0x7fffffff;
         so = a.ep_slots[(long)ep * n + q];
-        quad_load<QT>(Aq, a.A + (long)so.li * d * d, d, true);
+        int od = d;  // laundered: the reload's bounds masks are not hoisted out of the loop (SGPRs)
+        asm volatile("" : "+s"(od));
+        quad_load<QT>(Aq, a.A + (long)so.li * od * od, od, true);
         bo = in ? a.b[(long)so.li * d + lane] : 0.0;
         hy = 0.5 * a.yy[so.li];
       }
@@ -289,6 +300,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   };
   unsigned long long dv_pref = 0;  // decision wave, lane 0: decision[it + 1 - lag] prefetched
   int it = a.start_iter;
+  bool hard_stopped = false;
   long long ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   // Objective-ring posts of owned workers go out in the phase their wave idles in: heads post
   // theta^it during the tail phase, tails post theta^{it-1} at the start of iteration it
@@ -334,6 +346,10 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       ring_defer = false;
     }
     if (it > a.max_iter + a.lag) break;
+    if (a.hard_stop > 0 && it > a.hard_stop) {  // D-GADMM chunk end: state = after the hard stop
+      hard_stopped = true;
+      break;
+    }
     const bool stamp = TL && v == 0 && it - a.start_iter < a.timeline_iters;  // wave-uniform (SGPR stamps)
     if (stamp) ts[0] = (long long)now_ticks();
     if constexpr (DYN) {
@@ -349,12 +365,20 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         next_start = ep + 1 < a.n_epochs ? a.epoch_start[ep + 1] : 0x7fffffff;
         if (active) {
           sl = a.ep_slots[(long)ep * n + p];
+          // the new worker's old-chain neighbours when it was a head (pending-dual flush), -1: none
+          const int2 of = reinterpret_cast<const int2*>(a.ep_flush)[(long)ep * n + p];
           li = sl.li;
           w = sl.gid;
-          const int po = a.ep_pos[(long)(ep - 1) * n + w];       // the worker's old position
-          const PhaseSlot so = a.ep_slots[(long)(ep - 1) * n + po];
-          const bool flush = pending && (po % 2) == 0;           // it was a head: dual pending
-          const bool fl = flush && so.left >= 0, fr = flush && so.right >= 0;
+          {  // the new worker's inverse (zero-padded image, unmasked loads) and b: issued before the
+             // state poll below, so their latency overlaps the hand-off
+            const double* Mp = a.minv_pad + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)(64 * DB);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+#pragma unroll
+              for (int t = 0; t < QT; ++t) Mq[r][t] = Mp[((lane & 15) + 16 * r) * DB + (lane >> 4) + 4 * t];
+            bb = in ? a.b[(long)li * d + lane] : 0.0;
+          }
+          const bool fl = pending && of.x >= 0, fr = pending && of.y >= 0;  // it was a head: dual pending
           double t0 = 0.0, t1 = 0.0, tl = 0.0, tr = 0.0;
           bool ok = true;
           for (int spin = 0;; ++spin) {
@@ -363,8 +387,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
               const long b0 = eb + (long)w * 2 * d;
               g0 &= load_granule<SYS>(rtab, (int)((b0 + lane) * 16), tag, &t0);
               g0 &= load_granule<SYS>(rtab, (int)((b0 + d + lane) * 16), tag, &t1);
-              if (fl) g0 &= load_granule<SYS>(rtab, (int)((eb + (long)so.left * 2 * d + lane) * 16), tag, &tl);
-              if (fr) g0 &= load_granule<SYS>(rtab, (int)((eb + (long)so.right * 2 * d + lane) * 16), tag, &tr);
+              if (fl) g0 &= load_granule<SYS>(rtab, (int)((eb + (long)of.x * 2 * d + lane) * 16), tag, &tl);
+              if (fr) g0 &= load_granule<SYS>(rtab, (int)((eb + (long)of.y * 2 * d + lane) * 16), tag, &tr);
             }
             if (__all(g0)) break;
             if ((spin & 7) == 7 && now_ticks() > deadline) {
@@ -379,8 +403,6 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
           if (fl) m = m - rho * (tl - th);  // the old chain's end-of-iteration dual
           if (fr) m = m + rho * (th - tr);
           mu = in ? m : 0.0;
-          bb = in ? a.b[(long)li * d + lane] : 0.0;
-          quad_load<QT>(Mq, a.Minv + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)d * d, d, true);
           thS[u * 64 + lane] = th;
         }
         pending = 0;
@@ -563,6 +585,9 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       a.ctl->iter = it;
       a.ctl->pending = 1;
       a.ctl->monitored = stop_iter_lds;
+    } else if (g == 0 && hard_stopped) {  // done / conv_iter come from the monitor
+      a.ctl->iter = it;
+      a.ctl->pending = 1;
     }
   }
 }
@@ -891,6 +916,10 @@ int gadmm_chain_blocked_plan2(int n, int d, int want_k, int want_pw, int* k_out,
   return W;
 }
 
+// Row length of PersistArgs::minv_pad for dimension d (the kernel instantiation's DB): the padded
+// inverse image is [n_local][nvar][64][pad_dim].
+int gadmm_chain_blocked_pad_dim(int d) { return d <= 32 ? 32 : 52; }
+
 // Plan of the data-local multi-GPU mode for a segment of nseg positions: one workgroup computing the
 // whole segment when it fits the 12 waves (no intra-rank exchange at all: k = 2^20 never comes), else
 // the one-GPU plan inside the segment (k = 2, owned runs of L, halos clipped at the segment edges).
@@ -983,8 +1012,10 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   const void* fn;
   const bool tl = a.timeline != nullptr;
   if (a.n_epochs > 0) {  // D-GADMM in one launch: one GPU, 12-wave layout, no instrumentation
-    if (multi || tl || a.sys_scope || !a.epoch_start || !a.ep_slots || !a.ep_pos) {
-      gadmm_set_error("blocked chain kernel: dynamic epochs need one GPU, epoch tables, no timeline");
+    if (multi || tl || a.sys_scope || !a.epoch_start || !a.ep_slots || !a.ep_pos || !a.minv_pad || !a.ep_flush ||
+        a.hard_stop < 0 || (a.hard_stop > 0 && a.hard_stop < a.start_iter)) {
+      gadmm_set_error("blocked chain kernel: dynamic epochs need one GPU, epoch tables, the padded inverses "
+                      "(gadmm_chain_blocked_pad_dim), no timeline");
       return -1;
     }
     fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, false, false, true>

@@ -327,7 +327,8 @@ int gadmm_abi_layout(long long* out, int n) {
                    (long long)sizeof(PersistArgs), (long long)offsetof(PersistArgs, rho),
                    (long long)offsetof(PersistArgs, ctl), (long long)offsetof(PhaseArgs, lgid),
                    (long long)offsetof(EngineDesc, xport), (long long)offsetof(PersistArgs, xchk),
-                   (long long)offsetof(PersistArgs, dl_tab)};
+                   (long long)offsetof(PersistArgs, dl_tab), (long long)offsetof(PersistArgs, minv_pad),
+                   (long long)offsetof(PersistArgs, ep_flush)};
   const int k = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n && i < k; ++i) out[i] = v[i];
   return k;

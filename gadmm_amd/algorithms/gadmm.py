@@ -367,8 +367,6 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             chunk = max(16, int(hints[hint_key]) + 8)
         else:
             chunk = 128
-        if eng.dynamic_uses_blocked(fabric):  # the blocked kernel's dynamic mode runs every epoch in one launch
-            chunk = len(rechains) + 1
         saved = schedule.save()
         E_total = 1 + len(rechains)
         # epoch e's chain is row e of one (E_total, N) table, filled as chains are drawn (epoch 0: the

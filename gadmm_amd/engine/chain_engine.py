@@ -67,6 +67,26 @@ def epoch_tables_numpy(P: np.ndarray, loc: np.ndarray):
     return slots, k.astype(np.int32)
 
 
+def epoch_flush_table(P: np.ndarray, pos_of: Optional[np.ndarray] = None) -> np.ndarray:
+    """(E, n, 2) int32: for epoch e >= 1 and chain position p, the OLD-chain neighbours (worker ids,
+    -1 = none) of the worker that epoch e places at p, if that worker was a head of epoch e - 1's
+    chain (a head's end-of-iteration dual is still pending at the re-chain and is flushed with them,
+    dynamic_group_ADMM_closedForm.m:153-168); -1 everywhere for tails and for epoch 0. ``P``: (E, n)
+    position -> worker; ``pos_of``: its inverse permutation per row (computed if None)."""
+    P = np.asarray(P, dtype=np.int64)
+    E, n = P.shape
+    if pos_of is None:
+        pos_of = np.argsort(P, axis=1)
+    fl = np.full((E, n, 2), -1, dtype=np.int32)
+    if E > 1:
+        po = np.take_along_axis(pos_of[:-1], P[1:], axis=1)  # the new worker's old position
+        was_head = (po % 2) == 0
+        fl[1:, :, 0] = np.where(was_head & (po > 0), np.take_along_axis(P[:-1], np.maximum(po - 1, 0), axis=1), -1)
+        fl[1:, :, 1] = np.where(was_head & (po < n - 1),
+                                np.take_along_axis(P[:-1], np.minimum(po + 1, n - 1), axis=1), -1)
+    return fl
+
+
 class NativeChainEngine:
     def __init__(self, X_loc: torch.Tensor, y_loc: torch.Tensor, local_ids: Sequence[int], n_total: int,
                  model: str = "linear", rho: float = 1.0, obj0: float = 0.0, tol: float = 1e-4,
@@ -437,9 +457,9 @@ class NativeChainEngine:
         return 0 if int(self.lib.gadmm_chain_persistent_lds(self.d, 0)) > 0 else 1
 
     def dynamic_uses_blocked(self, fabric=None) -> bool:
-        """Whether a one-launch D-GADMM run takes the blocked kernel's dynamic mode (opt-in
-        GADMM_BLOCKED_DYN=1, one GPU, 12-wave layout) rather than the per-worker kernel. Only the
-        per-worker kernel runs epoch chunks (hard stop + continuation)."""
+        """Whether a one-launch D-GADMM run takes the blocked kernel's dynamic mode (GADMM_BLOCKED_DYN=1,
+        one GPU, 12-wave layout) rather than the per-worker kernel. Both run epoch chunks (hard stop +
+        continuation)."""
         plan = self.blocked_plan(fabric) if self.model == "linear" else None
         return (plan is not None and plan[3] == 1 and self.n_local == self.n_total
                 and os.environ.get("GADMM_BLOCKED_DYN", "0") == "1")
@@ -499,12 +519,9 @@ class NativeChainEngine:
         elif not self.persistent_eligible(fabric):
             raise RuntimeError("persistent kernel not eligible for this engine/config")
         plan = self.blocked_plan(fabric, timeline=timeline_iters > 0) if self.model == "linear" else None
-        if epochs is not None and (not self.dynamic_uses_blocked(fabric) or timeline_iters > 0 or hard_stop > 0
-                                   or cont):
-            # D-GADMM: the blocked kernel's dynamic mode (opt-in GADMM_BLOCKED_DYN=1; one GPU, 12-wave
-            # layout) is bit-identical but not faster: its epoch state pushes the kernel past the
-            # SGPR budget (165 SGPR + 10 VGPR spills in the hot loop), 1.616 vs 1.623 ms per solve
-            # (profiles/r01c_dgadmm_blocked)
+        if epochs is not None and (not self.dynamic_uses_blocked(fabric) or timeline_iters > 0):
+            # D-GADMM on the per-worker kernel unless the blocked kernel's dynamic mode is selected
+            # (dynamic_uses_blocked); both run epoch chunks (hard stop + continuation)
             plan = None
         if plan is not None:
             lag = max(lag, 8)  # the objective takes one more hop (worker -> objective wave -> monitor)
@@ -615,6 +632,7 @@ class NativeChainEngine:
                 rgt = np.concatenate([P[:, 1:], np.full((E, 1), -1, dtype=np.int64)], axis=1)
                 es = np.stack([li_of[P], P, lft, rgt], axis=-1).astype(np.int32).reshape(-1)
                 pp = pos_of.astype(np.int32).reshape(-1)
+                fl = epoch_flush_table(P, pos_of).reshape(-1)  # PersistArgs::ep_flush
             else:
                 # per-worker kernel: the slot / position of every LOCAL worker per epoch (native C++
                 # builder, csrc/runtime/topology.cpp; the numpy equivalent is epoch_tables_numpy)
@@ -638,8 +656,10 @@ class NativeChainEngine:
                 pm = mask.astype(np.int32).reshape(-1)
             else:
                 pm = np.zeros((0,), dtype=np.int32)
+            if plan is None:
+                fl = np.zeros((0,), dtype=np.int32)
             ns, nes = len(starts), es.size
-            total = ns + nes + pp.size + pm.size
+            total = ns + nes + pp.size + pm.size + fl.size
             stage = getattr(self, "_ep_stage", None)
             if stage is None or stage[0].numel() < total:
                 cap = max(total, 4096)
@@ -650,12 +670,16 @@ class NativeChainEngine:
             host[:ns] = starts
             host[ns:ns + nes] = es
             host[ns + nes:ns + nes + pp.size] = pp
-            host[ns + nes + pp.size:total] = pm
+            host[ns + nes + pp.size:ns + nes + pp.size + pm.size] = pm
+            host[total - fl.size:total] = fl
             with torch.cuda.stream(self.stream):
                 stage[1][:total].copy_(stage[0][:total], non_blocking=True)
             st_t, es_t = stage[1][:ns], stage[1][ns:ns + nes]
-            pp_t, pm_t = stage[1][ns + nes:ns + nes + pp.size], stage[1][ns + nes + pp.size:total]
-            ep_keep = (st_t, es_t, pp_t, pm_t)
+            pp_t, pm_t = stage[1][ns + nes:ns + nes + pp.size], stage[1][ns + nes + pp.size:total - fl.size]
+            fl_t = stage[1][total - fl.size:total]
+            ep_keep = (st_t, es_t, pp_t, pm_t, fl_t)
+            if fl.size:
+                pa.ep_flush = fl_t.data_ptr()
             pa.n_epochs = len(starts)
             pa.epoch_start, pa.ep_slots, pa.ep_pos = st_t.data_ptr(), es_t.data_ptr(), pp_t.data_ptr()
             if fabric is not None:
@@ -672,6 +696,18 @@ class NativeChainEngine:
                 self._blk_tab = torch.zeros((ng * 4,), dtype=torch.int32, device=dev)
             pa.blk_k, pa.blk_len, pa.blk_pw = plan[0], plan[1], plan[3]
             pa.blk_tab = self._blk_tab.data_ptr()
+            if epochs is not None:
+                # D-GADMM in the blocked kernel: the inverses zero-padded to [n_local][nvar][64][DB], reloaded
+                # by every re-chain without bounds masks (PersistArgs::minv_pad); refreshed from this solve's
+                # inverses on the engine stream, ahead of the launch
+                DB = int(self.lib.gadmm_chain_blocked_pad_dim(self.d))
+                pad = getattr(self, "_minv_pad", None)
+                if pad is None or pad.shape[-1] != DB:
+                    pad = torch.zeros((self.n_local, self.nvar, 64, DB), dtype=torch.float64, device=dev)
+                    self._minv_pad = pad
+                with torch.cuda.stream(self.stream):
+                    pad[:, :, :self.d, :self.d].copy_(self.Minv.reshape(self.n_local, self.nvar, self.d, self.d))
+                pa.minv_pad = pad.data_ptr()
         self.last_kernel = ("blocked%s(k=%d,L=%d,W=%d,pw=%d)" % ((("-dyn" if epochs is not None else ""),) + tuple(plan))
                             if plan is not None else "per-worker")
         with torch.cuda.stream(self.stream):

@@ -111,7 +111,8 @@ class PersistArgs(ctypes.Structure):
         ("tstamp", c_void_p), ("ep_push", c_void_p), ("peer_thg", c_void_p), ("rres", c_void_p),
         ("hard_stop", c_int), ("cont", c_int),
         ("xchk", c_void_p), ("xcd", c_int), ("pad_xcd", c_int),
-        ("blk_dl", c_int), ("pad_dl", c_int), ("dl_tab", c_void_p * 2),
+        ("blk_dl", c_int), ("pad_dl", c_int), ("dl_tab", c_void_p * 2), ("minv_pad", c_void_p),
+        ("ep_flush", c_void_p),
     ]
 
 
@@ -204,6 +205,7 @@ def _declare(lib: ctypes.CDLL) -> None:
                                               ctypes.POINTER(c_int)]),
         "gadmm_chain_blocked_lds": (c_long, [c_int, c_int]),
         "gadmm_chain_blocked_plan_dl": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+        "gadmm_chain_blocked_pad_dim": (c_int, [c_int]),
         "gadmm_chain_blocked_tab_granules": (c_long, [c_int, c_int, c_int]),
         "gadmm_chain_blocked_tab_granules_dyn": (c_long, [c_int, c_int, c_int]),
         "gadmm_epoch_tables": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),

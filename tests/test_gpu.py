@@ -757,20 +757,25 @@ def test_logistic_persistent_kernel_matches_graph_engine(log24, log_obj0):
     assert np.all(np.diff(a.time_trace) >= 0) and a.time_trace[-1] > 0
 
 
-@pytest.mark.parametrize("coherence,chunk", [(10, 4), (1, 16)])
-def test_dgadmm_epoch_chunks_bit_identical(lin24, lin_obj0, coherence, chunk):
+@pytest.mark.parametrize("coherence,chunk,blocked", [(10, 4, "0"), (1, 16, "0"), (10, 4, "1"), (1, 16, "1"),
+                                                     (3, 5, "1")])
+def test_dgadmm_epoch_chunks_bit_identical(lin24, lin_obj0, coherence, chunk, blocked, monkeypatch):
     """D-GADMM in chunks of persistent launches (hard stop before the chunk's last+1 epoch, then a
     continuation with the same tag salt that flushes the pending head duals with the old chain) ==
     one launch holding every epoch == the epoch-by-epoch graph engine: iterations, objective trace and
-    energy trace bit for bit; only the chains the solve reaches are drawn."""
+    energy trace bit for bit; only the chains the solve reaches are drawn. blocked = "1": the
+    blocked kernel's dynamic mode (its monitor, objective and worker waves stop at the hard stop)."""
     from gadmm_amd.models import LinearRegression
     from gadmm_amd.algorithms import dynamic_group_admm
     from gadmm_amd.parallel import topology as T
+    monkeypatch.setenv("GADMM_BLOCKED_DYN", blocked)
     m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
     p0, c0, _ = T.find_path(24, np.random.default_rng(5))
     run = lambda **o: dynamic_group_admm(m, 1.0, lin_obj0, 1e-4, 3000, p0, c0, coherence, seed=99,
                                          engine_opts=dict(cache=False, **o))
     a = run(epoch_chunk=chunk)
+    kern = a.extra["engine_obj"].last_kernel
+    assert kern.startswith("blocked-dyn(") if blocked == "1" else kern == "per-worker", kern
     b = run(epoch_chunk=100000)
     e = run(persistent=False)
     assert a.extra["engine"] == b.extra["engine"] == "persistent-dynamic" and e.extra["engine"] == "epochs"

@@ -28,7 +28,8 @@ def test_abi_layout_matches_ctypes():
            native.PhaseArgs.inner_iters.offset, ctypes.sizeof(native.EngineDesc), native.EngineDesc.stream.offset,
            ctypes.sizeof(native.RunStats), ctypes.sizeof(native.PersistArgs), native.PersistArgs.rho.offset,
            native.PersistArgs.ctl.offset, native.PhaseArgs.lgid.offset, native.EngineDesc.xport.offset,
-           native.PersistArgs.xchk.offset, native.PersistArgs.dl_tab.offset]
+           native.PersistArgs.xchk.offset, native.PersistArgs.dl_tab.offset, native.PersistArgs.minv_pad.offset,
+           native.PersistArgs.ep_flush.offset]
     assert got == exp
 
 
@@ -142,3 +143,22 @@ def test_blocked_plan_fits_one_xcd():
         W = lib.gadmm_chain_blocked_plan(n, 50, 0, ctypes.byref(k), ctypes.byref(L))
         assert (k.value, L.value, W) == (2, want_L, (n + want_L - 1) // want_L), (n, k.value, L.value, W)
     assert lib.gadmm_chain_blocked_plan(24, 100, 0, ctypes.byref(k), ctypes.byref(L)) == 0  # d > 52
+
+
+def test_epoch_flush_table_matches_the_kernels_old_lookup():
+    """PersistArgs::ep_flush (built on the host) == what the blocked D-GADMM kernel used to derive at
+    every re-chain from ep_pos / ep_slots: the new worker's old neighbours iff it was an old head."""
+    import numpy as np
+    from gadmm_amd.engine.chain_engine import epoch_flush_table
+    rng = np.random.default_rng(3)
+    for E, n in ((1, 5), (6, 9), (11, 24)):
+        P = np.stack([rng.permutation(n) for _ in range(E)])
+        fl = epoch_flush_table(P)
+        pos_of = np.argsort(P, axis=1)
+        assert fl.shape == (E, n, 2) and (fl[0] == -1).all()
+        for e in range(1, E):
+            for p in range(n):
+                op = pos_of[e - 1][P[e][p]]
+                exp = (P[e - 1][op - 1] if op > 0 else -1, P[e - 1][op + 1] if op < n - 1 else -1) \
+                    if op % 2 == 0 else (-1, -1)
+                assert tuple(fl[e, p]) == exp
