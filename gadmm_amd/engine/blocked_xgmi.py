@@ -194,9 +194,14 @@ class BlockedXgmiEngine:
             gram(self.X, self.y, out=(self.A, self.b, self.yy))
             self._inverses(out=self.Minv)
 
-    def run(self, timeout_s: float = 20.0):
+    def run(self, timeout_s: float = 20.0, timeline_iters: int = 0, dbg: int = 0):
         """Reset the state and solve; returns (iters, done, wall_ms). Collective in effect (every rank
-        must run it; the kernels hand off to each other)."""
+        must run it; the kernels hand off to each other). ``timeline_iters > 0``: the instrumented
+        kernel records s_memrealtime stamps (10 ns, one clock for the chip) of the first iterations
+        into ``self.last_timeline`` (rows g: wave 0 of workgroup g [start, after exchange, -, -, after
+        the head phase, after the tail phase, before / after its head solve]; rows 128 + g: the
+        workgroup's tail wave MAXW/2 + ((dbg >> 4) & 7) [start, after its poll, after its solve, after
+        its stores, after the phase barrier]); ``dbg``: PersistArgs::dbg experiment bits."""
         import time
 
         self.epoch = self.epoch % 4095 + 1
@@ -224,6 +229,11 @@ class BlockedXgmiEngine:
         pa.blk_peer_tab = self.peer_tab_t.data_ptr()
         pa.blk_dl = 1 if self.data_local else 0
         pa.dl_tab[0], pa.dl_tab[1] = self.dl_ptrs[0] or None, self.dl_ptrs[1] or None
+        pa.dbg = int(dbg)
+        tl = None
+        if timeline_iters > 0:
+            tl = torch.zeros((256, int(timeline_iters), 8), dtype=torch.int64, device=self.device)
+            pa.timeline, pa.timeline_iters = tl.data_ptr(), int(timeline_iters)
         with torch.cuda.stream(self.stream):
             self.theta.zero_()
             self.mu.zero_()
@@ -234,6 +244,7 @@ class BlockedXgmiEngine:
             self.stream.synchronize()
             t1 = time.perf_counter()
         c = self.ctl.cpu().tolist()
+        self.last_timeline = tl.cpu().numpy() if tl is not None else None
         if c[1] == 4:
             raise RuntimeError("blocked xgmi kernel timed out (hand-off never completed)")
         return c[2], c[1], (t1 - t0) * 1e3
