@@ -925,7 +925,10 @@ int gadmm_chain_blocked_pad_dim(int d) { return d <= 32 ? 32 : 52; }
 // the one-GPU plan inside the segment (k = 2, owned runs of L, halos clipped at the segment edges).
 int gadmm_chain_blocked_plan_dl(int nseg, int d, int want_k, int* k_out, int* len_out) {
   if (d > 52 || nseg < 1) return 0;
-  if (nseg <= MAXW) {
+  // GADMM_DL_PLAN=blocked (A/B): the one-GPU plan inside the segment even when one workgroup fits it
+  const char* e = getenv("GADMM_DL_PLAN");
+  const bool force_blocked = e && e[0] == 'b' && nseg >= 2;
+  if (nseg <= MAXW && !force_blocked) {
     *k_out = 1 << 20;
     *len_out = nseg;
     return 1;
