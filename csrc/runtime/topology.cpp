@@ -109,6 +109,44 @@ extern "C" int gadmm_greedy_chains(const double* uv, int E, int n, double side, 
 // from the chains P [E][n] (position -> worker): for each local worker li (global id loc[li]) its
 // slot (li, gid, left, right) and chain position in every epoch. Replaces ~0.5 ms of numpy per
 // solve (argsort + fancy indexing over ~300 epochs) on the host path of every D-GADMM solve.
+// The blocked kernel's D-GADMM tables (one GPU, every worker local: li == worker id) from the chains
+// P [E][n]: per (epoch, chain POSITION) the slot (li, gid, left, right); per (epoch, worker) its
+// position; and per (epoch, position) the flush pair (PersistArgs::ep_flush): the old-chain
+// neighbours of the worker placed there if it was a head of the previous epoch's chain, else -1.
+// The numpy equivalent (chain_engine.py: epoch_flush_table) cost ~0.1-0.2 ms per solve.
+extern "C" int gadmm_epoch_tables_blocked(const long long* P, int E, int n, int* slots, int* pos, int* flush) {
+  if (E < 0 || n < 1 || !P || (E > 0 && (!slots || !pos || !flush))) return -1;
+  std::vector<int> pos_prev(n), pos_cur(n);
+  for (int e = 0; e < E; ++e) {
+    const long long* pe = P + (size_t)e * n;
+    for (int p = 0; p < n; ++p) {
+      const long long w = pe[p];
+      if (w < 0 || w >= n) return -2;
+      pos_cur[w] = p;
+    }
+    for (int p = 0; p < n; ++p) {
+      int* s = slots + ((size_t)e * n + p) * 4;
+      s[0] = (int)pe[p];
+      s[1] = (int)pe[p];
+      s[2] = p > 0 ? (int)pe[p - 1] : -1;
+      s[3] = p + 1 < n ? (int)pe[p + 1] : -1;
+      int* f = flush + ((size_t)e * n + p) * 2;
+      f[0] = f[1] = -1;
+      if (e > 0) {
+        const long long* pp = P + (size_t)(e - 1) * n;
+        const int po = pos_prev[pe[p]];
+        if (po % 2 == 0) {
+          f[0] = po > 0 ? (int)pp[po - 1] : -1;
+          f[1] = po + 1 < n ? (int)pp[po + 1] : -1;
+        }
+      }
+    }
+    for (int w = 0; w < n; ++w) pos[(size_t)e * n + w] = pos_cur[w];
+    pos_prev.swap(pos_cur);
+  }
+  return 0;
+}
+
 extern "C" int gadmm_epoch_tables(const long long* P, int E, int n, const long long* loc, int nloc, int* slots,
                                   int* pos) {
   if (E < 0 || n < 1 || nloc < 0 || !P || (nloc > 0 && (!loc || !slots || !pos))) return -1;

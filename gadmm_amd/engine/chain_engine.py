@@ -249,6 +249,7 @@ class NativeChainEngine:
 
     # ---------------------------------------------------------------------------------------------
     def _build_inverses(self, in_place: bool = False, check: bool = True):
+        self._minv_version = getattr(self, "_minv_version", 0) + 1  # the blocked D-GADMM pad follows it
         rho = self.rho
         if self.n_total == 1:
             shifts, self.deg_to_var = [0.0], (0, 0, 0)
@@ -623,16 +624,16 @@ class NativeChainEngine:
             E, n = P.shape
             loc = np.asarray([int(w) for w in self.local_ids], dtype=np.int64)
             if plan is not None:
-                pos_of = np.argsort(P, axis=1)                                      # worker -> position
-                # blocked kernel: slots in chain-POSITION order per epoch (li, gid, left, right), and
-                # worker -> position
-                li_of = np.full(self.n_total, -1, dtype=np.int64)
-                li_of[loc] = np.arange(len(loc))
-                lft = np.concatenate([np.full((E, 1), -1, dtype=np.int64), P[:, :-1]], axis=1)
-                rgt = np.concatenate([P[:, 1:], np.full((E, 1), -1, dtype=np.int64)], axis=1)
-                es = np.stack([li_of[P], P, lft, rgt], axis=-1).astype(np.int32).reshape(-1)
-                pp = pos_of.astype(np.int32).reshape(-1)
-                fl = epoch_flush_table(P, pos_of).reshape(-1)  # PersistArgs::ep_flush
+                # blocked kernel (one GPU, every worker local: li == worker id): slots in chain-POSITION
+                # order per epoch (li, gid, left, right), worker -> position, and the flush pairs
+                # (PersistArgs::ep_flush) -- native C++ builder (csrc/runtime/topology.cpp; the numpy
+                # equivalent is epoch_flush_table + fancy indexing)
+                P = np.ascontiguousarray(P)
+                es = np.empty((E * n * 4,), dtype=np.int32)
+                pp = np.empty((E * n,), dtype=np.int32)
+                fl = np.empty((E * n * 2,), dtype=np.int32)
+                native.check(self.lib.gadmm_epoch_tables_blocked(P.ctypes.data, E, n, es.ctypes.data, pp.ctypes.data,
+                                                                 fl.ctypes.data), "epoch_tables_blocked")
             else:
                 # per-worker kernel: the slot / position of every LOCAL worker per epoch (native C++
                 # builder, csrc/runtime/topology.cpp; the numpy equivalent is epoch_tables_numpy)
@@ -705,8 +706,11 @@ class NativeChainEngine:
                 if pad is None or pad.shape[-1] != DB:
                     pad = torch.zeros((self.n_local, self.nvar, 64, DB), dtype=torch.float64, device=dev)
                     self._minv_pad = pad
-                with torch.cuda.stream(self.stream):
-                    pad[:, :, :self.d, :self.d].copy_(self.Minv.reshape(self.n_local, self.nvar, self.d, self.d))
+                    self._minv_pad_version = -1
+                if self._minv_pad_version != self._minv_version:  # only after the inverses changed
+                    with torch.cuda.stream(self.stream):
+                        pad[:, :, :self.d, :self.d].copy_(self.Minv.reshape(self.n_local, self.nvar, self.d, self.d))
+                    self._minv_pad_version = self._minv_version
                 pa.minv_pad = pad.data_ptr()
         self.last_kernel = ("blocked%s(k=%d,L=%d,W=%d,pw=%d)" % ((("-dyn" if epochs is not None else ""),) + tuple(plan))
                             if plan is not None else "per-worker")

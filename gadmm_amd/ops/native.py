@@ -209,6 +209,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_chain_blocked_tab_granules": (c_long, [c_int, c_int, c_int]),
         "gadmm_chain_blocked_tab_granules_dyn": (c_long, [c_int, c_int, c_int]),
         "gadmm_epoch_tables": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
+        "gadmm_epoch_tables_blocked": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
         "gadmm_chain_blocked_launch": (c_int, [ctypes.POINTER(PersistArgs), c_void_p]),
         "gadmm_fo_lds": (c_long, [c_int, c_int, c_int, c_int, c_int]),
         "gadmm_fo_tab_granules": (c_long, [c_int, c_int, c_int]),

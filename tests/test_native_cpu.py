@@ -162,3 +162,23 @@ def test_epoch_flush_table_matches_the_kernels_old_lookup():
                 exp = (P[e - 1][op - 1] if op > 0 else -1, P[e - 1][op + 1] if op < n - 1 else -1) \
                     if op % 2 == 0 else (-1, -1)
                 assert tuple(fl[e, p]) == exp
+
+
+def test_native_blocked_epoch_tables_match_numpy():
+    """gadmm_epoch_tables_blocked (C++) == the numpy construction of the blocked D-GADMM tables."""
+    import ctypes
+    import numpy as np
+    from gadmm_amd.engine.chain_engine import epoch_flush_table
+    lib = native.require()
+    rng = np.random.default_rng(7)
+    for E, n in ((1, 4), (9, 24), (40, 7)):
+        P = np.ascontiguousarray(np.stack([rng.permutation(n) for _ in range(E)]).astype(np.int64))
+        es = np.empty((E * n * 4,), dtype=np.int32)
+        pp = np.empty((E * n,), dtype=np.int32)
+        fl = np.empty((E * n * 2,), dtype=np.int32)
+        assert lib.gadmm_epoch_tables_blocked(P.ctypes.data, E, n, es.ctypes.data, pp.ctypes.data, fl.ctypes.data) == 0
+        lft = np.concatenate([np.full((E, 1), -1), P[:, :-1]], axis=1)
+        rgt = np.concatenate([P[:, 1:], np.full((E, 1), -1)], axis=1)
+        assert np.array_equal(es.reshape(E, n, 4), np.stack([P, P, lft, rgt], axis=-1))
+        assert np.array_equal(pp.reshape(E, n), np.argsort(P, axis=1))
+        assert np.array_equal(fl.reshape(E, n, 2), epoch_flush_table(P))

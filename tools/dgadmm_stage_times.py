@@ -26,17 +26,20 @@ p0, c0, _ = T.find_path(24, np.random.default_rng(5))
 COH = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 lib = native.require()
 stamps = {}
-orig = lib.gadmm_chain_persistent_launch
 
 
-def wrapped(*a):
-    stamps["launch"] = time.perf_counter()
-    rc = orig(*a)
-    stamps["launched"] = time.perf_counter()
-    return rc
+def _wrap(orig):
+    def wrapped(*a):
+        stamps["launch"] = time.perf_counter()
+        rc = orig(*a)
+        stamps["launched"] = time.perf_counter()
+        return rc
+    return wrapped
 
 
-lib.gadmm_chain_persistent_launch = wrapped
+# both D-GADMM kernels: the per-worker one and the blocked dynamic mode (GADMM_BLOCKED_DYN=1)
+lib.gadmm_chain_persistent_launch = _wrap(lib.gadmm_chain_persistent_launch)
+lib.gadmm_chain_blocked_launch = _wrap(lib.gadmm_chain_blocked_launch)
 orig_sync = torch.cuda.Stream.synchronize
 
 
