@@ -35,6 +35,54 @@
 namespace {
 
 constexpr int MAXW = 12;  // computed workers (waves) per workgroup: 3 waves per SIMD -> <= 170 VGPRs
+// DYN: epochs per launch whose tables are staged in LDS at the kernel start (epoch starts, and per
+// computed / objective position its slot and flush pair), so a re-chain reads them in ~0.1 us
+// instead of a cold HBM round trip; the host caps a launch at EPL epochs.
+constexpr int EPL = 256;
+// DYN LDS after the worker / objective layout, per wave (each wave stages and reads only its own
+// rows: no barrier): [MAXW][EPL] slots (int4), [MAXW][EPL] flush pairs (int2), [MAXW][EPL] epoch starts
+constexpr long DYN_LDS_BYTES = (long)MAXW * EPL * (16 + 8 + 4);
+struct EpochLds {
+  int4* sl;
+  int2* fl;
+  int* st;
+};
+__device__ __forceinline__ EpochLds epoch_lds(double* base, int v) {
+  int4* sl = reinterpret_cast<int4*>(base);
+  int2* fl = reinterpret_cast<int2*>(sl + MAXW * EPL);
+  int* st = reinterpret_cast<int*>(fl + MAXW * EPL);
+  return {sl + v * EPL, fl + v * EPL, st + v * EPL};
+}
+
+// Padded inverse image of PersistArgs::minv_pad, per (worker, variant): the quad register layout of
+// quad_load<QT> stored lane-major in (t, t + 1) pairs -- element Mq[r][t] of lane l at
+// ((t >> 1) * 4 + r) * 128 + 2 l + (t & 1) (quad_store_lds's layout), zero beyond d. A reload is then
+// 4 * ceil(QT / 2) coalesced 16-byte loads per lane (1 KB contiguous per wave instruction) with no
+// bounds masks.
+template <int QT>
+__device__ __forceinline__ void quad_load_image(double (&m)[4][QT], const double* img) {
+  const int lane = threadIdx.x & 63;
+  const double2* p = reinterpret_cast<const double2*>(img) + lane;
+#pragma unroll
+  for (int t = 0; t < QT; t += 2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double2 v = p[((t >> 1) * 4 + r) * 64];
+      m[r][t] = v.x;
+      if (t + 1 < QT) m[r][t + 1] = v.y;
+    }
+}
+
+// Stages a launch's epoch tables for chain position q into this wave's LDS rows (DYN); the wave's
+// own later LDS reads are ordered after these stores (in-order LDS within a wave).
+__device__ __forceinline__ void stage_epochs(const PersistArgs& a, int q, const EpochLds& el, bool flush) {
+  const int lane = threadIdx.x & 63;
+  for (int e = lane; e < a.n_epochs; e += 64) {
+    el.sl[e] = reinterpret_cast<const int4*>(a.ep_slots)[(long)e * a.n + q];
+    if (flush) el.fl[e] = reinterpret_cast<const int2*>(a.ep_flush)[(long)e * a.n + q];
+    el.st[e] = a.epoch_start[e];
+  }
+}
 }  // namespace
 
 
@@ -102,6 +150,9 @@ __device__ __forceinline__ void blocked_objective(const PersistArgs& a, double* 
                                                   __amdgpu_buffer_rsrc_t rtab, bool local = false) {
   const int d = a.d, n = a.n;
   const long ring_base = 2L * n * 2 * d;  // theta ring [ring][n][d] after the exchange table
+  // DYN: this wave's epoch rows staged in LDS after the staging area (see DYN_LDS_BYTES)
+  const EpochLds el = epoch_lds(lds + MAXW * 64 + MAXW * QSTAGE, v);
+  if constexpr (DYN) stage_epochs(a, q, el, false);
   PhaseSlot so = DYN ? a.ep_slots[q] : a.slots[q];
   const bool in = lane < d;
   double Aq[4][QT];
@@ -109,14 +160,18 @@ __device__ __forceinline__ void blocked_objective(const PersistArgs& a, double* 
   double bo = in ? a.b[(long)so.li * d + lane] : 0.0;
   double hy = 0.5 * a.yy[so.li];
   double* xo = lds + v * QSTAGE;
-  int ep = 0, next_start = (DYN && a.n_epochs > 1) ? a.epoch_start[1] : 0x7fffffff;
+  int ep = 0, next_start = (DYN && a.n_epochs > 1) ? el.st[1] : 0x7fffffff;
   for (int it = a.start_iter;; ++it) {
     if (a.hard_stop > 0 && it > a.hard_stop) return;  // D-GADMM chunk end: no theta^it comes
     if constexpr (DYN) {
       if (it == next_start) {  // D-GADMM re-chain: another worker now sits at position q
         ++ep;
-        next_start = ep + 1 < a.n_epochs ? a.epoch_start[ep + 1] : 0x7fffffff;
-        so = a.ep_slots[(long)ep * n + q];
+        next_start = ep + 1 < a.n_epochs ? el.st[ep + 1] : 0x7fffffff;
+        {
+          const int4 s4 = el.sl[ep];
+          so.li = s4.x;
+          so.gid = s4.y;
+        }
         int od = d;  // laundered: the reload's bounds masks are not hoisted out of the loop (SGPRs)
         asm volatile("" : "+s"(od));
         quad_load<QT>(Aq, a.A + (long)so.li * od * od, od, true);
@@ -256,6 +311,16 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   const bool rl = dl && has_l && p == seg_lo, rr = dl && has_r && p == seg_hi;
   const bool rpush = owned && (rl || rr);
 
+  // DYN: this wave's epoch rows in LDS (after thS and the staging area; see DYN_LDS_BYTES)
+  const EpochLds el = epoch_lds(lds + MAXW * 64 + MAXW * QSTAGE, v);
+  if constexpr (DYN) {
+    if (active) stage_epochs(a, p, el, true);
+  }
+  // Positions that ever solve: in a block, phase phi solves the owned range widened by 2k - 1 - phi,
+  // so heads up to 2k - 1 and tails up to 2k - 2 positions away from it; the outermost halo only
+  // carries theta. DYN: only these reload an inverse at a re-chain.
+  const int odist = u < s0 - ra ? (s0 - ra) - u : (u > e0 - ra ? u - (e0 - ra) : 0);
+  const bool solver = active && odist <= (head ? 2 * k - 1 : 2 * k - 2);
   double Mq[4][QT];
   quad_load<QT>(Mq, a.Minv + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)d * d, d, active);
   // y = (A + deg rho I)^{-1} r for this wave's worker (r: this lane's element)
@@ -270,7 +335,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   int pending = a.pending_in;
   // DYN: epoch cursor, regular exchange schedule (restarts after every re-chain) and its slot
   // counter, and the epoch exchange table [2][n][2][d] after the theta ring
-  int ep = 0, next_start = (DYN && a.n_epochs > 1) ? a.epoch_start[1] : 0x7fffffff;
+  int ep = 0, next_start = (DYN && a.n_epochs > 1) ? el.st[1] : 0x7fffffff;
   int next_x = a.start_iter + k, xc = 0;
   // Only the positions whose result still reaches an owned one before the next exchange are solved:
   // in phase phi of a block (phi = 0, 1 the head / tail phase of its first iteration, ...) that is the
@@ -362,20 +427,20 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
           put_granule<SYS>(local, rtab, (int)((base + d + lane) * 16), tag, mu);
         }
         ++ep;
-        next_start = ep + 1 < a.n_epochs ? a.epoch_start[ep + 1] : 0x7fffffff;
+        next_start = ep + 1 < a.n_epochs ? el.st[ep + 1] : 0x7fffffff;
         if (active) {
-          sl = a.ep_slots[(long)ep * n + p];
+          {
+            const int4 s4 = el.sl[ep];
+            sl.li = s4.x;
+            sl.gid = s4.y;
+          }
           // the new worker's old-chain neighbours when it was a head (pending-dual flush), -1: none
-          const int2 of = reinterpret_cast<const int2*>(a.ep_flush)[(long)ep * n + p];
+          const int2 of = el.fl[ep];
           li = sl.li;
           w = sl.gid;
-          {  // the new worker's inverse (zero-padded image, unmasked loads) and b: issued before the
-             // state poll below, so their latency overlaps the hand-off
-            const double* Mp = a.minv_pad + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)(64 * DB);
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-#pragma unroll
-              for (int t = 0; t < QT; ++t) Mq[r][t] = Mp[((lane & 15) + 16 * r) * DB + (lane >> 4) + 4 * t];
+          if (solver) {  // the new worker's inverse (lane-major padded image, coalesced unmasked loads)
+                         // and b: issued before the state poll below, so they overlap the hand-off
+            quad_load_image<QT>(Mq, a.minv_pad + ((long)li * a.nvar + a.deg_to_var[deg]) * (long)(512 * ((QT + 1) / 2)));
             bb = in ? a.b[(long)li * d + lane] : 0.0;
           }
           const bool fl = pending && of.x >= 0, fr = pending && of.y >= 0;  // it was a head: dual pending
@@ -919,6 +984,13 @@ int gadmm_chain_blocked_plan2(int n, int d, int want_k, int want_pw, int* k_out,
 // Row length of PersistArgs::minv_pad for dimension d (the kernel instantiation's DB): the padded
 // inverse image is [n_local][nvar][64][pad_dim].
 int gadmm_chain_blocked_pad_dim(int d) { return d <= 32 ? 32 : 52; }
+// Doubles per matrix of the lane-major image (quad_load_image): 4 x 64 x QT rounded up to even.
+long gadmm_chain_blocked_pad_len(int d) {
+  const int qt = gadmm_chain_blocked_pad_dim(d) / 4;
+  return 512L * ((qt + 1) / 2);
+}
+// Epochs one launch of the blocked kernel's dynamic mode can take (its tables are staged in LDS).
+int gadmm_chain_blocked_max_epochs() { return EPL; }
 
 // Plan of the data-local multi-GPU mode for a segment of nseg positions: one workgroup computing the
 // whole segment when it fits the 12 waves (no intra-rank exchange at all: k = 2^20 never comes), else
@@ -1016,11 +1088,12 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   const bool tl = a.timeline != nullptr;
   if (a.n_epochs > 0) {  // D-GADMM in one launch: one GPU, 12-wave layout, no instrumentation
     if (multi || tl || a.sys_scope || !a.epoch_start || !a.ep_slots || !a.ep_pos || !a.minv_pad || !a.ep_flush ||
-        a.hard_stop < 0 || (a.hard_stop > 0 && a.hard_stop < a.start_iter)) {
-      gadmm_set_error("blocked chain kernel: dynamic epochs need one GPU, epoch tables, the padded inverses "
-                      "(gadmm_chain_blocked_pad_dim), no timeline");
+        a.hard_stop < 0 || (a.hard_stop > 0 && a.hard_stop < a.start_iter) || a.n_epochs > EPL) {
+      gadmm_set_error("blocked chain kernel: dynamic epochs need one GPU, epoch tables (at most %d epochs per "
+                      "launch), the padded inverse image (gadmm_chain_blocked_pad_len), no timeline", EPL);
       return -1;
     }
+    lds = gadmm_chain_blocked_lds(a.d, a.blk_len) + DYN_LDS_BYTES;  // + the staged epoch tables
     fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, false, false, true>
                    : (const void*)chain_blocked_kernel<52, false, false, true>;
   } else if (a.sys_scope) {

@@ -367,6 +367,11 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             chunk = max(16, int(hints[hint_key]) + 8)
         else:
             chunk = 128
+        # the blocked kernel's dynamic mode stages a launch's epoch tables in LDS: at most
+        # gadmm_chain_blocked_max_epochs rows per launch (this chunk + the look-ahead epoch)
+        use_blk = eng.dynamic_uses_blocked(fabric, schedule.coherence)
+        cap = int(eng.lib.gadmm_chain_blocked_max_epochs()) - 1 if use_blk else 1 << 30
+        chunk = min(chunk, cap)
         saved = schedule.save()
         E_total = 1 + len(rechains)
         # epoch e's chain is row e of one (E_total, N) table, filled as chains are drawn (epoch 0: the
@@ -398,7 +403,8 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             timed_out = None
             try:
                 r = eng.run_persistent(epochs=(st_arr, P_arr), fabric=fabric, start_iter=start_iter,
-                                       pending_in=pending_in, hard_stop=hard_stop, cont=cont, fetch_trace=True)
+                                       pending_in=pending_in, hard_stop=hard_stop, cont=cont, fetch_trace=True,
+                                       blocked_dyn=use_blk)
             except HandoffTimeout as e:
                 if comm.nranks == 1:
                     raise
@@ -428,7 +434,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
                 break
             start_iter, pending_in, cont = hard_stop + 1, 1, True
             e0 = e1 - 1  # epoch 0 of the next launch: this chunk's last (the flush of pending duals)
-            chunk *= 2
+            chunk = min(2 * chunk, cap)
         if done == 5:
             done = 2
         ep_start = ep_start[:n_drawn[0]]

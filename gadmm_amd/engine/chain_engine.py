@@ -67,6 +67,34 @@ def epoch_tables_numpy(P: np.ndarray, loc: np.ndarray):
     return slots, k.astype(np.int32)
 
 
+_QUAD_IDX: dict = {}
+
+
+def quad_pad_image(M: torch.Tensor, db: int) -> torch.Tensor:
+    """Lane-major image of the quad register layout of each (d, d) matrix in ``M`` (B, d, d), as
+    ``quad_load_image`` in csrc/kernels/chain_blocked.hip reads it: lane l = i + 16c holds
+    M[i + 16r, c + 4t] (r < 4, t < db / 4) at ((t >> 1) * 4 + r) * 128 + 2 l + (t & 1); zero outside d.
+    Returns (B, 512 * ceil(db / 8)) float64 on M's device."""
+    B, d = int(M.shape[0]), int(M.shape[1])
+    qt = db // 4
+    key = (d, db, M.device)
+    idx = _QUAD_IDX.get(key)
+    if idx is None:
+        n_el = 512 * ((qt + 1) // 2)
+        src = np.full((n_el,), -1, dtype=np.int64)
+        for t in range(qt):
+            for r in range(4):
+                for lane in range(64):
+                    row, col = (lane & 15) + 16 * r, (lane >> 4) + 4 * t
+                    if row < d and col < d:
+                        src[((t >> 1) * 4 + r) * 128 + 2 * lane + (t & 1)] = row * d + col
+        idx = (torch.from_numpy(np.maximum(src, 0)).to(M.device), torch.from_numpy(src >= 0).to(M.device))
+        _QUAD_IDX[key] = idx
+    gi, mask = idx
+    flat = M.reshape(B, d * d).to(torch.float64)
+    return torch.where(mask.unsqueeze(0), flat[:, gi], torch.zeros((), dtype=torch.float64, device=M.device)).contiguous()
+
+
 def epoch_flush_table(P: np.ndarray, pos_of: Optional[np.ndarray] = None) -> np.ndarray:
     """(E, n, 2) int32: for epoch e >= 1 and chain position p, the OLD-chain neighbours (worker ids,
     -1 = none) of the worker that epoch e places at p, if that worker was a head of epoch e - 1's
@@ -457,13 +485,23 @@ class NativeChainEngine:
             return 0 if int(self.lib.gadmm_chain_persistent_lds_dyn(self.d, 0, self.nvar)) > 0 else 1
         return 0 if int(self.lib.gadmm_chain_persistent_lds(self.d, 0)) > 0 else 1
 
-    def dynamic_uses_blocked(self, fabric=None) -> bool:
-        """Whether a one-launch D-GADMM run takes the blocked kernel's dynamic mode (GADMM_BLOCKED_DYN=1,
-        one GPU, 12-wave layout) rather than the per-worker kernel. Both run epoch chunks (hard stop +
-        continuation)."""
+    # coherence (iterations per epoch) from which the blocked kernel's dynamic mode is the default:
+    # per epoch it costs ~9.1 + 1.03 (c - 1) us against the per-worker kernel's ~4.8 + 2.03 (c - 1) us
+    # (profiles/r03_dgadmm_rechain), so they cross near c = 5
+    BLOCKED_DYN_MIN_COHERENCE = 5
+
+    def dynamic_uses_blocked(self, fabric=None, coherence=None) -> bool:
+        """Whether a one-launch D-GADMM run takes the blocked kernel's dynamic mode (one GPU, 12-wave
+        layout) rather than the per-worker kernel: GADMM_BLOCKED_DYN=1 / 0 forces it on / off; unset,
+        it is on when the schedule re-chains every ``BLOCKED_DYN_MIN_COHERENCE`` or more iterations
+        (``coherence``; None: off). Both run epoch chunks (hard stop + continuation)."""
         plan = self.blocked_plan(fabric) if self.model == "linear" else None
-        return (plan is not None and plan[3] == 1 and self.n_local == self.n_total
-                and os.environ.get("GADMM_BLOCKED_DYN", "0") == "1")
+        if plan is None or plan[3] != 1 or self.n_local != self.n_total:
+            return False
+        env = os.environ.get("GADMM_BLOCKED_DYN", "")
+        if env in ("0", "1"):
+            return env == "1"
+        return coherence is not None and float(coherence) >= self.BLOCKED_DYN_MIN_COHERENCE
 
     def dynamic_eligible(self, fabric=None) -> bool:
         """One-launch D-GADMM (per-epoch chains in device tables): linear, every degree's inverse
@@ -495,7 +533,7 @@ class NativeChainEngine:
     def run_persistent(self, lag: int = 4, timeout_s: float = 20.0, start_iter: int = 1,
                        pending_in: int = 0, fabric=None, timeline_iters: int = 0,
                        epochs: Optional[Sequence] = None, hard_stop: int = 0, cont: bool = False,
-                       fetch_trace: bool = False) -> EngineRun:
+                       fetch_trace: bool = False, blocked_dyn: Optional[bool] = None) -> EngineRun:
         """Whole solve in one launch per GPU. State must be reset (``reset()``) or resumed by the
         caller. ``fabric``: an ``XgmiFabric`` for the multi-GPU device-initiated transport.
         ``timeline_iters > 0`` records s_memrealtime stamps (10 ns) of the first iterations into
@@ -513,14 +551,17 @@ class NativeChainEngine:
         the previous chunk from ``start_iter = hard_stop + 1`` with the same tag salt, epoch 0 being the
         previous chunk's last epoch (its heads' pending duals are flushed with that chain).
         ``fetch_trace``: the objective trace and clock come back behind the same stream sync (for a
-        caller that reads ``traces()`` next; a benchmark loop that does not leaves it off)."""
+        caller that reads ``traces()`` next; a benchmark loop that does not leaves it off).
+        ``blocked_dyn``: D-GADMM on the blocked kernel's dynamic mode (None: ``dynamic_uses_blocked``)."""
         if epochs is not None:
             if not self.dynamic_eligible(fabric):
                 raise RuntimeError("dynamic persistent kernel not eligible for this engine/config")
         elif not self.persistent_eligible(fabric):
             raise RuntimeError("persistent kernel not eligible for this engine/config")
         plan = self.blocked_plan(fabric, timeline=timeline_iters > 0) if self.model == "linear" else None
-        if epochs is not None and (not self.dynamic_uses_blocked(fabric) or timeline_iters > 0):
+        if blocked_dyn is None:
+            blocked_dyn = self.dynamic_uses_blocked(fabric)
+        if epochs is not None and (not blocked_dyn or timeline_iters > 0):
             # D-GADMM on the per-worker kernel unless the blocked kernel's dynamic mode is selected
             # (dynamic_uses_blocked); both run epoch chunks (hard stop + continuation)
             plan = None
@@ -698,20 +739,16 @@ class NativeChainEngine:
             pa.blk_k, pa.blk_len, pa.blk_pw = plan[0], plan[1], plan[3]
             pa.blk_tab = self._blk_tab.data_ptr()
             if epochs is not None:
-                # D-GADMM in the blocked kernel: the inverses zero-padded to [n_local][nvar][64][DB], reloaded
-                # by every re-chain without bounds masks (PersistArgs::minv_pad); refreshed from this solve's
-                # inverses on the engine stream, ahead of the launch
-                DB = int(self.lib.gadmm_chain_blocked_pad_dim(self.d))
-                pad = getattr(self, "_minv_pad", None)
-                if pad is None or pad.shape[-1] != DB:
-                    pad = torch.zeros((self.n_local, self.nvar, 64, DB), dtype=torch.float64, device=dev)
-                    self._minv_pad = pad
-                    self._minv_pad_version = -1
-                if self._minv_pad_version != self._minv_version:  # only after the inverses changed
+                # D-GADMM in the blocked kernel: every inverse as a lane-major image of the kernel's quad
+                # register layout (quad_pad_image), reloaded by a re-chain with coalesced unmasked loads
+                # (PersistArgs::minv_pad); rebuilt from this solve's inverses on the engine stream, ahead of
+                # the launch, only after the inverses changed
+                if getattr(self, "_minv_pad", None) is None or self._minv_pad_version != self._minv_version:
                     with torch.cuda.stream(self.stream):
-                        pad[:, :, :self.d, :self.d].copy_(self.Minv.reshape(self.n_local, self.nvar, self.d, self.d))
+                        self._minv_pad = quad_pad_image(self.Minv.reshape(self.n_local * self.nvar, self.d, self.d),
+                                                        int(self.lib.gadmm_chain_blocked_pad_dim(self.d)))
                     self._minv_pad_version = self._minv_version
-                pa.minv_pad = pad.data_ptr()
+                pa.minv_pad = self._minv_pad.data_ptr()
         self.last_kernel = ("blocked%s(k=%d,L=%d,W=%d,pw=%d)" % ((("-dyn" if epochs is not None else ""),) + tuple(plan))
                             if plan is not None else "per-worker")
         with torch.cuda.stream(self.stream):

@@ -206,6 +206,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_chain_blocked_lds": (c_long, [c_int, c_int]),
         "gadmm_chain_blocked_plan_dl": (c_int, [c_int, c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
         "gadmm_chain_blocked_pad_dim": (c_int, [c_int]),
+        "gadmm_chain_blocked_pad_len": (c_long, [c_int]),
+        "gadmm_chain_blocked_max_epochs": (c_int, []),
         "gadmm_chain_blocked_tab_granules": (c_long, [c_int, c_int, c_int]),
         "gadmm_chain_blocked_tab_granules_dyn": (c_long, [c_int, c_int, c_int]),
         "gadmm_epoch_tables": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),

@@ -182,3 +182,25 @@ def test_native_blocked_epoch_tables_match_numpy():
         assert np.array_equal(es.reshape(E, n, 4), np.stack([P, P, lft, rgt], axis=-1))
         assert np.array_equal(pp.reshape(E, n), np.argsort(P, axis=1))
         assert np.array_equal(fl.reshape(E, n, 2), epoch_flush_table(P))
+
+
+def test_quad_pad_image_layout():
+    """The lane-major padded inverse image (chain_engine.quad_pad_image) holds, for lane l = i + 16c,
+    M[i + 16r, c + 4t] at ((t >> 1) * 4 + r) * 128 + 2 l + (t & 1), and zeros outside d -- the order
+    quad_load_image in chain_blocked.hip reads (its per-matrix length is gadmm_chain_blocked_pad_len)."""
+    import torch
+    from gadmm_amd.engine.chain_engine import quad_pad_image
+    from gadmm_amd.ops import native
+
+    for d, db in ((50, 52), (20, 32)):
+        M = torch.randn(3, d, d, dtype=torch.float64)
+        im = quad_pad_image(M, db)
+        assert im.shape == (3, int(native.require().gadmm_chain_blocked_pad_len(d)))
+        qt = db // 4
+        for b in range(3):
+            for t in range(qt):
+                for r in range(4):
+                    for lane in range(64):
+                        row, col = (lane & 15) + 16 * r, (lane >> 4) + 4 * t
+                        want = float(M[b, row, col]) if row < d and col < d else 0.0
+                        assert float(im[b, ((t >> 1) * 4 + r) * 128 + 2 * lane + (t & 1)]) == want
