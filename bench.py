@@ -12,8 +12,12 @@ only theta, to the two chain neighbours (group_ADMM_closedForm.m:18-27, 62-70):
 * 1 GPU: the temporally blocked persistent kernel (one launch per solve);
 * N GPUs (``--fabric auto``/``xgmi``): the temporally blocked kernel run inside every rank's segment
   (data-local mode: only the segment-edge workers' theta crosses, every phase, pushed into the
-  neighbour GPU's ring over xGMI -- device-initiated, IPC-mapped fine-grained memory); if that is
-  unavailable, the per-worker persistent kernel over the same fabric;
+  neighbour GPU's ring over xGMI -- device-initiated, IPC-mapped fine-grained memory). When every
+  segment has >= 2 workers (N <= 12 GPUs at 24 workers) it runs in the one-position halo mode: at each
+  rank boundary the rank holding the tail also solves the other rank's boundary head (its 20 KB shard
+  is fetched once and reported as replicated_shard_bytes, data_local then reads false), so each
+  iteration carries one cross-GPU hop on the critical cycle instead of two (GADMM_DL_HALO=0: off);
+  if the blocked kernel is unavailable, the per-worker persistent kernel over the same fabric;
 * fallbacks, taken by every rank together: the graph-replayed phase kernels with RCCL send/recv
   (``--fabric rccl``), or with the device-copy transport (``--fabric ipc``; also the fallback when
   ranks share one GPU, where RCCL cannot run).
@@ -170,7 +174,8 @@ def run_headline(args, rank, world, device, share):
         p2p, wire, mon, repl = int(sm[1]), int(sm[2]), int(sm[3]), int(sm[4])
     tr = sol.objective_trace(iters)
     gap = abs(float(tr[iters - 1]) - obj0) if iters > 0 else float("nan")
-    data_local = sol.blk is None or sol.blk.data_local
+    dl_mode = sol.blk is None or sol.blk.data_local  # theta-only exchange (payload formula below)
+    data_local = dl_mode and repl == 0  # the halo mode also holds one neighbour head's shard per boundary
     per = np.diff(np.asarray([t0] + stamps)) * 1e3  # this rank's per-step wall times
     if rank == 0:
         value = ms / 1e3
@@ -200,7 +205,7 @@ def run_headline(args, rank, world, device, share):
             # 2 messages of d doubles per rank boundary per iteration (group_ADMM_closedForm.m:18-27, 62-70)
             "comm_bytes_per_solve": p2p,
             "theta_payload_bytes_per_solve": p2p,
-            "theta_payload_bytes_formula": 2 * (world - 1) * d * 8 * iters if data_local else None,
+            "theta_payload_bytes_formula": 2 * (world - 1) * d * 8 * iters if dl_mode else None,
             "wire_bytes_per_solve": wire,
             "monitor_bytes_per_solve": mon,
             "replicated_shard_bytes": repl,

@@ -182,13 +182,17 @@ struct PersistArgs {
   // pushes theta^j of position p into the neighbour rank's ring (slot j % ring, row p, tag j), readers
   // poll their own ring (group_ADMM_closedForm.m:18-27,62-70: only theta crosses, never mu).
   // dl_tab[0] / [1]: blk_tab of the rank owning seg_lo - 1 / seg_hi + 1 (null at the chain ends).
-  int blk_dl, pad_dl;
+  // dl_halo = 1: the boundary tail's wave also solves the other rank's boundary head from that head's
+  // shard (Minv / b / mu rows of the ext range, slots[h].li), one hop per iteration on the critical
+  // cycle instead of two (chain_blocked.hip; one workgroup per segment, every segment >= 2 positions).
+  int blk_dl, dl_halo;
   u32x4* dl_tab[2];
-  // D-GADMM in the blocked kernel (DYN): the cached inverses zero-padded to [n_local][nvar][64][52]
-  // (rows >= d and columns >= d zero), so a re-chain reloads a position's inverse with 52 unmasked
-  // loads: the bounds masks of a d x d reload are loop-invariant, and hoisted out of the main loop
-  // they held ~100 SGPRs for the whole solve (spilled into VGPR lanes, which spilled the inverse
-  // itself to scratch in every GEMV). Null outside DYN.
+  // D-GADMM in the blocked kernel (DYN): the cached inverses as lane-major images of the quad register
+  // layout, zero beyond d ([n_local][nvar][gadmm_chain_blocked_pad_len(d)], engine/chain_engine.py:
+  // quad_pad_image), so a re-chain reloads a position's inverse with coalesced unmasked 16-byte loads:
+  // the bounds masks of a d x d reload are loop-invariant, and hoisted out of the main loop they held
+  // ~100 SGPRs for the whole solve (spilled into VGPR lanes, which spilled the inverse itself to
+  // scratch in every GEMV). Null outside DYN.
   const double* minv_pad;
   // DYN: per (epoch, chain position) the OLD chain neighbours (worker ids, -1: none) of the worker
   // the epoch puts there, when that worker was a head of the old chain (its pending dual is flushed

@@ -217,7 +217,9 @@ __device__ __forceinline__ void blocked_objective(const PersistArgs& a, double* 
 // A worker that was a head owes its dual of the last iteration of the old chain: the loader applies
 // it with the worker's OLD neighbours' theta, read from the same table (the reference order,
 // dynamic_group_ADMM_closedForm.m:153-168). The regular halo schedule restarts after the switch.
-template <int DB, bool SYS, bool TL, bool DYN = false>
+// HALO (SYS only): the data-local halo mode (PersistArgs::dl_halo, one workgroup per segment: no
+// intra-rank exchange is compiled in).
+template <int DB, bool SYS, bool TL, bool DYN = false, bool HALO = false>
 __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a) {
   constexpr int QT = DB / 4;  // quad layout: columns per lane
   extern __shared__ __attribute__((aligned(16))) double lds[];
@@ -265,7 +267,10 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   // ---------------------------------------------------------------------- worker workgroup
   const int g = bid;
   const int s0 = seg_lo + g * L, e0 = min(seg_hi + 1, s0 + L) - 1;  // owned chain positions [s0, e0]
-  const int ra = max(dl ? seg_lo : 0, s0 - H), rb = min(dl ? seg_hi : n - 1, e0 + H);
+  // HALO: the range also takes the other rank's boundary head next to a boundary tail of this rank
+  // (see dlh below): one more wave on that side
+  const int hl = HALO && dl && seg_lo > 0 && (seg_lo % 2) == 1, hr = HALO && dl && seg_hi < n - 1 && (seg_hi % 2) == 1;
+  const int ra = max(dl ? seg_lo - hl : 0, s0 - H), rb = min(dl ? seg_hi + hr : n - 1, e0 + H);
   const int nv = rb - ra + 1;
   // Wave v computes local position u. Waves are dealt to the 4 SIMDs round-robin (v mod 4), so
   // v < MAXW/2 take the heads and the rest the tails: each phase keeps every SIMD busy with
@@ -308,8 +313,25 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   // j % ring, tag j), pushed there by its owner right after its solve; the owner of an edge position
   // pushes its own theta^j into the neighbour rank's ring the same way (no mu, no shard crosses).
   // (p == seg_lo implies u == 0 and p == seg_hi implies u == nv - 1, so nbl / nbr are false there.)
-  const bool rl = dl && has_l && p == seg_lo, rr = dl && has_r && p == seg_hi;
-  const bool rpush = owned && (rl || rr);
+  // (the range edges: ra / rb; p == ra implies u == 0 and p == rb implies u == nv - 1)
+  const bool rl = dl && has_l && p == ra, rr = dl && has_r && p == rb;
+  // Halo mode (HALO, PersistArgs::dl_halo; one workgroup per segment, every segment >= 2 positions,
+  // segment + halo within MAXW waves): at a rank boundary whose near side is a TAIL t, this rank also
+  // computes the other rank's boundary head h (one more wave, h's inverse from h's shard, which this
+  // rank holds). h polls its far neighbour f = t -+ 2 (another rank's tail, pushed after f's tail
+  // phase) in the head phase; t then reads h from LDS and needs no hand-off, and h's owner no longer
+  // pushes h. Per boundary and iteration still two pushes (t's and f's), but both go tail phase ->
+  // next head phase, so the two ranks pipeline one phase apart and the critical cycle carries one
+  // cross-rank hop per iteration instead of two (head -> tail -> head).
+  const bool dlh = HALO && dl;
+  const bool lb_tail = hl != 0, rb_tail = hr != 0;
+  // pushes of this wave's theta^j into the left / right neighbour rank's ring (row p, slot j % ring)
+  // (without the halo: the edge positions themselves, rl / rr; push_remote runs only when rpush)
+  const bool pl = dlh ? (owned && !head && ((p == seg_lo && has_l) || (p == seg_lo + 1 && seg_lo > 0 && !lb_tail)))
+                      : rl;
+  const bool pr = dlh ? (owned && !head && ((p == seg_hi && has_r) || (p == seg_hi - 1 && seg_hi < n - 1 && !rb_tail)))
+                      : rr;
+  const bool rpush = dlh ? (pl || pr) : owned && (rl || rr);
 
   // DYN: this wave's epoch rows in LDS (after thS and the staging area; see DYN_LDS_BYTES)
   const EpochLds el = epoch_lds(lds + MAXW * 64 + MAXW * QSTAGE, v);
@@ -376,8 +398,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   const bool ring_post = owned && in && !(TL && (a.dbg & 2));
   const int ring_l = (int)((ring_base + (long)(rl ? p - 1 : 0) * d + lane) * 16);  // slot 0, row p - 1
   const int ring_r = (int)((ring_base + (long)(rr ? p + 1 : 0) * d + lane) * 16);  // slot 0, row p + 1
-  const __amdgpu_buffer_rsrc_t rdl0 = rsrc_of(rl && a.dl_tab[0] ? (const void*)a.dl_tab[0] : (const void*)a.blk_tab);
-  const __amdgpu_buffer_rsrc_t rdl1 = rsrc_of(rr && a.dl_tab[1] ? (const void*)a.dl_tab[1] : (const void*)a.blk_tab);
+  const __amdgpu_buffer_rsrc_t rdl0 = rsrc_of(pl && a.dl_tab[0] ? (const void*)a.dl_tab[0] : (const void*)a.blk_tab);
+  const __amdgpu_buffer_rsrc_t rdl1 = rsrc_of(pr && a.dl_tab[1] ? (const void*)a.dl_tab[1] : (const void*)a.blk_tab);
   // other-rank neighbours' theta^j (ring slot `slot`) into tl / tr; false on a deadline
   auto poll_remote = [&](int slot, int j, double& tl, double& tr) -> bool {
     const unsigned tag = make_tag(a.epoch, j);
@@ -397,8 +419,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   auto push_remote = [&](int slot, int j) {
     const unsigned tag = make_tag(a.epoch, j);
     const int off = ring_p + slot * ring_slot_bytes;
-    if (rl) store_granule<SYS>(rdl0, off, tag, th);
-    if (rr) store_granule<SYS>(rdl1, off, tag, th);
+    if (pl) store_granule<SYS>(rdl0, off, tag, th);
+    if (pr) store_granule<SYS>(rdl1, off, tag, th);
   };
   bool ring_defer = false;
   int rslot = a.start_iter % a.ring;                  // == it % ring
@@ -479,7 +501,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     }
     // ---- halo exchange every k iterations (state after iteration it - 1); the owned workers
     // published theirs during the tail phase of it - 1 (publish() below)
-    if (it == next_x) {
+    if (!HALO && it == next_x) {  // (HALO: one workgroup per segment, no intra-rank exchange)
       if (active && !owned) {
         const unsigned tag = make_tag(a.epoch, it);
         const int sel = xc & 1;
@@ -548,7 +570,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
 
     // ---- tail phase; the (idle head) decision wave fetches decision[it + 1 - lag]
     // the next iteration starts with a regular exchange (DYN: unless it starts a new epoch)
-    const bool xnext = it + 1 == next_x && !(DYN && it + 1 == next_start);
+    const bool xnext = !HALO && it + 1 == next_x && !(DYN && it + 1 == next_start);
     // tail-wave stamps (wave MAXW/2 by default), timeline row 128 + g: [start, rhs, gemv, stores, barrier]
     // (GADMM_BLK_DBG bits 4-6 pick another tail wave: MAXW/2 + ((dbg >> 4) & 7))
     const bool tstamp = TL && v == MAXW / 2 + ((a.dbg >> 4) & 7) && it - a.start_iter < a.timeline_iters && g < 128;
@@ -1029,10 +1051,12 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   if (dl) {  // data-local mode: SYS scope, 12-wave layout, static chain, every computed range within MAXW
     const int nseg_dl = a.seg_hi - a.seg_lo + 1;
     const int W_dl = nseg_dl > 0 && a.blk_len > 0 ? (nseg_dl + a.blk_len - 1) / a.blk_len : 0;
-    const long span = W_dl == 1 ? nseg_dl : (long)a.blk_len + 4L * a.blk_k;
+    const int nhalo = a.dl_halo ? (int)(a.seg_lo > 0 && a.seg_lo % 2 == 1) + (int)(a.seg_hi < a.n - 1 && a.seg_hi % 2 == 1) : 0;
+    const long span = W_dl == 1 ? nseg_dl + nhalo : (long)a.blk_len + 4L * a.blk_k;
     if (!multi || !a.sys_scope || a.blk_pw != 1 || a.n_epochs != 0 || a.blk_npeer != 0 || a.blk_k < 1 ||
         a.blk_len < 1 || nseg_dl < 1 || span > MAXW || (W_dl > 1 && a.ring < 2 * a.blk_k + 4) ||
-        (a.seg_lo > 0 && !a.dl_tab[0]) || (a.seg_hi < a.n - 1 && !a.dl_tab[1])) {
+        (a.seg_lo > 0 && !a.dl_tab[0]) || (a.seg_hi < a.n - 1 && !a.dl_tab[1]) ||
+        (a.dl_halo && (W_dl != 1 || nseg_dl < 2 || a.d > 52))) {
       gadmm_set_error("blocked chain kernel (data-local): unsupported configuration (seg %d..%d, L=%d, k=%d)",
                       a.seg_lo, a.seg_hi, a.blk_len, a.blk_k);
       return -1;
@@ -1096,6 +1120,13 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
     lds = gadmm_chain_blocked_lds(a.d, a.blk_len) + DYN_LDS_BYTES;  // + the staged epoch tables
     fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, false, false, true>
                    : (const void*)chain_blocked_kernel<52, false, false, true>;
+  } else if (a.sys_scope && dl && a.dl_halo) {
+    if (tl) {
+      gadmm_set_error("blocked chain kernel: no timeline build of the data-local halo mode");
+      return -1;
+    }
+    fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, true, false, false, true>
+                   : (const void*)chain_blocked_kernel<52, true, false, false, true>;
   } else if (a.sys_scope) {
     if (tl) fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, true, true> : (const void*)chain_blocked_kernel<52, true, true>;
     else fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, true, false> : (const void*)chain_blocked_kernel<52, true, false>;

@@ -26,6 +26,7 @@ Identity chain (the static GADMM of the headline benchmark).
 from __future__ import annotations
 
 import ctypes
+import os
 from typing import List, Optional
 
 import torch
@@ -39,13 +40,20 @@ from ..parallel.xgmi import _Buf, preflight
 
 class BlockedXgmiEngine:
     LAG = 8
+    MAXW = 12  # waves (computed positions) per workgroup of chain_blocked_kernel
 
     def __init__(self, X_all: torch.Tensor, y_all: torch.Tensor, n_total: int, placement: Placement, rank: int,
                  rho: float, obj0: float, tol: float, max_iter: int, device: torch.device, group=None,
-                 want_k: int = 0, data_local: bool = False):
+                 want_k: int = 0, data_local: bool = False, dl_halo: Optional[bool] = None):
         """Collective over ``group``. ``data_local=False``: ``X_all`` / ``y_all`` hold the shards of at
         least this rank's computed range (indexable by global worker id); only those rows are read.
-        ``data_local=True``: ``X_all`` / ``y_all`` are this rank's own shards, in segment order."""
+        ``data_local=True``: ``X_all`` / ``y_all`` are this rank's own shards, in segment order.
+        ``dl_halo`` (data-local only; None: on unless GADMM_DL_HALO=0, when every segment has >= 2
+        positions and fits one workgroup): the one-position halo mode -- at each rank boundary whose near
+        side is a tail, this rank also holds the other rank's boundary head's shard (fetched once here
+        from its owner) and solves it on one more wave, so only one cross-rank hop per iteration is on
+        the critical cycle (chain_blocked.hip, PersistArgs::dl_halo). Needs segment + halo heads <= 12
+        waves on every rank: 4 and 8 ranks at 24 workers, not 2."""
         self.lib = native.require()
         self.rank, self.nranks, self.device = rank, placement.nranks, device
         self.n, self.d = int(n_total), int(X_all.shape[2])
@@ -75,11 +83,26 @@ class BlockedXgmiEngine:
         self.H = H
         comp = [(max(0, lo - H), min(self.n - 1, hi + H)) for lo, hi in segs]
         self.ext_lo, self.ext_hi = comp[rank]
+        self.halo = []  # data-local halo mode: the other ranks' boundary heads this rank solves too
+        if self.data_local:
+            # every segment >= 2 positions, and segment + its halo heads within one 12-wave workgroup on
+            # every rank (2 ranks x 12 workers do not fit: 13 waves)
+            def _span(lo, hi):
+                return hi - lo + 1 + int(lo > 0 and lo % 2 == 1) + int(hi < self.n - 1 and hi % 2 == 1)
+            ok_h = (dl_halo is not False and os.environ.get("GADMM_DL_HALO", "1") != "0" and self.d <= 52
+                    and self.L >= self.seg_hi - self.seg_lo + 1 and all(hi - lo + 1 >= 2 for lo, hi in segs)
+                    and all(_span(lo, hi) <= self.MAXW for lo, hi in segs) and len(segs) > 1)
+            if dl_halo and not ok_h:
+                raise ValueError("data-local halo mode needs segments of >= 2 positions that fit one workgroup "
+                                 "with their halo heads")
+            self._halo_on = ok_h
+            if ok_h:
+                X_all, y_all = self._fetch_halo_shards(X_all, y_all, group)
         self.ring = self.LAG + 4
         torch.cuda.set_device(device)
         f64 = torch.float64
         ext = list(range(self.ext_lo, self.ext_hi + 1))
-        if self.data_local:
+        if self.data_local:  # own shards (+ the halo heads' in the halo mode), in position order
             self.X = X_all.to(device).contiguous()
             self.y = y_all.to(device).contiguous()
         else:
@@ -168,11 +191,41 @@ class BlockedXgmiEngine:
         self.epoch = 0
         if self.data_local:
             W = (self.seg_hi - self.seg_lo + self.L) // self.L
-            self.last_kernel = "blocked-dl(k=%s,L=%d,W=%d,nbr=%s)" % ("inf" if W == 1 else self.k, self.L, W,
-                                                                      self.dl_ranks)
+            self.last_kernel = "blocked-dl%s(k=%s,L=%d,W=%d,nbr=%s)" % (
+                ("-halo%s" % self.halo) if self._halo_mode() else "", "inf" if W == 1 else self.k, self.L, W,
+                self.dl_ranks)
         else:
             self.last_kernel = "blocked-xgmi(k=%d,L=%d,H=%d,pw=%d,peers=%s)" % (self.k, self.L, H, self.pw,
                                                                                 self.peers)
+
+    def _fetch_halo_shards(self, X_own: torch.Tensor, y_own: torch.Tensor, group):
+        """Collective: the halo mode's one-time shard exchange. Every rank offers the shards of its
+        boundary HEADS (a head at seg_lo > 0 / seg_hi < n - 1); a rank whose boundary position is a tail
+        takes its neighbour's head. Returns this rank's ext-range shards (halo, own, halo) and sets
+        ``ext_lo`` / ``ext_hi`` / ``halo``."""
+        lo, hi, n = self.seg_lo, self.seg_hi, self.n
+        offer = {}
+        if lo > 0 and lo % 2 == 0:
+            offer[lo] = (X_own[0].cpu().numpy(), y_own[0].cpu().numpy())
+        if hi < n - 1 and hi % 2 == 0:
+            offer[hi] = (X_own[-1].cpu().numpy(), y_own[-1].cpu().numpy())
+        allo = [None] * self.nranks
+        dist.all_gather_object(allo, offer, group=group)
+        pool = {}
+        for o in allo:
+            pool.update(o)
+        Xs, ys = [X_own.cpu()], [y_own.cpu()]
+        if lo > 0 and lo % 2 == 1:  # seg_lo is a tail: solve the left rank's head lo - 1 too
+            Xs.insert(0, torch.from_numpy(pool[lo - 1][0]).unsqueeze(0))
+            ys.insert(0, torch.from_numpy(pool[lo - 1][1]).unsqueeze(0))
+            self.halo.append(lo - 1)
+        if hi < n - 1 and hi % 2 == 1:  # seg_hi is a tail: the right rank's head hi + 1
+            Xs.append(torch.from_numpy(pool[hi + 1][0]).unsqueeze(0))
+            ys.append(torch.from_numpy(pool[hi + 1][1]).unsqueeze(0))
+            self.halo.append(hi + 1)
+        self.ext_lo = lo - (1 if (lo - 1) in self.halo else 0)
+        self.ext_hi = hi + (1 if (hi + 1) in self.halo else 0)
+        return torch.cat(Xs).contiguous(), torch.cat(ys).contiguous()
 
     def _open(self, hbytes: bytes, key) -> int:
         p = ctypes.c_void_p()
@@ -228,6 +281,7 @@ class BlockedXgmiEngine:
             pa.blk_peer_lo[i], pa.blk_peer_hi[i] = lo, hi
         pa.blk_peer_tab = self.peer_tab_t.data_ptr()
         pa.blk_dl = 1 if self.data_local else 0
+        pa.dl_halo = 1 if self._halo_mode() else 0
         pa.dl_tab[0], pa.dl_tab[1] = self.dl_ptrs[0] or None, self.dl_ptrs[1] or None
         pa.dbg = int(dbg)
         tl = None
@@ -266,10 +320,15 @@ class BlockedXgmiEngine:
         owned = self.seg_hi - self.seg_lo + 1
         return iters * (owned * 16 if self.rank != 0 else 8 * (self.nranks - 1))
 
+    def _halo_mode(self) -> bool:
+        """The halo mode is on for every rank together (a rank with no tail-side boundary holds no halo
+        shard but still runs the halo kernel: its boundary heads stop pushing, their far neighbours push)."""
+        return getattr(self, "_halo_on", False)
+
     def replicated_shard_bytes(self) -> int:
         """Bytes of OTHER ranks' shards this rank holds for its halo (X and y of the halo workers)."""
         if self.data_local:
-            return 0
+            return len(self.halo) * int(self.X.shape[1]) * (self.d + 1) * 8
         halo = (self.ext_hi - self.ext_lo + 1) - (self.seg_hi - self.seg_lo + 1)
         return halo * int(self.X.shape[1]) * (self.d + 1) * 8
 

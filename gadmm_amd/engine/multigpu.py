@@ -8,7 +8,11 @@ order ``engine="auto"`` tries them:
 1. ``xgmi(blocked-dl)`` -- the temporally blocked kernel run inside each rank's segment
    (chain_blocked.hip, data-local mode, engine/blocked_xgmi.py): the segment's intra-rank hand-offs
    are LDS barriers (one workgroup when the segment fits 12 waves) as on one GPU, and only the two
-   segment-edge workers exchange theta with the neighbouring ranks, every phase, over xGMI.
+   segment-edge workers exchange theta with the neighbouring ranks, every phase, over xGMI. When every
+   segment has >= 2 positions and fits one workgroup it runs in the one-position halo mode
+   (``xgmi(blocked-dl-halo)``, GADMM_DL_HALO=0 disables it): at each boundary the rank holding the tail
+   also solves the other rank's boundary head from that head's shard (20 KB, fetched once and reported
+   as ``replicated_bytes``), which leaves one cross-rank hop per iteration on the critical cycle.
 2. ``xgmi`` -- the per-worker persistent kernel (chain_persistent.hip, SYS scope): one workgroup per
    local worker, boundary theta stored straight into the neighbour GPU's table over xGMI, objective
    granules to rank 0's monitor, decisions fanned back out. One launch per solve.
@@ -111,7 +115,9 @@ class DistributedChainSolver:
             if self.rank == 0:
                 print("DistributedChainSolver: data-local blocked fabric unavailable (%s)" % e, file=sys.stderr)
             return
-        self.blk, self.persistent, self.kind = blk, True, "xgmi(blocked-dl)"
+        self.blk, self.persistent = blk, True
+        self.kind = "xgmi(blocked-dl-halo)" if blk._halo_mode() else "xgmi(blocked-dl)"
+        self.replicated_bytes = blk.replicated_shard_bytes()  # halo mode: one neighbour head's shard per tail-side boundary
 
     def _try_xgmi(self):
         from ..parallel.comm import RankInfo

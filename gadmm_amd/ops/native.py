@@ -111,7 +111,7 @@ class PersistArgs(ctypes.Structure):
         ("tstamp", c_void_p), ("ep_push", c_void_p), ("peer_thg", c_void_p), ("rres", c_void_p),
         ("hard_stop", c_int), ("cont", c_int),
         ("xchk", c_void_p), ("xcd", c_int), ("pad_xcd", c_int),
-        ("blk_dl", c_int), ("pad_dl", c_int), ("dl_tab", c_void_p * 2), ("minv_pad", c_void_p),
+        ("blk_dl", c_int), ("dl_halo", c_int), ("dl_tab", c_void_p * 2), ("minv_pad", c_void_p),
         ("ep_flush", c_void_p),
     ]
 

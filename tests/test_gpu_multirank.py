@@ -247,9 +247,13 @@ def test_dgadmm_multirank_matches_one_gpu(world, mode, chunk, lin24):
 
 # ------------------------------------------------------------------------------------------------
 def _solver_rank(rank, world, n, delay_rank, timeout_s, engine="auto"):
+    import os
     import torch
     from gadmm_amd.benchmarks import headline_rank_problem
     from gadmm_amd.engine.multigpu import DistributedChainSolver
+    if engine == "nohalo":  # the data-local blocked kernel without the one-position halo
+        os.environ["GADMM_DL_HALO"] = "0"
+        engine = "auto"
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     X, y, loc, pl, obj0 = headline_rank_problem(n, rank, world)
@@ -268,25 +272,35 @@ def _solver_rank(rank, world, n, delay_rank, timeout_s, engine="auto"):
 
 
 @pytest.mark.parametrize("world,n,engine", [(2, 24, "auto"), (4, 24, "auto"), (8, 24, "auto"), (4, 8, "auto"),
-                                             (8, 8, "auto"), (2, 24, "per-worker"), (4, 8, "per-worker")])
+                                             (8, 8, "auto"), (8, 24, "nohalo"), (4, 24, "nohalo"),
+                                             (2, 24, "per-worker"), (4, 8, "per-worker")])
 def test_data_local_xgmi_default_exact_bytes(world, n, engine, lin24):
-    """The multi-GPU engines, each rank holding only its shards and shipping only theta: the default
-    (auto) = the temporally blocked kernel inside every rank's segment, edge workers exchanging theta
-    every phase; per-worker = the one-workgroup-per-worker kernel. Payload == 2 (N_ranks - 1) d 8
-    iters exactly; wire == 2 x payload (16-B granules); iterations and trace == one GPU, bit for bit.
-    n = 8 on 8 ranks: each GPU is one worker (both of its neighbours on other GPUs)."""
+    """The multi-GPU engines, shipping only theta: the default (auto) = the temporally blocked kernel
+    inside every rank's segment, edge workers exchanging theta every phase -- in the one-position halo
+    mode when every segment has >= 2 workers and fits one workgroup with its halo heads (the rank
+    holding a boundary tail also solves the other rank's boundary head, whose shard it holds: one per
+    boundary), plain data-local otherwise (n = 24 on 2 ranks: 13 waves; n = 8 on 8 ranks) or with
+    GADMM_DL_HALO=0 (nohalo); per-worker = the one-workgroup-per-worker kernel.
+    Payload == 2 (N_ranks - 1) d 8 iters exactly in every mode; wire == 2 x payload (16-B granules);
+    iterations and trace == one GPU, bit for bit. n = 8 on 8 ranks: each GPU is one worker (both of its
+    neighbours on other GPUs)."""
     from gadmm_amd.parallel.launch import spawn
     from gadmm_amd.benchmarks import EXPECTED_ITERS_1E8
     res = spawn(_solver_rank, world, n, -1, 20.0, engine, timeout=300)
     it = EXPECTED_ITERS_1E8[(n, 3.0)]
-    want = "xgmi(blocked-dl)" if engine == "auto" else "xgmi"
+    # the halo mode needs every segment >= 2 workers and segment + halo heads <= 12 waves on every rank
+    segs = [(r * n // world, (r + 1) * n // world - 1) for r in range(world)]
+    span = [hi - lo + 1 + int(lo > 0 and lo % 2 == 1) + int(hi < n - 1 and hi % 2 == 1) for lo, hi in segs]
+    halo = engine == "auto" and all(hi > lo for lo, hi in segs) and max(span) <= 12
+    want = "xgmi(blocked-dl-halo)" if halo else ("xgmi(blocked-dl)" if engine in ("auto", "nohalo") else "xgmi")
     for r in res:
         assert r["kind0"] == want and r["kind"] == want and not r["fallbacks"], (r["kind0"], r["fallbacks"])
-        assert r["replicated"] == 0
-        if engine == "auto":
-            assert r["kernel"].startswith("blocked-dl(")
+        if engine in ("auto", "nohalo"):
+            assert r["kernel"].startswith("blocked-dl-halo[" if halo else "blocked-dl("), r["kernel"]
         for o in r["outs"]:
             assert o[0] == it and o[1] == 1
+    # one neighbour head's shard (m x (d + 1) doubles) per rank boundary in the halo mode, none otherwise
+    assert sum(r["replicated"] for r in res) == ((world - 1) * 50 * 51 * 8 if halo else 0)
     pay = sum(r["outs"][-1][2] for r in res)
     assert pay == 2 * (world - 1) * 50 * 8 * it
     assert sum(r["outs"][-1][3] for r in res) == 2 * pay
