@@ -180,15 +180,20 @@ class NativeChainEngine:
             self.theta = torch.zeros((self.n_total, d), dtype=f64, device=dev)
             self.mu = torch.zeros((nl, d), dtype=f64, device=dev)
             self.objw = torch.zeros((nl,), dtype=f64, device=dev)
-            self.trace = torch.full((self.max_iter,), float("nan"), dtype=f64, device=dev)
+            # read-back block, one device buffer so that a persistent solve's results come back in ONE
+            # device-to-host copy: [ctl (8 x i32) | t0stamp | pad x 3 | trace (max_iter) | tstamp (max_iter)]
+            mi = self.max_iter
+            self._rb = torch.zeros((8 + 2 * mi,), dtype=f64, device=dev)
+            self.ctl = self._rb[0:4].view(torch.int32)
+            self.t0stamp = self._rb[4:5].view(torch.int64)
+            self.trace = self._rb[8:8 + mi]
+            self.trace.fill_(float("nan"))
             # multi-rank stop rule: per-worker objectives [ring][n_total] (gid-indexed, see gadmm_chain.h)
             self.part = torch.zeros((self.ring * self.n_total,), dtype=f64, device=dev)
             self.reduced = torch.zeros((self.ring * self.n_total,), dtype=f64, device=dev)
             self.lgid = torch.tensor(self.local_ids, dtype=torch.int32, device=dev)
-            # real clock: s_memrealtime (100 MHz) of each iteration's decision, and of the solve start
-            self.tstamp = torch.zeros((self.max_iter,), dtype=torch.int64, device=dev)
-            self.t0stamp = torch.zeros((1,), dtype=torch.int64, device=dev)
-            self.ctl = torch.zeros((8,), dtype=torch.int32, device=dev)
+            # real clock: s_memrealtime (100 MHz) of each iteration's decision (and t0stamp: the solve start)
+            self.tstamp = self._rb[8 + mi:8 + 2 * mi].view(torch.int64)
             self.slots = torch.zeros((max(2 * nl, 2) * 4,), dtype=torch.int32, device=dev)
             self.inner_iters = torch.zeros((max(nl, 1),), dtype=torch.int32, device=dev)
             self.A = self.b = self.yy = self.Minv = None
@@ -782,19 +787,18 @@ class NativeChainEngine:
                 native.check(rc, "chain_persistent_launch")
             # the control block comes back with the same stream sync (pinned buffer, async copy queued
             # behind the kernel): no second blocking round trip per solve
-            if getattr(self, "_ctl_host", None) is None:
-                self._ctl_host = torch.empty(self.ctl.shape, dtype=self.ctl.dtype, pin_memory=True)
-            self._ctl_host.copy_(self.ctl, non_blocking=True)
-            # the objective trace and the clock come back behind the same sync too (short traces:
-            # traces() then reads the pinned copy instead of a second blocking device round trip)
+            # the objective trace and the clock come back behind the same sync as the control block, in
+            # one copy of the read-back block (short traces: traces() then reads the pinned copy instead of
+            # a second blocking device round trip); without them, only the control block's words
             nt = self.trace.numel()
             fetch = fetch_trace and nt <= 16384
+            if getattr(self, "_rb_host", None) is None:
+                self._rb_host = torch.empty(self._rb.shape, dtype=torch.float64, pin_memory=True)
+                self._ctl_host = self._rb_host[0:4].view(torch.int32)
             if fetch:
-                if getattr(self, "_tr_host", None) is None or self._tr_host.numel() != 2 * nt + 1:
-                    self._tr_host = torch.empty((2 * nt + 1,), dtype=torch.float64, pin_memory=True)
-                self._tr_host[:nt].copy_(self.trace, non_blocking=True)
-                self._tr_host[nt:2 * nt].copy_(self.tstamp[:nt].view(torch.float64), non_blocking=True)
-                self._tr_host[2 * nt:].copy_(self.t0stamp.view(torch.float64), non_blocking=True)
+                self._rb_host.copy_(self._rb, non_blocking=True)
+            else:
+                self._rb_host[0:4].copy_(self._rb[0:4], non_blocking=True)
             self.stream.synchronize()
             self._tr_valid = fetch
             t1 = _time.perf_counter()
@@ -836,11 +840,11 @@ class NativeChainEngine:
         if upto <= 0:
             return np.zeros((0,), dtype=np.float64), np.zeros((0,), dtype=np.float64)
         if getattr(self, "_tr_valid", False) and upto <= self.trace.numel():  # pinned copy of the last persistent run
-            h = self._tr_host.numpy()
+            h = self._rb_host.numpy()
             nt = self.trace.numel()
-            t = h[nt:nt + upto].view(np.int64)
-            t0 = int(h[2 * nt:].view(np.int64)[0])
-            return h[:upto].copy(), np.where(t > 0, (t - t0) * 1e-8, 0.0)
+            t = h[8 + nt:8 + nt + upto].view(np.int64)
+            t0 = int(h[4:5].view(np.int64)[0])
+            return h[8:8 + upto].copy(), np.where(t > 0, (t - t0) * 1e-8, 0.0)
         with torch.cuda.stream(self.stream):
             buf = torch.cat([self.trace[:upto], self.tstamp[:upto].view(torch.float64),
                              self.t0stamp.view(torch.float64)]).cpu().numpy()

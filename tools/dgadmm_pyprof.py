@@ -40,3 +40,4 @@ pr.disable()
 print("engine", r.extra.get("engine"), "iters", r.iters)
 st = pstats.Stats(pr)
 st.sort_stats("tottime").print_stats(30)
+st.sort_stats("cumulative").print_stats(45)
