@@ -21,6 +21,7 @@ Two executions of the same schedule:
 """
 from __future__ import annotations
 
+import os
 import time
 from typing import List, Optional, Sequence
 
@@ -30,6 +31,7 @@ import torch
 from ..parallel.comm import Comm, LocalComm
 from ..parallel.topology import rechain_iterations, PathSchedule, Placement, chain_plan
 from .base import global_objective_and_residual, RunResult, Stopper, total_bytes, global_objective, run_bytes
+from ..utils import timing as _timing
 from ..utils.timing import roctx_range
 
 
@@ -230,6 +232,11 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
 _RECHAINS: dict = {}
 
 
+# streamed D-GADMM epochs: chains drawn before the launch (epoch 0 + the next ones); the kernel spends
+# ~17 us per epoch at coherence 10, the host ~1 us per drawn chain, so the stream stays ahead
+STREAM_K0 = 4
+
+
 def _rechains(max_iter: int, coherence) -> np.ndarray:
     """``rechain_iterations`` memoised per (max_iter, coherence) (read-only array)."""
     key = (int(max_iter), float(coherence))
@@ -260,6 +267,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     iterations ``start_iter..iters`` like the torch path's."""
     from ..engine.chain_engine import NativeChainEngine, ResidencyError, HandoffTimeout
 
+    _timing.host_stamp("native:start")
     rank = comm.rank
     rcomm = comm if comm.nranks > 1 else None
     fabric = opts.get("fabric")
@@ -292,7 +300,9 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             cache[key] = eng
     else:
         eng.set_targets(obj0, tol)
+    _timing.host_stamp("native:engine")
     eng.set_path(schedule.path, placement, rank)
+    _timing.host_stamp("native:set_path")
     start = 1 if state is None else int(state[2])
     static = _static_schedule(schedule, max_iter)
     if state is not None and not (static and comm.nranks == 1):
@@ -307,6 +317,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
                 eng.mu.copy_(state[1].to(eng.mu.device, torch.float64).reshape(eng.mu.shape))
 
     load_state()
+    _timing.host_stamp("native:reset")
     stop_iter = int(opts.get("stop_iter", 0))
     if fresh or state is not None:
         # inputs made on other streams (a new engine's set-up, a loaded state) are complete before the
@@ -396,15 +407,28 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         while True:
             e1 = min(e0 + chunk, E_total)  # this launch executes epochs e0 .. e1 - 1
             look = e1 if e1 < E_total else e1 - 1  # + the next epoch's chain (push targets of theta^hard_stop)
-            ensure(look)
+            _timing.host_stamp("dyn:chunk_setup")
+            # streamed epochs (blocked dynamic mode, first launch): only the first STREAM_K0 chains are
+            # drawn before the launch; the kernel runs epoch 0 while run_persistent draws the rest (the
+            # same RNG stream, in order) and streams their table rows in
+            stream = use_blk and not cont and comm.nranks == 1 and os.environ.get("GADMM_DYN_STREAM", "0") == "1" \
+                and look - e0 + 1 > STREAM_K0
+            ensure(e0 + STREAM_K0 - 1 if stream else look)
+            _timing.host_stamp("dyn:draws")
             hard_stop = ep_start[e1] - 1 if e1 < E_total else 0
             st_arr = ep_start[e0:look + 1]
-            P_arr = Pall[e0:look + 1]
+            P_arr = Pall[e0:e0 + STREAM_K0] if stream else Pall[e0:look + 1]
+
+            def feed(c):
+                first = n_drawn[0]
+                ensure(first + c - 1)
+                return Pall[first:first + c]
+
             timed_out = None
             try:
                 r = eng.run_persistent(epochs=(st_arr, P_arr), fabric=fabric, start_iter=start_iter,
                                        pending_in=pending_in, hard_stop=hard_stop, cont=cont, fetch_trace=True,
-                                       blocked_dyn=use_blk)
+                                       blocked_dyn=use_blk, feed=feed if stream else None)
             except HandoffTimeout as e:
                 if comm.nranks == 1:
                     raise
@@ -435,6 +459,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             start_iter, pending_in, cont = hard_stop + 1, 1, True
             e0 = e1 - 1  # epoch 0 of the next launch: this chunk's last (the flush of pending duals)
             chunk = min(2 * chunk, cap)
+        _timing.host_stamp("dyn:launches_done")
         if done == 5:
             done = 2
         ep_start = ep_start[:n_drawn[0]]
@@ -486,6 +511,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             if comm.nranks > 1:
                 eng.exchange("tail")  # refresh ghost rows of the new cross-rank neighbours
             it = nxt
+    _timing.host_stamp("native:solved")
     eng.stream.synchronize()  # every engine path has synchronised its stream already: cheap
     wall = time.perf_counter() - t0
     tr, tt = eng.traces(iters)
@@ -524,6 +550,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
                            "solver": local_solver, "monitor_bytes": int(mon), "wire_bytes": int(wire),
                            "transport": getattr(comm, "backend", "local") if fabric is None else "xgmi"})
     res.extra["engine_obj"] = eng
+    _timing.host_stamp("native:result")
     if opts.get("state", True):
         # resumable state for checkpoints: apply the heads' pending (lazy) duals with the current
         # chain, so (theta, mu) is the reference state after iteration next-1

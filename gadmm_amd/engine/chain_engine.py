@@ -23,6 +23,7 @@ import numpy as np
 import torch
 
 from ..ops import native
+from ..utils import timing as _timing
 from ..ops.linalg import gram, spd_inverse
 from ..parallel.topology import Placement, chain_plan, RankPlan
 
@@ -441,11 +442,16 @@ class NativeChainEngine:
         """Workgroups of the per-worker persistent kernel this device can keep resident at once
         (occupancy x CUs, ``GADMM_CU_BUDGET`` shrinks the CU count): a persistent launch needs all of
         them together, so eligibility is decided here, up front, not by a spin deadline."""
-        pa = native.PersistArgs()
-        pa.d, pa.n, pa.nvar, pa.obj_mode = self.d, self.n_total, self.nvar, self._obj_mode(dynamic)
-        pa.n_epochs = 1 if dynamic else 0
-        pa.sys_scope = 1 if sys_scope else 0
-        return int(self.lib.gadmm_chain_persistent_capacity(ctypes.byref(pa)))
+        # memoised per (mode, the env switches the launcher reads): a D-GADMM solve asks on every call
+        key = (bool(dynamic), bool(sys_scope), os.environ.get("GADMM_CU_BUDGET"), os.environ.get("GADMM_PERSIST_LDS"))
+        memo = self.__dict__.setdefault("_cap_memo", {})
+        if key not in memo:
+            pa = native.PersistArgs()
+            pa.d, pa.n, pa.nvar, pa.obj_mode = self.d, self.n_total, self.nvar, self._obj_mode(dynamic)
+            pa.n_epochs = 1 if dynamic else 0
+            pa.sys_scope = 1 if sys_scope else 0
+            memo[key] = int(self.lib.gadmm_chain_persistent_capacity(ctypes.byref(pa)))
+        return memo[key]
 
     def _logi_args(self) -> native.LogiArgs:
         g = native.LogiArgs()
@@ -525,20 +531,25 @@ class NativeChainEngine:
         """(k, L, W, pw) of the temporally blocked kernel for this engine, or None (multi-GPU, d > 64,
         GADMM_BLOCKED=0). pw = positions per wave: 1 = the 12-wave kernel (default, also the only
         instrumented one, so ``timeline`` selects it), 2 = the paired 8-wave kernel (GADMM_BLOCK_PW=2)."""
-        import os
-
         if fabric is not None or self.nranks > 1 or self.d > 64 or os.environ.get("GADMM_BLOCKED", "1") == "0":
             return None
-        kk, ll, pp = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
-        want = int(os.environ.get("GADMM_BLOCK_K", "0"))
-        W = int(self.lib.gadmm_chain_blocked_plan2(self.n_total, self.d, want, 1 if timeline else 0, ctypes.byref(kk),
-                                                   ctypes.byref(ll), ctypes.byref(pp)))
-        return (kk.value, ll.value, W, pp.value) if W > 0 else None
+        # memoised per (timeline, the env switches the planner reads)
+        key = (bool(timeline), os.environ.get("GADMM_BLOCK_K"), os.environ.get("GADMM_BLOCK_L"),
+               os.environ.get("GADMM_BLOCK_PW"), os.environ.get("GADMM_CU_BUDGET"))
+        memo = self.__dict__.setdefault("_plan2_memo", {})
+        if key not in memo:
+            kk, ll, pp = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
+            want = int(os.environ.get("GADMM_BLOCK_K", "0"))
+            W = int(self.lib.gadmm_chain_blocked_plan2(self.n_total, self.d, want, 1 if timeline else 0,
+                                                       ctypes.byref(kk), ctypes.byref(ll), ctypes.byref(pp)))
+            memo[key] = (kk.value, ll.value, W, pp.value) if W > 0 else None
+        return memo[key]
 
     def run_persistent(self, lag: int = 4, timeout_s: float = 20.0, start_iter: int = 1,
                        pending_in: int = 0, fabric=None, timeline_iters: int = 0,
                        epochs: Optional[Sequence] = None, hard_stop: int = 0, cont: bool = False,
-                       fetch_trace: bool = False, blocked_dyn: Optional[bool] = None) -> EngineRun:
+                       fetch_trace: bool = False, blocked_dyn: Optional[bool] = None,
+                       feed=None, feed_batch: int = 8) -> EngineRun:
         """Whole solve in one launch per GPU. State must be reset (``reset()``) or resumed by the
         caller. ``fabric``: an ``XgmiFabric`` for the multi-GPU device-initiated transport.
         ``timeline_iters > 0`` records s_memrealtime stamps (10 ns) of the first iterations into
@@ -557,7 +568,13 @@ class NativeChainEngine:
         previous chunk's last epoch (its heads' pending duals are flushed with that chain).
         ``fetch_trace``: the objective trace and clock come back behind the same stream sync (for a
         caller that reads ``traces()`` next; a benchmark loop that does not leaves it off).
-        ``blocked_dyn``: D-GADMM on the blocked kernel's dynamic mode (None: ``dynamic_uses_blocked``)."""
+        ``blocked_dyn``: D-GADMM on the blocked kernel's dynamic mode (None: ``dynamic_uses_blocked``).
+        ``feed`` (blocked dynamic mode, one GPU, first launch of a solve): streamed epochs -- ``epochs``
+        holds the starts of ALL the launch's epochs but the chains of only the first few; the kernel is
+        launched at once, and ``feed(count)`` (the caller's chain draws, (count, n) rows) supplies the
+        rest ``feed_batch`` at a time while it runs: each batch's table rows go up on a side stream,
+        followed by the count of valid rows (PersistArgs::ep_ready), which a re-chain waits for."""
+        _timing.host_stamp("rp:start")
         if epochs is not None:
             if not self.dynamic_eligible(fabric):
                 raise RuntimeError("dynamic persistent kernel not eligible for this engine/config")
@@ -657,7 +674,7 @@ class NativeChainEngine:
                 self._xchk = torch.zeros((256 * 4,), dtype=torch.int32, device=dev)
             pa.xchk, pa.xcd = self._xchk.data_ptr(), int(self.xcd)
         pa.hard_stop, pa.cont = int(hard_stop), 1 if cont else 0
-        ep_keep = None
+        _timing.host_stamp("rp:args")
         if epochs is not None:
             if isinstance(epochs, tuple) and len(epochs) == 2 and isinstance(epochs[1], np.ndarray):
                 starts = np.asarray(epochs[0], dtype=np.int64)                      # (starts, paths) arrays
@@ -667,7 +684,12 @@ class NativeChainEngine:
                 P = np.asarray([list(e[1]) for e in epochs], dtype=np.int64)       # (E, n) position -> worker
             if (starts[0] > int(start_iter) if cont else starts[0] != int(start_iter)) or np.any(starts[1:] <= starts[:-1]):
                 raise ValueError("epochs must start at start_iter (continuations: at or before it) and increase")
-            E, n = P.shape
+            K, n = P.shape  # chains known now (streamed epochs: the first K of len(starts))
+            E = len(starts) if feed is not None else K
+            if feed is not None and (plan is None or fabric is not None or not 1 <= K <= E):
+                raise ValueError("streamed epochs: blocked dynamic mode on one GPU, 1 <= known chains <= epochs")
+            if feed is None and K != len(starts):
+                raise ValueError("epochs: one chain per start")
             loc = np.asarray([int(w) for w in self.local_ids], dtype=np.int64)
             if plan is not None:
                 # blocked kernel (one GPU, every worker local: li == worker id): slots in chain-POSITION
@@ -678,7 +700,7 @@ class NativeChainEngine:
                 es = np.empty((E * n * 4,), dtype=np.int32)
                 pp = np.empty((E * n,), dtype=np.int32)
                 fl = np.empty((E * n * 2,), dtype=np.int32)
-                native.check(self.lib.gadmm_epoch_tables_blocked(P.ctypes.data, E, n, es.ctypes.data, pp.ctypes.data,
+                native.check(self.lib.gadmm_epoch_tables_blocked(P.ctypes.data, K, n, es.ctypes.data, pp.ctypes.data,
                                                                  fl.ctypes.data), "epoch_tables_blocked")
             else:
                 # per-worker kernel: the slot / position of every LOCAL worker per epoch (native C++
@@ -710,27 +732,38 @@ class NativeChainEngine:
             stage = getattr(self, "_ep_stage", None)
             if stage is None or stage[0].numel() < total:
                 cap = max(total, 4096)
-                stage = (torch.empty((cap,), dtype=torch.int32, pin_memory=True),
-                         torch.empty((cap,), dtype=torch.int32, device=dev))
+                h_t = torch.empty((cap,), dtype=torch.int32, pin_memory=True)
+                d_t = torch.empty((cap,), dtype=torch.int32, device=dev)
+                stage = (h_t, d_t, h_t.numpy(), h_t.data_ptr(), d_t.data_ptr())
                 self._ep_stage = stage
-            host = stage[0].numpy()
+            host, hptr, dptr = stage[2], stage[3], stage[4]
+            o_es, o_pp, o_pm, o_fl = ns, ns + nes, ns + nes + pp.size, total - fl.size
             host[:ns] = starts
-            host[ns:ns + nes] = es
-            host[ns + nes:ns + nes + pp.size] = pp
-            host[ns + nes + pp.size:ns + nes + pp.size + pm.size] = pm
-            host[total - fl.size:total] = fl
-            with torch.cuda.stream(self.stream):
-                stage[1][:total].copy_(stage[0][:total], non_blocking=True)
-            st_t, es_t = stage[1][:ns], stage[1][ns:ns + nes]
-            pp_t, pm_t = stage[1][ns + nes:ns + nes + pp.size], stage[1][ns + nes + pp.size:total - fl.size]
-            fl_t = stage[1][total - fl.size:total]
-            ep_keep = (st_t, es_t, pp_t, pm_t, fl_t)
+            host[o_es:o_pp] = es
+            host[o_pp:o_pm] = pp
+            host[o_pm:o_fl] = pm
+            host[o_fl:total] = fl
+            if feed is None:
+                native.check(self.lib.gadmm_memcpy_h2d_async(dptr, hptr, total * 4, self.stream.cuda_stream), "h2d")
+            else:
+                # streamed epochs: the kernel reads every table row straight from a mapped host buffer
+                # (no copy and no second stream: a persistent kernel waiting on another stream's copies
+                # can deadlock when the streams share a hardware queue); rows >= K and then the count of
+                # valid rows are written by _stream_epochs while it runs
+                mh = self._mapped_stage(total + 1)
+                hm, hm_ptr, dm_ptr = mh
+                hm[:total] = host[:total]
+                hm[total] = 0  # the valid-row count (PersistArgs::ep_ready)
+                dptr = dm_ptr
+                pa.ep_ready, pa.ep_ready0 = dm_ptr + 4 * total, int(K)
+                stream_state = (K, n, E, P[-1].copy(), o_es, o_fl, hm, total)
             if fl.size:
-                pa.ep_flush = fl_t.data_ptr()
+                pa.ep_flush = dptr + 4 * o_fl
             pa.n_epochs = len(starts)
-            pa.epoch_start, pa.ep_slots, pa.ep_pos = st_t.data_ptr(), es_t.data_ptr(), pp_t.data_ptr()
+            pa.epoch_start, pa.ep_slots, pa.ep_pos = dptr, dptr + 4 * o_es, dptr + 4 * o_pp
             if fabric is not None:
-                pa.ep_push, pa.peer_thg = pm_t.data_ptr(), keep[0].data_ptr()
+                pa.ep_push, pa.peer_thg = dptr + 4 * o_pm, keep[0].data_ptr()
+        _timing.host_stamp("rp:tables")
         tl = None
         if timeline_iters > 0:
             tl = torch.zeros((max(len(slots), 256) + 1, int(timeline_iters), 8), dtype=torch.int64, device=dev)
@@ -759,8 +792,13 @@ class NativeChainEngine:
         with torch.cuda.stream(self.stream):
             t0 = _time.perf_counter()
             rc = None
+            _timing.host_stamp("rp:prelaunch")
             if plan is not None:
                 rc = int(self.lib.gadmm_chain_blocked_launch(ctypes.byref(pa), self.stream.cuda_stream))
+                _timing.host_stamp("rp:launched")
+                if rc == 0 and feed is not None:
+                    self._stream_epochs(feed, int(feed_batch), *stream_state)
+                    _timing.host_stamp("rp:streamed")
                 if rc == -2 and epochs is None:  # its workgroups cannot all be resident: the per-worker kernel
                     plan, rc = None, None
                     self.last_kernel = "per-worker"
@@ -799,7 +837,9 @@ class NativeChainEngine:
                 self._rb_host.copy_(self._rb, non_blocking=True)
             else:
                 self._rb_host[0:4].copy_(self._rb[0:4], non_blocking=True)
+            _timing.host_stamp("rp:copies_queued")
             self.stream.synchronize()
+            _timing.host_stamp("rp:synced")
             self._tr_valid = fetch
             t1 = _time.perf_counter()
         self.last_timeline = tl.cpu().numpy() if tl is not None else None
@@ -834,6 +874,42 @@ class NativeChainEngine:
             p2p = msgs * self.d * 8
             mon = ran * (len(slots) * 16 if self.rank != 0 else 8 * (self.nranks - 1))
         return EngineRun(conv, done, nxt - start_iter, 1, (t1 - t0) * 1e3, p2p, msgs, mon, 2 * p2p)
+
+    def _mapped_stage(self, count: int):
+        """(numpy int32 view, host ptr, device ptr) of a mapped coherent host buffer of >= ``count``
+        ints (gadmm_host_alloc), kept per engine."""
+        ms = getattr(self, "_mstage", None)
+        if ms is None or ms[0].size < count:
+            if ms is not None:
+                self.lib.gadmm_host_free(ms[1])
+            cap = max(count, 65536)
+            hp, dp = ctypes.c_void_p(), ctypes.c_void_p()
+            native.check(self.lib.gadmm_host_alloc(cap * 4, ctypes.byref(hp), ctypes.byref(dp)), "host_alloc")
+            arr = np.ctypeslib.as_array(ctypes.cast(hp, ctypes.POINTER(ctypes.c_int32)), shape=(cap,))
+            ms = (arr, hp.value, dp.value)
+            self._mstage = ms
+        return ms
+
+    def _stream_epochs(self, feed, batch: int, K: int, n: int, E: int, last: np.ndarray, o_es: int, o_fl: int,
+                       hm: np.ndarray, cnt_at: int):
+        """Streamed epochs (run_persistent ``feed``): draws epochs K..E-1 in batches while the kernel runs,
+        builds their slot / flush rows (a batch's first flush row needs the previous chain) into the
+        mapped host buffer the kernel reads, then raises the valid-row count (x86 stores stay in order)."""
+        rows, prev = K, last
+        while rows < E:
+            c = min(max(batch, 1), E - rows)
+            Pn = np.ascontiguousarray(np.vstack([prev[None, :], np.asarray(feed(c), dtype=np.int64)]))
+            es = np.empty(((c + 1) * n * 4,), dtype=np.int32)
+            pp = np.empty(((c + 1) * n,), dtype=np.int32)
+            fl = np.empty(((c + 1) * n * 2,), dtype=np.int32)
+            native.check(self.lib.gadmm_epoch_tables_blocked(Pn.ctypes.data, c + 1, n, es.ctypes.data, pp.ctypes.data,
+                                                             fl.ctypes.data), "epoch_tables_blocked")
+            a_es, a_fl = o_es + rows * n * 4, o_fl + rows * n * 2
+            hm[a_es:a_es + c * n * 4] = es[n * 4:]
+            hm[a_fl:a_fl + c * n * 2] = fl[n * 2:]
+            rows += c
+            hm[cnt_at] = rows
+            prev = Pn[-1]
 
     def traces(self, upto: int):
         """(objective trace, measured clock) of iterations 1..upto in ONE device-to-host copy."""
@@ -889,6 +965,10 @@ class NativeChainEngine:
         if getattr(self, "handle", None):
             self.lib.gadmm_chain_engine_destroy(self.handle)
             self.handle = None
+        ms = getattr(self, "_mstage", None)
+        if ms is not None:  # no kernel reads it any more: every launch ended in its stream's sync
+            self._mstage = None
+            self.lib.gadmm_host_free(ms[1])
 
     def __del__(self):  # pragma: no cover
         try:

@@ -7,6 +7,8 @@
   (``group_ADMM_closedForm.m:39-42,53-55``). Useful to regenerate the paper's "clock time" panels;
   real wall time (including communication) is what the framework reports by default.
 * ``roctx_range``: named ranges for rocprofv3 traces when roctx is available (no-op otherwise).
+* ``host_stamp``: labelled host clock stamps at fixed points of the native solve path, recorded only
+  while a tool has set ``HOST_STAMPS`` to a list (tools/dgadmm_host_stamps.py); a no-op otherwise.
 """
 from __future__ import annotations
 
@@ -17,6 +19,14 @@ from typing import Optional
 
 import numpy as np
 import torch
+
+
+HOST_STAMPS: Optional[list] = None
+
+
+def host_stamp(label: str) -> None:
+    if HOST_STAMPS is not None:
+        HOST_STAMPS.append((label, time.perf_counter()))
 
 
 class WallTimer:
