@@ -199,12 +199,5 @@ struct PersistArgs {
   // with them at the re-chain), as int pairs [n_epochs][n][2]. Built on the host, so a re-chain
   // issues two independent table loads instead of a chain of three dependent ones.
   const int* ep_flush;
-  // DYN, streamed epochs (blocked kernel): when ep_ready is set, only the slot / flush rows of epochs
-  // [0, ep_ready0) are valid at the launch; the host draws the later chains while the kernel runs,
-  // copies their rows in, and then raises *ep_ready (device memory, written by a copy queued behind
-  // the rows on another stream) to the number of valid rows. A re-chain to an epoch beyond the rows a
-  // wave has staged polls it (system scope). epoch_start is complete at the launch.
-  const int* ep_ready;
-  int ep_ready0, pad_ep;
 };
 constexpr int XCHK = 256;  // placement-check granules (>= workgroups of any XCD-packed launch)

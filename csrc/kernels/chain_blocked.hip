@@ -73,53 +73,15 @@ __device__ __forceinline__ void quad_load_image(double (&m)[4][QT], const double
     }
 }
 
-// Stages a launch's epoch tables for chain position q into this wave's LDS rows (DYN): the epoch
-// starts of every epoch, and the slot / flush rows of the epochs valid at the launch (all of them, or
-// [0, ep_ready0) when the host streams the rest); returns the number of staged rows. The wave's own
-// later LDS reads are ordered after these stores (in-order LDS within a wave).
-__device__ __forceinline__ int stage_epochs(const PersistArgs& a, int q, const EpochLds& el, bool flush) {
+// Stages a launch's epoch tables for chain position q into this wave's LDS rows (DYN); the wave's
+// own later LDS reads are ordered after these stores (in-order LDS within a wave).
+__device__ __forceinline__ void stage_epochs(const PersistArgs& a, int q, const EpochLds& el, bool flush) {
   const int lane = threadIdx.x & 63;
-  const int rows = a.ep_ready ? a.ep_ready0 : a.n_epochs;
   for (int e = lane; e < a.n_epochs; e += 64) {
-    if (e < rows) {
-      el.sl[e] = reinterpret_cast<const int4*>(a.ep_slots)[(long)e * a.n + q];
-      if (flush) el.fl[e] = reinterpret_cast<const int2*>(a.ep_flush)[(long)e * a.n + q];
-    }
+    el.sl[e] = reinterpret_cast<const int4*>(a.ep_slots)[(long)e * a.n + q];
+    if (flush) el.fl[e] = reinterpret_cast<const int2*>(a.ep_flush)[(long)e * a.n + q];
     el.st[e] = a.epoch_start[e];
   }
-  return rows;
-}
-
-// Streamed epochs: waits until the host has delivered row `need - 1` (ep_ready >= need, polled at
-// system scope: the counter and the rows are written by copies, never cached here before), then stages
-// rows [staged, ready) with system-scope loads; returns the new staged count, or -1 on the deadline.
-__device__ __forceinline__ int stage_more(const PersistArgs& a, int q, const EpochLds& el, bool flush, int staged,
-                                       int need, unsigned long long deadline) {
-  const int lane = threadIdx.x & 63;
-  int ready = 0;
-  for (int spin = 0;; ++spin) {
-    ready = __hip_atomic_load(a.ep_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    ready = __builtin_amdgcn_readfirstlane(ready);
-    if (ready >= need) break;
-    if ((spin & 7) == 7 && now_ticks() > deadline) return -1;
-    GADMM_POLL_PAUSE();
-  }
-  if (ready > a.n_epochs) ready = a.n_epochs;
-  for (int e = staged + lane; e < ready; e += 64) {
-    const int* s4 = reinterpret_cast<const int*>(a.ep_slots) + ((long)e * a.n + q) * 4;
-    int4 v;
-    v.x = __hip_atomic_load(s4, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    v.y = __hip_atomic_load(s4 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    v.z = __hip_atomic_load(s4 + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    v.w = __hip_atomic_load(s4 + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    el.sl[e] = v;
-    if (flush) {
-      const int* f2 = a.ep_flush + ((long)e * a.n + q) * 2;
-      el.fl[e] = make_int2(__hip_atomic_load(f2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                           __hip_atomic_load(f2 + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-    }
-  }
-  return ready;
 }
 }  // namespace
 
@@ -190,8 +152,7 @@ __device__ __forceinline__ void blocked_objective(const PersistArgs& a, double* 
   const long ring_base = 2L * n * 2 * d;  // theta ring [ring][n][d] after the exchange table
   // DYN: this wave's epoch rows staged in LDS after the staging area (see DYN_LDS_BYTES)
   const EpochLds el = epoch_lds(lds + MAXW * 64 + MAXW * QSTAGE, v);
-  int staged = 0;
-  if constexpr (DYN) staged = stage_epochs(a, q, el, false);
+  if constexpr (DYN) stage_epochs(a, q, el, false);
   PhaseSlot so = DYN ? a.ep_slots[q] : a.slots[q];
   const bool in = lane < d;
   double Aq[4][QT];
@@ -206,17 +167,13 @@ __device__ __forceinline__ void blocked_objective(const PersistArgs& a, double* 
       if (it == next_start) {  // D-GADMM re-chain: another worker now sits at position q
         ++ep;
         next_start = ep + 1 < a.n_epochs ? el.st[ep + 1] : 0x7fffffff;
-        if (ep >= staged) {  // streamed epochs: the host has not delivered this row yet
-          staged = stage_more(a, q, el, false, staged, ep + 1, deadline);
-          if (staged < 0) return;  // the monitor times out and reports it
-        }
         {
           const int4 s4 = el.sl[ep];
           so.li = s4.x;
           so.gid = s4.y;
         }
-        int od = __builtin_amdgcn_readfirstlane(d);  // laundered: the reload's bounds masks are not
-        asm volatile("" : "+s"(od));                   // hoisted out of the loop (SGPRs)
+        int od = d;  // laundered: the reload's bounds masks are not hoisted out of the loop (SGPRs)
+        asm volatile("" : "+s"(od));
         quad_load<QT>(Aq, a.A + (long)so.li * od * od, od, true);
         bo = in ? a.b[(long)so.li * d + lane] : 0.0;
         hy = 0.5 * a.yy[so.li];
@@ -378,9 +335,8 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
 
   // DYN: this wave's epoch rows in LDS (after thS and the staging area; see DYN_LDS_BYTES)
   const EpochLds el = epoch_lds(lds + MAXW * 64 + MAXW * QSTAGE, v);
-  int staged = 0;
   if constexpr (DYN) {
-    if (active) staged = stage_epochs(a, p, el, true);
+    if (active) stage_epochs(a, p, el, true);
   }
   // Positions that ever solve: in a block, phase phi solves the owned range widened by 2k - 1 - phi,
   // so heads up to 2k - 1 and tails up to 2k - 2 positions away from it; the outermost halo only
@@ -494,13 +450,6 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
         }
         ++ep;
         next_start = ep + 1 < a.n_epochs ? el.st[ep + 1] : 0x7fffffff;
-        if (active && ep >= staged) {  // streamed epochs: the host has not delivered this row yet
-          staged = stage_more(a, p, el, true, staged, ep + 1, deadline);
-          if (staged < 0) {
-            if (lane == 0) abort_lds = 1;
-            staged = a.n_epochs;  // stale rows below; the abort ends the solve at the barrier
-          }
-        }
         if (active) {
           {
             const int4 s4 = el.sl[ep];
@@ -1163,8 +1112,7 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   const bool tl = a.timeline != nullptr;
   if (a.n_epochs > 0) {  // D-GADMM in one launch: one GPU, 12-wave layout, no instrumentation
     if (multi || tl || a.sys_scope || !a.epoch_start || !a.ep_slots || !a.ep_pos || !a.minv_pad || !a.ep_flush ||
-        a.hard_stop < 0 || (a.hard_stop > 0 && a.hard_stop < a.start_iter) || a.n_epochs > EPL ||
-        (a.ep_ready && (a.ep_ready0 < 1 || a.ep_ready0 > a.n_epochs))) {
+        a.hard_stop < 0 || (a.hard_stop > 0 && a.hard_stop < a.start_iter) || a.n_epochs > EPL) {
       gadmm_set_error("blocked chain kernel: dynamic epochs need one GPU, epoch tables (at most %d epochs per "
                       "launch), the padded inverse image (gadmm_chain_blocked_pad_len), no timeline", EPL);
       return -1;

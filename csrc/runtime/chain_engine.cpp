@@ -223,21 +223,6 @@ int gadmm_memcpy_h2d_async(void* dst, const void* src, size_t bytes, hipStream_t
   return 0;
 }
 
-// Mapped, coherent pinned host memory the persistent kernels read directly (the streamed D-GADMM epoch
-// rows and their valid-row count: the host writes rows, then the count; x86 stores stay in order, and
-// the kernel polls with system-scope loads). *hptr for the CPU, *dptr for kernels.
-int gadmm_host_alloc(size_t bytes, void** hptr, void** dptr) {
-  GADMM_CHECK(hipHostMalloc(hptr, bytes, hipHostMallocMapped | hipHostMallocCoherent));
-  memset(*hptr, 0, bytes);
-  GADMM_CHECK(hipHostGetDevicePointer(dptr, *hptr, 0));
-  return 0;
-}
-
-int gadmm_host_free(void* hptr) {
-  GADMM_CHECK(hipHostFree(hptr));
-  return 0;
-}
-
 int gadmm_chain_engine_reset(void* h, int start_iter, int pending) {
   ChainEngine* e = (ChainEngine*)h;
   return gadmm_chain_reset(e->desc.base.ctl, start_iter, pending, e->desc.stream);
@@ -350,8 +335,7 @@ int gadmm_abi_layout(long long* out, int n) {
                    (long long)offsetof(PersistArgs, ctl), (long long)offsetof(PhaseArgs, lgid),
                    (long long)offsetof(EngineDesc, xport), (long long)offsetof(PersistArgs, xchk),
                    (long long)offsetof(PersistArgs, dl_tab), (long long)offsetof(PersistArgs, minv_pad),
-                   (long long)offsetof(PersistArgs, ep_flush), (long long)offsetof(PersistArgs, ep_ready),
-                   (long long)offsetof(PersistArgs, ep_ready0)};
+                   (long long)offsetof(PersistArgs, ep_flush)};
   const int k = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n && i < k; ++i) out[i] = v[i];
   return k;

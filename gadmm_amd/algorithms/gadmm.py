@@ -21,7 +21,6 @@ Two executions of the same schedule:
 """
 from __future__ import annotations
 
-import os
 import time
 from typing import List, Optional, Sequence
 
@@ -232,11 +231,6 @@ def _chain_admm_torch(model, local_ids, n_total, rho, obj0, tol, max_iter, comm,
 _RECHAINS: dict = {}
 
 
-# streamed D-GADMM epochs: chains drawn before the launch (epoch 0 + the next ones); the kernel spends
-# ~17 us per epoch at coherence 10, the host ~1 us per drawn chain, so the stream stays ahead
-STREAM_K0 = 4
-
-
 def _rechains(max_iter: int, coherence) -> np.ndarray:
     """``rechain_iterations`` memoised per (max_iter, coherence) (read-only array)."""
     key = (int(max_iter), float(coherence))
@@ -408,27 +402,16 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             e1 = min(e0 + chunk, E_total)  # this launch executes epochs e0 .. e1 - 1
             look = e1 if e1 < E_total else e1 - 1  # + the next epoch's chain (push targets of theta^hard_stop)
             _timing.host_stamp("dyn:chunk_setup")
-            # streamed epochs (blocked dynamic mode, first launch): only the first STREAM_K0 chains are
-            # drawn before the launch; the kernel runs epoch 0 while run_persistent draws the rest (the
-            # same RNG stream, in order) and streams their table rows in
-            stream = use_blk and not cont and comm.nranks == 1 and os.environ.get("GADMM_DYN_STREAM", "0") == "1" \
-                and look - e0 + 1 > STREAM_K0
-            ensure(e0 + STREAM_K0 - 1 if stream else look)
+            ensure(look)
             _timing.host_stamp("dyn:draws")
             hard_stop = ep_start[e1] - 1 if e1 < E_total else 0
             st_arr = ep_start[e0:look + 1]
-            P_arr = Pall[e0:e0 + STREAM_K0] if stream else Pall[e0:look + 1]
-
-            def feed(c):
-                first = n_drawn[0]
-                ensure(first + c - 1)
-                return Pall[first:first + c]
-
+            P_arr = Pall[e0:look + 1]
             timed_out = None
             try:
                 r = eng.run_persistent(epochs=(st_arr, P_arr), fabric=fabric, start_iter=start_iter,
                                        pending_in=pending_in, hard_stop=hard_stop, cont=cont, fetch_trace=True,
-                                       blocked_dyn=use_blk, feed=feed if stream else None)
+                                       blocked_dyn=use_blk)
             except HandoffTimeout as e:
                 if comm.nranks == 1:
                     raise

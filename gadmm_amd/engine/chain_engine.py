@@ -548,8 +548,7 @@ class NativeChainEngine:
     def run_persistent(self, lag: int = 4, timeout_s: float = 20.0, start_iter: int = 1,
                        pending_in: int = 0, fabric=None, timeline_iters: int = 0,
                        epochs: Optional[Sequence] = None, hard_stop: int = 0, cont: bool = False,
-                       fetch_trace: bool = False, blocked_dyn: Optional[bool] = None,
-                       feed=None, feed_batch: int = 8) -> EngineRun:
+                       fetch_trace: bool = False, blocked_dyn: Optional[bool] = None) -> EngineRun:
         """Whole solve in one launch per GPU. State must be reset (``reset()``) or resumed by the
         caller. ``fabric``: an ``XgmiFabric`` for the multi-GPU device-initiated transport.
         ``timeline_iters > 0`` records s_memrealtime stamps (10 ns) of the first iterations into
@@ -568,12 +567,7 @@ class NativeChainEngine:
         previous chunk's last epoch (its heads' pending duals are flushed with that chain).
         ``fetch_trace``: the objective trace and clock come back behind the same stream sync (for a
         caller that reads ``traces()`` next; a benchmark loop that does not leaves it off).
-        ``blocked_dyn``: D-GADMM on the blocked kernel's dynamic mode (None: ``dynamic_uses_blocked``).
-        ``feed`` (blocked dynamic mode, one GPU, first launch of a solve): streamed epochs -- ``epochs``
-        holds the starts of ALL the launch's epochs but the chains of only the first few; the kernel is
-        launched at once, and ``feed(count)`` (the caller's chain draws, (count, n) rows) supplies the
-        rest ``feed_batch`` at a time while it runs: each batch's table rows go up on a side stream,
-        followed by the count of valid rows (PersistArgs::ep_ready), which a re-chain waits for."""
+        ``blocked_dyn``: D-GADMM on the blocked kernel's dynamic mode (None: ``dynamic_uses_blocked``)."""
         _timing.host_stamp("rp:start")
         if epochs is not None:
             if not self.dynamic_eligible(fabric):
@@ -684,11 +678,8 @@ class NativeChainEngine:
                 P = np.asarray([list(e[1]) for e in epochs], dtype=np.int64)       # (E, n) position -> worker
             if (starts[0] > int(start_iter) if cont else starts[0] != int(start_iter)) or np.any(starts[1:] <= starts[:-1]):
                 raise ValueError("epochs must start at start_iter (continuations: at or before it) and increase")
-            K, n = P.shape  # chains known now (streamed epochs: the first K of len(starts))
-            E = len(starts) if feed is not None else K
-            if feed is not None and (plan is None or fabric is not None or not 1 <= K <= E):
-                raise ValueError("streamed epochs: blocked dynamic mode on one GPU, 1 <= known chains <= epochs")
-            if feed is None and K != len(starts):
+            E, n = P.shape
+            if E != len(starts):
                 raise ValueError("epochs: one chain per start")
             loc = np.asarray([int(w) for w in self.local_ids], dtype=np.int64)
             if plan is not None:
@@ -700,7 +691,7 @@ class NativeChainEngine:
                 es = np.empty((E * n * 4,), dtype=np.int32)
                 pp = np.empty((E * n,), dtype=np.int32)
                 fl = np.empty((E * n * 2,), dtype=np.int32)
-                native.check(self.lib.gadmm_epoch_tables_blocked(P.ctypes.data, K, n, es.ctypes.data, pp.ctypes.data,
+                native.check(self.lib.gadmm_epoch_tables_blocked(P.ctypes.data, E, n, es.ctypes.data, pp.ctypes.data,
                                                                  fl.ctypes.data), "epoch_tables_blocked")
             else:
                 # per-worker kernel: the slot / position of every LOCAL worker per epoch (native C++
@@ -743,20 +734,7 @@ class NativeChainEngine:
             host[o_pp:o_pm] = pp
             host[o_pm:o_fl] = pm
             host[o_fl:total] = fl
-            if feed is None:
-                native.check(self.lib.gadmm_memcpy_h2d_async(dptr, hptr, total * 4, self.stream.cuda_stream), "h2d")
-            else:
-                # streamed epochs: the kernel reads every table row straight from a mapped host buffer
-                # (no copy and no second stream: a persistent kernel waiting on another stream's copies
-                # can deadlock when the streams share a hardware queue); rows >= K and then the count of
-                # valid rows are written by _stream_epochs while it runs
-                mh = self._mapped_stage(total + 1)
-                hm, hm_ptr, dm_ptr = mh
-                hm[:total] = host[:total]
-                hm[total] = 0  # the valid-row count (PersistArgs::ep_ready)
-                dptr = dm_ptr
-                pa.ep_ready, pa.ep_ready0 = dm_ptr + 4 * total, int(K)
-                stream_state = (K, n, E, P[-1].copy(), o_es, o_fl, hm, total)
+            native.check(self.lib.gadmm_memcpy_h2d_async(dptr, hptr, total * 4, self.stream.cuda_stream), "h2d")
             if fl.size:
                 pa.ep_flush = dptr + 4 * o_fl
             pa.n_epochs = len(starts)
@@ -796,9 +774,6 @@ class NativeChainEngine:
             if plan is not None:
                 rc = int(self.lib.gadmm_chain_blocked_launch(ctypes.byref(pa), self.stream.cuda_stream))
                 _timing.host_stamp("rp:launched")
-                if rc == 0 and feed is not None:
-                    self._stream_epochs(feed, int(feed_batch), *stream_state)
-                    _timing.host_stamp("rp:streamed")
                 if rc == -2 and epochs is None:  # its workgroups cannot all be resident: the per-worker kernel
                     plan, rc = None, None
                     self.last_kernel = "per-worker"
@@ -875,42 +850,6 @@ class NativeChainEngine:
             mon = ran * (len(slots) * 16 if self.rank != 0 else 8 * (self.nranks - 1))
         return EngineRun(conv, done, nxt - start_iter, 1, (t1 - t0) * 1e3, p2p, msgs, mon, 2 * p2p)
 
-    def _mapped_stage(self, count: int):
-        """(numpy int32 view, host ptr, device ptr) of a mapped coherent host buffer of >= ``count``
-        ints (gadmm_host_alloc), kept per engine."""
-        ms = getattr(self, "_mstage", None)
-        if ms is None or ms[0].size < count:
-            if ms is not None:
-                self.lib.gadmm_host_free(ms[1])
-            cap = max(count, 65536)
-            hp, dp = ctypes.c_void_p(), ctypes.c_void_p()
-            native.check(self.lib.gadmm_host_alloc(cap * 4, ctypes.byref(hp), ctypes.byref(dp)), "host_alloc")
-            arr = np.ctypeslib.as_array(ctypes.cast(hp, ctypes.POINTER(ctypes.c_int32)), shape=(cap,))
-            ms = (arr, hp.value, dp.value)
-            self._mstage = ms
-        return ms
-
-    def _stream_epochs(self, feed, batch: int, K: int, n: int, E: int, last: np.ndarray, o_es: int, o_fl: int,
-                       hm: np.ndarray, cnt_at: int):
-        """Streamed epochs (run_persistent ``feed``): draws epochs K..E-1 in batches while the kernel runs,
-        builds their slot / flush rows (a batch's first flush row needs the previous chain) into the
-        mapped host buffer the kernel reads, then raises the valid-row count (x86 stores stay in order)."""
-        rows, prev = K, last
-        while rows < E:
-            c = min(max(batch, 1), E - rows)
-            Pn = np.ascontiguousarray(np.vstack([prev[None, :], np.asarray(feed(c), dtype=np.int64)]))
-            es = np.empty(((c + 1) * n * 4,), dtype=np.int32)
-            pp = np.empty(((c + 1) * n,), dtype=np.int32)
-            fl = np.empty(((c + 1) * n * 2,), dtype=np.int32)
-            native.check(self.lib.gadmm_epoch_tables_blocked(Pn.ctypes.data, c + 1, n, es.ctypes.data, pp.ctypes.data,
-                                                             fl.ctypes.data), "epoch_tables_blocked")
-            a_es, a_fl = o_es + rows * n * 4, o_fl + rows * n * 2
-            hm[a_es:a_es + c * n * 4] = es[n * 4:]
-            hm[a_fl:a_fl + c * n * 2] = fl[n * 2:]
-            rows += c
-            hm[cnt_at] = rows
-            prev = Pn[-1]
-
     def traces(self, upto: int):
         """(objective trace, measured clock) of iterations 1..upto in ONE device-to-host copy."""
         if upto <= 0:
@@ -965,10 +904,6 @@ class NativeChainEngine:
         if getattr(self, "handle", None):
             self.lib.gadmm_chain_engine_destroy(self.handle)
             self.handle = None
-        ms = getattr(self, "_mstage", None)
-        if ms is not None:  # no kernel reads it any more: every launch ended in its stream's sync
-            self._mstage = None
-            self.lib.gadmm_host_free(ms[1])
 
     def __del__(self):  # pragma: no cover
         try:

@@ -112,7 +112,7 @@ class PersistArgs(ctypes.Structure):
         ("hard_stop", c_int), ("cont", c_int),
         ("xchk", c_void_p), ("xcd", c_int), ("pad_xcd", c_int),
         ("blk_dl", c_int), ("dl_halo", c_int), ("dl_tab", c_void_p * 2), ("minv_pad", c_void_p),
-        ("ep_flush", c_void_p), ("ep_ready", c_void_p), ("ep_ready0", c_int), ("pad_ep", c_int),
+        ("ep_flush", c_void_p),
     ]
 
 
@@ -209,8 +209,6 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_chain_blocked_pad_len": (c_long, [c_int]),
         "gadmm_chain_blocked_max_epochs": (c_int, []),
         "gadmm_memcpy_h2d_async": (c_int, [c_void_p, c_void_p, ctypes.c_size_t, c_void_p]),
-        "gadmm_host_alloc": (c_int, [ctypes.c_size_t, ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p)]),
-        "gadmm_host_free": (c_int, [c_void_p]),
         "gadmm_chain_blocked_tab_granules": (c_long, [c_int, c_int, c_int]),
         "gadmm_chain_blocked_tab_granules_dyn": (c_long, [c_int, c_int, c_int]),
         "gadmm_epoch_tables": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),

@@ -29,7 +29,7 @@ def test_abi_layout_matches_ctypes():
            ctypes.sizeof(native.RunStats), ctypes.sizeof(native.PersistArgs), native.PersistArgs.rho.offset,
            native.PersistArgs.ctl.offset, native.PhaseArgs.lgid.offset, native.EngineDesc.xport.offset,
            native.PersistArgs.xchk.offset, native.PersistArgs.dl_tab.offset, native.PersistArgs.minv_pad.offset,
-           native.PersistArgs.ep_flush.offset, native.PersistArgs.ep_ready.offset, native.PersistArgs.ep_ready0.offset]
+           native.PersistArgs.ep_flush.offset]
     assert got == exp
 
 
