@@ -98,6 +98,9 @@ class BlockedXgmiEngine:
             self._halo_on = ok_h
             if ok_h:
                 X_all, y_all = self._fetch_halo_shards(X_all, y_all, group)
+        # stop-decision lag in iterations (GADMM_DL_LAG: A/B of the objective -> monitor -> decision
+        # pipeline's slack; every rank must use the same value)
+        self.LAG = int(os.environ.get("GADMM_DL_LAG", str(self.LAG)))
         self.ring = self.LAG + 4
         torch.cuda.set_device(device)
         f64 = torch.float64
