@@ -150,37 +150,38 @@ __device__ __forceinline__ void blocked_objective(const PersistArgs& a, double* 
                                                   __amdgpu_buffer_rsrc_t rtab, bool local = false) {
   const int d = a.d, n = a.n;
   const long ring_base = 2L * n * 2 * d;  // theta ring [ring][n][d] after the exchange table
-  // DYN: this wave's epoch rows staged in LDS after the staging area (see DYN_LDS_BYTES)
+  // DYN (one GPU, li == worker id): the wave follows WORKER q instead of position q -- its Gram stays
+  // resident and a re-chain only changes which ring row carries theta_q (ep_pos [E][n], staged in LDS
+  // with the epoch starts), so no A / b / yy reload lands on the stop-rule pipeline at a re-chain
   const EpochLds el = epoch_lds(lds + MAXW * 64 + MAXW * QSTAGE, v);
-  if constexpr (DYN) stage_epochs(a, q, el, false);
-  PhaseSlot so = DYN ? a.ep_slots[q] : a.slots[q];
+  int* posl = reinterpret_cast<int*>(el.fl);  // [EPL] position of worker q per epoch (DYN)
+  if constexpr (DYN) {
+    for (int e = lane; e < a.n_epochs; e += 64) {
+      posl[e] = a.ep_pos[(long)e * n + q];
+      el.st[e] = a.epoch_start[e];
+    }
+  }
+  const PhaseSlot so = a.slots[DYN ? 0 : q];
+  const int li = DYN ? q : so.li, gid = DYN ? q : so.gid;
+  int row = DYN ? posl[0] : q;  // the ring row carrying this wave's theta
   const bool in = lane < d;
   double Aq[4][QT];
-  quad_load<QT>(Aq, a.A + (long)so.li * d * d, d, true);
-  double bo = in ? a.b[(long)so.li * d + lane] : 0.0;
-  double hy = 0.5 * a.yy[so.li];
+  quad_load<QT>(Aq, a.A + (long)li * d * d, d, true);
+  const double bo = in ? a.b[(long)li * d + lane] : 0.0;
+  const double hy = 0.5 * a.yy[li];
   double* xo = lds + v * QSTAGE;
   int ep = 0, next_start = (DYN && a.n_epochs > 1) ? el.st[1] : 0x7fffffff;
   for (int it = a.start_iter;; ++it) {
     if (a.hard_stop > 0 && it > a.hard_stop) return;  // D-GADMM chunk end: no theta^it comes
     if constexpr (DYN) {
-      if (it == next_start) {  // D-GADMM re-chain: another worker now sits at position q
+      if (it == next_start) {  // D-GADMM re-chain: worker q now sits at another position
         ++ep;
         next_start = ep + 1 < a.n_epochs ? el.st[ep + 1] : 0x7fffffff;
-        {
-          const int4 s4 = el.sl[ep];
-          so.li = s4.x;
-          so.gid = s4.y;
-        }
-        int od = d;  // laundered: the reload's bounds masks are not hoisted out of the loop (SGPRs)
-        asm volatile("" : "+s"(od));
-        quad_load<QT>(Aq, a.A + (long)so.li * od * od, od, true);
-        bo = in ? a.b[(long)so.li * d + lane] : 0.0;
-        hy = 0.5 * a.yy[so.li];
+        row = posl[ep];
       }
     }
     const unsigned tag = make_tag(a.epoch, it);
-    const long off = (ring_base + ((long)(it % a.ring) * n + q) * d + lane) * 16;
+    const long off = (ring_base + ((long)(it % a.ring) * n + row) * d + lane) * 16;
     double x = 0.0;
     for (int spin = 0;; ++spin) {
       const bool ok = !in || load_granule<SYS>(rtab, (int)off, tag, &x);
@@ -199,7 +200,7 @@ __device__ __forceinline__ void blocked_objective(const PersistArgs& a, double* 
     const double qv = quad_gemv<QT>(Aq, in ? x : 0.0, xo);  // (A th)_i in the order of every other engine
     const double part = in ? (0.5 * qv - bo) * x : 0.0;
     const double f = wave_sum_f64(part) + hy;
-    if (lane == 0) put_granule<SYS>(local, rob, ((it % a.ring) * n + so.gid) * 16, tag, f);
+    if (lane == 0) put_granule<SYS>(local, rob, ((it % a.ring) * n + gid) * 16, tag, f);
   }
 }
 

@@ -497,9 +497,9 @@ class NativeChainEngine:
         return 0 if int(self.lib.gadmm_chain_persistent_lds(self.d, 0)) > 0 else 1
 
     # coherence (iterations per epoch) from which the blocked kernel's dynamic mode is the default:
-    # per epoch it costs ~9.1 + 1.03 (c - 1) us against the per-worker kernel's ~4.8 + 2.03 (c - 1) us
-    # (profiles/r03_dgadmm_rechain), so they cross near c = 5
-    BLOCKED_DYN_MIN_COHERENCE = 5
+    # measured per solve (profiles/r03_dgadmm_rechain) 1.01 vs 1.47 ms at coherence 10, 0.96 vs 1.12 ms
+    # at 3, but 1.38 vs 1.16 ms at 1 (every iteration re-chains)
+    BLOCKED_DYN_MIN_COHERENCE = 3
 
     def dynamic_uses_blocked(self, fabric=None, coherence=None) -> bool:
         """Whether a one-launch D-GADMM run takes the blocked kernel's dynamic mode (one GPU, 12-wave
