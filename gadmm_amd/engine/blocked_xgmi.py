@@ -38,9 +38,25 @@ from ..parallel.topology import Placement
 from ..parallel.xgmi import _Buf, preflight
 
 
+MAXW = 12  # waves (computed positions) per workgroup of chain_blocked_kernel
+
+
+def halo_heads(lo: int, hi: int, n: int) -> list:
+    """The other ranks' boundary heads a rank owning chain positions [lo, hi] solves in the halo mode:
+    the neighbour of each boundary of its segment whose near side is a tail (odd position)."""
+    return ([lo - 1] if lo > 0 and lo % 2 == 1 else []) + ([hi + 1] if hi < n - 1 and hi % 2 == 1 else [])
+
+
+def dl_halo_eligible(segs, n: int, d: int) -> bool:
+    """Whether the data-local halo mode can run on every rank: more than one rank, every segment >= 2
+    positions, and segment + its halo heads within one 12-wave workgroup everywhere (24 workers: 4 and
+    8 ranks yes, 2 ranks no -- 13 waves)."""
+    return (len(segs) > 1 and d <= 52 and all(hi - lo + 1 >= 2 for lo, hi in segs)
+            and all(hi - lo + 1 + len(halo_heads(lo, hi, n)) <= MAXW for lo, hi in segs))
+
+
 class BlockedXgmiEngine:
     LAG = 8
-    MAXW = 12  # waves (computed positions) per workgroup of chain_blocked_kernel
 
     def __init__(self, X_all: torch.Tensor, y_all: torch.Tensor, n_total: int, placement: Placement, rank: int,
                  rho: float, obj0: float, tol: float, max_iter: int, device: torch.device, group=None,
@@ -85,13 +101,8 @@ class BlockedXgmiEngine:
         self.ext_lo, self.ext_hi = comp[rank]
         self.halo = []  # data-local halo mode: the other ranks' boundary heads this rank solves too
         if self.data_local:
-            # every segment >= 2 positions, and segment + its halo heads within one 12-wave workgroup on
-            # every rank (2 ranks x 12 workers do not fit: 13 waves)
-            def _span(lo, hi):
-                return hi - lo + 1 + int(lo > 0 and lo % 2 == 1) + int(hi < self.n - 1 and hi % 2 == 1)
-            ok_h = (dl_halo is not False and os.environ.get("GADMM_DL_HALO", "1") != "0" and self.d <= 52
-                    and self.L >= self.seg_hi - self.seg_lo + 1 and all(hi - lo + 1 >= 2 for lo, hi in segs)
-                    and all(_span(lo, hi) <= self.MAXW for lo, hi in segs) and len(segs) > 1)
+            ok_h = (dl_halo is not False and os.environ.get("GADMM_DL_HALO", "1") != "0"
+                    and self.L >= self.seg_hi - self.seg_lo + 1 and dl_halo_eligible(segs, self.n, self.d))
             if dl_halo and not ok_h:
                 raise ValueError("data-local halo mode needs segments of >= 2 positions that fit one workgroup "
                                  "with their halo heads")
@@ -218,14 +229,15 @@ class BlockedXgmiEngine:
         for o in allo:
             pool.update(o)
         Xs, ys = [X_own.cpu()], [y_own.cpu()]
-        if lo > 0 and lo % 2 == 1:  # seg_lo is a tail: solve the left rank's head lo - 1 too
-            Xs.insert(0, torch.from_numpy(pool[lo - 1][0]).unsqueeze(0))
-            ys.insert(0, torch.from_numpy(pool[lo - 1][1]).unsqueeze(0))
-            self.halo.append(lo - 1)
-        if hi < n - 1 and hi % 2 == 1:  # seg_hi is a tail: the right rank's head hi + 1
-            Xs.append(torch.from_numpy(pool[hi + 1][0]).unsqueeze(0))
-            ys.append(torch.from_numpy(pool[hi + 1][1]).unsqueeze(0))
-            self.halo.append(hi + 1)
+        for h in halo_heads(lo, hi, n):  # seg_lo / seg_hi is a tail: solve the neighbour rank's head too
+            X_h, y_h = torch.from_numpy(pool[h][0]).unsqueeze(0), torch.from_numpy(pool[h][1]).unsqueeze(0)
+            if h < lo:
+                Xs.insert(0, X_h)
+                ys.insert(0, y_h)
+            else:
+                Xs.append(X_h)
+                ys.append(y_h)
+            self.halo.append(h)
         self.ext_lo = lo - (1 if (lo - 1) in self.halo else 0)
         self.ext_hi = hi + (1 if (hi + 1) in self.halo else 0)
         return torch.cat(Xs).contiguous(), torch.cat(ys).contiguous()

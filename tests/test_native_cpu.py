@@ -204,3 +204,28 @@ def test_quad_pad_image_layout():
                         row, col = (lane & 15) + 16 * r, (lane >> 4) + 4 * t
                         want = float(M[b, row, col]) if row < d and col < d else 0.0
                         assert float(im[b, ((t >> 1) * 4 + r) * 128 + 2 * lane + (t & 1)]) == want
+
+
+def test_dl_halo_eligibility_and_heads():
+    """The data-local halo mode's plan (engine/blocked_xgmi.py): which boundary heads each rank solves
+    and when the mode fits the 12-wave workgroup on every rank (must agree with chain_blocked.hip's
+    range hl / hr and the launcher's span check)."""
+    from gadmm_amd.engine.blocked_xgmi import dl_halo_eligible, halo_heads
+
+    def segs(n, world):
+        return [(r * n // world, (r + 1) * n // world - 1) for r in range(world)]
+
+    assert not dl_halo_eligible(segs(24, 2), 24, 50)       # rank 0: 12 positions + head 12 = 13 waves
+    assert dl_halo_eligible(segs(24, 4), 24, 50)
+    assert dl_halo_eligible(segs(24, 8), 24, 50)
+    assert not dl_halo_eligible(segs(8, 8), 8, 50)         # one-position segments
+    assert not dl_halo_eligible(segs(24, 1), 24, 50)       # one rank: nothing to halo
+    assert not dl_halo_eligible(segs(24, 4), 24, 60)       # d > 52
+    assert halo_heads(0, 11, 24) == [12] and halo_heads(12, 23, 24) == []  # 2 ranks: 11 is the tail
+    assert halo_heads(3, 5, 24) == [2, 6]                  # 8 ranks, rank 1: both edges are tails
+    assert halo_heads(0, 2, 24) == [] and halo_heads(6, 8, 24) == []       # heads at the edges
+    # every boundary is halo'd by exactly one side
+    for world in (4, 8):
+        sg = segs(24, world)
+        got = sorted(h for lo, hi in sg for h in halo_heads(lo, hi, 24))
+        assert len(got) == world - 1 and len(set(got)) == world - 1
