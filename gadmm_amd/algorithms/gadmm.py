@@ -461,9 +461,8 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         which = np.searchsorted(starts, np.arange(1, iters + 1), side="right") - 1
         com_cost = np.cumsum(per_it[which])
         # leave the schedule (and the engine's plan) where the epoch-by-epoch run would have left them
-        schedule.skip(saved, Pn, Cn, int(np.sum(np.asarray(rechains) <= iters)))
-        eng.set_path([int(v) for v in P[int(np.searchsorted(starts, max(last_launched, 1), side="right") - 1)]],
-                     placement, rank)
+        schedule.skip(saved, Pn, Cn, int(np.searchsorted(rechains, iters, side="right")))  # rechains ascend
+        eng.set_path(P[int(np.searchsorted(starts, max(last_launched, 1), side="right") - 1)], placement, rank)
     else:
         # D-GADMM: run epoch by epoch; at a re-chain iteration flush the heads' pending duals with the
         # old chain, install the new chain, continue. Every rank draws the same chain sequence.

@@ -345,11 +345,16 @@ class NativeChainEngine:
         """Install the chain ``path`` (position -> global worker id) for this rank."""
         # validated plans are memoised per (chain, rank, placement): a D-GADMM solve installs the same
         # initial and final chains on every repeat, and building a plan in Python costs ~50 us
-        key = (tuple(int(w) for w in path), int(rank), tuple(int(o) for o in placement.owner))
+        pl = path.tolist() if isinstance(path, np.ndarray) else [int(w) for w in path]
+        ok = getattr(self, "_owner_memo", None)  # the placement's owner tuple, memoised per object
+        if ok is None or ok[0] is not placement:
+            ok = (placement, tuple(int(o) for o in placement.owner))
+            self._owner_memo = ok
+        key = (tuple(pl), int(rank), ok[1])
         memo = self.__dict__.setdefault("_plan_memo", {})
         plan = memo.get(key)
         if plan is None:
-            plan = chain_plan(path, placement, rank)
+            plan = chain_plan(pl, placement, rank)
             lidx = {w: i for i, w in enumerate(self.local_ids)}
             for s in plan.head + plan.tail:
                 if self.local_ids[s.li] != s.gid or lidx[s.gid] != s.li:
@@ -362,9 +367,9 @@ class NativeChainEngine:
         if plan is not getattr(self, "plan", None):
             self._plan_dirty = True
         self.plan = plan
-        self.path = [int(w) for w in path]
+        self.path = pl
         self.rank = rank
-        self._placement_owner = [int(o) for o in placement.owner]
+        self._placement_owner = list(ok[1])
 
     def _sync_plan(self):
         """Install self.plan into the native (graph / eager) engine if set_path changed it."""
