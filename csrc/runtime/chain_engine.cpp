@@ -223,6 +223,12 @@ int gadmm_memcpy_h2d_async(void* dst, const void* src, size_t bytes, hipStream_t
   return 0;
 }
 
+// Device -> host copy queued on `st` (a persistent solve's read-back block into its pinned buffer).
+int gadmm_memcpy_d2h_async(void* dst, const void* src, size_t bytes, hipStream_t st) {
+  GADMM_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+  return 0;
+}
+
 int gadmm_chain_engine_reset(void* h, int start_iter, int pending) {
   ChainEngine* e = (ChainEngine*)h;
   return gadmm_chain_reset(e->desc.base.ctl, start_iter, pending, e->desc.stream);

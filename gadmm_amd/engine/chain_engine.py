@@ -772,56 +772,57 @@ class NativeChainEngine:
                 pa.minv_pad = self._minv_pad.data_ptr()
         self.last_kernel = ("blocked%s(k=%d,L=%d,W=%d,pw=%d)" % ((("-dyn" if epochs is not None else ""),) + tuple(plan))
                             if plan is not None else "per-worker")
-        with torch.cuda.stream(self.stream):
-            t0 = _time.perf_counter()
-            rc = None
-            _timing.host_stamp("rp:prelaunch")
-            if plan is not None:
-                rc = int(self.lib.gadmm_chain_blocked_launch(ctypes.byref(pa), self.stream.cuda_stream))
-                _timing.host_stamp("rp:launched")
-                if rc == -2 and epochs is None:  # its workgroups cannot all be resident: the per-worker kernel
-                    plan, rc = None, None
-                    self.last_kernel = "per-worker"
-                else:
-                    native.check(rc, "chain_blocked_launch")
-            if plan is None and self.model == "logistic":
-                if epochs is not None:
-                    raise RuntimeError("persistent logistic kernel: static chains only")
-                self._logi = self._logi_args()
-                if self.local_solver == "newton":
-                    self.last_kernel = "per-worker-newton"
-                    launch = self.lib.gadmm_chain_persistent_newton_launch
-                else:
-                    self.last_kernel = "per-worker-logistic"
-                    launch = self.lib.gadmm_chain_persistent_logistic_launch
-                rc = int(launch(ctypes.byref(pa), ctypes.byref(self._logi), self.stream.cuda_stream))
-                if rc == -2:
-                    raise ResidencyError(self.lib.gadmm_last_error().decode())
-                native.check(rc, "chain_persistent_logistic_launch")
-            elif plan is None:
-                rc = int(self.lib.gadmm_chain_persistent_launch(ctypes.byref(pa), self.stream.cuda_stream))
-                if rc == -2:
-                    raise ResidencyError(self.lib.gadmm_last_error().decode())
-                native.check(rc, "chain_persistent_launch")
-            # the control block comes back with the same stream sync (pinned buffer, async copy queued
-            # behind the kernel): no second blocking round trip per solve
-            # the objective trace and the clock come back behind the same sync as the control block, in
-            # one copy of the read-back block (short traces: traces() then reads the pinned copy instead of
-            # a second blocking device round trip); without them, only the control block's words
-            nt = self.trace.numel()
-            fetch = fetch_trace and nt <= 16384
-            if getattr(self, "_rb_host", None) is None:
-                self._rb_host = torch.empty(self._rb.shape, dtype=torch.float64, pin_memory=True)
-                self._ctl_host = self._rb_host[0:4].view(torch.int32)
-            if fetch:
-                self._rb_host.copy_(self._rb, non_blocking=True)
+        # launches name the engine stream explicitly
+        t0 = _time.perf_counter()
+        rc = None
+        _timing.host_stamp("rp:prelaunch")
+        if plan is not None:
+            rc = int(self.lib.gadmm_chain_blocked_launch(ctypes.byref(pa), self.stream.cuda_stream))
+            _timing.host_stamp("rp:launched")
+            if rc == -2 and epochs is None:  # its workgroups cannot all be resident: the per-worker kernel
+                plan, rc = None, None
+                self.last_kernel = "per-worker"
             else:
-                self._rb_host[0:4].copy_(self._rb[0:4], non_blocking=True)
-            _timing.host_stamp("rp:copies_queued")
-            self.stream.synchronize()
-            _timing.host_stamp("rp:synced")
-            self._tr_valid = fetch
-            t1 = _time.perf_counter()
+                native.check(rc, "chain_blocked_launch")
+        if plan is None and self.model == "logistic":
+            if epochs is not None:
+                raise RuntimeError("persistent logistic kernel: static chains only")
+            self._logi = self._logi_args()
+            if self.local_solver == "newton":
+                self.last_kernel = "per-worker-newton"
+                launch = self.lib.gadmm_chain_persistent_newton_launch
+            else:
+                self.last_kernel = "per-worker-logistic"
+                launch = self.lib.gadmm_chain_persistent_logistic_launch
+            rc = int(launch(ctypes.byref(pa), ctypes.byref(self._logi), self.stream.cuda_stream))
+            if rc == -2:
+                raise ResidencyError(self.lib.gadmm_last_error().decode())
+            native.check(rc, "chain_persistent_logistic_launch")
+        elif plan is None:
+            rc = int(self.lib.gadmm_chain_persistent_launch(ctypes.byref(pa), self.stream.cuda_stream))
+            if rc == -2:
+                raise ResidencyError(self.lib.gadmm_last_error().decode())
+            native.check(rc, "chain_persistent_launch")
+        # the control block comes back with the same stream sync (pinned buffer, async copy queued
+        # behind the kernel): no second blocking round trip per solve
+        # the objective trace and the clock come back behind the same sync as the control block, in
+        # one copy of the read-back block (short traces: traces() then reads the pinned copy instead of
+        # a second blocking device round trip); without them, only the control block's words
+        nt = self.trace.numel()
+        fetch = fetch_trace and nt <= 16384
+        if getattr(self, "_rb_host", None) is None:
+            self._rb_host = torch.empty(self._rb.shape, dtype=torch.float64, pin_memory=True)
+            self._ctl_host = self._rb_host[0:4].view(torch.int32)
+        # native async copy on the engine stream (every launch above names that stream explicitly, so no
+        # torch stream context is needed around this block)
+        nb = self._rb.numel() * 8 if fetch else 32  # all of it, or the control block (8 x i32)
+        native.check(self.lib.gadmm_memcpy_d2h_async(self._rb_host.data_ptr(), self._rb.data_ptr(), nb,
+                                                     self.stream.cuda_stream), "d2h")
+        _timing.host_stamp("rp:copies_queued")
+        self.stream.synchronize()
+        _timing.host_stamp("rp:synced")
+        self._tr_valid = fetch
+        t1 = _time.perf_counter()
         self.last_timeline = tl.cpu().numpy() if tl is not None else None
         self.last_timeline_slots = [(s.gid, p) for s, p in zip(slots, pos)] if tl is not None else None
         c = self._ctl_host.tolist()

@@ -209,6 +209,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_chain_blocked_pad_len": (c_long, [c_int]),
         "gadmm_chain_blocked_max_epochs": (c_int, []),
         "gadmm_memcpy_h2d_async": (c_int, [c_void_p, c_void_p, ctypes.c_size_t, c_void_p]),
+        "gadmm_memcpy_d2h_async": (c_int, [c_void_p, c_void_p, ctypes.c_size_t, c_void_p]),
         "gadmm_chain_blocked_tab_granules": (c_long, [c_int, c_int, c_int]),
         "gadmm_chain_blocked_tab_granules_dyn": (c_long, [c_int, c_int, c_int]),
         "gadmm_epoch_tables": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
