@@ -74,10 +74,11 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--engine", choices=["auto", "persistent", "blocked-dl", "per-worker", "graph", "replicated-halo"],
                     default="auto",
-                    help="auto: persistent single-launch kernel when eligible (N GPUs: the data-local blocked "
-                         "kernel, then the per-worker kernel), else graph-replayed phases; blocked-dl / "
-                         "per-worker: only that persistent kernel; replicated-halo: opt-in blocked kernel "
-                         "across GPUs (ranks hold halo shards)")
+                    help="auto: one GPU = the persistent single-launch kernel; N GPUs = an engine tournament in "
+                         "the untimed warm-up (data-local blocked with / without its halo mode, per-worker, "
+                         "replicated-halo: each timed, the fastest agreed by all ranks), the graph engine if "
+                         "none runs; blocked-dl / per-worker: only that persistent kernel; replicated-halo: "
+                         "opt-in blocked kernel across GPUs (ranks hold halo shards)")
     ap.add_argument("--fabric", choices=["auto", "xgmi", "rccl", "ipc"], default="auto",
                     help="multi-GPU transport: xgmi = device-initiated theta pushes between persistent kernels, "
                          "rccl = RCCL send/recv between graph-replayed phases, ipc = the device-copy transport "
@@ -90,6 +91,8 @@ def main():
                     help="dgadmm: iterations between re-chains (1 = BASELINE configs[3]'s 're-chaining each round')")
     ap.add_argument("--rows", type=int, default=1_250_000, help="real10m: rows per GPU")
     ap.add_argument("--dim", type=int, default=10_000, help="real10m: features")
+    ap.add_argument("--timeout", type=float, default=20.0,
+                    help="multi-GPU hand-off deadline in seconds (a stalled peer ends a solve with done=4)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -123,6 +126,32 @@ def main():
         dist.destroy_process_group()
 
 
+def _headline_candidates(args, X_cpu, y_cpu, local, placement, rank, world, device, share, obj0, timeout_s):
+    """(name, factory) of every multi-GPU engine the tournament times, in preference order."""
+    from gadmm_amd.engine.multigpu import DistributedChainSolver
+
+    def make(engine, **kw):
+        def factory():
+            return DistributedChainSolver(X_cpu.to(device).contiguous(), y_cpu.to(device).contiguous(), local,
+                                          args.workers, placement, rank, world, device, args.rho, obj0, args.tol,
+                                          engine=engine, fabric=args.fabric, share=share, block=args.block,
+                                          use_graph=not args.no_graph, timeout_s=timeout_s, strict=True, **kw)
+        return factory
+
+    def replicated():
+        from gadmm_amd.data import linear_synthetic
+        ds_all = linear_synthetic(args.workers)  # the halo engine holds other ranks' shards (reported)
+        return make("replicated-halo", halo_data=(ds_all.X, ds_all.y))()
+
+    cands = []
+    if args.fabric in ("auto", "xgmi"):
+        cands += [("blocked-dl-halo", make("blocked-dl", dl_halo=True)),
+                  ("blocked-dl", make("blocked-dl", dl_halo=False)),
+                  ("per-worker", make("per-worker")),
+                  ("replicated-halo", replicated)]
+    return cands
+
+
 def run_headline(args, rank, world, device, share):
     from gadmm_amd.benchmarks import headline_rank_problem, EXPECTED_ITERS_1E8
     from gadmm_amd.engine.multigpu import DistributedChainSolver, all_ok
@@ -130,37 +159,68 @@ def run_headline(args, rank, world, device, share):
 
     X_cpu, y_cpu, local, placement, obj0 = headline_rank_problem(args.workers, rank, world)
     d, m = int(X_cpu.shape[2]), int(X_cpu.shape[1])
-    halo = None
-    if args.engine == "replicated-halo" and world > 1:
-        from gadmm_amd.data import linear_synthetic
-        ds_all = linear_synthetic(args.workers)  # opt-in: the halo engine needs other ranks' shards
-        halo = (ds_all.X, ds_all.y)
-    sol = DistributedChainSolver(X_cpu.to(device).contiguous(), y_cpu.to(device).contiguous(), local, args.workers,
-                                 placement, rank, world, device, args.rho, obj0, args.tol, engine=args.engine,
-                                 fabric=args.fabric, share=share, block=args.block, halo_data=halo,
-                                 use_graph=not args.no_graph)
     expect = EXPECTED_ITERS_1E8.get((args.workers, float(args.rho))) if args.tol == 1e-8 else None
-    for _ in range(args.warmup):
-        if sol.solve_agreed().done != 1:  # collective: a failure anywhere moves every rank to the graph engine
-            raise BenchFailure("a warm-up solve did not converge (fabric %s, fallbacks %s)" % (sol.kind, sol.fallbacks))
-    torch.cuda.synchronize(device)
+    timeout_s = float(args.timeout)
+    hop = None
     if world > 1:
-        dist.barrier()
-    results, stamps = [], []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        results.append(sol.guarded_solve())
-        stamps.append(time.perf_counter())  # every solve ends in its own stream sync (per-step record)
-    torch.cuda.synchronize(device)
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    # every timed solve must have converged in the same (reference) iteration count
-    its = {r.iters for r in results}
-    good = all(r.done == 1 for r in results) and len(its) == 1 and (expect is None or its == {expect})
-    if not all_ok(good, world):
-        raise BenchFailure("timed solves: done=%s iterations=%s (expected %s)"
-                           % (sorted({r.done for r in results}), sorted(its), expect))
+        # one-way hop latency of every chain boundary (the quantity that decides the engine ranking)
+        from gadmm_amd.parallel.hop_probe import hop_probe
+        hop = hop_probe(rank, world, device)
+    sol, tournament = None, None
+    if world > 1 and args.engine == "auto":
+        # untimed: build and time every eligible multi-GPU engine, agree on the fastest (max over ranks)
+        from gadmm_amd.engine.tournament import engine_tournament
+        cands = _headline_candidates(args, X_cpu, y_cpu, local, placement, rank, world, device, share, obj0,
+                                     timeout_s)
+        log = (lambda msg: print("bench.py: " + msg, file=sys.stderr, flush=True)) if rank == 0 else None
+        name, sol, tournament = engine_tournament(cands, world, solves=3, warm=1, expect=expect,
+                                                  sync=lambda: torch.cuda.synchronize(device), log=log)
+    if sol is None:
+        halo = None
+        if args.engine == "replicated-halo" and world > 1:
+            from gadmm_amd.data import linear_synthetic
+            ds_all = linear_synthetic(args.workers)  # opt-in: the halo engine needs other ranks' shards
+            halo = (ds_all.X, ds_all.y)
+        eng = "graph" if (tournament is not None) else args.engine  # nothing won: the graph engine
+        sol = DistributedChainSolver(X_cpu.to(device).contiguous(), y_cpu.to(device).contiguous(), local,
+                                     args.workers, placement, rank, world, device, args.rho, obj0, args.tol,
+                                     engine=eng, fabric=args.fabric, share=share, block=args.block,
+                                     halo_data=halo, use_graph=not args.no_graph, timeout_s=timeout_s)
+    stall = os.environ.get("GADMM_BENCH_STALL", "")  # test hook "step:rank": that rank stalls before that step
+    stall_step, stall_rank = (int(v) for v in stall.split(":")) if stall else (-1, -1)
+    restarts = 0
+    while True:
+        for _ in range(args.warmup):
+            if sol.solve_agreed().done != 1:  # collective: a failure anywhere moves every rank to the graph engine
+                raise BenchFailure("a warm-up solve did not converge (fabric %s, fallbacks %s)"
+                                   % (sol.kind, sol.fallbacks))
+        torch.cuda.synchronize(device)
+        if world > 1:
+            dist.barrier()
+        results, stamps = [], []
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            if k == stall_step and rank == stall_rank and restarts == 0:
+                sol.delay_next_s = 3.0 * timeout_s
+            results.append(sol.guarded_solve())
+            stamps.append(time.perf_counter())  # every solve ends in its own stream sync (per-step record)
+        torch.cuda.synchronize(device)
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        # every timed solve must have converged in the same (reference) iteration count
+        its = {r.iters for r in results}
+        good = all(r.done == 1 for r in results) and len(its) == 1 and (expect is None or its == {expect})
+        if all_ok(good, world):
+            break
+        # collective fallback: every rank leaves the persistent engine for the graph engine together and
+        # the timing restarts there (warm-up + K steps); the JSON line names the fallback
+        if world == 1 or not sol.persistent or restarts >= 1:
+            raise BenchFailure("timed solves: done=%s iterations=%s (expected %s)"
+                               % (sorted({r.done for r in results}), sorted(its), expect))
+        sol.fall_back("timed solve failed on some rank (done=%s here); timing restarted"
+                      % sorted({r.done for r in results}))
+        restarts += 1
     ms = (t1 - t0) * 1e3 / max(args.steps, 1)
     last = results[-1]
     iters, p2p, wire, mon, repl = last.iters, last.theta_bytes, last.wire_bytes, last.monitor_bytes, sol.replicated_bytes
@@ -218,8 +278,15 @@ def run_headline(args, rank, world, device, share):
             "kernel": sol.kernel,
             "fabric": sol.kind,
             "fallbacks": sol.fallbacks,
+            "timing_restarts": restarts,
+            "setup_in_timed_region": True,  # every step: Gram + b + y'y (f64 MFMA), inverses, iterations
             "baseline_s": BASELINE_S,
         }
+        if hop is not None:
+            out["xgmi_hop_us"] = hop.get("hop_us")  # one-way, per chain boundary (rank r -> r + 1)
+            out["hop_probe_same_device"] = hop.get("same_device")  # ranks sharing one GPU (rehearsal)
+        if tournament is not None:
+            out["engine_tournament"] = tournament  # every candidate's untimed-warm-up time (max over ranks)
         print(json.dumps(out), flush=True)
     sol.close()
 
@@ -286,7 +353,7 @@ def run_other(args, rank, world, device, share):
     comm = None
     args.share = share
     if world > 1:
-        if share:
+        if share or args.fabric == "ipc":
             comm = None  # RCCL cannot run with ranks on one GPU: the bodies build an IPC transport
         else:
             from gadmm_amd.parallel.comm import RcclComm

@@ -295,6 +295,10 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   // Next best: an idle wave (u >= nv: no position). A computed tail can never be it (it is busy in
   // exactly the phase the poll runs in) -- a workgroup whose only position is a tail (one worker per
   // rank, odd position) polls on an idle wave.
+  // Invariant: every wave of the workgroup, inactive ones included, executes the same sequence of
+  // lds_barrier()s (exchange, re-chain, stop) -- the decision wave may be an idle one, which is only
+  // correct because idle waves follow the active waves' schedule exactly (DYN: from the same staged
+  // epoch starts, see stage_epochs below).
   int vdec = -1;
   for (int u = 0; u < nv && vdec < 0; ++u)
     if (((ra + u) % 2) == 0 && (ra + u < s0 || ra + u > e0)) vdec = u;
@@ -337,7 +341,10 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   // DYN: this wave's epoch rows in LDS (after thS and the staging area; see DYN_LDS_BYTES)
   const EpochLds el = epoch_lds(lds + MAXW * 64 + MAXW * QSTAGE, v);
   if constexpr (DYN) {
-    if (active) stage_epochs(a, p, el, true);
+    // EVERY wave stages the epoch starts: inactive waves (u >= nv, e.g. an idle decision wave) run the
+    // same per-iteration barrier schedule, re-chain barrier included, off `next_start`, so they must
+    // read the same starts as the active ones; their slot rows (position 0) go unused
+    stage_epochs(a, active ? p : 0, el, active);
   }
   // Positions that ever solve: in a block, phase phi solves the owned range widened by 2k - 1 - phi,
   // so heads up to 2k - 1 and tails up to 2k - 2 positions away from it; the outermost halo only

@@ -10,6 +10,9 @@
 // Every rank owns one fine-grained (uncached) mailbox, exported by IPC (parallel/ipc.py):
 //   theta area  [R][n_total][d]   16-B granules; slot = code % R, code = 4 * iteration + phase
 //   obj area    [2][n_total][ring] 16-B granules; parity = all-gather sequence & 1
+//   coll area   [COLL_SLOTS][nranks][2 d + 8] 16-B granules: the device collectives of the large-d
+//               star ADMM (reduce to the hub rank, broadcast from it, all-reduce of the objective,
+//               standared_ADMM.m:66-71,86), slot = host sequence % COLL_SLOTS, row = source rank
 // A send op stores its row straight into the peer's mailbox as {tag, lo, tag, hi} write-through
 // granules (the data-is-flag form of chain_persistent.hip; a torn store is caught by the tags); the
 // receiving rank's recv op re-reads its own mailbox row until every granule carries the expected
@@ -35,13 +38,18 @@ struct XchgBatch {
   XchgOp op[MAX_BATCH];
 };
 
+constexpr int COLL_SLOTS = 8;
+
+__host__ __device__ inline long coll_cmax(int d) { return 2L * d + 8; }
+
 struct IpcXport {
   int rank, nranks, d, n_total, ring, R;
+  long coll_base;           // granule index of the coll area
   u32x4* box;               // this rank's mailbox
   u32x4** d_boxes;          // device [nranks]: every rank's mailbox (own included), IPC-mapped
   unsigned* d_word;         // device [4]: [0] solve epoch, [1] all-gather sequence
   long long timeout_ticks;  // s_memrealtime ticks (100 MHz)
-  long long payload_bytes = 0, wire_bytes = 0, msgs = 0, obj_bytes = 0;
+  long long payload_bytes = 0, wire_bytes = 0, msgs = 0, obj_bytes = 0, coll_payload = 0, coll_wire = 0;
 };
 
 __device__ __forceinline__ void give_up(ChainCtl* ctl) {
@@ -127,6 +135,89 @@ __global__ void __launch_bounds__(256) ipc_allgather_kernel(const double* part, 
   }
 }
 
+// Device collectives (one kernel per collective, thread i owns element i; order-deterministic sums):
+//   kind 0 reduce:    non-root ranks push src into the root's coll row [me]; the root sums every
+//                     rank's row in RANK ORDER (its own from src) into dst
+//   kind 1 broadcast: the root pushes src into every other rank's row [root]; they copy it into dst
+//   kind 2 allreduce: every rank pushes src into every other rank's row [me]; every rank sums all
+//                     rows in rank order -> the same bits on every rank (the stop rule agrees)
+// Overwrite safety: the star iteration ends in an all-reduce, so no rank is more than 3
+// collectives ahead of another; COLL_SLOTS = 8. `done` (decided from the all-reduced objective, the
+// same on every rank) skips the collective on every rank alike; a peer that never arrives sets
+// done = 4 on the waiting rank at the deadline.
+__global__ void __launch_bounds__(256) ipc_coll_kernel(int kind, int root, const double* src, double* dst, int count,
+                                                       int me, int nranks, long slot_base, long cmax,
+                                                       u32x4* const* boxes, u32x4* my_box, const unsigned* word,
+                                                       unsigned seq, ChainCtl* ctl, long long timeout_ticks) {
+  if (ctl->done) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  const unsigned tag = make_tag(word[0], (int)(0x80000u | (seq & 0x7ffffu)));
+  const double v = src[i];
+  const bool pushes = kind == 2 || (kind == 0 && me != root) || (kind == 1 && me == root);
+  if (pushes) {
+    for (int r = 0; r < nranks; ++r) {
+      if (r == me || (kind == 0 && r != root)) continue;
+      store_granule<true>(rsrc_of(boxes[r] + slot_base + (long)me * cmax), i * 16, tag, v);
+    }
+  }
+  const bool reads = kind == 2 || (kind == 0 && me == root) || (kind == 1 && me != root);
+  if (!reads) return;
+  const unsigned long long deadline = now_ticks() + (unsigned long long)timeout_ticks;
+  double acc = 0.0;
+  for (int r = 0; r < nranks; ++r) {
+    if (kind == 1 && r != root) continue;
+    double x = v;
+    if (r != me) {
+      const __amdgpu_buffer_rsrc_t rs = rsrc_of(my_box + slot_base + (long)r * cmax);
+      for (int spin = 0;; ++spin) {
+        if (load_granule<true>(rs, i * 16, tag, &x)) break;
+        if ((spin & 7) == 7 && now_ticks() > deadline) {
+          give_up(ctl);
+          return;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    acc = (kind == 1) ? x : (r == 0 ? x : acc + x);
+  }
+  dst[i] = acc;
+}
+
+// One-way hop probe between two ranks (bench.py: ``xgmi_hop_us`` per chain boundary): one wave on each
+// side ping-pongs a 64-granule row (the theta-row format of the persistent kernels, system-scope
+// write-through stores into the peer's mailbox, polls of the own one) `n` times; the initiator times
+// the round trips with s_memrealtime (after one untimed round that absorbs the launch skew).
+// out[0] = ticks for n round trips (0: timed out), out[1] = XCC.
+__global__ void __launch_bounds__(64) ipc_hop_probe_kernel(u32x4* mine, u32x4* peer, int initiator, int n,
+                                                           unsigned salt, long long timeout_ticks,
+                                                           unsigned long long* out) {
+  const int lane = threadIdx.x;
+  const __amdgpu_buffer_rsrc_t rs_peer = rsrc_of(peer), rs_mine = rsrc_of(mine);
+  const unsigned long long deadline = now_ticks() + (unsigned long long)timeout_ticks;
+  unsigned long long t0 = 0;
+  bool good = true;
+  for (int i = 1; i <= n + 1 && good; ++i) {
+    if (i == 2) t0 = now_ticks();  // round 1 absorbs the two launches' skew: n timed round trips after it
+    const unsigned tag = make_tag(salt, i);
+    if (initiator) store_granule<true>(rs_peer, lane * 16, tag, (double)i);
+    double v = 0.0;
+    for (int spin = 0;; ++spin) {
+      if (__all(load_granule<true>(rs_mine, lane * 16, tag, &v))) break;
+      if ((spin & 63) == 63 && now_ticks() > deadline) {
+        good = false;
+        break;
+      }
+    }
+    if (!initiator && good) store_granule<true>(rs_peer, lane * 16, tag, (double)i);
+  }
+  const unsigned long long t1 = now_ticks();
+  if (lane == 0) {
+    out[0] = good ? t1 - t0 : 0ull;
+    out[1] = xcc_id();
+  }
+}
+
 // A new epoch restarts the all-gather sequence too: a rank that returned early (ctl->done) and one
 // whose all-gather timed out have advanced word[1] differently, and the parity / tag derived from
 // it must agree across ranks for every later solve on this transport. The epoch salts the tags, so
@@ -142,9 +233,9 @@ __global__ void ipc_new_epoch_kernel(unsigned* word) {
 
 extern "C" {
 
-long gadmm_ipc_box_bytes(int n_total, int d, int ring) {
+long gadmm_ipc_box_bytes(int n_total, int d, int ring, int nranks) {
   const long R = 8L * ring + 8;
-  return (R * n_total * d + 2L * n_total * ring) * 16;
+  return (R * n_total * d + 2L * n_total * ring + (long)COLL_SLOTS * nranks * coll_cmax(d)) * 16;
 }
 
 void* gadmm_ipc_xport_create(int rank, int nranks, int d, int n_total, int ring, void* my_box,
@@ -160,6 +251,7 @@ void* gadmm_ipc_xport_create(int rank, int nranks, int d, int n_total, int ring,
   x->n_total = n_total;
   x->ring = ring;
   x->R = 8 * ring + 8;
+  x->coll_base = (long)x->R * n_total * d + 2L * n_total * ring;
   x->box = (u32x4*)my_box;
   x->timeout_ticks = (long long)(timeout_s * 1e8);
   if (hipMalloc((void**)&x->d_boxes, sizeof(void*) * nranks) != hipSuccess ||
@@ -243,6 +335,60 @@ int gadmm_ipc_allgather(void* h, const double* part, double* reduced, int ring, 
   hipLaunchKernelGGL(ipc_allgather_kernel, dim3(1), dim3(256), 0, st, part, reduced, ring, x->n_total, lgid, n_local,
                      x->nranks, obj_base, x->d_boxes, x->box, x->d_word, ctl, x->timeout_ticks);
   GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+// One device collective on `st` (kind 0 reduce to root / 1 broadcast from root / 2 all-reduce, all
+// sums in rank order), `seq` = the caller's collective counter (every rank calls the same sequence
+// after the same gadmm_ipc_new_epoch). In place (src == dst) is allowed: a thread reads its element
+// before it writes it.
+int gadmm_ipc_collective(void* h, int kind, int root, const double* src, double* dst, int count, unsigned seq,
+                         ChainCtl* ctl, hipStream_t st) {
+  IpcXport* x = (IpcXport*)h;
+  if (!x || kind < 0 || kind > 2 || root < 0 || root >= x->nranks || count < 1 || count > coll_cmax(x->d) ||
+      !src || !dst || !ctl) {
+    gadmm_set_error("ipc_collective: bad arguments (kind %d, root %d, count %d)", kind, root, count);
+    return -1;
+  }
+  const long cmax = coll_cmax(x->d);
+  const long slot_base = x->coll_base + (long)(seq % COLL_SLOTS) * x->nranks * cmax;
+  const int R = x->nranks, me = x->rank;
+  const long long sent = kind == 2 ? (long long)(R - 1) : kind == 0 ? (me != root ? 1 : 0) : (me == root ? R - 1 : 0);
+  x->coll_payload += sent * count * 8;
+  x->coll_wire += sent * count * 16;
+  hipLaunchKernelGGL(ipc_coll_kernel, dim3((count + 255) / 256), dim3(256), 0, st, kind, root, src, dst, count, me, R,
+                     slot_base, cmax, x->d_boxes, x->box, x->d_word, seq, ctl, x->timeout_ticks);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+// out2: collective payload bytes this rank sent (8 B per double), collective wire bytes (16-B granules).
+int gadmm_ipc_coll_counters(void* h, long long* out2) {
+  IpcXport* x = (IpcXport*)h;
+  out2[0] = x->coll_payload;
+  out2[1] = x->coll_wire;
+  return 0;
+}
+
+// Hop probe (see ipc_hop_probe_kernel): `mine` / `peer` are 64-granule rows in IPC-mapped fine-grained
+// memory (the caller's own and the peer rank's), both sides launch together. Synchronous. Returns the
+// median-free raw measurement: out2[0] = ticks (100 MHz) for n round trips, 0 on a timeout.
+int gadmm_ipc_hop_probe(void* mine, void* peer, int initiator, int n, unsigned salt, double timeout_s,
+                        unsigned long long* out2) {
+  if (!mine || !peer || n < 1 || !out2) {
+    gadmm_set_error("ipc_hop_probe: bad arguments");
+    return -1;
+  }
+  unsigned long long* d_out = nullptr;
+  GADMM_CHECK(hipMalloc((void**)&d_out, 2 * sizeof(unsigned long long)));
+  GADMM_CHECK(hipMemset(d_out, 0, 2 * sizeof(unsigned long long)));
+  hipLaunchKernelGGL(ipc_hop_probe_kernel, dim3(1), dim3(64), 0, 0, (u32x4*)mine, (u32x4*)peer, initiator, n,
+                     salt & 0xfffu, (long long)(timeout_s * 1e8), d_out);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpy(out2, d_out, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+  hipFree(d_out);
+  GADMM_CHECK(e);
   return 0;
 }
 

@@ -15,7 +15,9 @@
 //   sb_gemv   th_hub = (A_h + (N-1) rho I)^{-1} r_h   (hub rank)
 //   -- broadcast(th_hub) from the hub rank (RCCL ncclBroadcast)
 //   sb_post   lam_i += rho (th_i - th_hub), f_i(th_i), f_h(th_hub)                        (:84-88)
-//   -- allreduce(local objective) (RCCL; nothing on one rank)
+//   -- allreduce(objp) (RCCL or the IPC device collective; nothing on one rank): objp holds one
+//      slot per GLOBAL worker, non-zero only on its owner, so the sum is exact and sb_finish adds
+//      the N objectives in worker order -- the same bits as one rank, on every rank
 //   sb_finish trace[it] = obj, |obj - obj0| < tol -> done                                  (:95-107)
 // Objective: identity mode f = (1/2 (r - c rho th) - b)^T th + 1/2 y^T y, from (A + c rho I) th = r
 // (no extra pass over the inverse); exact mode (obj_mode 0) adds one GEMV with A per worker.
@@ -39,10 +41,11 @@ struct StarBigArgs {
   double* agg;         // [2 d] reduce buffer
   double* rbuf;        // [n_local][rstride(d)] right-hand sides + objective partials
   double* objw;        // [n_local] per-worker objective
-  double* objp;        // [1] this rank's objective (allreduce buffer)
+  double* objp;        // [n_total] per-worker objectives, this rank's slots only (allreduce buffer)
   double* trace;       // [max_iter]
   ChainCtl* ctl;       // iter (next iteration), done, conv_iter
   long long* tstamp;   // [max_iter] s_memrealtime (100 MHz) when each iteration's stop rule ran
+  const int* gid;      // [n_local] global worker id of each local worker
 };
 
 namespace {
@@ -156,10 +159,10 @@ __global__ void __launch_bounds__(1024) sb_post(StarBigArgs a) {
 }
 
 __global__ void sb_local_obj(StarBigArgs a) {
-  if (a.ctl->done || threadIdx.x != 0) return;
-  double f = 0.0;
-  for (int s = 0; s < a.n_local; ++s) f += a.objw[s];  // worker order
-  a.objp[0] = f;
+  if (a.ctl->done) return;
+  for (int g = threadIdx.x; g < a.n_total; g += blockDim.x) a.objp[g] = 0.0;
+  __syncthreads();
+  for (int s = threadIdx.x; s < a.n_local; s += blockDim.x) a.objp[a.gid[s]] = a.objw[s];
 }
 
 __global__ void sb_finish(StarBigArgs a) {
@@ -167,7 +170,8 @@ __global__ void sb_finish(StarBigArgs a) {
   ChainCtl* ctl = a.ctl;
   if (ctl->done) return;
   const int it = ctl->iter;
-  const double obj = a.objp[0];
+  double obj = 0.0;
+  for (int g = 0; g < a.n_total; ++g) obj += a.objp[g];  // worker order
   if (it - 1 < a.max_iter) {
     a.trace[it - 1] = obj;
     a.tstamp[it - 1] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -190,7 +194,7 @@ extern "C" {
 int gadmm_star_big_abi_layout(long long* out, int n) {
   long long v[] = {(long long)sizeof(StarBigArgs), (long long)offsetof(StarBigArgs, rho),
                    (long long)offsetof(StarBigArgs, Minv), (long long)offsetof(StarBigArgs, ctl),
-                   (long long)offsetof(StarBigArgs, tstamp)};
+                   (long long)offsetof(StarBigArgs, tstamp), (long long)offsetof(StarBigArgs, gid)};
   const int k = (int)(sizeof(v) / sizeof(v[0]));
   for (int i = 0; i < n && i < k; ++i) out[i] = v[i];
   return k;
@@ -200,7 +204,7 @@ long gadmm_star_big_rstride(int d) { return rstride(d); }
 
 static bool sb_ok(const StarBigArgs& a) {
   return a.d >= 1 && a.n_local >= 1 && a.n_total >= a.n_local && a.hub_li < a.n_local && a.Minv && a.b && a.yy &&
-         a.theta && a.lam && a.th_hub && a.agg && a.rbuf && a.objw && a.objp && a.trace && a.ctl && a.tstamp &&
+         a.theta && a.lam && a.th_hub && a.agg && a.rbuf && a.objw && a.objp && a.trace && a.ctl && a.tstamp && a.gid &&
          (a.obj_mode != 0 || a.A) && a.max_iter >= 1;
 }
 

@@ -105,23 +105,22 @@ extern "C" int gadmm_greedy_chains(const double* uv, int E, int n, double side, 
   return 0;
 }
 
-// Per-epoch device tables of the one-launch D-GADMM kernel (chain_persistent.hip, dynamic mode),
-// from the chains P [E][n] (position -> worker): for each local worker li (global id loc[li]) its
-// slot (li, gid, left, right) and chain position in every epoch. Replaces ~0.5 ms of numpy per
-// solve (argsort + fancy indexing over ~300 epochs) on the host path of every D-GADMM solve.
 // The blocked kernel's D-GADMM tables (one GPU, every worker local: li == worker id) from the chains
 // P [E][n]: per (epoch, chain POSITION) the slot (li, gid, left, right); per (epoch, worker) its
 // position; and per (epoch, position) the flush pair (PersistArgs::ep_flush): the old-chain
 // neighbours of the worker placed there if it was a head of the previous epoch's chain, else -1.
 // The numpy equivalent (chain_engine.py: epoch_flush_table) cost ~0.1-0.2 ms per solve.
+// Every row of P must be a permutation of 0..n-1 (-2 otherwise: a duplicate would leave a stale
+// position of the previous epoch in pos / the flush pairs).
 extern "C" int gadmm_epoch_tables_blocked(const long long* P, int E, int n, int* slots, int* pos, int* flush) {
   if (E < 0 || n < 1 || !P || (E > 0 && (!slots || !pos || !flush))) return -1;
-  std::vector<int> pos_prev(n), pos_cur(n);
+  std::vector<int> pos_prev(n), pos_cur(n), seen(n, -1);
   for (int e = 0; e < E; ++e) {
     const long long* pe = P + (size_t)e * n;
     for (int p = 0; p < n; ++p) {
       const long long w = pe[p];
-      if (w < 0 || w >= n) return -2;
+      if (w < 0 || w >= n || seen[w] == e) return -2;
+      seen[w] = e;
       pos_cur[w] = p;
     }
     for (int p = 0; p < n; ++p) {
@@ -147,15 +146,21 @@ extern "C" int gadmm_epoch_tables_blocked(const long long* P, int E, int n, int*
   return 0;
 }
 
+// Per-epoch device tables of the one-launch D-GADMM kernel (chain_persistent.hip, dynamic mode),
+// from the chains P [E][n] (position -> worker): for each local worker li (global id loc[li]) its
+// slot (li, gid, left, right) and chain position in every epoch. Replaces ~0.5 ms of numpy per
+// solve (argsort + fancy indexing over ~300 epochs) on the host path of every D-GADMM solve.
+// Rows of P must be permutations (-2 otherwise).
 extern "C" int gadmm_epoch_tables(const long long* P, int E, int n, const long long* loc, int nloc, int* slots,
                                   int* pos) {
   if (E < 0 || n < 1 || nloc < 0 || !P || (nloc > 0 && (!loc || !slots || !pos))) return -1;
-  std::vector<int> pos_of(n);
+  std::vector<int> pos_of(n), seen(n, -1);
   for (int e = 0; e < E; ++e) {
     const long long* pe = P + (size_t)e * n;
     for (int p = 0; p < n; ++p) {
       const long long w = pe[p];
-      if (w < 0 || w >= n) return -2;
+      if (w < 0 || w >= n || seen[w] == e) return -2;
+      seen[w] = e;
       pos_of[w] = p;
     }
     for (int li = 0; li < nloc; ++li) {

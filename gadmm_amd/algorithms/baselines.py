@@ -116,7 +116,17 @@ def _fo_engine(ctx: _Ctx, backend: str, alg: str = "GD"):
     return FirstOrderEngine.get(ctx.model, ctx.comm, ctx.placement, ctx.n_total)
 
 
-def _native_result(name, out, obj0, units, **extra) -> RunResult:
+def model_bytes(units: np.ndarray, d: int) -> int:
+    """The reference's communication model in bytes: every comm unit is one d-row transmission of f64
+    (GD_DGD_LAG.m:102 and LinearRegression_Synthetic.m:100-142: a parameter-server iteration = the
+    workers' uploads + ONE broadcast of theta down; DGD / dual averaging = one transmission per worker
+    to its chain neighbours). This is the byte axis on which GD / LAG / IAG, star ADMM and GADMM compare
+    (E1 / E7 curves), independent of how the fabric realises the server: the native engine replicates
+    the server's table on every rank, so its FABRIC bytes (``bytes_sent``) grow with the rank count."""
+    return int(round(float(units[-1]))) * int(d) * 8 if len(units) else 0
+
+
+def _native_result(name, out, obj0, units, d: int, **extra) -> RunResult:
     obj = out["obj"]
     n = len(obj)
     return RunResult(algorithm=name, obj=obj, loss=np.abs(obj - obj0), iters=out["iters"] if out["converged"] else n,
@@ -124,7 +134,8 @@ def _native_result(name, out, obj0, units, **extra) -> RunResult:
                      time_trace=out["times"], comm_units=units, bytes_sent=int(out.get("payload_bytes", 0)),
                      bytes_total=int(out.get("payload_bytes", 0)),
                      extra=dict(extra, engine="native-persistent", rows_pushed=out.get("rows_pushed", 0),
-                                flags_pushed=out.get("flags_pushed", 0), wire_bytes=out.get("wire_bytes", 0)))
+                                flags_pushed=out.get("flags_pushed", 0), wire_bytes=out.get("wire_bytes", 0),
+                                model_bytes=model_bytes(units, d)))
 
 
 def _result(name, stop: Stopper, ctx: _Ctx, units: np.ndarray, converged: bool, iters: int, **extra):
@@ -132,7 +143,7 @@ def _result(name, stop: Stopper, ctx: _Ctx, units: np.ndarray, converged: bool, 
     return RunResult(algorithm=name, obj=obj, loss=loss, iters=iters, converged=converged,
                      wall_s=float(times[-1]) if len(times) else 0.0, time_trace=times, comm_units=units,
                      bytes_sent=run_bytes(ctx.comm, ctx.snap), bytes_total=total_bytes(ctx.comm, ctx.snap),
-                     extra=extra)
+                     extra=dict(extra, model_bytes=model_bytes(units, ctx.d)))
 
 
 # ------------------------------------------------------------------------------------------------- GD
@@ -143,7 +154,7 @@ def gradient_descent(model, local_ids, n_total, num_iter, obj0, stepsize, comm=N
     if eng is not None:
         out = eng.run("GD", num_iter, stepsize, obj0, tol, faithful)
         n = len(out["obj"])
-        return _native_result("GD", out, obj0, np.arange(1, n + 1, dtype=np.float64) * (n_total + 1),
+        return _native_result("GD", out, obj0, np.arange(1, n + 1, dtype=np.float64) * (n_total + 1), ctx.d,
                               final_theta=None)
     d = ctx.d
     theta = torch.zeros(d, dtype=torch.float64, device=ctx.dev)
@@ -179,7 +190,7 @@ def decentralized_gd(model, local_ids, n_total, num_iter, obj0, stepsize, comm=N
     if eng is not None:
         out = eng.run("DGD", num_iter, stepsize / 100.0, obj0, tol, faithful)
         n = len(out["obj"])
-        return _native_result("DGD", out, obj0, np.arange(1, n + 1, dtype=np.float64) * n_total)
+        return _native_result("DGD", out, obj0, np.arange(1, n + 1, dtype=np.float64) * n_total, ctx.d)
     d, dev = ctx.d, ctx.dev
     nl = len(ctx.local_ids)
     theta = torch.zeros((nl, d), dtype=torch.float64, device=dev)
@@ -290,7 +301,8 @@ def lag(model, local_ids, n_total, num_iter, obj0, stepsize, hmax_full: torch.Te
     if eng is not None:
         out = eng.run("LAG-" + variant, num_iter, stepsize, obj0, tol, faithful, thrd=thrd,
                       hsq=hmax_full.to(dev, torch.float64) ** 2)
-        return _native_result("LAG-" + variant, out, obj0, _lag_units(out["cnt"]), uploads=int(round(out["uploads"])))
+        return _native_result("LAG-" + variant, out, obj0, _lag_units(out["cnt"]), ctx.d,
+                              uploads=int(round(out["uploads"])))
     ids = torch.tensor(ctx.local_ids, dtype=torch.long, device=dev)
     nl = len(ctx.local_ids)
     server = _Server(ctx, torch.ones((N, d), dtype=torch.float64, device=dev))
@@ -382,7 +394,7 @@ def iag(model, local_ids, n_total, num_iter, obj0, stepsize, mode: str = "cyclic
     if eng is not None:
         out = eng.run("IAG", num_iter, stepsize / n_total, obj0, tol, faithful, sched=sched)
         n = len(out["obj"])
-        return _native_result(name, out, obj0, np.arange(1, n + 1, dtype=np.float64) * 2)
+        return _native_result(name, out, obj0, np.arange(1, n + 1, dtype=np.float64) * 2, ctx.d)
     d, dev = ctx.d, ctx.dev
     N = n_total
     step = stepsize / N

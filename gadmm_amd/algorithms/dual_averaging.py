@@ -44,7 +44,8 @@ def dual_averaging(model, local_ids: Sequence[int], n_total: int, alpha: float, 
                              comm_units=np.arange(1, n + 1, dtype=np.float64) * n_total,
                              bytes_sent=int(out["payload_bytes"]), bytes_total=int(out["payload_bytes"]),
                              extra={"jacobi": jacobi, "nranks": comm.nranks, "engine": "native-persistent",
-                                    "rows_pushed": out["rows_pushed"], "wire_bytes": out["wire_bytes"]})
+                                    "rows_pushed": out["rows_pushed"], "wire_bytes": out["wire_bytes"],
+                                    "model_bytes": n * n_total * model.d * 8, "dim": model.d})
         if backend == "native":
             raise RuntimeError("native dual averaging needs GPU ranks with contiguous segments and d <= 128")
     dev, d = model.device, model.d
@@ -111,4 +112,4 @@ def dual_averaging(model, local_ids: Sequence[int], n_total: int, alpha: float, 
                      wall_s=float(times[-1]) if n else 0.0, time_trace=times,
                      comm_units=np.arange(1, n + 1, dtype=np.float64) * n_total,
                      bytes_sent=run_bytes(comm, snap), bytes_total=total_bytes(comm, snap),
-                     extra={"jacobi": jacobi, "nranks": R})
+                     extra={"jacobi": jacobi, "nranks": R, "model_bytes": n * n_total * d * 8, "dim": d})

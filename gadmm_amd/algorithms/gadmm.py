@@ -251,7 +251,7 @@ def _static_schedule(schedule, max_iter) -> bool:
 def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, schedule, local_solver,
                        step, max_inner, inner_tol, cost_quirk, name, opts, state=None):
     """``opts``: ``block`` (iterations per graph replay), ``persistent`` (auto/True/False), ``graph``,
-    ``cache``, ``state``, ``fabric`` (an ``XgmiFabric``: the device-initiated multi-GPU persistent
+    ``cache``, ``state``, ``refresh`` (recompute Gram + inverses from the raw shards first), ``fabric`` (an ``XgmiFabric``: the device-initiated multi-GPU persistent
     kernels; with ``table_slots >= lag + 4`` it also runs multi-rank D-GADMM in one launch),
     ``stop_iter`` (static chains: run no iteration past it, on the graph engine - the persistent
     kernels stop only at the decision).
@@ -279,6 +279,14 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     cache = getattr(model, "_chain_engines", None) if rcomm is None else None
     eng = cache.get(key) if cache is not None else None
     fresh = eng is None
+    # ``refresh``: the solve starts from the raw shards -- the Gram (K1) and the cached inverses (K2) are
+    # recomputed (benchmarks time the same set-up in every config: bench.py's headline does this too)
+    refresh = bool(opts.get("refresh", False)) and kind == "linear"
+    if eng is None and refresh:
+        from ..ops.linalg import gram
+        gram(model.X, model.y, out=(model.A, model.b, model.yy))  # the new engine inverts the fresh Gram
+    if eng is not None and refresh:
+        eng.refresh(model.X, model.y)  # in place on the engine's stream (Gram, then inverses)
     if eng is None:
         eng = NativeChainEngine(model.X, model.y, local_ids, n_total, kind, rho=rho, obj0=obj0, tol=tol,
                                 max_iter=max_iter, lam=getattr(model, "lam", 0.0), step=step, max_inner=max_inner,
@@ -530,7 +538,12 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
                     primal_res=pres,
                     extra={"backend": "native", "engine": engine_kind, "rank": rank, "nranks": comm.nranks,
                            "solver": local_solver, "monitor_bytes": int(mon), "wire_bytes": int(wire),
-                           "transport": getattr(comm, "backend", "local") if fabric is None else "xgmi"})
+                           "transport": getattr(comm, "backend", "local") if fabric is None else "xgmi",
+                           # effective settings (engine-dependent defaults): the objective
+                           # evaluation of the phase kernels and, for Newton, the chord threshold used
+                           "obj_mode": eng.obj_mode_name})
+    if local_solver == "newton":
+        res.extra["chord"] = eng.chord_persistent if str(engine_kind).startswith("persistent") else eng.chord
     res.extra["engine_obj"] = eng
     _timing.host_stamp("native:result")
     if opts.get("state", True):

@@ -114,6 +114,8 @@ def _standard_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, c
         if not eng.eligible():
             return None
         cache[key] = eng
+    elif opts.get("refresh"):
+        eng.refresh(model.X, model.y)  # Gram + cached inverses from the raw shards, on the engine stream
     eng.obj0, eng.tol = float(obj0), float(tol)
     t0 = _time.perf_counter()
     iters, done, _ = eng.run(timeout_s=float(opts.get("timeout_s", 20.0)))
@@ -151,10 +153,15 @@ def _standard_admm_big(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     with roctx_range("%s native-big N=%d" % (name, n_total)):
         iters, done, wall = eng.run(obj0, tol, max_iter, block=int(opts.get("block", 8)))
     tr, tt = eng.objective_trace(iters), eng.time_trace(iters)
+    # the host enqueues whole blocks: collectives enqueued after the device-side stop are no-ops that
+    # move nothing, so the bytes are the per-iteration payload times the iterations run (the comm's
+    # enqueue counters, ``enqueued_coll_bytes``, include the skipped ones)
     coll = int(comm.stats.delta(snap).get("coll_bytes", 0)) if comm.nranks > 1 else 0
+    sent = eng.coll_bytes_per_iteration() * iters
     return RunResult(algorithm=name, obj=tr, loss=np.abs(tr - obj0), iters=iters, converged=(done == 1), wall_s=wall,
                      time_trace=tt,
                      comm_units=np.arange(1, iters + 1, dtype=np.float64) * 2 * (n_total - 1),
-                     bytes_sent=eng.coll_bytes_per_iteration() * iters, bytes_total=coll,
+                     bytes_sent=sent, bytes_total=sent,
                      extra={"hub": n_total - 1, "hub_rank": hub_rank, "nranks": comm.nranks, "backend": "native",
-                            "engine": eng.last_kernel, "inverse_setup_s": eng.setup_s, "engine_obj": eng})
+                            "engine": eng.last_kernel, "inverse_setup_s": eng.setup_s, "engine_obj": eng,
+                            "transport": getattr(comm, "backend", "local"), "enqueued_coll_bytes": coll})

@@ -58,7 +58,12 @@ class DistributedChainSolver:
     def __init__(self, X_loc: torch.Tensor, y_loc: torch.Tensor, local: Sequence[int], n_total: int, placement,
                  rank: int, world: int, device: torch.device, rho: float, obj0: float, tol: float,
                  max_iter: int = 20000, engine: str = "auto", fabric: str = "auto", share: bool = False,
-                 block: int = 0, halo_data=None, timeout_s: float = 20.0, use_graph: bool = True):
+                 block: int = 0, halo_data=None, timeout_s: float = 20.0, use_graph: bool = True,
+                 dl_halo: Optional[bool] = None, strict: bool = False):
+        """``dl_halo`` (data-local blocked engine): None = the halo mode where eligible, True = only the
+        halo mode, False = never. ``strict``: raise (on every rank together) when the requested
+        persistent engine cannot run instead of falling back to the graph engine (the engine
+        tournament of bench.py builds each candidate this way)."""
         from .chain_engine import NativeChainEngine
 
         self.X, self.y = X_loc, y_loc
@@ -72,6 +77,7 @@ class DistributedChainSolver:
         self.eng = self.comm = self.fab = self.blk = None
         self.kind, self.persistent, self.replicated_bytes = "local", False, 0
         self.fallbacks = []
+        self.dl_halo = dl_halo
         self.delay_next_s = 0.0  # test hook: sleep before the next launch (a slow / stalled peer)
         self._NCE = NativeChainEngine
         if world == 1:
@@ -91,6 +97,8 @@ class DistributedChainSolver:
             if self.blk is None and fabric in ("auto", "xgmi") and engine in ("auto", "persistent", "per-worker"):
                 self._try_xgmi()
             if self.eng is None and self.blk is None:
+                if strict and engine != "graph":
+                    raise RuntimeError("engine %r unavailable on some rank" % engine)
                 self._graph_engine()
 
     # ---------------------------------------------------------------------------------------------
@@ -110,7 +118,7 @@ class DistributedChainSolver:
             return
         try:
             blk = BlockedXgmiEngine(self.X, self.y, self.n, self.placement, self.rank, self.rho, self.obj0, self.tol,
-                                    self.max_iter, self.device, data_local=True)
+                                    self.max_iter, self.device, data_local=True, dl_halo=self.dl_halo)
         except Exception as e:  # collective inside the constructor: every rank raises together
             if self.rank == 0:
                 print("DistributedChainSolver: data-local blocked fabric unavailable (%s)" % e, file=sys.stderr)

@@ -9,7 +9,11 @@ device (``ctl.done``) and every kernel of later iterations returns at once, so t
 
 Collectives go through the run's comm on the engine stream: on one rank (``LocalComm``) they are
 no-ops, across GPUs ``RcclComm`` issues ``ncclReduce`` / ``ncclBroadcast`` / ``ncclAllReduce`` (the
-star's reduce + broadcast of SURVEY.md C5; 2d + d doubles per non-hub rank and iteration).
+star's reduce + broadcast of SURVEY.md C5; 2d + d doubles per non-hub rank and iteration), and
+``IpcComm`` runs the same three as device kernels over IPC-mapped mailboxes (``ipc_coll_kernel``:
+tagged granules pushed straight into the hub's / every rank's memory, sums in rank order). The IPC
+path needs no RCCL, so it also runs with several ranks sharing one GPU (the rehearsal of BASELINE
+configs[4] on a one-GPU box) and is an RCCL-free data plane on a node.
 """
 from __future__ import annotations
 
@@ -33,13 +37,14 @@ class StarBigArgs(ctypes.Structure):
         ("Minv", ctypes.c_void_p), ("A", ctypes.c_void_p), ("b", ctypes.c_void_p), ("yy", ctypes.c_void_p),
         ("theta", ctypes.c_void_p), ("lam", ctypes.c_void_p), ("th_hub", ctypes.c_void_p), ("agg", ctypes.c_void_p),
         ("rbuf", ctypes.c_void_p), ("objw", ctypes.c_void_p), ("objp", ctypes.c_void_p), ("trace", ctypes.c_void_p),
-        ("ctl", ctypes.c_void_p), ("tstamp", ctypes.c_void_p),
+        ("ctl", ctypes.c_void_p), ("tstamp", ctypes.c_void_p), ("gid", ctypes.c_void_p),
     ]
 
 
 def comm_ok(comm) -> bool:
-    """Comms whose collectives are stream-ordered device operations: one rank, or RCCL."""
-    return comm is None or comm.nranks == 1 or getattr(comm, "backend", "") == "rccl"
+    """Comms whose collectives are stream-ordered device operations: one rank, RCCL, or the IPC
+    device-copy transport."""
+    return comm is None or comm.nranks == 1 or getattr(comm, "backend", "") in ("rccl", "ipc")
 
 
 class StarBigEngine:
@@ -78,7 +83,8 @@ class StarBigEngine:
             self.agg = torch.zeros((2 * d,), dtype=f64, device=dev)
             self.rbuf = torch.zeros((nl * int(self.lib.gadmm_star_big_rstride(d)),), dtype=f64, device=dev)
             self.objw = torch.zeros((nl,), dtype=f64, device=dev)
-            self.objp = torch.zeros((1,), dtype=f64, device=dev)
+            self.objp = torch.zeros((self.n,), dtype=f64, device=dev)  # per global worker (exact all-reduce)
+            self.gid = torch.tensor(self.local, dtype=torch.int32, device=dev)
             self.ctl = torch.zeros((8,), dtype=torch.int32, device=dev)
             self.t0stamp = torch.zeros((1,), dtype=torch.int64, device=dev)
             self.trace = self.tstamp = None
@@ -95,12 +101,14 @@ class StarBigEngine:
                                            self.agg.data_ptr())
         a.rbuf, a.objw, a.objp = self.rbuf.data_ptr(), self.objw.data_ptr(), self.objp.data_ptr()
         a.trace, a.ctl, a.tstamp = self.trace.data_ptr(), self.ctl.data_ptr(), self.tstamp.data_ptr()
+        a.gid = self.gid.data_ptr()
         return a
 
     def run(self, obj0: float, tol: float, max_iter: int, block: int = 8):
         """One solve from theta = lam = 0. Returns (iters, done, wall_s); traces in ``self.trace``.
         Collective across the comm's ranks (every rank enqueues the same iterations)."""
         multi = self.comm is not None and self.comm.nranks > 1
+        ipc = multi and getattr(self.comm, "backend", "") == "ipc"
         dev = self.device
         self.trace = torch.full((int(max_iter),), float("nan"), dtype=torch.float64, device=dev)
         self.tstamp = torch.zeros((int(max_iter),), dtype=torch.int64, device=dev)
@@ -117,19 +125,27 @@ class StarBigEngine:
             self.ctl.zero_()
             self.ctl[0] = 1  # iter
             native.check(self.lib.gadmm_write_stamp(self.t0stamp.data_ptr(), st), "write_stamp")
+            if ipc:
+                self.comm.new_epoch(st)
+                coll = self.comm.device_collective
+                reduce = lambda t, root: coll("reduce", t, root, self.ctl, st)  # noqa: E731
+                bcast = lambda t, root: coll("broadcast", t, root, self.ctl, st)  # noqa: E731
+                allred = lambda t: coll("allreduce", t, 0, self.ctl, st)  # noqa: E731
+            elif multi:
+                reduce, bcast, allred = self.comm.reduce_sum, self.comm.broadcast, self.comm.allreduce_sum
             it = 0
             done = 0
             while it < max_iter and not done:
                 for _ in range(min(block, max_iter - it)):
                     ch(self.lib.gadmm_star_big_workers(ctypes.byref(a), st), "star_big_workers")
                     if multi:
-                        self.comm.reduce_sum(self.agg, self.hub_rank)
+                        reduce(self.agg, self.hub_rank)
                     ch(self.lib.gadmm_star_big_hub(ctypes.byref(a), st), "star_big_hub")
                     if multi:
-                        self.comm.broadcast(self.th_hub, self.hub_rank)
+                        bcast(self.th_hub, self.hub_rank)
                     ch(self.lib.gadmm_star_big_post(ctypes.byref(a), st), "star_big_post")
                     if multi:
-                        self.comm.allreduce_sum(self.objp)
+                        allred(self.objp)
                     ch(self.lib.gadmm_star_big_finish(ctypes.byref(a), st), "star_big_finish")
                     it += 1
                 done = int(self.ctl[1].item())  # one host look per block (synchronises the stream)
@@ -149,10 +165,12 @@ class StarBigEngine:
 
     def coll_bytes_per_iteration(self) -> int:
         """Collective payload leaving this rank per iteration: [sum lam, sum theta] to the hub (2d
-        doubles, non-hub ranks), theta_hub to every other rank (d doubles, hub rank), the objective."""
+        doubles, non-hub ranks), theta_hub to every other rank (d doubles, hub rank), the per-worker
+        objective slots (N doubles; the IPC all-reduce pushes them to every other rank)."""
         if self.comm is None or self.comm.nranks == 1:
             return 0
         R = self.comm.nranks
+        obj = 8 * self.n * ((R - 1) if getattr(self.comm, "backend", "") == "ipc" else 1)
         if self.comm.rank == self.hub_rank:
-            return self.d * 8 * (R - 1) + 8
-        return 2 * self.d * 8 + 8
+            return self.d * 8 * (R - 1) + obj
+        return 2 * self.d * 8 + obj

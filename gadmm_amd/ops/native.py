@@ -195,7 +195,13 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_star_capacity": (c_long, [ctypes.POINTER(StarArgs)]),
         "gadmm_star_launch": (c_int, [ctypes.POINTER(StarArgs), c_void_p]),
         "gadmm_star_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
-        "gadmm_ipc_box_bytes": (c_long, [c_int, c_int, c_int]),
+        "gadmm_star_big_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
+        "gadmm_ipc_box_bytes": (c_long, [c_int, c_int, c_int, c_int]),
+        "gadmm_ipc_collective": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, ctypes.c_uint, c_void_p,
+                                         c_void_p]),
+        "gadmm_ipc_coll_counters": (c_int, [c_void_p, ctypes.POINTER(c_longlong)]),
+        "gadmm_ipc_hop_probe": (c_int, [c_void_p, c_void_p, c_int, c_int, ctypes.c_uint, c_double,
+                                        ctypes.POINTER(ctypes.c_ulonglong)]),
         "gadmm_ipc_xport_create": (c_void_p, [c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_double]),
         "gadmm_ipc_xport_destroy": (c_int, [c_void_p]),
         "gadmm_ipc_new_epoch": (c_int, [c_void_p, c_void_p]),

@@ -44,7 +44,7 @@ class IpcTransport:
         torch.cuda.set_device(device)
         err, mine = "", None
         try:
-            self.box = _Buf(self.lib, int(self.lib.gadmm_ipc_box_bytes(self.n_total, self.d, self.ring)))
+            self.box = _Buf(self.lib, int(self.lib.gadmm_ipc_box_bytes(self.n_total, self.d, self.ring, nranks)))
             mine = bytes(self.box.handle.raw)
         except Exception as e:  # pragma: no cover - box dependent
             err = "rank %d mailbox: %s" % (rank, e)
@@ -118,7 +118,45 @@ class IpcComm(Comm):
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return t
 
-    def allreduce_sum(self, t):  # one-time set-up only (oracles); the hot path never comes here
+    # device collectives on a stream (csrc/kernels/ipc_xport.hip: ipc_coll_kernel), sums in rank order;
+    # every rank must issue the same sequence. ``ctl``: the caller's ChainCtl (done skips, timeouts set 4)
+    KIND = {"reduce": 0, "broadcast": 1, "allreduce": 2}
+
+    def device_collective(self, kind: str, t, root: int, ctl, stream) -> None:
+        from ..ops import native
+        k = self.KIND[kind]
+        seq = self._seq = getattr(self, "_seq", 0) + 1
+        native.check(self.transport.lib.gadmm_ipc_collective(self.xport, k, int(root), t.data_ptr(), t.data_ptr(),
+                                                             int(t.numel()), seq & 0xffffffff, ctl.data_ptr(),
+                                                             stream), "ipc_collective(%s)" % kind)
+        R, me = self.nranks, self.rank
+        sent = (R - 1) if k == 2 else (1 if (k == 0 and me != root) else (R - 1 if (k == 1 and me == root) else 0))
+        self.stats.coll_bytes += sent * t.numel() * t.element_size()
+
+    def new_epoch(self, stream) -> None:
+        """Start a new solve on this transport: granules of earlier solves stop matching (every rank)."""
+        from ..ops import native
+        native.check(self.transport.lib.gadmm_ipc_new_epoch(self.xport, stream), "ipc_new_epoch")
+
+    def allreduce_sum(self, t):
+        """One-time set-up all-reduce (oracles: the d x d Gram of SURVEY.md C10). A large f64 device
+        tensor goes through the device collective in chunks of the coll row (2 d + 8 doubles; no host
+        staging of an 800 MB Gram at d = 10k), anything else over the gloo control plane."""
+        if t.is_cuda and t.dtype == torch.float64 and t.is_contiguous() and t.numel() > 4096:
+            from ..ops import native
+            lib = self.transport.lib
+            st = torch.cuda.current_stream(self.device).cuda_stream
+            if getattr(self, "_ctl", None) is None:
+                self._ctl = torch.zeros((8,), dtype=torch.int32, device=self.device)
+            self._ctl.zero_()
+            self.new_epoch(st)
+            flat = t.view(-1)
+            step = 2 * self.transport.d + 8
+            for c0 in range(0, flat.numel(), step):
+                self.device_collective("allreduce", flat[c0:c0 + step], 0, self._ctl, st)
+            if int(self._ctl[1].item()) != 0:
+                native.check(-1, "ipc allreduce_sum: a peer did not arrive (done=%d)" % int(self._ctl[1].item()))
+            return t
         h = t.detach().cpu()
         dist.all_reduce(h, group=self.group)
         t.copy_(h)

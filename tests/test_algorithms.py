@@ -183,3 +183,26 @@ def test_primal_residual_trace(lin_model, lin_obj0):
     r = group_admm_closed_form(lin_model, 3.0, lin_obj0, 1e-8, 3000, backend="torch")
     assert r.primal_res is not None and len(r.primal_res) == r.iters == 1373
     assert r.primal_res[-1] < 1e-6 * r.primal_res[:10].max()
+
+
+def test_first_order_model_bytes_follow_reference_units(lin24):
+    """GD / LAG / IAG / DGD / dual averaging report the reference's communication model
+    in bytes (one d-row of f64 per comm unit: uploads + one broadcast down per server iteration), the
+    byte axis shared with star ADMM and GADMM, next to the fabric bytes."""
+    import numpy as np
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import gradient_descent, lag, iag, decentralized_gd, dual_averaging, global_constants
+    m = LinearRegression(lin24.X, lin24.y)
+    s = global_constants(m)["stepsize"]
+    ids, n, d = list(range(24)), 24, 50
+    gd = gradient_descent(m, ids, n, 40, 218.6486436261889, s)
+    assert gd.extra["model_bytes"] == 40 * (n + 1) * d * 8  # N uploads + 1 broadcast per iteration
+    lw = lag(m, ids, n, 40, 218.6486436261889, s, m.hmax(), "WK")
+    assert lw.extra["model_bytes"] == int(round(lw.comm_units[-1])) * d * 8
+    ia = iag(m, ids, n, 40, 218.6486436261889, s, "cyclic", None)
+    assert ia.extra["model_bytes"] == 40 * 2 * d * 8
+    dg = decentralized_gd(m, ids, n, 40, 218.6486436261889, s)
+    assert dg.extra["model_bytes"] == 40 * n * d * 8
+    da = dual_averaging(m, ids, n, s, 218.6486436261889, 1e-12, 40)
+    assert da.extra["model_bytes"] == len(da.obj) * n * d * 8
+    assert np.isfinite(gd.obj).all()

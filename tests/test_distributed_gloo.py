@@ -179,3 +179,64 @@ def test_iag_dgd_gd_gloo(lin_obj0):
 def test_global_optimum_allreduce(lin_obj0):
     res = spawn(_rank_fn, 2, "optimum", {"obj0": lin_obj0})
     assert res[0] == pytest.approx(lin_obj0, rel=1e-12)
+
+
+# ------------------------------------------------------------------------------------------------
+# bench.py's multi-GPU engine tournament (gadmm_amd/engine/tournament.py): the agreement logic with
+# stand-in solvers on gloo CPU ranks (no device).
+class _FakeSolver:
+    def __init__(self, rank, delays, fail_at=None, iters=10):
+        self.rank, self.delays, self.fail_at, self.iters = rank, delays, fail_at, iters
+        self.n, self.closed = 0, False
+
+    def guarded_solve(self):
+        import time
+        from gadmm_amd.engine.multigpu import SolveOut
+        time.sleep(self.delays[self.rank])
+        self.n += 1
+        done = 4 if self.fail_at is not None and self.n == self.fail_at[1] and self.rank == self.fail_at[0] else 1
+        return SolveOut(self.iters, done, 0, 0, 0)
+
+    def close(self):
+        self.closed = True
+
+
+def _tournament_rank(rank, world):
+    from gadmm_amd.engine.tournament import engine_tournament
+    made = {}
+
+    def fac(name, delays, fail_at=None, raise_on=None, iters=10):
+        def f():
+            if raise_on is not None and rank == raise_on:
+                raise RuntimeError("not eligible here")
+            made[name] = _FakeSolver(rank, delays, fail_at, iters)
+            return made[name]
+        return (name, f)
+
+    cands = [fac("slow-everywhere", [0.03, 0.03]),
+             fac("fast-on-0-only", [0.002, 0.05]),       # max over ranks = 50 ms: must lose
+             fac("missing-on-1", [0.001, 0.001], raise_on=1),
+             fac("fails-a-solve", [0.001, 0.001], fail_at=(1, 2)),
+             fac("wrong-iterations", [0.001, 0.001], iters=11),
+             fac("steady", [0.012, 0.012])]
+    name, sol, table = engine_tournament(cands, world, solves=3, warm=1, expect=10)
+    return {"winner": name, "winner_is_made": sol is made.get(name), "table": table,
+            "closed": {k: v.closed for k, v in made.items()}}
+
+
+def test_engine_tournament_agreement_on_gloo_ranks():
+    res = spawn(_tournament_rank, 2, timeout=120)
+    for r in res:
+        assert r["winner"] == "steady" and r["winner_is_made"]
+        rows = {row["engine"]: row for row in r["table"]}
+        assert [row["engine"] for row in r["table"]][:2] == ["slow-everywhere", "fast-on-0-only"]
+        assert rows["fast-on-0-only"]["ok"] and rows["fast-on-0-only"]["ms"] >= 45  # max over ranks
+        assert not rows["missing-on-1"]["ok"] and rows["missing-on-1"]["ms"] is None
+        assert not rows["fails-a-solve"]["ok"]
+        assert not rows["wrong-iterations"]["ok"]
+        assert rows["steady"]["ok"] and rows["steady"]["iters"] == 10
+        # every loser is closed as soon as it loses, the winner stays open
+        assert all(v for k, v in r["closed"].items() if k != "steady") and not r["closed"]["steady"]
+    # both ranks ranked from identical numbers
+    assert [(x["engine"], x["ok"], x["ms"]) for x in res[0]["table"]] == \
+        [(x["engine"], x["ok"], x["ms"]) for x in res[1]["table"]]

@@ -218,6 +218,9 @@ def test_logistic_newton_kernel_matches_torch(log24, log_obj0, chord, persistent
     assert b.extra["backend"] == "torch"
     assert a.iters == b.iters == 424 and a.converged and b.converged
     np.testing.assert_allclose(a.obj, b.obj, rtol=1e-12, atol=0)
+    # the effective chord is recorded: the engine default (0.02 graph / 0.3 persistent) when none is given
+    assert a.extra["chord"] == (chord if chord is not None else (0.3 if persistent else 0.02))
+    assert a.extra["obj_mode"] == "exact"
     print("newton(chord=%s, persistent=%s): native %.1f ms, torch %.1f ms, %d iterations"
           % (chord, persistent, a.wall_s * 1e3, t_torch * 1e3, a.iters))
 
@@ -490,6 +493,34 @@ def test_dgadmm_persistent_dynamic_matches_epoch_path(lin24, lin_obj0, coh, bloc
     assert a.iters == b.iters and a.converged
     assert np.array_equal(a.obj, b.obj)
     assert np.allclose(a.com_cost, b.com_cost, rtol=1e-14)
+
+
+@pytest.mark.parametrize("n", [2, 3, 5])
+def test_dgadmm_blocked_dynamic_small_chains_idle_decision_wave(n, monkeypatch):
+    """in the blocked kernel's dynamic mode a short chain leaves idle waves
+    (u >= nv), and the stop-decision poll may run on one. Idle waves follow the same barrier schedule
+    as the active ones, re-chain barriers included, so they must read the same staged epoch starts;
+    with unstaged starts an idle decision wave drifted one barrier per re-chain and the launch hung
+    (done = 4). Coherence 3 re-chains often: == the epoch-by-epoch engine, bit for bit."""
+    import numpy as np
+    from gadmm_amd.data import linear_synthetic
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.oracle.reference import opt_linear
+    from gadmm_amd.algorithms import dynamic_group_admm
+    from gadmm_amd.parallel import topology as T
+
+    monkeypatch.setenv("GADMM_BLOCKED_DYN", "1")
+    ds = linear_synthetic(n)
+    Xf, yf = ds.stacked()
+    obj0 = opt_linear(Xf.numpy(), yf.numpy())
+    m = LinearRegression(ds.X.to(DEV), ds.y.to(DEV))
+    p0, c0, _ = T.find_path(n, np.random.default_rng(5))
+    a = dynamic_group_admm(m, 1.0, obj0, 1e-4, 2000, p0, c0, 3, seed=99)
+    assert a.extra["engine_obj"].last_kernel.startswith("blocked-dyn("), a.extra["engine_obj"].last_kernel
+    b = dynamic_group_admm(m, 1.0, obj0, 1e-4, 2000, p0, c0, 3, seed=99, engine_opts={"persistent": False})
+    assert a.extra["engine"] == "persistent-dynamic" and b.extra["engine"] == "epochs"
+    assert a.iters == b.iters and a.converged == b.converged
+    assert np.array_equal(a.obj, b.obj)
 
 
 def _blocked_xgmi_rank(rank, world, rho, tol):

@@ -538,3 +538,173 @@ def test_ipc_graph_engine_recovers_after_a_stalled_solve():
     assert all(r["kind"] == "ipc" for r in res)
     assert any(r["first"] == 4 for r in res)  # the stalled solve did time out somewhere
     assert all(r["second"] == (1373, 1) for r in res), res
+
+
+# ------------------------------------------------------------------------------------------------
+# BASELINE configs[4] (LinearRegression_Real.m:84-98 vs standared_ADMM.m:57-88) at large d across ranks:
+# the chain_big GADMM phases on the graph engine and the star_big engine, both over the IPC transport
+# (device collectives for the star), at a reduced shape, against the one-rank run with the same N.
+def _big_problem(n, rows, dim, ids, dev):
+    from gadmm_amd.data import gaussian_regression
+    from gadmm_amd.models import LinearRegression
+    ds = gaussian_regression(n, rows, dim, seed=0, labels="linear", device=dev, worker_ids=ids)
+    return LinearRegression(ds.X, ds.y)
+
+
+def _big_solves(m, ids, n, comm, pl, rows):
+    from gadmm_amd.algorithms import chain_admm, standard_admm
+    obj0 = m.optimum(comm, n_total=n)
+    rho, tol = 0.5 * rows, 1e-8 * abs(obj0)
+    g = chain_admm(m, ids, n, rho, obj0, tol, 2000, comm=comm, placement=pl,
+                   engine_opts={"cache": False, "residual": False})
+    s = [standard_admm(m, ids, n, rho, obj0, tol, 2000, comm=comm, placement=pl) for _ in range(2)]
+    return obj0, g, s
+
+
+def _big_rank(rank, world, wpg, rows, dim):
+    import torch
+    from gadmm_amd.parallel.ipc import IpcComm
+    from gadmm_amd.parallel.topology import Placement
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    n = wpg * world
+    ids = list(range(rank * wpg, (rank + 1) * wpg))
+    m = _big_problem(n, rows, dim, ids, dev)
+    comm = IpcComm(n, dim, 16, dev)
+    obj0, g, s = _big_solves(m, ids, n, comm, Placement.contiguous(n, world), rows)
+    out = {"obj0": obj0, "g": (g.iters, g.converged, g.extra.get("engine"), int(g.bytes_sent)), "g_trace": g.obj,
+           "s": [(r.iters, r.converged, r.extra.get("backend"), int(r.bytes_sent), int(r.bytes_total)) for r in s],
+           "s_trace": [r.obj for r in s], "theta": g.extra["engine_obj"].local_theta().cpu().numpy()}
+    g.extra["engine_obj"].close()
+    comm.close()
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_large_d_gadmm_and_star_across_ranks_match_one_rank(world):
+    """configs[4] at 2 workers x 20k rows x d = 2048 per rank, ranks sharing the GPU: GADMM (chain_big
+    phases, graph engine, 16-KB theta rows over the IPC transport) and the large-d star (star_big with
+    the IPC reduce / broadcast / all-reduce device collectives) == one rank with the same N: same
+    iterations, GADMM traces bit for bit, star traces to 1e-12 (the hub's [sum lam, sum theta] adds
+    per-rank partial sums in rank order; at 2 ranks that is the one-rank order exactly, and the
+    objective all-reduce is exact at every rank count), exact bytes."""
+    import torch
+    from gadmm_amd.parallel.launch import spawn
+    wpg, rows, dim = 2, 20000, 2048
+    n = wpg * world
+    res = spawn(_big_rank, world, wpg, rows, dim, timeout=600)
+    m = _big_problem(n, rows, dim, None, torch.device(DEV))
+    obj0, g, s = _big_solves(m, list(range(n)), n, None, None, rows)
+    assert g.converged and s[0].converged and s[0].extra["backend"] == "native"
+    assert s[1].iters == s[0].iters and np.array_equal(s[1].obj, s[0].obj)
+    d = dim
+    for rk, r in enumerate(res):
+        assert abs(r["obj0"] - obj0) <= 1e-12 * abs(obj0)
+        it, conv, eng, pay = r["g"]
+        assert it == g.iters and conv and eng == "graph", r["g"]
+        assert np.array_equal(r["g_trace"], g.obj)
+        nb = (rk > 0) + (rk < world - 1)  # rank boundaries: one 8-d-byte row per phase each way
+        assert pay == nb * d * 8 * g.iters
+        for (si, sconv, sbe, sb, stot), tr in zip(r["s"], r["s_trace"]):
+            assert si == s[0].iters and sconv and sbe == "native"
+            if world == 2:
+                assert np.array_equal(tr, s[0].obj)
+            else:
+                np.testing.assert_allclose(tr, s[0].obj, rtol=1e-12, atol=0)
+            hub = rk == world - 1
+            per_it = (d * 8 * (world - 1) if hub else 2 * d * 8) + 8 * n * (world - 1)
+            assert sb == per_it * si and stot == sb, (rk, sb, stot, per_it * si)
+    # several ranks decide at block ends (one rank right after the converging iteration), so their state
+    # may be up to block - 1 iterations further along: equal up to convergence
+    th = np.concatenate([r["theta"] for r in res])
+    ref = g.extra["engine_obj"].local_theta().cpu().numpy()
+    assert np.allclose(th, ref, rtol=1e-5, atol=1e-8), float(np.max(np.abs(th - ref)))
+
+
+# ------------------------------------------------------------------------------------------------
+# bench.py's multi-GPU path end to end (ranks sharing the GPU): the hop probe, the engine tournament and
+# the collective fallback of a failed timed solve.
+def _bench_json(world, extra_env, *args, timeout=400):
+    import json
+    import os
+    import subprocess
+    import sys
+    from gadmm_amd.parallel.launch import free_port
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GADMM_BENCH_SHARE_GPU="1", MASTER_ADDR="127.0.0.1", **extra_env)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(root, "bench.py"),
+           "--gpus", str(world)] + list(args)
+    p = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert p.returncode == 0 and len(lines) == 1, (p.returncode, p.stdout[-3000:], p.stderr[-3000:])
+    return json.loads(lines[0]), p.stderr
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_tournament_and_hop_probe(world):
+    """The 2 / 4-rank headline: a one-way hop per chain boundary, every candidate engine timed in the
+    warm-up (the halo mode only where it fits), the winner is the fastest agreed candidate and runs
+    the timed loop at the reference iteration count."""
+    out, _ = _bench_json(world, {}, "--steps", "5", "--warmup", "2")
+    assert out["iterations_to_tol"] == 1373 and out["iterations_match_reference"]
+    hops = out["xgmi_hop_us"]
+    assert len(hops) == world - 1 and all(h is not None and 0 < h < 50 for h in hops), hops
+    assert out["hop_probe_same_device"] is True
+    rows = {r["engine"]: r for r in out["engine_tournament"]}
+    assert set(rows) == {"blocked-dl-halo", "blocked-dl", "per-worker", "replicated-halo"}
+    ok = {k: r["ms"] for k, r in rows.items() if r["ok"]}
+    assert "blocked-dl" in ok and "per-worker" in ok and "replicated-halo" in ok
+    assert ("blocked-dl-halo" in ok) == (world == 4)  # 2 ranks: segment + halo head = 13 waves > 12
+    assert out["fallbacks"] == [] and out["timing_restarts"] == 0
+    best = min(ok, key=ok.get)
+    want = {"blocked-dl-halo": "xgmi(blocked-dl-halo)", "blocked-dl": "xgmi(blocked-dl)", "per-worker": "xgmi",
+            "replicated-halo": "xgmi(replicated-halo)"}[best]
+    assert out["fabric"] == want, (best, out["fabric"], rows)
+
+
+def test_bench_timed_loop_stall_falls_back_collectively():
+    """A rank that stalls inside the timed loop (test hook: 3 x the 2 s hand-off deadline before its
+    2nd timed solve) no longer costs the run: every rank falls back to the graph engine together, the
+    timing restarts there, and the rc-0 JSON line names the fallback."""
+    out, err = _bench_json(2, {"GADMM_BENCH_STALL": "1:1"}, "--steps", "4", "--warmup", "1", "--timeout", "2",
+                           "--engine", "blocked-dl")
+    assert out["timing_restarts"] == 1 and len(out["fallbacks"]) == 1, out
+    assert "timed solve failed" in out["fallbacks"][0]
+    assert out["fabric"] == "ipc" and out["engine"] in ("graph", "eager")
+    assert out["iterations_to_tol"] == 1373
+
+
+def _fo_wrap_rank(rank, world):
+    import torch
+    from gadmm_amd.benchmarks import headline_rank_problem
+    from gadmm_amd.data import linear_synthetic
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import gradient_descent, iag, global_constants
+    from gadmm_amd.parallel.comm import RankInfo
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    X, y, loc, pl, obj0 = headline_rank_problem(24, rank, world)
+    s = global_constants(LinearRegression(linear_synthetic(24).X.to(dev), linear_synthetic(24).y.to(dev)))["stepsize"]
+    m = LinearRegression(X.to(dev), y.to(dev))
+    kw = dict(comm=RankInfo(rank, world), placement=pl, backend="native")
+    a = iag(m, loc, 24, 400, obj0, s, "cyclic", None, **kw)
+    eng = m._fo_engine_mr
+    eng.epoch = 0xFFF  # the next run wraps the 12-bit tag salt back to 1
+    b = iag(m, loc, 24, 400, obj0, s, "cyclic", None, **kw)
+    wrapped = eng.epoch
+    c = gradient_descent(m, loc, 24, 400, obj0, s, **kw)
+    eng.close()
+    return {"a": a.obj, "b": b.obj, "c": c.obj, "epoch": wrapped}
+
+
+def test_first_order_epoch_wrap_clears_tables_collectively():
+    """when the first-order engine's 12-bit tag salt wraps, every rank clears its fabric
+    tables and all meet before epoch 1 is reused (a stale IAG ring slot of an earlier epoch-1 run can no
+    longer match); the runs around the wrap are unchanged."""
+    from gadmm_amd.parallel.launch import spawn
+    res = spawn(_fo_wrap_rank, 2, timeout=300)
+    for r in res:
+        assert r["epoch"] == 1
+        assert np.array_equal(r["a"], r["b"])
+    assert np.array_equal(res[0]["c"], res[1]["c"])

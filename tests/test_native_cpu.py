@@ -182,6 +182,12 @@ def test_native_blocked_epoch_tables_match_numpy():
         assert np.array_equal(es.reshape(E, n, 4), np.stack([P, P, lft, rgt], axis=-1))
         assert np.array_equal(pp.reshape(E, n), np.argsort(P, axis=1))
         assert np.array_equal(fl.reshape(E, n, 2), epoch_flush_table(P))
+    # a row that is not a permutation (duplicate id) is refused by both table builders
+    P = np.ascontiguousarray(np.stack([rng.permutation(6), np.array([0, 1, 2, 3, 3, 5])]).astype(np.int64))
+    es, pp, fl = (np.empty((2 * 6 * k,), dtype=np.int32) for k in (4, 1, 2))
+    assert lib.gadmm_epoch_tables_blocked(P.ctypes.data, 2, 6, es.ctypes.data, pp.ctypes.data, fl.ctypes.data) == -2
+    loc = np.arange(6, dtype=np.int64)
+    assert lib.gadmm_epoch_tables(P.ctypes.data, 2, 6, loc.ctypes.data, 6, es.ctypes.data, pp.ctypes.data) == -2
 
 
 def test_quad_pad_image_layout():
@@ -229,3 +235,13 @@ def test_dl_halo_eligibility_and_heads():
         sg = segs(24, world)
         got = sorted(h for lo, hi in sg for h in halo_heads(lo, hi, 24))
         assert len(got) == world - 1 and len(set(got)) == world - 1
+
+
+def test_star_big_abi_layout_matches_ctypes():
+    from gadmm_amd.engine.star_big import StarBigArgs
+    lib = native.require()
+    buf = (ctypes.c_longlong * 8)()
+    k = lib.gadmm_star_big_abi_layout(buf, 8)
+    exp = [ctypes.sizeof(StarBigArgs), StarBigArgs.rho.offset, StarBigArgs.Minv.offset, StarBigArgs.ctl.offset,
+           StarBigArgs.tstamp.offset, StarBigArgs.gid.offset]
+    assert list(buf[:k]) == exp
