@@ -5,6 +5,7 @@
 // so results are deterministic and identical between the kernels that share it.
 #pragma once
 #include "gadmm_common.h"
+#include "sym_gemv.h"
 
 namespace biggemv {
 
@@ -12,8 +13,14 @@ constexpr int NT = 256;
 constexpr int RPW = 2;  // rows per wave
 constexpr int ROWS_PER_WG = RPW * (NT / 64);
 
-// stride of a worker's r-buffer: d entries + one objective partial per workgroup + 1
-__device__ __host__ __forceinline__ long rstride(int d) { return (long)d + (d + ROWS_PER_WG - 1) / ROWS_PER_WG + 1; }
+// A worker's r-buffer (large-d kernels): [ r, zero padded to symv::padded(d) | one objective partial per
+// row-GEMV workgroup + 1 | the symmetric GEMV's partial table P (symv::part_doubles) ]. The padding
+// stays zero (allocated zeroed, only r[0, d) is ever written): the packed GEMV reads whole blocks of r.
+__device__ __host__ __forceinline__ long obj_off(int d) { return symv::padded(d); }
+__device__ __host__ __forceinline__ long part_off(int d) {
+  return (obj_off(d) + (d + ROWS_PER_WG - 1) / ROWS_PER_WG + 1 + 31) / 32 * 32;
+}
+__device__ __host__ __forceinline__ long rstride(int d) { return part_off(d) + symv::part_doubles(d); }
 
 // y[row] = sum_j M[row][j] x[j] for RPW consecutive rows per wave; returns sums on lane 0.
 __device__ __forceinline__ void wave_rows_dot(const double* __restrict__ M, const double* __restrict__ x, int d,

@@ -130,6 +130,31 @@ __device__ __forceinline__ double quad_gemv_lds(const double* Ml, double x, doub
   return quad_reduce(p);
 }
 
+// quad_gemv_lds with one 16-B LDS read in flight per step (a wave that must not grow its VGPR
+// footprint: the hosted halo head of chain_blocked.hip runs next to its tail's register-resident
+// inverse). Every accumulator p[r] sees the same FMAs in the same order: bit-identical.
+template <int T>
+__device__ __forceinline__ double quad_gemv_lds_lean(const double* Ml, double x, double* st) {
+  static_assert(T >= 1 && T <= 16, "quad layout covers d <= 64");
+  const int lane = threadIdx.x & 63, c = lane >> 4;
+  st[(lane & 3) * QX + (lane >> 2)] = x;
+  asm volatile("" ::: "memory");
+  const double* xs = st + c * QX;
+  double p[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll 1
+  for (int t = 0; t < T; t += 2) {
+    const double2 xp = *reinterpret_cast<const double2*>(xs + t);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double2 mv = *reinterpret_cast<const double2*>(Ml + ((t >> 1) * 4 + r) * 128 + 2 * lane);
+      p[r] = fma(mv.x, xp.x, p[r]);
+      if (t + 1 < T) p[r] = fma(mv.y, xp.y, p[r]);
+    }
+  }
+  asm volatile("" ::: "memory");
+  return quad_reduce(p);
+}
+
 // Paired layout for two matrices with <= 52 rows held by one wave (chain_blocked_pair_kernel):
 // each keeps its row groups r = 0..2 (rows i + 16r) as in quad_load, and the two share ONE register
 // block for rows 48..51: lanes with i < 4 hold matrix 0's row 48 + i, lanes with 4 <= i < 8 hold

@@ -2,11 +2,12 @@
 // (BASELINE.json configs[4]). Per worker the cached inverse is 10k x 10k f64 = 800 MB, so one
 // phase is an HBM-streaming GEMV over the whole chip, split into three launches:
 //   chain_big_rhs   r_n = b_n - mu_n + rho th_l + rho th_r      (+ lazy head dual), one thread/elem
-//   chain_big_gemv  th_n = (A_n + deg rho I)^{-1} r_n            one wave per 2 rows, 16-B loads
+//   chain_big_sym_* th_n = (A_n + deg rho I)^{-1} r_n            the inverse stored as its block-packed
+//                   lower triangle (sym_gemv.h: half the bytes of the full matrix), partials + reduce
 //   [chain_big_obj] (A_n th_n)_i -> per-workgroup objective partials   (exact objective mode)
 //   chain_big_post  tail dual update, local objective, last-arriver iteration close
-// Row-per-wave keeps every load of the matrix a contiguous 1-KiB wave access and the reduction
-// inside the wave (no split-K, deterministic). r (80 KB) is re-read from L2 by every wave.
+// Every load of the matrix is a contiguous 1-KiB wave access, every reduction has a fixed order
+// (deterministic). r (80 KB) is re-read from L2 by every workgroup.
 // Objective, exact mode: f = sum_i (1/2 (A th)_i - b_i) th_i + 1/2 y^T y with partials per workgroup
 // summed in a fixed order; identity mode uses A th = r - deg rho th (no second 800 MB pass).
 #include "gadmm_common.h"
@@ -53,21 +54,24 @@ __global__ void __launch_bounds__(NT) chain_big_rhs(PhaseArgs a) {
   a.rbuf[s.li * rstride(a.d) + j] = r;
 }
 
-__global__ void __launch_bounds__(NT) chain_big_gemv(PhaseArgs a) {
+// th_n = M r_n with M the block-packed lower triangle of (A_n + deg rho I)^{-1} (sym_gemv.h): partials
+// of every stored block, then their fixed-order reduction straight into the theta table
+__global__ void __launch_bounds__(symv::NT) chain_big_sym_part(PhaseArgs a) {
+  __shared__ symv::dv2 tl[symv::NT / 64][64];
   if (a.ctl->done) return;
   const SlotView s = slot_view(a, blockIdx.y);
   const int d = a.d;
-  const int row0 = blockIdx.x * ROWS_PER_WG + (threadIdx.x >> 6) * RPW;
-  if (row0 >= d) return;
-  const double* Mi = a.Minv + ((long)s.li * a.nvar + a.deg_to_var[s.deg]) * (long)d * d;
-  const double* r = a.rbuf + s.li * rstride(d);
-  double out[RPW];
-  wave_rows_dot(Mi, r, d, row0, out);
-  if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-    for (int q = 0; q < RPW; ++q)
-      if (row0 + q < d) a.theta[(long)s.gid * d + row0 + q] = out[q];
-  }
+  const double* Mp = a.Minv + ((long)s.li * a.nvar + a.deg_to_var[s.deg]) * symv::packed_doubles(d);
+  double* rb = a.rbuf + s.li * rstride(d);
+  symv::part_block(Mp, rb, rb + part_off(d), symv::nblk(d), blockIdx.x, tl);
+}
+
+__global__ void __launch_bounds__(symv::B) chain_big_sym_reduce(PhaseArgs a) {
+  if (a.ctl->done) return;
+  const SlotView s = slot_view(a, blockIdx.y);
+  const int d = a.d, t = blockIdx.x, k = threadIdx.x;
+  const double y = symv::reduce_elem(a.rbuf + s.li * rstride(d) + part_off(d), symv::nblk(d), t, k);
+  if (t * symv::B + k < d) a.theta[(long)s.gid * d + t * symv::B + k] = y;
 }
 
 // exact objective: per-workgroup partial of sum_i (1/2 (A th)_i - b_i) th_i
@@ -93,7 +97,7 @@ __global__ void __launch_bounds__(NT) chain_big_obj(PhaseArgs a) {
   if (threadIdx.x == 0) {
     double t = 0.0;
     for (int k = 0; k < NT / 64; ++k) t += wsum[k];
-    a.rbuf[s.li * rstride(d) + d + blockIdx.x] = t;
+    a.rbuf[s.li * rstride(d) + obj_off(d) + blockIdx.x] = t;
   }
 }
 
@@ -135,7 +139,7 @@ __global__ void __launch_bounds__(1024) chain_big_post(PhaseArgs a) {
     // deterministic block reduction (same order every call)
     const int nblk = (a.d + ROWS_PER_WG - 1) / ROWS_PER_WG;
     double t = 0.0;
-    for (int k = threadIdx.x; k < nblk; k += blockDim.x) t += r[d + k];
+    for (int k = threadIdx.x; k < nblk; k += blockDim.x) t += r[obj_off(a.d) + k];
     f = block_sum_f64(t, scratch);
   }
   if (threadIdx.x == 0) a.objw[s.li] = f + 0.5 * a.yy[s.li];
@@ -144,9 +148,44 @@ __global__ void __launch_bounds__(1024) chain_big_post(PhaseArgs a) {
   }
 }
 
+// full [count][d][d] -> block-packed lower triangles [count][packed_doubles(d)]; the diagonal blocks'
+// upper halves are mirrored from their lower halves (the stored matrix is exactly symmetric), padding 0
+__global__ void __launch_bounds__(256) sym_pack_kernel(const double* __restrict__ full, double* __restrict__ packed,
+                                                       int d) {
+  int I, J;
+  symv::block_ij(blockIdx.x, I, J);
+  const long m = blockIdx.y;
+  const double* F = full + m * (long)d * d;
+  double* out = packed + m * symv::packed_doubles(d) + (long)blockIdx.x * symv::B * symv::B;
+  for (int e = threadIdx.x; e < symv::B * symv::B; e += blockDim.x) {
+    const int rr = e / symv::B, cc = e % symv::B;
+    int row = I * symv::B + rr, col = J * symv::B + cc;
+    if (I == J && cc > rr) {  // upper half of a diagonal block: its mirror
+      const int t = row;
+      row = col;
+      col = t;
+    }
+    out[e] = (row < d && col < d) ? F[(long)row * d + col] : 0.0;
+  }
+}
+
 extern "C" {
 
-long gadmm_chain_big_rbuf_stride(int d) { return (long)d + (d + ROWS_PER_WG - 1) / ROWS_PER_WG + 1; }
+// Pack `count` full symmetric d x d matrices into the block-packed lower-triangle layout of sym_gemv.h.
+int gadmm_sym_pack_f64(const double* full, double* packed, int count, int d, hipStream_t st) {
+  if (!full || !packed || count < 1 || d < 1) {
+    gadmm_set_error("sym_pack: bad arguments");
+    return -1;
+  }
+  hipLaunchKernelGGL(sym_pack_kernel, dim3((unsigned)symv::nstored(d), count), dim3(256), 0, st, full, packed, d);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+long gadmm_chain_big_rbuf_stride(int d) { return rstride(d); }
+
+// doubles of one block-packed lower-triangle matrix (sym_gemv.h)
+long gadmm_sym_packed_doubles(int d) { return symv::packed_doubles(d); }
 
 int gadmm_chain_phase_big(const PhaseArgs* args, hipStream_t st) {
   const PhaseArgs& a = *args;
@@ -158,7 +197,8 @@ int gadmm_chain_phase_big(const PhaseArgs* args, hipStream_t st) {
   const int d = a.d;
   hipLaunchKernelGGL(chain_big_rhs, dim3((d + NT - 1) / NT, a.n_slots), dim3(NT), 0, st, a);
   const int nblk = (d + ROWS_PER_WG - 1) / ROWS_PER_WG;
-  hipLaunchKernelGGL(chain_big_gemv, dim3(nblk, a.n_slots), dim3(NT), 0, st, a);
+  hipLaunchKernelGGL(chain_big_sym_part, dim3((unsigned)symv::nstored(d), a.n_slots), dim3(symv::NT), 0, st, a);
+  hipLaunchKernelGGL(chain_big_sym_reduce, dim3(symv::nblk(d), a.n_slots), dim3(symv::B), 0, st, a);
   if (a.obj_mode == 0 && (a.flags & PH_OBJ))
     hipLaunchKernelGGL(chain_big_obj, dim3(nblk, a.n_slots), dim3(NT), 0, st, a);
   hipLaunchKernelGGL(chain_big_post, dim3(a.n_slots), dim3(1024), 0, st, a);

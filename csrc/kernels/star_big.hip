@@ -8,11 +8,11 @@
 // round trip per block, not per iteration. Per iteration (N workers, the hub = worker N - 1 also
 // owns a shard):
 //   sb_rhs    (non-hub local workers)  r_i = b_i - lam_i + rho th_hub                        (:42)
-//   sb_gemv   th_i = (A_i + rho I)^{-1} r_i           [row-per-wave streaming, big_gemv.h]
+//   sb_sym_*  th_i = (A_i + rho I)^{-1} r_i           [packed lower triangle, sym_gemv.h]
 //   sb_sum    agg = [sum_i lam_i, sum_i th_i] over this rank's non-hub workers (worker order)
 //   -- reduce(agg) to the hub rank (RCCL ncclReduce; nothing on one rank)                  (:66-71)
 //   sb_hubrhs r_h = b_h + agg_lam + rho agg_th                                            (:73)
-//   sb_gemv   th_hub = (A_h + (N-1) rho I)^{-1} r_h   (hub rank)
+//   sb_sym_*  th_hub = (A_h + (N-1) rho I)^{-1} r_h   (hub rank)
 //   -- broadcast(th_hub) from the hub rank (RCCL ncclBroadcast)
 //   sb_post   lam_i += rho (th_i - th_hub), f_i(th_i), f_h(th_hub)                        (:84-88)
 //   -- allreduce(objp) (RCCL or the IPC device collective; nothing on one rank): objp holds one
@@ -31,7 +31,8 @@ struct StarBigArgs {
   int d, n_total, n_local, hub_li;  // hub_li: local index of the hub (-1: the hub is on another rank)
   int max_iter, obj_mode, pad0, pad1;
   double rho, obj0, tol;
-  const double* Minv;  // [n_local][d][d]: (A_i + rho I)^-1, the hub's (A_h + (N-1) rho I)^-1
+  const double* Minv;  // [n_local][packed_doubles(d)]: block-packed lower triangles (sym_gemv.h) of
+                       // (A_i + rho I)^-1, the hub's (A_h + (N-1) rho I)^-1
   const double* A;     // [n_local][d][d] (exact objective mode)
   const double* b;     // [n_local][d]
   const double* yy;    // [n_local]
@@ -60,23 +61,27 @@ __global__ void __launch_bounds__(NT) sb_rhs(StarBigArgs a) {
   a.rbuf[s * rstride(a.d) + j] = a.b[s * d + j] - a.lam[s * d + j] + a.rho * a.th_hub[j];
 }
 
-// theta_s = Minv_s r_s for the local workers s with (s == hub_li) == hub (one wave per RPW rows)
-__global__ void __launch_bounds__(NT) sb_gemv(StarBigArgs a, int hub) {
+// theta_s = Minv_s r_s for the local workers s with (s == hub_li) == hub: Minv_s block-packed lower
+// triangles (sym_gemv.h), partials of every stored block, then the fixed-order reduction
+__global__ void __launch_bounds__(symv::NT) sb_sym_part(StarBigArgs a, int hub) {
+  __shared__ symv::dv2 tl[symv::NT / 64][64];
   if (a.ctl->done) return;
   const int s = blockIdx.y;
   if ((s == a.hub_li) != (hub != 0)) return;
   const int d = a.d;
-  const int row0 = blockIdx.x * ROWS_PER_WG + (threadIdx.x >> 6) * RPW;
-  if (row0 >= d) return;
-  double out[RPW];
-  wave_rows_dot(a.Minv + (long)s * d * d, a.rbuf + s * rstride(d), d, row0, out);
-  if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-    for (int q = 0; q < RPW; ++q)
-      if (row0 + q < d) {
-        a.theta[(long)s * d + row0 + q] = out[q];
-        if (hub) a.th_hub[row0 + q] = out[q];
-      }
+  double* rb = a.rbuf + s * rstride(d);
+  symv::part_block(a.Minv + (long)s * symv::packed_doubles(d), rb, rb + part_off(d), symv::nblk(d), blockIdx.x, tl);
+}
+
+__global__ void __launch_bounds__(symv::B) sb_sym_reduce(StarBigArgs a, int hub) {
+  if (a.ctl->done) return;
+  const int s = blockIdx.y;
+  if ((s == a.hub_li) != (hub != 0)) return;
+  const int d = a.d, t = blockIdx.x, k = threadIdx.x, j = t * symv::B + k;
+  const double y = symv::reduce_elem(a.rbuf + s * rstride(d) + part_off(d), symv::nblk(d), t, k);
+  if (j < d) {
+    a.theta[(long)s * d + j] = y;
+    if (hub) a.th_hub[j] = y;
   }
 }
 
@@ -127,7 +132,7 @@ __global__ void __launch_bounds__(NT) sb_obj(StarBigArgs a) {
   if (threadIdx.x == 0) {
     double t = 0.0;
     for (int k = 0; k < NT / 64; ++k) t += wsum[k];
-    a.rbuf[s * rstride(d) + d + blockIdx.x] = t;
+    a.rbuf[s * rstride(d) + obj_off(d) + blockIdx.x] = t;
   }
 }
 
@@ -152,7 +157,7 @@ __global__ void __launch_bounds__(1024) sb_post(StarBigArgs a) {
   } else {
     const int nblk = (a.d + ROWS_PER_WG - 1) / ROWS_PER_WG;
     double t = 0.0;
-    for (int k = threadIdx.x; k < nblk; k += blockDim.x) t += r[d + k];
+    for (int k = threadIdx.x; k < nblk; k += blockDim.x) t += r[obj_off(a.d) + k];
     f = block_sum_f64(t, scratch);
   }
   if (threadIdx.x == 0) a.objw[s] = f + 0.5 * a.yy[s];
@@ -216,8 +221,10 @@ int gadmm_star_big_workers(const StarBigArgs* args, hipStream_t st) {
     return -1;
   }
   const int d = a.d, nb = (d + NT - 1) / NT, nblk = (d + ROWS_PER_WG - 1) / ROWS_PER_WG;
+  (void)nblk;
   hipLaunchKernelGGL(sb_rhs, dim3(nb, a.n_local), dim3(NT), 0, st, a);
-  hipLaunchKernelGGL(sb_gemv, dim3(nblk, a.n_local), dim3(NT), 0, st, a, 0);
+  hipLaunchKernelGGL(sb_sym_part, dim3((unsigned)symv::nstored(d), a.n_local), dim3(symv::NT), 0, st, a, 0);
+  hipLaunchKernelGGL(sb_sym_reduce, dim3(symv::nblk(d), a.n_local), dim3(symv::B), 0, st, a, 0);
   hipLaunchKernelGGL(sb_sum, dim3(nb), dim3(NT), 0, st, a);
   GADMM_CHECK(hipGetLastError());
   return 0;
@@ -228,8 +235,10 @@ int gadmm_star_big_hub(const StarBigArgs* args, hipStream_t st) {
   const StarBigArgs& a = *args;
   if (a.hub_li < 0) return 0;
   const int d = a.d, nb = (d + NT - 1) / NT, nblk = (d + ROWS_PER_WG - 1) / ROWS_PER_WG;
+  (void)nblk;
   hipLaunchKernelGGL(sb_hubrhs, dim3(nb), dim3(NT), 0, st, a);
-  hipLaunchKernelGGL(sb_gemv, dim3(nblk, a.n_local), dim3(NT), 0, st, a, 1);
+  hipLaunchKernelGGL(sb_sym_part, dim3((unsigned)symv::nstored(d), a.n_local), dim3(symv::NT), 0, st, a, 1);
+  hipLaunchKernelGGL(sb_sym_reduce, dim3(symv::nblk(d), a.n_local), dim3(symv::B), 0, st, a, 1);
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

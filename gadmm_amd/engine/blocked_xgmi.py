@@ -49,10 +49,16 @@ def halo_heads(lo: int, hi: int, n: int) -> list:
 
 def dl_halo_eligible(segs, n: int, d: int) -> bool:
     """Whether the data-local halo mode can run on every rank: more than one rank, every segment >= 2
-    positions, and segment + its halo heads within one 12-wave workgroup everywhere (24 workers: 4 and
-    8 ranks yes, 2 ranks no -- 13 waves)."""
+    positions and within one 12-wave workgroup. A halo head that does not fit a wave of its own (24
+    workers on 2 ranks: 12 + 1) is hosted by its boundary tail (chain_blocked.hip: the tail computes it
+    in the head phase, from the head's inverse in LDS)."""
     return (len(segs) > 1 and d <= 52 and all(hi - lo + 1 >= 2 for lo, hi in segs)
-            and all(hi - lo + 1 + len(halo_heads(lo, hi, n)) <= MAXW for lo, hi in segs))
+            and all(hi - lo + 1 <= MAXW for lo, hi in segs))
+
+
+def dl_halo_hosted(lo: int, hi: int, n: int) -> bool:
+    """Whether the segment [lo, hi] runs its halo heads hosted (segment + halo heads > 12 waves)."""
+    return hi - lo + 1 + len(halo_heads(lo, hi, n)) > MAXW
 
 
 class BlockedXgmiEngine:
@@ -68,8 +74,9 @@ class BlockedXgmiEngine:
         positions and fits one workgroup): the one-position halo mode -- at each rank boundary whose near
         side is a tail, this rank also holds the other rank's boundary head's shard (fetched once here
         from its owner) and solves it on one more wave, so only one cross-rank hop per iteration is on
-        the critical cycle (chain_blocked.hip, PersistArgs::dl_halo). Needs segment + halo heads <= 12
-        waves on every rank: 4 and 8 ranks at 24 workers, not 2."""
+        the critical cycle (chain_blocked.hip, PersistArgs::dl_halo). Needs every segment within one
+        12-wave workgroup; a halo head beyond the 12 waves (2 ranks at 24 workers) is hosted by the
+        boundary tail next to it."""
         self.lib = native.require()
         self.rank, self.nranks, self.device = rank, placement.nranks, device
         self.n, self.d = int(n_total), int(X_all.shape[2])
@@ -205,9 +212,10 @@ class BlockedXgmiEngine:
         self.epoch = 0
         if self.data_local:
             W = (self.seg_hi - self.seg_lo + self.L) // self.L
+            hosted = self._halo_mode() and dl_halo_hosted(self.seg_lo, self.seg_hi, self.n)
             self.last_kernel = "blocked-dl%s(k=%s,L=%d,W=%d,nbr=%s)" % (
-                ("-halo%s" % self.halo) if self._halo_mode() else "", "inf" if W == 1 else self.k, self.L, W,
-                self.dl_ranks)
+                ("-halo%s%s" % (self.halo, "-hosted" if hosted else "")) if self._halo_mode() else "",
+                "inf" if W == 1 else self.k, self.L, W, self.dl_ranks)
         else:
             self.last_kernel = "blocked-xgmi(k=%d,L=%d,H=%d,pw=%d,peers=%s)" % (self.k, self.L, H, self.pw,
                                                                                 self.peers)

@@ -24,7 +24,7 @@ import torch
 
 from ..ops import native
 from ..utils import timing as _timing
-from ..ops.linalg import gram, spd_inverse
+from ..ops.linalg import gram, spd_inverse, sym_pack
 from ..parallel.topology import Placement, chain_plan, RankPlan
 
 
@@ -233,7 +233,7 @@ class NativeChainEngine:
         for i, v in enumerate(self.deg_to_var if model == "linear" else (0, 0, 0)):
             args.deg_to_var[i] = v
         args.model = native.MODEL_LINEAR if model == "linear" else native.MODEL_LOGISTIC
-        args.Minv = native.ptr(self.Minv if self.hinv is None else self.hinv)
+        args.Minv = native.ptr(self.hinv if self.hinv is not None else self._kernel_minv())
         args.A = native.ptr(self.A)
         args.b = native.ptr(self.b)
         args.yy = native.ptr(self.yy)
@@ -303,6 +303,14 @@ class NativeChainEngine:
             spd_inverse(self.A, self._shifts, out=self.Minv, check_status=check, status=st)
         else:
             self.Minv = spd_inverse(self.A, self._shifts, check_status=check, status=st)
+        if self.d > 256:
+            # the large-d phases (chain_big.hip) stream the block-packed lower triangles: half the bytes
+            self.Mpk = sym_pack(self.Minv, out=self.Mpk if in_place and getattr(self, "Mpk", None) is not None
+                                else None)
+
+    def _kernel_minv(self):
+        """The inverses as the phase kernels read them: block-packed lower triangles at d > 256."""
+        return getattr(self, "Mpk", None) if self.d > 256 else self.Minv
 
     def refresh(self, X_loc: torch.Tensor, y_loc: torch.Tensor):
         """Recompute the loop-invariant set-up (Gram + cached inverses) from the raw shards, in place
@@ -321,7 +329,7 @@ class NativeChainEngine:
         if self.model == "linear":
             with torch.cuda.stream(self.stream):
                 self._build_inverses()
-            self._desc.base.Minv = self.Minv.data_ptr()
+            self._desc.base.Minv = self._kernel_minv().data_ptr()
         self._desc.base.rho = self.rho
         self._recreate()
 

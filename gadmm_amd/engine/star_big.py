@@ -25,7 +25,7 @@ import numpy as np
 import torch
 
 from ..ops import native
-from ..ops.linalg import spd_inverse
+from ..ops.linalg import spd_inverse, sym_pack
 
 
 class StarBigArgs(ctypes.Structure):
@@ -74,7 +74,9 @@ class StarBigEngine:
             shifts = torch.tensor([[(self.n - 1) * self.rho if w == self.hub else self.rho] for w in self.local],
                                   dtype=f64, device=dev)
             t0 = time.perf_counter()
-            self.Minv = spd_inverse(model.A, shifts)  # (nl, 1, d, d): K2 on the device
+            full = spd_inverse(model.A, shifts)  # (nl, 1, d, d): K2 on the device
+            self.Minv = sym_pack(full)  # (nl, packed): the block-packed lower triangles the kernels stream
+            del full
             self.stream.synchronize()
             self.setup_s = time.perf_counter() - t0
             self.theta = torch.zeros((nl, d), dtype=f64, device=dev)

@@ -128,6 +128,36 @@ def spd_inverse_blocked(A: torch.Tensor, shifts: torch.Tensor, out: Optional[tor
     return out
 
 
+def sym_pack(M: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Block-packed lower triangles (csrc/include/sym_gemv.h) of the symmetric matrices ``M`` (..., d, d):
+    returns (count, packed_doubles(d)) f64 on M's device (the large-d kernels' cached inverses: half
+    the bytes an iteration streams)."""
+    lib = native.require()
+    d = int(M.shape[-1])
+    cnt = int(M.numel() // (d * d))
+    n = int(lib.gadmm_sym_packed_doubles(d))
+    if out is None:
+        out = torch.empty((cnt, n), dtype=torch.float64, device=M.device)
+    Mc = M.contiguous()
+    native.check(lib.gadmm_sym_pack_f64(Mc.data_ptr(), out.data_ptr(), cnt, d, native.stream_handle()), "sym_pack")
+    return out
+
+
+def sym_unpack_torch(P: torch.Tensor, d: int, B: int = 128) -> torch.Tensor:
+    """The full symmetric matrices of block-packed lower triangles (reference / tests)."""
+    nb = (d + B - 1) // B
+    out = torch.zeros((P.shape[0], nb * B, nb * B), dtype=P.dtype, device=P.device)
+    b = 0
+    for i in range(nb):
+        for j in range(i + 1):
+            blk = P[:, b * B * B:(b + 1) * B * B].reshape(-1, B, B)
+            out[:, i * B:(i + 1) * B, j * B:(j + 1) * B] = blk
+            if i != j:
+                out[:, j * B:(j + 1) * B, i * B:(i + 1) * B] = blk.transpose(1, 2)
+            b += 1
+    return out[:, :d, :d]
+
+
 def gemm_f64(A: torch.Tensor, B: torch.Tensor) -> torch.Tensor:
     """``A @ B`` (row-major f64) with the MFMA tile kernel of the blocked inverse (tests)."""
     lib = native.require()

@@ -196,6 +196,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_star_launch": (c_int, [ctypes.POINTER(StarArgs), c_void_p]),
         "gadmm_star_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
         "gadmm_star_big_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
+        "gadmm_sym_pack_f64": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p]),
+        "gadmm_sym_packed_doubles": (c_long, [c_int]),
         "gadmm_ipc_box_bytes": (c_long, [c_int, c_int, c_int, c_int]),
         "gadmm_ipc_collective": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_int, ctypes.c_uint, c_void_p,
                                          c_void_p]),

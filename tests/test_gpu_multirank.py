@@ -279,7 +279,7 @@ def test_data_local_xgmi_default_exact_bytes(world, n, engine, lin24):
     inside every rank's segment, edge workers exchanging theta every phase -- in the one-position halo
     mode when every segment has >= 2 workers and fits one workgroup with its halo heads (the rank
     holding a boundary tail also solves the other rank's boundary head, whose shard it holds: one per
-    boundary), plain data-local otherwise (n = 24 on 2 ranks: 13 waves; n = 8 on 8 ranks) or with
+    boundary; n = 24 on 2 ranks: hosted by the boundary tail), plain data-local otherwise (n = 8 on 8 ranks) or with
     GADMM_DL_HALO=0 (nohalo); per-worker = the one-workgroup-per-worker kernel.
     Payload == 2 (N_ranks - 1) d 8 iters exactly in every mode; wire == 2 x payload (16-B granules);
     iterations and trace == one GPU, bit for bit. n = 8 on 8 ranks: each GPU is one worker (both of its
@@ -288,10 +288,10 @@ def test_data_local_xgmi_default_exact_bytes(world, n, engine, lin24):
     from gadmm_amd.benchmarks import EXPECTED_ITERS_1E8
     res = spawn(_solver_rank, world, n, -1, 20.0, engine, timeout=300)
     it = EXPECTED_ITERS_1E8[(n, 3.0)]
-    # the halo mode needs every segment >= 2 workers and segment + halo heads <= 12 waves on every rank
+    # the halo mode needs every segment >= 2 workers within one 12-wave workgroup (a 13th position, the
+    # halo head at 2 ranks x 12 workers, is hosted by its boundary tail)
     segs = [(r * n // world, (r + 1) * n // world - 1) for r in range(world)]
-    span = [hi - lo + 1 + int(lo > 0 and lo % 2 == 1) + int(hi < n - 1 and hi % 2 == 1) for lo, hi in segs]
-    halo = engine == "auto" and all(hi > lo for lo, hi in segs) and max(span) <= 12
+    halo = engine == "auto" and all(hi > lo for lo, hi in segs) and max(hi - lo + 1 for lo, hi in segs) <= 12
     want = "xgmi(blocked-dl-halo)" if halo else ("xgmi(blocked-dl)" if engine in ("auto", "nohalo") else "xgmi")
     for r in res:
         assert r["kind0"] == want and r["kind"] == want and not r["fallbacks"], (r["kind0"], r["fallbacks"])
@@ -644,8 +644,8 @@ def _bench_json(world, extra_env, *args, timeout=400):
 @pytest.mark.parametrize("world", [2, 4])
 def test_bench_tournament_and_hop_probe(world):
     """The 2 / 4-rank headline: a one-way hop per chain boundary, every candidate engine timed in the
-    warm-up (the halo mode only where it fits), the winner is the fastest agreed candidate and runs
-    the timed loop at the reference iteration count."""
+    warm-up (the halo mode hosted at 2 ranks), the winner is the fastest agreed candidate and runs the
+    timed loop at the reference iteration count."""
     out, _ = _bench_json(world, {}, "--steps", "5", "--warmup", "2")
     assert out["iterations_to_tol"] == 1373 and out["iterations_match_reference"]
     hops = out["xgmi_hop_us"]
@@ -655,7 +655,7 @@ def test_bench_tournament_and_hop_probe(world):
     assert set(rows) == {"blocked-dl-halo", "blocked-dl", "per-worker", "replicated-halo"}
     ok = {k: r["ms"] for k, r in rows.items() if r["ok"]}
     assert "blocked-dl" in ok and "per-worker" in ok and "replicated-halo" in ok
-    assert ("blocked-dl-halo" in ok) == (world == 4)  # 2 ranks: segment + halo head = 13 waves > 12
+    assert "blocked-dl-halo" in ok  # 2 ranks: the 13th position (halo head) hosted by the boundary tail
     assert out["fallbacks"] == [] and out["timing_restarts"] == 0
     best = min(ok, key=ok.get)
     want = {"blocked-dl-halo": "xgmi(blocked-dl-halo)", "blocked-dl": "xgmi(blocked-dl)", "per-worker": "xgmi",
