@@ -216,12 +216,15 @@ def test_dl_halo_eligibility_and_heads():
     """The data-local halo mode's plan (engine/blocked_xgmi.py): which boundary heads each rank solves
     and when the mode fits the 12-wave workgroup on every rank (must agree with chain_blocked.hip's
     range hl / hr and the launcher's span check)."""
-    from gadmm_amd.engine.blocked_xgmi import dl_halo_eligible, halo_heads
+    from gadmm_amd.engine.blocked_xgmi import dl_halo_eligible, dl_halo_hosted, halo_heads
 
     def segs(n, world):
         return [(r * n // world, (r + 1) * n // world - 1) for r in range(world)]
 
-    assert not dl_halo_eligible(segs(24, 2), 24, 50)       # rank 0: 12 positions + head 12 = 13 waves
+    # rank 0: 12 positions + head 12 = 13 waves: the head is hosted by tail 11 (round 4)
+    assert dl_halo_eligible(segs(24, 2), 24, 50)
+    assert dl_halo_hosted(0, 11, 24) and not dl_halo_hosted(12, 23, 24) and not dl_halo_hosted(6, 11, 24)
+    assert not dl_halo_eligible([(0, 12), (13, 23)], 24, 50)  # a 13-position segment never fits
     assert dl_halo_eligible(segs(24, 4), 24, 50)
     assert dl_halo_eligible(segs(24, 8), 24, 50)
     assert not dl_halo_eligible(segs(8, 8), 8, 50)         # one-position segments
