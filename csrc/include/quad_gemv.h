@@ -130,29 +130,27 @@ __device__ __forceinline__ double quad_gemv_lds(const double* Ml, double x, doub
   return quad_reduce(p);
 }
 
-// quad_gemv_lds with one 16-B LDS read in flight per step (a wave that must not grow its VGPR
-// footprint: the hosted halo head of chain_blocked.hip runs next to its tail's register-resident
-// inverse). Every accumulator p[r] sees the same FMAs in the same order: bit-identical.
+// One row group r of quad_gemv_lds (rows i + 16 r): lane (i, c)'s partial p[r] -- the accumulator
+// quad_gemv keeps for that group, same FMAs in the same order. Four waves running r = 0..3 and a
+// quad_reduce of their four partials (in lane order) give quad_gemv's result bit for bit; each wave
+// reads a quarter of the image (chain_blocked.hip: the hosted halo head).
 template <int T>
-__device__ __forceinline__ double quad_gemv_lds_lean(const double* Ml, double x, double* st) {
+__device__ __forceinline__ double quad_rowgroup_lds(const double* Ml, int r, double x, double* st) {
   static_assert(T >= 1 && T <= 16, "quad layout covers d <= 64");
   const int lane = threadIdx.x & 63, c = lane >> 4;
   st[(lane & 3) * QX + (lane >> 2)] = x;
   asm volatile("" ::: "memory");
   const double* xs = st + c * QX;
-  double p[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll 1
+  double p = 0.0;
+#pragma unroll
   for (int t = 0; t < T; t += 2) {
     const double2 xp = *reinterpret_cast<const double2*>(xs + t);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const double2 mv = *reinterpret_cast<const double2*>(Ml + ((t >> 1) * 4 + r) * 128 + 2 * lane);
-      p[r] = fma(mv.x, xp.x, p[r]);
-      if (t + 1 < T) p[r] = fma(mv.y, xp.y, p[r]);
-    }
+    const double2 mv = *reinterpret_cast<const double2*>(Ml + ((t >> 1) * 4 + r) * 128 + 2 * lane);
+    p = fma(mv.x, xp.x, p);
+    if (t + 1 < T) p = fma(mv.y, xp.y, p);
   }
-  asm volatile("" ::: "memory");
-  return quad_reduce(p);
+  asm volatile("" ::: "memory");  // the next call's x store stays behind this call's x reads
+  return p;
 }
 
 // Paired layout for two matrices with <= 52 rows held by one wave (chain_blocked_pair_kernel):

@@ -35,7 +35,7 @@
 namespace {
 
 constexpr int MAXW = 12;  // computed workers (waves) per workgroup: 3 waves per SIMD -> <= 170 VGPRs
-// one quad_store_lds image at DB = 52 (T = 13): a hosted halo head's inverse in LDS (HALO)
+// one quad_store_lds image at DB = 52 (T = 13): the hosted halo head's inverse in LDS (HALO)
 constexpr int HIMG52 = 4 * 64 * 14;
 // DYN: epochs per launch whose tables are staged in LDS at the kernel start (epoch starts, and per
 // computed / objective position its slot and flush pair), so a re-chain reads them in ~0.1 us
@@ -273,11 +273,17 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   // HALO: the range also takes the other rank's boundary head next to a boundary tail of this rank
   // (see dlh below): one more wave on that side
   const int hl = HALO && dl && seg_lo > 0 && (seg_lo % 2) == 1, hr = HALO && dl && seg_hi < n - 1 && (seg_hi % 2) == 1;
-  // Hosted halo heads: when the segment and its halo heads exceed MAXW waves (2 ranks x 12 workers:
-  // 13), the waves stay the segment's own and the boundary TAIL next to each halo head also computes
-  // that head -- in the head phase, where a tail idles -- from the head's inverse in LDS
-  // (quad_gemv_lds: the register GEMV's FMA order, so bit-identical to the head's owner)
+  // Hosted halo head: when the segment and its halo head exceed MAXW waves (2 ranks x 12 workers: 13),
+  // the waves stay the segment's own and the halo head h is computed by the segment's TAIL waves in
+  // the head phase, where tails idle: h's inverse sits in LDS as a quad image, four tail waves (one
+  // per SIMD) each run one of its four row groups (13 FMAs after 7 + 7 LDS reads, in parallel), and
+  // the boundary tail next to h folds the four partials with quad_reduce at the start of its tail
+  // phase -- the register GEMV's FMA and reduction order, so h's theta is bit-identical to its
+  // owner's. (Round 3's single-wave LDS GEMV put ~1 us on the head phase.) One hosted side per
+  // segment (the launcher checks it).
   const bool hosted = HALO && dl && (seg_hi - seg_lo + 1 + hl + hr > MAXW);
+  const int hd = hosted ? (hr ? 1 : -1) : 0;                   // side of the hosted head
+  const int hp = hd > 0 ? seg_hi + 1 : (hd < 0 ? seg_lo - 1 : 0);  // its chain position
   const int ra = max(dl ? seg_lo - (hosted ? 0 : hl) : 0, s0 - H), rb = min(dl ? seg_hi + (hosted ? 0 : hr) : n - 1, e0 + H);
   const int nv = rb - ra + 1;
   // Wave v computes local position u. Waves are dealt to the 4 SIMDs round-robin (v mod 4), so
@@ -326,8 +332,10 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   // pushes its own theta^j into the neighbour rank's ring the same way (no mu, no shard crosses).
   // (p == seg_lo implies u == 0 and p == seg_hi implies u == nv - 1, so nbl / nbr are false there.)
   // (the range edges: ra / rb; p == ra implies u == 0 and p == rb implies u == nv - 1)
-  // hosted mode: this wave (a boundary tail) also computes the halo head h = p + hdir
-  const int hdir = (hosted && active && hr && p == seg_hi) ? 1 : ((hosted && active && hl && p == seg_lo) ? -1 : 0);
+  // hosted mode: hdir != 0 on the boundary tail next to the hosted head (h = p + hdir); hq = 0..3 on the
+  // four tail waves (v = MAXW/2 .. MAXW/2 + 3: one per SIMD) that run h's row groups
+  const int hdir = (hosted && active && p == hp - hd) ? hd : 0;
+  const int hq = (hosted && v >= MAXW / 2 && v < MAXW / 2 + 4) ? v - MAXW / 2 : -1;
   const bool rl = dl && has_l && p == ra && hdir != -1, rr = dl && has_r && p == rb && hdir != 1;
   // Halo mode (HALO, PersistArgs::dl_halo; one workgroup per segment, every segment >= 2 positions,
   // segment + halo within MAXW waves): at a rank boundary whose near side is a TAIL t, this rank also
@@ -371,22 +379,23 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   double mu = (active && in) ? a.mu[(long)li * d + lane] : 0.0;
   double bb = (active && in) ? a.b[(long)li * d + lane] : 0.0;
   thS[u * 64 + lane] = th;
-  // hosted halo head (HALO): its inverse as a quad image in LDS (after thS and the staging area), its
-  // state in registers; hsl / hsr: the head has a left / right neighbour
-  // (theta, mu, b of the head live in LDS too, hst[0 / 64 / 128 + lane]: no VGPRs for a state that
-  // only the host wave touches, twice per iteration)
-  double* Mh = lds + MAXW * 64 + MAXW * QSTAGE + (hdir > 0 ? HIMG52 : 0);
-  double* hst = lds + MAXW * 64 + MAXW * QSTAGE + 2 * HIMG52 + (hdir > 0 ? 192 : 0);
+  // hosted halo head (HALO): its inverse as a quad image in LDS (after thS and the staging area) and its
+  // state in LDS: hst = [theta 64 | mu, two iteration-parity buffers 2 x 64 | b 64 | row-group partials
+  // 4 x 64]; hsl / hsr: the head has a left / right neighbour (uniform)
+  double* Mh = lds + MAXW * 64 + MAXW * QSTAGE;
+  double* hst = Mh + HIMG52;
   bool hsl = false, hsr = false;
-  if (HALO && hdir != 0) {
-    const PhaseSlot sh = a.slots[p + hdir];
+  if (HALO && hosted) {
+    const PhaseSlot sh = a.slots[hp];
     hsl = sh.left >= 0;
     hsr = sh.right >= 0;
-    const int deg_h = (int)hsl + (int)hsr;
-    quad_store_lds<QT>(Mh, a.Minv + ((long)sh.li * a.nvar + a.deg_to_var[deg_h]) * (long)d * d, d, true);
-    hst[lane] = in ? a.theta[(long)sh.gid * d + lane] : 0.0;
-    hst[64 + lane] = in ? a.mu[(long)sh.li * d + lane] : 0.0;
-    hst[128 + lane] = in ? a.b[(long)sh.li * d + lane] : 0.0;
+    if (hdir != 0) {  // the boundary tail stages h's inverse and state once
+      const int deg_h = (int)hsl + (int)hsr;
+      quad_store_lds<QT>(Mh, a.Minv + ((long)sh.li * a.nvar + a.deg_to_var[deg_h]) * (long)d * d, d, true);
+      hst[lane] = in ? a.theta[(long)sh.gid * d + lane] : 0.0;
+      hst[64 + (a.start_iter & 1) * 64 + lane] = in ? a.mu[(long)sh.li * d + lane] : 0.0;
+      hst[192 + lane] = in ? a.b[(long)sh.li * d + lane] : 0.0;
+    }
   }
   int pending = a.pending_in;
   // DYN: epoch cursor, regular exchange schedule (restarts after every re-chain) and its slot
@@ -453,7 +462,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   auto poll_far = [&](int slot, int j, double& tf) -> bool {
     const unsigned tag = make_tag(a.epoch, j);
     // ring row of the far neighbour (another rank's tail, pushed after its tail phase)
-    const int so = slot * ring_slot_bytes + (int)((ring_base + (long)(p + 2 * hdir) * d + lane) * 16);
+    const int so = slot * ring_slot_bytes + (int)((ring_base + (long)(hp + hd) * d + lane) * 16);
     for (int spin = 0;; ++spin) {
       const bool g0 = !in || load_granule<SYS>(rtab, so, tag, &tf);
       if (__all(g0)) return true;
@@ -610,28 +619,28 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
       if (rpush && in) push_remote(rslot, it);  // first: the other rank's tail waits on it
       thS[u * 64 + lane] = th;
     }
-    if (HALO && hdir != 0) {  // hosted halo head h = p + hdir: the head's solve of iteration it
+    if (HALO && hq >= 0) {  // hosted halo head h: row group hq of its solve of iteration it
       double tf = 0.0;  // the far neighbour's theta^{it-1} (its initial theta at the first iteration)
-      if (hdir > 0 ? hsr : hsl) {
+      if (hd > 0 ? hsr : hsl) {
         if (it == a.start_iter) {
-          if (in) tf = a.theta[(long)(p + 2 * hdir) * d + lane];
+          if (in) tf = a.theta[(long)(hp + hd) * d + lane];
         } else if (!poll_far(rslot == 0 ? a.ring - 1 : rslot - 1, it - 1, tf) && lane == 0) {
           abort_lds = 1;
         }
       }
-      const double tl = hdir > 0 ? th : tf, tr = hdir > 0 ? tf : th;  // th: this tail's theta^{it-1}
+      const double tn = thS[(hp - hd - ra) * 64 + lane];  // the boundary tail's theta^{it-1}
+      const double tl = hd > 0 ? tn : tf, tr = hd > 0 ? tf : tn;
       const double th_h = hst[lane];
-      double m = hst[64 + lane];
+      double m = hst[64 + (it & 1) * 64 + lane];
       if (pending) {  // lazy end-of-iteration dual (reference order)
         if (hsl) m = m - rho * (tl - th_h);
         if (hsr) m = m + rho * (th_h - tr);
       }
-      hst[64 + lane] = m;
-      double r = hst[128 + lane] - m;
+      if (hq == 0) hst[64 + ((it + 1) & 1) * 64 + lane] = m;  // parity buffers: no reader races the write
+      double r = hst[192 + lane] - m;
       if (hsl) r = r + rho * tl;
       if (hsr) r = r + rho * tr;
-      const double y = quad_gemv_lds_lean<QT>(Mh, in ? r : 0.0, myx);
-      hst[lane] = in ? y : 0.0;
+      hst[256 + hq * 64 + lane] = quad_rowgroup_lds<QT>(Mh, hq, in ? r : 0.0, myx);
     }
     pending = 1;
     lds_barrier();
@@ -647,8 +656,14 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
     if (active && !head && u >= uo_lo - (slack - 1) && u <= uo_hi + (slack - 1)) {
       if (tstamp) tt[0] = (long long)now_ticks();
       double tl = nbl ? thL[lane] : 0.0, tr = nbr ? thR[lane] : 0.0;
-      if (HALO && hdir > 0) tr = hst[lane];  // the hosted halo head's theta^it (this wave, head phase)
-      if (HALO && hdir < 0) tl = hst[lane];
+      if (HALO && hdir != 0) {  // the hosted halo head's theta^it: fold the four row-group partials
+        double pq[4] = {hst[256 + lane], hst[320 + lane], hst[384 + lane], hst[448 + lane]};
+        const double y = quad_reduce(pq);
+        const double th_h = in ? y : 0.0;
+        hst[lane] = th_h;  // read by the next head phase (after this phase's barrier)
+        if (hdir > 0) tr = th_h;
+        else tl = th_h;
+      }
       if ((rl || rr) && !poll_remote(rslot, it, tl, tr) && lane == 0) abort_lds = 1;  // other ranks' heads' theta^it
       double r = bb - mu;
       if (has_l) r = r + rho * tl;
@@ -1123,9 +1138,13 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
     const int nseg_dl = a.seg_hi - a.seg_lo + 1;
     const int W_dl = nseg_dl > 0 && a.blk_len > 0 ? (nseg_dl + a.blk_len - 1) / a.blk_len : 0;
     const int nhalo = a.dl_halo ? (int)(a.seg_lo > 0 && a.seg_lo % 2 == 1) + (int)(a.seg_hi < a.n - 1 && a.seg_hi % 2 == 1) : 0;
-    // one workgroup: segment + halo heads (a halo head beyond MAXW is hosted by its boundary tail)
-    const long span = W_dl == 1 ? (a.dl_halo ? nseg_dl : nseg_dl + nhalo) : (long)a.blk_len + 4L * a.blk_k;
-    (void)nhalo;
+    // one workgroup: segment + halo heads, or (hosted) a full segment whose one halo head the tails run
+    const bool hosted_dl = a.dl_halo && nseg_dl + nhalo > MAXW;
+    const long span = W_dl == 1 ? (hosted_dl ? nseg_dl : nseg_dl + nhalo) : (long)a.blk_len + 4L * a.blk_k;
+    if (hosted_dl && (nhalo != 1 || nseg_dl < 8)) {
+      gadmm_set_error("blocked chain kernel (data-local halo): a hosted halo needs one hosted side and >= 4 tails");
+      return -1;
+    }
     if (!multi || !a.sys_scope || a.blk_pw != 1 || a.n_epochs != 0 || a.blk_npeer != 0 || a.blk_k < 1 ||
         a.blk_len < 1 || nseg_dl < 1 || span > MAXW || (W_dl > 1 && a.ring < 2 * a.blk_k + 4) ||
         (a.seg_lo > 0 && !a.dl_tab[0]) || (a.seg_hi < a.n - 1 && !a.dl_tab[1]) ||
@@ -1200,7 +1219,7 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
     }
     fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, true, false, false, true>
                    : (const void*)chain_blocked_kernel<52, true, false, false, true>;
-    lds += (2L * HIMG52 + 2 * 192) * 8;  // the hosted halo heads' inverse images + states (segment + halo > MAXW)
+    lds += (long)(HIMG52 + 512) * 8;  // the hosted halo head's inverse image + state (segment + halo > MAXW)
   } else if (a.sys_scope) {
     if (tl) fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, true, true> : (const void*)chain_blocked_kernel<52, true, true>;
     else fn = a.d <= 32 ? (const void*)chain_blocked_kernel<32, true, false> : (const void*)chain_blocked_kernel<52, true, false>;

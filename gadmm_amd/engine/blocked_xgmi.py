@@ -50,10 +50,15 @@ def halo_heads(lo: int, hi: int, n: int) -> list:
 def dl_halo_eligible(segs, n: int, d: int) -> bool:
     """Whether the data-local halo mode can run on every rank: more than one rank, every segment >= 2
     positions and within one 12-wave workgroup. A halo head that does not fit a wave of its own (24
-    workers on 2 ranks: 12 + 1) is hosted by its boundary tail (chain_blocked.hip: the tail computes it
-    in the head phase, from the head's inverse in LDS)."""
+    workers on 2 ranks: 12 + 1) is hosted by the segment's tails (chain_blocked.hip: four tail waves
+    run its row groups in the head phase, from its inverse in LDS; one hosted head per segment)."""
+    def fits(lo, hi):
+        nh = len(halo_heads(lo, hi, n))
+        # one wave per position; or hosted: one halo head run by >= 4 of the segment's tails
+        return hi - lo + 1 + nh <= MAXW or (hi - lo + 1 <= MAXW and nh == 1 and hi - lo + 1 >= 8)
+
     return (len(segs) > 1 and d <= 52 and all(hi - lo + 1 >= 2 for lo, hi in segs)
-            and all(hi - lo + 1 <= MAXW for lo, hi in segs))
+            and all(fits(lo, hi) for lo, hi in segs))
 
 
 def dl_halo_hosted(lo: int, hi: int, n: int) -> bool:
