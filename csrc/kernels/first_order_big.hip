@@ -1,0 +1,397 @@
+// Large-d first-order comparators (d > 128; the real-shaped 10k config): GD, DGD, LAG-PS / LAG-WK,
+// cyclic / randomized IAG and dual averaging of GD_DGD_LAG.m / dual_averaging.m,
+// as stream-ordered kernels with the stop rule on the device (engine/first_order_big.py enqueues
+// blocks of iterations and looks at the control word once per block, like star_big.hip).
+//
+// An iteration is HBM-bound on the d x d Grams: every A_n (and the local sum A_sum for the server's
+// objective) is stored as its block-packed lower triangle (sym_gemv.h: 400 MB instead of 800 MB at
+// d = 10k) and multiplied by the symmetric GEMV of sym_gemv.h. Everything else is O(N d) and fused
+// into one or two elementwise kernels per iteration:
+//   GD     q = A_sum th                 obj(th), th -= a g with g = q - b_sum (ones at it = 1)
+//   DGD    q_n = A_n th_n               G[n] = q_n - b_n, obj; th_n -= a/100 * (neighbour average of G)
+//   IAG    q = A_w th (refreshing w), q' = A_sum th: T[w] = q - b_w; obj; th -= a/N sum_n T[n]
+//   LAG    q_n = A_n th (every worker)  triggers from the 10-deep history of |th^k - th^{k-1}|^2,
+//                                       conditional uploads into T, th -= a sum_n T[n]
+//   DualAv q_n = A_n th_n               obj of the previous iterate; the Gauss-Seidel (or Jacobi)
+//                                       sweep Z_n = mix(Z_nbr) + g_n, th_n = -a Z_n, per element
+// Vectors are zero padded to symv::padded(d) (the GEMV reads whole 128-blocks); the padding is never
+// written. Objective partials are per (worker, 128-element block) and summed in a fixed order.
+#include "gadmm_common.h"
+#include "gadmm_chain.h"
+#include "sym_gemv.h"
+
+namespace {
+
+constexpr int EB = 128;  // elementwise block = one symv block row
+constexpr int TRIG = 10;  // LAG trigger slot (GD_DGD_LAG.m:18)
+
+// y_s = M_s x_s (count slots; padded vectors, M_s block-packed); work: count x part_doubles
+__global__ void __launch_bounds__(symv::NT) fob_symv_part(const double* Mp, long mstride, const double* x,
+                                                          long xstride, double* work, int d, const ChainCtl* ctl) {
+  __shared__ symv::dv2 tl[symv::NT / 64][64];
+  if (ctl && ctl->done) return;
+  const int s = blockIdx.y;
+  symv::part_block(Mp + s * mstride, x + s * xstride, work + s * symv::part_doubles(d), symv::nblk(d), blockIdx.x, tl);
+}
+
+__global__ void __launch_bounds__(symv::B) fob_symv_reduce(const double* work, double* y, long ystride, int d,
+                                                           const ChainCtl* ctl) {
+  if (ctl && ctl->done) return;
+  const int s = blockIdx.y, t = blockIdx.x, k = threadIdx.x, j = t * symv::B + k;
+  const double v = symv::reduce_elem(work + s * symv::part_doubles(d), symv::nblk(d), t, k);
+  if (j < d) y[s * ystride + j] = v;
+}
+
+__device__ __forceinline__ double block_sum(double v, double* sh) {
+  v = wave_sum_f64(v);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x == 0)
+    for (int q = 0; q < (int)(blockDim.x >> 6); ++q) t += sh[q];
+  __syncthreads();
+  return t;  // valid on thread 0
+}
+
+// ---- GD (server step with the stacked gradient, GD_DGD_LAG.m:88-118): obj partials at th, th -= a g
+__global__ void __launch_bounds__(EB) fob_gd(const double* q, const double* bsum, double* th, double* part, int d,
+                                             double step, int faithful, const ChainCtl* ctl) {
+  __shared__ double sh[2];
+  if (ctl->done) return;
+  const int j = blockIdx.x * EB + threadIdx.x;
+  double p = 0.0;
+  if (j < d) {
+    const double t = th[j];
+    p = (0.5 * q[j] - bsum[j]) * t;
+    const double g = (faithful && ctl->iter == 1) ? 1.0 : q[j] - bsum[j];
+    th[j] = t - step * g;
+  }
+  const double s = block_sum(p, sh);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// ---- DGD: G[gid] = q_n - b_n (ones at it = 1) + obj partials of th_n
+__global__ void __launch_bounds__(EB) fob_dgd_grad(const double* q, long dp, const double* b, const double* th,
+                                                   double* G, double* part, int d, int w_lo, int faithful,
+                                                   const ChainCtl* ctl) {
+  __shared__ double sh[2];
+  if (ctl->done) return;
+  const int n = blockIdx.y, j = blockIdx.x * EB + threadIdx.x;
+  double p = 0.0;
+  if (j < d) {
+    const double qq = q[n * dp + j], bb = b[(long)n * d + j];
+    p = (0.5 * qq - bb) * th[n * dp + j];
+    G[(long)(w_lo + n) * d + j] = (faithful && ctl->iter == 1) ? 1.0 : qq - bb;
+  }
+  const double s = block_sum(p, sh);
+  if (threadIdx.x == 0) part[(long)n * gridDim.x + blockIdx.x] = s;
+}
+
+// th_n -= a/100 * neighbour average of G (GD_DGD_LAG.m:155-171; the torch path's operation order)
+__global__ void __launch_bounds__(EB) fob_dgd_update(double* th, long dp, const double* G, int d, int w_lo,
+                                                     int n_total, double step, const ChainCtl* ctl) {
+  if (ctl->done) return;
+  const int n = blockIdx.y, j = blockIdx.x * EB + threadIdx.x;
+  if (j >= d) return;
+  const int w = w_lo + n;
+  const double t = th[n * dp + j], gw = G[(long)w * d + j];
+  double v;
+  if (n_total == 1) v = t - step * gw;
+  else if (w == 0) v = t - 0.5 * step * (gw + G[(long)(w + 1) * d + j]);
+  else if (w == n_total - 1) v = t - 0.5 * step * (gw + G[(long)(w - 1) * d + j]);
+  else v = t - (1.0 / 3.0) * step * (gw + G[(long)(w + 1) * d + j] + G[(long)(w - 1) * d + j]);
+  th[n * dp + j] = v;
+}
+
+// ---- server tables (IAG, LAG): obj partials of the replicated th from q = A_sum th (IAG) and the
+// server step th -= a * sum_n T[n] (worker order); dth: |th_new - th|^2 partials (LAG triggers)
+__global__ void __launch_bounds__(EB) fob_server(const double* q, const double* bsum, double* th, const double* T,
+                                                 double* part, double* dpart, int d, int n_total, double step,
+                                                 const ChainCtl* ctl) {
+  __shared__ double sh[2];
+  if (ctl->done) return;
+  const int j = blockIdx.x * EB + threadIdx.x;
+  double p = 0.0, dd = 0.0;
+  if (j < d) {
+    const double t = th[j];
+    if (q) p = (0.5 * q[j] - bsum[j]) * t;
+    double s = 0.0;
+    for (int n = 0; n < n_total; ++n) s += T[(long)n * d + j];
+    const double tn = t - step * s;
+    th[j] = tn;
+    dd = (tn - t) * (tn - t);
+  }
+  const double s1 = block_sum(p, sh);
+  if (threadIdx.x == 0 && part) part[blockIdx.x] = s1;
+  const double s2 = block_sum(dd, sh);
+  if (threadIdx.x == 0 && dpart) dpart[blockIdx.x] = s2;
+}
+
+// IAG refresh of worker w (local index li): T[w] = q - b_li
+__global__ void __launch_bounds__(EB) fob_iag_refresh(const double* q, const double* b, double* T, int d, int li,
+                                                      int w, const ChainCtl* ctl) {
+  if (ctl->done || ctl->iter <= 1) return;
+  const int j = blockIdx.x * EB + threadIdx.x;
+  if (j < d) T[(long)w * d + j] = q[j] - b[(long)li * d + j];
+}
+
+// ---- LAG: grads at th for every worker (q_n - b_n), obj partials, trigger distances per block
+__global__ void __launch_bounds__(EB) fob_lag_grad(const double* q, long dp, const double* b, const double* th,
+                                                   double* GN, const double* Gl, const double* thhat, double* part,
+                                                   double* ddpart, int d, int ps, const ChainCtl* ctl) {
+  __shared__ double sh[2];
+  if (ctl->done) return;
+  const int n = blockIdx.y, j = blockIdx.x * EB + threadIdx.x;
+  double p = 0.0, dd = 0.0;
+  if (j < d) {
+    const double qq = q[n * dp + j], bb = b[(long)n * d + j], t = th[j];
+    const double g = qq - bb;
+    GN[(long)n * d + j] = g;
+    p = (0.5 * qq - bb) * t;
+    const double df = ps ? thhat[(long)n * d + j] - t : g - Gl[(long)n * d + j];
+    dd = df * df;
+  }
+  const double s1 = block_sum(p, sh);
+  if (threadIdx.x == 0) part[(long)n * gridDim.x + blockIdx.x] = s1;
+  const double s2 = block_sum(dd, sh);
+  if (threadIdx.x == 0) ddpart[(long)n * gridDim.x + blockIdx.x] = s2;
+}
+
+// LAG decisions (one thread per local worker): mask_n from the trigger of GD_DGD_LAG.m:211-227 /
+// :287-300 (nothing before iter > 10), the upload count into cnt[it - 1]; ring[TRIG + 2] holds
+// |th^k - th^{k-1}|^2 of the last iterations (slot k % (TRIG + 1))
+__global__ void fob_lag_decide(const double* ddpart, int nblk, const double* hsq, const double* ring, int* mask,
+                               double* cnt, int n_local, int w_lo, int ps, double thrd, int faithful,
+                               const ChainCtl* ctl) {
+  if (ctl->done || threadIdx.x != 0) return;
+  const int it = ctl->iter;
+  double trig = 0.0;
+  if (it > TRIG)
+    for (int k = 1; k <= TRIG; ++k) trig += ring[(it - k) % (TRIG + 1)];  // the torch path's order: n = 1..10
+  int c = 0;
+  for (int n = 0; n < n_local; ++n) {
+    int m = 0;
+    if (it > TRIG) {
+      double dd = 0.0;
+      for (int k = 0; k < nblk; ++k) dd += ddpart[(long)n * nblk + k];
+      m = ps ? (hsq[w_lo + n] * dd > thrd * trig) : (dd > thrd * trig);
+    }
+    c += m;
+    // forced refresh of worker 1 every iteration > 1 (LAG-PS quirk 4), not counted: mask 2
+    mask[n] = m ? 1 : ((ps && faithful && it > 1 && w_lo + n == 0) ? 2 : 0);
+  }
+  if (it - 1 >= 0) cnt[it - 1] = (double)c;
+}
+
+// LAG uploads: masked workers take their new gradient (and PS its th-hat) into G_loc and the table
+__global__ void __launch_bounds__(EB) fob_lag_apply(const double* GN, double* Gl, double* thhat, const double* th,
+                                                    double* T, const int* mask, int d, int w_lo, int ps,
+                                                    const ChainCtl* ctl) {
+  if (ctl->done) return;
+  const int n = blockIdx.y, j = blockIdx.x * EB + threadIdx.x;
+  const int m = mask[n];
+  if (j >= d || m == 0) return;
+  const double g = GN[(long)n * d + j];
+  Gl[(long)n * d + j] = g;
+  if (ps && m == 1) thhat[(long)n * d + j] = th[j];
+  T[(long)(w_lo + n) * d + j] = g;
+}
+
+// ---- dual averaging: obj partials of th_n^{it-1} (the previous iterate) and the sweep
+__global__ void __launch_bounds__(EB) fob_da_obj(const double* q, long dp, const double* b, const double* th,
+                                                 double* part, int d, const ChainCtl* ctl) {
+  __shared__ double sh[2];
+  if (ctl->done) return;
+  const int n = blockIdx.y, j = blockIdx.x * EB + threadIdx.x;
+  double p = 0.0;
+  if (j < d) p = (0.5 * q[n * dp + j] - b[(long)n * d + j]) * th[n * dp + j];
+  const double s = block_sum(p, sh);
+  if (threadIdx.x == 0) part[(long)n * gridDim.x + blockIdx.x] = s;
+}
+
+// one thread per element: the workers in chain order (Z overwritten in place: Gauss-Seidel, or
+// the previous sweep's Z for both neighbours in Jacobi mode), th_n = -a Z_n (dual_averaging.m:34-44)
+__global__ void __launch_bounds__(EB) fob_da_sweep(const double* q, long dp, const double* b, double* th, double* Z,
+                                                   double* Zp, int d, int n, double alpha, int jacobi,
+                                                   const ChainCtl* ctl) {
+  if (ctl->done) return;
+  const int j = blockIdx.x * EB + threadIdx.x;
+  if (j >= d) return;
+  for (int k = 0; k < n; ++k) Zp[(long)k * d + j] = Z[(long)k * d + j];
+  for (int k = 0; k < n; ++k) {
+    const double g = q[k * dp + j] - b[(long)k * d + j];
+    const bool hl = k > 0, hr = k < n - 1;
+    const double left = hl ? (jacobi ? Zp[(long)(k - 1) * d + j] : Z[(long)(k - 1) * d + j]) : 0.0;
+    const double right = hr ? Zp[(long)(k + 1) * d + j] : 0.0;
+    double zn;
+    if (!hl && !hr) zn = g;
+    else if (!hl) zn = right + g;
+    else if (!hr) zn = left + g;
+    else zn = 0.5 * right + 0.5 * left + g;
+    Z[(long)k * d + j] = zn;
+    th[k * dp + j] = -alpha * zn;
+  }
+}
+
+__global__ void fob_objw(const double* part, int nblk, const double* yy, double* objw, int n_local, int w_lo,
+                         int n_total, const ChainCtl* ctl) {
+  if (ctl->done) return;
+  for (int g = threadIdx.x; g < n_total; g += blockDim.x) objw[g] = 0.0;
+  __syncthreads();
+  for (int n = threadIdx.x; n < n_local; n += blockDim.x) {
+    double f = 0.0;
+    for (int k = 0; k < nblk; ++k) f += part[(long)n * nblk + k];
+    objw[w_lo + n] = f + 0.5 * yy[n];
+  }
+}
+
+// ---- finish: per-worker objectives (partials in block order + 1/2 y'y) -> trace, stop rule, iter.
+// nw objective rows of nblk partials each (nw = 1: the replicated-theta algorithms, yy = y'y sum).
+// `shift` = 1: the objective belongs to the previous iteration (dual averaging evaluates th^{it-1}
+// with the GEMV of iteration it); ring / dpart: LAG's |dth|^2 history.
+__global__ void fob_finish(const double* part, int nw, int nblk, const double* yy, double* trace, long long* tstamp,
+                           int max_iter, double obj0, double tol, int shift, const double* dpart, double* ring,
+                           ChainCtl* ctl) {
+  if (threadIdx.x != 0 || ctl->done) return;
+  const int it = ctl->iter;
+  if (dpart) {  // LAG: |th^{it} - th^{it-1}|^2 into the ring slot it % 11 (read from iteration it + 1 on)
+    double s = 0.0;
+    for (int k = 0; k < nblk; ++k) s += dpart[k];
+    ring[it % (TRIG + 1)] = s;
+  }
+  const int rec = it - shift;  // the iteration this objective belongs to
+  if (rec >= 1) {
+    double obj = 0.0;
+    for (int w = 0; w < nw; ++w) {
+      double f = 0.0;
+      for (int k = 0; k < nblk; ++k) f += part[(long)w * nblk + k];
+      obj += f + 0.5 * yy[w];
+    }
+    if (rec - 1 < max_iter) {
+      trace[rec - 1] = obj;
+      tstamp[rec - 1] = (long long)__builtin_amdgcn_s_memrealtime();
+    }
+    int code = 0;
+    if (!(obj == obj) || isinf(obj)) code = 3;
+    else if (tol >= 0.0 && fabs(obj - obj0) < tol) code = 1;
+    else if (rec >= max_iter) code = 2;
+    if (code) {
+      ctl->done = code;
+      ctl->conv_iter = rec;
+    }
+  }
+  ctl->iter = it + 1;
+}
+
+}  // namespace
+
+extern "C" {
+
+// y_s = M_s x_s for `count` slots: M block-packed (stride mstride doubles), x zero padded (xstride),
+// y (ystride); work: count * part_doubles(d). ctl: optional skip word (done != 0: no-op).
+int gadmm_symv_batch(const double* Mp, long mstride, const double* x, long xstride, double* y, long ystride,
+                     double* work, int count, int d, const ChainCtl* ctl, hipStream_t st) {
+  if (!Mp || !x || !y || !work || count < 1 || d < 1) {
+    gadmm_set_error("symv_batch: bad arguments");
+    return -1;
+  }
+  hipLaunchKernelGGL(fob_symv_part, dim3((unsigned)symv::nstored(d), count), dim3(symv::NT), 0, st, Mp, mstride, x,
+                     xstride, work, d, ctl);
+  hipLaunchKernelGGL(fob_symv_reduce, dim3(symv::nblk(d), count), dim3(symv::B), 0, st, work, y, ystride, d, ctl);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+long gadmm_symv_work_doubles(int d) { return symv::part_doubles(d); }
+long gadmm_sym_padded(int d) { return symv::padded(d); }
+
+int gadmm_fob_gd(const double* q, const double* bsum, double* th, double* part, int d, double step, int faithful,
+                 const ChainCtl* ctl, hipStream_t st) {
+  hipLaunchKernelGGL(fob_gd, dim3((d + EB - 1) / EB), dim3(EB), 0, st, q, bsum, th, part, d, step, faithful, ctl);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+int gadmm_fob_dgd_grad(const double* q, long dp, const double* b, const double* th, double* G, double* part, int d,
+                       int n_local, int w_lo, int faithful, const ChainCtl* ctl, hipStream_t st) {
+  hipLaunchKernelGGL(fob_dgd_grad, dim3((d + EB - 1) / EB, n_local), dim3(EB), 0, st, q, dp, b, th, G, part, d, w_lo,
+                     faithful, ctl);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+int gadmm_fob_dgd_update(double* th, long dp, const double* G, int d, int n_local, int w_lo, int n_total, double step,
+                         const ChainCtl* ctl, hipStream_t st) {
+  hipLaunchKernelGGL(fob_dgd_update, dim3((d + EB - 1) / EB, n_local), dim3(EB), 0, st, th, dp, G, d, w_lo, n_total,
+                     step, ctl);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+int gadmm_fob_server(const double* q, const double* bsum, double* th, const double* T, double* part, double* dpart,
+                     int d, int n_total, double step, const ChainCtl* ctl, hipStream_t st) {
+  hipLaunchKernelGGL(fob_server, dim3((d + EB - 1) / EB), dim3(EB), 0, st, q, bsum, th, T, part, dpart, d, n_total,
+                     step, ctl);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+int gadmm_fob_iag_refresh(const double* q, const double* b, double* T, int d, int li, int w, const ChainCtl* ctl,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(fob_iag_refresh, dim3((d + EB - 1) / EB), dim3(EB), 0, st, q, b, T, d, li, w, ctl);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+int gadmm_fob_lag(const double* q, long dp, const double* b, const double* th, double* GN, double* Gl, double* thhat,
+                  double* T, double* part, double* ddpart, const double* hsq, const double* ring, int* mask,
+                  double* cnt, int d, int n_local, int w_lo, int ps, double thrd, int faithful, const ChainCtl* ctl,
+                  hipStream_t st) {
+  const int nblk = (d + EB - 1) / EB;
+  hipLaunchKernelGGL(fob_lag_grad, dim3(nblk, n_local), dim3(EB), 0, st, q, dp, b, th, GN, Gl, thhat, part, ddpart, d,
+                     ps, ctl);
+  hipLaunchKernelGGL(fob_lag_decide, dim3(1), dim3(64), 0, st, ddpart, nblk, hsq, ring, mask, cnt, n_local, w_lo, ps,
+                     thrd, faithful, ctl);
+  hipLaunchKernelGGL(fob_lag_apply, dim3(nblk, n_local), dim3(EB), 0, st, GN, Gl, thhat, th, T, mask, d, w_lo, ps, ctl);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+// per-worker objective partials of th_n (rows of q / th with stride dp), e.g. dual averaging's
+// previous iterate
+int gadmm_fob_worker_obj(const double* q, long dp, const double* b, const double* th, double* part, int d, int n,
+                         const ChainCtl* ctl, hipStream_t st) {
+  const int nblk = (d + EB - 1) / EB;
+  hipLaunchKernelGGL(fob_da_obj, dim3(nblk, n), dim3(EB), 0, st, q, dp, b, th, part, d, ctl);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+// per-worker objectives into global slots: objw[w_lo + n] = sum_k part[n][k] + 1/2 yy_n (block order),
+// every other slot 0 (so an all-reduce of objw over the ranks is exact)
+int gadmm_fob_objw(const double* part, int nblk, const double* yy, double* objw, int n_local, int w_lo, int n_total,
+                   const ChainCtl* ctl, hipStream_t st) {
+  hipLaunchKernelGGL(fob_objw, dim3(1), dim3(64), 0, st, part, nblk, yy, objw, n_local, w_lo, n_total, ctl);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+int gadmm_fob_da_sweep(const double* q, long dp, const double* b, double* th, double* Z, double* Zp, int d, int n,
+                       double alpha, int jacobi, const ChainCtl* ctl, hipStream_t st) {
+  hipLaunchKernelGGL(fob_da_sweep, dim3((d + EB - 1) / EB), dim3(EB), 0, st, q, dp, b, th, Z, Zp, d, n, alpha, jacobi,
+                     ctl);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+int gadmm_fob_finish(const double* part, int nw, int nblk, const double* yy, double* trace, long long* tstamp,
+                     int max_iter, double obj0, double tol, int shift, const double* dpart, double* ring, ChainCtl* ctl,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(fob_finish, dim3(1), dim3(64), 0, st, part, nw, nblk, yy, trace, tstamp, max_iter, obj0, tol,
+                     shift, dpart, ring, ctl);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+}  // extern "C"

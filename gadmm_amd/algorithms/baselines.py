@@ -107,13 +107,24 @@ def _fo_engine(ctx: _Ctx, backend: str, alg: str = "GD"):
     if backend == "torch":
         return None
     from ..engine.first_order import FirstOrderEngine
+    from ..engine.first_order_big import FirstOrderBigEngine
 
     ok = FirstOrderEngine.eligible(ctx.model, ctx.comm, ctx.n_total, ctx.local_ids, ctx.placement, alg)
-    if not ok:
-        if backend == "native":
-            raise RuntimeError("native first-order engine needs GPU ranks with contiguous segments and d <= 128")
-        return None
-    return FirstOrderEngine.get(ctx.model, ctx.comm, ctx.placement, ctx.n_total)
+    if ok:
+        return FirstOrderEngine.get(ctx.model, ctx.comm, ctx.placement, ctx.n_total)
+    # d > 128, linear: the stream-ordered large-d engine (packed Grams, device stop rule)
+    big = getattr(ctx.model, "kind", "") == "linear" and int(ctx.model.d) > 128
+    if big and ctx.comm.nranks > 1:  # collective: every rank takes the same path
+        from ..engine.first_order import _all_ok
+        big = _all_ok(FirstOrderBigEngine.eligible(ctx.model, ctx.comm, ctx.n_total, ctx.local_ids, ctx.placement,
+                                                   alg), ctx.comm)
+    elif big:
+        big = FirstOrderBigEngine.eligible(ctx.model, ctx.comm, ctx.n_total, ctx.local_ids, ctx.placement, alg)
+    if big:
+        return FirstOrderBigEngine.get(ctx.model, ctx.comm, ctx.placement, ctx.n_total)
+    if backend == "native":
+        raise RuntimeError("native first-order engine needs GPU ranks with contiguous segments")
+    return None
 
 
 def model_bytes(units: np.ndarray, d: int) -> int:
@@ -133,7 +144,7 @@ def _native_result(name, out, obj0, units, d: int, **extra) -> RunResult:
                      converged=out["converged"], wall_s=float(out["times"][-1]) if n else 0.0,
                      time_trace=out["times"], comm_units=units, bytes_sent=int(out.get("payload_bytes", 0)),
                      bytes_total=int(out.get("payload_bytes", 0)),
-                     extra=dict(extra, engine="native-persistent", rows_pushed=out.get("rows_pushed", 0),
+                     extra=dict(extra, engine=out.get("engine", "native-persistent"), rows_pushed=out.get("rows_pushed", 0),
                                 flags_pushed=out.get("flags_pushed", 0), wire_bytes=out.get("wire_bytes", 0),
                                 model_bytes=model_bytes(units, d)))
 

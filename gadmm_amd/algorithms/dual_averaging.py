@@ -46,8 +46,21 @@ def dual_averaging(model, local_ids: Sequence[int], n_total: int, alpha: float, 
                              extra={"jacobi": jacobi, "nranks": comm.nranks, "engine": "native-persistent",
                                     "rows_pushed": out["rows_pushed"], "wire_bytes": out["wire_bytes"],
                                     "model_bytes": n * n_total * model.d * 8, "dim": model.d})
+        from ..engine.first_order_big import FirstOrderBigEngine
+        if comm.nranks == 1 and FirstOrderBigEngine.eligible(model, comm, n_total, local_ids, placement, "DualAvg"):
+            # d > 128 on one rank: the stream-ordered large-d engine (packed Grams, device stop rule)
+            out = FirstOrderBigEngine.get(model, comm, placement, n_total).run("DualAvg", max_iter, alpha, obj0, tol,
+                                                                                 jacobi=jacobi)
+            obj = out["obj"]
+            n = len(obj)
+            return RunResult(algorithm=name, obj=obj, loss=np.abs(obj - obj0),
+                             iters=out["iters"] if out["converged"] else n, converged=out["converged"],
+                             wall_s=float(out["times"][-1]) if n else 0.0, time_trace=out["times"],
+                             comm_units=np.arange(1, n + 1, dtype=np.float64) * n_total, bytes_sent=0, bytes_total=0,
+                             extra={"jacobi": jacobi, "nranks": 1, "engine": "native-big",
+                                    "model_bytes": n * n_total * model.d * 8, "dim": model.d})
         if backend == "native":
-            raise RuntimeError("native dual averaging needs GPU ranks with contiguous segments and d <= 128")
+            raise RuntimeError("native dual averaging needs GPU ranks with contiguous segments")
     dev, d = model.device, model.d
     local_ids = [int(w) for w in local_ids]
     if local_ids != sorted(local_ids) or (local_ids and local_ids[-1] - local_ids[0] + 1 != len(local_ids)):

@@ -133,6 +133,29 @@ class IpcComm(Comm):
         sent = (R - 1) if k == 2 else (1 if (k == 0 and me != root) else (R - 1 if (k == 1 and me == root) else 0))
         self.stats.coll_bytes += sent * t.numel() * t.element_size()
 
+    def exchange_rows_dev(self, table, ops, phase: int, ctl, stream) -> None:
+        """Grouped row exchange on a stream (the chain engine's ``gadmm_ipc_exchange_rows``): ``ops`` =
+        (peer, row, is_send) over ``table`` (n_total, d); tags from ``4 * ctl.iter + phase``, so every rank
+        must issue the same exchanges per iteration. Stalled peers set ctl.done = 4."""
+        from ..ops import native
+        lib = self.transport.lib
+        fn = lib.gadmm_ipc_exchange_rows
+        fn.restype = ctypes.c_int
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                       ctypes.c_void_p, ctypes.c_void_p]
+        arr = (native.XchgOp * len(ops))()
+        for i, (peer, row, snd) in enumerate(ops):
+            arr[i].peer, arr[i].row, arr[i].is_send, arr[i].count = int(peer), int(row), int(snd), 0
+        d = int(table.shape[1])
+        native.check(fn(self.xport, ctypes.cast(arr, ctypes.c_void_p), len(ops), table.data_ptr(), d, int(phase),
+                        ctl.data_ptr(), stream), "ipc_exchange_rows")
+        for peer, row, snd in ops:
+            if snd:
+                self.stats.bytes_sent += d * 8
+                self.stats.msgs_sent += 1
+            else:
+                self.stats.bytes_recv += d * 8
+
     def new_epoch(self, stream) -> None:
         """Start a new solve on this transport: granules of earlier solves stop matching (every rank)."""
         from ..ops import native

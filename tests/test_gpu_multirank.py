@@ -708,3 +708,53 @@ def test_first_order_epoch_wrap_clears_tables_collectively():
         assert r["epoch"] == 1
         assert np.array_equal(r["a"], r["b"])
     assert np.array_equal(res[0]["c"], res[1]["c"])
+
+
+def _fo_big_rank(rank, world, n, m_rows, d, iters):
+    import torch
+    from gadmm_amd.data import gaussian_regression
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import gradient_descent, decentralized_gd, iag
+    from gadmm_amd.parallel.ipc import IpcComm
+    from gadmm_amd.parallel.topology import Placement
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    pl = Placement.contiguous(n, world)
+    ids = pl.local_workers(rank)
+    ds = gaussian_regression(n, m_rows, d, seed=11, labels="linear", device=dev, worker_ids=ids)
+    m = LinearRegression(ds.X, ds.y)
+    comm = IpcComm(n, d, 16, dev)
+    s, obj0 = 1e-4, 0.0
+    out = {}
+    for name, fn in (("GD", lambda: gradient_descent(m, ids, n, iters, obj0, s, comm=comm, placement=pl)),
+                     ("DGD", lambda: decentralized_gd(m, ids, n, iters, obj0, s, comm=comm, placement=pl)),
+                     ("cIAG", lambda: iag(m, ids, n, iters, obj0, s, "cyclic", None, comm=comm, placement=pl))):
+        r = fn()
+        out[name] = (r.obj, r.extra.get("engine"), r.bytes_sent)
+    comm.close()
+    return out
+
+
+def test_first_order_big_across_ranks():
+    """The large-d GD (all-reduce of the local Gram-sum GEMV), DGD (boundary gradients to the neighbour
+    ranks) and IAG (the refreshing worker's row broadcast from its owner) over the IPC device transport,
+    2 ranks sharing the GPU, == one rank to 1e-11; payload = the per-iteration collective bytes."""
+    import torch
+    from gadmm_amd.parallel.launch import spawn
+    from gadmm_amd.data import gaussian_regression
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import gradient_descent, decentralized_gd, iag
+    n, m_rows, d, iters = 4, 400, 256 + 44, 200
+    res = spawn(_fo_big_rank, 2, n, m_rows, d, iters, timeout=300)
+    ds = gaussian_regression(n, m_rows, d, seed=11, labels="linear", device=DEV)
+    m = LinearRegression(ds.X, ds.y)
+    one = {"GD": gradient_descent(m, list(range(n)), n, iters, 0.0, 1e-4),
+           "DGD": decentralized_gd(m, list(range(n)), n, iters, 0.0, 1e-4),
+           "cIAG": iag(m, list(range(n)), n, iters, 0.0, 1e-4, "cyclic", None)}
+    for r in res:
+        for k, ref in one.items():
+            obj, eng, _ = r[k]
+            assert eng == "native-big" and ref.extra["engine"] == "native-big", (k, eng)
+            np.testing.assert_allclose(obj, ref.obj, rtol=1e-11, atol=0)
+    assert res[0]["GD"][2] == iters * 2 * d * 8          # each rank pushes its d-row partial to the other
+    assert res[0]["DGD"][2] == iters * 2 * d * 8         # one boundary: a gradient row each way
