@@ -81,17 +81,62 @@ def global_constants(model, comm: Optional[Comm] = None) -> Dict[str, object]:
     """Hmax per worker, Hmax_all and the GD step 1/Hmax_all (GD_DGD_LAG.m:19-47; logistic
     GD_DGD_LAG_logistic.m:24). One all-reduce of the d x d Gram / all-gather of Hmax."""
     comm = comm if comm is not None else LocalComm()
-    G = torch.bmm(model.X.transpose(1, 2), model.X).sum(0).contiguous()
+    big = int(model.d) > 128
+    if big and model.kind == "linear":
+        G = model.A.sum(0).contiguous()  # the cached Grams (K1): no second pass over a 100 GB shard
+    else:
+        G = torch.bmm(model.X.transpose(1, 2), model.X).sum(0).contiguous()
     if comm.nranks > 1:
         comm.allreduce_sum(G)
-    ev = torch.linalg.eigvalsh(G)
+    if big:  # Lanczos instead of a dense eigensolve of a 10k x 10k matrix (K12 of SURVEY.md §2.5)
+        lo, hi = extreme_eigs(G)
+        ev = torch.tensor([lo, hi], dtype=torch.float64)
+    else:
+        ev = torch.linalg.eigvalsh(G)
     if model.kind == "linear":
         hmax_all = float(ev[-1])
     else:
         hmax_all = 0.25 * float(ev[-1]) + model.lam
-    hmax_loc = model.hmax()
+    if big and model.kind == "linear":
+        hmax_loc = torch.tensor([extreme_eigs(model.A[i])[1] for i in range(int(model.n_local))],
+                                dtype=torch.float64, device=model.A.device) + model.lam
+    else:
+        hmax_loc = model.hmax()
     return {"hmax_local": hmax_loc, "hmax_all": hmax_all, "stepsize": 1.0 / hmax_all,
             "cond": float(ev[-1] / ev[0]) if float(ev[0]) > 0 else float("inf")}
+
+
+def extreme_eigs(M: torch.Tensor, k: int = 96, seed: int = 0):
+    """(lambda_min, lambda_max) of a symmetric matrix by Lanczos with full reorthogonalisation: ``k``
+    GEMVs with M (on its device) and a k x k tridiagonal eigensolve. The extreme Ritz values converge
+    first; at k = 96 they match a dense eigensolve to ~1e-12 relative on the real-shaped Grams
+    (tests/test_algorithms.py::test_lanczos_extreme_eigs)."""
+    d = int(M.shape[0])
+    k = min(k, d)
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    v = torch.randn(d, generator=g, dtype=torch.float64).to(M.device)
+    v = v / torch.linalg.norm(v)
+    V = torch.zeros((k, d), dtype=torch.float64, device=M.device)
+    alpha = torch.zeros(k, dtype=torch.float64)
+    beta = torch.zeros(k, dtype=torch.float64)
+    m = k
+    for j in range(k):
+        V[j] = v
+        w = M @ v
+        a = float(w @ v)
+        alpha[j] = a
+        w = w - V[: j + 1].T @ (V[: j + 1] @ w)  # full reorthogonalisation (twice is enough)
+        w = w - V[: j + 1].T @ (V[: j + 1] @ w)
+        b = float(torch.linalg.norm(w))
+        if j + 1 < k:
+            beta[j] = b
+            if b < 1e-300:
+                m = j + 1
+                break
+            v = w / b
+    Tm = torch.diag(alpha[:m]) + torch.diag(beta[: m - 1], 1) + torch.diag(beta[: m - 1], -1)
+    ev = torch.linalg.eigvalsh(Tm)
+    return float(ev[0]), float(ev[-1])
 
 
 def _gather_hmax(ctx: _Ctx, hmax_local: torch.Tensor) -> torch.Tensor:

@@ -11,6 +11,7 @@ the row-blocked HIP engine (RCCL p2p of 80 KB theta per boundary per phase) unti
 
     torchrun --nproc-per-node 8 -m gadmm_amd LinearRegression_RealShaped
     python -m gadmm_amd LinearRegression_RealShaped --set dim=2048 rows_per_worker=200000   # 1 GPU
+    python -m gadmm_amd LinearRegression_RealShaped --set run_baselines=1 run_dualavg=1   # + the bundle
 """
 import time
 
@@ -26,6 +27,7 @@ ENTRY = "LinearRegression_RealShaped"
 PRESETS.setdefault(ENTRY, ExperimentConfig(
     name=ENTRY, model="linear", data="gaussian", num_workers=0, rows_per_worker=1_250_000, dim=10_000,
     gadmm_iters=2000, rhos=[0.0], acc=1e-8, run_baselines=False, run_dualavg=False, run_star=True,
+    baseline_iters=400,
     reference="BASELINE.json configs[4]; LinearRegression_Real.m shapes scaled to 10M x 10k"))
 
 
@@ -77,6 +79,24 @@ def body(cfg, sess, args, writer):
         s = standard_admm(prob.model, ids, n_total, rho, prob.obj0, tol_abs, min(cfg.gadmm_iters, 500),
                           comm=sess.comm, placement=prob.placement)
         runs["ADMM(star)"] = s
+    if cfg.run_baselines:
+        # the reference's baseline bundle on the real-shaped data (LinearRegression_Real.m:66-69, 78): at
+        # d > 128 every algorithm runs on the stream-ordered large-d engine (engine/first_order_big.py;
+        # GD / DGD / IAG across ranks, LAG and dual averaging on one rank, else the torch loop)
+        from ..algorithms import gd_dgd_lag, dual_averaging, global_constants
+        t2 = time.perf_counter()
+        bl = gd_dgd_lag(prob.model, ids, n_total, cfg.baseline_iters, prob.obj0, comm=sess.comm,
+                        placement=prob.placement, backend=args.backend)
+        for k in ("GD", "DGD", "LAG-PS", "LAG-WK", "cIAG", "R-IAG"):
+            if k in bl:
+                runs[k] = bl[k]
+        if cfg.run_dualavg:
+            c = global_constants(prob.model, sess.comm)
+            runs["DualAvg"] = dual_averaging(prob.model, ids, n_total, c["stepsize"], prob.obj0, tol_abs,
+                                             cfg.dualavg_iters or cfg.baseline_iters, comm=sess.comm,
+                                             placement=prob.placement, backend=args.backend)
+        out["t_baselines_s"] = time.perf_counter() - t2
+        sess.log("  baselines (%d iterations each): %.2fs" % (cfg.baseline_iters, out["t_baselines_s"]))
     out["figure_groups"] = {"10M x 10k real-shaped": runs}
     return out
 

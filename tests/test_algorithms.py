@@ -206,3 +206,18 @@ def test_first_order_model_bytes_follow_reference_units(lin24):
     da = dual_averaging(m, ids, n, s, 218.6486436261889, 1e-12, 40)
     assert da.extra["model_bytes"] == len(da.obj) * n * d * 8
     assert np.isfinite(gd.obj).all()
+
+
+def test_lanczos_extreme_eigs():
+    """extreme_eigs (large-d global_constants): Lanczos with full reorthogonalisation == a dense
+    eigensolve on a real-shaped Gram (Gaussian rows: a clustered spectrum, the slow case for power
+    iteration)."""
+    import torch
+    from gadmm_amd.algorithms.baselines import extreme_eigs
+    g = torch.Generator().manual_seed(3)
+    X = torch.randn(900, 300, generator=g, dtype=torch.float64)
+    G = X.T @ X
+    lo, hi = extreme_eigs(G)
+    ev = torch.linalg.eigvalsh(G)
+    assert abs(hi - float(ev[-1])) <= 1e-10 * float(ev[-1])
+    assert abs(lo - float(ev[0])) <= 1e-8 * float(ev[-1])
