@@ -85,6 +85,116 @@ struct GramTile {
   static constexpr int PER_THREAD = BK * BT / NT;
 };
 
+// The K loop of one tile: slabs of BK rows staged through two LDS buffers. DIAG (uniform per
+// workgroup: a diagonal tile reads one panel) is a template parameter and the full slabs of an
+// interior tile run a loop with NO branch around the next slab's global loads, so those loads stay in
+// flight across the current slab's MFMAs (the wait lands right before the stash). With a branch (the
+// old `if (interior) ... else ...` / `if (!diag)` fetch), the compiler merged the two paths' registers
+// with moves right after the loads and drained vmcnt(0) there, exposing the load latency on every slab.
+// The remaining rows (every slab of a tile with columns past the shard, the partial last slab) take
+// synchronous clamped loads. Same MFMA order either way (bit-identical results).
+template <int BT, int NT, bool DIAG>
+__device__ __forceinline__ void gram_slabs(const double* __restrict__ H, const double* __restrict__ yv, int d,
+                                           long kbeg, long kend, long nfull, int row0, int col0,
+                                           double (*lds)[2 * BK * GramTile<BT, NT>::LDSROW],
+                                           f64x4 (&acc)[GramTile<BT, NT>::TMR][GramTile<BT, NT>::TMC]) {
+  using T = GramTile<BT, NT>;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  double ri[T::PER_THREAD], rj[T::PER_THREAD];
+  auto fetch_in = [&](long k0) {  // branch-free 8-B loads (every column < d, every row < kend)
+#pragma unroll
+    for (int p = 0; p < T::PER_THREAD / 2; ++p) {
+      const int e2 = tid + NT * p;
+      const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
+      const double* src = H + (k0 + r) * (long)d;
+      ri[2 * p] = src[row0 + c];
+      ri[2 * p + 1] = src[row0 + c + 1];
+      if constexpr (!DIAG) {
+        rj[2 * p] = src[col0 + c];
+        rj[2 * p + 1] = src[col0 + c + 1];
+      }
+    }
+  };
+  auto fetch_cl = [&](long k0) {  // clamped loads + selects: the y column, zero padding, rows past kend
+#pragma unroll
+    for (int p = 0; p < T::PER_THREAD / 2; ++p) {
+      const int e2 = tid + NT * p;
+      const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
+      const long k = k0 + r;
+      const long kk = k < kend ? k : (kend - 1);
+      const double yk = yv[kk];
+      const bool kin = k < kend;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int ca = row0 + c + q, cb = col0 + c + q;
+        const double va = H[kk * d + (ca < d ? ca : d - 1)];
+        ri[2 * p + q] = kin ? (ca < d ? va : (ca == d ? yk : 0.0)) : 0.0;
+        if constexpr (!DIAG) {
+          const double vb = H[kk * d + (cb < d ? cb : d - 1)];
+          rj[2 * p + q] = kin ? (cb < d ? vb : (cb == d ? yk : 0.0)) : 0.0;
+        }
+      }
+    }
+  };
+  auto stash = [&](int buf) {
+    double* Si = lds[buf];
+    double* Sj = lds[buf] + BK * T::LDSROW;
+#pragma unroll
+    for (int p = 0; p < T::PER_THREAD / 2; ++p) {
+      const int e2 = tid + NT * p;
+      const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
+      *reinterpret_cast<double2*>(Si + r * T::LDSROW + c) = make_double2(ri[2 * p], ri[2 * p + 1]);
+      if constexpr (!DIAG) *reinterpret_cast<double2*>(Sj + r * T::LDSROW + c) = make_double2(rj[2 * p], rj[2 * p + 1]);
+    }
+  };
+  auto mma = [&](int buf) {
+    const double* Ci = lds[buf];
+    const double* Cb = DIAG ? Ci : lds[buf] + BK * T::LDSROW;
+#pragma unroll
+    for (int ks = 0; ks < BK / 4; ++ks) {
+      const int kr = ks * 4 + (lane >> 4);
+      double a[T::TMR], b[T::TMC];
+#pragma unroll
+      for (int t = 0; t < T::TMR; ++t) a[t] = Ci[kr * T::LDSROW + wr * T::WTR + t * 16 + (lane & 15)];
+#pragma unroll
+      for (int t = 0; t < T::TMC; ++t) b[t] = Cb[kr * T::LDSROW + wc * T::WTC + t * 16 + (lane & 15)];
+#pragma unroll
+      for (int x = 0; x < T::TMR; ++x)
+#pragma unroll
+        for (int yq = 0; yq < T::TMC; ++yq)
+          acc[x][yq] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[x], b[yq], acc[x][yq], 0, 0, 0);
+    }
+  };
+
+  int cur = 0;
+  long k0 = kbeg;
+  if (nfull > 0) {
+    fetch_in(k0);
+    stash(0);
+    lds_barrier();
+    for (long s = 1; s < nfull; ++s) {  // slab s - 1 in LDS buffer cur; slab s loads during its MFMAs
+      fetch_in(k0 + BK);
+      mma(cur);
+      stash(cur ^ 1);  // the other buffer: nobody reads it during this slab
+      lds_barrier();   // slab s visible, and every wave is done reading slab s - 1
+      cur ^= 1;
+      k0 += BK;
+    }
+    mma(cur);
+    lds_barrier();  // every wave is done with the last full slab before any buffer is rewritten
+    cur ^= 1;
+    k0 += BK;
+  }
+  for (; k0 < kend; k0 += BK) {  // synchronous clamped slabs, alternating buffers (one barrier each)
+    fetch_cl(k0);
+    stash(cur);
+    lds_barrier();
+    mma(cur);
+    cur ^= 1;
+  }
+}
+
 template <int BT, int NT>
 __global__ void __launch_bounds__(NT)
 gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int m, int d,
@@ -96,8 +206,6 @@ gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int 
   // into the other one, so each K step needs ONE LDS-only barrier and the staging stores issue
   // behind the MFMAs instead of between two barriers
   __shared__ __attribute__((aligned(16))) double lds[2][2 * BK * T::LDSROW];
-  double* Li = lds[0];
-  double* Lj = lds[0] + BK * T::LDSROW;
 
   const int nwg = gridDim.x;
   const int gid = xcd_remap(blockIdx.x, nwg);
@@ -127,89 +235,12 @@ gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int 
 #pragma unroll
     for (int b = 0; b < T::TMC; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
 
-  // staging: thread t loads slab element pair e2 = t + NT*p  (row = e2 / (BT/2), col = 2 (e2 % (BT/2))).
-  // Interior tiles (every column < d, every row < kend) take branch-free 8-byte loads;
-  // boundary tiles take branch-free clamped loads + selects. A per-element branch around each load
-  // would make hipcc drain vmcnt(0) per element (cdna_hip_programming.md §5, trap (c)).
-  double ri[T::PER_THREAD], rj[T::PER_THREAD];
+  // interior tiles (every column < d) run their full slabs branch-free; see gram_slabs
   const bool cols_in = (row0 + BT <= d) && (diag || col0 + BT <= d);
-  auto fetch = [&](long k0) {
-    const bool interior = cols_in && (k0 + BK <= kend);
-    if (interior) {  // branch-free 8-B loads (measured faster than 16-B loads for every d: tools/gram_ab.py)
-#pragma unroll
-      for (int p = 0; p < T::PER_THREAD / 2; ++p) {
-        const int e2 = tid + NT * p;
-        const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
-        const double* src = H + (k0 + r) * (long)d;
-        ri[2 * p] = src[row0 + c];
-        ri[2 * p + 1] = src[row0 + c + 1];
-        if (!diag) {
-          rj[2 * p] = src[col0 + c];
-          rj[2 * p + 1] = src[col0 + c + 1];
-        }
-      }
-    } else {
-#pragma unroll
-      for (int p = 0; p < T::PER_THREAD / 2; ++p) {
-        const int e2 = tid + NT * p;
-        const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
-        const long k = k0 + r;
-        const long kk = k < kend ? k : (kend - 1);
-        const double yk = yv[kk];
-        const bool kin = k < kend;
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          const int ca = row0 + c + q, cb = col0 + c + q;
-          const double va = H[kk * d + (ca < d ? ca : d - 1)];
-          ri[2 * p + q] = kin ? (ca < d ? va : (ca == d ? yk : 0.0)) : 0.0;
-          if (!diag) {
-            const double vb = H[kk * d + (cb < d ? cb : d - 1)];
-            rj[2 * p + q] = kin ? (cb < d ? vb : (cb == d ? yk : 0.0)) : 0.0;
-          }
-        }
-      }
-    }
-  };
-  auto stash = [&](int buf) {
-    double* Si = lds[buf];
-    double* Sj = lds[buf] + BK * T::LDSROW;
-#pragma unroll
-    for (int p = 0; p < T::PER_THREAD / 2; ++p) {
-      const int e2 = tid + NT * p;
-      const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
-      *reinterpret_cast<double2*>(Si + r * T::LDSROW + c) = make_double2(ri[2 * p], ri[2 * p + 1]);
-      if (!diag) *reinterpret_cast<double2*>(Sj + r * T::LDSROW + c) = make_double2(rj[2 * p], rj[2 * p + 1]);
-    }
-  };
-
+  const long nfull = (cols_in && kend > kbeg) ? (kend - kbeg) / BK : 0;
   if (kbeg < kend) {
-    fetch(kbeg);
-    stash(0);
-  }
-  lds_barrier();
-  int cur = 0;
-  for (long k0 = kbeg; k0 < kend; k0 += BK) {
-    const bool more = k0 + BK < kend;
-    if (more) fetch(k0 + BK);  // next slab into registers (lands during this slab's MFMAs)
-    const double* Ci = lds[cur];
-    const double* Cb = diag ? Ci : lds[cur] + BK * T::LDSROW;
-#pragma unroll
-    for (int ks = 0; ks < BK / 4; ++ks) {
-      const int kr = ks * 4 + (lane >> 4);
-      double a[T::TMR], b[T::TMC];
-#pragma unroll
-      for (int t = 0; t < T::TMR; ++t) a[t] = Ci[kr * T::LDSROW + wr * T::WTR + t * 16 + (lane & 15)];
-#pragma unroll
-      for (int t = 0; t < T::TMC; ++t) b[t] = Cb[kr * T::LDSROW + wc * T::WTC + t * 16 + (lane & 15)];
-#pragma unroll
-      for (int x = 0; x < T::TMR; ++x)
-#pragma unroll
-        for (int yq = 0; yq < T::TMC; ++yq)
-          acc[x][yq] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[x], b[yq], acc[x][yq], 0, 0, 0);
-    }
-    if (more) stash(cur ^ 1);  // the other buffer: nobody reads it during this slab
-    lds_barrier();             // slab s+1 visible, and every wave is done reading slab s
-    cur ^= 1;
+    if (diag) gram_slabs<BT, NT, true>(H, yv, d, kbeg, kend, nfull, row0, col0, lds, acc);
+    else gram_slabs<BT, NT, false>(H, yv, d, kbeg, kend, nfull, row0, col0, lds, acc);
   }
 
   // epilogue
