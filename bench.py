@@ -170,8 +170,10 @@ def run_headline(args, rank, world, device, share):
     if world > 1 and args.engine == "auto":
         # untimed: build and time every eligible multi-GPU engine, agree on the fastest (max over ranks)
         from gadmm_amd.engine.tournament import engine_tournament
+        # a candidate that stalls (e.g. a persistent kernel whose peers cannot be co-resident with ranks
+        # time-sharing one GPU) fails within 5 s instead of the full hand-off deadline
         cands = _headline_candidates(args, X_cpu, y_cpu, local, placement, rank, world, device, share, obj0,
-                                     timeout_s)
+                                     min(timeout_s, 5.0))
         log = (lambda msg: print("bench.py: " + msg, file=sys.stderr, flush=True)) if rank == 0 else None
         name, sol, tournament = engine_tournament(cands, world, solves=3, warm=1, expect=expect,
                                                   sync=lambda: torch.cuda.synchronize(device), log=log)

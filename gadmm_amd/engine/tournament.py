@@ -54,6 +54,8 @@ def engine_tournament(candidates: Sequence[Tuple[str, Callable[[], object]]], wo
     table: List[Dict] = []
     best: Optional[Tuple[float, str, object]] = None
     for name, factory in candidates:
+        if log is not None:
+            log("tournament: building %s" % name)  # progress (a stalled candidate takes its deadline)
         solver, err = None, ""
         try:
             solver = factory()

@@ -925,11 +925,12 @@ def _fo_big_problem(n=4, m=600, d=300):
     return LinearRegression(ds.X, ds.y)
 
 
-@pytest.mark.parametrize("alg", ["GD", "DGD", "LAG-PS", "LAG-WK", "cIAG", "R-IAG", "DualAvg", "DualAvg-J"])
+@pytest.mark.parametrize("alg", ["GD", "DGD", "cIAG", "R-IAG", "DualAvg", "DualAvg-J"])
 def test_first_order_big_matches_torch(alg):
-    """GD / DGD / LAG-PS / LAG-WK / cyclic and randomized IAG / dual averaging (Gauss-Seidel and Jacobi)
-    at d = 300 on the stream-ordered large-d engine (packed Grams, symmetric GEMV, device stop rule) ==
-    the torch loop: objective traces to 1e-9, LAG upload counts equal."""
+    """GD / DGD / cyclic and randomized IAG / dual averaging (Gauss-Seidel and Jacobi) at d = 300 on the
+    stream-ordered large-d engine (packed Grams, symmetric GEMV, device stop rule) == the torch loop:
+    objective traces to 1e-9. (LAG's triggers are comparisons: two summation orders flip near-ties and
+    the runs part ways, so LAG is pinned by the reference goldens below.)"""
     from gadmm_amd.algorithms import gradient_descent, decentralized_gd, lag, iag, dual_averaging, global_constants
     m = _fo_big_problem()
     ids, n, iters = list(range(4)), 4, 300
@@ -952,10 +953,32 @@ def test_first_order_big_matches_torch(alg):
     assert a.extra.get("engine") == "native-big", a.extra.get("engine")
     assert len(a.obj) == len(b.obj) == iters
     np.testing.assert_allclose(a.obj, b.obj, rtol=1e-9, atol=0)
-    if alg.startswith("LAG"):
-        assert a.extra["uploads"] == b.extra["uploads"], (a.extra["uploads"], b.extra["uploads"])
-        assert np.array_equal(a.comm_units, b.comm_units)
     assert np.all(np.diff(a.time_trace) >= 0)
+
+
+def test_first_order_big_lag_goldens(lin24, lin_obj0):
+    """The large-d engine's GD / LAG-PS / LAG-WK logic on the reference problem (run directly at d = 50):
+    the BASELINE.md goldens over the reference budget of 60,000 iterations -- GD first below 1e-4 at
+    53,891; LAG-PS 52,890 with 342,113 uploads; LAG-WK 44,368 with 58,186 uploads."""
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import global_constants
+    from gadmm_amd.engine.first_order_big import FirstOrderBigEngine
+    m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
+    s = global_constants(m)["stepsize"]
+    hsq = m.hmax() ** 2
+    eng = FirstOrderBigEngine(m, n_total=24)
+    N = 24
+
+    def first(o):
+        hit = np.nonzero(np.abs(o["obj"] - lin_obj0) < 1e-4)[0]
+        return int(hit[0]) + 1 if len(hit) else None
+
+    gd = eng.run("GD", 60000, s, lin_obj0, None, True, block=256)
+    assert gd["engine"] == "native-big" and first(gd) == 53891
+    ps = eng.run("LAG-PS", 60000, s, lin_obj0, None, True, thrd=10.0 / (s ** 2 * N ** 2) / 10, hsq=hsq, block=256)
+    assert first(ps) == 52890 and int(ps["uploads"]) == 342113, (first(ps), ps["uploads"])
+    wk = eng.run("LAG-WK", 60000, s, lin_obj0, None, True, thrd=1.0 / (s ** 2 * N ** 2) / 10, hsq=hsq, block=256)
+    assert first(wk) == 44368 and int(wk["uploads"]) == 58186, (first(wk), wk["uploads"])
 
 
 def test_first_order_big_stops_on_device():
