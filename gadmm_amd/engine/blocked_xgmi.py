@@ -71,7 +71,8 @@ class BlockedXgmiEngine:
 
     def __init__(self, X_all: torch.Tensor, y_all: torch.Tensor, n_total: int, placement: Placement, rank: int,
                  rho: float, obj0: float, tol: float, max_iter: int, device: torch.device, group=None,
-                 want_k: int = 0, data_local: bool = False, dl_halo: Optional[bool] = None):
+                 want_k: int = 0, data_local: bool = False, dl_halo: Optional[bool] = None,
+                 stream: Optional[torch.cuda.Stream] = None):
         """Collective over ``group``. ``data_local=False``: ``X_all`` / ``y_all`` hold the shards of at
         least this rank's computed range (indexable by global worker id); only those rows are read.
         ``data_local=True``: ``X_all`` / ``y_all`` are this rank's own shards, in segment order.
@@ -134,7 +135,7 @@ class BlockedXgmiEngine:
         else:
             self.X = X_all[ext].to(device).contiguous()
             self.y = y_all[ext].to(device).contiguous()
-        self.stream = torch.cuda.Stream(device)
+        self.stream = stream if stream is not None else torch.cuda.Stream(device)
         with torch.cuda.stream(self.stream):
             self.A, self.b, self.yy = gram(self.X, self.y)
             self._inverses()

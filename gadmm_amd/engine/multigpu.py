@@ -54,6 +54,23 @@ def all_ok(flag: bool, world: int) -> bool:
     return float(t.item()) == 0.0
 
 
+_STREAMS: dict = {}
+
+
+def solver_stream(device: torch.device) -> torch.cuda.Stream:
+    """One engine stream per process and device, shared by every DistributedChainSolver (the engine
+    tournament builds several): persistent kernels of several ranks must run at the same time, and with
+    ranks time-sharing one GPU every extra stream a process touches is one more hardware queue for the
+    GPU's scheduler to multiplex -- past its slots, queues are time-sliced and cross-rank hand-offs stall
+    until their deadline (8 ranks on one MI355X, the second tournament candidate on)."""
+    key = torch.device(device).index
+    st = _STREAMS.get(key)
+    if st is None:
+        st = torch.cuda.Stream(device)
+        _STREAMS[key] = st
+    return st
+
+
 class DistributedChainSolver:
     def __init__(self, X_loc: torch.Tensor, y_loc: torch.Tensor, local: Sequence[int], n_total: int, placement,
                  rank: int, world: int, device: torch.device, rho: float, obj0: float, tol: float,
@@ -88,7 +105,7 @@ class DistributedChainSolver:
             if halo_data is None:
                 raise ValueError("replicated-halo needs the halo workers' shards (halo_data=(X_all, y_all))")
             self.blk = BlockedXgmiEngine(halo_data[0], halo_data[1], n_total, placement, rank, rho, obj0, tol,
-                                         max_iter, device)
+                                         max_iter, device, stream=solver_stream(device))
             self.replicated_bytes = self.blk.replicated_shard_bytes()
             self.persistent, self.kind = True, "xgmi(replicated-halo)"
         else:
@@ -104,7 +121,7 @@ class DistributedChainSolver:
     # ---------------------------------------------------------------------------------------------
     def _engine(self, comm):
         e = self._NCE(self.X, self.y, self.local, self.n, "linear", rho=self.rho, obj0=self.obj0, tol=self.tol,
-                      max_iter=self.max_iter, comm=comm, block=self.block)
+                      max_iter=self.max_iter, comm=comm, block=self.block, stream=solver_stream(self.device))
         e.set_path(self.path, self.placement, self.rank)
         return e
 
@@ -118,7 +135,8 @@ class DistributedChainSolver:
             return
         try:
             blk = BlockedXgmiEngine(self.X, self.y, self.n, self.placement, self.rank, self.rho, self.obj0, self.tol,
-                                    self.max_iter, self.device, data_local=True, dl_halo=self.dl_halo)
+                                    self.max_iter, self.device, data_local=True, dl_halo=self.dl_halo,
+                                    stream=solver_stream(self.device))
         except Exception as e:  # collective inside the constructor: every rank raises together
             if self.rank == 0:
                 print("DistributedChainSolver: data-local blocked fabric unavailable (%s)" % e, file=sys.stderr)
