@@ -14,12 +14,13 @@ constexpr int RPW = 2;  // rows per wave
 constexpr int ROWS_PER_WG = RPW * (NT / 64);
 
 // A worker's r-buffer (large-d kernels): [ r, zero padded to symv::padded(d) | one objective partial per
-// row-GEMV workgroup + 1 | the symmetric GEMV's partial table P (symv::part_doubles) ]. The padding
-// stays zero (allocated zeroed, only r[0, d) is ever written): the packed GEMV reads whole blocks of r.
+// row-GEMV workgroup + 1 | two partials per symmetric-GEMV block row (objective, primal residual: the
+// reduce kernels' fused elementwise tails) | the symmetric GEMV's partial table P (symv::part_doubles) ].
+// The padding stays zero (allocated zeroed, only r[0, d) is ever written): the packed GEMV reads whole
+// blocks of r.
 __device__ __host__ __forceinline__ long obj_off(int d) { return symv::padded(d); }
-__device__ __host__ __forceinline__ long part_off(int d) {
-  return (obj_off(d) + (d + ROWS_PER_WG - 1) / ROWS_PER_WG + 1 + 31) / 32 * 32;
-}
+__device__ __host__ __forceinline__ long fz_off(int d) { return obj_off(d) + (d + ROWS_PER_WG - 1) / ROWS_PER_WG + 1; }
+__device__ __host__ __forceinline__ long part_off(int d) { return (fz_off(d) + 2L * symv::nblk(d) + 31) / 32 * 32; }
 __device__ __host__ __forceinline__ long rstride(int d) { return part_off(d) + symv::part_doubles(d); }
 
 // y[row] = sum_j M[row][j] x[j] for RPW consecutive rows per wave; returns sums on lane 0.

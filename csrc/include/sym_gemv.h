@@ -14,7 +14,7 @@
 //               two columns -- one 1-KiB contiguous load per row; the transposed sums accumulate in the
 //               lane's registers, the direct ones are row sums across the wave, folded by a 5-stage
 //               reduce-scatter of 32 rows over the 64 lanes: one shuffle per row instead of six)
-//   sym_reduce  y[t B + k] = sum_s P[t][s][k] in fixed s order
+//   sym_reduce  y[t B + k] = sum_s P[t][s][k] in a fixed order (reduce_row: RG groups of s per block row)
 // Every partial has exactly one writer and the reduction order is fixed: deterministic.
 #pragma once
 #include "gadmm_common.h"
@@ -99,12 +99,34 @@ __device__ __forceinline__ void part_block(const double* __restrict__ Mp, const 
   }
 }
 
-// y[t B + k] (< d) = sum_s P[t][s][k]; one workgroup of B threads per block row t.
-__device__ __forceinline__ double reduce_elem(const double* __restrict__ P, int nb, int t, int k) {
-  double s = 0.0;
+// y[t B + k] (< d) = sum_s P[t][s][k] for one block row t, by a workgroup of RNT = RG x B threads:
+// thread (g, k) sums the s of group g = [g S, (g + 1) S) (S = ceil(nb / RG), eight loads in flight at a
+// time), then thread (0, k) adds the RG group sums in group order. Fixed order, so deterministic; the
+// whole workgroup must call it (one barrier). Valid in the threads < B (k = threadIdx.x).
+constexpr int RG = 8;
+constexpr int RNT = RG * B;
+
+__device__ __forceinline__ double reduce_row(const double* __restrict__ P, int nb, int t, double (*red)[B]) {
+  const int k = threadIdx.x & (B - 1), g = threadIdx.x / B;
+  const int per = (nb + RG - 1) / RG, s0 = g * per, s1 = s0 + per < nb ? s0 + per : nb;
   const double* q = P + (long)t * nb * B + k;
-  for (int src = 0; src < nb; ++src) s += q[(long)src * B];
-  return s;
+  double acc = 0.0;
+  for (int s = s0; s < s1; s += 8) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = s + u < s1 ? q[(long)(s + u) * B] : 0.0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += v[u];
+  }
+  red[g][k] = acc;
+  __syncthreads();
+  double y = 0.0;
+  if (g == 0) {
+    y = red[0][k];
+#pragma unroll
+    for (int h = 1; h < RG; ++h) y += red[h][k];
+  }
+  return y;
 }
 
 }  // namespace symv

@@ -5,7 +5,9 @@
 //   chain_big_sym_* th_n = (A_n + deg rho I)^{-1} r_n            the inverse stored as its block-packed
 //                   lower triangle (sym_gemv.h: half the bytes of the full matrix), partials + reduce
 //   [chain_big_obj] (A_n th_n)_i -> per-workgroup objective partials   (exact objective mode)
-//   chain_big_post  tail dual update, local objective, last-arriver iteration close
+//                   (the reduce also applies the tail dual update and emits per-row objective /
+//                   residual partials)
+//   chain_big_post  per-worker sums of those partials, local objective, last-arriver iteration close
 // Every load of the matrix is a contiguous 1-KiB wave access, every reduction has a fixed order
 // (deterministic). r (80 KB) is re-read from L2 by every workgroup.
 // Objective, exact mode: f = sum_i (1/2 (A th)_i - b_i) th_i + 1/2 y^T y with partials per workgroup
@@ -66,12 +68,48 @@ __global__ void __launch_bounds__(symv::NT) chain_big_sym_part(PhaseArgs a) {
   symv::part_block(Mp, rb, rb + part_off(d), symv::nblk(d), blockIdx.x, tl);
 }
 
-__global__ void __launch_bounds__(symv::B) chain_big_sym_reduce(PhaseArgs a) {
+// th_n: the fixed-order reduction of the block partials straight into the theta table, fused with the
+// elementwise tail of the phase -- the tails' dual update, the K4 primal residual and the identity-mode
+// objective term of every element -- whose per-block-row partials chain_big_post sums in row order
+__global__ void __launch_bounds__(symv::RNT) chain_big_sym_reduce(PhaseArgs a) {
+  __shared__ double red[symv::RG][symv::B];
+  __shared__ double wpart[2][2];
   if (a.ctl->done) return;
   const SlotView s = slot_view(a, blockIdx.y);
-  const int d = a.d, t = blockIdx.x, k = threadIdx.x;
-  const double y = symv::reduce_elem(a.rbuf + s.li * rstride(d) + part_off(d), symv::nblk(d), t, k);
-  if (t * symv::B + k < d) a.theta[(long)s.gid * d + t * symv::B + k] = y;
+  const int d = a.d, t = blockIdx.x, k = threadIdx.x, j = t * symv::B + k;
+  const int lane = k & 63, w = k >> 6;
+  double* rb = a.rbuf + s.li * rstride(d);
+  const double y = symv::reduce_row(rb + part_off(d), symv::nblk(d), t, red);
+  double po = 0.0, pr = 0.0;
+  if (k < symv::B && j < d) {
+    const long dl = d;
+    const double* th = a.theta;
+    a.theta[s.gid * dl + j] = y;
+    if (a.flags & PH_POST_DUAL) {
+      const double tl = s.left >= 0 ? th[s.left * dl + j] : 0.0;
+      const double tr = s.right >= 0 ? th[s.right * dl + j] : 0.0;
+      double m = a.mu[s.li * dl + j];
+      if (s.left >= 0) m = m - a.rho * (tl - y);
+      if (s.right >= 0) m = m + a.rho * (y - tr);
+      a.mu[s.li * dl + j] = m;
+      if (s.left >= 0) pr = fma(tl - y, tl - y, pr);
+      if (s.right >= 0) pr = fma(y - tr, y - tr, pr);
+    }
+    if (a.obj_mode != 0) po = (0.5 * (rb[j] - s.deg * a.rho * y) - a.b[s.li * dl + j]) * y;
+  }
+  if (w < 2) {  // the B = 2 waves that own elements (wave-uniform)
+    po = wave_sum_f64(po);
+    pr = wave_sum_f64(pr);
+    if (lane == 0) {
+      wpart[w][0] = po;
+      wpart[w][1] = pr;
+    }
+  }
+  __syncthreads();
+  if (k == 0) {
+    rb[fz_off(d) + t] = wpart[0][0] + wpart[1][0];
+    rb[fz_off(d) + symv::nblk(d) + t] = wpart[0][1] + wpart[1][1];
+  }
 }
 
 // exact objective: per-workgroup partial of sum_i (1/2 (A th)_i - b_i) th_i
@@ -101,47 +139,31 @@ __global__ void __launch_bounds__(NT) chain_big_obj(PhaseArgs a) {
   }
 }
 
-__global__ void __launch_bounds__(1024) chain_big_post(PhaseArgs a) {
+// the phase's per-worker sums (fixed order: strided per thread, then the block reduction), the local
+// objective, and the last arriver's iteration close
+__global__ void __launch_bounds__(256) chain_big_post(PhaseArgs a) {
   __shared__ double scratch[16];
   __shared__ int flag_lds;
   if (a.ctl->done) return;
   const int it = a.ctl->iter;
   const SlotView s = slot_view(a, blockIdx.x);
-  const long d = a.d;
-  const double* th = a.theta;
   const double* r = a.rbuf + s.li * rstride(a.d);
-  const double crho = s.deg * a.rho;
-  double part = 0.0, rpart = 0.0;
-  for (long j = threadIdx.x; j < d; j += blockDim.x) {
-    const double t = th[s.gid * d + j];
-    if (a.flags & PH_POST_DUAL) {
-      double m = a.mu[s.li * d + j];
-      if (s.left >= 0) m = m - a.rho * (th[s.left * d + j] - t);
-      if (s.right >= 0) m = m + a.rho * (t - th[s.right * d + j]);
-      a.mu[s.li * d + j] = m;
-      if (a.rres) {  // K4 primal residual of the tail's two edges
-        if (s.left >= 0) rpart = fma(th[s.left * d + j] - t, th[s.left * d + j] - t, rpart);
-        if (s.right >= 0) rpart = fma(t - th[s.right * d + j], t - th[s.right * d + j], rpart);
-      }
-    }
-    if (a.obj_mode != 0) part += (0.5 * (r[j] - crho * t) - a.b[s.li * d + j]) * t;
-  }
-  if (a.rres && (a.flags & PH_POST_DUAL)) {
-    const double rs = block_sum_f64(rpart, scratch);
+  const int nbr = symv::nblk(a.d);
+  if (a.rres && (a.flags & PH_POST_DUAL)) {  // K4 primal residual of the tail's two edges
+    double t = 0.0;
+    for (int k = threadIdx.x; k < nbr; k += blockDim.x) t += r[fz_off(a.d) + nbr + k];
+    const double rs = block_sum_f64(t, scratch);
     if (threadIdx.x == 0 && it - 1 < a.max_iter) a.rres[(long)(it - 1) * a.n_total + s.gid] = rs;
     __syncthreads();  // scratch is reused below
   }
-  double f;
+  double t = 0.0;
   if (a.obj_mode != 0) {
-    f = block_sum_f64(part, scratch);
-  } else {
-    // fixed-order sum of the per-workgroup partials of chain_big_obj: strided per thread, then the
-    // deterministic block reduction (same order every call)
+    for (int k = threadIdx.x; k < nbr; k += blockDim.x) t += r[fz_off(a.d) + k];
+  } else {  // chain_big_obj's per-workgroup partials
     const int nblk = (a.d + ROWS_PER_WG - 1) / ROWS_PER_WG;
-    double t = 0.0;
     for (int k = threadIdx.x; k < nblk; k += blockDim.x) t += r[obj_off(a.d) + k];
-    f = block_sum_f64(t, scratch);
   }
+  const double f = block_sum_f64(t, scratch);
   if (threadIdx.x == 0) a.objw[s.li] = f + 0.5 * a.yy[s.li];
   if (a.flags & PH_FINISH) {
     if (phase_arrive(a.ctl, a.n_slots, &flag_lds)) finish_iteration(a, it);
@@ -198,10 +220,10 @@ int gadmm_chain_phase_big(const PhaseArgs* args, hipStream_t st) {
   hipLaunchKernelGGL(chain_big_rhs, dim3((d + NT - 1) / NT, a.n_slots), dim3(NT), 0, st, a);
   const int nblk = (d + ROWS_PER_WG - 1) / ROWS_PER_WG;
   hipLaunchKernelGGL(chain_big_sym_part, dim3((unsigned)symv::nstored(d), a.n_slots), dim3(symv::NT), 0, st, a);
-  hipLaunchKernelGGL(chain_big_sym_reduce, dim3(symv::nblk(d), a.n_slots), dim3(symv::B), 0, st, a);
+  hipLaunchKernelGGL(chain_big_sym_reduce, dim3(symv::nblk(d), a.n_slots), dim3(symv::RNT), 0, st, a);
   if (a.obj_mode == 0 && (a.flags & PH_OBJ))
     hipLaunchKernelGGL(chain_big_obj, dim3(nblk, a.n_slots), dim3(NT), 0, st, a);
-  hipLaunchKernelGGL(chain_big_post, dim3(a.n_slots), dim3(1024), 0, st, a);
+  hipLaunchKernelGGL(chain_big_post, dim3(a.n_slots), dim3(256), 0, st, a);
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

@@ -34,12 +34,13 @@ __global__ void __launch_bounds__(symv::NT) fob_symv_part(const double* Mp, long
   symv::part_block(Mp + s * mstride, x + s * xstride, work + s * symv::part_doubles(d), symv::nblk(d), blockIdx.x, tl);
 }
 
-__global__ void __launch_bounds__(symv::B) fob_symv_reduce(const double* work, double* y, long ystride, int d,
-                                                           const ChainCtl* ctl) {
+__global__ void __launch_bounds__(symv::RNT) fob_symv_reduce(const double* work, double* y, long ystride, int d,
+                                                             const ChainCtl* ctl) {
+  __shared__ double red[symv::RG][symv::B];
   if (ctl && ctl->done) return;
   const int s = blockIdx.y, t = blockIdx.x, k = threadIdx.x, j = t * symv::B + k;
-  const double v = symv::reduce_elem(work + s * symv::part_doubles(d), symv::nblk(d), t, k);
-  if (j < d) y[s * ystride + j] = v;
+  const double v = symv::reduce_row(work + s * symv::part_doubles(d), symv::nblk(d), t, red);
+  if (k < symv::B && j < d) y[s * ystride + j] = v;
 }
 
 __device__ __forceinline__ double block_sum(double v, double* sh) {
@@ -298,7 +299,7 @@ int gadmm_symv_batch(const double* Mp, long mstride, const double* x, long xstri
   }
   hipLaunchKernelGGL(fob_symv_part, dim3((unsigned)symv::nstored(d), count), dim3(symv::NT), 0, st, Mp, mstride, x,
                      xstride, work, d, ctl);
-  hipLaunchKernelGGL(fob_symv_reduce, dim3(symv::nblk(d), count), dim3(symv::B), 0, st, work, y, ystride, d, ctl);
+  hipLaunchKernelGGL(fob_symv_reduce, dim3(symv::nblk(d), count), dim3(symv::RNT), 0, st, work, y, ystride, d, ctl);
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

@@ -73,13 +73,14 @@ __global__ void __launch_bounds__(symv::NT) sb_sym_part(StarBigArgs a, int hub) 
   symv::part_block(a.Minv + (long)s * symv::packed_doubles(d), rb, rb + part_off(d), symv::nblk(d), blockIdx.x, tl);
 }
 
-__global__ void __launch_bounds__(symv::B) sb_sym_reduce(StarBigArgs a, int hub) {
+__global__ void __launch_bounds__(symv::RNT) sb_sym_reduce(StarBigArgs a, int hub) {
+  __shared__ double red[symv::RG][symv::B];
   if (a.ctl->done) return;
   const int s = blockIdx.y;
   if ((s == a.hub_li) != (hub != 0)) return;
   const int d = a.d, t = blockIdx.x, k = threadIdx.x, j = t * symv::B + k;
-  const double y = symv::reduce_elem(a.rbuf + s * rstride(d) + part_off(d), symv::nblk(d), t, k);
-  if (j < d) {
+  const double y = symv::reduce_row(a.rbuf + s * rstride(d) + part_off(d), symv::nblk(d), t, red);
+  if (k < symv::B && j < d) {
     a.theta[(long)s * d + j] = y;
     if (hub) a.th_hub[j] = y;
   }
@@ -136,35 +137,46 @@ __global__ void __launch_bounds__(NT) sb_obj(StarBigArgs a) {
   }
 }
 
-// dual update (non-hub workers) and the local objective of every local worker
-__global__ void __launch_bounds__(1024) sb_post(StarBigArgs a) {
-  __shared__ double scratch[16];
+// dual update (non-hub workers) and the objective term of every element, one block row of B elements
+// per workgroup; per-row partials into the worker's r-buffer (sb_local_obj sums them in row order)
+__global__ void __launch_bounds__(symv::B) sb_post(StarBigArgs a) {
+  __shared__ double wpart[symv::B / 64];
   if (a.ctl->done) return;
-  const int s = blockIdx.x;
+  const int s = blockIdx.y, t = blockIdx.x, k = threadIdx.x, j = t * symv::B + k;
   const long d = a.d;
   const bool hub = s == a.hub_li;
   const double c = hub ? (double)(a.n_total - 1) * a.rho : a.rho;
-  const double* r = a.rbuf + s * rstride(a.d);
+  double* r = a.rbuf + s * rstride(a.d);
   double part = 0.0;
-  for (long j = threadIdx.x; j < d; j += blockDim.x) {
-    const double t = a.theta[s * d + j];
-    if (!hub) a.lam[s * d + j] += a.rho * (t - a.th_hub[j]);
-    if (a.obj_mode != 0) part += (0.5 * (r[j] - c * t) - a.b[s * d + j]) * t;
+  if (j < d) {
+    const double th = a.theta[s * d + j];
+    if (!hub) a.lam[s * d + j] += a.rho * (th - a.th_hub[j]);
+    if (a.obj_mode != 0) part = (0.5 * (r[j] - c * th) - a.b[s * d + j]) * th;
   }
-  double f;
-  if (a.obj_mode != 0) {
-    f = block_sum_f64(part, scratch);
-  } else {
-    const int nblk = (a.d + ROWS_PER_WG - 1) / ROWS_PER_WG;
-    double t = 0.0;
-    for (int k = threadIdx.x; k < nblk; k += blockDim.x) t += r[obj_off(a.d) + k];
-    f = block_sum_f64(t, scratch);
-  }
-  if (threadIdx.x == 0) a.objw[s] = f + 0.5 * a.yy[s];
+  part = wave_sum_f64(part);
+  if ((k & 63) == 0) wpart[k >> 6] = part;
+  __syncthreads();
+  if (k == 0) r[fz_off(a.d) + t] = wpart[0] + wpart[1];
 }
 
-__global__ void sb_local_obj(StarBigArgs a) {
+// the local objectives (fixed order: strided per thread, then the block reduction) and this rank's
+// per-global-worker objective slots
+__global__ void __launch_bounds__(256) sb_local_obj(StarBigArgs a) {
+  __shared__ double scratch[16];
   if (a.ctl->done) return;
+  const int nbr = symv::nblk(a.d), nblk = (a.d + ROWS_PER_WG - 1) / ROWS_PER_WG;
+  for (int s = 0; s < a.n_local; ++s) {
+    const double* r = a.rbuf + s * rstride(a.d);
+    double t = 0.0;
+    if (a.obj_mode != 0) {
+      for (int k = threadIdx.x; k < nbr; k += blockDim.x) t += r[fz_off(a.d) + k];
+    } else {  // sb_obj's per-workgroup partials
+      for (int k = threadIdx.x; k < nblk; k += blockDim.x) t += r[obj_off(a.d) + k];
+    }
+    const double f = block_sum_f64(t, scratch);
+    if (threadIdx.x == 0) a.objw[s] = f + 0.5 * a.yy[s];
+    __syncthreads();  // scratch is reused by the next worker
+  }
   for (int g = threadIdx.x; g < a.n_total; g += blockDim.x) a.objp[g] = 0.0;
   __syncthreads();
   for (int s = threadIdx.x; s < a.n_local; s += blockDim.x) a.objp[a.gid[s]] = a.objw[s];
@@ -224,7 +236,7 @@ int gadmm_star_big_workers(const StarBigArgs* args, hipStream_t st) {
   (void)nblk;
   hipLaunchKernelGGL(sb_rhs, dim3(nb, a.n_local), dim3(NT), 0, st, a);
   hipLaunchKernelGGL(sb_sym_part, dim3((unsigned)symv::nstored(d), a.n_local), dim3(symv::NT), 0, st, a, 0);
-  hipLaunchKernelGGL(sb_sym_reduce, dim3(symv::nblk(d), a.n_local), dim3(symv::B), 0, st, a, 0);
+  hipLaunchKernelGGL(sb_sym_reduce, dim3(symv::nblk(d), a.n_local), dim3(symv::RNT), 0, st, a, 0);
   hipLaunchKernelGGL(sb_sum, dim3(nb), dim3(NT), 0, st, a);
   GADMM_CHECK(hipGetLastError());
   return 0;
@@ -238,7 +250,7 @@ int gadmm_star_big_hub(const StarBigArgs* args, hipStream_t st) {
   (void)nblk;
   hipLaunchKernelGGL(sb_hubrhs, dim3(nb), dim3(NT), 0, st, a);
   hipLaunchKernelGGL(sb_sym_part, dim3((unsigned)symv::nstored(d), a.n_local), dim3(symv::NT), 0, st, a, 1);
-  hipLaunchKernelGGL(sb_sym_reduce, dim3(symv::nblk(d), a.n_local), dim3(symv::B), 0, st, a, 1);
+  hipLaunchKernelGGL(sb_sym_reduce, dim3(symv::nblk(d), a.n_local), dim3(symv::RNT), 0, st, a, 1);
   GADMM_CHECK(hipGetLastError());
   return 0;
 }
@@ -248,8 +260,8 @@ int gadmm_star_big_post(const StarBigArgs* args, hipStream_t st) {
   const StarBigArgs& a = *args;
   const int d = a.d, nblk = (d + ROWS_PER_WG - 1) / ROWS_PER_WG;
   if (a.obj_mode == 0) hipLaunchKernelGGL(sb_obj, dim3(nblk, a.n_local), dim3(NT), 0, st, a);
-  hipLaunchKernelGGL(sb_post, dim3(a.n_local), dim3(1024), 0, st, a);
-  hipLaunchKernelGGL(sb_local_obj, dim3(1), dim3(64), 0, st, a);
+  hipLaunchKernelGGL(sb_post, dim3(symv::nblk(d), a.n_local), dim3(symv::B), 0, st, a);
+  hipLaunchKernelGGL(sb_local_obj, dim3(1), dim3(256), 0, st, a);
   GADMM_CHECK(hipGetLastError());
   return 0;
 }
