@@ -91,9 +91,10 @@ struct GramTile {
 // flight across the current slab's MFMAs (the wait lands right before the stash). With a branch (the
 // old `if (interior) ... else ...` / `if (!diag)` fetch), the compiler merged the two paths' registers
 // with moves right after the loads and drained vmcnt(0) there, exposing the load latency on every slab.
-// The remaining rows (every slab of a tile with columns past the shard, the partial last slab) take
-// synchronous clamped loads. Same MFMA order either way (bit-identical results).
-template <int BT, int NT, bool DIAG>
+// Tiles with columns past the shard (the y column, the zero padding) run the same pipelined loop with
+// clamped loads + selects (CLAMP); only the partial last slab takes the synchronous clamped path.
+// Same MFMA order either way (bit-identical results).
+template <int BT, int NT, bool DIAG, bool CLAMP>
 __device__ __forceinline__ void gram_slabs(const double* __restrict__ H, const double* __restrict__ yv, int d,
                                            long kbeg, long kend, long nfull, int row0, int col0,
                                            double (*lds)[2 * BK * GramTile<BT, NT>::LDSROW],
@@ -167,14 +168,18 @@ __device__ __forceinline__ void gram_slabs(const double* __restrict__ H, const d
     }
   };
 
+  auto fetch = [&](long k0) {
+    if constexpr (CLAMP) fetch_cl(k0);
+    else fetch_in(k0);
+  };
   int cur = 0;
   long k0 = kbeg;
   if (nfull > 0) {
-    fetch_in(k0);
+    fetch(k0);
     stash(0);
     lds_barrier();
     for (long s = 1; s < nfull; ++s) {  // slab s - 1 in LDS buffer cur; slab s loads during its MFMAs
-      fetch_in(k0 + BK);
+      fetch(k0 + BK);
       mma(cur);
       stash(cur ^ 1);  // the other buffer: nobody reads it during this slab
       lds_barrier();   // slab s visible, and every wave is done reading slab s - 1
@@ -235,12 +240,18 @@ gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int 
 #pragma unroll
     for (int b = 0; b < T::TMC; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
 
-  // interior tiles (every column < d) run their full slabs branch-free; see gram_slabs
+  // every tile runs its full slabs in the pipelined loop: interior tiles (every column < d) with
+  // branch-free loads, boundary tiles (the y column, zero padding) with the clamped ones; see gram_slabs
   const bool cols_in = (row0 + BT <= d) && (diag || col0 + BT <= d);
-  const long nfull = (cols_in && kend > kbeg) ? (kend - kbeg) / BK : 0;
+  const long nfull = kend > kbeg ? (kend - kbeg) / BK : 0;
   if (kbeg < kend) {
-    if (diag) gram_slabs<BT, NT, true>(H, yv, d, kbeg, kend, nfull, row0, col0, lds, acc);
-    else gram_slabs<BT, NT, false>(H, yv, d, kbeg, kend, nfull, row0, col0, lds, acc);
+    if (cols_in) {
+      if (diag) gram_slabs<BT, NT, true, false>(H, yv, d, kbeg, kend, nfull, row0, col0, lds, acc);
+      else gram_slabs<BT, NT, false, false>(H, yv, d, kbeg, kend, nfull, row0, col0, lds, acc);
+    } else {
+      if (diag) gram_slabs<BT, NT, true, true>(H, yv, d, kbeg, kend, nfull, row0, col0, lds, acc);
+      else gram_slabs<BT, NT, false, true>(H, yv, d, kbeg, kend, nfull, row0, col0, lds, acc);
+    }
   }
 
   // epilogue

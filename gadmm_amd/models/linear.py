@@ -11,12 +11,23 @@ from typing import Optional
 
 import torch
 
-from ..ops.linalg import gram, spd_inverse
+from ..ops.linalg import gram, spd_inverse, spd_inverse_blocked
 
 
 def _spd_solve(M: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
     """Solve the SPD normal equations by Cholesky (half the flops of LU, no pivoting); LU only if
-    the factorisation reports the matrix is not positive definite."""
+    the factorisation reports the matrix is not positive definite. On a HIP device with d > 256 (the
+    real-shaped oracle, inside the timed set-up of the 10M x 10k config): the native blocked
+    Gauss-Jordan inverse (f64 MFMA, csrc/kernels/spd_inverse_blocked.hip) and one GEMV. rocSOLVER's
+    potrf / trsv spent ~0.3 s there, mostly first-call library loading between their kernels
+    (profiles/r04_real10m), against ~50 ms for the inverse."""
+    if M.is_cuda and M.shape[-1] > 256:
+        st = torch.zeros((1,), dtype=torch.int32, device=M.device)
+        inv = spd_inverse_blocked(M.unsqueeze(0), torch.zeros((1, 1), dtype=torch.float64), check_status=False,
+                                  status=st)[0, 0]
+        if int(st.item()) == 0:
+            return torch.mv(inv, r)
+        del inv
     L, info = torch.linalg.cholesky_ex(M)
     if int(info.item()) != 0:
         return torch.linalg.solve(M, r)
@@ -137,9 +148,11 @@ class LinearRegression:
             As = buf[: d * d].reshape(d, d)
             bs = buf[d * d: d * d + d]
             yy = buf[-1]
-        eye = torch.eye(self.d, dtype=As.dtype, device=As.device)
         lam_tot = self.lam * (n_total if n_total is not None else self.n_local)
-        x = _spd_solve(As + lam_tot * eye, bs)
+        if lam_tot:  # ridge: the diagonal only (no d x d identity: 800 MB at d = 10k)
+            As = As.clone()
+            As.diagonal().add_(lam_tot)
+        x = _spd_solve(As, bs)
         r = torch.matmul(self.X.to(x.dtype), x) - self.y.to(x.dtype)  # (n_loc, m) residuals
         f = (0.5 * (r * r).sum()).reshape(1)
         if comm is not None and comm.nranks > 1:
