@@ -7,6 +7,7 @@ per-iteration quantities are O(d^2) in these, independent of the shard height m.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -21,7 +22,7 @@ def _spd_solve(M: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
     Gauss-Jordan inverse (f64 MFMA, csrc/kernels/spd_inverse_blocked.hip) and one GEMV. rocSOLVER's
     potrf / trsv spent ~0.3 s there, mostly first-call library loading between their kernels
     (profiles/r04_real10m), against ~50 ms for the inverse."""
-    if M.is_cuda and M.shape[-1] > 256:
+    if M.is_cuda and M.shape[-1] > 256 and os.environ.get("GADMM_OPT_SOLVER", "native") != "rocsolver":
         st = torch.zeros((1,), dtype=torch.int32, device=M.device)
         inv = spd_inverse_blocked(M.unsqueeze(0), torch.zeros((1, 1), dtype=torch.float64), check_status=False,
                                   status=st)[0, 0]
