@@ -316,7 +316,7 @@ def test_stalled_peer_every_rank_falls_back_together():
     from gadmm_amd.parallel.launch import spawn
     res = spawn(_solver_rank, 2, 24, 1, 2.0, timeout=300)
     for r in res:
-        assert r["kind0"] == "xgmi(blocked-dl)" and r["kind"] == "ipc"
+        assert r["kind0"] in ("xgmi(blocked-dl)", "xgmi(blocked-dl-halo)") and r["kind"] == "ipc"  # halo hosted at 2 ranks
         assert len(r["fallbacks"]) == 1
         assert [o[:2] for o in r["outs"]] == [(1373, 1), (1373, 1)]
 
