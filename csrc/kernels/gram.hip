@@ -138,7 +138,44 @@ __device__ __forceinline__ void gram_slabs(const double* __restrict__ H, const d
       }
     }
   };
+  // CLAMP tiles in the pipelined loop: raw clamped loads at the top of a slab (fetch_raw), the selects
+  // (y column, zero padding, rows past kend) applied at the stash, after the MFMAs, so the loads stay
+  // in flight across them like fetch_in's
+  double yr[CLAMP ? T::PER_THREAD / 2 : 1];
+  long kraw = 0;
+  auto fetch_raw = [&](long k0) {
+    kraw = k0;
+#pragma unroll
+    for (int p = 0; p < T::PER_THREAD / 2; ++p) {
+      const int e2 = tid + NT * p;
+      const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
+      const long k = k0 + r;
+      const long kk = k < kend ? k : (kend - 1);
+      yr[p] = yv[kk];
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int ca = row0 + c + q, cb = col0 + c + q;
+        ri[2 * p + q] = H[kk * d + (ca < d ? ca : d - 1)];
+        if constexpr (!DIAG) rj[2 * p + q] = H[kk * d + (cb < d ? cb : d - 1)];
+      }
+    }
+  };
+  auto select_raw = [&]() {
+#pragma unroll
+    for (int p = 0; p < T::PER_THREAD / 2; ++p) {
+      const int e2 = tid + NT * p;
+      const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
+      const bool kin = kraw + r < kend;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int ca = row0 + c + q, cb = col0 + c + q;
+        ri[2 * p + q] = kin ? (ca < d ? ri[2 * p + q] : (ca == d ? yr[p] : 0.0)) : 0.0;
+        if constexpr (!DIAG) rj[2 * p + q] = kin ? (cb < d ? rj[2 * p + q] : (cb == d ? yr[p] : 0.0)) : 0.0;
+      }
+    }
+  };
   auto stash = [&](int buf) {
+    if constexpr (CLAMP) select_raw();
     double* Si = lds[buf];
     double* Sj = lds[buf] + BK * T::LDSROW;
 #pragma unroll
@@ -169,7 +206,7 @@ __device__ __forceinline__ void gram_slabs(const double* __restrict__ H, const d
   };
 
   auto fetch = [&](long k0) {
-    if constexpr (CLAMP) fetch_cl(k0);
+    if constexpr (CLAMP) fetch_raw(k0);
     else fetch_in(k0);
   };
   int cur = 0;
@@ -192,7 +229,8 @@ __device__ __forceinline__ void gram_slabs(const double* __restrict__ H, const d
     k0 += BK;
   }
   for (; k0 < kend; k0 += BK) {  // synchronous clamped slabs, alternating buffers (one barrier each)
-    fetch_cl(k0);
+    if constexpr (CLAMP) fetch_raw(k0);  // selected by the stash
+    else fetch_cl(k0);
     stash(cur);
     lds_barrier();
     mma(cur);
@@ -296,14 +334,14 @@ __device__ __forceinline__ void glds16(const double* src, double* lds_row) {
   __builtin_amdgcn_global_load_lds(src, lds_row, 16, 0, 0);
 }
 
-template <int BT, int NT>
+template <int BT, int NT, int NS>
 __global__ void __launch_bounds__(NT)
 gram_glds_kernel(const double* __restrict__ X, const double* __restrict__ Y, int m, int d,
                  int ntiles, int ksplit, long rows_per_split,
                  double* __restrict__ A, double* __restrict__ B, double* __restrict__ YY,
                  double* __restrict__ slab, int nt, int ST) {
   using T = GramTile<BT, NT>;
-  constexpr int NS = 3;
+  static_assert(NS == 2 || NS == 3, "two- or three-stage ring");
   constexpr int STAGE = 2 * BK * T::LDSROW;  // doubles per stage (two panels)
   extern __shared__ __attribute__((aligned(16))) double lds[];  // NS * STAGE doubles (dynamic: > 64 KB)
 
@@ -364,7 +402,17 @@ gram_glds_kernel(const double* __restrict__ X, const double* __restrict__ Y, int
       glds16(src, base + (panel * BK + r) * T::LDSROW);
     }
   };
-  if (nfull > 0) {
+  if (nfull > 0 && NS == 2) {
+    // two stages (two workgroups per CU): slab s + 1's DMAs fly during slab s's MFMAs; at the top of
+    // slab s every wave has only slab s's own DMAs outstanding
+    issue(kbeg, 0);
+    for (long s = 0; s < nfull; ++s) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // everyone's DMAs of s landed, everyone is done reading s - 1
+      if (s + 1 < nfull) issue(kbeg + (s + 1) * BK, (int)((s + 1) & 1));
+      compute(lds + (s & 1) * STAGE);
+    }
+  } else if (nfull > 0) {
     issue(kbeg, 0);
     if (nfull > 1) issue(kbeg + BK, 1);
     int cur = 0;
@@ -468,10 +516,11 @@ gram_reduce_kernel(const double* __restrict__ slab, int d, int ntiles, int kspli
   }
 }
 
-// GADMM_GRAM_GLDS=1: the LDS-DMA kernel for 128-wide tiles (A/B switch; one workgroup per CU)
-bool gram_glds() {
-  static const bool on = getenv("GADMM_GRAM_GLDS") && atoi(getenv("GADMM_GRAM_GLDS")) == 1;
-  return on;
+// GADMM_GRAM_GLDS=1: the LDS-DMA kernel for 128-wide tiles with a 3-stage ring (one workgroup per CU);
+// =2: a 2-stage ring (two workgroups per CU). A/B switches; 0 = the register-staged kernel.
+int gram_glds() {
+  static const int v = getenv("GADMM_GRAM_GLDS") ? atoi(getenv("GADMM_GRAM_GLDS")) : 0;
+  return v == 1 || v == 2 ? v : 0;
 }
 
 template <int BT>
@@ -495,15 +544,20 @@ int launch_gram(const double* X, const double* Y, int N, int m, int d, int kspli
   bool launched = false;
   if constexpr (BT == 128) {
     if (gram_glds()) {
-      const size_t lds = (size_t)3 * 2 * BK * (BT + PAD) * sizeof(double);
+      const int ns = gram_glds() == 1 ? 3 : 2;
+      const size_t lds = (size_t)ns * 2 * BK * (BT + PAD) * sizeof(double);
+      const void* fn = ns == 3 ? (const void*)gram_glds_kernel<BT, 512, 3> : (const void*)gram_glds_kernel<BT, 512, 2>;
       static bool attr = false;
       if (!attr) {
-        GADMM_CHECK(hipFuncSetAttribute((const void*)gram_glds_kernel<BT, 512>,
-                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
         attr = true;
       }
-      hipLaunchKernelGGL((gram_glds_kernel<BT, 512>), dim3((unsigned)nwg), dim3(512), lds, st, X, Y, m, d, ntiles,
-                         ksplit, rows, A, B, YY, slab, nt, ST);
+      if (ns == 3)
+        hipLaunchKernelGGL((gram_glds_kernel<BT, 512, 3>), dim3((unsigned)nwg), dim3(512), lds, st, X, Y, m, d,
+                           ntiles, ksplit, rows, A, B, YY, slab, nt, ST);
+      else
+        hipLaunchKernelGGL((gram_glds_kernel<BT, 512, 2>), dim3((unsigned)nwg), dim3(512), lds, st, X, Y, m, d,
+                           ntiles, ksplit, rows, A, B, YY, slab, nt, ST);
       launched = true;
     }
   }
@@ -548,7 +602,7 @@ int gadmm_gram_pick_ksplit(int N, int m, int d) {
   int cus = gadmm_cu_count();
   if (cus <= 0) cus = 256;
   // 2 resident workgroups per CU (LDS / VGPR bound); 1 for the LDS-DMA kernel's 3-stage ring
-  const long slots = (long)cus * (BT == 128 && gram_glds() ? 1 : 2);
+  const long slots = (long)cus * (BT == 128 && gram_glds() == 1 ? 1 : 2);
   long maxk = (m + 255) / 256;       // keep >= 256 rows per split
   if (maxk > 64) maxk = 64;
   if (maxk < 1) maxk = 1;
