@@ -15,14 +15,77 @@ import torch
 from ..ops.linalg import gram, spd_inverse, spd_inverse_blocked
 
 
+def _cg_solve(M: torch.Tensor, r: torch.Tensor, tol: float = 1e-13, maxit: int = 96, check: int = 8):
+    """Jacobi-preconditioned conjugate gradients for the SPD system M x = r: x once the TRUE residual
+    ||r - M x|| <= tol ||r|| (tested every `check` iterations, one host sync each), None if that takes
+    more than `maxit` iterations. Fixed operation sequence (deterministic). On a HIP device the matrix
+    is block-packed once and every product is the native symmetric GEMV (half the bytes, and no
+    first-call library loading inside a timed set-up: rocBLAS gemv / dot cost ~0.2 s on first use);
+    the dots are elementwise products + sums."""
+    d = int(M.shape[-1])
+    diag = torch.diagonal(M)
+    rn0 = float(torch.sqrt((r * r).sum()))
+    if rn0 == 0.0:
+        return torch.zeros_like(r)
+    if not bool((diag > 0).all()):
+        return None
+    if M.is_cuda:
+        from ..ops.linalg import sym_pack, sym_padded, symv_packed, symv_work_doubles
+        dp = sym_padded(d)
+        Mp = sym_pack(M.unsqueeze(0))[0]
+        work = torch.empty((symv_work_doubles(d),), dtype=torch.float64, device=M.device)
+
+        def pad(v):
+            out = torch.zeros((dp,), dtype=torch.float64, device=M.device)
+            out[:d] = v
+            return out
+
+        def mv(v):  # v zero padded; the product's padding stays zero (only out[:d] is written)
+            return symv_packed(Mp, v, torch.zeros((dp,), dtype=torch.float64, device=M.device), work, d)
+
+        r, dinv = pad(r), pad(1.0 / diag)
+    else:
+        dinv = 1.0 / diag
+
+        def mv(v):
+            return torch.mv(M, v)
+
+    x = dinv * r
+    res = r - mv(x)
+    z = dinv * res
+    p = z.clone()
+    rz = (res * z).sum()
+    for k in range(1, maxit + 1):
+        q = mv(p)
+        alpha = rz / (p * q).sum()
+        x.add_(alpha * p)
+        res.sub_(alpha * q)
+        if k % check == 0:
+            e = r - mv(x)
+            if float(torch.sqrt((e * e).sum())) <= tol * rn0:
+                return x[:d].clone()
+        z = dinv * res
+        rz_new = (res * z).sum()
+        p = z + (rz_new / rz) * p
+        rz = rz_new
+    return None
+
+
 def _spd_solve(M: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
     """Solve the SPD normal equations by Cholesky (half the flops of LU, no pivoting); LU only if
     the factorisation reports the matrix is not positive definite. On a HIP device with d > 256 (the
-    real-shaped oracle, inside the timed set-up of the 10M x 10k config): the native blocked
-    Gauss-Jordan inverse (f64 MFMA, csrc/kernels/spd_inverse_blocked.hip) and one GEMV. rocSOLVER's
-    potrf / trsv spent ~0.3 s there, mostly first-call library loading between their kernels
-    (profiles/r04_real10m), against ~50 ms for the inverse."""
-    if M.is_cuda and M.shape[-1] > 256 and os.environ.get("GADMM_OPT_SOLVER", "native") != "rocsolver":
+    real-shaped oracle, inside the timed set-up of the 10M x 10k config): Jacobi-preconditioned CG to a
+    1e-13 relative residual when the Gram is well conditioned (a tall Gaussian shard: ~20 GEMVs of the
+    d x d matrix, a few ms at d = 10k), else the native blocked Gauss-Jordan inverse (f64 MFMA,
+    csrc/kernels/spd_inverse_blocked.hip, ~50 ms at d = 10k) and one GEMV. rocSOLVER's potrf / trsv
+    spent ~0.3 s there, mostly first-call library loading between their kernels, and was not
+    deterministic with ranks sharing a GPU (profiles/r04_real10m)."""
+    native_ok = os.environ.get("GADMM_OPT_SOLVER", "native") != "rocsolver"
+    if M.is_cuda and M.shape[-1] > 256 and native_ok and os.environ.get("GADMM_OPT_CG", "1") != "0":
+        x = _cg_solve(M, r)
+        if x is not None:
+            return x
+    if M.is_cuda and M.shape[-1] > 256 and native_ok:
         st = torch.zeros((1,), dtype=torch.int32, device=M.device)
         inv = spd_inverse_blocked(M.unsqueeze(0), torch.zeros((1, 1), dtype=torch.float64), check_status=False,
                                   status=st)[0, 0]

@@ -12,6 +12,7 @@ torch, which is also the fp64 reference the kernels are tested against.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 from typing import Optional, Tuple
 
@@ -141,6 +142,36 @@ def sym_pack(M: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tenso
     Mc = M.contiguous()
     native.check(lib.gadmm_sym_pack_f64(Mc.data_ptr(), out.data_ptr(), cnt, d, native.stream_handle()), "sym_pack")
     return out
+
+
+def symv_packed(Mp: torch.Tensor, x: torch.Tensor, out: torch.Tensor, work: torch.Tensor, d: int) -> torch.Tensor:
+    """``out = M x`` for ONE block-packed symmetric matrix (``sym_pack``) on the current stream: the
+    symmetric GEMV of the large-d engines (csrc/kernels/first_order_big.hip: gadmm_symv_batch, one read
+    of each stored block for both products, fixed-order reduction). ``x`` / ``out`` are zero padded to
+    ``sym_padded(d)`` (only out[:d] is written); ``work``: ``symv_work_doubles(d)`` doubles."""
+    lib = native.require()
+    fn = lib.gadmm_symv_batch
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long,
+                   ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+    native.check(fn(Mp.data_ptr(), 0, x.data_ptr(), 0, out.data_ptr(), 0, work.data_ptr(), 1, int(d), None,
+                    native.stream_handle()), "symv_batch")
+    return out
+
+
+def sym_padded(d: int) -> int:
+    """Length of a vector zero padded for the block-packed symmetric GEMV (sym_gemv.h)."""
+    lib = native.require()
+    lib.gadmm_sym_padded.restype = ctypes.c_long
+    lib.gadmm_sym_padded.argtypes = [ctypes.c_int]
+    return int(lib.gadmm_sym_padded(int(d)))
+
+
+def symv_work_doubles(d: int) -> int:
+    lib = native.require()
+    lib.gadmm_symv_work_doubles.restype = ctypes.c_long
+    lib.gadmm_symv_work_doubles.argtypes = [ctypes.c_int]
+    return int(lib.gadmm_symv_work_doubles(int(d)))
 
 
 def sym_unpack_torch(P: torch.Tensor, d: int, B: int = 128) -> torch.Tensor:

@@ -428,6 +428,28 @@ def test_large_d_engine_matches_torch(d, obj_mode):
     assert float((th - x).abs().max()) < 1e-6 * float(x.abs().max())
 
 
+@pytest.mark.parametrize("rows", [20000, 330])
+def test_large_d_optimum_solve_paths(rows, monkeypatch):
+    """The large-d oracle solve on the device (models/linear.py:_spd_solve, d > 256): CG for a
+    well-conditioned Gram (rows >> d), the native Gauss-Jordan inverse when CG does not reach its
+    residual (rows ~ d), both against torch's LU to 1e-10, and repeat calls bit-identical."""
+    from gadmm_amd.models.linear import _spd_solve, _cg_solve
+    d = 300
+    g = torch.Generator(device="cpu").manual_seed(3)
+    X = torch.randn(rows, d, dtype=torch.float64, generator=g).to(DEV)
+    M = X.T @ X
+    b = torch.randn(d, dtype=torch.float64, generator=g).to(DEV)
+    ref = torch.linalg.solve(M, b)
+    cg = _cg_solve(M, b)
+    assert (cg is not None) == (rows > 10 * d)
+    x1, x2 = _spd_solve(M, b), _spd_solve(M, b)
+    assert torch.equal(x1, x2)
+    assert float((x1 - ref).abs().max() / ref.abs().max()) < 1e-10
+    monkeypatch.setenv("GADMM_OPT_CG", "0")  # the Gauss-Jordan path alone
+    xg = _spd_solve(M, b)
+    assert float((xg - ref).abs().max() / ref.abs().max()) < 1e-10
+
+
 @pytest.mark.parametrize("d", [129, 300, 1001, 2048])
 def test_sym_pack_roundtrip(d):
     """sym_pack (csrc/kernels/chain_big.hip): the block-packed lower triangle of a symmetric matrix holds
