@@ -221,3 +221,25 @@ def test_lanczos_extreme_eigs():
     ev = torch.linalg.eigvalsh(G)
     assert abs(hi - float(ev[-1])) <= 1e-10 * float(ev[-1])
     assert abs(lo - float(ev[0])) <= 1e-8 * float(ev[-1])
+
+
+def test_cg_oracle_solve_and_fallback():
+    """The large-d optimum's CG attempt (models/linear.py:_cg_solve, torch path on the CPU): a tall
+    well-conditioned Gram converges to LU's solution at 1e-13; a Gram with rows ~ d returns None, so
+    _spd_solve falls back to a direct solve."""
+    import torch
+    from gadmm_amd.models.linear import _cg_solve, _spd_solve
+    g = torch.Generator().manual_seed(11)
+    d = 120
+    b = torch.randn(d, dtype=torch.float64, generator=g)
+    X = torch.randn(12000, d, dtype=torch.float64, generator=g)
+    M = X.T @ X
+    x = _cg_solve(M, b)
+    ref = torch.linalg.solve(M, b)
+    assert x is not None and float((x - ref).abs().max() / ref.abs().max()) < 1e-13
+    assert torch.equal(_cg_solve(M, b), x)  # fixed operation sequence
+    X = torch.randn(d + 5, d, dtype=torch.float64, generator=g)
+    M = X.T @ X
+    assert _cg_solve(M, b, maxit=16) is None
+    xs = _spd_solve(M, b)
+    assert float((M @ xs - b).abs().max()) < 1e-8 * float(b.abs().max()) * float(torch.linalg.cond(M))
