@@ -3,7 +3,7 @@
 set -o pipefail
 O=gpurun_out/r3_dlplan
 mkdir -p $O
-. tools/gpu_step.sh
+. tools/gpu_runs/gpu_step.sh
 export GADMM_BENCH_SHARE_GPU=1
 run() {  # name nranks [env...]
   local name=$1 n=$2; shift 2

@@ -3,7 +3,7 @@
 set -o pipefail
 O=gpurun_out/r3_pipe
 mkdir -p $O
-. tools/gpu_step.sh
+. tools/gpu_runs/gpu_step.sh
 step tests 600 python3 -u -m pytest tests/test_gpu.py tests/test_gpu_multirank.py -x -v --timeout 170 --timeout-method thread \
   -k "persistent or blocked or dgadmm or dynamic or data_local or stalled or xgmi or newton or headline or xcd"
 grep -q "passed" $O/tests.log && ! grep -qE "[0-9]+ failed" $O/tests.log || exit 1
