@@ -285,6 +285,95 @@ __global__ void fob_finish(const double* part, int nw, int nblk, const double* y
   ctl->iter = it + 1;
 }
 
+// ---- Jacobi-preconditioned CG for the large-d optimum oracle (models/linear.py:_cg_solve) -----------
+// One workgroup of CG_NT threads runs every vector step of an iteration (d = 10k: ten elements per
+// thread); the products are the block-packed symmetric GEMV above (gadmm_symv_batch). Dot products are
+// block sums in a fixed order, broadcast to every thread: deterministic. sc = [r.z, scratch, bad].
+constexpr int CG_NT = 1024;
+
+__device__ __forceinline__ double cg_allsum(double v, double* sh) {
+  v = wave_sum_f64(v);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __syncthreads();  // sh is reused by the next call
+  if (lane == 0) sh[w] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int q = 0; q < CG_NT / 64; ++q) t += sh[q];  // the same order on every thread
+  return t;
+}
+
+// dinv = 1 / diag(M) (M full d x d), x = dinv * b, sc[1] = |b|^2, sc[2] = number of non-positive pivots
+__global__ void __launch_bounds__(CG_NT) cg_begin(const double* M, const double* b, double* dinv, double* x,
+                                                   double* sc, int d) {
+  __shared__ double sh[CG_NT / 64];
+  double bb = 0.0, bad = 0.0;
+  for (int j = threadIdx.x; j < d; j += CG_NT) {
+    const double m = M[(long)j * (d + 1)];
+    const double di = 1.0 / m;
+    bad += (m > 0.0) ? 0.0 : 1.0;
+    dinv[j] = di;
+    x[j] = di * b[j];
+    bb = fma(b[j], b[j], bb);
+  }
+  bb = cg_allsum(bb, sh);
+  bad = cg_allsum(bad, sh);
+  if (threadIdx.x == 0) {
+    sc[1] = bb;
+    sc[2] = bad;
+  }
+}
+
+// q = M x0: res = b - q, z = dinv res, p = z, sc[0] = res . z
+__global__ void __launch_bounds__(CG_NT) cg_begin2(const double* b, const double* dinv, const double* q, double* res,
+                                                    double* z, double* p, double* sc, int d) {
+  __shared__ double sh[CG_NT / 64];
+  double rz = 0.0;
+  for (int j = threadIdx.x; j < d; j += CG_NT) {
+    const double r = b[j] - q[j], zz = dinv[j] * r;
+    res[j] = r;
+    z[j] = zz;
+    p[j] = zz;
+    rz = fma(r, zz, rz);
+  }
+  rz = cg_allsum(rz, sh);
+  if (threadIdx.x == 0) sc[0] = rz;
+}
+
+// q = M p: one CG iteration's vector work
+__global__ void __launch_bounds__(CG_NT) cg_step(const double* q, const double* dinv, double* x, double* res, double* z,
+                                                  double* p, double* sc, int d) {
+  __shared__ double sh[CG_NT / 64];
+  const double rz = sc[0];
+  double pq = 0.0;
+  for (int j = threadIdx.x; j < d; j += CG_NT) pq = fma(p[j], q[j], pq);
+  pq = cg_allsum(pq, sh);
+  const double alpha = rz / pq;
+  double rzn = 0.0;
+  for (int j = threadIdx.x; j < d; j += CG_NT) {
+    x[j] = fma(alpha, p[j], x[j]);
+    const double r = fma(-alpha, q[j], res[j]), zz = dinv[j] * r;
+    res[j] = r;
+    z[j] = zz;
+    rzn = fma(r, zz, rzn);
+  }
+  rzn = cg_allsum(rzn, sh);
+  const double beta = rzn / rz;
+  for (int j = threadIdx.x; j < d; j += CG_NT) p[j] = fma(beta, p[j], z[j]);
+  if (threadIdx.x == 0) sc[0] = rzn;  // every thread read sc[0] before cg_allsum's barriers
+}
+
+// q = M x: sc[1] = |b - q|^2 (the true residual)
+__global__ void __launch_bounds__(CG_NT) cg_resid(const double* b, const double* q, double* sc, int d) {
+  __shared__ double sh[CG_NT / 64];
+  double e2 = 0.0;
+  for (int j = threadIdx.x; j < d; j += CG_NT) {
+    const double e = b[j] - q[j];
+    e2 = fma(e, e, e2);
+  }
+  e2 = cg_allsum(e2, sh);
+  if (threadIdx.x == 0) sc[1] = e2;
+}
+
 }  // namespace
 
 extern "C" {
@@ -391,6 +480,30 @@ int gadmm_fob_finish(const double* part, int nw, int nblk, const double* yy, dou
                      hipStream_t st) {
   hipLaunchKernelGGL(fob_finish, dim3(1), dim3(64), 0, st, part, nw, nblk, yy, trace, tstamp, max_iter, obj0, tol,
                      shift, dpart, ring, ctl);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+// CG steps of the large-d optimum oracle (see cg_begin ...): single-workgroup launches on `st`
+int gadmm_cg_begin(const double* M, const double* b, double* dinv, double* x, double* sc, int d, hipStream_t st) {
+  hipLaunchKernelGGL(cg_begin, dim3(1), dim3(CG_NT), 0, st, M, b, dinv, x, sc, d);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+int gadmm_cg_begin2(const double* b, const double* dinv, const double* q, double* res, double* z, double* p, double* sc,
+                    int d, hipStream_t st) {
+  hipLaunchKernelGGL(cg_begin2, dim3(1), dim3(CG_NT), 0, st, b, dinv, q, res, z, p, sc, d);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+int gadmm_cg_step(const double* q, const double* dinv, double* x, double* res, double* z, double* p, double* sc, int d,
+                  hipStream_t st) {
+  hipLaunchKernelGGL(cg_step, dim3(1), dim3(CG_NT), 0, st, q, dinv, x, res, z, p, sc, d);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+int gadmm_cg_resid(const double* b, const double* q, double* sc, int d, hipStream_t st) {
+  hipLaunchKernelGGL(cg_resid, dim3(1), dim3(CG_NT), 0, st, b, q, sc, d);
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

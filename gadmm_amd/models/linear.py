@@ -18,56 +18,79 @@ from ..ops.linalg import gram, spd_inverse, spd_inverse_blocked
 def _cg_solve(M: torch.Tensor, r: torch.Tensor, tol: float = 1e-13, maxit: int = 96, check: int = 8):
     """Jacobi-preconditioned conjugate gradients for the SPD system M x = r: x once the TRUE residual
     ||r - M x|| <= tol ||r|| (tested every `check` iterations, one host sync each), None if that takes
-    more than `maxit` iterations. Fixed operation sequence (deterministic). On a HIP device the matrix
-    is block-packed once and every product is the native symmetric GEMV (half the bytes, and no
-    first-call library loading inside a timed set-up: rocBLAS gemv / dot cost ~0.2 s on first use);
-    the dots are elementwise products + sums."""
+    more than `maxit` iterations or a diagonal entry is not positive. Fixed operation sequence
+    (deterministic). On a HIP device everything runs in native kernels (csrc/kernels/first_order_big.hip:
+    cg_begin / cg_step / cg_resid, one workgroup each, and the block-packed symmetric GEMV for the
+    products): a cold solve pays no first-use loading of rocBLAS or of a dozen torch kernels (~0.2 s /
+    ~50 ms measured inside the timed set-up)."""
     d = int(M.shape[-1])
+    if M.is_cuda:
+        return _cg_solve_native(M.contiguous(), r.contiguous(), tol, maxit, check)
     diag = torch.diagonal(M)
     rn0 = float(torch.sqrt((r * r).sum()))
     if rn0 == 0.0:
         return torch.zeros_like(r)
     if not bool((diag > 0).all()):
         return None
-    if M.is_cuda:
-        from ..ops.linalg import sym_pack, sym_padded, symv_packed, symv_work_doubles
-        dp = sym_padded(d)
-        Mp = sym_pack(M.unsqueeze(0))[0]
-        work = torch.empty((symv_work_doubles(d),), dtype=torch.float64, device=M.device)
-
-        def pad(v):
-            out = torch.zeros((dp,), dtype=torch.float64, device=M.device)
-            out[:d] = v
-            return out
-
-        def mv(v):  # v zero padded; the product's padding stays zero (only out[:d] is written)
-            return symv_packed(Mp, v, torch.zeros((dp,), dtype=torch.float64, device=M.device), work, d)
-
-        r, dinv = pad(r), pad(1.0 / diag)
-    else:
-        dinv = 1.0 / diag
-
-        def mv(v):
-            return torch.mv(M, v)
-
+    dinv = 1.0 / diag
     x = dinv * r
-    res = r - mv(x)
+    res = r - torch.mv(M, x)
     z = dinv * res
     p = z.clone()
     rz = (res * z).sum()
     for k in range(1, maxit + 1):
-        q = mv(p)
+        q = torch.mv(M, p)
         alpha = rz / (p * q).sum()
         x.add_(alpha * p)
         res.sub_(alpha * q)
         if k % check == 0:
-            e = r - mv(x)
+            e = r - torch.mv(M, x)
             if float(torch.sqrt((e * e).sum())) <= tol * rn0:
-                return x[:d].clone()
+                return x
         z = dinv * res
         rz_new = (res * z).sum()
         p = z + (rz_new / rz) * p
         rz = rz_new
+    return None
+
+
+def _cg_solve_native(M: torch.Tensor, r: torch.Tensor, tol: float, maxit: int, check: int):
+    import ctypes
+    from ..ops import native
+    from ..ops.linalg import sym_pack, sym_padded, symv_packed, symv_work_doubles
+    lib = native.require()
+    P, I = ctypes.c_void_p, ctypes.c_int
+    sigs = {"gadmm_cg_begin": [P, P, P, P, P, I, P], "gadmm_cg_begin2": [P, P, P, P, P, P, P, I, P],
+            "gadmm_cg_step": [P, P, P, P, P, P, P, I, P], "gadmm_cg_resid": [P, P, P, I, P]}
+    for name, args in sigs.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = ctypes.c_int, args
+    d, dev, st = int(M.shape[-1]), M.device, native.stream_handle()
+    dp = sym_padded(d)
+    V = torch.zeros((7, dp), dtype=torch.float64, device=dev)  # zero padding: the GEMV reads whole blocks
+    b, dinv, x, res, z, p, q = V.unbind(0)
+    b[:d].copy_(r)
+    sc = torch.zeros((3,), dtype=torch.float64, device=dev)
+    ptr = native.ptr
+    native.check(lib.gadmm_cg_begin(ptr(M), ptr(b), ptr(dinv), ptr(x), ptr(sc), d, st), "cg_begin")
+    Mp = sym_pack(M.unsqueeze(0))[0]
+    work = torch.empty((symv_work_doubles(d),), dtype=torch.float64, device=dev)
+    head = sc.cpu()
+    if float(head[2]) > 0:
+        return None
+    rn0 = float(head[1]) ** 0.5
+    if rn0 == 0.0:
+        return torch.zeros_like(r)
+    symv_packed(Mp, x, q, work, d)
+    native.check(lib.gadmm_cg_begin2(ptr(b), ptr(dinv), ptr(q), ptr(res), ptr(z), ptr(p), ptr(sc), d, st), "cg_begin2")
+    for k in range(1, maxit + 1):
+        symv_packed(Mp, p, q, work, d)
+        native.check(lib.gadmm_cg_step(ptr(q), ptr(dinv), ptr(x), ptr(res), ptr(z), ptr(p), ptr(sc), d, st), "cg_step")
+        if k % check == 0:
+            symv_packed(Mp, x, q, work, d)
+            native.check(lib.gadmm_cg_resid(ptr(b), ptr(q), ptr(sc), d, st), "cg_resid")
+            if float(sc[1].item()) ** 0.5 <= tol * rn0:
+                return x[:d].clone()
     return None
 
 
