@@ -222,8 +222,8 @@ int blocked_inplace(double* W, int d, int nb, double* ws, int* status, hipStream
 
 extern "C" {
 
-// Workspace doubles (zeroed by the caller) for block size nb.
-long gadmm_spd_inverse_blocked_workspace(int d, int nb) { return ws_doubles(d, nb <= 0 ? 128 : nb); }
+// Workspace doubles (zeroed by the caller) for block size nb: one region per concurrent matrix stream.
+long gadmm_spd_inverse_blocked_workspace(int d, int nb) { return 2 * ws_doubles(d, nb <= 0 ? 128 : nb); }
 
 // out[n][v] = (A_n + shift[n][v] I)^-1, d x d each; shift_host: host array [N][nvar]. status: int
 // (1 = a pivot was not positive). nb: 64 or 128 (0: 128).
@@ -235,6 +235,44 @@ int gadmm_spd_inverse_blocked_f64(const double* A, const double* shift_host, int
     return -1;
   }
   const long dd = (long)d * d;
+  // Two matrices in flight: odd ones run on a second stream with their own workspace, so one matrix's
+  // latency-bound pivot-block chain (panel, 128-block inverse, cross: ~15 launches per pivot block)
+  // overlaps the other's MFMA rank-nb update (the real-shaped config inverts two 10k matrices per
+  // engine). Each matrix's arithmetic is unchanged: bit-identical. The second stream waits for
+  // everything enqueued on `st` before, and `st` waits for it at the end.
+  const int total = N * nvar;
+  hipStream_t st2 = nullptr;
+  if (total > 1) {
+    int dev = 0;
+    GADMM_CHECK(hipGetDevice(&dev));
+    static hipStream_t side[64] = {};
+    static hipEvent_t ev_in[64] = {}, ev_out[64] = {};
+    if (dev < 0 || dev >= 64) {
+      gadmm_set_error("spd_inverse_blocked: device %d", dev);
+      return -1;
+    }
+    if (!side[dev]) {
+      GADMM_CHECK(hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking));
+      GADMM_CHECK(hipEventCreateWithFlags(&ev_in[dev], hipEventDisableTiming));
+      GADMM_CHECK(hipEventCreateWithFlags(&ev_out[dev], hipEventDisableTiming));
+    }
+    st2 = side[dev];
+    GADMM_CHECK(hipEventRecord(ev_in[dev], st));
+    GADMM_CHECK(hipStreamWaitEvent(st2, ev_in[dev], 0));
+    for (int m = 0; m < total; ++m) {
+      const int n = m / nvar, v = m % nvar;
+      hipStream_t sm = (m & 1) ? st2 : st;
+      double* W = out + (long)m * dd;
+      hipLaunchKernelGGL(shift_copy_kernel, dim3(grid_for(dd)), dim3(256), 0, sm, A + (long)n * dd,
+                         shift_host[n * nvar + v], d, W);
+      GADMM_CHECK(hipGetLastError());
+      const int rc = blocked_inplace(W, d, nb, ws + ((m & 1) ? ws_doubles(d, nb) : 0), status, sm);
+      if (rc) return rc;
+    }
+    GADMM_CHECK(hipEventRecord(ev_out[dev], st2));
+    GADMM_CHECK(hipStreamWaitEvent(st, ev_out[dev], 0));
+    return 0;
+  }
   for (int n = 0; n < N; ++n)
     for (int v = 0; v < nvar; ++v) {
       double* W = out + ((long)n * nvar + v) * dd;
