@@ -486,23 +486,39 @@ int gadmm_fob_finish(const double* part, int nw, int nblk, const double* yy, dou
 
 // CG steps of the large-d optimum oracle (see cg_begin ...): single-workgroup launches on `st`
 int gadmm_cg_begin(const double* M, const double* b, double* dinv, double* x, double* sc, int d, hipStream_t st) {
+  if (!M || !b || !dinv || !x || !sc || d < 1) {
+    gadmm_set_error("cg_begin: bad arguments (d=%d)", d);
+    return -1;
+  }
   hipLaunchKernelGGL(cg_begin, dim3(1), dim3(CG_NT), 0, st, M, b, dinv, x, sc, d);
   GADMM_CHECK(hipGetLastError());
   return 0;
 }
 int gadmm_cg_begin2(const double* b, const double* dinv, const double* q, double* res, double* z, double* p, double* sc,
                     int d, hipStream_t st) {
+  if (!b || !dinv || !q || !res || !z || !p || !sc || d < 1) {
+    gadmm_set_error("cg_begin2: bad arguments (d=%d)", d);
+    return -1;
+  }
   hipLaunchKernelGGL(cg_begin2, dim3(1), dim3(CG_NT), 0, st, b, dinv, q, res, z, p, sc, d);
   GADMM_CHECK(hipGetLastError());
   return 0;
 }
 int gadmm_cg_step(const double* q, const double* dinv, double* x, double* res, double* z, double* p, double* sc, int d,
                   hipStream_t st) {
+  if (!q || !dinv || !x || !res || !z || !p || !sc || d < 1) {
+    gadmm_set_error("cg_step: bad arguments (d=%d)", d);
+    return -1;
+  }
   hipLaunchKernelGGL(cg_step, dim3(1), dim3(CG_NT), 0, st, q, dinv, x, res, z, p, sc, d);
   GADMM_CHECK(hipGetLastError());
   return 0;
 }
 int gadmm_cg_resid(const double* b, const double* q, double* sc, int d, hipStream_t st) {
+  if (!b || !q || !sc || d < 1) {
+    gadmm_set_error("cg_resid: bad arguments (d=%d)", d);
+    return -1;
+  }
   hipLaunchKernelGGL(cg_resid, dim3(1), dim3(CG_NT), 0, st, b, q, sc, d);
   GADMM_CHECK(hipGetLastError());
   return 0;
