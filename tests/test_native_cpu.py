@@ -248,3 +248,17 @@ def test_star_big_abi_layout_matches_ctypes():
     exp = [ctypes.sizeof(StarBigArgs), StarBigArgs.rho.offset, StarBigArgs.Minv.offset, StarBigArgs.ctl.offset,
            StarBigArgs.tstamp.offset, StarBigArgs.gid.offset]
     assert list(buf[:k]) == exp
+
+
+def test_cg_entry_points_refuse_bad_arguments():
+    """The large-d oracle's CG kernels (first_order_big.hip: gadmm_cg_*) validate before launching, so a
+    bad call fails loudly on any host (no GPU needed)."""
+    lib = native.require()
+    P, I = ctypes.c_void_p, ctypes.c_int
+    lib.gadmm_cg_begin.restype = ctypes.c_int
+    lib.gadmm_cg_begin.argtypes = [P, P, P, P, P, I, P]
+    lib.gadmm_cg_resid.restype = ctypes.c_int
+    lib.gadmm_cg_resid.argtypes = [P, P, P, I, P]
+    assert lib.gadmm_cg_begin(None, None, None, None, None, 10, None) == -1
+    assert lib.gadmm_cg_resid(None, None, None, 0, None) == -1
+    assert b"cg_" in lib.gadmm_last_error()
