@@ -94,6 +94,24 @@ def _cg_solve_native(M: torch.Tensor, r: torch.Tensor, tol: float, maxit: int, c
     return None
 
 
+def _resid_sq(X: torch.Tensor, y: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
+    """(1,) device tensor sum_rows (X_row . x - y_row)^2 over the local shards X (n_loc, m, d), f64:
+    csrc/kernels/first_order_big.hip:gadmm_resid_sq (fixed-order partials: deterministic)."""
+    import ctypes
+    from ..ops import native
+    lib = native.require()
+    fn = lib.gadmm_resid_sq
+    P = ctypes.c_void_p
+    fn.restype, fn.argtypes = ctypes.c_int, [P, P, P, ctypes.c_long, ctypes.c_int, P, P, P]
+    Xc, yc, xc = X.contiguous(), y.contiguous(), x.contiguous()
+    rows = int(Xc.numel() // Xc.shape[-1])
+    part = torch.empty((4096,), dtype=torch.float64, device=X.device)
+    out = torch.empty((1,), dtype=torch.float64, device=X.device)
+    native.check(fn(Xc.data_ptr(), yc.data_ptr(), xc.data_ptr(), rows, int(Xc.shape[-1]), part.data_ptr(),
+                    out.data_ptr(), native.stream_handle()), "resid_sq")
+    return out
+
+
 def _spd_solve(M: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
     """Solve the SPD normal equations by Cholesky (half the flops of LU, no pivoting); LU only if
     the factorisation reports the matrix is not positive definite. On a HIP device with d > 256 (the
@@ -240,8 +258,11 @@ class LinearRegression:
             As = As.clone()
             As.diagonal().add_(lam_tot)
         x = _spd_solve(As, bs)
-        r = torch.matmul(self.X.to(x.dtype), x) - self.y.to(x.dtype)  # (n_loc, m) residuals
-        f = (0.5 * (r * r).sum()).reshape(1)
+        if self.X.is_cuda and self.d > 256 and self.X.dtype == torch.float64:
+            f = 0.5 * _resid_sq(self.X, self.y, x)  # one native pass over the shard at HBM speed
+        else:
+            r = torch.matmul(self.X.to(x.dtype), x) - self.y.to(x.dtype)  # (n_loc, m) residuals
+            f = (0.5 * (r * r).sum()).reshape(1)
         if comm is not None and comm.nranks > 1:
             comm.allreduce_sum(f)
         return float(f.item() + 0.5 * lam_tot * (x @ x).item())

@@ -450,6 +450,21 @@ def test_large_d_optimum_solve_paths(rows, monkeypatch):
     assert float((xg - ref).abs().max() / ref.abs().max()) < 1e-10
 
 
+@pytest.mark.parametrize("d", [300, 301])
+def test_resid_sq_matches_torch(d):
+    """The optimum oracle's residual pass at d > 256 (models/linear.py:_resid_sq, one native pass over
+    the shard) == torch's ||X x - y||^2 to 1e-12, bit-identical on repeat calls (even and odd d)."""
+    from gadmm_amd.models.linear import _resid_sq
+    g = torch.Generator(device="cpu").manual_seed(5)
+    X = torch.randn(2, 3000, d, dtype=torch.float64, generator=g).to(DEV)
+    y = torch.randn(2, 3000, dtype=torch.float64, generator=g).to(DEV)
+    x = torch.randn(d, dtype=torch.float64, generator=g).to(DEV)
+    ref = float(((torch.matmul(X, x) - y) ** 2).sum())
+    a, b = _resid_sq(X, y, x), _resid_sq(X, y, x)
+    assert torch.equal(a, b)
+    assert abs(float(a) - ref) <= 1e-12 * ref
+
+
 @pytest.mark.parametrize("d", [129, 300, 1001, 2048])
 def test_sym_pack_roundtrip(d):
     """sym_pack (csrc/kernels/chain_big.hip): the block-packed lower triangle of a symmetric matrix holds
