@@ -1017,6 +1017,19 @@ __global__ void __launch_bounds__(64 * PWW) chain_blocked_pair_kernel(PersistArg
   }
 }
 
+// out[b][e] = src[e] >= 0 ? M[b][src[e]] : 0 -- the lane-major inverse image of the dynamic mode
+// (engine/chain_engine.py:quad_pad_image) rebuilt in place after a refresh, one launch
+__global__ void __launch_bounds__(256) pad_image_kernel(const double* __restrict__ M, long mstride,
+                                                        const long long* __restrict__ src, long n_el, int batch,
+                                                        double* __restrict__ out) {
+  const long tot = n_el * batch;
+  for (long e = (long)blockIdx.x * 256 + threadIdx.x; e < tot; e += (long)gridDim.x * 256) {
+    const long b = e / n_el, k = e - b * n_el;
+    const long long s = src[k];
+    out[e] = s >= 0 ? M[b * mstride + s] : 0.0;
+  }
+}
+
 extern "C" {
 
 // Pick (k, L) for n workers; returns the number of worker workgroups, 0 if not applicable.
@@ -1099,6 +1112,21 @@ long gadmm_chain_blocked_pad_len(int d) {
 }
 // Epochs one launch of the blocked kernel's dynamic mode can take (its tables are staged in LDS).
 int gadmm_chain_blocked_max_epochs() { return EPL; }
+
+// The lane-major image of `batch` matrices (mstride doubles apart) into out [batch][n_el]: src[k] = the
+// element index read for image slot k, < 0 for a zero slot (engine/chain_engine.py:quad_pad_image).
+int gadmm_pad_image_f64(const double* M, long mstride, const long long* src, long n_el, int batch, double* out,
+                        hipStream_t st) {
+  if (!M || !src || !out || n_el < 1 || batch < 1) {
+    gadmm_set_error("pad_image: bad arguments");
+    return -1;
+  }
+  const long tot = n_el * batch;
+  const int grid = (int)((tot + 255) / 256 < 4096 ? (tot + 255) / 256 : 4096);
+  hipLaunchKernelGGL(pad_image_kernel, dim3(grid), dim3(256), 0, st, M, mstride, src, n_el, batch, out);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
 
 // Plan of the data-local multi-GPU mode for a segment of nseg positions: one workgroup computing the
 // whole segment when it fits the 12 waves (no intra-rank exchange at all: k = 2^20 never comes), else

@@ -69,13 +69,15 @@ def epoch_tables_numpy(P: np.ndarray, loc: np.ndarray):
 
 
 _QUAD_IDX: dict = {}
+_QUAD_SRC: dict = {}
 
 
-def quad_pad_image(M: torch.Tensor, db: int) -> torch.Tensor:
+def quad_pad_image(M: torch.Tensor, db: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Lane-major image of the quad register layout of each (d, d) matrix in ``M`` (B, d, d), as
     ``quad_load_image`` in csrc/kernels/chain_blocked.hip reads it: lane l = i + 16c holds
     M[i + 16r, c + 4t] (r < 4, t < db / 4) at ((t >> 1) * 4 + r) * 128 + 2 l + (t & 1); zero outside d.
-    Returns (B, 512 * ceil(db / 8)) float64 on M's device."""
+    Returns (B, 512 * ceil(db / 8)) float64 on M's device; on a HIP device with ``out`` given, written
+    in place by one native launch (gadmm_pad_image_f64: the D-GADMM bench rebuilds it every solve)."""
     B, d = int(M.shape[0]), int(M.shape[1])
     qt = db // 4
     key = (d, db, M.device)
@@ -92,6 +94,19 @@ def quad_pad_image(M: torch.Tensor, db: int) -> torch.Tensor:
         idx = (torch.from_numpy(np.maximum(src, 0)).to(M.device), torch.from_numpy(src >= 0).to(M.device))
         _QUAD_IDX[key] = idx
     gi, mask = idx
+    lib = native.require() if (out is not None and M.is_cuda) else None
+    if lib is not None and hasattr(lib, "gadmm_pad_image_f64") and M.dtype == torch.float64 and M.is_contiguous():
+        src = _QUAD_SRC.get(key)
+        if src is None:
+            src = torch.where(mask, gi, torch.full_like(gi, -1)).contiguous()
+            _QUAD_SRC[key] = src
+        fn = lib.gadmm_pad_image_f64
+        fn.restype = ctypes.c_int
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long, ctypes.c_int,
+                       ctypes.c_void_p, ctypes.c_void_p]
+        native.check(fn(M.data_ptr(), d * d, src.data_ptr(), int(src.numel()), B, out.data_ptr(),
+                        native.stream_handle()), "pad_image")
+        return out
     flat = M.reshape(B, d * d).to(torch.float64)
     return torch.where(mask.unsqueeze(0), flat[:, gi], torch.zeros((), dtype=torch.float64, device=M.device)).contiguous()
 
@@ -773,9 +788,10 @@ class NativeChainEngine:
                 # (PersistArgs::minv_pad); rebuilt from this solve's inverses on the engine stream, ahead of
                 # the launch, only after the inverses changed
                 if getattr(self, "_minv_pad", None) is None or self._minv_pad_version != self._minv_version:
-                    with torch.cuda.stream(self.stream):
+                    with torch.cuda.stream(self.stream):  # in place after the first build (one launch)
                         self._minv_pad = quad_pad_image(self.Minv.reshape(self.n_local * self.nvar, self.d, self.d),
-                                                        int(self.lib.gadmm_chain_blocked_pad_dim(self.d)))
+                                                        int(self.lib.gadmm_chain_blocked_pad_dim(self.d)),
+                                                        out=getattr(self, "_minv_pad", None))
                     self._minv_pad_version = self._minv_version
                 pa.minv_pad = self._minv_pad.data_ptr()
         self.last_kernel = ("blocked%s(k=%d,L=%d,W=%d,pw=%d)" % ((("-dyn" if epochs is not None else ""),) + tuple(plan))

@@ -450,6 +450,19 @@ def test_large_d_optimum_solve_paths(rows, monkeypatch):
     assert float((xg - ref).abs().max() / ref.abs().max()) < 1e-10
 
 
+@pytest.mark.parametrize("d,db", [(50, 52), (30, 32)])
+def test_quad_pad_image_native_matches_torch(d, db):
+    """The D-GADMM lane-major inverse image rebuilt in place by the native gather (gadmm_pad_image_f64)
+    == the torch-built image, bit for bit."""
+    from gadmm_amd.engine.chain_engine import quad_pad_image
+    M = torch.randn(6, d, d, dtype=torch.float64, device=DEV)
+    ref = quad_pad_image(M, db)
+    out = torch.full_like(ref, float("nan"))
+    got = quad_pad_image(M, db, out=out)
+    torch.cuda.synchronize()
+    assert got.data_ptr() == out.data_ptr() and torch.equal(got, ref)
+
+
 @pytest.mark.parametrize("d", [300, 301])
 def test_resid_sq_matches_torch(d):
     """The optimum oracle's residual pass at d > 256 (models/linear.py:_resid_sq, one native pass over

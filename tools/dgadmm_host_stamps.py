@@ -1,7 +1,7 @@
 """Host clock between labelled points of a D-GADMM solve (the bench config): the median time from each
 stamp to the next over repeated solves (gadmm_amd.utils.timing.host_stamp). Segment names are
 "from -> to"; "solve:begin" / "solve:end" bracket the whole call.
-Usage: python tools/dgadmm_host_stamps.py [coherence] [solves]"""
+Usage: python tools/dgadmm_host_stamps.py [coherence] [solves] [refresh]"""
 import os
 import sys
 import time
@@ -25,11 +25,12 @@ m = LinearRegression(ds.X.to(dev).contiguous(), ds.y.to(dev).contiguous())
 p0, c0, _ = T.find_path(24, np.random.default_rng(5))
 COH = int(sys.argv[1]) if len(sys.argv) > 1 else 10
 NS = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+REFRESH = len(sys.argv) > 3 and sys.argv[3] == "refresh"  # the bench's step: Gram + inverses per solve
 
 
 def solve():
     return dynamic_group_admm(m, 1.0, obj0, 1e-4, 3000, p0, c0, COH, seed=99, n_total=24, local_ids=list(range(24)),
-                              engine_opts={"state": False, "residual": False})
+                              engine_opts={"state": False, "residual": False, "refresh": REFRESH})
 
 
 for _ in range(3):
