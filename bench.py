@@ -126,29 +126,56 @@ def main():
         dist.destroy_process_group()
 
 
-def _headline_candidates(args, X_cpu, y_cpu, local, placement, rank, world, device, share, obj0, timeout_s):
-    """(name, factory) of every multi-GPU engine the tournament times, in preference order."""
+# Per-iteration cost of each engine family's kernel on ONE MI355X with no cross-GPU hop (measured:
+# profiles/r04_final e1 1.755 ms / 1373 for the blocked layout, README per-worker 3.07 ms / 1373, the
+# paired layout 2.80 ms / 1373 in profiles/r01c_pair_layout): the compute term of the tournament's model
+# predicted_ms = iters x (one_gpu_us + hops_per_iter x xgmi_hop_us) / 1e3.
+ONE_GPU_US = {"blocked": 1.28, "per-worker": 2.24, "paired": 2.04}
+
+
+def _headline_candidates(args, X_cpu, y_cpu, local, placement, rank, world, device, share, obj0):
+    """Every multi-GPU engine the tournament times, in preference order: dicts with ``name``, ``build``
+    (timeout_s -> solver; collective), ``hops`` (cross-GPU hand-offs on the critical cycle per iteration,
+    group_ADMM_closedForm.m:18-27, 62-70: the data-local kernel pays head -> tail -> head = 2, its halo
+    mode 1, the replicated-halo kernel 1 per k iterations) and ``base`` (its ONE_GPU_US family)."""
     from gadmm_amd.engine.multigpu import DistributedChainSolver
 
-    def make(engine, **kw):
-        def factory():
-            return DistributedChainSolver(X_cpu.to(device).contiguous(), y_cpu.to(device).contiguous(), local,
-                                          args.workers, placement, rank, world, device, args.rho, obj0, args.tol,
-                                          engine=engine, fabric=args.fabric, share=share, block=args.block,
-                                          use_graph=not args.no_graph, timeout_s=timeout_s, strict=True, **kw)
-        return factory
+    def make(engine, fabric=None, **kw):
+        def build(timeout_s):
+            sol = DistributedChainSolver(X_cpu.to(device).contiguous(), y_cpu.to(device).contiguous(), local,
+                                         args.workers, placement, rank, world, device, args.rho, obj0, args.tol,
+                                         engine=engine, fabric=fabric or args.fabric, share=share,
+                                         block=args.block, use_graph=not args.no_graph, timeout_s=timeout_s,
+                                         strict=True, **kw)
+            if fabric is not None and engine == "graph" and sol.kind != fabric:  # e.g. RCCL fell back to IPC
+                got = sol.kind
+                sol.close()
+                raise RuntimeError("graph engine over %s unavailable (got %s)" % (fabric, got))
+            return sol
+        return build
 
-    def replicated():
-        from gadmm_amd.data import linear_synthetic
-        ds_all = linear_synthetic(args.workers)  # the halo engine holds other ranks' shards (reported)
-        return make("replicated-halo", halo_data=(ds_all.X, ds_all.y))()
+    def replicated(k, pw):
+        def build(timeout_s):
+            from gadmm_amd.data import linear_synthetic
+            ds_all = linear_synthetic(args.workers)  # the halo engine holds other ranks' shards (reported)
+            return make("replicated-halo", halo_data=(ds_all.X, ds_all.y), halo_k=k, halo_pw=pw)(timeout_s)
+        return build
 
     cands = []
     if args.fabric in ("auto", "xgmi"):
-        cands += [("blocked-dl-halo", make("blocked-dl", dl_halo=True)),
-                  ("blocked-dl", make("blocked-dl", dl_halo=False)),
-                  ("per-worker", make("per-worker")),
-                  ("replicated-halo", replicated)]
+        cands += [dict(name="blocked-dl-halo", build=make("blocked-dl", dl_halo=True), hops=1.0, base="blocked"),
+                  dict(name="blocked-dl", build=make("blocked-dl", dl_halo=False), hops=2.0, base="blocked"),
+                  dict(name="per-worker", build=make("per-worker"), hops=2.0, base="per-worker")]
+        from gadmm_amd.engine.blocked_xgmi import replicated_plans
+        for k, pw in replicated_plans(args.workers, placement, int(X_cpu.shape[2])):
+            cands.append(dict(name="replicated-halo-k%d%s" % (k, "-pw2" if pw == 2 else ""), build=replicated(k, pw),
+                              hops=1.0 / k, base="paired" if pw == 2 else "blocked"))
+    if os.environ.get("GADMM_TOURNAMENT_GRAPH", "1") != "0":
+        # the graph-replayed phase kernels over the node's data planes (measured, never expected to win):
+        # the IPC transport always, RCCL on distinct GPUs (non-blocking, watchdog-bounded waits)
+        cands.append(dict(name="graph-ipc", build=make("graph", fabric="ipc"), hops=2.0, base=None))
+        if not share:
+            cands.append(dict(name="graph-rccl", build=make("graph", fabric="rccl"), hops=2.0, base=None))
     return cands
 
 
@@ -161,22 +188,35 @@ def run_headline(args, rank, world, device, share):
     d, m = int(X_cpu.shape[2]), int(X_cpu.shape[1])
     expect = EXPECTED_ITERS_1E8.get((args.workers, float(args.rho))) if args.tol == 1e-8 else None
     timeout_s = float(args.timeout)
+    tour_timeout_s = min(timeout_s, 5.0)
     hop = None
     if world > 1:
         # one-way hop latency of every chain boundary (the quantity that decides the engine ranking)
         from gadmm_amd.parallel.hop_probe import hop_probe
         hop = hop_probe(rank, world, device)
-    sol, tournament = None, None
+    sol, tournament, winner = None, None, None
     if world > 1 and args.engine == "auto":
-        # untimed: build and time every eligible multi-GPU engine, agree on the fastest (max over ranks)
+        # untimed: build and time every eligible multi-GPU engine, agree on the fastest (max over ranks).
+        # A candidate that stalls (e.g. a persistent kernel whose peers cannot be co-resident with ranks
+        # time-sharing one GPU) fails within the tournament's 5 s deadline instead of the full one; the
+        # winner is then REBUILT with the requested --timeout for the warm-up and the timed solves.
         from gadmm_amd.engine.tournament import engine_tournament
-        # a candidate that stalls (e.g. a persistent kernel whose peers cannot be co-resident with ranks
-        # time-sharing one GPU) fails within 5 s instead of the full hand-off deadline
-        cands = _headline_candidates(args, X_cpu, y_cpu, local, placement, rank, world, device, share, obj0,
-                                     min(timeout_s, 5.0))
+        cands = _headline_candidates(args, X_cpu, y_cpu, local, placement, rank, world, device, share, obj0)
         log = (lambda msg: print("bench.py: " + msg, file=sys.stderr, flush=True)) if rank == 0 else None
-        name, sol, tournament = engine_tournament(cands, world, solves=3, warm=1, expect=expect,
-                                                  sync=lambda: torch.cuda.synchronize(device), log=log)
+        winner, sol, tournament = engine_tournament([(c["name"], (lambda b=c["build"]: b(tour_timeout_s)))
+                                                     for c in cands], world, solves=3, warm=1, expect=expect,
+                                                    sync=lambda: torch.cuda.synchronize(device), log=log)
+        hop_us = max([h for h in (hop or {}).get("hop_us", []) if h is not None], default=None)
+        info = {c["name"]: c for c in cands}
+        for row in tournament:
+            c = info[row["engine"]]
+            row["hops_per_iter"] = round(c["hops"], 4)
+            its = row["iters"] if isinstance(row["iters"], int) else expect
+            row["predicted_ms"] = (round(its * (ONE_GPU_US[c["base"]] + c["hops"] * hop_us) / 1e3, 4)
+                                   if (c["base"] and hop_us is not None and its) else None)
+        if sol is not None:
+            sol.close()  # rebuilt below with the requested hand-off deadline (collective)
+            sol = info[winner]["build"](timeout_s)
     if sol is None:
         halo = None
         if args.engine == "replicated-halo" and world > 1:
@@ -210,14 +250,17 @@ def run_headline(args, rank, world, device, share):
         t1 = time.perf_counter()
         if world > 1:
             dist.barrier()
-        # every timed solve must have converged in the same (reference) iteration count
+        # every timed solve must have converged in the same (reference) iteration count, on every rank
         its = {r.iters for r in results}
         good = all(r.done == 1 for r in results) and len(its) == 1 and (expect is None or its == {expect})
+        if good and world > 1:
+            from gadmm_amd.engine.tournament import ranks_agree
+            good = ranks_agree(next(iter(its)), world)
         if all_ok(good, world):
             break
         # collective fallback: every rank leaves the persistent engine for the graph engine together and
         # the timing restarts there (warm-up + K steps); the JSON line names the fallback
-        if world == 1 or not sol.persistent or restarts >= 1:
+        if world == 1 or not sol.can_fall_back() or restarts >= 1:
             raise BenchFailure("timed solves: done=%s iterations=%s (expected %s)"
                                % (sorted({r.done for r in results}), sorted(its), expect))
         sol.fall_back("timed solve failed on some rank (done=%s here); timing restarted"
@@ -289,6 +332,9 @@ def run_headline(args, rank, world, device, share):
             out["hop_probe_same_device"] = hop.get("same_device")  # ranks sharing one GPU (rehearsal)
         if tournament is not None:
             out["engine_tournament"] = tournament  # every candidate's untimed-warm-up time (max over ranks)
+            out["tournament_winner"] = winner
+            out["tournament_deadline_s"] = tour_timeout_s
+        out["handoff_deadline_s"] = timeout_s  # the deadline of the warm-up and timed solves
         print(json.dumps(out), flush=True)
     sol.close()
 
@@ -354,15 +400,11 @@ def run_other(args, rank, world, device, share):
 
     comm = None
     args.share = share
-    if world > 1:
-        if share or args.fabric == "ipc":
-            comm = None  # RCCL cannot run with ranks on one GPU: the bodies build an IPC transport
-        else:
-            from gadmm_amd.parallel.comm import RcclComm
-            comm = RcclComm(device)
-    else:
+    if world == 1:
         from gadmm_amd.parallel.comm import LocalComm
         comm = LocalComm()
+    # several ranks: no communicator up front -- a body that needs a data plane builds it lazily
+    # (benchmarks.rank_comm: the IPC transport by default, RCCL with its watchdog for --fabric rccl)
     r = CONFIGS[args.config](args, rank, world, device, comm)
     if rank == 0:
         value = r["ms"] / 1e3

@@ -20,6 +20,14 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
     }                                                                                  \
   } while (0)
 
+// Return code of every RCCL-backed entry point whose communicator its watchdog aborted (a deadline
+// passed): the caller falls back to another data plane (Python: native.RcclDead).
+#define GADMM_RCCL_DEAD (-77)
+// Return code of a bounded host wait of the chain engine whose deadline passed (Python: NativeTimeout).
+#define GADMM_ENGINE_TIMEOUT (-78)
+// A watchdog abort after which the stream still did not drain: no fallback, the process must exit.
+#define GADMM_RCCL_WEDGED (-79)
+
 #ifdef __cplusplus
 extern "C" {
 #endif

@@ -40,7 +40,26 @@ __global__ void __launch_bounds__(256) lds_probe_kernel(unsigned long long* out,
 
 }  // namespace
 
+// One wave that keeps its stream busy for `ticks` of the 100 MHz s_memrealtime clock, then exits: a
+// bounded stand-in for a stalled peer in the watchdog tests (tests/test_gpu.py), never unbounded.
+__global__ void __launch_bounds__(64) busy_wait_kernel(unsigned long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 extern "C" {
+
+// Occupy `st` for `seconds` (at most 30 s): see busy_wait_kernel.
+int gadmm_debug_busy_wait(double seconds, hipStream_t st) {
+  if (!(seconds > 0.0) || seconds > 30.0) {
+    gadmm_set_error("debug_busy_wait: %g s out of (0, 30]", seconds);
+    return -1;
+  }
+  hipLaunchKernelGGL(busy_wait_kernel, dim3(1), dim3(64), 0, st, (unsigned long long)(seconds * 1e8));
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
 
 // out: [blocks][words] u64, the LDS content each probe workgroup found at start.
 int gadmm_lds_probe(void* out, int blocks, int words, hipStream_t st) {

@@ -302,13 +302,15 @@ __device__ __forceinline__ double cg_allsum(double v, double* sh) {
   return t;
 }
 
-// dinv = 1 / diag(M) (M full d x d), x = dinv * b, sc[1] = |b|^2, sc[2] = number of non-positive pivots
-__global__ void __launch_bounds__(CG_NT) cg_begin(const double* M, const double* b, double* dinv, double* x,
-                                                   double* sc, int d) {
+// dinv = 1 / diag(M), x = dinv * b, sc[1] = |b|^2, sc[2] = number of non-positive pivots. The diagonal
+// is read with stride `ds`: d + 1 for a full d x d M, 1 for a diagonal vector (the distributed CG,
+// whose M = sum over ranks of the local Grams exists only as its all-reduced diagonal)
+__global__ void __launch_bounds__(CG_NT) cg_begin(const double* M, long ds, const double* b, double* dinv,
+                                                   double* x, double* sc, int d) {
   __shared__ double sh[CG_NT / 64];
   double bb = 0.0, bad = 0.0;
   for (int j = threadIdx.x; j < d; j += CG_NT) {
-    const double m = M[(long)j * (d + 1)];
+    const double m = M[(long)j * ds];
     const double di = 1.0 / m;
     bad += (m > 0.0) ? 0.0 : 1.0;
     dinv[j] = di;
@@ -545,7 +547,18 @@ int gadmm_cg_begin(const double* M, const double* b, double* dinv, double* x, do
     gadmm_set_error("cg_begin: bad arguments (d=%d)", d);
     return -1;
   }
-  hipLaunchKernelGGL(cg_begin, dim3(1), dim3(CG_NT), 0, st, M, b, dinv, x, sc, d);
+  hipLaunchKernelGGL(cg_begin, dim3(1), dim3(CG_NT), 0, st, M, (long)d + 1, b, dinv, x, sc, d);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+// the same from diag(M) alone (distributed CG: the all-reduced diagonal of the rank-summed Gram)
+int gadmm_cg_begin_diag(const double* diag, const double* b, double* dinv, double* x, double* sc, int d,
+                        hipStream_t st) {
+  if (!diag || !b || !dinv || !x || !sc || d < 1) {
+    gadmm_set_error("cg_begin_diag: bad arguments (d=%d)", d);
+    return -1;
+  }
+  hipLaunchKernelGGL(cg_begin, dim3(1), dim3(CG_NT), 0, st, diag, 1L, b, dinv, x, sc, d);
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

@@ -22,6 +22,7 @@
 // rows padded by 4 doubles), the next chunk fetched into registers while the current one issues.
 #include "gadmm_common.h"
 #include <stdlib.h>
+#include <mutex>
 
 extern "C" int gadmm_spd_inverse_small_f64(const double* A, const double* shift, int N, int d, int nvar,
                                            double* out, int* status, hipStream_t st);
@@ -241,8 +242,12 @@ int gadmm_spd_inverse_blocked_f64(const double* A, const double* shift_host, int
   // engine). Each matrix's arithmetic is unchanged: bit-identical. The second stream waits for
   // everything enqueued on `st` before, and `st` waits for it at the end.
   const int total = N * nvar;
-  hipStream_t st2 = nullptr;
   if (total > 1) {
+    // The side stream and its fork / join events are per device and process-wide: one caller at a
+    // time enqueues through them (the lock covers the whole fork ... join, so two threads' matrices
+    // never interleave on the shared side stream or overwrite each other's events).
+    static std::mutex mu;
+    std::lock_guard<std::mutex> lock(mu);
     int dev = 0;
     GADMM_CHECK(hipGetDevice(&dev));
     static hipStream_t side[64] = {};
@@ -256,21 +261,30 @@ int gadmm_spd_inverse_blocked_f64(const double* A, const double* shift_host, int
       GADMM_CHECK(hipEventCreateWithFlags(&ev_in[dev], hipEventDisableTiming));
       GADMM_CHECK(hipEventCreateWithFlags(&ev_out[dev], hipEventDisableTiming));
     }
-    st2 = side[dev];
+    hipStream_t st2 = side[dev];
     GADMM_CHECK(hipEventRecord(ev_in[dev], st));
     GADMM_CHECK(hipStreamWaitEvent(st2, ev_in[dev], 0));
-    for (int m = 0; m < total; ++m) {
+    int rc = 0;
+    for (int m = 0; m < total && rc == 0; ++m) {
       const int n = m / nvar, v = m % nvar;
       hipStream_t sm = (m & 1) ? st2 : st;
       double* W = out + (long)m * dd;
       hipLaunchKernelGGL(shift_copy_kernel, dim3(grid_for(dd)), dim3(256), 0, sm, A + (long)n * dd,
                          shift_host[n * nvar + v], d, W);
-      GADMM_CHECK(hipGetLastError());
-      const int rc = blocked_inplace(W, d, nb, ws + ((m & 1) ? ws_doubles(d, nb) : 0), status, sm);
-      if (rc) return rc;
+      const hipError_t le = hipGetLastError();
+      if (le != hipSuccess) {
+        gadmm_set_error("spd_inverse_blocked: shift_copy launch: %s", hipGetErrorString(le));
+        rc = (int)le;
+        break;
+      }
+      rc = blocked_inplace(W, d, nb, ws + ((m & 1) ? ws_doubles(d, nb) : 0), status, sm);
     }
-    GADMM_CHECK(hipEventRecord(ev_out[dev], st2));
-    GADMM_CHECK(hipStreamWaitEvent(st, ev_out[dev], 0));
+    // Join the side stream on EVERY path (an error included): the caller frees `ws` / `out` once `st`
+    // is done, so `st` must not finish before work already queued on st2; a capture's fork is joined too.
+    const hipError_t e1 = hipEventRecord(ev_out[dev], st2);
+    const hipError_t e2 = e1 == hipSuccess ? hipStreamWaitEvent(st, ev_out[dev], 0) : e1;
+    if (rc) return rc;
+    GADMM_CHECK(e2);
     return 0;
   }
   for (int n = 0; n < N; ++n)

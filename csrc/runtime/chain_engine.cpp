@@ -15,6 +15,7 @@
 #include <vector>
 #include <chrono>
 #include <cstddef>
+#include <thread>
 
 #include "gadmm_common.h"
 #include "gadmm_chain.h"
@@ -33,6 +34,7 @@ int gadmm_ipc_exchange_rows(void* h, const XchgOp* ops, int nops, double* table,
                             hipStream_t st);
 int gadmm_ipc_allgather(void* h, const double* part, double* reduced, int ring, const int* lgid, int n_local,
                         ChainCtl* ctl, hipStream_t st);
+int gadmm_rccl_abort(void* h);
 }
 
 struct ChainEngine {
@@ -45,7 +47,49 @@ struct ChainEngine {
   int graph_block = 0, graph_plan = -1;
   ChainCtl* h_ctl = nullptr;  // pinned [2]
   hipEvent_t ev[2];
+  hipEvent_t ev_sync = nullptr;
   bool graph_ok = true;
+  // Watchdog of the host waits (gadmm_chain_engine_set_timeout; 0 = unbounded, the one-rank default).
+  // RCCL has no deadline of its own: a graph whose send/recv never matches would block
+  // hipEventSynchronize forever. With a deadline the waits poll; when it passes, an RCCL communicator
+  // is aborted (its kernels observe the abort flag and exit), the stream is drained, and the run
+  // returns GADMM_ENGINE_TIMEOUT -- the caller falls back with every rank (engine/multigpu.py). The IPC
+  // transport's kernels have their own deadlines (done = 4) and never need the abort.
+  double timeout_s = 0.0;
+
+  int wait_event(hipEvent_t ev) {
+    if (timeout_s <= 0) {
+      GADMM_CHECK(hipEventSynchronize(ev));
+      return 0;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    auto el = [&]() { return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count(); };
+    for (int k = 0;; ++k) {
+      hipError_t q = hipEventQuery(ev);
+      if (q == hipSuccess) return 0;
+      if (q != hipErrorNotReady) GADMM_CHECK(q);
+      if (el() > timeout_s) break;
+      if (k > 256) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+    if (desc.comm) gadmm_rccl_abort(desc.comm);
+    const auto t1 = std::chrono::steady_clock::now();
+    while (hipEventQuery(ev) == hipErrorNotReady &&
+           std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count() < 10.0)
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    if (hipEventQuery(ev) == hipErrorNotReady) {
+      gadmm_set_error("chain engine: a host wait passed its %.3f s deadline and the stream did not drain%s",
+                      timeout_s, desc.comm ? " after the RCCL abort" : "");
+      return GADMM_RCCL_WEDGED;
+    }
+    gadmm_set_error("chain engine: a host wait passed its %.3f s deadline%s", timeout_s,
+                    desc.comm ? " (RCCL communicator aborted)" : "");
+    return GADMM_ENGINE_TIMEOUT;
+  }
+
+  int wait_stream() {
+    GADMM_CHECK(hipEventRecord(ev_sync, desc.stream));
+    return wait_event(ev_sync);
+  }
 
   int flags_head() const {
     int f = PH_PRE_DUAL | PH_OBJ;
@@ -172,6 +216,7 @@ void* gadmm_chain_engine_create(const EngineDesc* desc) {
   memset(e->h_ctl, 0, 2 * sizeof(ChainCtl));
   hipEventCreateWithFlags(&e->ev[0], hipEventDisableTiming);
   hipEventCreateWithFlags(&e->ev[1], hipEventDisableTiming);
+  hipEventCreateWithFlags(&e->ev_sync, hipEventDisableTiming);
   return e;
 }
 
@@ -181,6 +226,7 @@ void gadmm_chain_engine_destroy(void* h) {
   e->drop_graph();
   hipEventDestroy(e->ev[0]);
   hipEventDestroy(e->ev[1]);
+  if (e->ev_sync) hipEventDestroy(e->ev_sync);
   if (e->h_ctl) hipHostFree(e->h_ctl);
   delete e;
 }
@@ -260,7 +306,7 @@ int gadmm_chain_engine_run(void* h, int block, int stop_iter, int use_graph, Run
   ChainCtl last{};
   // read the starting iteration
   GADMM_CHECK(hipMemcpyAsync(&e->h_ctl[0], e->desc.base.ctl, sizeof(ChainCtl), hipMemcpyDeviceToHost, st));
-  GADMM_CHECK(hipStreamSynchronize(st));
+  if (int w = e->wait_stream()) return w;
   const int start = e->h_ctl[0].iter;
   if (e->h_ctl[0].done) {
     last = e->h_ctl[0];
@@ -285,13 +331,13 @@ int gadmm_chain_engine_run(void* h, int block, int stop_iter, int use_graph, Run
       GADMM_CHECK(hipMemcpyAsync(&e->h_ctl[k & 1], e->desc.base.ctl, sizeof(ChainCtl), hipMemcpyDeviceToHost, st));
       GADMM_CHECK(hipEventRecord(e->ev[k & 1], st));
       if (k > 0) {
-        GADMM_CHECK(hipEventSynchronize(e->ev[(k - 1) & 1]));
+        if (int w = e->wait_event(e->ev[(k - 1) & 1])) return w;
         if (e->h_ctl[(k - 1) & 1].done) stop = true;  // one replay in flight beyond the decision
       }
       if (budget <= 0) stop = true;
       ++k;
     }
-    GADMM_CHECK(hipStreamSynchronize(st));
+    if (int w = e->wait_stream()) return w;
     last = e->h_ctl[(k - 1) & 1];
   }
   auto t1 = std::chrono::steady_clock::now();
@@ -318,6 +364,16 @@ int gadmm_chain_engine_run(void* h, int block, int stop_iter, int use_graph, Run
   return 0;
 }
 
+int gadmm_chain_engine_set_timeout(void* h, double timeout_s) {
+  ChainEngine* e = (ChainEngine*)h;
+  if (!e) {
+    gadmm_set_error("chain_engine_set_timeout: null engine");
+    return -1;
+  }
+  e->timeout_s = timeout_s > 0 ? timeout_s : 0.0;
+  return 0;
+}
+
 int gadmm_chain_engine_graph_ok(void* h) { return ((ChainEngine*)h)->graph_ok ? 1 : 0; }
 
 // One eager exchange with the current plan (which = 0: after-head messages, 1: after-tail).
@@ -327,8 +383,7 @@ int gadmm_chain_engine_exchange(void* h, int which) {
   if (ops.empty()) return 0;
   int r = e->exchange_ops(ops, 2 + (which != 0));  // phase codes 2/3: never collide with the in-loop 0/1
   if (r) return r;
-  GADMM_CHECK(hipStreamSynchronize(e->desc.stream));
-  return 0;
+  return e->wait_stream();
 }
 
 // ABI self-description: sizes and a few offsets of every struct shared with Python (ctypes).

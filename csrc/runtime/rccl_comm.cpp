@@ -13,33 +13,84 @@
 #include <rccl/rccl.h>
 #include <string.h>
 #include <atomic>
+#include <chrono>
+#include <thread>
 
 #include "gadmm_common.h"
 #include "gadmm_chain.h"
 
 
+// Watchdog (RCCL has no deadline of its own): the communicator is created NON-BLOCKING, so neither its
+// set-up nor a grouped enqueue can block the host forever -- both are polled with
+// ncclCommGetAsyncError against `timeout_s`; host waits on a stream that carries RCCL work go through
+// gadmm_rccl_wait (event polling against the deadline, async errors checked). A deadline that passes
+// aborts the communicator (ncclCommAbort: the RCCL kernels in flight observe the abort flag and exit),
+// marks it dead, and returns an error: the caller falls back, together with every other rank, to the
+// IPC transport (engine/multigpu.py, parallel/dataplane.py). A dead communicator refuses every call.
 struct RcclComm {
-  ncclComm_t comm;
-  int rank, nranks, device;
+  ncclComm_t comm = nullptr;
+  int rank = 0, nranks = 0, device = 0;
+  double timeout_s = 60.0;
+  bool aborted = false;
+  hipEvent_t ev = nullptr;
   std::atomic<long long> bytes_sent{0}, bytes_recv{0}, msgs_sent{0}, coll_bytes{0};
 };
 
+namespace {
+
+double since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+void abort_comm(RcclComm* c) {
+  if (c->comm && !c->aborted) ncclCommAbort(c->comm);  // frees the communicator
+  c->comm = nullptr;
+  c->aborted = true;
+}
+
+// Drive a non-blocking call to completion: ncclInProgress is polled until the communicator reports
+// success or an error, or the deadline passes (then the communicator is aborted).
+ncclResult_t settle(RcclComm* c, ncclResult_t r) {
+  if (r != ncclInProgress) return r;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int k = 0;; ++k) {
+    ncclResult_t a = ncclSuccess;
+    ncclResult_t q = ncclCommGetAsyncError(c->comm, &a);
+    if (q != ncclSuccess) return q;
+    if (a != ncclInProgress) return a;
+    if (since(t0) > c->timeout_s) {
+      abort_comm(c);
+      return ncclSystemError;
+    }
+    if (k > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
+}  // namespace
+
 // Every entry point takes the handle from Python / the engine: a null one is an error, not a crash.
-#define RCCL_HANDLE(h)                                         \
-  RcclComm* c = (RcclComm*)(h);                                \
-  do {                                                         \
-    if (!c) {                                                  \
-      gadmm_set_error("%s: null RCCL communicator", __func__); \
-      return -1;                                               \
-    }                                                          \
+#define RCCL_HANDLE(h)                                                                  \
+  RcclComm* c = (RcclComm*)(h);                                                         \
+  do {                                                                                  \
+    if (!c) {                                                                           \
+      gadmm_set_error("%s: null RCCL communicator", __func__);                          \
+      return -1;                                                                        \
+    }                                                                                   \
+    if (c->aborted) {                                                                   \
+      gadmm_set_error("%s: RCCL communicator aborted by its watchdog", __func__);       \
+      return GADMM_RCCL_DEAD;                                                           \
+    }                                                                                   \
   } while (0)
 
+// Every RCCL call of this file: ncclInProgress (non-blocking communicator) is settled against the
+// watchdog deadline; a communicator aborted meanwhile reports GADMM_RCCL_DEAD.
 #define NCCL_CHECK(expr)                                                                  \
   do {                                                                                    \
-    ncclResult_t _r = (expr);                                                             \
+    ncclResult_t _r = settle(c, (expr));                                                  \
     if (_r != ncclSuccess) {                                                              \
-      gadmm_set_error("%s:%d %s -> %s", __FILE__, __LINE__, #expr, ncclGetErrorString(_r)); \
-      return -(int)_r - 1000;                                                             \
+      gadmm_set_error("%s:%d %s -> %s%s", __FILE__, __LINE__, #expr, ncclGetErrorString(_r), \
+                      c->aborted ? " (watchdog: communicator aborted)" : "");            \
+      return c->aborted ? GADMM_RCCL_DEAD : -(int)_r - 1000;                              \
     }                                                                                     \
   } while (0)
 
@@ -47,7 +98,11 @@ extern "C" {
 
 int gadmm_rccl_unique_id(char* out128) {
   ncclUniqueId id;
-  NCCL_CHECK(ncclGetUniqueId(&id));
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) {
+    gadmm_set_error("ncclGetUniqueId: %s", ncclGetErrorString(r));
+    return -(int)r - 1000;
+  }
   static_assert(sizeof(ncclUniqueId) == 128, "unexpected ncclUniqueId size");
   memcpy(out128, &id, 128);
   return 0;
@@ -59,7 +114,9 @@ int gadmm_rccl_version(void) {
   return v;
 }
 
-void* gadmm_rccl_init(const char* id128, int nranks, int rank, int device) {
+// Non-blocking communicator set-up with a deadline (timeout_s <= 0: 60 s). nullptr on failure or timeout
+// (gadmm_last_error says which); a timed-out set-up is aborted, never left half-initialised.
+void* gadmm_rccl_init_timeout(const char* id128, int nranks, int rank, int device, double timeout_s) {
   hipError_t he = hipSetDevice(device);
   if (he != hipSuccess) {
     gadmm_set_error("hipSetDevice(%d): %s", device, hipGetErrorString(he));
@@ -71,19 +128,91 @@ void* gadmm_rccl_init(const char* id128, int nranks, int rank, int device) {
   c->rank = rank;
   c->nranks = nranks;
   c->device = device;
-  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+  c->timeout_s = timeout_s > 0 ? timeout_s : 60.0;
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  ncclResult_t r = ncclCommInitRankConfig(&c->comm, nranks, id, rank, &cfg);
+  if (r == ncclInProgress || r == ncclSuccess) r = settle(c, ncclInProgress);
   if (r != ncclSuccess) {
-    gadmm_set_error("ncclCommInitRank: %s", ncclGetErrorString(r));
+    gadmm_set_error("ncclCommInitRankConfig: %s%s", ncclGetErrorString(r),
+                    c->aborted ? " (set-up deadline passed: aborted)" : "");
+    if (!c->aborted && c->comm) ncclCommAbort(c->comm);
+    delete c;
+    return nullptr;
+  }
+  if (hipEventCreateWithFlags(&c->ev, hipEventDisableTiming) != hipSuccess) {
+    gadmm_set_error("rccl_init: hipEventCreate failed");
+    ncclCommDestroy(c->comm);
     delete c;
     return nullptr;
   }
   return c;
 }
 
+void* gadmm_rccl_init(const char* id128, int nranks, int rank, int device) {
+  return gadmm_rccl_init_timeout(id128, nranks, rank, device, 60.0);
+}
+
+int gadmm_rccl_set_timeout(void* h, double timeout_s) {
+  RCCL_HANDLE(h);
+  c->timeout_s = timeout_s > 0 ? timeout_s : 60.0;
+  return 0;
+}
+
+// 1 = usable, 0 = aborted by the watchdog (or a null handle).
+int gadmm_rccl_alive(void* h) {
+  RcclComm* c = (RcclComm*)h;
+  return (c && !c->aborted && c->comm) ? 1 : 0;
+}
+
+// Abort the communicator now (a peer is known to be gone). Idempotent.
+int gadmm_rccl_abort(void* h) {
+  RcclComm* c = (RcclComm*)h;
+  if (!c) return 0;
+  abort_comm(c);
+  return 0;
+}
+
+// Host wait for the work queued on `st` so far (RCCL included), bounded by the watchdog deadline
+// (timeout_s <= 0: the communicator's). 0 = done; GADMM_RCCL_DEAD = the deadline passed or RCCL
+// reported an asynchronous error: the communicator was aborted (its kernels exit), the stream is
+// drained for up to 10 s more, and the caller must fall back.
+int gadmm_rccl_wait(void* h, hipStream_t st, double timeout_s) {
+  RCCL_HANDLE(h);
+  const double lim = timeout_s > 0 ? timeout_s : c->timeout_s;
+  GADMM_CHECK(hipEventRecord(c->ev, st));
+  const auto t0 = std::chrono::steady_clock::now();
+  for (int k = 0;; ++k) {
+    hipError_t q = hipEventQuery(c->ev);
+    if (q == hipSuccess) return 0;
+    if (q != hipErrorNotReady) GADMM_CHECK(q);
+    ncclResult_t a = ncclSuccess;
+    ncclCommGetAsyncError(c->comm, &a);
+    const bool bad = a != ncclSuccess && a != ncclInProgress;
+    if (bad || since(t0) > lim) {
+      abort_comm(c);
+      const auto t1 = std::chrono::steady_clock::now();
+      while (hipEventQuery(c->ev) == hipErrorNotReady && since(t1) < 10.0)
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+      if (hipEventQuery(c->ev) == hipErrorNotReady) {
+        // the stream did not drain after the abort: nothing further may run on this device
+        gadmm_set_error("rccl_wait: %s after %.3f s; communicator aborted but the stream did not drain in 10 s",
+                        bad ? ncclGetErrorString(a) : "deadline passed", since(t0));
+        return GADMM_RCCL_WEDGED;
+      }
+      gadmm_set_error("rccl_wait: %s after %.3f s: communicator aborted", bad ? ncclGetErrorString(a) : "deadline passed",
+                      since(t0));
+      return GADMM_RCCL_DEAD;
+    }
+    if (k > 64) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
 int gadmm_rccl_destroy(void* h) {
   RcclComm* c = (RcclComm*)h;
   if (!c) return 0;
-  ncclCommDestroy(c->comm);
+  if (c->comm && !c->aborted) ncclCommDestroy(c->comm);
+  if (c->ev) hipEventDestroy(c->ev);
   delete c;
   return 0;
 }

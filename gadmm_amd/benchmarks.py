@@ -35,6 +35,71 @@ EXPECTED_ITERS_1E8 = {(24, 3.0): 1373, (24, 5.0): 758, (24, 7.0): 428,
                       (16, 3.0): 588, (16, 5.0): 254, (16, 7.0): 249,
                       (8, 3.0): 93, (8, 5.0): 126, (8, 7.0): 131}
 
+# The correctness gate of every other bench config: iterations of the reference semantics for the
+# bench's exact problem, seeds and stop rule, keyed by (config, workers[, coherence]). Each entry is
+# reproduced by ``reference_expected`` (tests/test_bench_contract.py asserts the table against it):
+# * dgadmm: oracle.reference.dgadmm_linear (dynamic_group_ADMM_closedForm.m:16-186) on
+#   linear_synthetic(N), rho = 1, 1e-4, initial chain find_path(N, seed 5), re-chains
+#   find_path2(N, seed 99) every `coherence` iterations -- the stream PathSchedule(seed=99) draws;
+# * logistic: oracle.reference.gadmm_logistic_gd (group_ADMM_logistic_GD.m + logReg_GD.m),
+#   rho = 2e-4, step 2.2, lambda = 1e-5, 1e-4;
+# * star: oracle.reference.std_admm_linear (standared_ADMM.m), rho = 1, 1e-4; gadmm_rho1 is the
+#   GADMM the star config runs next to it (group_ADMM_closedForm.m, rho = 1);
+# * logistic_exact: the exact-prox variant (group_ADMM_logistic.m is CVX, dead code upstream) has
+#   no MATLAB-semantics oracle; its spec is the torch Newton path (algorithms.gadmm
+#   .group_admm_logistic_exact), rho = 1e-3, 1e-8.
+EXPECTED_OTHER = {("dgadmm", 24, 10): 510, ("dgadmm", 24, 1): 252, ("dgadmm", 8, 10): 83, ("dgadmm", 8, 1): 49,
+                  ("logistic", 24): 53, ("logistic", 8): 113,
+                  ("logistic_exact", 24): 424, ("logistic_exact", 8): 109,
+                  ("star", 24): 348, ("star", 8): 55, ("gadmm_rho1", 24): 2425, ("gadmm_rho1", 8): 196}
+
+
+def reference_expected(config: str, n: int, coherence: int = 10):
+    """Iterations of the reference semantics for ``bench.py --config <config> --workers n`` (see
+    EXPECTED_OTHER), computed on the CPU (< 1 s for N <= 24 except logistic_exact, ~3 s)."""
+    from .oracle import reference as R
+    from .parallel import topology as T
+    from .data import linear_synthetic, logistic_synthetic
+
+    if config in ("dgadmm", "star", "gadmm_rho1"):
+        ds = linear_synthetic(n)
+        X, y = ds.X.numpy(), ds.y.numpy()
+        obj0 = R.opt_linear(X.reshape(-1, X.shape[2]), y.reshape(-1))
+        if config == "star":
+            return R.std_admm_linear(X, y, 1.0, 20000, obj0, 1e-4).iters
+        if config == "gadmm_rho1":
+            return R.gadmm_linear(X, y, 1.0, 20000, obj0, 1e-4).iters
+        p0, c0, _ = T.find_path(n, np.random.default_rng(5))
+        rng, seq = np.random.default_rng(99), {}
+
+        def rechain(it):
+            if it not in seq:
+                p, c, _, _, _ = T.find_path2(n, rng)
+                seq[it] = (p, c)
+            return seq[it]
+
+        return R.dgadmm_linear(X, y, 1.0, 3000, obj0, 1e-4, p0, c0, coherence, rechain).iters
+    from .models import LogisticRegression
+    ds = logistic_synthetic(n)
+    m = LogisticRegression(ds.X, ds.y, lam=1e-5)
+    obj0 = m.optimum(None, n_total=n)
+    if config == "logistic":
+        return R.gadmm_logistic_gd(ds.X.numpy(), ds.y.numpy(), 2e-4, 400, obj0, 1e-5, 1e-4, 2.2).iters
+    if config == "logistic_exact":
+        from .algorithms.gadmm import group_admm_logistic_exact
+        return group_admm_logistic_exact(m, 1e-3, obj0, 1e-8, 2000).iters
+    raise KeyError(config)
+
+
+def expected_for(config: str, n: int, coherence: int = 10):
+    """The pinned count, or (a worker count outside the table, N <= 64) the oracle's, or None."""
+    key = (config, n, coherence) if config == "dgadmm" else (config, n)
+    if key in EXPECTED_OTHER:
+        return EXPECTED_OTHER[key]
+    if n <= 64:
+        return int(reference_expected(config, n, coherence))
+    return None
+
 
 def headline_rank_problem(workers: int, rank: int, world: int, builder=None):
     """This rank's part of the headline problem, data-local: only the rank's own workers' shards are
@@ -98,13 +163,22 @@ def linear_obj0_distributed(X, y, local, workers: int, world: int) -> float:
 
 
 def rank_comm(args, world: int, device, comm, n_total: int, d: int, ring: int = 16):
-    """The data plane of a config body: the given communicator (RCCL on a node, LocalComm on one
-    GPU), or -- ranks sharing one GPU (``GADMM_BENCH_SHARE_GPU=1``), where RCCL cannot run -- an IPC
-    device-copy transport sized for this problem."""
-    if comm is not None or world == 1:
+    """The data plane of a config body, built lazily (only bodies that need one call this): the given
+    comm if any, LocalComm on one rank, else ``parallel/dataplane.make_data_plane`` -- the IPC
+    device-copy transport by default (the rehearsed path, on a node and with ranks sharing a GPU),
+    RCCL with its watchdog only for ``--fabric rccl`` on distinct GPUs (an RCCL set-up failure on any
+    rank sends every rank to IPC)."""
+    if comm is not None:
         return comm
-    from .parallel.ipc import IpcComm
-    return IpcComm(n_total, d, ring, device)
+    from .parallel.dataplane import make_data_plane
+    return make_data_plane(getattr(args, "fabric", "auto"), world, device, bool(getattr(args, "share", False)),
+                           n_total, d, ring, timeout_s=float(getattr(args, "timeout", 20.0)))
+
+
+def data_plane_fields(comm) -> Dict:
+    """JSON fields naming the data plane a body used and why (``make_data_plane``'s selection)."""
+    sel = getattr(comm, "selection", None) or {"data_plane": getattr(comm, "backend", "local")}
+    return {"data_plane": sel.get("data_plane"), "data_plane_reason": sel.get("reason")}
 
 
 def _timed(solve: Callable, steps: int, warmup: int, device, world: int):
@@ -180,10 +254,10 @@ def run_logistic(args, rank, world, device, comm) -> Dict:
         fabric.close()
     return {"metric": "wall-clock to 1e-4 objective gap, GADMM logistic regression, inner-GD HIP kernel "
                       "(LogisticRegression_Synthetic)",
-            "ms": ms, "iters": r.iters, "expected": 53 if n == 24 else None, "backend": r.extra.get("backend"),
+            "ms": ms, "iters": r.iters, "expected": expected_for("logistic", n), "backend": r.extra.get("backend"),
             "engine": r.extra.get("engine"), "transport": r.extra.get("transport"),
             "theta_payload_bytes_per_solve": _sum_ranks(r.bytes_sent, world),
-            "wire_bytes_per_solve": _sum_ranks(r.extra.get("wire_bytes", 0), world),
+            "wire_bytes_per_solve": _sum_ranks(r.extra.get("wire_bytes", 0), world), **data_plane_fields(comm),
             "config": {"model": "LogisticRegression_Synthetic GADMM inner-GD", "workers": n, "features": ds.dim,
                        "samples_per_worker": ds.rows_per_worker, "rho": rho, "gd_step": 2.2, "lam": 1e-5,
                        "tol": tol, "global_batch": n * ds.rows_per_worker, "seq_len": 1,
@@ -214,7 +288,8 @@ def run_logistic_exact(args, rank, world, device, comm) -> Dict:
     ms, r = _timed(solve, args.steps, args.warmup, device, world)
     return {"metric": "wall-clock to 1e-8 objective gap, GADMM logistic regression, exact (Newton) local solves "
                       "(LogisticRegression_Synthetic)",
-            "ms": ms, "iters": r.iters, "expected": 424 if n == 24 else None, "backend": r.extra.get("backend"),
+            "ms": ms, "iters": r.iters, "expected": expected_for("logistic_exact", n), "backend": r.extra.get("backend"),
+            **data_plane_fields(comm),
             "config": {"model": "LogisticRegression_Synthetic GADMM exact-prox", "workers": n, "features": ds.dim,
                        "samples_per_worker": ds.rows_per_worker, "rho": rho, "lam": 1e-5, "tol": tol,
                        "global_batch": n * ds.rows_per_worker, "seq_len": 1,
@@ -268,7 +343,7 @@ def run_dgadmm(args, rank, world, device, comm) -> Dict:
     ms, r = _timed(solve, args.steps, args.warmup, device, world)
     out = {"metric": "wall-clock to 1e-4 objective gap, D-GADMM (findPath2 re-chaining every %d iteration%s), "
                      "linear regression (LinearRegression_Synthetic)" % (coh, "" if coh == 1 else "s"),
-           "ms": ms, "iters": r.iters, "expected": None, "backend": r.extra.get("backend"),
+           "ms": ms, "iters": r.iters, "expected": expected_for("dgadmm", n, coh), "backend": r.extra.get("backend"),
            "engine": r.extra.get("engine"), "transport": r.extra.get("transport"),
            "theta_payload_bytes_per_solve": _sum_ranks(r.bytes_sent, world),
            "wire_bytes_per_solve": _sum_ranks(r.extra.get("wire_bytes", 0), world),
@@ -393,6 +468,8 @@ def run_real10m(args, rank, world, device, comm) -> Dict:
     out["star_admm_transport"] = s.extra.get("transport", getattr(comm, "backend", "local"))
     out["gadmm_engine"] = r.extra.get("engine")
     out["transport"] = getattr(comm, "backend", "local")
+    out.update(data_plane_fields(comm))
+    out["optimum_path"] = getattr(state["m"], "last_optimum_path", None)  # distributed-cg / gram-allreduce / local
     out["gadmm_theta_bytes_per_solve"] = _sum_ranks(r.bytes_sent, world)
     out["star_coll_bytes_per_solve"] = _sum_ranks(s.bytes_sent, world)
     return out
@@ -422,8 +499,8 @@ def run_star(args, rank, world, device, comm) -> Dict:
             from .parallel.comm import RankInfo
             sopts["fabric"] = fabric
             comm = RankInfo(rank, world)
-        elif comm is None:
-            raise RuntimeError("run_star: no xGMI fabric and no RCCL communicator (ranks sharing one GPU)")
+        else:
+            comm = rank_comm(args, world, device, comm, n, d, 16)
 
     def solve():
         return standard_admm(m, local, n, rho, obj0, tol, 20000, comm=comm, placement=pl, engine_opts=sopts)
@@ -446,13 +523,13 @@ def run_star(args, rank, world, device, comm) -> Dict:
     gs = time.perf_counter() - t0
     out = {"metric": "wall-clock to 1e-4 objective gap, star (parameter-server) ADMM, linear regression "
                      "(LinearRegression_gadmm_vs_admm)",
-           "ms": ms, "iters": r.iters, "expected": 348 if n == 24 else None, "backend": r.extra.get("backend"),
+           "ms": ms, "iters": r.iters, "expected": expected_for("star", n), "backend": r.extra.get("backend"),
            "engine": r.extra.get("engine"),
            "theta_payload_bytes_per_solve": _sum_ranks(r.bytes_sent, world),
            "wire_bytes_per_solve": _sum_ranks(r.extra.get("wire_bytes", 0), world),
            "monitor_bytes_per_solve": _sum_ranks(r.extra.get("monitor_bytes", 0), world),
            "setup_in_timed_region": True, "setup_ms": _setup_ms(r.extra["engine_obj"], m, device),
-           "gadmm_s": gs, "gadmm_iters": g.iters, "gadmm_expected_iters": 2425 if n == 24 else None,
+           "gadmm_s": gs, "gadmm_iters": g.iters, "gadmm_expected_iters": expected_for("gadmm_rho1", n),
            "gadmm_theta_payload_bytes_per_solve": _sum_ranks(g.bytes_sent, world),
            "reference_comm_units": {"star": 2 * (n - 1) * r.iters, "gadmm": n * g.iters},
            "config": {"model": "LinearRegression_Synthetic star-ADMM closed-form", "workers": n, "features": d,

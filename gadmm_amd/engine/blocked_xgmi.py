@@ -27,7 +27,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from typing import List, Optional
+from typing import List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -35,7 +35,7 @@ import torch.distributed as dist
 from ..ops import native
 from ..ops.linalg import gram, spd_inverse
 from ..parallel.topology import Placement
-from ..parallel.xgmi import _Buf, preflight
+from ..parallel.xgmi import _Buf, device_identity, preflight
 
 
 MAXW = 12  # waves (computed positions) per workgroup of chain_blocked_kernel
@@ -66,13 +66,33 @@ def dl_halo_hosted(lo: int, hi: int, n: int) -> bool:
     return hi - lo + 1 + len(halo_heads(lo, hi, n)) > MAXW
 
 
+def replicated_plans(n_total: int, placement: Placement, d: int, max_k: int = 6) -> List[Tuple[int, int]]:
+    """Every (k, pw) the replicated-halo kernel admits for this chain (``gadmm_chain_blocked_plan2``
+    with want_k = 1..max_k for both wave layouts, deduplicated): the engine tournament times each. A
+    larger k exchanges (theta, mu) once per k iterations -- fewer cross-GPU hops per iteration -- at the
+    cost of a 2k-position halo (more replicated shards, more halo GEMVs)."""
+    lib = native.require()
+    segs = [placement.local_workers(r) for r in range(placement.nranks)]
+    nseg = max(len(s) for s in segs)
+    out: List[Tuple[int, int]] = []
+    for pw in (1, 2):
+        for k in range(1, max_k + 1):
+            kk, ll, pp = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(1)
+            if int(lib.gadmm_chain_blocked_plan2(nseg, int(d), k, pw, ctypes.byref(kk), ctypes.byref(ll),
+                                                 ctypes.byref(pp))) <= 0:
+                continue
+            if kk.value == k and pp.value == pw and (k, pw) not in out:
+                out.append((k, pw))
+    return out
+
+
 class BlockedXgmiEngine:
     LAG = 8
 
     def __init__(self, X_all: torch.Tensor, y_all: torch.Tensor, n_total: int, placement: Placement, rank: int,
                  rho: float, obj0: float, tol: float, max_iter: int, device: torch.device, group=None,
                  want_k: int = 0, data_local: bool = False, dl_halo: Optional[bool] = None,
-                 stream: Optional[torch.cuda.Stream] = None):
+                 stream: Optional[torch.cuda.Stream] = None, want_pw: int = 0):
         """Collective over ``group``. ``data_local=False``: ``X_all`` / ``y_all`` hold the shards of at
         least this rank's computed range (indexable by global worker id); only those rows are read.
         ``data_local=True``: ``X_all`` / ``y_all`` are this rank's own shards, in segment order.
@@ -104,9 +124,12 @@ class BlockedXgmiEngine:
                 raise RuntimeError("data-local blocked engine: no plan for d=%d, %d positions" % (self.d, nseg))
         else:
             nseg = max(hi - lo + 1 for lo, hi in segs)
-            if int(self.lib.gadmm_chain_blocked_plan2(nseg, self.d, int(want_k), 0, ctypes.byref(kk), ctypes.byref(ll),
-                                                      ctypes.byref(pp))) <= 0:
+            if int(self.lib.gadmm_chain_blocked_plan2(nseg, self.d, int(want_k), int(want_pw), ctypes.byref(kk),
+                                                      ctypes.byref(ll), ctypes.byref(pp))) <= 0:
                 raise RuntimeError("blocked xgmi engine: no blocking plan for d=%d" % self.d)
+            if want_k > 0 and kk.value != int(want_k):
+                raise ValueError("blocked xgmi engine: k = %d is not admitted (plan gives k = %d, pw = %d)"
+                                 % (want_k, kk.value, pp.value))
         self.k, self.L, self.pw = kk.value, ll.value, pp.value
         H = 0 if self.data_local else 2 * self.k
         self.H = H
@@ -164,7 +187,7 @@ class BlockedXgmiEngine:
         except Exception as e:  # pragma: no cover - box dependent
             err = "rank %d alloc: %s" % (rank, e)
         allh = [None] * self.nranks
-        dist.all_gather_object(allh, (h, err, torch.cuda.current_device()), group=group)
+        dist.all_gather_object(allh, (h, err, device_identity()), group=group)
         errs = [e for _, e, _ in allh if e]
         devs = [dv for _, _, dv in allh]
         ok = not errs

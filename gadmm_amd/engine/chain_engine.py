@@ -458,6 +458,10 @@ class NativeChainEngine:
         if blk > self.ring and self.nranks > 1:
             raise ValueError("block must be <= ring for multi-rank runs")
         self._sync_plan()
+        # the watchdog of the host waits: an RCCL data plane has no deadline of its own (the engine
+        # aborts the communicator when it passes; native.RcclDead / NativeTimeout reach the caller)
+        tmo = float(getattr(self.comm, "timeout_s", 0.0) or 0.0) if getattr(self.comm, "backend", "") == "rccl" else 0.0
+        native.check(self.lib.gadmm_chain_engine_set_timeout(self.handle, tmo), "chain_engine_set_timeout")
         rc = self.lib.gadmm_chain_engine_run(self.handle, blk, int(stop_iter), 1 if use_graph else 0,
                                              ctypes.byref(st))
         native.check(rc, "chain_engine_run")

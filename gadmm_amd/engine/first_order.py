@@ -55,7 +55,7 @@ class FoFabric:
 
     def __init__(self, n_total: int, d: int, rank: int, nranks: int, device: torch.device, comm=None,
                  ring: int = RING):
-        from ..parallel.xgmi import _Buf, preflight
+        from ..parallel.xgmi import _Buf, device_identity, preflight
 
         self.lib = native.require()
         self.n, self.d, self.rank, self.nranks, self.ring = int(n_total), int(d), rank, nranks, ring
@@ -71,7 +71,7 @@ class FoFabric:
         except Exception as e:  # pragma: no cover - box dependent
             err = "rank %d alloc: %s" % (rank, e)
         allh = [None] * nranks
-        dist.all_gather_object(allh, (mine, err, torch.cuda.current_device()), group=_group(comm))
+        dist.all_gather_object(allh, (mine, err, device_identity()), group=_group(comm))
         errs = [e for _, e, _ in allh if e]
         ok = not errs
         if ok:

@@ -238,7 +238,10 @@ class FirstOrderBigEngine:
                     if alg == "GD":
                         ck(symv(self.Asum.data_ptr(), 0, th.data_ptr(), 0, q.data_ptr(), 0, work, 1, d, ctl, st), "symv")
                         if self.multi:
-                            self._allreduce(q[0])
+                            # the d real entries only (a contiguous view): the zero padding of q[0]
+                            # would cross the fabric every iteration and the bytes would disagree with
+                            # the reported payload
+                            self._allreduce(q[0, :d])
                             pay[-1] += d * 8 * (self.nranks - 1)
                         ck(L.gadmm_fob_gd(q.data_ptr(), self.bsum.data_ptr(), th.data_ptr(), part.data_ptr(), d,
                                           float(step), int(faithful), ctl, st), "fob_gd")

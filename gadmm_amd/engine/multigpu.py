@@ -16,8 +16,10 @@ order ``engine="auto"`` tries them:
 2. ``xgmi`` -- the per-worker persistent kernel (chain_persistent.hip, SYS scope): one workgroup per
    local worker, boundary theta stored straight into the neighbour GPU's table over xGMI, objective
    granules to rank 0's monitor, decisions fanned back out. One launch per solve.
-3. ``rccl`` / ``ipc`` -- the graph-replayed phase kernels (chain_engine.cpp) with RCCL send/recv, or
-   with the device-copy transport (parallel/ipc.py; the only option when ranks share one GPU).
+3. ``ipc`` / ``rccl`` -- the graph-replayed phase kernels (chain_engine.cpp) with the device-copy
+   transport (parallel/ipc.py; the default data plane, and the only one when ranks share one GPU), or
+   with RCCL send/recv when ``fabric="rccl"`` is asked for (non-blocking communicator, bounded host
+   waits: a hung RCCL graph is aborted and every rank moves to ``ipc``).
 
 Every choice is agreed by all ranks (an all-reduce of a success flag), and so is every fallback: a
 solve that fails on ANY rank (a stalled hand-off reaches its deadline: ``done == 4``) makes every
@@ -76,7 +78,7 @@ class DistributedChainSolver:
                  rank: int, world: int, device: torch.device, rho: float, obj0: float, tol: float,
                  max_iter: int = 20000, engine: str = "auto", fabric: str = "auto", share: bool = False,
                  block: int = 0, halo_data=None, timeout_s: float = 20.0, use_graph: bool = True,
-                 dl_halo: Optional[bool] = None, strict: bool = False):
+                 dl_halo: Optional[bool] = None, strict: bool = False, halo_k: int = 0, halo_pw: int = 0):
         """``dl_halo`` (data-local blocked engine): None = the halo mode where eligible, True = only the
         halo mode, False = never. ``strict``: raise (on every rank together) when the requested
         persistent engine cannot run instead of falling back to the graph engine (the engine
@@ -105,9 +107,11 @@ class DistributedChainSolver:
             if halo_data is None:
                 raise ValueError("replicated-halo needs the halo workers' shards (halo_data=(X_all, y_all))")
             self.blk = BlockedXgmiEngine(halo_data[0], halo_data[1], n_total, placement, rank, rho, obj0, tol,
-                                         max_iter, device, stream=solver_stream(device))
+                                         max_iter, device, stream=solver_stream(device), want_k=halo_k,
+                                         want_pw=halo_pw)
             self.replicated_bytes = self.blk.replicated_shard_bytes()
-            self.persistent, self.kind = True, "xgmi(replicated-halo)"
+            self.persistent = True
+            self.kind = "xgmi(replicated-halo,k=%d,pw=%d)" % (self.blk.k, self.blk.pw)
         else:
             if fabric in ("auto", "xgmi") and engine in ("auto", "persistent", "blocked-dl"):
                 self._try_blocked_dl()
@@ -170,21 +174,28 @@ class DistributedChainSolver:
         self.fab = None
         eng.close()
 
-    def _graph_engine(self):
-        if self.fabric_req == "ipc" or self.share:
-            from ..parallel.ipc import IpcComm
-            self.comm = IpcComm(self.n, self.d, self.block, self.device, timeout_s=self.timeout_s)
-            self.kind = "ipc"
-        else:
-            from ..parallel.comm import RcclComm
-            self.comm = RcclComm(self.device)
-            self.kind = "rccl"
+    def _graph_engine(self, force_ipc: bool = False):
+        """The graph-replayed phase kernels over the data plane of ``parallel/dataplane.py``: the IPC
+        transport by default (``--fabric auto`` / ``ipc``, and always with ranks sharing a GPU), RCCL
+        only for ``--fabric rccl`` -- with its watchdog (the engine's bounded waits abort a hung
+        communicator; ``fall_back`` then moves every rank to IPC). Collective."""
+        from ..parallel.dataplane import make_data_plane
+        fabric = "ipc" if force_ipc else self.fabric_req
+        self.comm = make_data_plane(fabric, self.world, self.device, self.share, self.n, self.d, self.block,
+                                    timeout_s=self.timeout_s)
+        self.kind = self.comm.selection["data_plane"]
         self.eng = self._engine(self.comm)
         self.persistent = False
 
+    def can_fall_back(self) -> bool:
+        """A persistent kernel (-> the graph engine) or an RCCL graph engine (-> the IPC transport)."""
+        return self.world > 1 and (self.persistent or self.kind == "rccl")
+
     def fall_back(self, why: str):
-        """Collective: every rank drops the persistent kernels for the graph engine."""
+        """Collective: every rank drops the persistent kernels for the graph engine, or the RCCL data
+        plane for the IPC transport."""
         self.fallbacks.append(why)
+        from_rccl = (not self.persistent) and self.kind == "rccl"
         if self.blk is not None:
             self.blk.close()
             self.blk = None
@@ -194,7 +205,12 @@ class DistributedChainSolver:
         if self.eng is not None:
             self.eng.close()
             self.eng = None
-        self._graph_engine()
+        if self.comm is not None:
+            if from_rccl:
+                self.comm.abort()  # peers may be gone or aborted: never a collective destroy
+            self.comm.close()
+            self.comm = None
+        self._graph_engine(force_ipc=from_rccl)
 
     # ---------------------------------------------------------------------------------------------
     def solve(self) -> SolveOut:
@@ -230,8 +246,8 @@ class DistributedChainSolver:
         out = self.guarded_solve()
         if all_ok(out.done == 1, self.world):
             return out
-        if self.world > 1 and self.persistent:
-            self.fall_back("persistent solve failed on some rank (done=%d here)" % out.done)
+        if self.can_fall_back():
+            self.fall_back("%s solve failed on some rank (done=%d here)" % (self.kind, out.done))
             out = self.guarded_solve()
         return out
 

@@ -17,6 +17,7 @@ configs[4] on a one-GPU box) and is an RCCL-free data plane on a node.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import time
 from typing import Optional, Sequence
@@ -135,21 +136,28 @@ class StarBigEngine:
                 allred = lambda t: coll("allreduce", t, 0, self.ctl, st)  # noqa: E731
             elif multi:
                 reduce, bcast, allred = self.comm.reduce_sum, self.comm.broadcast, self.comm.allreduce_sum
+            # RCCL: the collectives are enqueued without a host wait each (batched) and the block's one
+            # host look goes through the communicator's bounded wait (its watchdog aborts a hung block)
+            rccl_wait = getattr(self.comm, "wait", None) if (multi and not ipc) else None
+            batch = self.comm.batched() if rccl_wait is not None else contextlib.nullcontext()
             it = 0
             done = 0
             while it < max_iter and not done:
-                for _ in range(min(block, max_iter - it)):
-                    ch(self.lib.gadmm_star_big_workers(ctypes.byref(a), st), "star_big_workers")
-                    if multi:
-                        reduce(self.agg, self.hub_rank)
-                    ch(self.lib.gadmm_star_big_hub(ctypes.byref(a), st), "star_big_hub")
-                    if multi:
-                        bcast(self.th_hub, self.hub_rank)
-                    ch(self.lib.gadmm_star_big_post(ctypes.byref(a), st), "star_big_post")
-                    if multi:
-                        allred(self.objp)
-                    ch(self.lib.gadmm_star_big_finish(ctypes.byref(a), st), "star_big_finish")
-                    it += 1
+                with batch:
+                    for _ in range(min(block, max_iter - it)):
+                        ch(self.lib.gadmm_star_big_workers(ctypes.byref(a), st), "star_big_workers")
+                        if multi:
+                            reduce(self.agg, self.hub_rank)
+                        ch(self.lib.gadmm_star_big_hub(ctypes.byref(a), st), "star_big_hub")
+                        if multi:
+                            bcast(self.th_hub, self.hub_rank)
+                        ch(self.lib.gadmm_star_big_post(ctypes.byref(a), st), "star_big_post")
+                        if multi:
+                            allred(self.objp)
+                        ch(self.lib.gadmm_star_big_finish(ctypes.byref(a), st), "star_big_finish")
+                        it += 1
+                if rccl_wait is not None:
+                    rccl_wait(st)
                 done = int(self.ctl[1].item())  # one host look per block (synchronises the stream)
             c = self.ctl.cpu().tolist()
         wall = time.perf_counter() - t0

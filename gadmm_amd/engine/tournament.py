@@ -11,8 +11,8 @@ eligible candidate is built and timed here and the ranks AGREE on the fastest:
 * ``warm`` untimed solves, then ``solves`` timed ones between a device sync + barrier on both sides;
   the candidate's time is the MAX over ranks (an all-reduce), so every rank ranks the candidates
   from identical numbers and picks the same winner;
-* a candidate counts only if every solve on every rank converged, in one iteration count (``expect``
-  when given: the reference count);
+* a candidate counts only if every solve on every rank converged, in one iteration count that all
+  ranks agree on (``ranks_agree``; ``expect`` when given: the reference count);
 * the winner stays built, every other candidate is closed as soon as it loses.
 
 Everything collective goes over the default (gloo) group, so this module runs unchanged on CPU ranks
@@ -41,6 +41,15 @@ def _max(v: float, world: int) -> float:
     t = torch.tensor([float(v)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def ranks_agree(v: int, world: int) -> bool:
+    """Collective: every rank holds the same integer (an all-reduce of its min and max)."""
+    if world == 1:
+        return True
+    t = torch.tensor([float(v), -float(v)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0]) == -float(t[1])
 
 
 def engine_tournament(candidates: Sequence[Tuple[str, Callable[[], object]]], world: int, solves: int = 3,
@@ -88,6 +97,8 @@ def engine_tournament(candidates: Sequence[Tuple[str, Callable[[], object]]], wo
                 dist.barrier()
             ms = _max(ms, world)
             ok = _agree_ok(ok and len(its) == 1 and (expect is None or its == {int(expect)}), world)
+            # the same count on EVERY rank, not just one count per rank
+            ok = ok and ranks_agree(next(iter(its)), world)
         row = {"engine": name, "ok": bool(ok), "ms": round(ms, 4) if ms is not None else None,
                "iters": sorted(its)[0] if len(its) == 1 else sorted(its), "error": "" if ok else
                ("a solve failed or disagreed on some rank" if ms is not None else "warm-up solve failed")}

@@ -54,13 +54,20 @@ def _cg_solve(M: torch.Tensor, r: torch.Tensor, tol: float = 1e-13, maxit: int =
     return None
 
 
-def _cg_solve_native(M: torch.Tensor, r: torch.Tensor, tol: float, maxit: int, check: int):
+def _cg_solve_native(M: torch.Tensor, r: torch.Tensor, tol: float, maxit: int, check: int, comm=None):
+    """``comm`` (several ranks): the distributed CG of the large-d optimum -- ``M`` is this rank's LOCAL
+    Gram sum and the system matrix is the sum of every rank's, which is never formed: each product is the
+    local block-packed GEMV followed by an all-reduce of the d-vector (d-vector
+    collectives instead of the one-time d x d all-reduce, 80 KB instead of 800 MB per collective at d =
+    10k), and the Jacobi diagonal is all-reduced once. The all-reduced products are bit-identical on every
+    rank (the collectives sum in rank order), so every rank runs the same iterations and stops together."""
     import ctypes
     from ..ops import native
     from ..ops.linalg import sym_pack, sym_padded, symv_packed, symv_work_doubles
     lib = native.require()
     P, I = ctypes.c_void_p, ctypes.c_int
-    sigs = {"gadmm_cg_begin": [P, P, P, P, P, I, P], "gadmm_cg_begin2": [P, P, P, P, P, P, P, I, P],
+    sigs = {"gadmm_cg_begin": [P, P, P, P, P, I, P], "gadmm_cg_begin_diag": [P, P, P, P, P, I, P],
+            "gadmm_cg_begin2": [P, P, P, P, P, P, P, I, P],
             "gadmm_cg_step": [P, P, P, P, P, P, P, I, P], "gadmm_cg_resid": [P, P, P, I, P]}
     for name, args in sigs.items():
         fn = getattr(lib, name)
@@ -72,26 +79,47 @@ def _cg_solve_native(M: torch.Tensor, r: torch.Tensor, tol: float, maxit: int, c
     b[:d].copy_(r)
     sc = torch.zeros((3,), dtype=torch.float64, device=dev)
     ptr = native.ptr
-    native.check(lib.gadmm_cg_begin(ptr(M), ptr(b), ptr(dinv), ptr(x), ptr(sc), d, st), "cg_begin")
+    multi = comm is not None and comm.nranks > 1
+    if multi:
+        diag = torch.diagonal(M).contiguous()
+        comm.allreduce_sum(diag)
+        native.check(lib.gadmm_cg_begin_diag(ptr(diag), ptr(b), ptr(dinv), ptr(x), ptr(sc), d, st), "cg_begin_diag")
+    else:
+        native.check(lib.gadmm_cg_begin(ptr(M), ptr(b), ptr(dinv), ptr(x), ptr(sc), d, st), "cg_begin")
     Mp = sym_pack(M.unsqueeze(0))[0]
     work = torch.empty((symv_work_doubles(d),), dtype=torch.float64, device=dev)
+
+    def symv(v, out):
+        symv_packed(Mp, v, out, work, d)
+        if multi:
+            comm.allreduce_sum(out[:d])  # in place, contiguous view; the padding stays zero
+        return out
+
     head = sc.cpu()
     if float(head[2]) > 0:
         return None
     rn0 = float(head[1]) ** 0.5
     if rn0 == 0.0:
         return torch.zeros_like(r)
-    symv_packed(Mp, x, q, work, d)
+    symv(x, q)
     native.check(lib.gadmm_cg_begin2(ptr(b), ptr(dinv), ptr(q), ptr(res), ptr(z), ptr(p), ptr(sc), d, st), "cg_begin2")
     for k in range(1, maxit + 1):
-        symv_packed(Mp, p, q, work, d)
+        symv(p, q)
         native.check(lib.gadmm_cg_step(ptr(q), ptr(dinv), ptr(x), ptr(res), ptr(z), ptr(p), ptr(sc), d, st), "cg_step")
         if k % check == 0:
-            symv_packed(Mp, x, q, work, d)
+            symv(x, q)
             native.check(lib.gadmm_cg_resid(ptr(b), ptr(q), ptr(sc), d, st), "cg_resid")
             if float(sc[1].item()) ** 0.5 <= tol * rn0:
                 return x[:d].clone()
     return None
+
+
+def _distributed_cg_ok(model) -> bool:
+    """The large-d optimum runs the distributed CG (d-vector all-reduces) on HIP devices with d > 256
+    (GADMM_OPT_DIST=0: the one-time d x d Gram all-reduce instead)."""
+    return (model.A.is_cuda and model.d > 256 and os.environ.get("GADMM_OPT_DIST", "1") != "0"
+            and os.environ.get("GADMM_OPT_SOLVER", "native") != "rocsolver"
+            and os.environ.get("GADMM_OPT_CG", "1") != "0")
 
 
 def _resid_sq(X: torch.Tensor, y: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
@@ -239,25 +267,41 @@ class LinearRegression:
 
     # ---- global oracle ----------------------------------------------------------------------------
     def optimum(self, comm=None, n_total=None) -> float:
-        """Optimal objective of the stacked problem: ``x = (sum A_n)^{-1} sum b_n`` (one-time all-reduce
-        of the d x d Gram), evaluated as ``1/2 ||X x - y||^2`` from the raw rows, as
+        """Optimal objective of the stacked problem: ``x = (sum A_n)^{-1} sum b_n``, evaluated as ``1/2 ||X x - y||^2`` from the raw rows, as
         ``opt_sol_closedForm.m:2-3`` does (the quadratic form ``x'Ax/2 - b'x + y'y/2`` cancels badly:
-        ~1e-10 absolute on the E1 problem, more than the margin of its 1e-8 stop)."""
+        ~1e-10 absolute on the E1 problem, more than the margin of its 1e-8 stop).
+
+        Across ranks: at d > 256 on HIP devices a distributed CG whose collectives are
+        d-vectors (``_cg_solve_native(comm=...)``); otherwise, or if CG does not converge, the one-time
+        all-reduce of the d x d Gram. ``last_optimum_path`` names the one taken."""
+        self.last_optimum_path = "local" if comm is None or comm.nranks == 1 else "gram-allreduce"
         As = self.A.sum(0)
         bs = self.b.sum(0)
         yy = self.yy.sum()
-        if comm is not None and comm.nranks > 1:
+        lam_tot = self.lam * (n_total if n_total is not None else self.n_local)
+        x = None
+        if comm is not None and comm.nranks > 1 and _distributed_cg_ok(self):
+            # d-vector collectives only: b, the Jacobi diagonal and one product per CG iteration
+            if lam_tot:
+                As.diagonal().add_(lam_tot / comm.nranks)  # the ridge split evenly over the rank sums
+            bs = bs.contiguous()
+            comm.allreduce_sum(bs)
+            x = _cg_solve_native(As.contiguous(), bs, 1e-13, 96, 8, comm=comm)
+            self.last_optimum_path = "distributed-cg" if x is not None else "gram-allreduce"
+            if x is None:  # ill-conditioned: the one-time d x d all-reduce below
+                As, bs = self.A.sum(0), self.b.sum(0)
+        if x is None and comm is not None and comm.nranks > 1:
             buf = torch.cat([As.reshape(-1), bs, yy.reshape(1)]).contiguous()
             comm.allreduce_sum(buf)
             d = self.d
             As = buf[: d * d].reshape(d, d)
             bs = buf[d * d: d * d + d]
             yy = buf[-1]
-        lam_tot = self.lam * (n_total if n_total is not None else self.n_local)
-        if lam_tot:  # ridge: the diagonal only (no d x d identity: 800 MB at d = 10k)
-            As = As.clone()
-            As.diagonal().add_(lam_tot)
-        x = _spd_solve(As, bs)
+        if x is None:
+            if lam_tot:  # ridge: the diagonal only (no d x d identity: 800 MB at d = 10k)
+                As = As.clone()
+                As.diagonal().add_(lam_tot)
+            x = _spd_solve(As, bs)
         if self.X.is_cuda and self.d > 256 and self.X.dtype == torch.float64:
             f = 0.5 * _resid_sq(self.X, self.y, x)  # one native pass over the shard at HBM speed
         else:

@@ -233,6 +233,13 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_rccl_unique_id": (c_int, [ctypes.c_char_p]),
         "gadmm_rccl_version": (c_int, []),
         "gadmm_rccl_init": (c_void_p, [ctypes.c_char_p, c_int, c_int, c_int]),
+        "gadmm_rccl_init_timeout": (c_void_p, [ctypes.c_char_p, c_int, c_int, c_int, ctypes.c_double]),
+        "gadmm_rccl_set_timeout": (c_int, [c_void_p, ctypes.c_double]),
+        "gadmm_rccl_alive": (c_int, [c_void_p]),
+        "gadmm_rccl_abort": (c_int, [c_void_p]),
+        "gadmm_rccl_wait": (c_int, [c_void_p, c_void_p, ctypes.c_double]),
+        "gadmm_debug_busy_wait": (c_int, [ctypes.c_double, c_void_p]),
+        "gadmm_chain_engine_set_timeout": (c_int, [c_void_p, ctypes.c_double]),
         "gadmm_rccl_destroy": (c_int, [c_void_p]),
         "gadmm_rccl_exchange_rows": (c_int, [c_void_p, ctypes.POINTER(XchgOp), c_int, c_void_p, c_int, c_void_p]),
         "gadmm_rccl_allreduce_sum_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_long, c_void_p]),
@@ -291,10 +298,40 @@ def require() -> ctypes.CDLL:
     return lib
 
 
+RCCL_DEAD = -77  # csrc/include/gadmm_common.h: GADMM_RCCL_DEAD
+
+
+class RcclDead(RuntimeError):
+    """An RCCL communicator's watchdog deadline passed (or RCCL reported an asynchronous error): the
+    communicator was aborted and refuses further calls; the caller falls back to another data plane."""
+
+
+class NativeTimeout(RuntimeError):
+    """A bounded host wait of the native engine passed its deadline (a stalled peer or collective)."""
+
+
+ENGINE_TIMEOUT = -78  # csrc/runtime/chain_engine.cpp: a bounded wait passed its deadline
+RCCL_WEDGED = -79     # a watchdog abort after which the stream did not drain
+
+
+class DeviceWedged(SystemExit):
+    """The device stream did not drain after a watchdog abort: no fallback may run on this device.
+    A SystemExit (not caught by the ``except RuntimeError`` fallbacks): the process exits non-zero."""
+
+
 def check(rc: int, what: str = "native call") -> None:
     if rc != 0:
         msg = require().gadmm_last_error()
-        raise RuntimeError("%s failed (rc=%d): %s" % (what, rc, msg.decode() if msg else "?"))
+        text = "%s failed (rc=%d): %s" % (what, rc, msg.decode() if msg else "?")
+        if rc == RCCL_DEAD:
+            raise RcclDead(text)
+        if rc == ENGINE_TIMEOUT:
+            raise NativeTimeout(text)
+        if rc == RCCL_WEDGED:
+            import sys
+            print("gadmm_amd: " + text, file=sys.stderr, flush=True)
+            raise DeviceWedged(5)
+        raise RuntimeError(text)
 
 
 def poison_lds(per_cu: int = 4, sync: bool = True) -> None:

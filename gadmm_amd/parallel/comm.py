@@ -196,11 +196,19 @@ class TorchDistComm(Comm):
 
 class RcclComm(Comm):
     """Native RCCL communicator (libgadmm_native). The unique id travels over an existing
-    torch.distributed group (the gloo control plane)."""
+    torch.distributed group (the gloo control plane).
+
+    Watchdog (csrc/runtime/rccl_comm.cpp): the communicator is non-blocking, its set-up and every
+    enqueue are bounded by ``timeout_s``, and host waits on RCCL work go through ``wait`` (or the chain
+    engine's bounded waits). A deadline that passes aborts the communicator and raises
+    ``native.RcclDead``; callers fall back to the IPC transport together (``parallel/dataplane.py``).
+    Host-called collectives (set-up, oracles, the star comparator) wait after every call unless they
+    run inside ``with comm.batched():`` (an engine loop that waits once per block)."""
 
     backend = "rccl"
 
-    def __init__(self, device: torch.device, control_group=None):
+    def __init__(self, device: torch.device, control_group=None, timeout_s: float = 60.0,
+                 init_timeout_s: float = 120.0):
         super().__init__()
         from ..ops import native
 
@@ -209,6 +217,8 @@ class RcclComm(Comm):
         self.rank = dist.get_rank(control_group)
         self.nranks = dist.get_world_size(control_group)
         self.device = torch.device(device)
+        self.timeout_s = float(timeout_s)
+        self._batched = 0
         idbuf = ctypes.create_string_buffer(128)
         if self.rank == 0:
             native.check(self.lib.gadmm_rccl_unique_id(idbuf), "rccl_unique_id")
@@ -216,9 +226,46 @@ class RcclComm(Comm):
         dist.broadcast_object_list(obj, src=0, group=control_group)
         idbytes = ctypes.create_string_buffer(obj[0], 128)
         self.control_group = control_group
-        self.handle = self.lib.gadmm_rccl_init(idbytes, self.nranks, self.rank, self.device.index or 0)
+        # the set-up (topology discovery, transports: seconds on an 8-GPU node) gets its own deadline;
+        # every later enqueue / wait gets ``timeout_s``
+        self.handle = self.lib.gadmm_rccl_init_timeout(idbytes, self.nranks, self.rank, self.device.index or 0,
+                                                      max(float(init_timeout_s), self.timeout_s))
         if not self.handle:
             native.check(-1, "rccl_init")
+        native.check(self.lib.gadmm_rccl_set_timeout(self.handle, self.timeout_s), "rccl_set_timeout")
+
+    @property
+    def alive(self) -> bool:
+        return bool(self.handle) and int(self.lib.gadmm_rccl_alive(self.handle)) == 1
+
+    def wait(self, stream=None, timeout_s: float = 0.0) -> None:
+        """Bounded host wait for everything queued on ``stream`` (default: the current one). Raises
+        native.RcclDead after aborting the communicator when the deadline passes."""
+        st = stream if stream is not None else self._stream()
+        self.native.check(self.lib.gadmm_rccl_wait(self.handle, st, float(timeout_s)), "rccl_wait")
+
+    def abort(self) -> None:
+        if self.handle:
+            self.lib.gadmm_rccl_abort(self.handle)
+
+    class _Batch:
+        def __init__(self, c):
+            self.c = c
+
+        def __enter__(self):
+            self.c._batched += 1
+            return self.c
+
+        def __exit__(self, *exc):
+            self.c._batched -= 1
+            return False
+
+    def batched(self):
+        return RcclComm._Batch(self)
+
+    def _settle(self):
+        if not self._batched:
+            self.wait()
 
     def _stream(self):
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -232,6 +279,7 @@ class RcclComm(Comm):
         d = table.shape[1]
         self.native.check(self.lib.gadmm_rccl_exchange_rows(self.handle, arr, len(ops), table.data_ptr(), d,
                                                             self._stream()), "rccl_exchange_rows")
+        self._settle()
         for peer, row, snd in ops:
             if snd:
                 self.stats.bytes_sent += d * 8
@@ -256,6 +304,7 @@ class RcclComm(Comm):
         fn.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int),
                        ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_long), ctypes.c_void_p]
         self.native.check(fn(self.handle, n, peers, sends, bufs, counts, self._stream()), "rccl_sendrecv")
+        self._settle()
         for p, s, t in items:
             if s:
                 self.stats.bytes_sent += t.numel() * 8
@@ -267,21 +316,25 @@ class RcclComm(Comm):
         self.native.check(self.lib.gadmm_rccl_allreduce_sum_f64(self.handle, t.data_ptr(), t.data_ptr(), t.numel(),
                                                                 self._stream()), "rccl_allreduce")
         self.stats.coll_bytes += t.numel() * 8
+        self._settle()
         return t
 
     def reduce_sum(self, t, root):
         self.native.check(self.lib.gadmm_rccl_reduce_sum_f64(self.handle, t.data_ptr(), t.data_ptr(), t.numel(), root,
                                                              self._stream()), "rccl_reduce")
         self.stats.coll_bytes += t.numel() * 8
+        self._settle()
         return t
 
     def broadcast(self, t, root):
         self.native.check(self.lib.gadmm_rccl_bcast_f64(self.handle, t.data_ptr(), t.numel(), root, self._stream()),
                           "rccl_bcast")
         self.stats.coll_bytes += t.numel() * 8
+        self._settle()
         return t
 
     def barrier(self):
+        self.wait()
         torch.cuda.synchronize(self.device)
         dist.barrier(group=self.control_group)
 

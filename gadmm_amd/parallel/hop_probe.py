@@ -22,7 +22,7 @@ import torch
 import torch.distributed as dist
 
 from ..ops import native
-from .xgmi import _Buf, preflight
+from .xgmi import _Buf, device_identity, preflight, same_physical_device
 
 
 def hop_probe(rank: int, world: int, device: torch.device, n: int = 2000, timeout_s: float = 5.0,
@@ -38,8 +38,9 @@ def hop_probe(rank: int, world: int, device: torch.device, n: int = 2000, timeou
     except Exception as e:  # pragma: no cover - box dependent
         mine_h, err = None, str(e)
     dev = torch.cuda.current_device()
+    ident = device_identity(dev)
     allh = [None] * world
-    dist.all_gather_object(allh, (mine_h, dev, err), group=group)
+    dist.all_gather_object(allh, (mine_h, ident, err), group=group)
     opened = {}
     try:
         if any(e for _, _, e in allh):  # the same on every rank
@@ -80,9 +81,11 @@ def hop_probe(rank: int, world: int, device: torch.device, n: int = 2000, timeou
         t = torch.tensor([(-1.0 if v is None else v) for v in mine], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
         hops = [None if v < 0 else round(float(v), 4) for v in t.tolist()]
-        # every rank on one device index: the one-GPU rehearsal (a cross-process hop inside one MI355X)
+        # every rank on one PHYSICAL device (PCI address / UUID, not the ordinal -- per-process
+        # HIP_VISIBLE_DEVICES makes every rank's GPU device 0): the one-GPU rehearsal
         return {"hop_us": hops, "ok": all(h is not None for h in hops),
-                "same_device": len({h[1] for h in allh}) == 1}
+                "same_device": same_physical_device(h[1] for h in allh),
+                "devices": [h[1].split("|")[0] for h in allh]}
     finally:
         for p in opened.values():
             lib.gadmm_xgmi_close(p)

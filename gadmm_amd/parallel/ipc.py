@@ -11,8 +11,9 @@ Why it exists:
 * RCCL refuses two ranks on one device, so the engine's multi-rank code (chain plans, ghost rows,
   the objective ring and monitor, D-GADMM re-plans, logistic across ranks) could never run on a
   one-GPU box. With this transport it runs with 2..16 processes sharing one MI355X.
-* On a node it is an RCCL-free data plane between graph-replayed phases (every MI355X pair is one
-  xGMI hop; the stores go straight over the link).
+* On a node it is the DEFAULT data plane between graph-replayed phases and for the set-up / oracle
+  collectives (parallel/dataplane.py): every MI355X pair is one xGMI hop, the stores go straight over
+  the link, and every wait has a deadline in the kernel (RCCL is opt-in, behind a watchdog).
 
 Handles travel over the gloo control plane, like ``parallel/xgmi.py``.
 """
@@ -161,27 +162,58 @@ class IpcComm(Comm):
         from ..ops import native
         native.check(self.transport.lib.gadmm_ipc_new_epoch(self.xport, stream), "ipc_new_epoch")
 
+    def _device_collective_sync(self, kind: str, t, root: int) -> bool:
+        """A host-called collective on a CUDA f64 tensor through the device collective (chunks of the
+        coll row, 2 d + 8 doubles; no host staging of e.g. an 800 MB Gram at d = 10k), synchronised and
+        checked. False: not eligible (the caller uses the gloo control plane)."""
+        step = 2 * self.transport.d + 8
+        if not (t.is_cuda and t.dtype == torch.float64 and t.is_contiguous() and t.numel() >= 64):
+            return False
+        if kind != "allreduce" and t.numel() > 4 * step:
+            # a reduce / broadcast is not a rendezvous for its pushing ranks: more chunks than the
+            # transport's collective slots (8) could lap a slow reader -- the control plane instead
+            return False
+        from ..ops import native
+        st = torch.cuda.current_stream(self.device).cuda_stream
+        if getattr(self, "_ctl", None) is None:
+            self._ctl = torch.zeros((8,), dtype=torch.int32, device=self.device)
+        self._ctl.zero_()
+        self.new_epoch(st)
+        flat = t.view(-1)
+        for c0 in range(0, flat.numel(), step):
+            self.device_collective(kind, flat[c0:c0 + step], root, self._ctl, st)
+        if int(self._ctl[1].item()) != 0:
+            native.check(-1, "ipc %s: a peer did not arrive (done=%d)" % (kind, int(self._ctl[1].item())))
+        return True
+
     def allreduce_sum(self, t):
-        """One-time set-up all-reduce (oracles: the d x d Gram of SURVEY.md C10). A large f64 device
-        tensor goes through the device collective in chunks of the coll row (2 d + 8 doubles; no host
-        staging of an 800 MB Gram at d = 10k), anything else over the gloo control plane."""
-        if t.is_cuda and t.dtype == torch.float64 and t.is_contiguous() and t.numel() > 4096:
-            from ..ops import native
-            lib = self.transport.lib
-            st = torch.cuda.current_stream(self.device).cuda_stream
-            if getattr(self, "_ctl", None) is None:
-                self._ctl = torch.zeros((8,), dtype=torch.int32, device=self.device)
-            self._ctl.zero_()
-            self.new_epoch(st)
-            flat = t.view(-1)
-            step = 2 * self.transport.d + 8
-            for c0 in range(0, flat.numel(), step):
-                self.device_collective("allreduce", flat[c0:c0 + step], 0, self._ctl, st)
-            if int(self._ctl[1].item()) != 0:
-                native.check(-1, "ipc allreduce_sum: a peer did not arrive (done=%d)" % int(self._ctl[1].item()))
+        """Set-up / oracle all-reduce (the distributed CG's d-vector products): CUDA f64
+        tensors by the device collective, anything else over the gloo control plane."""
+        if self._device_collective_sync("allreduce", t, 0):
             return t
         h = t.detach().cpu()
         dist.all_reduce(h, group=self.group)
+        t.copy_(h)
+        self.stats.coll_bytes += t.numel() * t.element_size()
+        return t
+
+    def reduce_sum(self, t, root: int):
+        """Reduce to ``root`` (the star comparator's upload, standared_ADMM.m:66-71)."""
+        if self._device_collective_sync("reduce", t, root):
+            return t
+        h = t.detach().cpu()
+        dist.reduce(h, dst=root, group=self.group)
+        if self.rank == root:
+            t.copy_(h)
+        self.stats.coll_bytes += t.numel() * t.element_size()
+        return t
+
+    def broadcast(self, t, root: int):
+        """Broadcast from ``root`` (the star hub's theta, standared_ADMM.m:86)."""
+        if self._device_collective_sync("broadcast", t, root):
+            return t
+        h = t.detach().cpu()
+        dist.broadcast(h, src=root, group=self.group)
         t.copy_(h)
         self.stats.coll_bytes += t.numel() * t.element_size()
         return t

@@ -67,7 +67,7 @@ class XgmiFabric:
         except Exception as e:
             err = "rank %d alloc: %s" % (rank, e)
         allh = [None] * nranks
-        dist.all_gather_object(allh, (mine, err, torch.cuda.current_device()), group=group)
+        dist.all_gather_object(allh, (mine, err, device_identity()), group=group)
         errs = [e for _, e, _ in allh if e]
         if errs:
             self.close()
@@ -136,16 +136,48 @@ def peer_access_ok(nranks: int) -> bool:
                if i != j)
 
 
-def preflight(my_dev: int, peer_devs: Dict[int, int]) -> str:
-    """Pre-flight of the IPC / xGMI mappings a rank is about to open: every peer rank's device must
-    be reachable from this rank's device (hipDeviceCanAccessPeer) before ``hipIpcOpenMemHandle``
-    (which would otherwise fail -- or worse, map -- on a box without the link). Ranks sharing this
-    rank's device (the one-GPU rehearsal) need no peer access. Returns '' or the reason."""
+_IDENT: Dict[int, str] = {}
+
+
+def device_identity(index: Optional[int] = None) -> str:
+    """A physical identity of a visible device: PCI domain:bus:device plus the UUID when the runtime
+    reports one. Ranks compare THIS, never the logical ordinal: ranks launched with a per-process
+    HIP_VISIBLE_DEVICES all see their GPU as device 0, while ranks sharing one GPU (the one-box
+    rehearsal) see the same PCI address."""
+    i = torch.cuda.current_device() if index is None else int(index)
+    if i not in _IDENT:
+        p = torch.cuda.get_device_properties(i)
+        uuid = str(getattr(p, "uuid", "") or "")
+        _IDENT[i] = "%04x:%02x:%02x|%s" % (int(getattr(p, "pci_domain_id", 0)), int(getattr(p, "pci_bus_id", 0)),
+                                           int(getattr(p, "pci_device_id", 0)), uuid)
+    return _IDENT[i]
+
+
+def same_physical_device(idents) -> bool:
+    """All the identities (``device_identity``) name one GPU."""
+    return len({str(x) for x in idents}) == 1
+
+
+def preflight(my_dev: int, peer_devs: Dict[int, str]) -> str:
+    """Pre-flight of the IPC / xGMI mappings a rank is about to open: every peer rank's device (by its
+    ``device_identity``) must be reachable from this rank's device (hipDeviceCanAccessPeer) before
+    ``hipIpcOpenMemHandle`` (which would otherwise fail -- or worse, map -- on a box without the link).
+    A peer on this rank's own physical device (the one-GPU rehearsal) needs no peer access. A peer
+    device this process cannot see (per-process HIP_VISIBLE_DEVICES) cannot be checked here: it is
+    allowed, and the IPC open that follows is the check (its failure falls back collectively).
+    Returns '' or the reason."""
     lib = native.require()
+    mine = device_identity(my_dev)
+    visible = {device_identity(i): i for i in range(torch.cuda.device_count())}
     bad = []
-    for r, dv in sorted(peer_devs.items()):
-        if dv == my_dev:
+    for r, ident in sorted(peer_devs.items()):
+        if isinstance(ident, int):  # a bare ordinal (old callers): resolve it on this process
+            ident = device_identity(ident)
+        if ident == mine:
             continue
-        if int(lib.gadmm_device_can_access_peer(my_dev, dv)) != 1:
-            bad.append("rank %d (device %d)" % (r, dv))
-    return ("device %d cannot access %s" % (my_dev, ", ".join(bad))) if bad else ""
+        j = visible.get(ident)
+        if j is None:
+            continue
+        if int(lib.gadmm_device_can_access_peer(my_dev, j)) != 1:
+            bad.append("rank %d (device %s)" % (r, ident.split("|")[0]))
+    return ("device %s cannot access %s" % (mine.split("|")[0], ", ".join(bad))) if bad else ""

@@ -20,3 +20,22 @@ def test_bench_cpu_gloo_two_ranks():
     assert r["iterations_to_tol"] == 784 and r["cpu_ranks"] == 2 and r["n_gpus"] == 0
     assert r["theta_payload_bytes_per_solve"] == 2 * 50 * 8 * 784  # one rank boundary, both directions
     assert r["value"] > 0 and r["unit"] == "s"
+
+
+def test_expected_iteration_table_matches_reference_semantics():
+    """Every bench config's correctness gate (benchmarks.EXPECTED_OTHER / EXPECTED_ITERS_1E8) equals the
+    reference-semantics count for the bench's exact problem and seeds (VERDICT r04 next #4)."""
+    from gadmm_amd import benchmarks as B
+    from gadmm_amd.data import linear_synthetic
+    from gadmm_amd.oracle import reference as R
+
+    for key, want in B.EXPECTED_OTHER.items():
+        cfg, n = key[0], key[1]
+        coh = key[2] if len(key) > 2 else 10
+        assert B.reference_expected(cfg, n, coh) == want, key
+        assert B.expected_for(cfg, n, coh) == want
+    for (n, rho), want in B.EXPECTED_ITERS_1E8.items():
+        ds = linear_synthetic(n)
+        X, y = ds.X.numpy(), ds.y.numpy()
+        obj0 = R.opt_linear(X.reshape(-1, X.shape[2]), y.reshape(-1))
+        assert R.gadmm_linear(X, y, rho, 3000, obj0, 1e-8).iters == want, (n, rho)

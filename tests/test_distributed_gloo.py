@@ -240,3 +240,22 @@ def test_engine_tournament_agreement_on_gloo_ranks():
     # both ranks ranked from identical numbers
     assert [(x["engine"], x["ok"], x["ms"]) for x in res[0]["table"]] == \
         [(x["engine"], x["ok"], x["ms"]) for x in res[1]["table"]]
+
+
+def _tournament_rank_noexpect(rank, world):
+    from gadmm_amd.engine.tournament import engine_tournament
+
+    cands = [("differs-by-rank", lambda: _FakeSolver(rank, [0.001, 0.001], iters=10 + rank)),
+             ("agreed", lambda: _FakeSolver(rank, [0.004, 0.004], iters=12))]
+    name, sol, table = engine_tournament(cands, world, solves=2, warm=1, expect=None)
+    return {"winner": name, "table": table}
+
+
+def test_engine_tournament_rejects_rank_disagreement_without_expected_count():
+    """with no pinned count a candidate must still converge in the SAME count on every rank
+    (an all-reduce of the min and max), not merely in one count per rank."""
+    res = spawn(_tournament_rank_noexpect, 2, timeout=120)
+    for r in res:
+        rows = {row["engine"]: row for row in r["table"]}
+        assert not rows["differs-by-rank"]["ok"] and rows["agreed"]["ok"]
+        assert r["winner"] == "agreed"

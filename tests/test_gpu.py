@@ -176,6 +176,84 @@ def test_engine_monitor_path_with_rccl_one_rank(lin24, lin_obj0):
     comm._raw([(0, 1, src), (0, 0, dst)])
     torch.cuda.synchronize()
     assert torch.equal(src, dst)
+    assert comm.alive
+    eng.close()
+    comm.close()
+
+
+_RCCL_WATCHDOG_SCRIPT = r'''
+import time, torch, torch.distributed as dist
+from gadmm_amd.parallel.comm import RcclComm
+from gadmm_amd.parallel.launch import free_port
+from gadmm_amd.ops import native
+dist.init_process_group("gloo", rank=0, world_size=1, init_method="tcp://127.0.0.1:%d" % free_port())
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+c = RcclComm(dev, timeout_s=3.0)
+t = torch.arange(1000, dtype=torch.float64, device=dev)
+c.allreduce_sum(t)
+print("SUM", float(t.sum()), flush=True)
+st = torch.cuda.current_stream(dev).cuda_stream
+t0 = time.time()
+try:
+    # a stalled peer, bounded: the stream stays busy for 4 s, the watchdog's deadline is 1 s
+    native.check(native.require().gadmm_debug_busy_wait(4.0, st), "busy_wait")
+    c.wait(timeout_s=1.0)
+    print("NO_HANG", flush=True)
+except native.RcclDead as e:
+    print("WATCHDOG %.2f" % (time.time() - t0), flush=True)
+print("ALIVE", c.alive, flush=True)
+try:
+    c.allreduce_sum(t)
+    print("USED_AFTER_ABORT", flush=True)
+except native.RcclDead:
+    print("REFUSED", flush=True)
+c.close()
+torch.cuda.synchronize()
+print("CLEAN_EXIT", flush=True)
+'''
+
+
+def test_rccl_watchdog_aborts_a_stalled_wait():
+    """RCCL has no deadline of its own (VERDICT r04 missing #1): a host wait on a stream that does not
+    finish (a stalled peer; here a bounded 4 s busy kernel, the deadline 1 s) ends at the watchdog's
+    deadline -- the communicator is aborted (ncclCommAbort), the stream drains, native.RcclDead is raised
+    (the caller falls back), and the dead communicator refuses further calls. The communicator itself is
+    non-blocking (its set-up and the all-reduce before run through the deadline-bounded settle). Run in
+    a child process so that a watchdog that failed could only hang the child (killed at 90 s). (A lone
+    RCCL receive cannot stand in for the stalled peer on one rank: RCCL rejects it as invalid usage.)"""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, "-c", _RCCL_WATCHDOG_SCRIPT], cwd=root, capture_output=True, text=True,
+                       timeout=90, env=dict(os.environ, PYTHONPATH=root))
+    out = p.stdout
+    assert p.returncode == 0 and "CLEAN_EXIT" in out, (p.returncode, out[-2000:], p.stderr[-3000:])
+    assert "SUM 499500.0" in out and "NO_HANG" not in out
+    secs = float(out.split("WATCHDOG ")[1].split()[0])
+    assert 3.5 <= secs <= 15.0, out  # the 1 s deadline, then the drain of the 4 s kernel
+    assert "ALIVE False" in out and "REFUSED" in out
+
+
+def test_graph_engine_rccl_deadline_aborts_and_raises(lin24, lin_obj0):
+    """The chain engine's bounded host waits (chain_engine.cpp): with an RCCL data plane and a deadline
+    shorter than one replay, the run returns GADMM_ENGINE_TIMEOUT (native.NativeTimeout) after aborting
+    the communicator, instead of blocking in hipEventSynchronize."""
+    import torch.distributed as dist
+    from gadmm_amd.ops import native
+    from gadmm_amd.parallel.comm import RcclComm
+    from gadmm_amd.parallel.launch import free_port
+    if not dist.is_initialized():
+        dist.init_process_group("gloo", rank=0, world_size=1, init_method="tcp://127.0.0.1:%d" % free_port())
+    comm = RcclComm(DEV)
+    eng = _engine(lin24, 5.0, lin_obj0, 1e-8, comm=comm, force_monitor=True, block=16)
+    assert eng.run().iters == 758  # the normal deadline (60 s): converges
+    eng.reset()
+    comm.timeout_s = 1e-6
+    with pytest.raises(native.NativeTimeout):
+        eng.run()
+    assert not comm.alive
+    torch.cuda.synchronize()
     eng.close()
     comm.close()
 

@@ -572,7 +572,8 @@ def _big_rank(rank, world, wpg, rows, dim):
     m = _big_problem(n, rows, dim, ids, dev)
     comm = IpcComm(n, dim, 16, dev)
     obj0, g, s = _big_solves(m, ids, n, comm, Placement.contiguous(n, world), rows)
-    out = {"obj0": obj0, "g": (g.iters, g.converged, g.extra.get("engine"), int(g.bytes_sent)), "g_trace": g.obj,
+    out = {"obj0": obj0, "opt_path": m.last_optimum_path,
+           "g": (g.iters, g.converged, g.extra.get("engine"), int(g.bytes_sent)), "g_trace": g.obj,
            "s": [(r.iters, r.converged, r.extra.get("backend"), int(r.bytes_sent), int(r.bytes_total)) for r in s],
            "s_trace": [r.obj for r in s], "theta": g.extra["engine_obj"].local_theta().cpu().numpy()}
     g.extra["engine_obj"].close()
@@ -599,6 +600,8 @@ def test_large_d_gadmm_and_star_across_ranks_match_one_rank(world):
     assert s[1].iters == s[0].iters and np.array_equal(s[1].obj, s[0].obj)
     d = dim
     for rk, r in enumerate(res):
+        # the distributed CG optimum (d-vector all-reduces, no d x d Gram all-reduce) == the one-rank solve
+        assert r["opt_path"] == "distributed-cg"
         assert abs(r["obj0"] - obj0) <= 1e-12 * abs(obj0)
         it, conv, eng, pay = r["g"]
         assert it == g.iters and conv and eng == "graph", r["g"]
@@ -652,15 +655,30 @@ def test_bench_tournament_and_hop_probe(world):
     assert len(hops) == world - 1 and all(h is not None and 0 < h < 50 for h in hops), hops
     assert out["hop_probe_same_device"] is True
     rows = {r["engine"]: r for r in out["engine_tournament"]}
-    assert set(rows) == {"blocked-dl-halo", "blocked-dl", "per-worker", "replicated-halo"}
+    rep = sorted(k for k in rows if k.startswith("replicated-halo-k"))
+    # replicated-halo at every k the blocked plan admits (both wave layouts), then the graph engine over
+    # IPC; no RCCL candidate with ranks sharing a GPU (RCCL refuses it)
+    assert {"blocked-dl-halo", "blocked-dl", "per-worker", "graph-ipc"} <= set(rows), rows
+    assert set(rows) == {"blocked-dl-halo", "blocked-dl", "per-worker", "graph-ipc"} | set(rep)
+    assert {"replicated-halo-k1", "replicated-halo-k2"} <= set(rep), rep
     ok = {k: r["ms"] for k, r in rows.items() if r["ok"]}
-    assert "blocked-dl" in ok and "per-worker" in ok and "replicated-halo" in ok
-    assert "blocked-dl-halo" in ok  # 2 ranks: the 13th position (halo head) hosted by the boundary tail
+    assert {"blocked-dl", "per-worker", "graph-ipc", "blocked-dl-halo"} <= set(ok)  # 2 ranks: halo head hosted
+    assert all(rows[k]["ok"] and rows[k]["iters"] == 1373 for k in rep), [rows[k] for k in rep]
+    for k, r in rows.items():  # the model next to the measurement: hops per iteration, predicted time
+        assert r["hops_per_iter"] > 0
+        if r["ok"] and not k.startswith("graph"):
+            assert r["predicted_ms"] is not None and r["predicted_ms"] > 0, r
+    assert abs(rows["replicated-halo-k2"]["hops_per_iter"] - 0.5) < 1e-9
     assert out["fallbacks"] == [] and out["timing_restarts"] == 0
+    assert out["handoff_deadline_s"] == 20.0 and out["tournament_deadline_s"] == 5.0
     best = min(ok, key=ok.get)
+    assert out["tournament_winner"] == best
     want = {"blocked-dl-halo": "xgmi(blocked-dl-halo)", "blocked-dl": "xgmi(blocked-dl)", "per-worker": "xgmi",
-            "replicated-halo": "xgmi(replicated-halo)"}[best]
-    assert out["fabric"] == want, (best, out["fabric"], rows)
+            "graph-ipc": "ipc"}
+    if best.startswith("replicated-halo-k"):
+        assert out["fabric"].startswith("xgmi(replicated-halo,k=%s" % best.split("-k")[1][0]), (best, out["fabric"])
+    else:
+        assert out["fabric"] == want[best], (best, out["fabric"], rows)
 
 
 def test_bench_timed_loop_stall_falls_back_collectively():
