@@ -185,6 +185,15 @@ __global__ void fob_lag_decide(const double* ddpart, int nblk, const double* hsq
   if (it - 1 >= 0) cnt[it - 1] = (double)c;
 }
 
+// rows[it - 1] = how many of this rank's table rows travel this iteration (mask != 0: the triggered
+// uploads plus LAG-PS's forced worker-1 refresh): the conditional exchange's payload (multi-rank LAG)
+__global__ void fob_lag_rows(const int* mask, int n_local, double* rows, const ChainCtl* ctl) {
+  if (ctl->done || threadIdx.x != 0) return;
+  int r = 0;
+  for (int n = 0; n < n_local; ++n) r += mask[n] != 0;
+  if (ctl->iter >= 1) rows[ctl->iter - 1] = (double)r;
+}
+
 // LAG uploads: masked workers take their new gradient (and PS its th-hat) into G_loc and the table
 __global__ void __launch_bounds__(EB) fob_lag_apply(const double* GN, double* Gl, double* thhat, const double* th,
                                                     double* T, const int* mask, int d, int w_lo, int ps,
@@ -212,25 +221,32 @@ __global__ void __launch_bounds__(EB) fob_da_obj(const double* q, long dp, const
 }
 
 // one thread per element: the workers in chain order (Z overwritten in place: Gauss-Seidel, or
-// the previous sweep's Z for both neighbours in Jacobi mode), th_n = -a Z_n (dual_averaging.m:34-44)
+// the previous sweep's Z for both neighbours in Jacobi mode), th_n = -a Z_n (dual_averaging.m:34-44).
+// Z is the chain-wide table (n_total x d, global worker rows); this rank sweeps its rows w_lo ..
+// w_lo + n - 1 (one rank: all of them). Across ranks the rows next to the segment are ghosts filled by
+// the exchanges around the sweep (engine/first_order_big.py): row w_lo - 1 holds the left neighbour
+// rank's Z of THIS sweep (Gauss-Seidel; Jacobi: of the previous one), row w_lo + n its right neighbour's
+// of the previous sweep -- exactly the values the one-rank sweep reads there. Zp: (n x d) local copy.
 __global__ void __launch_bounds__(EB) fob_da_sweep(const double* q, long dp, const double* b, double* th, double* Z,
-                                                   double* Zp, int d, int n, double alpha, int jacobi,
-                                                   const ChainCtl* ctl) {
+                                                   double* Zp, int d, int n, int w_lo, int n_total, double alpha,
+                                                   int jacobi, const ChainCtl* ctl) {
   if (ctl->done) return;
   const int j = blockIdx.x * EB + threadIdx.x;
   if (j >= d) return;
-  for (int k = 0; k < n; ++k) Zp[(long)k * d + j] = Z[(long)k * d + j];
+  for (int k = 0; k < n; ++k) Zp[(long)k * d + j] = Z[(long)(w_lo + k) * d + j];
   for (int k = 0; k < n; ++k) {
+    const int w = w_lo + k;
     const double g = q[k * dp + j] - b[(long)k * d + j];
-    const bool hl = k > 0, hr = k < n - 1;
-    const double left = hl ? (jacobi ? Zp[(long)(k - 1) * d + j] : Z[(long)(k - 1) * d + j]) : 0.0;
-    const double right = hr ? Zp[(long)(k + 1) * d + j] : 0.0;
+    const bool hl = w > 0, hr = w < n_total - 1;
+    // the left ghost (k = 0) and right ghost (k = n - 1) rows already carry the right semantics
+    const double left = hl ? ((jacobi && k > 0) ? Zp[(long)(k - 1) * d + j] : Z[(long)(w - 1) * d + j]) : 0.0;
+    const double right = hr ? (k < n - 1 ? Zp[(long)(k + 1) * d + j] : Z[(long)(w + 1) * d + j]) : 0.0;
     double zn;
     if (!hl && !hr) zn = g;
     else if (!hl) zn = right + g;
     else if (!hr) zn = left + g;
     else zn = 0.5 * right + 0.5 * left + g;
-    Z[(long)k * d + j] = zn;
+    Z[(long)w * d + j] = zn;
     th[k * dp + j] = -alpha * zn;
   }
 }
@@ -505,6 +521,12 @@ int gadmm_fob_lag(const double* q, long dp, const double* b, const double* th, d
   return 0;
 }
 
+int gadmm_fob_lag_rows(const int* mask, int n_local, double* rows, const ChainCtl* ctl, hipStream_t st) {
+  hipLaunchKernelGGL(fob_lag_rows, dim3(1), dim3(64), 0, st, mask, n_local, rows, ctl);
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
 // per-worker objective partials of th_n (rows of q / th with stride dp), e.g. dual averaging's
 // previous iterate
 int gadmm_fob_worker_obj(const double* q, long dp, const double* b, const double* th, double* part, int d, int n,
@@ -525,9 +547,13 @@ int gadmm_fob_objw(const double* part, int nblk, const double* yy, double* objw,
 }
 
 int gadmm_fob_da_sweep(const double* q, long dp, const double* b, double* th, double* Z, double* Zp, int d, int n,
-                       double alpha, int jacobi, const ChainCtl* ctl, hipStream_t st) {
-  hipLaunchKernelGGL(fob_da_sweep, dim3((d + EB - 1) / EB), dim3(EB), 0, st, q, dp, b, th, Z, Zp, d, n, alpha, jacobi,
-                     ctl);
+                       int w_lo, int n_total, double alpha, int jacobi, const ChainCtl* ctl, hipStream_t st) {
+  if (n < 1 || w_lo < 0 || w_lo + n > n_total) {
+    gadmm_set_error("fob_da_sweep: rows %d + %d of %d", w_lo, n, n_total);
+    return -1;
+  }
+  hipLaunchKernelGGL(fob_da_sweep, dim3((d + EB - 1) / EB), dim3(EB), 0, st, q, dp, b, th, Z, Zp, d, n, w_lo, n_total,
+                     alpha, jacobi, ctl);
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

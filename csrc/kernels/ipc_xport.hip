@@ -93,6 +93,74 @@ __global__ void __launch_bounds__(64) ipc_xchg_kernel(XchgBatch b, double* table
   }
 }
 
+// Conditional row all-gather (LAG's uploads across ranks, GD_DGD_LAG.m:184-327): one workgroup per
+// global worker w of the table. The rank that owns w pushes a flag granule (code phase_f, granule 0 of
+// row w) to every other rank, and -- only when mask[w - w_lo] != 0 -- the row T[w] itself (code
+// phase_r); every other rank polls the flag in its own mailbox and copies the row only when the flag
+// says it was sent. So a worker that does not trigger moves 16 bytes per peer, not d x 16.
+__global__ void __launch_bounds__(256) ipc_cond_rows_kernel(double* T, const int* mask, int n_local, int w_lo, int d,
+                                                            int n_total, int R, int me, int nranks, int phase_r,
+                                                            int phase_f, u32x4* const* boxes, u32x4* my_box,
+                                                            const unsigned* word, ChainCtl* ctl,
+                                                            long long timeout_ticks) {
+  __shared__ int flag_sh;
+  if (ctl->done) return;
+  const int w = blockIdx.x;
+  const unsigned code_r = (unsigned)(4 * ctl->iter + phase_r) & 0xfffffu;
+  const unsigned code_f = (unsigned)(4 * ctl->iter + phase_f) & 0xfffffu;
+  const unsigned tag_r = make_tag(word[0], (int)code_r), tag_f = make_tag(word[0], (int)code_f);
+  const long base_r = ((long)(code_r % (unsigned)R) * n_total + w) * d;
+  const long base_f = ((long)(code_f % (unsigned)R) * n_total + w) * d;
+  double* row = T + (long)w * d;
+  if (w >= w_lo && w < w_lo + n_local) {
+    const int m = mask[w - w_lo];
+    for (int r = 0; r < nranks; ++r) {
+      if (r == me) continue;
+      if (threadIdx.x == 0) store_granule<true>(rsrc_of(boxes[r] + base_f), 0, tag_f, m ? 1.0 : 0.0);
+      if (m) {
+        const __amdgpu_buffer_rsrc_t rs = rsrc_of(boxes[r] + base_r);
+        for (int i = threadIdx.x; i < d; i += blockDim.x) store_granule<true>(rs, i * 16, tag_r, row[i]);
+      }
+    }
+    return;
+  }
+  const unsigned long long deadline = now_ticks() + (unsigned long long)timeout_ticks;
+  if (threadIdx.x == 0) {
+    const __amdgpu_buffer_rsrc_t rs = rsrc_of(my_box + base_f);
+    double f = 0.0;
+    int got = -1;
+    for (int spin = 0;; ++spin) {
+      if (load_granule<true>(rs, 0, tag_f, &f)) {
+        got = f != 0.0 ? 1 : 0;
+        break;
+      }
+      if ((spin & 7) == 7 && now_ticks() > deadline) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    flag_sh = got;
+  }
+  __syncthreads();
+  const int got = flag_sh;
+  if (got < 0) {
+    if (threadIdx.x == 0) give_up(ctl);
+    return;
+  }
+  if (!got) return;
+  const __amdgpu_buffer_rsrc_t rs = rsrc_of(my_box + base_r);
+  for (int i = threadIdx.x; i < d; i += blockDim.x) {
+    double v = 0.0;
+    for (int spin = 0;; ++spin) {
+      if (load_granule<true>(rs, i * 16, tag_r, &v)) break;
+      if ((spin & 7) == 7 && now_ticks() > deadline) {
+        give_up(ctl);
+        return;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    row[i] = v;
+  }
+}
+
 // Block-end reduction of the per-worker objective ring: every rank pushes its workers' entries into
 // every rank's obj area, then reads all n_total x ring entries back into `reduced` (worker-indexed, so
 // the monitor's worker-order sum is the same on every rank and equal to the single-rank sum).
@@ -319,6 +387,24 @@ int gadmm_ipc_exchange_rows(void* h, const XchgOp* ops, int nops, double* table,
     hipLaunchKernelGGL(ipc_xchg_kernel, dim3(b.n), dim3(64), 0, st, b, table, d, x->n_total, x->R, x->d_boxes,
                        x->box, x->d_word, ctl, x->timeout_ticks);
   }
+  GADMM_CHECK(hipGetLastError());
+  return 0;
+}
+
+// Conditional row all-gather over table T (n_total x d): see ipc_cond_rows_kernel. Codes 4 * iter +
+// phase_r / phase_f (every rank issues the same calls per iteration). The bytes depend on the device
+// mask, so they are not counted here: the caller derives them from its upload counts.
+int gadmm_ipc_cond_rows(void* h, double* T, const int* mask, int n_local, int w_lo, int d, int phase_r, int phase_f,
+                        ChainCtl* ctl, hipStream_t st) {
+  IpcXport* x = (IpcXport*)h;
+  if (!x || !T || !mask || !ctl || d != x->d || n_local < 0 || w_lo < 0 || w_lo + n_local > x->n_total ||
+      phase_r == phase_f) {
+    gadmm_set_error("ipc_cond_rows: bad arguments (d=%d transport d=%d, rows %d+%d of %d)", d, x ? x->d : -1, w_lo,
+                    n_local, x ? x->n_total : -1);
+    return -1;
+  }
+  hipLaunchKernelGGL(ipc_cond_rows_kernel, dim3(x->n_total), dim3(256), 0, st, T, mask, n_local, w_lo, d, x->n_total,
+                     x->R, x->rank, x->nranks, phase_r, phase_f, x->d_boxes, x->box, x->d_word, ctl, x->timeout_ticks);
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

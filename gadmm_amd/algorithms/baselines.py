@@ -373,6 +373,7 @@ def lag(model, local_ids, n_total, num_iter, obj0, stepsize, hmax_full: torch.Te
     stop = Stopper(obj0, tol if tol is not None else -1.0, num_iter)
     converged, iters = False, num_iter
     w0 = ctx.lidx.get(0)
+    margin = float("inf")
     for it in range(1, num_iter + 1):
         theta = hist[-1]
         rows, vals = [], []
@@ -385,10 +386,16 @@ def lag(model, local_ids, n_total, num_iter, obj0, stepsize, hmax_full: torch.Te
             trig = sum(float((hist[-n] - hist[-n - 1]) @ (hist[-n] - hist[-n - 1])) for n in range(1, TRIGGERSLOT + 1))
             if variant == "PS":
                 dd = ((theta_hat - theta) ** 2).sum(-1)
-                mask = hloc * dd > thrd * trig
+                lhs = hloc * dd
             else:
                 dd = ((grads_now - G) ** 2).sum(-1)
-                mask = dd > thrd * trig
+                lhs = dd
+            rhs = thrd * trig
+            mask = lhs > rhs
+            # the closest trigger decision of the run (relative): an engine whose reductions sum in
+            # another order can only flip decisions whose margin is at rounding level
+            rel = (lhs - rhs).abs() / torch.clamp(torch.maximum(lhs.abs(), torch.full_like(lhs, abs(rhs))), min=1e-300)
+            margin = min(margin, float(rel.min()))
         if bool(mask.any()):
             sel = mask.nonzero().flatten()
             G[sel] = grads_now[sel]
@@ -423,7 +430,8 @@ def lag(model, local_ids, n_total, num_iter, obj0, stepsize, hmax_full: torch.Te
     n = len(stop.obj)
     units = np.asarray(comm_final) + np.arange(1, n + 1)
     assert np.array_equal(units, _lag_units(np.asarray(counts_trace)))
-    return _result("LAG-" + variant, stop, ctx, units, converged, iters if converged else n, uploads=uploads)
+    return _result("LAG-" + variant, stop, ctx, units, converged, iters if converged else n, uploads=uploads,
+                   trigger_margin=margin)
 
 
 # ------------------------------------------------------------------------------------------------ IAG

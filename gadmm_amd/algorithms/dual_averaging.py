@@ -47,8 +47,13 @@ def dual_averaging(model, local_ids: Sequence[int], n_total: int, alpha: float, 
                                     "rows_pushed": out["rows_pushed"], "wire_bytes": out["wire_bytes"],
                                     "model_bytes": n * n_total * model.d * 8, "dim": model.d})
         from ..engine.first_order_big import FirstOrderBigEngine
-        if comm.nranks == 1 and FirstOrderBigEngine.eligible(model, comm, n_total, local_ids, placement, "DualAvg"):
-            # d > 128 on one rank: the stream-ordered large-d engine (packed Grams, device stop rule)
+        big = FirstOrderBigEngine.eligible(model, comm, n_total, local_ids, placement, "DualAvg")
+        if comm.nranks > 1 and getattr(model, "kind", "") == "linear" and int(model.d) > 128:
+            from ..engine.first_order import _all_ok
+            big = _all_ok(big, comm)  # collective: every rank takes the same path
+        if big:
+            # d > 128: the stream-ordered large-d engine (packed Grams, device stop rule); across ranks the
+            # Gauss-Seidel sweep is a pipeline over the IPC transport (first_order_big.py)
             out = FirstOrderBigEngine.get(model, comm, placement, n_total).run("DualAvg", max_iter, alpha, obj0, tol,
                                                                                  jacobi=jacobi)
             obj = out["obj"]
@@ -56,8 +61,10 @@ def dual_averaging(model, local_ids: Sequence[int], n_total: int, alpha: float, 
             return RunResult(algorithm=name, obj=obj, loss=np.abs(obj - obj0),
                              iters=out["iters"] if out["converged"] else n, converged=out["converged"],
                              wall_s=float(out["times"][-1]) if n else 0.0, time_trace=out["times"],
-                             comm_units=np.arange(1, n + 1, dtype=np.float64) * n_total, bytes_sent=0, bytes_total=0,
-                             extra={"jacobi": jacobi, "nranks": 1, "engine": "native-big",
+                             comm_units=np.arange(1, n + 1, dtype=np.float64) * n_total,
+                             bytes_sent=int(out["payload_bytes"]), bytes_total=int(out["payload_bytes"]),
+                             extra={"jacobi": jacobi, "nranks": comm.nranks, "engine": "native-big",
+                                    "wire_bytes": out["wire_bytes"],
                                     "model_bytes": n * n_total * model.d * 8, "dim": model.d})
         if backend == "native":
             raise RuntimeError("native dual averaging needs GPU ranks with contiguous segments")

@@ -15,8 +15,18 @@ the server objective, one GEMV).
 Ranks: GD (all-reduce of the local A_sum th, d doubles per iteration), DGD (boundary gradients to the
 chain neighbours' ranks) and IAG (the refreshing worker's row broadcast from its owner, the objective
 partials all-reduced) run across ranks over the run's communicator -- RCCL, or the IPC device
-transport (``parallel/ipc.py``: also with ranks sharing one GPU); LAG and dual averaging run on one
-rank (their multi-rank runs keep the torch path).
+transport (``parallel/ipc.py``: also with ranks sharing one GPU). LAG-PS / LAG-WK and dual averaging
+run across ranks over the IPC transport:
+* LAG (GD_DGD_LAG.m:184-327): every rank keeps the server's gradient table and theta replicated; each
+  iteration its workers decide their triggers on the device and a CONDITIONAL row all-gather
+  (``ipc_cond_rows_kernel``) pushes a 16-byte flag per worker and the gradient row only for the
+  workers that upload -- the reference's conditional uploads, with the flag as the control message;
+* dual averaging (dual_averaging.m:15-70): the Gauss-Seidel sweep as a cross-rank pipeline -- a rank
+  receives its left neighbour's boundary Z of the current sweep before sweeping and sends its own last
+  row on after it; the right neighbour's first row of the previous sweep arrives at the pass start
+  (Jacobi: both boundary rows of the previous sweep, before the sweep).
+Both stay bit-identical to one rank: the server sums its table in worker order, objectives are
+all-reduced per worker, and the sweep reads exactly the values the one-rank sweep reads.
 """
 from __future__ import annotations
 
@@ -33,7 +43,8 @@ from ..parallel.topology import chain_plan
 
 TRIG = 10
 TICKS_PER_S = 1e8
-MULTI_ALGS = ("GD", "DGD", "IAG")
+MULTI_ALGS = ("GD", "DGD", "IAG", "LAG-PS", "LAG-WK", "DualAvg")
+IPC_ONLY = ("LAG-PS", "LAG-WK", "DualAvg")  # device-side conditional / pipelined exchanges
 
 _SIGS = {
     "gadmm_symv_batch": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long,
@@ -59,14 +70,20 @@ _SIGS = {
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+    "gadmm_fob_lag_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p]),
+    "gadmm_ipc_cond_rows": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_void_p]),
     "gadmm_fob_worker_obj": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                             ctypes.c_void_p]),
     "gadmm_fob_objw": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int,
                                       ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
     "gadmm_fob_da_sweep": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_void_p,
-                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
-                                          ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]),
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_void_p,
+                                          ctypes.c_void_p]),
     "gadmm_fob_finish": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double,
                                         ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
@@ -137,7 +154,8 @@ class FirstOrderBigEngine:
         if not multi:
             return int(model.n_local) == int(n_total)
         ids = [int(w) for w in (local_ids if local_ids is not None else placement.local_workers(comm.rank))]
-        return (alg in MULTI_ALGS and getattr(comm, "backend", "") in ("rccl", "ipc") and placement is not None
+        backends = ("ipc",) if alg in IPC_ONLY else ("rccl", "ipc")
+        return (alg in MULTI_ALGS and getattr(comm, "backend", "") in backends and placement is not None
                 and ids == list(range(ids[0], ids[0] + len(ids))) and len(ids) == int(model.n_local))
 
     @staticmethod
@@ -176,8 +194,8 @@ class FirstOrderBigEngine:
             sched: Optional[np.ndarray] = None, block: int = 16) -> Dict[str, object]:
         """One run from theta = 0 (``alg``: GD, DGD, LAG-PS, LAG-WK, IAG, DualAvg). Output as
         ``FirstOrderEngine.run``: obj / cnt / times traces, iters, converged, uploads, theta, bytes."""
-        if self.multi and alg not in MULTI_ALGS:
-            raise ValueError("large-d %s runs on one rank" % alg)
+        if self.multi and (alg not in MULTI_ALGS or (alg in IPC_ONLY and getattr(self.comm, "backend", "") != "ipc")):
+            raise ValueError("large-d %s across ranks needs the IPC transport" % alg)
         lib, L, ctl = self.lib, self.lib, self.ctl.data_ptr()
         d, dp, nl, n, nblk = self.d, self.dp, self.nl, self.n, self.nblk
         f64, dev = torch.float64, self.device
@@ -218,9 +236,22 @@ class FirstOrderBigEngine:
                 mask = torch.zeros((nl,), dtype=torch.int32, device=dev)
                 ddpart = torch.zeros((nl * nblk,), dtype=f64, device=dev)
                 hsq_t = hsq.to(dev, f64).contiguous()
+                rows_tr = torch.zeros((int(max_iter),), dtype=f64, device=dev)  # rows this rank sends
             if alg == "DualAvg":
-                Z = torch.zeros((nl, d), dtype=f64, device=dev)
+                Z = torch.zeros((n, d), dtype=f64, device=dev)  # chain-wide table: own rows + ghosts
                 Zp = torch.zeros((nl, d), dtype=f64, device=dev)
+                if self.multi:
+                    R_, r_ = self.nranks, self.rank
+                    lo, hi = self.w_lo, self.w_lo + nl - 1
+                    if jacobi:  # both boundary rows of the previous sweep, before the sweep
+                        da_pre = ([(r_ - 1, lo, 1), (r_ - 1, lo - 1, 0)] if r_ > 0 else []) + \
+                                 ([(r_ + 1, hi, 1), (r_ + 1, hi + 1, 0)] if r_ + 1 < R_ else [])
+                        da_left, da_post = [], []
+                    else:  # right ghost (previous sweep) at the pass start; left ghost of THIS sweep; send on
+                        da_pre = ([(r_ - 1, lo, 1)] if r_ > 0 else []) + ([(r_ + 1, hi + 1, 0)] if r_ + 1 < R_ else [])
+                        da_left = [(r_ - 1, lo - 1, 0)] if r_ > 0 else []
+                        da_post = [(r_ + 1, hi, 1)] if r_ + 1 < R_ else []
+                    pay_da = sum(1 for _, _, snd in da_pre + da_post if snd) * d * 8
             if alg == "DGD" and self.multi:
                 plan = chain_plan(list(range(n)), self.placement, self.rank)
                 xops = plan.xchg_head + plan.xchg_tail
@@ -298,8 +329,14 @@ class FirstOrderBigEngine:
                                            ddpart.data_ptr(), hsq_t.data_ptr(), ring.data_ptr(), mask.data_ptr(),
                                            cnt.data_ptr(), d, nl, self.w_lo, ps, float(thrd), int(faithful), ctl, st),
                            "lag")
+                        if self.multi:  # the uploads: a flag per worker, the row only when it triggered
+                            ck(L.gadmm_fob_lag_rows(mask.data_ptr(), nl, rows_tr.data_ptr(), ctl, st), "lag_rows")
+                            ck(L.gadmm_ipc_cond_rows(self.comm.xport, T.data_ptr(), mask.data_ptr(), nl, self.w_lo, d,
+                                                     2, 3, ctl, st), "ipc_cond_rows")
                         ck(L.gadmm_fob_objw(part.data_ptr(), nblk, self.yy.data_ptr(), objw.data_ptr(), nl, self.w_lo,
                                             n, ctl, st), "objw")
+                        if self.multi:
+                            self._allreduce(objw)
                         ck(L.gadmm_fob_server(None, None, th.data_ptr(), T.data_ptr(), None, dpart.data_ptr(), d, n,
                                               float(step), ctl, st), "server")
                         ck(L.gadmm_fob_finish(objw.data_ptr(), n, 1, zeros_n.data_ptr(), trace.data_ptr(),
@@ -312,13 +349,21 @@ class FirstOrderBigEngine:
                                                   d, nl, ctl, st), "worker_obj")
                         ck(L.gadmm_fob_objw(part.data_ptr(), nblk, self.yy.data_ptr(), objw.data_ptr(), nl, self.w_lo,
                                             n, ctl, st), "objw")
+                        if self.multi:
+                            self._allreduce(objw)
                         ck(L.gadmm_fob_finish(objw.data_ptr(), n, 1, zeros_n.data_ptr(), trace.data_ptr(),
                                               tstamp.data_ptr(), max_iter, float(obj0), tolv, 1, None, None, ctl, st),
                            "finish")
                         if it <= max_iter:
+                            if self.multi:
+                                self._xchg(Z, da_pre, 1)
+                                self._xchg(Z, da_left, 0)
+                                pay[-1] += pay_da
                             ck(L.gadmm_fob_da_sweep(q.data_ptr(), dp, self.b.data_ptr(), th.data_ptr(), Z.data_ptr(),
-                                                    Zp.data_ptr(), d, nl, float(step), int(bool(jacobi)), ctl, st),
-                               "da_sweep")
+                                                    Zp.data_ptr(), d, nl, self.w_lo, n, float(step),
+                                                    int(bool(jacobi)), ctl, st), "da_sweep")
+                            if self.multi:
+                                self._xchg(Z, da_post, 0)
                 done = int(self.ctl[1].item())  # one host look per block
             c = self.ctl.cpu().tolist()
             wall = time.perf_counter() - t0
@@ -332,9 +377,20 @@ class FirstOrderBigEngine:
                "payload_bytes": 0, "wire_bytes": 0, "wall_s": wall}
         out["engine"] = "native-big"
         if self.multi:  # payload the iterations 1..k put on the fabric, all ranks (skipped ones moved nothing)
-            t = torch.tensor([float(sum(pay[:k]))], dtype=torch.float64)
             import torch.distributed as dist
-            dist.all_reduce(t, group=getattr(self.comm, "control_group", None))
+            grp = getattr(self.comm, "control_group", None)
+            if alg.startswith("LAG"):
+                # conditional uploads: the rows that travelled (to every other rank) + one flag per
+                # worker per iteration; the upload counts are summed over ranks
+                rows_sent = float(rows_tr[:k].sum().item())
+                pay_lag = (rows_sent * d + float(k) * nl) * 8 * (self.nranks - 1)
+                c = torch.from_numpy(np.ascontiguousarray(counts, dtype=np.float64))
+                dist.all_reduce(c, group=grp)
+                out["cnt"] = c.numpy()
+                out["uploads"] = float(out["cnt"].sum())
+                pay = [pay_lag]
+            t = torch.tensor([float(sum(pay[:k]))], dtype=torch.float64)
+            dist.all_reduce(t, group=grp)
             out["payload_bytes"] = int(round(float(t.item())))
             out["wire_bytes"] = out["payload_bytes"] * (2 if getattr(self.comm, "backend", "") == "ipc" else 1)
         return out

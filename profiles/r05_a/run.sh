@@ -4,6 +4,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/r5a; mkdir -p $O
+timeout -k 10 300 python -u tools/lag_diverge.py > $O/lag_diverge.log 2>&1 || exit $?
 timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu.py \
   -k "rccl or spd_inverse_blocked or large_d_optimum or first_order_big or bench_json or graft_smoke or gemm_f64" \
   > $O/t_gpu.log 2>&1 || exit $?

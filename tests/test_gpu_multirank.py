@@ -744,19 +744,29 @@ def _fo_big_rank(rank, world, n, m_rows, d, iters):
     comm = IpcComm(n, d, 16, dev)
     s, obj0 = 1e-4, 0.0
     out = {}
+    from gadmm_amd.algorithms import lag, dual_averaging
+    full = gaussian_regression(n, m_rows, d, seed=11, labels="linear", device=dev)
+    hmax = LinearRegression(full.X, full.y).hmax()  # every worker's (the LAG-PS trigger weights)
     for name, fn in (("GD", lambda: gradient_descent(m, ids, n, iters, obj0, s, comm=comm, placement=pl)),
                      ("DGD", lambda: decentralized_gd(m, ids, n, iters, obj0, s, comm=comm, placement=pl)),
-                     ("cIAG", lambda: iag(m, ids, n, iters, obj0, s, "cyclic", None, comm=comm, placement=pl))):
+                     ("cIAG", lambda: iag(m, ids, n, iters, obj0, s, "cyclic", None, comm=comm, placement=pl)),
+                     ("LAG-PS", lambda: lag(m, ids, n, iters, obj0, s, hmax, "PS", comm=comm, placement=pl)),
+                     ("LAG-WK", lambda: lag(m, ids, n, iters, obj0, s, hmax, "WK", comm=comm, placement=pl)),
+                     ("DualAvg", lambda: dual_averaging(m, ids, n, s, obj0, 1e-12, iters, comm=comm, placement=pl)),
+                     ("DualAvg-J", lambda: dual_averaging(m, ids, n, s, obj0, 1e-12, iters, comm=comm, placement=pl,
+                                                          jacobi=True))):
         r = fn()
-        out[name] = (r.obj, r.extra.get("engine"), r.bytes_sent)
+        out[name] = (r.obj, r.extra.get("engine"), r.bytes_sent, r.extra.get("uploads"))
     comm.close()
     return out
 
 
 def test_first_order_big_across_ranks():
     """The large-d GD (all-reduce of the local Gram-sum GEMV), DGD (boundary gradients to the neighbour
-    ranks) and IAG (the refreshing worker's row broadcast from its owner) over the IPC device transport,
-    2 ranks sharing the GPU, == one rank to 1e-11; payload = the per-iteration collective bytes."""
+    ranks), IAG (the refreshing worker's row broadcast from its owner), LAG-PS / LAG-WK (conditional
+    uploads: a flag per worker, the row only when it triggers) and dual averaging (Gauss-Seidel
+    pipeline and Jacobi) over the IPC device transport, 2 ranks sharing the GPU, == one rank to 1e-11
+    with the LAG upload counts exact; payload = the per-iteration bytes."""
     import torch
     from gadmm_amd.parallel.launch import spawn
     from gadmm_amd.data import gaussian_regression
@@ -766,13 +776,28 @@ def test_first_order_big_across_ranks():
     res = spawn(_fo_big_rank, 2, n, m_rows, d, iters, timeout=300)
     ds = gaussian_regression(n, m_rows, d, seed=11, labels="linear", device=DEV)
     m = LinearRegression(ds.X, ds.y)
-    one = {"GD": gradient_descent(m, list(range(n)), n, iters, 0.0, 1e-4),
-           "DGD": decentralized_gd(m, list(range(n)), n, iters, 0.0, 1e-4),
-           "cIAG": iag(m, list(range(n)), n, iters, 0.0, 1e-4, "cyclic", None)}
+    from gadmm_amd.algorithms import lag, dual_averaging
+    hmax = m.hmax()
+    al = list(range(n))
+    one = {"GD": gradient_descent(m, al, n, iters, 0.0, 1e-4),
+           "DGD": decentralized_gd(m, al, n, iters, 0.0, 1e-4),
+           "cIAG": iag(m, al, n, iters, 0.0, 1e-4, "cyclic", None),
+           "LAG-PS": lag(m, al, n, iters, 0.0, 1e-4, hmax, "PS"),
+           "LAG-WK": lag(m, al, n, iters, 0.0, 1e-4, hmax, "WK"),
+           "DualAvg": dual_averaging(m, al, n, 1e-4, 0.0, 1e-12, iters),
+           "DualAvg-J": dual_averaging(m, al, n, 1e-4, 0.0, 1e-12, iters, jacobi=True)}
     for r in res:
         for k, ref in one.items():
-            obj, eng, _ = r[k]
+            obj, eng, _, up = r[k]
             assert eng == "native-big" and ref.extra["engine"] == "native-big", (k, eng)
-            np.testing.assert_allclose(obj, ref.obj, rtol=1e-11, atol=0)
+            np.testing.assert_allclose(obj, ref.obj, rtol=1e-11, atol=0, err_msg=k)
+            if k.startswith("LAG"):  # the upload counts summed over ranks == one rank, exactly
+                assert up == ref.extra["uploads"], (k, up, ref.extra["uploads"])
+    # LAG: every iteration one 8-byte flag per worker to the other rank, plus the rows that travelled
+    for k in ("LAG-PS", "LAG-WK"):
+        assert res[0][k][2] == res[1][k][2] and res[0][k][2] >= iters * n * 8, (k, res[0][k][2])
+    # Gauss-Seidel: per iteration rank 0 sends its last row on and rank 1 its first row back (2 rows);
+    # Jacobi: the same two rows, before the sweep
+    assert res[0]["DualAvg"][2] == iters * 2 * d * 8 and res[0]["DualAvg-J"][2] == iters * 2 * d * 8
     assert res[0]["GD"][2] == iters * 2 * d * 8          # each rank pushes its d-row partial to the other
     assert res[0]["DGD"][2] == iters * 2 * d * 8         # one boundary: a gradient row each way
