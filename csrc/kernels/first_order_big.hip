@@ -268,13 +268,17 @@ __global__ void fob_objw(const double* part, int nblk, const double* yy, double*
 // `shift` = 1: the objective belongs to the previous iteration (dual averaging evaluates th^{it-1}
 // with the GEMV of iteration it); ring / dpart: LAG's |dth|^2 history.
 __global__ void fob_finish(const double* part, int nw, int nblk, const double* yy, double* trace, long long* tstamp,
-                           int max_iter, double obj0, double tol, int shift, const double* dpart, double* ring,
-                           ChainCtl* ctl) {
+                           int max_iter, double obj0, double tol, int shift, const double* dpart, int dnblk,
+                           double* ring, ChainCtl* ctl) {
   if (threadIdx.x != 0 || ctl->done) return;
   const int it = ctl->iter;
   if (dpart) {  // LAG: |th^{it} - th^{it-1}|^2 into the ring slot it % 11 (read from iteration it + 1 on)
+    // dpart has one partial per 128-element block of theta (dnblk of them), independent of the
+    // objective rows' `nblk` (LAG's objective comes as one entry per worker: nblk = 1). Summing only
+    // `nblk` partials here kept the first 128 coordinates of the step at d > 128 -- an underestimated
+    // trigger threshold, extra uploads (tools/lag_diverge.py, profiles/r05_a).
     double s = 0.0;
-    for (int k = 0; k < nblk; ++k) s += dpart[k];
+    for (int k = 0; k < dnblk; ++k) s += dpart[k];
     ring[it % (TRIG + 1)] = s;
   }
   const int rec = it - shift;  // the iteration this objective belongs to
@@ -559,10 +563,14 @@ int gadmm_fob_da_sweep(const double* q, long dp, const double* b, double* th, do
 }
 
 int gadmm_fob_finish(const double* part, int nw, int nblk, const double* yy, double* trace, long long* tstamp,
-                     int max_iter, double obj0, double tol, int shift, const double* dpart, double* ring, ChainCtl* ctl,
-                     hipStream_t st) {
+                     int max_iter, double obj0, double tol, int shift, const double* dpart, int dnblk, double* ring,
+                     ChainCtl* ctl, hipStream_t st) {
+  if (dpart && (dnblk < 1 || !ring)) {
+    gadmm_set_error("fob_finish: the step partials need their block count and the ring");
+    return -1;
+  }
   hipLaunchKernelGGL(fob_finish, dim3(1), dim3(64), 0, st, part, nw, nblk, yy, trace, tstamp, max_iter, obj0, tol,
-                     shift, dpart, ring, ctl);
+                     shift, dpart, dnblk, ring, ctl);
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

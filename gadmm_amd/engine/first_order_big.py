@@ -86,8 +86,8 @@ _SIGS = {
                                           ctypes.c_void_p]),
     "gadmm_fob_finish": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double,
-                                        ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
-                                        ctypes.c_void_p, ctypes.c_void_p]),
+                                        ctypes.c_double, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
 }
 
 
@@ -277,7 +277,7 @@ class FirstOrderBigEngine:
                         ck(L.gadmm_fob_gd(q.data_ptr(), self.bsum.data_ptr(), th.data_ptr(), part.data_ptr(), d,
                                           float(step), int(faithful), ctl, st), "fob_gd")
                         ck(L.gadmm_fob_finish(part.data_ptr(), 1, nblk, self.yysum.data_ptr(), trace.data_ptr(),
-                                              tstamp.data_ptr(), max_iter, float(obj0), tolv, 0, None, None, ctl, st),
+                                              tstamp.data_ptr(), max_iter, float(obj0), tolv, 0, None, 0, None, ctl, st),
                            "finish")
                     elif alg == "DGD":
                         ck(symv(self.Ap.data_ptr(), packed, th.data_ptr(), dp, q.data_ptr(), dp, work, nl, d, ctl, st),
@@ -294,7 +294,7 @@ class FirstOrderBigEngine:
                         ck(L.gadmm_fob_dgd_update(th.data_ptr(), dp, T.data_ptr(), d, nl, self.w_lo, n,
                                                   float(step), ctl, st), "dgd_update")
                         ck(L.gadmm_fob_finish(objw.data_ptr(), n, 1, zeros_n.data_ptr(), trace.data_ptr(),
-                                              tstamp.data_ptr(), max_iter, float(obj0), tolv, 0, None, None, ctl, st),
+                                              tstamp.data_ptr(), max_iter, float(obj0), tolv, 0, None, 0, None, ctl, st),
                            "finish")
                     elif alg == "IAG":
                         w = int(sched[it - 1])
@@ -319,7 +319,7 @@ class FirstOrderBigEngine:
                         if self.multi:
                             self._allreduce(part[:nblk])
                         ck(L.gadmm_fob_finish(part.data_ptr(), 1, nblk, self.yysum.data_ptr(), trace.data_ptr(),
-                                              tstamp.data_ptr(), max_iter, float(obj0), tolv, 0, None, None, ctl, st),
+                                              tstamp.data_ptr(), max_iter, float(obj0), tolv, 0, None, 0, None, ctl, st),
                            "finish")
                     elif alg.startswith("LAG"):
                         ck(symv(self.Ap.data_ptr(), packed, th.data_ptr(), 0, q.data_ptr(), dp, work, nl, d, ctl, st),
@@ -341,7 +341,7 @@ class FirstOrderBigEngine:
                                               float(step), ctl, st), "server")
                         ck(L.gadmm_fob_finish(objw.data_ptr(), n, 1, zeros_n.data_ptr(), trace.data_ptr(),
                                               tstamp.data_ptr(), max_iter, float(obj0), tolv, 0, dpart.data_ptr(),
-                                              ring.data_ptr(), ctl, st), "finish")
+                                              nblk, ring.data_ptr(), ctl, st), "finish")
                     else:  # DualAvg: pass `it` evaluates th^{it-1} (its stop rule) and sweeps to th^it
                         ck(symv(self.Ap.data_ptr(), packed, th.data_ptr(), dp, q.data_ptr(), dp, work, nl, d, ctl, st),
                            "symv")
@@ -352,7 +352,7 @@ class FirstOrderBigEngine:
                         if self.multi:
                             self._allreduce(objw)
                         ck(L.gadmm_fob_finish(objw.data_ptr(), n, 1, zeros_n.data_ptr(), trace.data_ptr(),
-                                              tstamp.data_ptr(), max_iter, float(obj0), tolv, 1, None, None, ctl, st),
+                                              tstamp.data_ptr(), max_iter, float(obj0), tolv, 1, None, 0, None, ctl, st),
                            "finish")
                         if it <= max_iter:
                             if self.multi:

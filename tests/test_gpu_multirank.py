@@ -801,3 +801,47 @@ def test_first_order_big_across_ranks():
     assert res[0]["DualAvg"][2] == iters * 2 * d * 8 and res[0]["DualAvg-J"][2] == iters * 2 * d * 8
     assert res[0]["GD"][2] == iters * 2 * d * 8          # each rank pushes its d-row partial to the other
     assert res[0]["DGD"][2] == iters * 2 * d * 8         # one boundary: a gradient row each way
+
+
+def _fo_big_golden_rank(rank, world):
+    import torch
+    from gadmm_amd.benchmarks import headline_rank_problem
+    from gadmm_amd.data import linear_synthetic
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import global_constants
+    from gadmm_amd.engine.first_order_big import FirstOrderBigEngine
+    from gadmm_amd.parallel.ipc import IpcComm
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    X, y, loc, pl, obj0 = headline_rank_problem(24, rank, world)
+    full = LinearRegression(linear_synthetic(24).X.to(dev), linear_synthetic(24).y.to(dev))
+    s = global_constants(full)["stepsize"]
+    hsq = full.hmax() ** 2
+    m = LinearRegression(X.to(dev), y.to(dev))
+    comm = IpcComm(24, 50, 16, dev)
+    eng = FirstOrderBigEngine(m, comm, pl, 24)
+
+    def first(o):
+        hit = np.nonzero(np.abs(o["obj"] - obj0) < 1e-4)[0]
+        return int(hit[0]) + 1 if len(hit) else None
+
+    out = {}
+    gd = eng.run("GD", 60000, s, obj0, None, True, block=256)
+    out["GD"] = (first(gd), None, gd["payload_bytes"])
+    for v, k in (("LAG-PS", 10.0), ("LAG-WK", 1.0)):
+        r = eng.run(v, 60000, s, obj0, None, True, thrd=k / (s ** 2 * 24 ** 2) / 10, hsq=hsq, block=256)
+        out[v] = (first(r), int(r["uploads"]), r["payload_bytes"])
+    comm.close()
+    return out
+
+
+def test_first_order_big_goldens_across_ranks():
+    """The reference goldens on the large-d engine's multi-rank path (run directly at d = 50, 2 ranks
+    sharing the GPU, IPC transport): GD first below 1e-4 at 53,891; LAG-PS 52,890 with
+    342,113 uploads; LAG-WK 44,368 with 58,186 uploads -- the upload counts summed over the ranks."""
+    from gadmm_amd.parallel.launch import spawn
+    res = spawn(_fo_big_golden_rank, 2, timeout=900)
+    for r in res:
+        assert r["GD"][0] == 53891
+        assert r["LAG-PS"][:2] == (52890, 342113), r["LAG-PS"]
+        assert r["LAG-WK"][:2] == (44368, 58186), r["LAG-WK"]
