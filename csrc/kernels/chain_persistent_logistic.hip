@@ -546,10 +546,13 @@ __global__ void __launch_bounds__(SPLIT_NT) chain_persistent_logistic_split_kern
 extern "C" long gadmm_resident_capacity(const void* fn, int threads, size_t shm);
 extern "C" int gadmm_xcd_mode(const PersistArgs* a, int blocks, long cap_total);  // chain_persistent.hip
 
-// GADMM_LOGISTIC_SPLIT=0: the one-wave-per-worker kernel (A/B reference); default: four waves per worker
+// GADMM_LOGISTIC_SPLIT=1: four waves per worker (opt-in). Measured on MI355X (profiles/r05_c, E3, same
+// box, alternating): 6.60 / 6.71 ms vs 6.37 / 6.39 ms for the one-wave kernel -- bit-identical, but slower:
+// the inner step is bound by its dependent chain (13-deep FMA chains, exp, divide, the LDS staging of x),
+// not by FMA issue, so a quarter of the FMAs per SIMD gains nothing and the step barrier adds latency.
 static bool logi_split() {
   const char* e = getenv("GADMM_LOGISTIC_SPLIT");
-  return !(e && e[0] == '0');
+  return e && e[0] == '1';
 }
 
 static const void* logi_variant(const PersistArgs& a, const LogiArgs& g) {

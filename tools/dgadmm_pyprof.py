@@ -1,5 +1,5 @@
 """cProfile of the host side of repeated D-GADMM solves (bench config, coherence 10): where the ~170 us
-before the persistent launch go. Usage: python tools/dgadmm_pyprof.py [coherence]"""
+before the persistent launch go. Usage: python tools/dgadmm_pyprof.py [coherence] [refresh]"""
 import cProfile
 import os
 import pstats
@@ -22,7 +22,8 @@ obj0 = opt_linear(Xf.numpy(), yf.numpy())
 m = LinearRegression(ds.X.to(dev).contiguous(), ds.y.to(dev).contiguous())
 p0, c0, _ = T.find_path(24, np.random.default_rng(5))
 COH = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-opts = {"state": False, "residual": False}
+REFRESH = len(sys.argv) > 2 and sys.argv[2] == "refresh"  # the bench's step: Gram + inverses per solve
+opts = {"state": False, "residual": False, "refresh": REFRESH}
 
 
 def solve():
