@@ -406,6 +406,27 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         e0, start_iter, pending_in, cont = 0, 1, 0, False
         done = iters = 0
         last_launched = 0
+        pre = {}
+        ep_all = ep_start  # every epoch's first iteration (ep_start is truncated after the launches)
+
+        def cost_arrays():
+            """Per-epoch chain costs of every epoch drawn so far and the cumulative com_cost of each
+            iteration they cover: needs no outcome, so it runs while the launch executes
+            (run_persistent's on_enqueued) instead of after it."""
+            nd = n_drawn[0]
+            if pre.get("nd") == nd:
+                return
+            if drawn_C and any(c.dtype == object for c in drawn_C):
+                Cn_ = np.empty(sum(len(c) for c in drawn_C), dtype=object)
+                Cn_[:] = [c for cc in drawn_C for c in cc]
+            else:
+                Cn_ = np.concatenate(drawn_C) if drawn_C else np.zeros((0, max(n_total - 1, 0)))
+            # per-epoch cost; the initial cost vector may be ragged (the v0 column-slice quirk)
+            csum = Cn_.sum(axis=1) if (len(Cn_) and Cn_.dtype != object) else np.asarray([float(np.sum(c)) for c in Cn_])
+            per_it_ = np.concatenate([[float(np.sum(saved[2]))], csum]) * (n_heads if cost_quirk else 1)
+            span = int(ep_all[nd] - 1) if nd < E_total else int(max_iter)  # iterations the drawn epochs cover
+            which_ = np.searchsorted(ep_all[:nd], np.arange(1, span + 1), side="right") - 1
+            pre.update(nd=nd, Cn=Cn_, com=np.cumsum(per_it_[which_]))
         while True:
             e1 = min(e0 + chunk, E_total)  # this launch executes epochs e0 .. e1 - 1
             look = e1 if e1 < E_total else e1 - 1  # + the next epoch's chain (push targets of theta^hard_stop)
@@ -419,7 +440,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             try:
                 r = eng.run_persistent(epochs=(st_arr, P_arr), fabric=fabric, start_iter=start_iter,
                                        pending_in=pending_in, hard_stop=hard_stop, cont=cont, fetch_trace=True,
-                                       blocked_dyn=use_blk)
+                                       blocked_dyn=use_blk, on_enqueued=cost_arrays)
             except HandoffTimeout as e:
                 if comm.nranks == 1:
                     raise
@@ -456,18 +477,11 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         ep_start = ep_start[:n_drawn[0]]
         hints[hint_key] = int(np.searchsorted(ep_start, max(last_launched, 1), side="right"))
         Pn = Pall[1:n_drawn[0]]
-        if drawn_C and any(c.dtype == object for c in drawn_C):
-            Cn = np.empty(sum(len(c) for c in drawn_C), dtype=object)
-            Cn[:] = [c for cc in drawn_C for c in cc]
-        else:
-            Cn = np.concatenate(drawn_C) if drawn_C else np.zeros((0, max(n_total - 1, 0)))
+        cost_arrays()  # already done while the last launch ran, unless it drew more epochs since
+        Cn = pre["Cn"]
         starts = ep_start
         P = Pall[:n_drawn[0]]
-        # per-epoch cost; the initial cost vector may be ragged (the v0 column-slice quirk)
-        csum = Cn.sum(axis=1) if (len(Cn) and Cn.dtype != object) else np.asarray([float(np.sum(c)) for c in Cn])
-        per_it = np.concatenate([[float(np.sum(saved[2]))], csum]) * (n_heads if cost_quirk else 1)
-        which = np.searchsorted(starts, np.arange(1, iters + 1), side="right") - 1
-        com_cost = np.cumsum(per_it[which])
+        com_cost = pre["com"][:iters]
         # leave the schedule (and the engine's plan) where the epoch-by-epoch run would have left them
         schedule.skip(saved, Pn, Cn, int(np.searchsorted(rechains, iters, side="right")))  # rechains ascend
         eng.set_path(P[int(np.searchsorted(starts, max(last_launched, 1), side="right") - 1)], placement, rank)

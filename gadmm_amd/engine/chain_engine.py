@@ -308,6 +308,8 @@ class NativeChainEngine:
             shifts, self.deg_to_var = [rho, 2.0 * rho], (0, 0, 1)
         self.nvar = len(shifts)
         key = (tuple(shifts), self.A.shape[0])
+        if getattr(self, "_shift_key", None) != key or not in_place:
+            self._refresh_fast = None  # its bound arguments name the shifts / inverse buffers
         if getattr(self, "_shift_key", None) != key:  # (N, V) shifts + status word, built once per rho
             self._shift_key = key
             self._shifts = torch.tensor(shifts, dtype=torch.float64, device=self.device).unsqueeze(0).expand(
@@ -329,7 +331,36 @@ class NativeChainEngine:
 
     def refresh(self, X_loc: torch.Tensor, y_loc: torch.Tensor):
         """Recompute the loop-invariant set-up (Gram + cached inverses) from the raw shards, in place
-        (device pointers, hence captured graphs, stay valid). No host synchronisation."""
+        (device pointers, hence captured graphs, stay valid). No host synchronisation.
+        Repeated refreshes of the same shards at d <= 128 (every bench step) take a prebound path: the
+        Gram and inverse launches go straight to the native library on the engine stream with their
+        arguments built once (the general path's torch stream context, workspace allocation and
+        argument checks were ~20 us of host time per solve, on the critical path of a 1 ms D-GADMM
+        solve). Same kernels, same arguments: bit-identical."""
+        fast = getattr(self, "_refresh_fast", None)
+        if fast is not None and fast[0] is X_loc and fast[1] is y_loc:
+            lib, g_args, i_args = fast[2], fast[3], fast[4]
+            native.check(lib.gadmm_gram_f64(*g_args), "gram_f64")
+            native.check(lib.gadmm_spd_inverse_small_f64(*i_args), "spd_inverse_small_f64")
+            self._minv_version = getattr(self, "_minv_version", 0) + 1
+            return
+        if (self.model == "linear" and X_loc.is_cuda and self.d <= 128 and X_loc.dtype == torch.float64
+                and y_loc.dtype == torch.float64 and X_loc.is_contiguous() and y_loc.is_contiguous()
+                and tuple(X_loc.shape) == (self.n_local, self.m, self.d) and self.Minv is not None
+                and getattr(self, "_shifts", None) is not None and getattr(self, "_inv_status", None) is not None):
+            lib = self.lib
+            N, m, d = int(X_loc.shape[0]), int(X_loc.shape[1]), int(X_loc.shape[2])
+            ks = int(lib.gadmm_gram_pick_ksplit(N, m, d))
+            ws_n = int(lib.gadmm_gram_workspace(N, m, d, ks))
+            self._refresh_ws = torch.empty((max(ws_n, 1),), dtype=torch.float64, device=self.device) \
+                if ws_n > 0 else None
+            st = self.stream.cuda_stream
+            g_args = (X_loc.data_ptr(), y_loc.data_ptr(), N, m, d, ks, self.A.data_ptr(), self.b.data_ptr(),
+                      self.yy.data_ptr(), self._refresh_ws.data_ptr() if self._refresh_ws is not None else None, st)
+            i_args = (self.A.data_ptr(), self._shifts.data_ptr(), N, d, int(self._shifts.shape[1]),
+                      self.Minv.data_ptr(), self._inv_status.data_ptr(), st)
+            self._refresh_fast = (X_loc, y_loc, lib, g_args, i_args)
+            return self.refresh(X_loc, y_loc)
         with torch.cuda.stream(self.stream):
             if self.model == "linear":
                 gram(X_loc, y_loc, out=(self.A, self.b, self.yy))
@@ -580,7 +611,8 @@ class NativeChainEngine:
     def run_persistent(self, lag: int = 4, timeout_s: float = 20.0, start_iter: int = 1,
                        pending_in: int = 0, fabric=None, timeline_iters: int = 0,
                        epochs: Optional[Sequence] = None, hard_stop: int = 0, cont: bool = False,
-                       fetch_trace: bool = False, blocked_dyn: Optional[bool] = None) -> EngineRun:
+                       fetch_trace: bool = False, blocked_dyn: Optional[bool] = None,
+                       on_enqueued=None) -> EngineRun:
         """Whole solve in one launch per GPU. State must be reset (``reset()``) or resumed by the
         caller. ``fabric``: an ``XgmiFabric`` for the multi-GPU device-initiated transport.
         ``timeline_iters > 0`` records s_memrealtime stamps (10 ns) of the first iterations into
@@ -599,7 +631,10 @@ class NativeChainEngine:
         previous chunk's last epoch (its heads' pending duals are flushed with that chain).
         ``fetch_trace``: the objective trace and clock come back behind the same stream sync (for a
         caller that reads ``traces()`` next; a benchmark loop that does not leaves it off).
-        ``blocked_dyn``: D-GADMM on the blocked kernel's dynamic mode (None: ``dynamic_uses_blocked``)."""
+        ``blocked_dyn``: D-GADMM on the blocked kernel's dynamic mode (None: ``dynamic_uses_blocked``).
+        ``on_enqueued``: a host callback run after the launch and its read-back copy are queued and
+        before the stream is synchronised -- host work of the caller that does not need the outcome
+        (e.g. D-GADMM's per-epoch cost arrays) overlaps the kernel instead of following it."""
         _timing.host_stamp("rp:start")
         if epochs is not None:
             if not self.dynamic_eligible(fabric):
@@ -792,10 +827,21 @@ class NativeChainEngine:
                 # (PersistArgs::minv_pad); rebuilt from this solve's inverses on the engine stream, ahead of
                 # the launch, only after the inverses changed
                 if getattr(self, "_minv_pad", None) is None or self._minv_pad_version != self._minv_version:
-                    with torch.cuda.stream(self.stream):  # in place after the first build (one launch)
-                        self._minv_pad = quad_pad_image(self.Minv.reshape(self.n_local * self.nvar, self.d, self.d),
-                                                        int(self.lib.gadmm_chain_blocked_pad_dim(self.d)),
-                                                        out=getattr(self, "_minv_pad", None))
+                    pf = getattr(self, "_pad_fast", None)
+                    if pf is not None and pf[0] is self.Minv and pf[1] is self._minv_pad:
+                        native.check(self.lib.gadmm_pad_image_f64(*pf[2]), "pad_image")  # in place, one launch
+                    else:
+                        with torch.cuda.stream(self.stream):  # in place after the first build (one launch)
+                            self._minv_pad = quad_pad_image(self.Minv.reshape(self.n_local * self.nvar, self.d, self.d),
+                                                            int(self.lib.gadmm_chain_blocked_pad_dim(self.d)),
+                                                            out=getattr(self, "_minv_pad", None))
+                        src = _QUAD_SRC.get((self.d, int(self.lib.gadmm_chain_blocked_pad_dim(self.d)), self.device))
+                        if src is not None and self.Minv.is_contiguous():
+                            # later rebuilds: the same native launch with its arguments bound once
+                            self._pad_fast = (self.Minv, self._minv_pad,
+                                              (self.Minv.data_ptr(), self.d * self.d, src.data_ptr(), int(src.numel()),
+                                               self.n_local * self.nvar, self._minv_pad.data_ptr(),
+                                               self.stream.cuda_stream))
                     self._minv_pad_version = self._minv_version
                 pa.minv_pad = self._minv_pad.data_ptr()
         self.last_kernel = ("blocked%s(k=%d,L=%d,W=%d,pw=%d)" % ((("-dyn" if epochs is not None else ""),) + tuple(plan))
@@ -847,6 +893,9 @@ class NativeChainEngine:
         native.check(self.lib.gadmm_memcpy_d2h_async(self._rb_host.data_ptr(), self._rb.data_ptr(), nb,
                                                      self.stream.cuda_stream), "d2h")
         _timing.host_stamp("rp:copies_queued")
+        if on_enqueued is not None:
+            on_enqueued()
+            _timing.host_stamp("rp:overlapped")
         self.stream.synchronize()
         _timing.host_stamp("rp:synced")
         self._tr_valid = fetch
