@@ -62,7 +62,10 @@ def make_data_plane(fabric: str, world: int, device, share: bool, n_total: int, 
         from .comm import RcclComm
         comm, err = None, ""
         try:
-            comm = RcclComm(device, control_group=group, timeout_s=max(float(timeout_s), 1.0))
+            # set-up deadline: 30 s at least (topology discovery on an 8-GPU node takes seconds), the
+            # per-operation watchdog: the caller's deadline
+            comm = RcclComm(device, control_group=group, timeout_s=max(float(timeout_s), 1.0),
+                            init_timeout_s=max(30.0, float(timeout_s)))
         except Exception as e:  # set-up error or the non-blocking set-up's deadline
             err = "%s: %s" % (type(e).__name__, e)
         if _agree(comm is not None, world, group):

@@ -38,7 +38,7 @@ def _select_rank(rank, world, fail_rank):
     class StubRccl:
         backend = "rccl"
 
-        def __init__(self, device, control_group=None, timeout_s=60.0):
+        def __init__(self, device, control_group=None, timeout_s=60.0, init_timeout_s=120.0):
             if rank == fail_rank:
                 raise RuntimeError("rccl_init failed: set-up deadline passed")
             self.aborted = self.closed = False
