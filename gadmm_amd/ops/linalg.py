@@ -29,12 +29,50 @@ def gram_torch(X: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.Te
     return A, b, yy
 
 
+_OZ_WS: dict = {}
+
+
+def gram_ozaki(X: torch.Tensor, y: torch.Tensor, out=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Batched augmented Gram on the INT8 matrix cores (csrc/kernels/gram_ozaki.hip: the Ozaki scheme --
+    7 int8 digits per f64 value after a per-column power-of-two scaling, exact int32 MFMA products of the
+    28 digit pairs that reach f64 precision, f64 recombination). Same outputs as ``gram``; not bit-equal
+    to the f64-MFMA Gram (a different, exactly summed evaluation), as accurate or more."""
+    lib = native.require()
+    X = X.contiguous()
+    y = y.contiguous()
+    N, m, d = X.shape
+    if out is not None:
+        A, b, yy = out
+    else:
+        A = torch.empty((N, d, d), dtype=torch.float64, device=X.device)
+        b = torch.empty((N, d), dtype=torch.float64, device=X.device)
+        yy = torch.empty((N,), dtype=torch.float64, device=X.device)
+    nb = int(lib.gadmm_gram_ozaki_workspace(int(m), int(d)))
+    key = (X.device, nb)
+    ws = _OZ_WS.get(key)
+    if ws is None:
+        _OZ_WS.clear()  # one workspace at a time (up to ~1.4 GB at d = 10k)
+        ws = torch.empty((nb,), dtype=torch.uint8, device=X.device)
+        _OZ_WS[key] = ws
+    native.check(lib.gadmm_gram_ozaki_f64(X.data_ptr(), y.data_ptr(), int(N), int(m), int(d), A.data_ptr(),
+                                          b.data_ptr(), yy.data_ptr(), ws.data_ptr(), nb, native.stream_handle()),
+                 "gram_ozaki_f64")
+    return A, b, yy
+
+
+def gram_uses_ozaki(m: int, d: int) -> bool:
+    """GADMM_GRAM_OZAKI=1: the int8 Ozaki Gram for shards with d > 256 (opt-in)."""
+    return os.environ.get("GADMM_GRAM_OZAKI", "0") == "1" and d > 256
+
+
 def gram(X: torch.Tensor, y: torch.Tensor, ksplit: Optional[int] = None, out=None
          ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Batched augmented Gram. ``X``: (N, m, d) f64 contiguous, ``y``: (N, m).
     ``out``: optional preallocated ``(A, b, yy)`` written in place."""
     if X.dtype != torch.float64 or y.dtype != torch.float64:
         raise TypeError("gram expects float64")
+    if X.is_cuda and ksplit is None and gram_uses_ozaki(int(X.shape[1]), int(X.shape[2])):
+        return gram_ozaki(X, y, out=out)
     if not X.is_cuda:
         res = gram_torch(X, y)
         if out is not None:

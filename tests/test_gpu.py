@@ -1124,3 +1124,30 @@ def test_first_order_big_stops_on_device():
     ref = iag(m, list(range(4)), 4, 400, obj0, c["stepsize"], "cyclic", None, tol=1e-2 * abs(obj0), backend="torch")
     a = iag(m, list(range(4)), 4, 400, obj0, c["stepsize"], "cyclic", None, tol=1e-2 * abs(obj0))
     assert ref.converged and a.converged and a.iters == ref.iters
+
+
+@pytest.mark.parametrize("N,m,d", [(2, 5000, 300), (1, 20000, 97), (1, 9000, 1000)])
+def test_gram_ozaki_matches_f64(N, m, d):
+    """The int8-MFMA Ozaki Gram (gram_ozaki.hip: 7 digits per value, exact int32 digit-pair products, f64
+    recombination) equals an f64 reference: every entry within 1e-13 of sqrt(A_aa A_bb) (the f64-MFMA Gram
+    is checked the same way), b and y'y likewise; chunk boundaries (8192 samples) and padded columns
+    included."""
+    from gadmm_amd.ops.linalg import gram, gram_ozaki
+    g = torch.Generator(device=DEV)
+    g.manual_seed(N * 1000 + d)
+    X = torch.randn((N, m, d), dtype=torch.float64, device=DEV, generator=g) * 3.0
+    X[:, :, 0] *= 1e-3  # columns of different scales: per-column exponents
+    y = torch.randn((N, m), dtype=torch.float64, device=DEV, generator=g)
+    A, b, yy = gram_ozaki(X, y)
+    Ar = torch.bmm(X.transpose(1, 2), X)
+    br = torch.bmm(X.transpose(1, 2), y.unsqueeze(-1)).squeeze(-1)
+    yr = (y * y).sum(1)
+    sc = torch.sqrt(torch.diagonal(Ar, dim1=1, dim2=2))
+    assert torch.equal(A, A.transpose(1, 2))
+    assert ((A - Ar).abs() / (sc.unsqueeze(2) * sc.unsqueeze(1))).max().item() < 1e-13
+    assert ((b - br).abs() / (sc * yr.sqrt().unsqueeze(1))).max().item() < 1e-13
+    assert ((yy - yr).abs() / yr).max().item() < 1e-13
+    A2, _, _ = gram_ozaki(X, y)
+    assert torch.equal(A, A2)  # deterministic
+    A64, _, _ = gram(X, y)
+    assert ((A64 - Ar).abs() / (sc.unsqueeze(2) * sc.unsqueeze(1))).max().item() < 1e-13
