@@ -6,13 +6,15 @@
 // per worker) is therefore computed here as
 //   x_ij = 2^{e_j} sum_{p=1..S} d_p(i, j) 2^{-7 p},     d_p in [-127, 127]  (digits of x / 2^{e_j})
 //   A_ab = 2^{e_a + e_b} sum_{L=2}^{S+1} 2^{-7 L} sum_{p+q=L} sum_i d_p(i, a) d_q(i, b)
-// where e_j is the column's exponent (|x_ij| < 2^{e_j}), the digits are the truncated base-128
-// expansion (every digit has the sign of x), and the pairs with p + q > S + 1 are dropped (each below
+// where e_j is the column's exponent (|x_ij| <= (127/128) 2^{e_j}), the digits are the round-to-nearest
+// base-128 expansion (first digit within +-127, the others +-64; the residual after S digits is at most
+// half a unit of the last one and unbiased -- truncated digits left a one-signed residual whose sum over
+// the m samples biased the diagonal by ~1e-13 relative), and the pairs with p + q > S + 1 are dropped (each below
 // 2^{-7(S+2)} of the column scales: far under f64 rounding). Every inner sum is an EXACT int32 MFMA
 // accumulation (|d_p d_q| < 2^14; a chunk of K samples with at most S pairs per level stays below
 // 2^31 for K * S * 127^2 < 2^31, K = 8192 here), so the only roundings are the f64 recombination and
 // the chunk sums -- the result is as accurate as the f64-MFMA Gram (whose K-sum rounds at every
-// step) or better; the S-digit truncation of the inputs is 2^{-7S} of the column scale (S = 7: 2^-49).
+// step) or better; the S-digit residual of the inputs is <= 2^{-7S-1} of the column scale (S = 7: 2^-50).
 //
 // Kernels (host driver gadmm_gram_ozaki_f64 below, one chunk of KC samples at a time):
 //   oz_colexp   column exponents of the augmented [X | y] over the whole shard (one pass)
@@ -67,14 +69,18 @@ __global__ void __launch_bounds__(CE_NT) oz_colmax_part(const double* X, const d
   part[(long)blockIdx.y * Dp + j] = mx;
 }
 
-// e_j with max |x_ij| < 2^{e_j} (frexp), 0 for an all-zero column
+// e_j with max |x_ij| <= (127/128) 2^{e_j}, 0 for an all-zero column: the first round-to-nearest digit
+// then stays within [-127, 127]
 __global__ void __launch_bounds__(CE_NT) oz_colexp(const double* part, int Dp, int* e) {
   const int j = blockIdx.x * CE_NT + threadIdx.x;
   if (j >= Dp) return;
   double mx = 0.0;
   for (int r = 0; r < CE_R; ++r) mx = fmax(mx, part[(long)r * Dp + j]);
   int E = 0;
-  if (mx > 0.0) (void)frexp(mx, &E);
+  if (mx > 0.0) {
+    const double f = frexp(mx, &E);  // mx = f 2^E, f in [0.5, 1)
+    if (f > 127.0 / 128.0) ++E;
+  }
   e[j] = E;
 }
 
@@ -90,12 +96,12 @@ __global__ void __launch_bounds__(SLICE_NT) oz_slice(const double* X, const doub
   const int ej = on ? e[j] : 0;
   for (int t = 0; t < 32; ++t) {
     const long i = i0 + (long)kb * 32 + t;
-    double v = on ? ldexp(aug_at(X, y, i, j, m, d), -ej) : 0.0;  // |v| < 1
+    double v = on ? ldexp(aug_at(X, y, i, j, m, d), -ej) : 0.0;  // |v| <= 127/128
 #pragma unroll
     for (int p = 0; p < SL; ++p) {
       v *= 128.0;                      // exact (power of two)
-      const double q = trunc(v);       // |q| <= 127
-      v -= q;                          // exact: the remainder of an exact scaling
+      const double q = rint(v);        // nearest: |q| <= 127 for the first digit, <= 64 after
+      v -= q;                          // exact (|v - q| <= 1/2, representable)
       dig[p][threadIdx.x][t] = (signed char)(int)q;
     }
   }
