@@ -25,6 +25,10 @@
 //   oz_finish   the f64 Gram -> A (full symmetric), b, y'y
 #include <stdlib.h>
 #include <string.h>
+#include <algorithm>
+#include <map>
+#include <mutex>
+#include <vector>
 #include "gadmm_common.h"
 
 typedef int v4i __attribute__((ext_vector_type(4)));
@@ -45,8 +49,8 @@ __global__ void __launch_bounds__(64) mfma_i8_probe_kernel(const v4i* a, const v
 constexpr int SL = 7;          // digits per value (7 bits each: 2^-49 of the column scale)
 constexpr int KC = 8192;       // samples per chunk: SL * 127^2 * KC < 2^31 (exact int32 levels)
 constexpr int KBC = KC / 32;   // 32-sample blocks per chunk
-constexpr int OT = 128;        // output tile (features) per workgroup: 4 x 4 waves of 32 x 32
-constexpr int GEMM_NT = 1024;  // 16 waves
+constexpr int OT = 64;         // output tile (features) per workgroup: 2 x 2 waves of 32 x 32
+constexpr int GEMM_NT = 256;   // 4 waves
 constexpr int CE_NT = 256;     // column-exponent threads per workgroup (one column each)
 constexpr int CE_R = 128;      // row splits of the column-exponent pass
 
@@ -123,56 +127,55 @@ __global__ void __launch_bounds__(SLICE_NT) oz_slice(const double* X, const doub
   }
 }
 
-// Lower-triangle tile id -> (ti, tj), ti >= tj
-__device__ __forceinline__ void oz_tri(int t, int& ti, int& tj) {
-  ti = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
-  while ((ti + 1) * (ti + 2) / 2 <= t) ++ti;
-  while (ti * (ti + 1) / 2 > t) --ti;
-  tj = t - ti * (ti + 1) / 2;
-}
-
 // One chunk: C[a][b] += 2^{e_a + e_b} sum_L 2^{-7L} sum_{p+q=L} S_p[:, a]^T S_q[:, b] for the tile's
-// lower blocks. LDS per K step: the A and B panels, [slice][32-block][half][feature in block][16 B]
-// (a wave's ds_read_b128 of 16 lanes covers 256 contiguous bytes: conflict-free), double-buffered;
-// the next step's panels are fetched into registers while this step's MFMAs issue.
-__global__ void __launch_bounds__(GEMM_NT) oz_gemm(const signed char* S, int Dp, int nt, const int* e, double* C) {
-  extern __shared__ __attribute__((aligned(16))) v4i lds4[];  // 2 buffers x 2 panels x SL x 4 x 2 x 32
-  constexpr int PANEL = SL * 4 * 2 * 32;                       // v4i per panel
-  int ti, tj;
-  oz_tri((int)blockIdx.x, ti, tj);
-  const bool diag = ti == tj;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, bi = wv >> 2, bj = wv & 3;
-  const int a0 = ti * OT + bi * 32, b0 = tj * OT + bj * 32;
-  const bool work = a0 < Dp && b0 < Dp && (!diag || bi >= bj);
-  const int r = lane & 31, h = lane >> 5;
-  // cooperative copy: element idx -> (panel, slice, block, feature r, half) ; 2 * SL * 4 * 32 * 2 v4i
+// lower blocks. A workgroup is 4 waves on a 64 x 64 tile (one 32 x 32 block per wave: 7 level
+// accumulators = 112 registers + 14 operand fragments; two workgroups per CU = 2 waves per SIMD, 256
+// registers each -- the first cut, 16 waves on a 128 tile at 128 registers, spilled 238 VGPRs per lane).
+// LDS per K step: the A and B panels, [slice][32-block][half][feature in block][16 B] (a ds_read_b128
+// of 32 lanes covers 512 contiguous bytes: conflict-free), double-buffered; the next step's panels are
+// fetched into registers while this step's MFMAs issue. Tile order (host-built list, oz_tile_list):
+// lower-triangle tiles grouped in 8 x 8 super-blocks and dealt XCD-major (workgroup i runs on XCD i % 8),
+// so the 64 workgroups an XCD runs at once share 16 panels in its L2 instead of one row's 65.
+__global__ void __launch_bounds__(GEMM_NT, 2) oz_gemm(const signed char* S, int Dp, int tiles, const int2* list,
+                                                      int kbn, const int* e, double* C) {
+  extern __shared__ __attribute__((aligned(16))) v4i lds4[];  // 2 buffers x 2 panels x PANEL
+  constexpr int NB = OT / 32;                                  // 32-feature blocks per tile side
+  constexpr int PANEL = SL * NB * 2 * 32;                      // v4i per panel
   constexpr int NEL = 2 * PANEL;
-  const int npanel = diag ? 1 : 2;
-  v4i pre[4];
-  auto fetch = [&](int kb) {
+  constexpr int PER = NEL / GEMM_NT;
+  const int per_xcd = (tiles + 7) / 8;
+  const int t = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
+  if (t >= tiles) return;
+  const int ti = list[t].x, tj = list[t].y;
+  const bool diag = ti == tj;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, bi = wv / NB, bj = wv % NB;
+  const int a0 = ti * OT + bi * 32, b0 = tj * OT + bj * 32;
+  const bool work = !diag || bi >= bj;
+  const int r = lane & 31, h = lane >> 5;
+  // Staging: element idx = threadIdx + u * GEMM_NT of the 2 panels, LDS image lane-linear
+  // ([panel][slice][block][half][feature]: idx itself), global offsets precomputed once (Dp is a
+  // multiple of OT, so every feature of every tile exists: no per-element bounds test -- the first
+  // version's per-step index arithmetic issued about as many VALU cycles as its MFMAs, r05_h2 PMC).
+  // A diagonal tile stages its one panel twice (uniform code; 1 tile in nt).
+  static_assert(NEL % GEMM_NT == 0, "staging elements must divide evenly");
+  unsigned off[PER];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int idx = threadIdx.x + u * GEMM_NT;
-      v4i v = {0, 0, 0, 0};
-      if (idx < npanel * PANEL) {
-        const int pn = idx / PANEL, rem = idx % PANEL;
-        const int hh = rem & 1, rr = (rem >> 1) & 31, blk = (rem >> 6) & 3, p = rem >> 8;
-        const int j = (pn == 0 ? ti : tj) * OT + blk * 32 + rr;
-        if (j < Dp) v = *reinterpret_cast<const v4i*>(S + (((long)p * KBC + kb) * Dp + j) * 32 + 16 * hh);
-      }
-      pre[u] = v;
-    }
+  for (int u = 0; u < PER; ++u) {
+    const int idx = threadIdx.x + u * GEMM_NT;
+    const int pn = idx / PANEL, rem = idx % PANEL;
+    const int rr = rem & 31, hh = (rem >> 5) & 1, blk = (rem >> 6) % NB, p = (rem >> 6) / NB;
+    const int j = (pn == 0 ? ti : tj) * OT + blk * 32 + rr;
+    off[u] = (unsigned)(((long)p * KBC * Dp + j) * 32 + 16 * hh);
+  }
+  v4i pre[PER];
+  auto fetch = [&](int kb) {
+    const signed char* base = S + (long)kb * Dp * 32;  // wave-uniform
+#pragma unroll
+    for (int u = 0; u < PER; ++u) pre[u] = *reinterpret_cast<const v4i*>(base + off[u]);
   };
   auto stash = [&](int buf) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int idx = threadIdx.x + u * GEMM_NT;
-      if (idx < npanel * PANEL) {
-        const int pn = idx / PANEL, rem = idx % PANEL;
-        const int hh = rem & 1, rr = (rem >> 1) & 31, blk = (rem >> 6) & 3, p = rem >> 8;
-        lds4[buf * NEL + pn * PANEL + ((p * 4 + blk) * 2 + hh) * 32 + rr] = pre[u];
-      }
-    }
+    for (int u = 0; u < PER; ++u) lds4[buf * NEL + threadIdx.x + u * GEMM_NT] = pre[u];
   };
   v16i acc[SL];
 #pragma unroll
@@ -180,27 +183,30 @@ __global__ void __launch_bounds__(GEMM_NT) oz_gemm(const signed char* S, int Dp,
   fetch(0);
   stash(0);
   __syncthreads();
-  for (int kb = 0; kb < KBC; ++kb) {
+  for (int kb = 0; kb < kbn; ++kb) {  // kbn: the chunk's 32-sample blocks (the last chunk is partial)
     const int buf = kb & 1;
-    if (kb + 1 < KBC) fetch(kb + 1);
+    if (kb + 1 < kbn) fetch(kb + 1);
     if (work) {
       const v4i* PA = lds4 + buf * NEL;
       const v4i* PB = lds4 + buf * NEL + (diag ? 0 : PANEL);
       v4i fa[SL], fb[SL];
 #pragma unroll
       for (int p = 0; p < SL; ++p) {
-        fa[p] = PA[((p * 4 + bi) * 2 + h) * 32 + r];
-        fb[p] = PB[((p * 4 + bj) * 2 + h) * 32 + r];
+        fa[p] = PA[((p * NB + bi) * 2 + h) * 32 + r];
+        fb[p] = PB[((p * NB + bj) * 2 + h) * 32 + r];
       }
+      // all 14 fragment reads in flight before the first MFMA (left alone, hipcc sinks each A read to
+      // its first use and waits lgkmcnt(0) there: seven exposed LDS round trips per step)
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int p = 0; p < SL; ++p)
 #pragma unroll
         for (int q = 0; q < SL - p; ++q)  // level p + q (digits p + 1, q + 1): sum <= SL + 1
           acc[p + q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[p], fb[q], acc[p + q], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
-    if (kb + 1 < KBC) {
-      stash(buf ^ 1);
-    }
+    if (kb + 1 < kbn) stash(buf ^ 1);
     __syncthreads();
   }
   if (!work) return;
@@ -233,40 +239,97 @@ __global__ void __launch_bounds__(256) oz_finish(const double* C, int Dp, int d,
 
 }  // namespace
 
+constexpr int OZ_SUPER = 8;  // tiles per super-block side
+
+// Device list of the nt (nt + 1) / 2 lower-triangle tiles in super-block order, built once per nt
+// (static cache; the Gram is never captured into a graph).
+const int2* oz_tile_list(int nt) {
+  static std::mutex mu;
+  static std::map<int, int2*> cache;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = cache.find(nt);
+  if (it != cache.end()) return it->second;
+  std::vector<int2> L;
+  L.reserve((size_t)nt * (nt + 1) / 2);
+  const int ns = (nt + OZ_SUPER - 1) / OZ_SUPER;
+  for (int I = 0; I < ns; ++I)
+    for (int J = 0; J <= I; ++J)
+      for (int i = I * OZ_SUPER; i < std::min((I + 1) * OZ_SUPER, nt); ++i)
+        for (int j = J * OZ_SUPER; j < std::min((J + 1) * OZ_SUPER, nt) && j <= i; ++j) L.push_back(int2{i, j});
+  int2* d = nullptr;
+  if (hipMalloc(&d, L.size() * sizeof(int2)) != hipSuccess) return nullptr;
+  if (hipMemcpy(d, L.data(), L.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess) {
+    (void)hipFree(d);
+    return nullptr;
+  }
+  cache[nt] = d;
+  return d;
+}
+
 extern "C" {
 
 // Workspace bytes of gadmm_gram_ozaki_f64 for a shard of m x d (plus y): the f64 Gram of the padded
-// augmented matrix, one chunk of digits, the column-max partials and exponents.
+// augmented matrix, two chunk buffers of digits, the column-max partials and exponents.
 long gadmm_gram_ozaki_workspace(long m, int d) {
   (void)m;
-  const long Dp = ((long)d + 1 + 31) / 32 * 32;
-  return Dp * Dp * 8 + (long)SL * KC * Dp + (long)CE_R * Dp * 8 + Dp * 4 + 256;
+  const long Dp = ((long)d + 1 + OT - 1) / OT * OT;
+  return Dp * Dp * 8 + 2L * SL * KC * Dp + (long)CE_R * Dp * 8 + Dp * 4 + 256;
 }
 
 // A_n = X_n^T X_n, b_n = X_n^T y_n, yy_n = y_n^T y_n for N shards X (N x m x d, row-major f64) on the
 // int8 matrix cores (see the file comment). Deterministic (fixed chunk order, exact int32 sums).
+// The memory-bound digit slicing of chunk c + 1 runs on a side stream into the other digit buffer
+// while the MFMA-bound oz_gemm of chunk c runs on `st` (r05_h3: slicing was 11 % of the serial time).
 int gadmm_gram_ozaki_f64(const double* X, const double* Y, int N, long m, int d, double* A, double* B, double* YY,
                          void* ws, long ws_bytes, hipStream_t st) {
   if (N <= 0 || m <= 0 || d <= 0) return 0;
-  const int Dp = (d + 1 + 31) / 32 * 32;
+  const int Dp = (d + 1 + OT - 1) / OT * OT;
   if (!X || !Y || !A || !B || !YY || !ws || ws_bytes < gadmm_gram_ozaki_workspace(m, d)) {
     gadmm_set_error("gram_ozaki: bad arguments or workspace (%ld < %ld bytes)", ws_bytes,
                     gadmm_gram_ozaki_workspace(m, d));
     return -1;
   }
+  if ((long)SL * KBC * Dp * 32 >= (1L << 32)) {
+    gadmm_set_error("gram_ozaki: d = %d exceeds the 32-bit staging offsets", d);
+    return -1;
+  }
   char* w = (char*)ws;
   double* C = (double*)w;
-  signed char* S = (signed char*)(w + (long)Dp * Dp * 8);
-  double* part = (double*)(w + (long)Dp * Dp * 8 + (long)SL * KC * Dp);
+  signed char* Sbuf[2] = {(signed char*)(w + (long)Dp * Dp * 8),
+                          (signed char*)(w + (long)Dp * Dp * 8 + (long)SL * KC * Dp)};
+  double* part = (double*)(w + (long)Dp * Dp * 8 + 2L * SL * KC * Dp);
   int* e = (int*)((char*)part + (long)CE_R * Dp * 8);
-  const int nt = (Dp + OT - 1) / OT;
+  const int nt = Dp / OT;
   const int tiles = nt * (nt + 1) / 2;
-  const size_t shm = (size_t)2 * 2 * SL * 4 * 2 * 32 * sizeof(v4i);  // 114,688 B
-  static bool attr = false;
-  if (!attr) {
-    GADMM_CHECK(hipFuncSetAttribute((const void*)oz_gemm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-    attr = true;
+  const int2* list = oz_tile_list(nt);
+  if (!list) {
+    gadmm_set_error("gram_ozaki: tile list allocation failed");
+    return -1;
   }
+  const size_t shm = (size_t)2 * 2 * SL * (OT / 32) * 2 * 32 * sizeof(v4i);  // 57,344 B: two per CU
+  // side stream + events, per device and process-wide: one caller at a time (the lock spans fork ... join)
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lock(mu);
+  int dev = 0;
+  GADMM_CHECK(hipGetDevice(&dev));
+  if (dev < 0 || dev >= 64) {
+    gadmm_set_error("gram_ozaki: device %d", dev);
+    return -1;
+  }
+  static hipStream_t side[64] = {};
+  static hipEvent_t ev[64][6] = {};  // fork, join, sliced[2], multiplied[2]
+  static bool attr[64] = {};
+  if (!side[dev]) {
+    GADMM_CHECK(hipStreamCreateWithFlags(&side[dev], hipStreamNonBlocking));
+    for (int k = 0; k < 6; ++k) GADMM_CHECK(hipEventCreateWithFlags(&ev[dev][k], hipEventDisableTiming));
+  }
+  if (!attr[dev]) {
+    GADMM_CHECK(hipFuncSetAttribute((const void*)oz_gemm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    attr[dev] = true;
+  }
+  hipStream_t s2 = side[dev];
+  hipEvent_t ev_fork = ev[dev][0], ev_join = ev[dev][1], *ev_s = &ev[dev][2], *ev_g = &ev[dev][4];
+  const int nc = (int)((m + KC - 1) / KC);
   for (int n = 0; n < N; ++n) {
     const double* Xn = X + (long)n * m * d;
     const double* Yn = Y + (long)n * m;
@@ -274,11 +337,37 @@ int gadmm_gram_ozaki_f64(const double* X, const double* Y, int N, long m, int d,
                        Dp, part);
     hipLaunchKernelGGL(oz_colexp, dim3((Dp + CE_NT - 1) / CE_NT), dim3(CE_NT), 0, st, part, Dp, e);
     GADMM_CHECK(hipMemsetAsync(C, 0, (size_t)Dp * Dp * 8, st));
-    for (long i0 = 0; i0 < m; i0 += KC) {
-      hipLaunchKernelGGL(oz_slice, dim3((Dp + SLICE_NT - 1) / SLICE_NT, KBC), dim3(SLICE_NT), 0, st, Xn, Yn, i0,
-                         (int)m, d, Dp, e, S);
-      hipLaunchKernelGGL(oz_gemm, dim3(tiles), dim3(GEMM_NT), shm, st, S, Dp, nt, e, C);
+    GADMM_CHECK(hipEventRecord(ev_fork, st));
+    hipError_t rc = hipStreamWaitEvent(s2, ev_fork, 0);
+    for (int c = -1; c < nc && rc == hipSuccess; ++c) {
+      if (c >= 0) {  // multiply chunk c (sliced on s2) on st
+        rc = hipStreamWaitEvent(st, ev_s[c & 1], 0);
+        if (rc != hipSuccess) break;
+        const int kbn = (int)((std::min<long>(KC, m - (long)c * KC) + 31) / 32);
+        hipLaunchKernelGGL(oz_gemm, dim3(8 * ((tiles + 7) / 8)), dim3(GEMM_NT), shm, st, Sbuf[c & 1], Dp, tiles,
+                           list, kbn, e, C);
+        rc = hipGetLastError();
+        if (rc == hipSuccess) rc = hipEventRecord(ev_g[c & 1], st);
+        if (rc != hipSuccess) break;
+      }
+      if (c + 1 < nc) {  // slice chunk c + 1 on s2 once chunk c - 1 (same buffer) is multiplied
+        const int b = (c + 1) & 1;
+        if (c >= 1) rc = hipStreamWaitEvent(s2, ev_g[b], 0);
+        if (rc != hipSuccess) break;
+        hipLaunchKernelGGL(oz_slice, dim3((Dp + SLICE_NT - 1) / SLICE_NT, KBC), dim3(SLICE_NT), 0, s2, Xn, Yn,
+                           (long)(c + 1) * KC, (int)m, d, Dp, e, Sbuf[b]);
+        rc = hipGetLastError();
+        if (rc == hipSuccess) rc = hipEventRecord(ev_s[b], s2);
+      }
     }
+    // join on every path: the caller frees the workspace once `st` is done
+    const hipError_t j1 = hipEventRecord(ev_join, s2);
+    const hipError_t j2 = j1 == hipSuccess ? hipStreamWaitEvent(st, ev_join, 0) : j1;
+    if (rc != hipSuccess) {
+      gadmm_set_error("gram_ozaki: %s", hipGetErrorString(rc));
+      return (int)rc;
+    }
+    GADMM_CHECK(j2);
     const long tot = (long)d * d + d + 1;
     hipLaunchKernelGGL(oz_finish, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, C, Dp, d,
                        A + (long)n * d * d, B + (long)n * d, YY + n);
