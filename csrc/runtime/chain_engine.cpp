@@ -269,6 +269,50 @@ int gadmm_memcpy_h2d_async(void* dst, const void* src, size_t bytes, hipStream_t
   return 0;
 }
 
+extern "C" int gadmm_epoch_tables_blocked(const long long* P, int E, int n, int* slots, int* pos, int* flush);
+
+// The blocked kernel's D-GADMM launch tables in one call (one GPU): checks the epoch starts (the first
+// at start_iter, at or before it for a continuation; strictly increasing), writes [starts | slots |
+// pos | flush] (gadmm_epoch_tables_blocked) straight into the pinned staging buffer `stage` and queues
+// its copy to `dstage` on `st`. Replaces ~10 numpy steps per launch on the host path before the
+// kernel (round 5: rp:args -> rp:tables). Returns the int32 words staged, or < 0 on an error.
+long gadmm_epoch_stage_blocked(const long long* starts, const long long* P, int E, int n, int start_iter, int cont,
+                               int* stage, long cap, void* dstage, hipStream_t st) {
+  if (E < 1 || n < 1 || !starts || !P || !stage || !dstage) {
+    gadmm_set_error("epoch_stage_blocked: bad arguments");
+    return -1;
+  }
+  if (cont ? starts[0] > start_iter : starts[0] != start_iter) {
+    gadmm_set_error("epochs must start at start_iter (continuations: at or before it)");
+    return -1;
+  }
+  for (int e = 1; e < E; ++e)
+    if (starts[e] <= starts[e - 1]) {
+      gadmm_set_error("epoch starts must increase");
+      return -1;
+    }
+  const long total = (long)E + (long)E * n * 7;  // starts, slots (4), pos (1), flush (2)
+  if (total > cap) {
+    gadmm_set_error("epoch_stage_blocked: staging buffer holds %ld words, %ld needed", cap, total);
+    return -1;
+  }
+  for (int e = 0; e < E; ++e) stage[e] = (int)starts[e];
+  int* slots = stage + E;
+  int* pos = slots + (long)E * n * 4;
+  int* flush = pos + (long)E * n;
+  const int rc = gadmm_epoch_tables_blocked(P, E, n, slots, pos, flush);
+  if (rc != 0) {
+    gadmm_set_error("epoch tables: every chain must be a permutation (rc %d)", rc);
+    return -2;
+  }
+  const hipError_t ce = hipMemcpyAsync(dstage, stage, (size_t)total * 4, hipMemcpyHostToDevice, st);
+  if (ce != hipSuccess) {  // negative: the return value is otherwise a word count
+    gadmm_set_error("epoch_stage_blocked: hipMemcpyAsync -> %s", hipGetErrorString(ce));
+    return -3;
+  }
+  return total;
+}
+
 // Device -> host copy queued on `st` (a persistent solve's read-back block into its pinned buffer).
 int gadmm_memcpy_d2h_async(void* dst, const void* src, size_t bytes, hipStream_t st) {
   GADMM_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));

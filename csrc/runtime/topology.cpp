@@ -6,8 +6,12 @@
 // of milliseconds of numpy dispatch. Bit-identical to PathSchedule.prefetch_arrays' numpy path: no
 // FMA contraction, the same operation order ((dx*dx) + (dy*dy); ((d2*eta)*bw)*f for energies).
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
 #include <cstdlib>
 #include <limits>
+#include <mutex>
 #include <thread>
 #include <vector>
 
@@ -176,4 +180,182 @@ extern "C" int gadmm_epoch_tables(const long long* P, int E, int n, const long l
     }
   }
   return 0;
+}
+
+// numpy's PCG64 (XSL-RR output of a 128-bit LCG; Generator.random() = (next64 >> 11) * 2^-53), so the
+// node geometries of a seeded D-GADMM schedule can be drawn here, bit for bit, from a state the caller
+// hands over (the numpy Generator is then advanced by the same count, or not materialised at all).
+namespace {
+typedef unsigned __int128 u128;
+constexpr u128 PCG_MULT = ((u128)0x2360ED051FC65DA4ULL << 64) | (u128)0x4385DF649FCCF645ULL;
+
+inline u128 pcg_advance(u128 state, u128 inc, unsigned long long delta) {
+  u128 acc_mult = 1, acc_plus = 0, cur_mult = PCG_MULT, cur_plus = inc;
+  while (delta > 0) {
+    if (delta & 1) {
+      acc_mult *= cur_mult;
+      acc_plus = acc_plus * cur_mult + cur_plus;
+    }
+    cur_plus = (cur_mult + 1) * cur_plus;
+    cur_mult *= cur_mult;
+    delta >>= 1;
+  }
+  return acc_mult * state + acc_plus;
+}
+
+inline void pcg_uniform(u128& state, u128 inc, long count, double* out) {
+  for (long i = 0; i < count; ++i) {
+    state = state * PCG_MULT + inc;
+    const unsigned long long x = (unsigned long long)(state >> 64) ^ (unsigned long long)state;
+    const unsigned rot = (unsigned)(state >> 122);
+    const unsigned long long r = (x >> rot) | (x << ((64 - rot) & 63));
+    out[i] = (double)(r >> 11) * (1.0 / 9007199254740992.0);
+  }
+}
+}  // namespace
+
+// `count` doubles of numpy's PCG64 Generator.random() from the state (s_hi:s_lo, increment i_hi:i_lo)
+// advanced by `ahead` outputs first.
+extern "C" int gadmm_pcg64_uniform(unsigned long long s_hi, unsigned long long s_lo, unsigned long long i_hi,
+                                   unsigned long long i_lo, unsigned long long ahead, long count, double* out) {
+  if (count < 0 || (count > 0 && !out)) return -1;
+  const u128 inc = ((u128)i_hi << 64) | i_lo;
+  u128 st = pcg_advance(((u128)s_hi << 64) | s_lo, inc, ahead);
+  pcg_uniform(st, inc, count, out);
+  return 0;
+}
+
+// Asynchronous greedy chains: one process-wide host worker thread runs gadmm_greedy_chains on a batch
+// while the caller keeps going (a D-GADMM solve draws its first launch's chains at the top of the
+// solve and joins them just before it builds the epoch tables: the greedy walks overlap the engine
+// refresh / reset / schedule set-up on the Python side instead of preceding the launch). One job at a
+// time: a submit while a job is pending first waits for it. The caller keeps uv / paths / costs alive
+// until gadmm_greedy_chains_wait returns.
+// Hand-offs are lock-free spins on an atomic state (a futex wake and a condition-variable round trip
+// cost tens of us on the sandboxed hosts measured, more than the walks themselves); the worker spins
+// for at most SPIN_NS after a job and then sleeps on the condition variable until the next submit.
+namespace {
+struct GreedyJob {
+  double* uv = nullptr;  // drawn first by the worker when rng is set
+  int E = 0, n = 0, energy = 0, rng = 0;
+  unsigned long long s_hi = 0, s_lo = 0, i_hi = 0, i_lo = 0, ahead = 0;
+  double side = 0, eta = 0, bw = 0, f = 0;
+  long long* paths = nullptr;
+  double* costs = nullptr;
+  int rc = 0;
+};
+enum { G_IDLE = 0, G_PENDING = 1, G_RUNNING = 2 };
+constexpr long long SPIN_NS = 3000000;  // 3 ms: covers back-to-back solves, then the worker sleeps
+
+// Heap-allocated and never destroyed: a static condition variable would be destroyed at process exit
+// while the detached worker still waits on it (glibc's pthread_cond_destroy then blocks the exit).
+struct GreedyPool {
+  std::mutex mu;
+  std::condition_variable cv;
+  GreedyJob job;
+  std::atomic<int> state{G_IDLE};
+  std::atomic<bool> sleeping{false};
+  std::once_flag started;
+};
+GreedyPool& pool() {
+  static GreedyPool* p = new GreedyPool();
+  return *p;
+}
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
+
+void greedy_worker() {
+  GreedyPool& P = pool();
+  for (;;) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (unsigned k = 1; P.state.load(std::memory_order_acquire) != G_PENDING; ++k) {
+      cpu_relax();
+      if ((k & 1023) == 0 && std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                 std::chrono::steady_clock::now() - t0).count() > SPIN_NS) {
+        std::unique_lock<std::mutex> lk(P.mu);
+        P.sleeping.store(true);  // seq_cst: ordered against the submitter's state store / sleeping load
+        P.cv.wait(lk, [&] { return P.state.load() == G_PENDING; });
+        P.sleeping.store(false);
+        break;
+      }
+    }
+    P.state.store(G_RUNNING, std::memory_order_relaxed);
+    const GreedyJob& j = P.job;
+    int rc = 0;
+    if (j.rng) rc = gadmm_pcg64_uniform(j.s_hi, j.s_lo, j.i_hi, j.i_lo, j.ahead, (long)j.E * j.n * 2, j.uv);
+    if (rc == 0) rc = gadmm_greedy_chains(j.uv, j.E, j.n, j.side, j.energy, j.eta, j.bw, j.f, j.paths, j.costs);
+    P.job.rc = rc;
+    P.state.store(G_IDLE, std::memory_order_release);
+  }
+}
+
+void wait_idle(GreedyPool& P) {
+  while (P.state.load(std::memory_order_acquire) != G_IDLE) cpu_relax();
+}
+}  // namespace
+
+namespace {
+int submit(const GreedyJob& nj) {
+  GreedyPool& P = pool();
+  std::call_once(P.started, [] { std::thread(greedy_worker).detach(); });  // lives for the process
+  wait_idle(P);
+  P.job = nj;
+  P.state.store(G_PENDING);  // seq_cst (see the worker's sleeping store)
+  if (P.sleeping.load()) {
+    std::lock_guard<std::mutex> lk(P.mu);
+    P.cv.notify_one();
+  }
+  return 0;
+}
+}  // namespace
+
+extern "C" int gadmm_greedy_chains_async(const double* uv, int E, int n, double side, int energy, double eta,
+                                         double bw, double f, long long* paths, double* costs) {
+  if (E < 0 || n < 1 || !uv || !paths || (n > 1 && !costs)) return -1;
+  GreedyJob j;
+  j.uv = const_cast<double*>(uv);
+  j.E = E;
+  j.n = n;
+  j.side = side;
+  j.energy = energy;
+  j.eta = eta;
+  j.bw = bw;
+  j.f = f;
+  j.paths = paths;
+  j.costs = costs;
+  return submit(j);
+}
+
+// The same, with the node geometries drawn by the worker too: uv (E x n x 2, written) from numpy's PCG64
+// state (s_hi:s_lo, inc i_hi:i_lo) advanced by `ahead` outputs -- exactly Generator.random((E, n, 2)).
+extern "C" int gadmm_draw_chains_async(unsigned long long s_hi, unsigned long long s_lo, unsigned long long i_hi,
+                                       unsigned long long i_lo, unsigned long long ahead, double* uv, int E, int n,
+                                       double side, int energy, double eta, double bw, double f, long long* paths,
+                                       double* costs) {
+  if (E < 0 || n < 1 || !uv || !paths || (n > 1 && !costs)) return -1;
+  GreedyJob j;
+  j.uv = uv;
+  j.E = E;
+  j.n = n;
+  j.side = side;
+  j.energy = energy;
+  j.eta = eta;
+  j.bw = bw;
+  j.f = f;
+  j.paths = paths;
+  j.costs = costs;
+  j.rng = 1;
+  j.s_hi = s_hi;
+  j.s_lo = s_lo;
+  j.i_hi = i_hi;
+  j.i_lo = i_lo;
+  j.ahead = ahead;
+  return submit(j);
+}
+
+// Waits for the job of the last gadmm_greedy_chains_async; its return code (0 when none is pending).
+extern "C" int gadmm_greedy_chains_wait() {
+  GreedyPool& P = pool();
+  wait_idle(P);
+  return P.job.rc;
 }

@@ -32,6 +32,7 @@ from ..parallel.topology import rechain_iterations, PathSchedule, Placement, cha
 from .base import global_objective_and_residual, RunResult, Stopper, total_bytes, global_objective, run_bytes
 from ..utils import timing as _timing
 from ..utils.timing import roctx_range
+from ..utils.env import getenv
 
 
 def _gather_rows(theta: torch.Tensor, ids: List[int]) -> torch.Tensor:
@@ -61,11 +62,10 @@ def chain_admm(model, local_ids: Sequence[int], n_total: int, rho: float, obj0: 
     dual is handed to a surviving chain neighbour (keeping sum(mu) = 0, the consensus-dual
     invariant) and the stopping target becomes the survivors' optimum (linear models; natively on
     one rank with a static chain, ``_chain_admm_native_elastic``; torch path otherwise)."""
-    import os
 
     comm = comm if comm is not None else LocalComm()
     if check_exchange is None:
-        check_exchange = os.environ.get("GADMM_CHECK_EXCHANGE", "0") == "1"
+        check_exchange = getenv("GADMM_CHECK_EXCHANGE", "0") == "1"
     placement = placement if placement is not None else Placement.contiguous(n_total, comm.nranks)
     if schedule is None:
         p0 = list(path) if path is not None else list(range(n_total))
@@ -243,6 +243,33 @@ def _rechains(max_iter: int, coherence) -> np.ndarray:
     return r
 
 
+def _dyn_early_draw(eng, schedule, max_iter, fabric, n_total):
+    """``(saved schedule state, epochs drawn, join)`` for the first D-GADMM launch's chains started
+    asynchronously (PathSchedule.prefetch_async), with the chunk / look-ahead rule of the launch loop in
+    ``_chain_admm_native``; None when the dynamic persistent path or the native builder does not
+    apply."""
+    if not eng.dynamic_eligible(fabric):
+        return None
+    rechains = _rechains(max_iter, schedule.coherence)
+    if len(rechains) >= (1 << 20):
+        return None
+    hints = eng.__dict__.get("_dyn_epoch_hint", {})
+    hk = (float(schedule.coherence), schedule.kind, int(max_iter), int(n_total))
+    chunk = max(16, int(hints[hk]) + 8) if hk in hints else 128
+    if eng.dynamic_uses_blocked(fabric, schedule.coherence):
+        chunk = min(chunk, int(eng.lib.gadmm_chain_blocked_max_epochs()) - 1)
+    E_total = 1 + len(rechains)
+    e1 = min(chunk, E_total)
+    look = e1 if e1 < E_total else e1 - 1
+    if look <= 0:
+        return None
+    saved = schedule.save()
+    join = schedule.prefetch_async(look)
+    if join is None:
+        return None
+    return saved, look, join
+
+
 def _static_schedule(schedule, max_iter) -> bool:
     return not schedule.coherence or not np.isfinite(schedule.coherence) or schedule.coherence <= 0 \
         or schedule.coherence >= max_iter + 1
@@ -285,6 +312,15 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     if eng is None and refresh:
         from ..ops.linalg import gram
         gram(model.X, model.y, out=(model.A, model.b, model.yy))  # the new engine inverts the fresh Gram
+    # D-GADMM on a cached engine: the first launch's chains start drawing now (geometries from the
+    # schedule's RNG here, greedy walks on the native host worker) and are joined where the launch's
+    # tables are built, so the walks overlap the refresh / set_path / reset below
+    early = None
+    if eng is not None and state is None and not _static_schedule(schedule, max_iter) \
+            and opts.get("persistent", "auto") in (True, "auto") and "epoch_chunk" not in opts \
+            and getenv("GADMM_DGADMM_EARLY", "1") != "0":
+        early = _dyn_early_draw(eng, schedule, max_iter, fabric, n_total)
+        _timing.host_stamp("native:early_draw")
     if eng is not None and refresh:
         eng.refresh(model.X, model.y)  # in place on the engine's stream (Gram, then inverses)
     if eng is None:
@@ -385,7 +421,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         use_blk = eng.dynamic_uses_blocked(fabric, schedule.coherence)
         cap = int(eng.lib.gadmm_chain_blocked_max_epochs()) - 1 if use_blk else 1 << 30
         chunk = min(chunk, cap)
-        saved = schedule.save()
+        saved = early[0] if early is not None else schedule.save()
         E_total = 1 + len(rechains)
         # epoch e's chain is row e of one (E_total, N) table, filled as chains are drawn (epoch 0: the
         # initial chain); epoch e starts at iteration ep_start[e]
@@ -395,8 +431,22 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         drawn_C = []
         n_drawn = [1]
 
+        pend = [early]
+
         def ensure(upto):  # epochs 0..upto drawn
             need = upto + 1 - n_drawn[0]
+            if pend[0] is not None:  # the early draw covers epochs 1..early[1]
+                e_ = pend[0]
+                pend[0] = None
+                if n_drawn[0] == 1 and need >= e_[1]:
+                    Pn_, Cn_ = e_[2]()
+                    Pall[1:1 + e_[1]] = Pn_
+                    n_drawn[0] += e_[1]
+                    drawn_C.append(Cn_)
+                    need -= e_[1]
+                else:  # not this shape (cannot happen: same chunk rule); the schedule restarts from it
+                    e_[2]()
+                    schedule.restore(e_[0])
             if need > 0:
                 Pn_, Cn_ = schedule.prefetch_arrays(need)
                 Pall[n_drawn[0]:n_drawn[0] + need] = Pn_
@@ -488,6 +538,9 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     else:
         # D-GADMM: run epoch by epoch; at a re-chain iteration flush the heads' pending duals with the
         # old chain, install the new chain, continue. Every rank draws the same chain sequence.
+        if early is not None:  # (not reached with an early draw: it requires the dynamic path) undo it
+            early[2]()
+            schedule.restore(early[0])
         engine_kind = "epochs"
         it = 1
         done = 0
@@ -516,7 +569,8 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
                 eng.exchange("tail")  # refresh ghost rows of the new cross-rank neighbours
             it = nxt
     _timing.host_stamp("native:solved")
-    eng.stream.synchronize()  # every engine path has synchronised its stream already: cheap
+    if engine_kind not in ("persistent", "persistent-dynamic"):  # those synchronised after their launch
+        eng.stream.synchronize()
     wall = time.perf_counter() - t0
     tr, tt = eng.traces(iters)
     if start > 1:  # a resumed solve reports iterations start..iters (as the torch path does)

@@ -26,7 +26,6 @@ Identity chain (the static GADMM of the headline benchmark).
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import List, Optional, Tuple
 
 import torch
@@ -36,6 +35,7 @@ from ..ops import native
 from ..ops.linalg import gram, spd_inverse
 from ..parallel.topology import Placement
 from ..parallel.xgmi import _Buf, device_identity, preflight
+from ..utils.env import getenv
 
 
 MAXW = 12  # waves (computed positions) per workgroup of chain_blocked_kernel
@@ -137,7 +137,7 @@ class BlockedXgmiEngine:
         self.ext_lo, self.ext_hi = comp[rank]
         self.halo = []  # data-local halo mode: the other ranks' boundary heads this rank solves too
         if self.data_local:
-            ok_h = (dl_halo is not False and os.environ.get("GADMM_DL_HALO", "1") != "0"
+            ok_h = (dl_halo is not False and getenv("GADMM_DL_HALO", "1") != "0"
                     and self.L >= self.seg_hi - self.seg_lo + 1 and dl_halo_eligible(segs, self.n, self.d))
             if dl_halo and not ok_h:
                 raise ValueError("data-local halo mode needs segments of >= 2 positions that fit one workgroup "
@@ -147,7 +147,7 @@ class BlockedXgmiEngine:
                 X_all, y_all = self._fetch_halo_shards(X_all, y_all, group)
         # stop-decision lag in iterations (GADMM_DL_LAG: A/B of the objective -> monitor -> decision
         # pipeline's slack; every rank must use the same value)
-        self.LAG = int(os.environ.get("GADMM_DL_LAG", str(self.LAG)))
+        self.LAG = int(getenv("GADMM_DL_LAG", str(self.LAG)))
         self.ring = self.LAG + 4
         torch.cuda.set_device(device)
         f64 = torch.float64

@@ -15,7 +15,6 @@ The iteration loop itself runs in C++ (graph-captured kernels + RCCL), so a solv
 from __future__ import annotations
 
 import ctypes
-import os
 from dataclasses import dataclass
 from typing import List, Optional, Sequence
 
@@ -26,6 +25,7 @@ from ..ops import native
 from ..utils import timing as _timing
 from ..ops.linalg import gram, spd_inverse, sym_pack
 from ..parallel.topology import Placement, chain_plan, RankPlan
+from ..utils.env import getenv
 
 
 class ResidencyError(RuntimeError):
@@ -226,7 +226,7 @@ class NativeChainEngine:
             if d > 256:
                 stride = int(native.require().gadmm_chain_big_rbuf_stride(d))
                 self.rbuf = torch.zeros((max(nl, 1) * stride,), dtype=f64, device=dev)
-            elif local_solver == "newton" and os.environ.get("GADMM_NEWTON_TL") == "1":
+            elif local_solver == "newton" and getenv("GADMM_NEWTON_TL") == "1":
                 # instrumented Newton kernel: s_memrealtime stamps [n_local][50 steps][5] (tools/newton_stats.py)
                 self.rbuf = torch.zeros((max(nl, 1) * 50 * 5,), dtype=torch.int64, device=dev)
             if model == "linear":
@@ -506,7 +506,7 @@ class NativeChainEngine:
         (occupancy x CUs, ``GADMM_CU_BUDGET`` shrinks the CU count): a persistent launch needs all of
         them together, so eligibility is decided here, up front, not by a spin deadline."""
         # memoised per (mode, the env switches the launcher reads): a D-GADMM solve asks on every call
-        key = (bool(dynamic), bool(sys_scope), os.environ.get("GADMM_CU_BUDGET"), os.environ.get("GADMM_PERSIST_LDS"))
+        key = (bool(dynamic), bool(sys_scope), getenv("GADMM_CU_BUDGET"), getenv("GADMM_PERSIST_LDS"))
         memo = self.__dict__.setdefault("_cap_memo", {})
         if key not in memo:
             pa = native.PersistArgs()
@@ -541,7 +541,7 @@ class NativeChainEngine:
             pa.d, pa.n, pa.sys_scope = self.d, self.n_total, 1 if fabric is not None else 0
             g = self._logi_args()
             if self.local_solver == "newton":
-                if os.environ.get("GADMM_NEWTON_PERSISTENT", "1") == "0":
+                if getenv("GADMM_NEWTON_PERSISTENT", "1") == "0":
                     return False
                 cap = int(self.lib.gadmm_chain_persistent_newton_capacity(ctypes.byref(pa), ctypes.byref(g)))
             else:
@@ -549,15 +549,25 @@ class NativeChainEngine:
             return self.n_local + 1 <= cap
         if self.model != "linear":
             return False
-        if int(self.lib.gadmm_chain_persistent_lds(self.d, self._obj_mode())) <= 0:
+        if self._lds_need(False, self._obj_mode()) <= 0:
             return False
         return self.n_local + 1 <= self.resident_capacity(sys_scope=fabric is not None)
 
+    def _lds_need(self, dynamic: bool, obj_mode: int) -> int:
+        """LDS bytes of the per-worker persistent kernel (gadmm_chain_persistent_lds[_dyn]; <= 0: does
+        not fit), memoised: a pure function of (d, nvar, mode), asked several times per solve."""
+        memo = self.__dict__.setdefault("_lds_memo", {})
+        key = (bool(dynamic), int(obj_mode))
+        v = memo.get(key)
+        if v is None:
+            v = int(self.lib.gadmm_chain_persistent_lds_dyn(self.d, obj_mode, self.nvar) if dynamic
+                    else self.lib.gadmm_chain_persistent_lds(self.d, obj_mode))
+            memo[key] = v
+        return v
+
     def _obj_mode(self, dynamic: bool = False) -> int:
         # exact objective (second GEMV with the Gram in LDS) whenever both matrices fit in LDS
-        if dynamic:
-            return 0 if int(self.lib.gadmm_chain_persistent_lds_dyn(self.d, 0, self.nvar)) > 0 else 1
-        return 0 if int(self.lib.gadmm_chain_persistent_lds(self.d, 0)) > 0 else 1
+        return 0 if self._lds_need(dynamic, 0) > 0 else 1
 
     # coherence (iterations per epoch) from which the blocked kernel's dynamic mode is the default:
     # measured per solve (profiles/r03_dgadmm_rechain) 1.01 vs 1.47 ms at coherence 10, 0.96 vs 1.12 ms
@@ -572,7 +582,7 @@ class NativeChainEngine:
         plan = self.blocked_plan(fabric) if self.model == "linear" else None
         if plan is None or plan[3] != 1 or self.n_local != self.n_total:
             return False
-        env = os.environ.get("GADMM_BLOCKED_DYN", "")
+        env = getenv("GADMM_BLOCKED_DYN", "")
         if env in ("0", "1"):
             return env == "1"
         return coherence is not None and float(coherence) >= self.BLOCKED_DYN_MIN_COHERENCE
@@ -586,7 +596,7 @@ class NativeChainEngine:
             return False
         if self.nranks == 1 and self.n_local != self.n_total:
             return False
-        if int(self.lib.gadmm_chain_persistent_lds_dyn(self.d, self._obj_mode(True), self.nvar)) <= 0:
+        if self._lds_need(True, self._obj_mode(True)) <= 0:
             return False
         return self.n_local + 1 <= self.resident_capacity(dynamic=True, sys_scope=fabric is not None)
 
@@ -594,15 +604,15 @@ class NativeChainEngine:
         """(k, L, W, pw) of the temporally blocked kernel for this engine, or None (multi-GPU, d > 64,
         GADMM_BLOCKED=0). pw = positions per wave: 1 = the 12-wave kernel (default, also the only
         instrumented one, so ``timeline`` selects it), 2 = the paired 8-wave kernel (GADMM_BLOCK_PW=2)."""
-        if fabric is not None or self.nranks > 1 or self.d > 64 or os.environ.get("GADMM_BLOCKED", "1") == "0":
+        if fabric is not None or self.nranks > 1 or self.d > 64 or getenv("GADMM_BLOCKED", "1") == "0":
             return None
         # memoised per (timeline, the env switches the planner reads)
-        key = (bool(timeline), os.environ.get("GADMM_BLOCK_K"), os.environ.get("GADMM_BLOCK_L"),
-               os.environ.get("GADMM_BLOCK_PW"), os.environ.get("GADMM_CU_BUDGET"))
+        key = (bool(timeline), getenv("GADMM_BLOCK_K"), getenv("GADMM_BLOCK_L"),
+               getenv("GADMM_BLOCK_PW"), getenv("GADMM_CU_BUDGET"))
         memo = self.__dict__.setdefault("_plan2_memo", {})
         if key not in memo:
             kk, ll, pp = ctypes.c_int(0), ctypes.c_int(0), ctypes.c_int(0)
-            want = int(os.environ.get("GADMM_BLOCK_K", "0"))
+            want = int(getenv("GADMM_BLOCK_K", "0"))
             W = int(self.lib.gadmm_chain_blocked_plan2(self.n_total, self.d, want, 1 if timeline else 0,
                                                        ctypes.byref(kk), ctypes.byref(ll), ctypes.byref(pp)))
             memo[key] = (kk.value, ll.value, W, pp.value) if W > 0 else None
@@ -736,7 +746,35 @@ class NativeChainEngine:
             pa.xchk, pa.xcd = self._xchk.data_ptr(), int(self.xcd)
         pa.hard_stop, pa.cont = int(hard_stop), 1 if cont else 0
         _timing.host_stamp("rp:args")
-        if epochs is not None:
+        fused = epochs is not None and plan is not None and fabric is None and isinstance(epochs, tuple) \
+            and len(epochs) == 2 and isinstance(epochs[1], np.ndarray) and isinstance(epochs[0], np.ndarray) \
+            and epochs[0].dtype == np.int64 and epochs[1].dtype == np.int64 and epochs[1].flags.c_contiguous \
+            and epochs[0].flags.c_contiguous
+        if fused:
+            # blocked kernel on one GPU: checks, tables, staging and the H2D copy in one native call
+            # (gadmm_epoch_stage_blocked), the layout of the general path below with no push masks
+            starts, P = epochs
+            E, n = P.shape
+            total = E + 7 * E * n
+            stage = getattr(self, "_ep_stage", None)
+            if stage is None or stage[0].numel() < total:
+                cap = max(total, 4096)
+                h_t = torch.empty((cap,), dtype=torch.int32, pin_memory=True)
+                d_t = torch.empty((cap,), dtype=torch.int32, device=dev)
+                stage = (h_t, d_t, h_t.numpy(), h_t.data_ptr(), d_t.data_ptr())
+                self._ep_stage = stage
+            if len(starts) != E:
+                raise ValueError("epochs: one chain per start")
+            got = int(self.lib.gadmm_epoch_stage_blocked(starts.ctypes.data, P.ctypes.data, E, n, int(start_iter),
+                                                         1 if cont else 0, stage[3], stage[0].numel(), stage[4],
+                                                         self.stream.cuda_stream))
+            if got < 0:
+                raise ValueError(self.lib.gadmm_last_error().decode())
+            dptr = stage[4]
+            pa.n_epochs = E
+            pa.epoch_start, pa.ep_slots = dptr, dptr + 4 * E
+            pa.ep_pos, pa.ep_flush = dptr + 4 * (E + 4 * E * n), dptr + 4 * (E + 5 * E * n)
+        elif epochs is not None:
             if isinstance(epochs, tuple) and len(epochs) == 2 and isinstance(epochs[1], np.ndarray):
                 starts = np.asarray(epochs[0], dtype=np.int64)                      # (starts, paths) arrays
                 P = np.asarray(epochs[1], dtype=np.int64)
@@ -886,6 +924,7 @@ class NativeChainEngine:
         fetch = fetch_trace and nt <= 16384
         if getattr(self, "_rb_host", None) is None:
             self._rb_host = torch.empty(self._rb.shape, dtype=torch.float64, pin_memory=True)
+            self._rb_host_np = self._rb_host.numpy()
             self._ctl_host = self._rb_host[0:4].view(torch.int32)
         # native async copy on the engine stream (every launch above names that stream explicitly, so no
         # torch stream context is needed around this block)
@@ -938,7 +977,7 @@ class NativeChainEngine:
         if upto <= 0:
             return np.zeros((0,), dtype=np.float64), np.zeros((0,), dtype=np.float64)
         if getattr(self, "_tr_valid", False) and upto <= self.trace.numel():  # pinned copy of the last persistent run
-            h = self._rb_host.numpy()
+            h = self._rb_host_np
             nt = self.trace.numel()
             t = h[8 + nt:8 + nt + upto].view(np.int64)
             t0 = int(h[4:5].view(np.int64)[0])

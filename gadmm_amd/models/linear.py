@@ -7,12 +7,12 @@ per-iteration quantities are O(d^2) in these, independent of the shard height m.
 """
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
 
 from ..ops.linalg import gram, spd_inverse, spd_inverse_blocked
+from ..utils.env import getenv
 
 
 def _cg_solve(M: torch.Tensor, r: torch.Tensor, tol: float = 1e-13, maxit: int = 96, check: int = 8):
@@ -117,9 +117,9 @@ def _cg_solve_native(M: torch.Tensor, r: torch.Tensor, tol: float, maxit: int, c
 def _distributed_cg_ok(model) -> bool:
     """The large-d optimum runs the distributed CG (d-vector all-reduces) on HIP devices with d > 256
     (GADMM_OPT_DIST=0: the one-time d x d Gram all-reduce instead)."""
-    return (model.A.is_cuda and model.d > 256 and os.environ.get("GADMM_OPT_DIST", "1") != "0"
-            and os.environ.get("GADMM_OPT_SOLVER", "native") != "rocsolver"
-            and os.environ.get("GADMM_OPT_CG", "1") != "0")
+    return (model.A.is_cuda and model.d > 256 and getenv("GADMM_OPT_DIST", "1") != "0"
+            and getenv("GADMM_OPT_SOLVER", "native") != "rocsolver"
+            and getenv("GADMM_OPT_CG", "1") != "0")
 
 
 def _resid_sq(X: torch.Tensor, y: torch.Tensor, x: torch.Tensor) -> torch.Tensor:
@@ -149,8 +149,8 @@ def _spd_solve(M: torch.Tensor, r: torch.Tensor) -> torch.Tensor:
     csrc/kernels/spd_inverse_blocked.hip, ~50 ms at d = 10k) and one GEMV. rocSOLVER's potrf / trsv
     spent ~0.3 s there, mostly first-call library loading between their kernels, and was not
     deterministic with ranks sharing a GPU (profiles/r04_real10m)."""
-    native_ok = os.environ.get("GADMM_OPT_SOLVER", "native") != "rocsolver"
-    if M.is_cuda and M.shape[-1] > 256 and native_ok and os.environ.get("GADMM_OPT_CG", "1") != "0":
+    native_ok = getenv("GADMM_OPT_SOLVER", "native") != "rocsolver"
+    if M.is_cuda and M.shape[-1] > 256 and native_ok and getenv("GADMM_OPT_CG", "1") != "0":
         x = _cg_solve(M, r)
         if x is not None:
             return x

@@ -13,12 +13,12 @@ torch, which is also the fp64 reference the kernels are tested against.
 from __future__ import annotations
 
 import ctypes
-import os
 from typing import Optional, Tuple
 
 import torch
 
 from . import native
+from ..utils.env import getenv
 
 
 def gram_torch(X: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
@@ -65,7 +65,7 @@ def gram_uses_ozaki(m: int, d: int) -> bool:
     d >= 3072 features and m >= 65536 samples, where it measured faster than the f64-MFMA Gram (1.11x at
     100k x 4096, 1.10x at 312k x 10k; real10m 2.11 -> 1.92 s at the same 25 iterations: profiles/r05_h);
     ``1`` for every d > 256; ``0`` never."""
-    mode = os.environ.get("GADMM_GRAM_OZAKI", "auto")
+    mode = getenv("GADMM_GRAM_OZAKI", "auto")
     if mode == "0":
         return False
     if mode == "1":
@@ -130,7 +130,7 @@ def spd_inverse(A: torch.Tensor, shifts: torch.Tensor, out: Optional[torch.Tenso
         shifts = shifts.contiguous()
     N, d, _ = A.shape
     V = shifts.shape[1]
-    if A.is_cuda and d > 128 and os.environ.get("GADMM_BIGINV", "native") != "rocsolver":
+    if A.is_cuda and d > 128 and getenv("GADMM_BIGINV", "native") != "rocsolver":
         return spd_inverse_blocked(A, shifts, out=out, check_status=check_status, status=status)
     if not A.is_cuda or d > 128:
         res = spd_inverse_torch(A, shifts)

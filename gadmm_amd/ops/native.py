@@ -222,6 +222,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_chain_blocked_tab_granules_dyn": (c_long, [c_int, c_int, c_int]),
         "gadmm_epoch_tables": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),
         "gadmm_epoch_tables_blocked": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+        "gadmm_epoch_stage_blocked": (c_long, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_long,
+                                               c_void_p, c_void_p]),
         "gadmm_chain_blocked_launch": (c_int, [ctypes.POINTER(PersistArgs), c_void_p]),
         "gadmm_fo_lds": (c_long, [c_int, c_int, c_int, c_int, c_int]),
         "gadmm_fo_tab_granules": (c_long, [c_int, c_int, c_int]),
@@ -230,6 +232,12 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_quad_gemv_test": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
         "gadmm_greedy_chains": (c_int, [c_void_p, c_int, c_int, c_double, c_int, c_double, c_double, c_double,
                                         c_void_p, c_void_p]),
+        "gadmm_greedy_chains_async": (c_int, [c_void_p, c_int, c_int, c_double, c_int, c_double, c_double,
+                                              c_double, c_void_p, c_void_p]),
+        "gadmm_greedy_chains_wait": (c_int, []),
+        "gadmm_pcg64_uniform": (c_int, [ctypes.c_ulonglong] * 5 + [c_long, c_void_p]),
+        "gadmm_draw_chains_async": (c_int, [ctypes.c_ulonglong] * 5 + [c_void_p, c_int, c_int, c_double, c_int, c_double,
+                                                                        c_double, c_double, c_void_p, c_void_p]),
         "gadmm_rccl_unique_id": (c_int, [ctypes.c_char_p]),
         "gadmm_rccl_version": (c_int, []),
         "gadmm_rccl_init": (c_void_p, [ctypes.c_char_p, c_int, c_int, c_int]),

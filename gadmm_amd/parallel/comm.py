@@ -21,6 +21,7 @@ from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
+from ..utils.env import getenv
 
 Op = Tuple[int, int, int]  # (peer, row, is_send)
 
@@ -352,10 +353,10 @@ def init_distributed(backend: Optional[str] = None):
     """Initialise torch.distributed from torchrun-style env vars (MASTER_ADDR defaults to 127.0.0.1).
     Returns (rank, world_size, local_rank)."""
     if dist.is_initialized():
-        return dist.get_rank(), dist.get_world_size(), int(os.environ.get("LOCAL_RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", str(rank)))
+        return dist.get_rank(), dist.get_world_size(), int(getenv("LOCAL_RANK", "0"))
+    world = int(getenv("WORLD_SIZE", "1"))
+    rank = int(getenv("RANK", "0"))
+    local_rank = int(getenv("LOCAL_RANK", str(rank)))
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
     if backend is None:

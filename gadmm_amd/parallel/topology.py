@@ -17,11 +17,11 @@ Indices are 0-based throughout (reference worker ``ii`` == our worker ``ii-1``).
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
+from ..utils.env import getenv
 
 ETA = 1e-6
 RATE = 10e6
@@ -155,17 +155,29 @@ def native_greedy_chains(uv: np.ndarray, side: float, energy: bool) -> Tuple[np.
     return paths, costs
 
 
+_ASYNC_KEEP = None  # buffers of the last asynchronous greedy-chain job (PathSchedule.prefetch_async)
+_SEED_STATE: Dict[int, Tuple[int, int]] = {}  # seed -> (state, inc) of default_rng(seed)'s PCG64
+
+
+_NATIVE_CHAINS = []  # [bool]: whether the built library has the chain builder (asked once)
+
+
 def _native_chains_ok() -> bool:
     """The native chain builder is used when the library is already built (never builds it)."""
-    if os.environ.get("GADMM_NATIVE_TOPOLOGY", "1") == "0":
+    if getenv("GADMM_NATIVE_TOPOLOGY", "1") == "0":
         return False
-    try:
-        from ..ops import native
+    if not _NATIVE_CHAINS:
+        try:
+            from ..ops import native
 
-        lib = native.load(build_if_missing=False)
-        return lib is not None and getattr(lib, "gadmm_greedy_chains", None) is not None
-    except Exception:
-        return False
+            lib = native.load(build_if_missing=False)
+            ok = lib is not None and getattr(lib, "gadmm_greedy_chains", None) is not None
+        except Exception:
+            ok = False
+        if not ok:
+            return False  # not cached: a later build may provide it
+        _NATIVE_CHAINS.append(True)
+    return True
 
 
 class PathSchedule:
@@ -181,18 +193,58 @@ class PathSchedule:
         self.n = n
         self.coherence = coherence
         self.kind = kind
-        self.rng = np.random.default_rng(seed)
+        # The numpy Generator (default_rng(seed)) is built on first use: until then the stream position
+        # is (seed, outputs consumed) -- a D-GADMM solve whose chains the native worker draws from that
+        # state (prefetch_async) never needs it (building one costs ~10-20 us per solve).
+        self._seed = seed
+        self._rng = None
+        self._ahead = 0
+        if not isinstance(seed, (int, np.integer)):  # entropy / SeedSequence seeds: no lazy replay
+            self._rng = np.random.default_rng(seed)
         self.path = list(initial_path)
         self.cost = np.asarray(initial_cost, dtype=np.float64)
         self.path_matrix = path_matrix
         self.cost_matrix = cost_matrix
         self.k = 1  # next row of the matrices
 
+    @property
+    def rng(self) -> np.random.Generator:
+        if self._rng is None:
+            g = np.random.default_rng(self._seed)
+            if self._ahead:
+                g.bit_generator.advance(self._ahead)
+            self._rng = g
+        return self._rng
+
+    def _pcg_state(self):
+        """(state, inc) of the PCG64 stream at the current position, as ints; the materialised
+        Generator (if any) is NOT advanced."""
+        if self._rng is not None:
+            st = self._rng.bit_generator.state["state"]
+            return st["state"], st["inc"], 0
+        st = _SEED_STATE.get(self._seed)
+        if st is None:
+            st = np.random.default_rng(self._seed).bit_generator.state["state"]
+            st = (st["state"], st["inc"])
+            if len(_SEED_STATE) < 256:
+                _SEED_STATE[self._seed] = st
+        return st[0], st[1], self._ahead
+
+    def _consume(self, outputs: int) -> None:
+        if self._rng is None:
+            self._ahead += outputs
+        else:
+            self._rng.bit_generator.advance(outputs)
+
     def save(self):
-        return (self.rng.bit_generator.state, list(self.path), self.cost.copy(), self.k)
+        rs = ("lazy", self._ahead) if self._rng is None else self._rng.bit_generator.state
+        return (rs, list(self.path), self.cost.copy(), self.k)
 
     def restore(self, st) -> None:
-        self.rng.bit_generator.state = st[0]
+        if isinstance(st[0], tuple) and st[0][0] == "lazy":
+            self._rng, self._ahead = None, int(st[0][1])
+        else:
+            self.rng.bit_generator.state = st[0]
         self.path, self.cost, self.k = list(st[1]), st[2].copy(), st[3]
 
     def prefetch_arrays(self, count: int) -> Tuple[np.ndarray, np.ndarray]:
@@ -230,6 +282,48 @@ class PathSchedule:
         self.path, self.cost = [int(v) for v in paths[-1]], np.asarray(costs[-1], dtype=np.float64)
         return paths, costs
 
+    def prefetch_async(self, count: int):
+        """Start drawing the next ``count`` chains on the native library's host worker thread: the
+        geometries (numpy's PCG64 stream from the schedule's current position, ``gadmm_draw_chains_async``)
+        and the greedy walks. The schedule's RNG position moves past them at once. Returns a callable
+        giving ``(paths, costs)`` exactly as ``prefetch_arrays(count)`` would (the current chain moves
+        at that call), or None where the native builder does not apply (the caller draws
+        synchronously)."""
+        if count <= 0 or self.kind == "matrix" or not _native_chains_ok():
+            return None
+        from ..ops import native
+
+        lib = native.load(build_if_missing=False)
+        if getattr(lib, "gadmm_draw_chains_async", None) is None:
+            return None
+        n = self.n
+        side = 50.0 if self.kind == "findPath" else 250.0
+        state, inc, ahead = self._pcg_state()
+        uv = np.empty((count, n, 2), dtype=np.float64)
+        paths = np.empty((count, n), dtype=np.int64)
+        costs = np.empty((count, max(n - 1, 0)), dtype=np.float64)
+        global _ASYNC_KEEP
+        lib.gadmm_greedy_chains_wait()  # a previous job (never joined) is done with its buffers
+        _ASYNC_KEEP = (uv, paths, costs)  # held until the next submit: the worker writes into them
+        M = (1 << 64) - 1
+        rc = lib.gadmm_draw_chains_async(state >> 64, state & M, inc >> 64, inc & M, ahead, uv.ctypes.data, count, n,
+                                         side, int(self.kind != "findPath"), ETA, BANDWIDTH, 2.0 ** (RATE / BANDWIDTH),
+                                         paths.ctypes.data, costs.ctypes.data)
+        if rc != 0:
+            raise RuntimeError("gadmm_draw_chains_async failed")
+        self._consume(2 * n * count)
+        box = []
+
+        def join():
+            if not box:
+                if lib.gadmm_greedy_chains_wait() != 0:
+                    raise RuntimeError("gadmm_greedy_chains failed")
+                self.path, self.cost = [int(v) for v in paths[-1]], np.asarray(costs[-1], dtype=np.float64)
+                box.append((paths, costs))
+            return box[0]
+
+        return join
+
     def prefetch(self, count: int):
         """``prefetch_arrays`` as a list ``[(path, cost), ...]``."""
         paths, costs = self.prefetch_arrays(count)
@@ -245,7 +339,7 @@ class PathSchedule:
         if self.kind == "matrix":
             self.k += count
         else:
-            self.rng.bit_generator.advance(2 * self.n * count)
+            self._consume(2 * self.n * count)
         self.path, self.cost = [int(v) for v in paths[count - 1]], np.asarray(costs[count - 1], dtype=np.float64)
 
     def step(self, it: int) -> bool:

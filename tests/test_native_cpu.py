@@ -98,6 +98,51 @@ def test_native_greedy_chains_match_numpy(monkeypatch):
     assert np.array_equal(Cn, d2[ar, P[:, :-1], P[:, 1:]])
 
 
+def test_async_greedy_chains_match_sync():
+    """PathSchedule.prefetch_async (geometries from the PCG64 stream and greedy walks on the native host
+    worker thread, joined later) == prefetch_arrays: the same chains, costs, current chain and RNG
+    position, with the schedule's Generator lazy or materialised; skip() after it; a job never joined is
+    drained by the next submit (its buffers stay alive until then)."""
+    import numpy as np
+    from gadmm_amd.parallel import topology as T
+
+    native.require()
+    for kind in ("findPath2", "findPath"):
+        s1 = T.PathSchedule(24, list(range(24)), np.zeros(23), 10, kind=kind, seed=99)
+        P, C = s1.prefetch_arrays(59)
+        s2 = T.PathSchedule(24, list(range(24)), np.zeros(23), 10, kind=kind, seed=99)
+        join = s2.prefetch_async(59)
+        assert join is not None
+        assert s2.path == list(range(24))  # the current chain moves only at the join
+        P2, C2 = join()
+        assert np.array_equal(P, P2) and np.array_equal(C, C2)
+        assert join()[0] is P2  # idempotent
+        assert s1.path == s2.path and np.array_equal(s1.cost, s2.cost)
+        assert np.array_equal(s1.rng.random(3), s2.rng.random(3))
+    # with the Generator already materialised (and advanced), and after a lazy skip()
+    s6 = T.PathSchedule(24, list(range(24)), np.zeros(23), 10, seed=7)
+    s6.rng.random(5)
+    P6, C6 = s6.prefetch_async(11)()
+    s7 = T.PathSchedule(24, list(range(24)), np.zeros(23), 10, seed=7)
+    s7.rng.random(5)
+    P7, C7 = s7.prefetch_arrays(11)
+    assert np.array_equal(P6, P7) and np.array_equal(C6, C7)
+    assert np.array_equal(s6.rng.random(2), s7.rng.random(2))
+    s8 = T.PathSchedule(24, list(range(24)), np.zeros(23), 10, seed=8)
+    sv = s8.save()
+    P8, C8 = s8.prefetch_async(9)()
+    s8.skip(sv, P8, C8, 4)
+    s9 = T.PathSchedule(24, list(range(24)), np.zeros(23), 10, seed=8)
+    s9.prefetch_arrays(4)
+    assert s8.path == s9.path and np.array_equal(s8.rng.random(3), s9.rng.random(3))
+    s3 = T.PathSchedule(24, list(range(24)), np.zeros(23), 10, seed=5)
+    s3.prefetch_async(200)  # dropped without a join
+    s4 = T.PathSchedule(24, list(range(24)), np.zeros(23), 10, seed=5)
+    P4, _ = s4.prefetch_async(3)()
+    s5 = T.PathSchedule(24, list(range(24)), np.zeros(23), 10, seed=5)
+    assert np.array_equal(P4, s5.prefetch_arrays(3)[0])
+
+
 def test_native_epoch_tables_match_numpy():
     """csrc/runtime/topology.cpp:gadmm_epoch_tables == the numpy reference (engine/chain_engine.py)."""
     import numpy as np
@@ -262,3 +307,40 @@ def test_cg_entry_points_refuse_bad_arguments():
     assert lib.gadmm_cg_begin(None, None, None, None, None, 10, None) == -1
     assert lib.gadmm_cg_resid(None, None, None, 0, None) == -1
     assert b"cg_" in lib.gadmm_last_error()
+
+
+def test_epoch_stage_blocked_layout_and_checks():
+    """gadmm_epoch_stage_blocked (the D-GADMM launch's fused table staging) writes [starts | slots |
+    pos | flush] exactly as gadmm_epoch_tables_blocked builds them and refuses bad starts and
+    non-permutations before any copy (here, without a GPU, the final copy itself fails: -3)."""
+    import numpy as np
+
+    lib = native.require()
+    rng = np.random.default_rng(4)
+    E, n = 7, 24
+    P = np.ascontiguousarray(np.stack([rng.permutation(n) for _ in range(E)]).astype(np.int64))
+    starts = np.arange(1, 1 + 10 * E, 10, dtype=np.int64)
+    cap = E + 7 * E * n
+    stage = np.zeros(cap, dtype=np.int32)
+    rc = lib.gadmm_epoch_stage_blocked(starts.ctypes.data, P.ctypes.data, E, n, 1, 0, stage.ctypes.data, cap,
+                                       ctypes.c_void_p(16), None)
+    assert rc in (cap, -3)
+    es = np.empty(E * n * 4, dtype=np.int32)
+    pp = np.empty(E * n, dtype=np.int32)
+    fl = np.empty(E * n * 2, dtype=np.int32)
+    assert lib.gadmm_epoch_tables_blocked(P.ctypes.data, E, n, es.ctypes.data, pp.ctypes.data, fl.ctypes.data) == 0
+    assert np.array_equal(stage, np.concatenate([starts.astype(np.int32), es, pp, fl]))
+    bad = starts.copy()
+    bad[3] = bad[2]
+    assert lib.gadmm_epoch_stage_blocked(bad.ctypes.data, P.ctypes.data, E, n, 1, 0, stage.ctypes.data, cap,
+                                         ctypes.c_void_p(16), None) == -1
+    assert lib.gadmm_epoch_stage_blocked(starts.ctypes.data, P.ctypes.data, E, n, 2, 0, stage.ctypes.data, cap,
+                                         ctypes.c_void_p(16), None) == -1  # first start != start_iter
+    assert lib.gadmm_epoch_stage_blocked(starts.ctypes.data, P.ctypes.data, E, n, 2, 1, stage.ctypes.data, cap,
+                                         ctypes.c_void_p(16), None) in (cap, -3)  # continuation: at or before
+    assert lib.gadmm_epoch_stage_blocked(starts.ctypes.data, P.ctypes.data, E, n, 1, 0, stage.ctypes.data, cap - 1,
+                                         ctypes.c_void_p(16), None) == -1  # too small
+    P2 = P.copy()
+    P2[2, 5] = P2[2, 6]
+    assert lib.gadmm_epoch_stage_blocked(starts.ctypes.data, P2.ctypes.data, E, n, 1, 0, stage.ctypes.data, cap,
+                                         ctypes.c_void_p(16), None) == -2
