@@ -1131,7 +1131,7 @@ def test_gram_ozaki_matches_f64(N, m, d):
     """The int8-MFMA Ozaki Gram (gram_ozaki.hip: 7 round-to-nearest digits per value, exact int32 digit-pair
     products, f64 recombination) equals an f64 reference (torch's bmm): every entry within 1e-14 of
     sqrt(A_aa A_bb), b and y'y likewise; chunk boundaries (8192 samples) and padded columns included;
-    deterministic."""
+    deterministic; both GEMM variants bit-identical."""
     from gadmm_amd.ops.linalg import gram, gram_ozaki
     g = torch.Generator(device=DEV)
     g.manual_seed(N * 1000 + d)
@@ -1152,3 +1152,11 @@ def test_gram_ozaki_matches_f64(N, m, d):
     assert ea < 1e-14 and eb < 1e-14 and ey < 1e-14, (ea, eb, ey, e64)
     A2, _, _ = gram_ozaki(X, y)
     assert torch.equal(A, A2)  # deterministic
+    # the LDS-DMA one-wave-per-SIMD GEMM (GADMM_OZ_GEMM=2): the same exact int32 chunk sums and the same
+    # f64 flush order, so bit-identical
+    os.environ["GADMM_OZ_GEMM"] = "2"
+    try:
+        A3, b3, yy3 = gram_ozaki(X, y)
+    finally:
+        del os.environ["GADMM_OZ_GEMM"]
+    assert torch.equal(A, A3) and torch.equal(b, b3) and torch.equal(yy, yy3)
