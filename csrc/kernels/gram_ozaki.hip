@@ -327,6 +327,121 @@ __global__ void __launch_bounds__(G2_NT) oz_gemm2(const signed char* S, int Dp, 
   }
 }
 
+// Variant 3 (GADMM_OZ_GEMM=3): variant 2 with the fragment reads software-pipelined: step k's MFMAs run
+// on fragments read during step k - 1 (two register sets, 84 VGPRs each; the accumulators stay in
+// AGPRs), while stage k + 1 is read; the ring then holds stage k + 1 (being read), k + 2 (DMA in flight)
+// and k + 3 (issued into step k's buffer, whose reads the lgkmcnt before the barrier retired).
+struct OzFrag {
+  v4i a[SL], b[2][SL];
+};
+
+__device__ __forceinline__ void oz_read_frags(OzFrag& F, const v4i* stage, int wa, int wb, int h, int r) {
+  const v4i* PA = stage;
+  const v4i* PB = stage + G2_FRA * 64;
+#pragma unroll
+  for (int p = 0; p < SL; ++p) {
+    F.a[p] = PA[((p * 2 + wa) * 2 + h) * 32 + r];
+    F.b[0][p] = PB[((p * 4 + 2 * wb) * 2 + h) * 32 + r];
+    F.b[1][p] = PB[((p * 4 + 2 * wb + 1) * 2 + h) * 32 + r];
+  }
+}
+
+__device__ __forceinline__ void oz_mfma_frags(v16i (&acc)[2][SL], const OzFrag& F) {
+#pragma unroll
+  for (int p = 0; p < SL; ++p)
+#pragma unroll
+    for (int q = 0; q < SL - p; ++q) {
+      acc[0][p + q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(F.a[p], F.b[0][q], acc[0][p + q], 0, 0, 0);
+      acc[1][p + q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(F.a[p], F.b[1][q], acc[1][p + q], 0, 0, 0);
+    }
+}
+
+__global__ void __launch_bounds__(G2_NT) oz_gemm3(const signed char* S, int Dp, int tiles, const int2* list, int kbn,
+                                                  const int* e, double* C) {
+  extern __shared__ __attribute__((aligned(16))) v4i lds4[];  // 3 stages
+  const int per_xcd = (tiles + 7) / 8;
+  const int t = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
+  if (t >= tiles) return;
+  const int ti = list[t].x, tj = list[t].y;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wa = wv >> 1, wb = wv & 1;
+  const int a0 = ti * G2_TA + wa * 32, b0 = tj * G2_TB + wb * 64;
+  const bool work = a0 >= b0;
+  const int r = lane & 31, h = lane >> 5;
+  unsigned off[G2_DMA];
+#pragma unroll
+  for (int u = 0; u < G2_DMA; ++u) {
+    int f = wv + 4 * u;
+    if (f >= G2_FR) f -= G2_FR;
+    int p, j;
+    if (f < G2_FRA) {
+      p = f / 2;
+      j = ti * G2_TA + (f % 2) * 32 + r;
+    } else {
+      p = (f - G2_FRA) / 4;
+      j = tj * G2_TB + ((f - G2_FRA) % 4) * 32 + r;
+    }
+    off[u] = (unsigned)(((long)p * KBC * Dp + j) * 32 + 16 * h);
+  }
+  auto issue = [&](int kb) {
+    const signed char* base = S + (long)kb * Dp * 32;
+    const int st = kb % 3;
+#pragma unroll
+    for (int u = 0; u < G2_DMA; ++u) {
+      int f = wv + 4 * u;
+      if (f >= G2_FR) f -= G2_FR;
+      __builtin_amdgcn_global_load_lds(base + off[u], lds4 + st * G2_STAGE + f * 64, 16, 0, 0);
+    }
+  };
+  v16i acc[2][SL];
+#pragma unroll
+  for (int q = 0; q < 2; ++q)
+#pragma unroll
+    for (int L = 0; L < SL; ++L) acc[q][L] = v16i{};
+  for (int s = 0; s < 3 && s < kbn; ++s) issue(s);
+  // stage 0 landed (this wave: the later stages' DMAs may fly), everyone's: the barrier
+  if (kbn > 2) asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
+  else if (kbn > 1) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  OzFrag F0, F1;
+  oz_read_frags(F0, lds4, wa, wb, h, r);
+  // one step: retire stage k + 1 (+ everyone's reads of stage k), issue k + 3 into stage k's buffer,
+  // read stage k + 1 into Fn, multiply Fc
+  auto step = [&](int k, OzFrag& Fc, OzFrag& Fn) {
+    if (k + 1 < kbn) {
+      if (k + 2 < kbn) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of stage k are done
+    __builtin_amdgcn_s_barrier();
+    if (k + 3 < kbn) issue(k + 3);
+    if (k + 1 < kbn) oz_read_frags(Fn, lds4 + ((k + 1) % 3) * G2_STAGE, wa, wb, h, r);
+    __builtin_amdgcn_s_setprio(1);
+    oz_mfma_frags(acc, Fc);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  int k = 0;
+  for (; k + 1 < kbn; k += 2) {
+    step(k, F0, F1);
+    step(k + 1, F1, F0);
+  }
+  if (k < kbn) step(k, F0, F1);
+  if (!work) return;
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int col = b0 + 32 * q + r;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) {
+      const int row = a0 + (g & 3) + 8 * (g >> 2) + 4 * h;
+      double v = 0.0;
+#pragma unroll
+      for (int L = SL - 1; L >= 0; --L) v = fma((double)acc[q][L][g], ldexp(1.0, -7 * (L + 2)), v);
+      C[(long)row * Dp + col] += ldexp(v, e[row] + e[col]);
+    }
+  }
+}
+
 // C (Dp x Dp, lower triangle) -> A (d x d, full symmetric), b (d), yy
 __global__ void __launch_bounds__(256) oz_finish(const double* C, int Dp, int d, double* A, double* b, double* yy) {
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
@@ -444,8 +559,8 @@ int gadmm_gram_ozaki_f64(const double* X, const double* Y, int N, long m, int d,
   const int variant = getenv("GADMM_OZ_GEMM") ? atoi(getenv("GADMM_OZ_GEMM")) : 1;  // A/B: read per call
   const size_t shm2 = (size_t)3 * G2_STAGE * sizeof(v4i);  // 129,024 B: one per CU
   int tiles2 = 0;
-  const int2* list2 = variant == 2 ? oz_tile_list2(Dp / G2_TA, Dp / G2_TB, &tiles2) : nullptr;
-  if (variant == 2 && !list2) {
+  const int2* list2 = variant >= 2 ? oz_tile_list2(Dp / G2_TA, Dp / G2_TB, &tiles2) : nullptr;
+  if (variant >= 2 && !list2) {
     gadmm_set_error("gram_ozaki: tile list allocation failed");
     return -1;
   }
@@ -468,6 +583,7 @@ int gadmm_gram_ozaki_f64(const double* X, const double* Y, int N, long m, int d,
   if (!attr[dev]) {
     GADMM_CHECK(hipFuncSetAttribute((const void*)oz_gemm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
     GADMM_CHECK(hipFuncSetAttribute((const void*)oz_gemm2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm2));
+    GADMM_CHECK(hipFuncSetAttribute((const void*)oz_gemm3, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm2));
     attr[dev] = true;
   }
   hipStream_t s2 = side[dev];
@@ -487,7 +603,10 @@ int gadmm_gram_ozaki_f64(const double* X, const double* Y, int N, long m, int d,
         rc = hipStreamWaitEvent(st, ev_s[c & 1], 0);
         if (rc != hipSuccess) break;
         const int kbn = (int)((std::min<long>(KC, m - (long)c * KC) + 31) / 32);
-        if (variant == 2)
+        if (variant == 3)
+          hipLaunchKernelGGL(oz_gemm3, dim3(8 * ((tiles2 + 7) / 8)), dim3(G2_NT), shm2, st, Sbuf[c & 1], Dp, tiles2,
+                             list2, kbn, e, C);
+        else if (variant == 2)
           hipLaunchKernelGGL(oz_gemm2, dim3(8 * ((tiles2 + 7) / 8)), dim3(G2_NT), shm2, st, Sbuf[c & 1], Dp, tiles2,
                              list2, kbn, e, C);
         else

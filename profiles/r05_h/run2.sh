@@ -10,6 +10,8 @@ timeout -k 10 400 python tools/gram_ozaki_bench.py 1 312500 10000 2 > $O/bench_1
 timeout -k 10 200 python tools/gram_ozaki_bench.py 1 100000 4096 2 > $O/bench_4096.log 2>&1 || exit $?
 GADMM_OZ_GEMM=2 timeout -k 10 400 python tools/gram_ozaki_bench.py 1 312500 10000 2 > $O/bench2_10k.log 2>&1 || exit $?
 GADMM_OZ_GEMM=2 timeout -k 10 200 python tools/gram_ozaki_bench.py 1 100000 4096 2 > $O/bench2_4096.log 2>&1 || exit $?
+GADMM_OZ_GEMM=3 timeout -k 10 400 python tools/gram_ozaki_bench.py 1 312500 10000 2 > $O/bench3_10k.log 2>&1 || exit $?
+GADMM_OZ_GEMM=3 timeout -k 10 200 python tools/gram_ozaki_bench.py 1 100000 4096 2 > $O/bench3_4096.log 2>&1 || exit $?
 GADMM_OZ_GEMM=2 timeout -s KILL 90 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
   SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES -d $O/pmc -o pmc -- \
   python3 tools/gram_ozaki_bench.py 1 100000 4096 1 > $O/pmc.log 2>&1 || exit $?

@@ -1154,9 +1154,10 @@ def test_gram_ozaki_matches_f64(N, m, d):
     assert torch.equal(A, A2)  # deterministic
     # the LDS-DMA one-wave-per-SIMD GEMM (GADMM_OZ_GEMM=2): the same exact int32 chunk sums and the same
     # f64 flush order, so bit-identical
-    os.environ["GADMM_OZ_GEMM"] = "2"
-    try:
-        A3, b3, yy3 = gram_ozaki(X, y)
-    finally:
-        del os.environ["GADMM_OZ_GEMM"]
-    assert torch.equal(A, A3) and torch.equal(b, b3) and torch.equal(yy, yy3)
+    for variant in ("2", "3"):  # the LDS-DMA GEMMs, plain and with pipelined fragment reads
+        os.environ["GADMM_OZ_GEMM"] = variant
+        try:
+            A3, b3, yy3 = gram_ozaki(X, y)
+        finally:
+            del os.environ["GADMM_OZ_GEMM"]
+        assert torch.equal(A, A3) and torch.equal(b, b3) and torch.equal(yy, yy3), variant
