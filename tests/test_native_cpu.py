@@ -344,3 +344,16 @@ def test_epoch_stage_blocked_layout_and_checks():
     P2[2, 5] = P2[2, 6]
     assert lib.gadmm_epoch_stage_blocked(starts.ctypes.data, P2.ctypes.data, E, n, 1, 0, stage.ctypes.data, cap,
                                          ctypes.c_void_p(16), None) == -2
+
+
+def test_fast_getenv_tracks_os_environ(monkeypatch):
+    """utils.env.getenv (the hot-path switch reader) == os.environ.get under set / monkeypatch / delete."""
+    from gadmm_amd.utils.env import getenv
+    monkeypatch.delenv("GADMM_ENV_PROBE", raising=False)
+    assert getenv("GADMM_ENV_PROBE") is None and getenv("GADMM_ENV_PROBE", "d") == "d"
+    monkeypatch.setenv("GADMM_ENV_PROBE", "7")
+    assert getenv("GADMM_ENV_PROBE") == "7"
+    os.environ["GADMM_ENV_PROBE"] = "ü"
+    assert getenv("GADMM_ENV_PROBE") == os.environ.get("GADMM_ENV_PROBE")
+    monkeypatch.delenv("GADMM_ENV_PROBE")
+    assert getenv("GADMM_ENV_PROBE", "x") == "x"
