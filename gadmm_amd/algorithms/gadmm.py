@@ -243,6 +243,14 @@ def _rechains(max_iter: int, coherence) -> np.ndarray:
     return r
 
 
+def _max_epochs(eng) -> int:
+    """gadmm_chain_blocked_max_epochs (a constant of the build), asked once per engine."""
+    v = eng.__dict__.get("_max_epochs")
+    if v is None:
+        v = eng._max_epochs = int(eng.lib.gadmm_chain_blocked_max_epochs())
+    return v
+
+
 def _dyn_early_draw(eng, schedule, max_iter, fabric, n_total):
     """``(saved schedule state, epochs drawn, join)`` for the first D-GADMM launch's chains started
     asynchronously (PathSchedule.prefetch_async), with the chunk / look-ahead rule of the launch loop in
@@ -257,7 +265,7 @@ def _dyn_early_draw(eng, schedule, max_iter, fabric, n_total):
     hk = (float(schedule.coherence), schedule.kind, int(max_iter), int(n_total))
     chunk = max(16, int(hints[hk]) + 8) if hk in hints else 128
     if eng.dynamic_uses_blocked(fabric, schedule.coherence):
-        chunk = min(chunk, int(eng.lib.gadmm_chain_blocked_max_epochs()) - 1)
+        chunk = min(chunk, _max_epochs(eng) - 1)
     E_total = 1 + len(rechains)
     e1 = min(chunk, E_total)
     look = e1 if e1 < E_total else e1 - 1
@@ -300,7 +308,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     pre = (model.A, model.b, model.yy) if kind == "linear" else None
     # one engine per (model, configuration) on a single rank: repeated solves (rho sweeps, benchmarks,
     # D-GADMM re-runs) reuse its device buffers, cached inverses and captured graph
-    key = (kind, local_solver, n_total, tuple(int(w) for w in local_ids), float(rho), int(max_iter), block,
+    key = (kind, local_solver, n_total, tuple(map(int, local_ids)), float(rho), int(max_iter), block,
            float(step), int(max_inner), float(inner_tol), float(getattr(model, "lam", 0.0)),
            opts.get("chord"), bool(opts.get("residual", True)))
     cache = getattr(model, "_chain_engines", None) if rcomm is None else None
@@ -419,7 +427,7 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         # the blocked kernel's dynamic mode stages a launch's epoch tables in LDS: at most
         # gadmm_chain_blocked_max_epochs rows per launch (this chunk + the look-ahead epoch)
         use_blk = eng.dynamic_uses_blocked(fabric, schedule.coherence)
-        cap = int(eng.lib.gadmm_chain_blocked_max_epochs()) - 1 if use_blk else 1 << 30
+        cap = _max_epochs(eng) - 1 if use_blk else 1 << 30
         chunk = min(chunk, cap)
         saved = early[0] if early is not None else schedule.save()
         E_total = 1 + len(rechains)
