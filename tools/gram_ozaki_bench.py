@@ -1,6 +1,7 @@
 """The int8 Ozaki Gram (csrc/kernels/gram_ozaki.hip) against the f64-MFMA Gram: accuracy (entries relative
 to sqrt(A_aa A_bb), against an f64 reference) and time, at a given shard shape.
 Usage: python tools/gram_ozaki_bench.py N m d [reps]"""
+import os
 import sys
 import time
 
@@ -31,7 +32,9 @@ def timed(f):
     return min(ts), out
 
 
+os.environ["GADMM_GRAM_OZAKI"] = "0"  # gram() would dispatch large shards to the Ozaki path itself
 t64, (A64, b64, yy64) = timed(lambda: gram(X, y))
+del os.environ["GADMM_GRAM_OZAKI"]
 toz, (Aoz, boz, yyoz) = timed(lambda: gram_ozaki(X, y))
 flops = 2.0 * N * m * (d + 1) * (d + 2) / 2
 scale = torch.sqrt(torch.diagonal(A64, dim1=1, dim2=2))
