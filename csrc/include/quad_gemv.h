@@ -88,6 +88,28 @@ __device__ __forceinline__ double quad_gemv(const double (&m)[4][T], double x, d
 #endif
 }
 
+// quad_gemv with the broadcast vector already staged by another wave in quad_gemv's x layout
+// (xs0[(l & 3) * QX + (l >> 2)] = x_l): the same FMAs and reduction, without this wave's staging write.
+template <int T>
+__device__ __forceinline__ double quad_gemv_staged(const double (&m)[4][T], const double* xs0) {
+  static_assert(T >= 1 && T <= 16, "quad layout covers d <= 64");
+  const int lane = threadIdx.x & 63, c = lane >> 4;
+  const double* xs = xs0 + c * QX;
+  double p[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+  for (int t = 0; t < T; t += 2) {
+    const double2 xp = *reinterpret_cast<const double2*>(xs + t);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p[r] = fma(m[r][t], xp.x, p[r]);
+    if (t + 1 < T) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p[r] = fma(m[r][t + 1], xp.y, p[r]);
+    }
+  }
+  asm volatile("" ::: "memory");
+  return quad_reduce(p);
+}
+
 // Quad layout kept in LDS instead of VGPRs (a matrix used off the critical path, e.g. the exact
 // objective's Gram): element m[r][t] of lane l at Ml[((t >> 1) * 4 + r) * 128 + 2 l + (t & 1)], so a
 // lane reads its (t, t + 1) pair with one 16-byte load. quad_gemv_lds performs quad_gemv's FMAs in

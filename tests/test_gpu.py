@@ -914,12 +914,17 @@ def test_native_primal_residual_large_d():
     np.testing.assert_allclose(a.primal_res, b.primal_res, rtol=1e-8)
 
 
-def test_logistic_persistent_kernel_matches_graph_engine(log24, log_obj0):
-    """Inner-GD logistic GADMM in ONE launch (chain_persistent_logistic.hip: one resident wave per
-    worker, shard in VGPRs, granule hand-offs) == the graph-replayed phase kernels bit for bit, and the
-    reference's 53 iterations (BASELINE configs[2])."""
+@pytest.mark.parametrize("zrec", ["0", "1"])
+def test_logistic_persistent_kernel_matches_graph_engine(log24, log_obj0, zrec, monkeypatch):
+    """Inner-GD logistic GADMM in ONE launch (chain_persistent_logistic.hip) at the reference's 53
+    iterations (BASELINE configs[2]). zrec = "0": one resident wave per worker (shard in VGPRs, granule
+    hand-offs) == the graph-replayed phase kernels bit for bit. zrec = "1" (the default): the margins
+    z = X x carried by a recursion on a second wave (z' = z - step (-K s + lam z + X sh), K = X X^T), so
+    each inner step's dependent chain holds one GEMV; s differs from X x in rounding only: the trace
+    equals the graph engine's and torch's to 1e-12."""
     from gadmm_amd.models import LogisticRegression
     from gadmm_amd.algorithms import chain_admm
+    monkeypatch.setenv("GADMM_LOGISTIC_ZREC", zrec)
     m = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
     kw = dict(local_solver="gd", step=2.2)
     a = chain_admm(m, list(range(24)), 24, 2e-4, log_obj0, 1e-4, 400, engine_opts={"cache": False}, **kw)
@@ -927,8 +932,12 @@ def test_logistic_persistent_kernel_matches_graph_engine(log24, log_obj0):
                    engine_opts={"cache": False, "persistent": False, "block": 8}, **kw)
     assert a.extra["engine"] == "persistent" and b.extra["engine"] == "graph"
     assert a.iters == b.iters == 53 and a.converged
-    assert np.array_equal(a.obj, b.obj)
-    np.testing.assert_allclose(a.primal_res, b.primal_res, rtol=0, atol=0)
+    if zrec == "0":
+        assert np.array_equal(a.obj, b.obj)
+        np.testing.assert_allclose(a.primal_res, b.primal_res, rtol=0, atol=0)
+    else:
+        np.testing.assert_allclose(a.obj, b.obj, rtol=1e-12, atol=0)
+        np.testing.assert_allclose(a.primal_res, b.primal_res, rtol=1e-8, atol=1e-20)
     t = chain_admm(m, list(range(24)), 24, 2e-4, log_obj0, 1e-4, 400, backend="torch", **kw)
     np.testing.assert_allclose(a.obj, t.obj[:53], rtol=1e-12)
     assert np.all(np.diff(a.time_trace) >= 0) and a.time_trace[-1] > 0

@@ -179,8 +179,8 @@ def test_ipc_transport_logistic_two_ranks(log24):
     m = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
     obj0 = res[0]["obj0"]
     single = chain_admm(m, list(range(24)), 24, 2e-4, obj0, 1e-4, 400, local_solver="gd", step=2.2,
-                        engine_opts={"block": 8, "cache": False})
-    assert single.iters == 53
+                        engine_opts={"block": 8, "cache": False, "persistent": False})  # the ranks' engine
+    assert single.iters == 53 and single.extra["engine"] == "graph"
     for r in res:
         assert r["iters"] == 53
         assert np.array_equal(np.asarray(r["trace"]), single.obj)
