@@ -590,8 +590,7 @@ __device__ __forceinline__ double zr_sigm(double yv, double z) {
   const double e = ldexp(fma(s1, r8, s0), (int)n);
   const double dd = 1.0 + e;
   double y = __builtin_amdgcn_rcp(dd);
-  y = fma(y, fma(-dd, y, 1.0), y);
-  y = fma(y, fma(-dd, y, 1.0), y);
+  y = fma(y, fma(-dd, y, 1.0), y);  // one Newton step squares v_rcp_f64's relative error
   return yv * y;
 }
 
@@ -692,9 +691,12 @@ __global__ void __launch_bounds__(ZR_NT) chain_persistent_logistic_zrec_kernel(P
         for (int t = 0; t < T; ++t) Kq[r][t] = Kb[(qi + 16 * r) * 64 + qc + 4 * t];  // built by wave 0 before start 1
       double z = zc[lane];
       double cc = 0.0;
+      const double decay = 1.0 - step * lam;
       bool ended = false;
       for (int k = 0; k < g.max_inner && !ended; ++k) {
         const double sv = ini ? (zr_fast ? zr_sigm(yv, z) : yv / (1.0 + exp(yv * z))) : 0.0;
+        // z' = (1 - step lam) z - step c + step (K s): the part without K s is formed while the GEMV runs
+        double zpart = fma(decay, z, -step * cc);
         if (k >= ZR_SLOTS - ZR_CHK && k % ZR_CHK == 0) {
           // slots of steps k .. k + ZR_CHK - 1 are free once steps <= k + ZR_CHK - 1 - ZR_SLOTS were read;
           // the iterate wave's end of the solve also ends this run-ahead
@@ -715,8 +717,9 @@ __global__ void __launch_bounds__(ZR_NT) chain_persistent_logistic_zrec_kernel(P
             if ((spin & 63) == 63 && now_ticks() > deadline) return;
           }
           cc = zc[64 + lane];
+          zpart = fma(decay, z, -step * cc);
         }
-        z = ini ? z - step * (-u + lam * z + cc) : 0.0;
+        z = ini ? fma(step, u, zpart) : 0.0;
       }
     }
   }
