@@ -27,6 +27,7 @@
 #include "gadmm_chain.h"
 #include "persist_device.h"
 #include "chain_device.h"
+#include "fast_sigm.h"
 #include <cstddef>
 #include <stdlib.h>
 
@@ -569,30 +570,10 @@ __device__ __forceinline__ void zr_store_rel(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// s = y / (1 + e^{y z}) on the margins wave's critical path: e^t by Cody-Waite reduction and a degree-12
-// Taylor polynomial in Estrin form (dependent depth ~8 f64 ops instead of a Horner chain), 1 / (1 + e)
-// by v_rcp_f64 and two Newton steps. Within ~2 ulp of the libm quotient -- inside the rounding the
-// recursion already changes (the traces stay within 1e-12 of torch). Measured 5.64 -> 5.21 ms on E3, one
-// box (profiles/r05_j/r5jf); the default (GADMM_LOGISTIC_FASTSIGM=0: libm exp and the IEEE quotient).
-__device__ __forceinline__ double zr_sigm(double yv, double z) {
-  const double t = fmin(fmax(yv * z, -746.0), 709.0);
-  const double n = rint(t * 1.4426950408889634);
-  const double r = fma(-n, 1.90821492927058770002e-10, fma(-n, 6.93147180369123816490e-01, t));
-  const double r2 = r * r, r4 = r2 * r2, r8 = r4 * r4;
-  const double p01 = 1.0 + r;
-  const double p23 = fma(r, 1.0 / 6.0, 0.5);
-  const double p45 = fma(r, 1.0 / 120.0, 1.0 / 24.0);
-  const double p67 = fma(r, 1.0 / 5040.0, 1.0 / 720.0);
-  const double p89 = fma(r, 1.0 / 362880.0, 1.0 / 40320.0);
-  const double p1011 = fma(r, 1.0 / 39916800.0, 1.0 / 3628800.0);
-  const double q0 = fma(p23, r2, p01), q1 = fma(p67, r2, p45), q2 = fma(p1011, r2, p89);
-  const double s0 = fma(q1, r4, q0), s1 = fma(1.0 / 479001600.0, r4, q2);
-  const double e = ldexp(fma(s1, r8, s0), (int)n);
-  const double dd = 1.0 + e;
-  double y = __builtin_amdgcn_rcp(dd);
-  y = fma(y, fma(-dd, y, 1.0), y);  // one Newton step squares v_rcp_f64's relative error
-  return yv * y;
-}
+// s = y / (1 + e^{y z}) on the margins wave's critical path: inv1pexp_fast (fast_sigm.h). Measured 5.64 ->
+// 5.21 ms on E3, one box (profiles/r05_j/r5jf); the default (GADMM_LOGISTIC_FASTSIGM=0: libm exp and
+// the IEEE quotient). The traces stay within 1e-12 of torch.
+__device__ __forceinline__ double zr_sigm(double yv, double z) { return yv * inv1pexp_fast(yv * z); }
 
 template <int T, bool SYS>
 __global__ void __launch_bounds__(ZR_NT) chain_persistent_logistic_zrec_kernel(PersistArgs a, LogiArgs g) {

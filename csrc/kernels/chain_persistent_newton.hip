@@ -27,6 +27,7 @@
 #include "gadmm_chain.h"
 #include "persist_device.h"
 #include "chain_device.h"
+#include "fast_sigm.h"
 #include <cstddef>
 
 struct LogiArgs {  // == chain_persistent_logistic.hip (one ABI for both persistent logistic kernels)
@@ -430,6 +431,7 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
   const bool inj = lane < d, ini = lane < m;
   const double yv = ini ? g.Y[(long)li * m + lane] : 0.0;
   double th = inj ? a.theta[(long)w * d + lane] : 0.0;
+  const bool fast_sig = (a.dbg & 32) == 0;
   double mu = inj ? a.mu[(long)li * d + lane] : 0.0;
   double tl = (inj && left >= 0) ? a.theta[(long)left * d + lane] : 0.0;
   double tr = (inj && right >= 0) ? a.theta[(long)right * d + lane] : 0.0;
@@ -506,7 +508,8 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
       if (right >= 0) cv = cv - rho * tr;
       x = th;
     }
-    // -- chord Newton from the inverse at the previous own iterate
+    // -- chord Newton from the inverse at the previous own iterate (the chord steps' sigmoid by
+    // inv1pexp_fast unless PersistArgs::dbg & 32: GADMM_NEWTON_FASTSIGM=0)
     const int kk_tl = it - a.start_iter;
     long long* tls = (a.timeline && kk_tl < 64) ? a.timeline + ((long)li * 128 + 64 + kk_tl) * 8 : nullptr;
     if (tls && lane == 0) tls[0] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -526,7 +529,7 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
     cur_fresh = false;
     for (int k = 0; k < NMAX; ++k) {
       const double z = quad_gemv<QT>(Xq, x, st);                     // margins
-      const double ps = ini ? 1.0 / (1.0 + exp(yv * z)) : 0.0;        // sigma(-y z)
+      const double ps = ini ? (fast_sig ? inv1pexp_fast(yv * z) : 1.0 / (1.0 + exp(yv * z))) : 0.0;  // sigma(-y z)
       const double gx = quad_gemv_lds<QT>(XTl, ini ? yv * ps : 0.0, st);  // (X^T (y . sigma))_j
       const double gr = inj ? -gx + shift * x + cv : 0.0;
       const double dx = quad_gemv_lds<QT>(hq, gr, st);
@@ -670,6 +673,8 @@ int gadmm_chain_persistent_newton_launch(const PersistArgs* args, const LogiArgs
   }
   if (shm > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   PersistArgs ka = a;
+  const char* fs = getenv("GADMM_NEWTON_FASTSIGM");
+  if (fs && fs[0] == '0') ka.dbg |= 32;
   void* kargs[] = {&ka, const_cast<LogiArgs*>(&g)};
   GADMM_CHECK(hipLaunchKernel(fn, dim3(blocks), dim3(NT), kargs, shm, st));
   GADMM_CHECK(hipGetLastError());
