@@ -37,6 +37,7 @@ struct LogiArgs {
   int m, max_inner;
   double lam, step, inner_tol;
   int* inner_iters;  // [n_local] optional: GD steps of the worker's last local solve
+  double* scratch;   // Newton pipeline only (chain_persistent_newton.hip): per-worker refresh images
 };
 
 template <int T, bool SYS>

@@ -29,6 +29,7 @@
 #include "chain_device.h"
 #include "fast_sigm.h"
 #include <cstddef>
+#include <cstdlib>
 
 struct LogiArgs {  // == chain_persistent_logistic.hip (one ABI for both persistent logistic kernels)
   const double* X;  // [n_local][m][d]
@@ -36,6 +37,7 @@ struct LogiArgs {  // == chain_persistent_logistic.hip (one ABI for both persist
   int m, max_inner;
   double lam, step, inner_tol;  // Newton: step = chord threshold (<= 0: a fresh inverse every step)
   int* inner_iters;             // [n_local] optional: Newton steps of the worker's last local solve
+  double* scratch;              // pipeline kernel: [n_local][RSLOTS][4 QB] refresh images (P | B | XP | XB)
 };
 
 namespace {
@@ -80,6 +82,7 @@ struct NCtl {        // LDS words of the solver <-> crew protocol
   int cnt;           // crew barrier counter
   int src;           // refresh mode: -1 Gauss-Jordan; r >= 0: one Newton-Schulz step from refresh r's inverse
   double shift;      // lam + deg rho of the requested refresh
+  int quit;          // the solve is over: the crew leaves once it has served every request posted before
 };
 
 // LDS-only ordering: the fences name the "local" address space, so they wait for LDS operations only
@@ -368,6 +371,7 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
     nc.cnt = 0;
     nc.src = -1;  // refresh 0: Gauss-Jordan
     nc.shift = shift;
+    nc.quit = 0;
   }
   // refresh 0 is built at the worker's start point theta^{start - 1}: w_i = sigma(z_i)(1 - sigma(z_i)),
   // z_i = X_i theta (zeros on a fresh solve: w = 1/4)
@@ -391,14 +395,17 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
     const int li_ = sl.li;
     int gen = 0, done_req = -1;
     for (;;) {
+      // quit is read BEFORE req: a quit seen here was posted after every request (same wave, release),
+      // so all four crew waves serve the same requests and leave together (none waits in crew_sync alone)
       int r;
       for (int spin = 0;; ++spin) {
+        const int q = lds_load_acq(&nc.quit);
         r = lds_load_acq(&nc.req);
         if (r != done_req) break;
+        if (q) return;
         if ((spin & 63) == 63 && now_ticks() > deadline + 100000000ull) return;  // solver gone (abort path)
         __builtin_amdgcn_s_sleep(1);
       }
-      if (r < 0) return;  // the solver quit
       // instrumented runs (PersistArgs::timeline, [n_local][128][8] stamps): refreshes 0..63 in rows 0..63
       long long* tl = (a.timeline && r < 64) ? a.timeline + ((long)li_ * 128 + r) * 8 : nullptr;
       if (tl && cw == 0 && lane == 0) tl[0] = (long long)__builtin_amdgcn_s_memrealtime();
@@ -610,7 +617,778 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
       post(pend);
     }
   }
-  lds_store_rel(&nc.req, -1);  // crew: quit (after its current refresh, if any)
+  lds_store_rel(&nc.quit, 1);  // crew: quit (after its current refresh, if any)
+  if (inj) {
+    a.theta[(long)w * d + lane] = th;
+    a.mu[(long)li * d + lane] = mu;
+  }
+  if (lane == 0) {
+    if (g.inner_iters) g.inner_iters[li] = used;
+    if (abort) {
+      a.ctl->done = 4;
+    } else if (bid == 0 && stop_code) {
+      a.ctl->done = stop_code;
+      a.ctl->conv_iter = stop_iter;
+      a.ctl->iter = it;
+      a.ctl->pending = 1;
+      a.ctl->monitored = stop_iter;
+    }
+  }
+}
+
+// ==================================================================================================
+// GADMM_NEWTON_REC (default): the chord steps as a FOUR-wave pipeline. One chord step
+//     z = X x,  s = y sigma(-y z),  dx = P (shift x + cv - X^T s),  x' = x - dx
+// is three dependent GEMVs on one wave above (two of them from LDS: ~1.6 us per step,
+// profiles/r03_newton). With the step's matrices formed once per inverse P (by the crew, MFMA):
+//     B = P X^T (d x m),  XP = X P (m x d),  XB = X B (m x m),
+// and y_k = shift x_k + cv, the step splits into
+//     dx_k = P y_k - B s_k,   x_{k+1} = x_k - dx_k,   z_{k+1} = X x_{k+1} = z_k - XP y_k + XB s_k,
+// so four waves, one register matrix each, run one GEMV per step in a pipeline:
+//     S (margins, XB):  s_k = y sigma(-y z_k) -> ring; z_{k+1} = (z_k - w_k) + XB s_k
+//     T (iterate, B):   dx_k = v_k - B s_k; x_{k+1}; y_{k+1} -> ring; the stop and chord rules
+//     V (P):            v_k = P y_k            W (XP):  w_k = XP y_k
+// The dependent chain of a step is S's sigmoid + one GEMV + one LDS hand-off; v_k and w_k are formed
+// while S works. Every segment (a local solve, or its continuation after an urgent refresh) restarts
+// the margins from the exact z_0 = X x_0 (wave W, X in LDS), which also gives the objective f_n and
+// the refresh weights. The crew (4 waves) builds P exactly as the one-wave kernel's crew (Hessian,
+// Gauss-Jordan or one Newton-Schulz step) plus the three products, into a per-worker global image
+// (LogiArgs::scratch, refresh r in slot r % 3) that the pipeline waves load into VGPRs off the critical
+// path (the next phase's inverse is known at the end of a phase). Which inverse each step uses is
+// fixed by the iterates alone (deterministic); only the margins differ from the one-wave kernel in
+// rounding (host emulation, tools/newton_recursion_emul.py: 424 iterations, theta within 1e-15).
+namespace {
+
+constexpr int RT = 512;           // 8 waves: S, T, V, W (SIMDs 0-3) + the crew (waves 4-7)
+constexpr int RR = 4;             // ring slots (a producer runs at most two steps ahead)
+constexpr int RSLOTS = 3;         // refresh images per worker
+constexpr int RIMG = 4 * QB;      // one image: P | B | XP | XB, quad-LDS layout each
+constexpr int REC_RLAG = 2;       // default refresh lag (iterations) and background-refresh step threshold
+constexpr int REC_BG = 1;
+
+struct RLds {  // doubles
+  int xt, xq, hs, hp, wq, slab, stage, sring, yring, vring, wring, z0v, xfin, total;
+  __host__ __device__ RLds() {
+    xt = 0;                    // X^T, quad-LDS layout (crew operands)
+    xq = xt + QB;              // X, quad-LDS layout (W's exact margins)
+    hs = xq + QB;              // [64][HS] Hessian, then Newton-Schulz T, then B row-major (crew)
+    hp = hs + 64 * HS;         // [64][HS] the new P row-major (crew)
+    wq = hp + 64 * HS;         // [64] refresh weights
+    slab = wq + 64;            // [2][4][64] Gauss-Jordan slabs
+    stage = slab + 512;        // W's quad GEMV staging
+    sring = stage + QSTAGE;    // [RR][4 QX] s_k (quad_gemv broadcast layout)
+    yring = sring + RR * 4 * QX;  // [RR][4 QX] y_k
+    vring = yring + RR * 4 * QX;  // [RR][64] v_k
+    wring = vring + RR * 64;      // [RR][64] w_k
+    z0v = wring + RR * 64;        // [64] exact margins of the next segment's start
+    xfin = z0v + 64;              // [64] a segment's final iterate
+    total = xfin + 64;
+  }
+};
+
+enum { PC_SEG, PC_CUR, PC_Z0, PC_S, PC_Y, PC_V, PC_W, PC_END, PC_QUIT, PC_EKIND, PC_EREQ, PC_ESRC, PC_ENEXT,
+       PC_EIT, PC_WDONE, PC_N };
+
+// Ordering of the refresh images, which never leave the CU (the crew stores them, waves of the same
+// workgroup load them): the crew waits for its stores (vmcnt 0) before `ready` is posted, and the
+// loads bypass L1 (load_img: sc0), so no agent-scope fence (an L2 write-back / invalidate of the whole
+// XCD, measured: refresh 15 -> 27 us) is needed.
+__device__ __forceinline__ void wg_release() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_s_waitcnt(0);
+}
+__device__ __forceinline__ void wg_acquire() { __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup"); }
+
+// wave max of |v| by DPP row rotations (within 16 lanes) and two permlane swaps (across rows): a few
+// dozen cycles instead of six ds_bpermute round trips (wave_max_abs)
+template <int CTL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)u, CTL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(u >> 32), CTL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double wave_max_abs_dpp(double v) {
+  v = fabs(v);
+  v = fmax(v, dpp_f64<0x128>(v));  // row_ror:8
+  v = fmax(v, dpp_f64<0x124>(v));  // row_ror:4
+  v = fmax(v, dpp_f64<0x122>(v));  // row_ror:2
+  v = fmax(v, dpp_f64<0x121>(v));  // row_ror:1
+  double a = v, b = v;
+  swap16_f64(a, b);
+  v = fmax(a, b);
+  a = v;
+  b = v;
+  swap32_f64(a, b);
+  return fmax(a, b);
+}
+
+// C (64 x 64 tile column cw) = A B over k < K: acc[R][reg] = C[16R + k4 + 4 reg][16 cw + c16]
+template <class FA, class FB>
+__device__ __forceinline__ void crew_mm(f64x4 (&acc)[4], int cw, int K, FA fa, FB fb) {
+  const int lane = threadIdx.x & 63, k4 = lane >> 4, c16 = lane & 15;
+#pragma unroll
+  for (int R = 0; R < 4; ++R) acc[R] = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 0; k0 < K; k0 += 4) {
+    const int kk = k0 + k4;
+    const double bv = fb(kk, 16 * cw + c16);
+#pragma unroll
+    for (int R = 0; R < 4; ++R) acc[R] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa(16 * R + c16, kk), bv, acc[R], 0, 0, 0);
+  }
+}
+
+// quad_gemv's register matrix from a quad-LDS-layout image in global memory (one 16-B load per pair,
+// sc0: past L1, which may still hold the slot's previous image)
+__device__ __forceinline__ void load_img(double (&M)[4][QT], const double* img) {
+  const int lane = threadIdx.x & 63;
+  const __amdgpu_buffer_rsrc_t rs = rsrc_of(img);
+#pragma unroll
+  for (int t = 0; t < QT; t += 2)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const u32x4 g = __builtin_amdgcn_raw_buffer_load_b128(rs, (((t >> 1) * 4 + r) * 128 + 2 * lane) * 8, 0, 1);
+      M[r][t] = __longlong_as_double((long long)(((unsigned long long)g.y << 32) | g.x));
+      if (t + 1 < QT) M[r][t + 1] = __longlong_as_double((long long)(((unsigned long long)g.w << 32) | g.z));
+    }
+}
+
+// crew_sync with a deadline (the pipeline kernel ends even if a crew wave is gone)
+__device__ __forceinline__ void crew_sync_dl(int* cnt, int& gen, unsigned long long dl) {
+  gen += CREW;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (int spin = 0; __hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < gen; ++spin) {
+    __builtin_amdgcn_s_sleep(1);
+    if ((spin & 255) == 255 && __builtin_amdgcn_s_memrealtime() > dl) break;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+// Coalesced write of a quad-LDS-layout image from a row-major LDS matrix M ([64][HS], element (row, col);
+// trans: element (col, row)) by the crew's 256 threads: one 16-byte store per (t, t + 1) pair
+__device__ __forceinline__ void crew_copy_out(double* img, const double* M, bool trans) {
+  for (int e2 = (int)threadIdx.x - 256; 2 * e2 < QB; e2 += 256) {
+    const int e = 2 * e2;  // elements e (t even) and e + 1 (t odd) of one lane's pair
+    const int blk = e >> 7, within = e & 127;
+    const int r = blk & 3, th = blk >> 2, lq = within >> 1;
+    const int row = (lq & 15) + 16 * r, c0 = (lq >> 4) + 8 * th, c1 = c0 + 4;
+    const double v0 = trans ? M[c0 * HS + row] : M[row * HS + c0];
+    const double v1 = trans ? M[c1 * HS + row] : M[row * HS + c1];
+    *reinterpret_cast<double2*>(img + e) = double2{v0, v1};
+  }
+}
+
+// One refresh for the pipeline: P (Gauss-Jordan, or one Newton-Schulz step from the image `src`), then
+// B = P X^T, XP = B^T (= X P: P symmetric) and XB = X B, all into the global image `out`.
+__device__ void crew_refresh_rec(double* lds, const RLds& L, int m, int d, double shift, int cw, int* cnt, int& gen,
+                                 double* out, long long* tl, const double* src,
+                                 unsigned long long dl) {
+  const int lane = threadIdx.x & 63, k4 = lane >> 4, c16 = lane & 15, cc = 16 * cw + c16;
+  const double* XT = lds + L.xt;  // X[i][j] = XT[qidx(j, i)]
+  double* Hs = lds + L.hs;
+  double* Hp = lds + L.hp;
+  const double* wq = lds + L.wq;
+  const int d4 = (d + 3) & ~3;
+  f64x4 acc[4];
+  // Hessian tiles: H = X^T diag(w) X + shift I (identity padding)
+  crew_mm(acc, cw, m, [&](int row, int kk) { return kk < m ? wq[kk] * XT[qidx(row, kk)] : 0.0; },
+          [&](int kk, int col) { return kk < m ? XT[qidx(col, kk)] : 0.0; });
+#pragma unroll
+  for (int R = 0; R < 4; ++R)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int row = 16 * R + k4 + 4 * reg;
+      Hs[row * HS + cc] = (row < d && cc < d) ? acc[R][reg] + (row == cc ? shift : 0.0) : (row == cc ? 1.0 : 0.0);
+    }
+  if (src) {  // the image's P into Hp (row-major, zero padding) while the Hessian completes (sc0 loads)
+    const __amdgpu_buffer_rsrc_t rs = rsrc_of(src);
+    for (int e2 = (int)threadIdx.x - 256; 2 * e2 < QB; e2 += 256) {
+      const u32x4 gv = __builtin_amdgcn_raw_buffer_load_b128(rs, e2 * 16, 0, 1);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int e = 2 * e2 + h;
+        const int blk = e >> 7, within = e & 127;
+        const int r = blk & 3, th = blk >> 2, lq = within >> 1, t = 2 * th + (within & 1);
+        Hp[((lq & 15) + 16 * r) * HS + (lq >> 4) + 4 * t] =
+            __longlong_as_double((long long)(((unsigned long long)(h ? gv.w : gv.y) << 32) | (h ? gv.z : gv.x)));
+      }
+    }
+    for (int e = (int)threadIdx.x - 256; e < 64 * 8; e += 256) Hp[(e >> 3) * HS + QCOLS + (e & 7)] = 0.0;
+  }
+  crew_sync_dl(cnt, gen, dl);
+  if (tl && cw == 0 && lane == 0) tl[1] = (long long)__builtin_amdgcn_s_memrealtime();
+  if (src) {
+    // T = H X0 -> Hs;  U = X0 T;  X1 = 2 X0 - U -> Hp
+    crew_mm(acc, cw, d4, [&](int row, int kk) { return Hs[row * HS + kk]; }, [&](int kk, int col) { return Hp[kk * HS + col]; });
+    crew_sync_dl(cnt, gen, dl);
+#pragma unroll
+    for (int R = 0; R < 4; ++R)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) Hs[(16 * R + k4 + 4 * reg) * HS + cc] = acc[R][reg];
+    crew_sync_dl(cnt, gen, dl);
+    crew_mm(acc, cw, d4, [&](int row, int kk) { return Hp[row * HS + kk]; }, [&](int kk, int col) { return Hs[kk * HS + col]; });
+    crew_sync_dl(cnt, gen, dl);  // every wave is done reading X0
+#pragma unroll
+    for (int R = 0; R < 4; ++R)
+#pragma unroll
+      for (int reg = 0; reg < 4; ++reg) {
+        const int row = 16 * R + k4 + 4 * reg;
+        Hp[row * HS + cc] = (row < d && cc < d) ? 2.0 * Hp[row * HS + cc] - acc[R][reg] : 0.0;
+      }
+  } else {
+    // in-place block Gauss-Jordan (the one-wave kernel's crew_refresh, same arithmetic)
+    const int i = lane;
+    double h[NCW];
+#pragma unroll
+    for (int c = 0; c < NCW; ++c) h[c] = Hs[i * HS + cw + CREW * c];
+    const int nb = (d + 3) >> 2;
+    double* slabs = lds + L.slab;
+    for (int bb = 0; bb < nb; ++bb) {
+      const int p = 4 * bb;
+      double* slab = slabs + (bb & 1) * 256;
+      {
+        double hv = 0.0;
+#pragma unroll
+        for (int c = 0; c < NCW; ++c) hv = (c == bb) ? h[c] : hv;
+        slab[cw * 64 + i] = hv;
+      }
+      crew_sync_dl(cnt, gen, dl);
+      double P[4][4], Rr[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        Rr[q] = slab[q * 64 + i];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) P[q][r] = slab[q * 64 + p + r];
+      }
+      const bool pivrow = (i >> 2) == bb;
+      if (pivrow) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Rr[q] = (q == (i & 3)) ? 1.0 : 0.0;
+      }
+      const double a00 = P[0][0], a01 = P[1][0], a11 = P[1][1];
+      const double ia = rcp_nr(fma(a00, a11, -a01 * a01));
+      const double A00 = a11 * ia, A01 = -a01 * ia, A11 = a00 * ia;
+      const double b00 = P[2][0], b01 = P[3][0], b10 = P[2][1], b11 = P[3][1];
+      const double w00 = fma(A00, b00, A01 * b10), w01 = fma(A00, b01, A01 * b11);
+      const double w10 = fma(A01, b00, A11 * b10), w11 = fma(A01, b01, A11 * b11);
+      const double s00 = P[2][2] - fma(b00, w00, b10 * w10);
+      const double s01 = P[3][2] - fma(b00, w01, b10 * w11);
+      const double s11 = P[3][3] - fma(b01, w01, b11 * w11);
+      const double is = rcp_nr(fma(s00, s11, -s01 * s01));
+      const double y0 = fma(A00, Rr[0], A01 * Rr[1]), y1 = fma(A01, Rr[0], A11 * Rr[1]);
+      const double z2 = Rr[2] - fma(b00, y0, b10 * y1), z3 = Rr[3] - fma(b01, y0, b11 * y1);
+      const double l2 = fma(s11, z2, -s01 * z3) * is, l3 = fma(s00, z3, -s01 * z2) * is;
+      const double l0 = y0 - fma(w00, l2, w01 * l3), l1 = y1 - fma(w10, l2, w11 * l3);
+      const double lw = cw == 0 ? l0 : (cw == 1 ? l1 : (cw == 2 ? l2 : l3));
+#pragma unroll
+      for (int c = 0; c < NCW; ++c) {
+        const int j = cw + CREW * c;
+        const double tq = fma(l0, slab[j], fma(l1, slab[64 + j], fma(l2, slab[128 + j], l3 * slab[192 + j])));
+        const bool inK = c == bb;
+        const double sg = j < p ? -1.0 : 1.0;
+        double v;
+        if (inK) v = pivrow ? lw : -lw;
+        else v = pivrow ? sg * tq : fma(-sg, tq, h[c]);
+        h[c] = v;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NCW; ++c) {
+      const int col = cw + CREW * c;
+      Hp[i * HS + col] = (i < d && col < d) ? h[c] : 0.0;
+    }
+  }
+  crew_sync_dl(cnt, gen, dl);
+  if (tl && cw == 0 && lane == 0) tl[2] = (long long)__builtin_amdgcn_s_memrealtime();
+  crew_copy_out(out, Hp, false);  // image 0: P
+  // B = P X^T (rows: features, cols: samples) -> Hs row-major -> image 1, its transpose XP -> image 2
+  crew_mm(acc, cw, d4, [&](int row, int kk) { return Hp[row * HS + kk]; },
+          [&](int kk, int col) { return col < QCOLS ? XT[qidx(kk, col)] : 0.0; });
+#pragma unroll
+  for (int R = 0; R < 4; ++R)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int row = 16 * R + k4 + 4 * reg;
+      Hs[row * HS + cc] = (row < d && cc < m) ? acc[R][reg] : 0.0;
+    }
+  crew_sync_dl(cnt, gen, dl);  // B complete in Hs; every read of P in Hp done
+  crew_copy_out(out + QB, Hs, false);
+  crew_copy_out(out + 2 * QB, Hs, true);
+  // XB = X B (m x m) -> image 3
+  crew_mm(acc, cw, d4, [&](int row, int kk) { return row < QCOLS ? XT[qidx(kk, row)] : 0.0; },
+          [&](int kk, int col) { return Hs[kk * HS + col]; });
+#pragma unroll
+  for (int R = 0; R < 4; ++R)
+#pragma unroll
+    for (int reg = 0; reg < 4; ++reg) {
+      const int row = 16 * R + k4 + 4 * reg;
+      Hp[row * HS + cc] = (row < m && cc < m) ? acc[R][reg] : 0.0;
+    }
+  crew_sync_dl(cnt, gen, dl);
+  crew_copy_out(out + 3 * QB, Hp, false);
+  wg_release();  // the image's global stores complete before `ready` is posted
+  crew_sync_dl(cnt, gen, dl);
+}
+
+}  // namespace
+
+template <bool SYS>
+__global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(PersistArgs a, LogiArgs g) {
+  extern __shared__ __attribute__((aligned(16))) double lds[];
+  __shared__ NCtl nc;
+  __shared__ int pc[PC_N];
+  const int d = a.d, n = a.n, m = g.m;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const __amdgpu_buffer_rsrc_t rth = rsrc_of(a.thg);
+  const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
+  const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
+  const int bid = (int)blockIdx.x;
+  const RLds L;
+
+  if (a.has_monitor && bid == a.n_local) {  // the monitor: the one-wave kernel's
+    if (wid != 0) return;
+    double* vals = lds;
+    for (int it = a.start_iter;; ++it) {
+      const unsigned tag = make_tag(a.epoch, it);
+      const int slot = it % a.ring;
+      bool okall = true;
+      for (int w = lane; w < n; w += 64) {
+        double v = 0.0;
+        for (int spin = 0;; ++spin) {
+          if (load_granule<SYS>(rob, (slot * n + w) * 16, tag, &v)) break;
+          if ((spin & 7) == 7 && now_ticks() > deadline) {
+            okall = false;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        vals[w] = v;
+      }
+      const bool ok = __all(okall);
+      unsigned code = 0;
+      if (lane == 0) {
+        if (!ok) {
+          code = 4;
+        } else {
+          double s = 0.0;
+          for (int w = 0; w < n; ++w) s += vals[w];
+          if (it - 1 < a.max_iter) a.trace[it - 1] = s;
+          if (!(s == s) || isinf(s)) code = 3;
+          else if (fabs(s - a.obj0) < a.tol) code = 1;
+          else if (it >= a.max_iter) code = 2;
+          if (a.tstamp && it - 1 < a.max_iter) a.tstamp[it - 1] = (long long)now_ticks();
+        }
+        const unsigned long long dv = ((unsigned long long)tag << 32) | code;
+        for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
+      }
+      if (__shfl((int)code, 0, 64)) return;
+    }
+  }
+  if (bid >= a.n_local) return;
+
+  const PhaseSlot sl = a.slots[bid];
+  const int li = sl.li, w = sl.gid, left = sl.left, right = sl.right;
+  const bool head = (a.pos[bid] % 2) == 0;
+  const double rho = a.rho, lam = g.lam, chord = g.step;
+  const double shift = lam + rho * (double)((left >= 0 ? 1 : 0) + (right >= 0 ? 1 : 0));
+  const double* Xg = g.X + (long)li * m * d;
+  double* const img0 = g.scratch + (long)li * RSLOTS * RIMG;
+  const bool inj = lane < d, ini = lane < m;
+  // set-up: X^T and X into LDS (quad-LDS layouts), protocol words, the exact margins and refresh
+  // weights at the start point theta^{start - 1}; the crew builds refresh 0 (Gauss-Jordan) from there
+  for (int e = threadIdx.x; e < QB; e += RT) {
+    const int blk = e >> 7, within = e & 127;
+    const int r = blk & 3, th = blk >> 2, lq = within >> 1, t = 2 * th + (within & 1);
+    const int row = (lq & 15) + 16 * r, col = (lq >> 4) + 4 * t;
+    lds[L.xt + e] = (row < d && col < m && t < QT) ? Xg[(long)col * d + row] : 0.0;  // (feature, sample)
+    lds[L.xq + e] = (row < m && col < d && t < QT) ? Xg[(long)row * d + col] : 0.0;  // (sample, feature)
+  }
+  if (threadIdx.x == 0) {
+    nc.req = 0;
+    nc.ready = -1;
+    nc.cnt = 0;
+    nc.src = -1;
+    nc.shift = shift;
+    nc.quit = 0;
+  }
+  if (threadIdx.x < PC_N) pc[threadIdx.x] = threadIdx.x == PC_Z0 ? 1 : 0;
+  if (threadIdx.x < 64) {
+    const int i = threadIdx.x;
+    double z = 0.0, wi = 0.0;
+    if (i < m) {
+      for (int j = 0; j < d; ++j) z = fma(Xg[(long)i * d + j], a.theta[(long)w * d + j], z);
+      const double pz = 1.0 / (1.0 + exp(g.Y[(long)li * m + i] * z));
+      wi = pz * (1.0 - pz);
+    }
+    lds[L.wq + i] = wi;
+    lds[L.z0v + i] = i < m ? z : 0.0;
+  }
+  lds_barrier();  // the only workgroup-wide barrier
+
+  const double yv = ini ? g.Y[(long)li * m + lane] : 0.0;
+  auto ready_or_quit = [&](int r) -> bool {  // the crew finished refresh r (false: quit / deadline)
+    for (int spin = 0;; ++spin) {
+      if (lds_load_acq(&nc.ready) >= r) {
+        wg_acquire();
+        return true;
+      }
+      if (lds_load_acq(&pc[PC_QUIT])) return false;
+      if ((spin & 63) == 63 && now_ticks() > deadline) return false;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  // a pipeline wave's wait for segment `sg` to start (false: quit / deadline)
+  auto wait_seg = [&](int sg) -> bool {
+    for (int spin = 0;; ++spin) {
+      if (lds_load_acq(&pc[PC_SEG]) >= sg) return true;
+      if (lds_load_acq(&pc[PC_QUIT])) return false;
+      if ((spin & 63) == 63 && now_ticks() > deadline) return false;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  // a pipeline wave's wait for pc[flag] >= want; 1: there, 0: segment sg ended, -1: quit / deadline
+  // Issue priorities: a pipeline wave computes at 2 and spins at 0, the crew runs at 1, so a spinning
+  // wave never takes a SIMD's issue slot from the crew wave it shares the SIMD with, nor the crew one
+  // from a pipeline wave that has work.
+  auto wait_step = [&](int flag, int want, int sg) -> int {
+    if (lds_load_acq(&pc[flag]) >= want) return 1;
+    __builtin_amdgcn_s_setprio(0);
+    int res = 0;
+    for (int spin = 0;; ++spin) {
+      if (lds_load_acq(&pc[flag]) >= want) { res = 1; break; }
+      if (lds_load_acq(&pc[PC_END]) >= sg) break;
+      if ((spin & 63) == 63) {
+        if (lds_load_acq(&pc[PC_QUIT]) || now_ticks() > deadline) { res = -1; break; }
+      }
+    }
+    __builtin_amdgcn_s_setprio(2);
+    return res;
+  };
+
+  if (wid >= 4) {
+    // ---------------------------------------------------------------- crew (waves 4-7)
+    const int cw = wid - 4;
+    int gen = 0, done_req = -1;
+    __builtin_amdgcn_s_setprio(1);
+    for (;;) {
+      int r;  // quit before req (see the one-wave kernel's crew): W's last request precedes T's quit
+      for (int spin = 0;; ++spin) {
+        const int q = lds_load_acq(&nc.quit);
+        r = lds_load_acq(&nc.req);
+        if (r != done_req) break;
+        if (q) return;
+        if ((spin & 63) == 63 && now_ticks() > deadline + 100000000ull) return;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      long long* tl = (a.timeline && r < 64) ? a.timeline + ((long)li * 128 + r) * 8 : nullptr;
+      if (tl && cw == 0 && lane == 0) tl[0] = (long long)__builtin_amdgcn_s_memrealtime();
+      const int srcr = nc.src;
+      crew_refresh_rec(lds, L, m, d, nc.shift, cw, &nc.cnt, gen, img0 + (long)(r % RSLOTS) * RIMG, tl,
+                       srcr >= 0 ? img0 + (long)(srcr % RSLOTS) * RIMG : nullptr, deadline + 50000000ull);
+      if (tl && cw == 0 && lane == 0) tl[3] = (long long)__builtin_amdgcn_s_memrealtime();
+      if (cw == 0 && lane == 0) lds_store_rel(&nc.ready, r);
+      done_req = r;
+    }
+  }
+
+  double* const sring = lds + L.sring;
+  double* const yring = lds + L.yring;
+  double* const vring = lds + L.vring;
+  double* const wring = lds + L.wring;
+  // This wave's register matrix (S: XB, T: B, V: P, W: XP), loaded at ONE place per loop (a conditional
+  // reload of a loop-carried register array made the compiler keep two copies and spill): refresh 0
+  // before the first segment, then at the end of every segment the matrix of the next one (pc[PC_ENEXT],
+  // the phase's idle time except after an urgent refresh).
+  double Mq[4][QT];
+  const int part = wid == 0 ? 3 : wid == 1 ? 1 : wid == 2 ? 0 : 2;
+  const double* const mimg = img0 + (long)part * QB;
+  if (wid != 1) {
+    // ------------------------------------------------ S (wave 0), V (wave 2), W (wave 3)
+    const bool fast_sig = (a.dbg & 32) == 0;
+    double* st = lds + L.stage;
+    __builtin_amdgcn_s_setprio(2);
+    if (!ready_or_quit(0)) return;
+    load_img(Mq, mimg);
+    for (int sg = 1;; ++sg) {
+      if (!wait_seg(sg)) return;
+      const int base = sg * 1024;
+      if (wid == 0) {  // S: the margins
+        for (int spin = 0;; ++spin) {
+          if (lds_load_acq(&pc[PC_Z0]) >= sg) break;
+          if ((spin & 63) == 63 && (lds_load_acq(&pc[PC_QUIT]) || now_ticks() > deadline)) return;
+        }
+        double z = lds[L.z0v + lane];
+        for (int k = 0;; ++k) {
+          const double sv = ini ? (fast_sig ? yv * inv1pexp_fast(yv * z) : yv / (1.0 + exp(yv * z))) : 0.0;
+          double* slot = sring + (k % RR) * 4 * QX;
+          slot[(lane & 3) * QX + (lane >> 2)] = sv;
+          lds_store_rel(&pc[PC_S], base + k + 1);
+          const double u = quad_gemv_staged<QT>(Mq, slot);  // (XB s_k)_i
+          const int got = wait_step(PC_W, base + k + 1, sg);
+          if (got < 0) return;
+          if (got == 0) break;
+          z = ini ? (z - wring[(k % RR) * 64 + lane]) + u : 0.0;
+        }
+      } else {  // V: v_k = P y_k;  W: w_k = XP y_k
+        const int flag = wid == 2 ? PC_V : PC_W;
+        double* ring = wid == 2 ? vring : wring;
+        for (int k = 0;; ++k) {
+          const int got = wait_step(PC_Y, base + k + 1, sg);
+          if (got < 0) return;
+          if (got == 0) break;
+          const double v = quad_gemv_staged<QT>(Mq, yring + (k % RR) * 4 * QX);
+          ring[(k % RR) * 64 + lane] = v;
+          lds_store_rel(&pc[flag], base + k + 1);
+        }
+        if (wid == 3) {  // W: the segment's end -- exact margins at its final iterate
+          for (int spin = 0;; ++spin) {
+            if (lds_load_acq(&pc[PC_END]) >= sg) break;
+            if ((spin & 63) == 63 && (lds_load_acq(&pc[PC_QUIT]) || now_ticks() > deadline)) return;
+          }
+          const double x = lds[L.xfin + lane];
+          const double z = quad_gemv_lds<QT>(lds + L.xq, x, st);
+          lds[L.z0v + lane] = ini ? z : 0.0;
+          lds_store_rel(&pc[PC_Z0], sg + 1);
+          const int kind = pc[PC_EKIND], req = pc[PC_EREQ], src = pc[PC_ESRC], it = pc[PC_EIT];
+          if (kind == 1) {  // a local solve ended: f_n(theta^it) -> monitor
+            const double partv = wave_sum_f64(ini ? softplus(-yv * z) : 0.0);
+            const double xx = wave_sum_f64(inj ? x * x : 0.0);
+            if (lane == 0)
+              store_granule<SYS>(rob, ((it % a.ring) * n + w) * 16, make_tag(a.epoch, it), lam * 0.5 * xx + partv);
+          }
+          if (req >= 0) {  // a refresh at this iterate (the crew is idle: see the iterate wave)
+            const double pz = ini ? 1.0 / (1.0 + exp(yv * z)) : 0.5;
+            lds[L.wq + lane] = ini ? pz * (1.0 - pz) : 0.0;
+            nc.src = src;
+            lds_store_rel(&nc.req, req);
+          }
+          lds_store_rel(&pc[PC_WDONE], sg);  // T's quit waits for this (no request after the quit)
+        }
+      }
+      if (wid != 3) {  // S / V: the segment is over once T posted its end
+        for (int spin = 0;; ++spin) {
+          if (lds_load_acq(&pc[PC_END]) >= sg) break;
+          if ((spin & 63) == 63 && (lds_load_acq(&pc[PC_QUIT]) || now_ticks() > deadline)) return;
+        }
+      }
+      const int nx = pc[PC_ENEXT];  // the next segment's matrix, loaded while idle
+      if (!ready_or_quit(nx)) return;
+      load_img(Mq, mimg + (long)(nx % RSLOTS) * RIMG);
+    }
+  }
+
+  // ------------------------------------------------------------------ T (wave 1): iterate + protocol
+  u32x4* const p0 = a.push ? a.push[2 * bid] : nullptr;
+  u32x4* const p1 = a.push ? a.push[2 * bid + 1] : nullptr;
+  const __amdgpu_buffer_rsrc_t rp0 = rsrc_of(p0 ? (const void*)p0 : (const void*)a.thg);
+  const __amdgpu_buffer_rsrc_t rp1 = rsrc_of(p1 ? (const void*)p1 : (const void*)a.thg);
+  double th = inj ? a.theta[(long)w * d + lane] : 0.0;
+  double mu = inj ? a.mu[(long)li * d + lane] : 0.0;
+  double tl = (inj && left >= 0) ? a.theta[(long)left * d + lane] : 0.0;
+  double tr = (inj && right >= 0) ? a.theta[(long)right * d + lane] : 0.0;
+  int pending = a.pending_in;
+  int stop_code = 0, stop_iter = 0, abort = 0, used = 0;
+  // a background refresh requested at iteration i is adopted at i + RLAG; one is requested when a solve
+  // took more than bg_steps chord steps (PersistArgs::dbg bits 8-11 / 12-15 override: GADMM_NEWTON_RLAG,
+  // GADMM_NEWTON_BG)
+  const int RLAG = ((a.dbg >> 8) & 15) ? ((a.dbg >> 8) & 15) : REC_RLAG;
+  int cur = 0, pend = -1, pend_it = 0, next_id = 0, sg = 0;
+  bool cur_fresh = true;
+  const int bg_steps = ((a.dbg >> 12) & 15) ? ((a.dbg >> 12) & 15)
+                                            : (g.max_inner >= 1 && g.max_inner < NMAX) ? g.max_inner : REC_BG;
+  const bool ns_bg = g.inner_tol >= 0.0;
+  auto wait_ready = [&](int r) -> bool {
+    for (int spin = 0;; ++spin) {
+      if (lds_load_acq(&nc.ready) >= r) {
+        wg_acquire();
+        return true;
+      }
+      if ((spin & 63) == 63 && now_ticks() > deadline) return false;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  if (!wait_ready(0)) abort = 1;
+  load_img(Mq, mimg);
+  __builtin_amdgcn_s_setprio(2);
+
+  int it = a.start_iter;
+  for (; !abort; ++it) {
+    if (it > a.max_iter + a.lag) break;
+    const bool check = it - a.start_iter >= a.lag;
+    const int jdec = it - a.lag;
+    const bool need_nb = head ? it > a.start_iter : true;
+    const int jnb = head ? it - 1 : it;
+    const unsigned tnb = make_tag(a.epoch, jnb), tj = make_tag(a.epoch, jdec);
+    const int ra = need_nb ? left : -1, rb = need_nb ? right : -1;
+    bool decided = !check;
+    unsigned long long dv = 0;
+    int outcome = 0;
+    for (int spin = 0;; ++spin) {
+      bool nb = true;
+      if (inj) {
+        if (ra >= 0) nb &= load_granule<SYS>(rth, (ra * d + lane) * 16, tnb, &tl);
+        if (rb >= 0) nb &= load_granule<SYS>(rth, (rb * d + lane) * 16, tnb, &tr);
+      }
+      if (!decided) {
+        dv = __shfl(load_dec<SYS>(&a.decg[jdec % a.ring]), 0, 64);
+        decided = (unsigned)(dv >> 32) == tj;
+      }
+      if (decided && (unsigned)(dv & 0xffffffffu) != 0u) { outcome = 2; break; }
+      if (decided && __all(nb)) { outcome = 1; break; }
+      if ((spin & 7) == 7 && now_ticks() > deadline) { outcome = 3; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (outcome != 1) {
+      if (outcome == 2) {
+        stop_code = (int)(unsigned)(dv & 0xffffffffu);
+        stop_iter = jdec;
+      } else {
+        abort = 1;
+      }
+      break;
+    }
+    double cv = 0.0, x = 0.0;
+    if (inj) {
+      double mm = mu;
+      if (head && pending) {
+        if (left >= 0) mm = mm - rho * (tl - th);
+        if (right >= 0) mm = mm + rho * (th - tr);
+        mu = mm;
+      }
+      cv = mm;
+      if (left >= 0) cv = cv - rho * tl;
+      if (right >= 0) cv = cv - rho * tr;
+      x = th;
+    }
+    const int kk_tl = it - a.start_iter;
+    long long* tls = (a.timeline && kk_tl < 64) ? a.timeline + ((long)li * 128 + 64 + kk_tl) * 8 : nullptr;
+    if (tls && lane == 0) tls[0] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (pend >= 0 && it - pend_it >= RLAG) {  // adopt the background refresh (preloaded by S, V, W)
+      cur = pend;
+      pend = -1;
+      cur_fresh = false;
+    }
+    double nd_prev = 0.0;
+    used = 0;
+    bool urgent = false, fresh = cur_fresh;
+    cur_fresh = false;
+    int ks = 0;  // chord steps of this local solve (all segments)
+    for (;;) {   // segments: the solve, and its continuation after each urgent refresh (Mq: refresh cur)
+      if (tls && lane == 0 && ks == 0) tls[1] = (long long)__builtin_amdgcn_s_memrealtime();
+      ++sg;
+      const int base = sg * 1024;
+      pc[PC_CUR] = cur;
+      lds_store_rel(&pc[PC_SEG], sg);
+      yring[(lane & 3) * QX + (lane >> 2)] = inj ? fma(shift, x, cv) : 0.0;  // y_0 (slot 0)
+      lds_store_rel(&pc[PC_Y], base + 1);
+      int reason = 0;  // 1: the solve ends, 2: urgent refresh
+      for (int k = 0;; ++k) {
+        const int want = base + k + 1;
+        bool got = lds_load_acq(&pc[PC_S]) >= want && lds_load_acq(&pc[PC_V]) >= want;
+        if (!got) {
+          __builtin_amdgcn_s_setprio(0);
+          for (int spin = 0;; ++spin) {
+            if (lds_load_acq(&pc[PC_S]) >= want && lds_load_acq(&pc[PC_V]) >= want) { got = true; break; }
+            if ((spin & 63) == 63 && now_ticks() > deadline) break;
+          }
+          __builtin_amdgcn_s_setprio(2);
+        }
+        if (!got) { abort = 1; break; }
+        const double bs = quad_gemv_staged<QT>(Mq, sring + (k % RR) * 4 * QX);  // (B s_k)_j
+        const double dxl = inj ? vring[(k % RR) * 64 + lane] - bs : 0.0;
+        x = inj ? x - dxl : 0.0;
+        yring[((k + 1) % RR) * 4 * QX + (lane & 3) * QX + (lane >> 2)] = inj ? fma(shift, x, cv) : 0.0;
+        lds_store_rel(&pc[PC_Y], want + 1);
+        const double mdx = wave_max_abs_dpp(dxl), mx = wave_max_abs_dpp(x);
+        used = ++ks;
+        if (mdx < NTOL * fmax(1.0, mx) || ks >= NMAX) { reason = 1; break; }
+        if (chord <= 0.0 || (!fresh && ks > 1 && mdx > chord * nd_prev)) { reason = 2; break; }
+        fresh = false;
+        nd_prev = mdx;
+      }
+      if (abort) break;
+      lds[L.xfin + lane] = x;
+      if (reason == 2) {
+        // contraction too slow: an exact inverse at the current x (W posts the request once it has the
+        // weights there); the crew first finishes a background refresh in progress
+        if (pend >= 0) {
+          if (!wait_ready(pend)) { abort = 1; break; }
+          pend = -1;
+        }
+        cur = ++next_id;
+        pc[PC_EKIND] = 0;
+        pc[PC_EREQ] = cur;
+        pc[PC_ESRC] = -1;
+        pc[PC_ENEXT] = cur;
+        pc[PC_EIT] = it;
+        lds_store_rel(&pc[PC_END], sg);
+        urgent = true;
+        fresh = true;
+        nd_prev = 0.0;
+        if (!wait_ready(cur)) { abort = 1; break; }
+        load_img(Mq, mimg + (long)(cur % RSLOTS) * RIMG);
+        continue;
+      }
+      break;
+    }
+    if (abort) break;
+    if (tls && lane == 0) {
+      tls[2] = (long long)__builtin_amdgcn_s_memrealtime();
+      tls[3] = used;
+      tls[4] = next_id;
+    }
+    // publish theta^it first (the neighbours wait for it)
+    const unsigned tag = make_tag(a.epoch, it);
+    if (inj) {
+      store_granule<SYS>(rth, (w * d + lane) * 16, tag, x);
+      if (p0) store_granule<SYS>(rp0, (w * d + lane) * 16, tag, x);
+      if (p1) store_granule<SYS>(rp1, (w * d + lane) * 16, tag, x);
+    }
+    // end of the solve: W takes f_n, the exact margins and (maybe) a background refresh request from here
+    int req = -1, src = -1;
+    if ((used > bg_steps || urgent) && pend < 0) {
+      pend = req = ++next_id;
+      pend_it = it;
+      src = ns_bg ? cur : -1;
+    }
+    const int nx = (pend >= 0 && it + 1 - pend_it >= RLAG) ? pend : cur;  // the next phase's inverse
+    pc[PC_EKIND] = 1;
+    pc[PC_EREQ] = req;
+    pc[PC_ESRC] = src;
+    pc[PC_ENEXT] = nx;
+    pc[PC_EIT] = it;
+    lds_store_rel(&pc[PC_END], sg);
+    if (!head) {
+      double rp = 0.0;
+      if (inj) {
+        double mm = mu;
+        if (left >= 0) mm = mm - rho * (tl - x);
+        if (right >= 0) mm = mm + rho * (x - tr);
+        mu = mm;
+        if (left >= 0) rp = fma(tl - x, tl - x, rp);
+        if (right >= 0) rp = fma(x - tr, x - tr, rp);
+      }
+      if (a.rres) {
+        const double rs = wave_sum_f64(rp);
+        if (lane == 0 && it - 1 < a.max_iter) a.rres[(long)(it - 1) * n + w] = rs;
+      }
+    } else {
+      pending = 1;
+    }
+    th = x;
+    if (!wait_ready(nx)) { abort = 1; break; }
+    load_img(Mq, mimg + (long)(nx % RSLOTS) * RIMG);
+    if (tls && lane == 0) tls[5] = (long long)__builtin_amdgcn_s_memrealtime();  // next inverse in VGPRs
+  }
+  if (!abort) {  // W's end-of-segment work (and its refresh request, if any) precedes the quit
+    for (int spin = 0;; ++spin) {
+      if (lds_load_acq(&pc[PC_WDONE]) >= sg) break;
+      if ((spin & 63) == 63 && now_ticks() > deadline) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  lds_store_rel(&pc[PC_QUIT], 1);  // S, V, W leave
+  lds_store_rel(&nc.quit, 1);      // the crew leaves after serving every request
   if (inj) {
     a.theta[(long)w * d + lane] = th;
     a.mu[(long)li * d + lane] = mu;
@@ -631,15 +1409,25 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
 
 extern "C" long gadmm_resident_capacity(const void* fn, int threads, size_t shm);
 
+// The pipeline kernel is the default; GADMM_NEWTON_REC=0 selects the one-wave solver kernel.
+static bool newton_rec(const LogiArgs& g) {
+  const char* e = getenv("GADMM_NEWTON_REC");
+  return g.scratch != nullptr && !(e && e[0] == '0');
+}
+
 static const void* newton_variant(const PersistArgs& a, const LogiArgs& g) {
   if (a.d > 4 * QT || g.m > 4 * QT || a.d < 1 || g.m < 1 || a.n_epochs > 0) return nullptr;
+  if (newton_rec(g))
+    return a.sys_scope ? (const void*)chain_persistent_newton_rec_kernel<true>
+                       : (const void*)chain_persistent_newton_rec_kernel<false>;
   return a.sys_scope ? (const void*)chain_persistent_newton_kernel<true>
                      : (const void*)chain_persistent_newton_kernel<false>;
 }
 
+static int newton_threads(const LogiArgs& g) { return newton_rec(g) ? RT : NT; }
+
 static size_t newton_shm(const PersistArgs& a, const LogiArgs& g) {
-  const NLds L(g.m, a.d);
-  size_t b = (size_t)L.total * 8;
+  size_t b = newton_rec(g) ? (size_t)RLds().total * 8 : (size_t)NLds(g.m, a.d).total * 8;
   if (b < (size_t)a.n * 8) b = (size_t)a.n * 8;  // the monitor stages one double per worker
   return b;
 }
@@ -648,7 +1436,7 @@ extern "C" {
 
 long gadmm_chain_persistent_newton_capacity(const PersistArgs* args, const LogiArgs* g) {
   const void* fn = newton_variant(*args, *g);
-  return fn ? gadmm_resident_capacity(fn, NT, newton_shm(*args, *g)) : 0;
+  return fn ? gadmm_resident_capacity(fn, newton_threads(*g), newton_shm(*args, *g)) : 0;
 }
 
 int gadmm_chain_persistent_newton_launch(const PersistArgs* args, const LogiArgs* gargs, hipStream_t st) {
@@ -666,7 +1454,8 @@ int gadmm_chain_persistent_newton_launch(const PersistArgs* args, const LogiArgs
     return -1;
   }
   const int blocks = a.n_local + (a.has_monitor ? 1 : 0);
-  const long cap = gadmm_resident_capacity(fn, NT, shm);
+  const int nt = newton_threads(g);
+  const long cap = gadmm_resident_capacity(fn, nt, shm);
   if (blocks > cap) {
     gadmm_set_error("persistent Newton kernel: %d workgroups but only %ld can be resident", blocks, cap);
     return -2;
@@ -675,10 +1464,17 @@ int gadmm_chain_persistent_newton_launch(const PersistArgs* args, const LogiArgs
   PersistArgs ka = a;
   const char* fs = getenv("GADMM_NEWTON_FASTSIGM");
   if (fs && fs[0] == '0') ka.dbg |= 32;
+  const char* rl = getenv("GADMM_NEWTON_RLAG");
+  if (rl && atoi(rl) > 0) ka.dbg |= (atoi(rl) & 15) << 8;
+  const char* bg = getenv("GADMM_NEWTON_BG");
+  if (bg && atoi(bg) > 0) ka.dbg |= (atoi(bg) & 15) << 12;
   void* kargs[] = {&ka, const_cast<LogiArgs*>(&g)};
-  GADMM_CHECK(hipLaunchKernel(fn, dim3(blocks), dim3(NT), kargs, shm, st));
+  GADMM_CHECK(hipLaunchKernel(fn, dim3(blocks), dim3(nt), kargs, shm, st));
   GADMM_CHECK(hipGetLastError());
   return 0;
 }
+
+// doubles of LogiArgs::scratch per local worker for the pipeline kernel
+long gadmm_newton_rec_scratch_doubles(void) { return (long)RSLOTS * RIMG; }
 
 }  // extern "C"

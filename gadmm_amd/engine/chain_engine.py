@@ -218,6 +218,9 @@ class NativeChainEngine:
             # Newton: per-worker inverse Hessian store (register image + valid flag + shift)
             self.hinv = torch.zeros((nl, 64 * 64 + 8), dtype=f64, device=dev) \
                 if local_solver == "newton" and nl > 0 else None
+            # the persistent Newton pipeline's refresh images (P | B | XP | XB per refresh slot, per worker)
+            self.newton_img = torch.zeros((max(nl, 1) * int(native.require().gadmm_newton_rec_scratch_doubles()),),
+                                          dtype=f64, device=dev) if local_solver == "newton" and nl > 0 else None
             self.chord = 0.02 if chord is None else float(chord)
             self.chord_persistent = 0.3 if chord is None else float(chord)
             self.xcd = int(xcd)
@@ -524,6 +527,7 @@ class NativeChainEngine:
         if self.local_solver == "newton":
             g.step = self.chord_persistent  # the persistent Newton kernel's chord contraction threshold
         g.inner_iters = self.inner_iters.data_ptr()
+        g.scratch = self.newton_img.data_ptr() if self.newton_img is not None else None
         return g
 
     def persistent_eligible(self, fabric=None) -> bool:

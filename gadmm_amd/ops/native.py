@@ -119,7 +119,8 @@ class PersistArgs(ctypes.Structure):
 class LogiArgs(ctypes.Structure):
     """Mirror of LogiArgs in csrc/kernels/chain_persistent_logistic.hip (persistent logistic GADMM)."""
     _fields_ = [("X", c_void_p), ("Y", c_void_p), ("m", c_int), ("max_inner", c_int),
-                ("lam", c_double), ("step", c_double), ("inner_tol", c_double), ("inner_iters", c_void_p)]
+                ("lam", c_double), ("step", c_double), ("inner_tol", c_double), ("inner_iters", c_void_p),
+                ("scratch", c_void_p)]
 
 
 class StarArgs(ctypes.Structure):
@@ -189,6 +190,7 @@ def _declare(lib: ctypes.CDLL) -> None:
                                                            c_void_p]),
         "gadmm_logi_abi_layout": (c_int, [ctypes.POINTER(c_longlong), c_int]),
         "gadmm_chain_persistent_newton_capacity": (c_long, [ctypes.POINTER(PersistArgs), ctypes.POINTER(LogiArgs)]),
+        "gadmm_newton_rec_scratch_doubles": (c_long, []),
         "gadmm_chain_persistent_newton_launch": (c_int, [ctypes.POINTER(PersistArgs), ctypes.POINTER(LogiArgs),
                                                          c_void_p]),
         "gadmm_write_stamp": (c_int, [c_void_p, c_void_p]),

@@ -93,6 +93,13 @@ def run(chord, bg, rho, gj=False, brief=False):
     # phase cadence: worker 0 (head) start-to-start
     st0 = so[0, :, 0][so[0, :, 0] > 0]
     print("worker 0 iteration period (us): median %.2f" % (np.median(np.diff(st0)) / 100.0))
+    okl = oks & (so[:, :, 5] > 0)
+    if okl.any():  # the pipeline kernel: end of the solve -> the next phase's matrix loaded
+        ld = (so[:, :, 5] - so[:, :, 2])[okl] / 100.0
+        print("pipeline: end of solve -> next inverse loaded (us) median / p90: %.2f / %.2f"
+              % (np.median(ld), np.percentile(ld, 90)))
+        per_step = ((so[:, :, 2] - so[:, :, 1]) / np.maximum(so[:, :, 3], 1))[oks] / 100.0
+        print("pipeline: solve time per chord step (us) median: %.3f" % np.median(per_step))
     req = so[:, :, 4][oks]
     print("refresh requests per worker after 64 iterations: mean %.1f (1 per iteration = background only)"
           % (np.mean(so[:, 63, 4]) if so.shape[1] > 63 else float("nan")))
