@@ -663,14 +663,14 @@ constexpr int RT = 512;           // 8 waves: S, T, V, W (SIMDs 0-3) + the crew 
 constexpr int RR = 4;             // ring slots (a producer runs at most two steps ahead)
 constexpr int RSLOTS = 3;         // refresh images per worker
 constexpr int RIMG = 4 * QB;      // one image: P | B | XP | XB, quad-LDS layout each
-constexpr int REC_RLAG = 2;       // default refresh lag (iterations) and background-refresh step threshold
-constexpr int REC_BG = 1;
+constexpr int REC_RLAG = 3;       // default refresh lag (iterations) and background-refresh step threshold: the
+constexpr int REC_BG = 3;         // best of a lag x threshold sweep (profiles/r05_l: 7.31 ms at 2 / 1, 6.02-6.07 at 3-4 / 3-4)
 
 struct RLds {  // doubles
   int xt, xq, hs, hp, wq, slab, stage, sring, yring, vring, wring, z0v, xfin, total;
   __host__ __device__ RLds() {
-    xt = 0;                    // X^T, quad-LDS layout (crew operands)
-    xq = xt + QB;              // X, quad-LDS layout (W's exact margins)
+    xt = 0;                    // [64][HS] X^T row-major, zero padded (crew operands: plain addressing)
+    xq = xt + 64 * HS;         // X, quad-LDS layout (W's exact margins)
     hs = xq + QB;              // [64][HS] Hessian, then Newton-Schulz T, then B row-major (crew)
     hp = hs + 64 * HS;         // [64][HS] the new P row-major (crew)
     wq = hp + 64 * HS;         // [64] refresh weights
@@ -723,13 +723,16 @@ __device__ __forceinline__ double wave_max_abs_dpp(double v) {
   return fmax(a, b);
 }
 
-// C (64 x 64 tile column cw) = A B over k < K: acc[R][reg] = C[16R + k4 + 4 reg][16 cw + c16]
+// C (64 x 64 tile column cw) = A B over k < 4 QT (operands zero beyond d / m): acc[R][reg] =
+// C[16R + k4 + 4 reg][16 cw + c16]. The k loop is unrolled (a fixed 13 steps), so the operand LDS
+// reads of later steps are issued ahead of the MFMAs.
 template <class FA, class FB>
-__device__ __forceinline__ void crew_mm(f64x4 (&acc)[4], int cw, int K, FA fa, FB fb) {
+__device__ __forceinline__ void crew_mm(f64x4 (&acc)[4], int cw, FA fa, FB fb) {
   const int lane = threadIdx.x & 63, k4 = lane >> 4, c16 = lane & 15;
 #pragma unroll
   for (int R = 0; R < 4; ++R) acc[R] = f64x4{0.0, 0.0, 0.0, 0.0};
-  for (int k0 = 0; k0 < K; k0 += 4) {
+#pragma unroll
+  for (int k0 = 0; k0 < 4 * QT; k0 += 4) {
     const int kk = k0 + k4;
     const double bv = fb(kk, 16 * cw + c16);
 #pragma unroll
@@ -780,19 +783,18 @@ __device__ __forceinline__ void crew_copy_out(double* img, const double* M, bool
 
 // One refresh for the pipeline: P (Gauss-Jordan, or one Newton-Schulz step from the image `src`), then
 // B = P X^T, XP = B^T (= X P: P symmetric) and XB = X B, all into the global image `out`.
-__device__ void crew_refresh_rec(double* lds, const RLds& L, int m, int d, double shift, int cw, int* cnt, int& gen,
+__device__ __attribute__((noinline)) void crew_refresh_rec(double* lds, const RLds& L, int m, int d, double shift, int cw, int* cnt, int& gen,
                                  double* out, long long* tl, const double* src,
                                  unsigned long long dl) {
   const int lane = threadIdx.x & 63, k4 = lane >> 4, c16 = lane & 15, cc = 16 * cw + c16;
-  const double* XT = lds + L.xt;  // X[i][j] = XT[qidx(j, i)]
+  const double* XT = lds + L.xt;  // X[i][j] = XT[j * HS + i] (zero for j >= d or i >= m)
   double* Hs = lds + L.hs;
   double* Hp = lds + L.hp;
   const double* wq = lds + L.wq;
-  const int d4 = (d + 3) & ~3;
   f64x4 acc[4];
   // Hessian tiles: H = X^T diag(w) X + shift I (identity padding)
-  crew_mm(acc, cw, m, [&](int row, int kk) { return kk < m ? wq[kk] * XT[qidx(row, kk)] : 0.0; },
-          [&](int kk, int col) { return kk < m ? XT[qidx(col, kk)] : 0.0; });
+  crew_mm(acc, cw, [&](int row, int kk) { return wq[kk] * XT[row * HS + kk]; },
+          [&](int kk, int col) { return XT[col * HS + kk]; });
 #pragma unroll
   for (int R = 0; R < 4; ++R)
 #pragma unroll
@@ -819,14 +821,14 @@ __device__ void crew_refresh_rec(double* lds, const RLds& L, int m, int d, doubl
   if (tl && cw == 0 && lane == 0) tl[1] = (long long)__builtin_amdgcn_s_memrealtime();
   if (src) {
     // T = H X0 -> Hs;  U = X0 T;  X1 = 2 X0 - U -> Hp
-    crew_mm(acc, cw, d4, [&](int row, int kk) { return Hs[row * HS + kk]; }, [&](int kk, int col) { return Hp[kk * HS + col]; });
+    crew_mm(acc, cw, [&](int row, int kk) { return Hs[row * HS + kk]; }, [&](int kk, int col) { return Hp[kk * HS + col]; });
     crew_sync_dl(cnt, gen, dl);
 #pragma unroll
     for (int R = 0; R < 4; ++R)
 #pragma unroll
       for (int reg = 0; reg < 4; ++reg) Hs[(16 * R + k4 + 4 * reg) * HS + cc] = acc[R][reg];
     crew_sync_dl(cnt, gen, dl);
-    crew_mm(acc, cw, d4, [&](int row, int kk) { return Hp[row * HS + kk]; }, [&](int kk, int col) { return Hs[kk * HS + col]; });
+    crew_mm(acc, cw, [&](int row, int kk) { return Hp[row * HS + kk]; }, [&](int kk, int col) { return Hs[kk * HS + col]; });
     crew_sync_dl(cnt, gen, dl);  // every wave is done reading X0
 #pragma unroll
     for (int R = 0; R < 4; ++R)
@@ -902,8 +904,8 @@ __device__ void crew_refresh_rec(double* lds, const RLds& L, int m, int d, doubl
   if (tl && cw == 0 && lane == 0) tl[2] = (long long)__builtin_amdgcn_s_memrealtime();
   crew_copy_out(out, Hp, false);  // image 0: P
   // B = P X^T (rows: features, cols: samples) -> Hs row-major -> image 1, its transpose XP -> image 2
-  crew_mm(acc, cw, d4, [&](int row, int kk) { return Hp[row * HS + kk]; },
-          [&](int kk, int col) { return col < QCOLS ? XT[qidx(kk, col)] : 0.0; });
+  crew_mm(acc, cw, [&](int row, int kk) { return Hp[row * HS + kk]; },
+          [&](int kk, int col) { return XT[kk * HS + col]; });
 #pragma unroll
   for (int R = 0; R < 4; ++R)
 #pragma unroll
@@ -915,7 +917,7 @@ __device__ void crew_refresh_rec(double* lds, const RLds& L, int m, int d, doubl
   crew_copy_out(out + QB, Hs, false);
   crew_copy_out(out + 2 * QB, Hs, true);
   // XB = X B (m x m) -> image 3
-  crew_mm(acc, cw, d4, [&](int row, int kk) { return row < QCOLS ? XT[qidx(kk, row)] : 0.0; },
+  crew_mm(acc, cw, [&](int row, int kk) { return XT[kk * HS + row]; },
           [&](int kk, int col) { return Hs[kk * HS + col]; });
 #pragma unroll
   for (int R = 0; R < 4; ++R)
@@ -942,7 +944,16 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
   const __amdgpu_buffer_rsrc_t rth = rsrc_of(a.thg);
   const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
   const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
-  const int bid = (int)blockIdx.x;
+  // XCD packing (PersistArgs::xcd, one GPU): the launch has 8x the blocks and only every 8th works, so
+  // all of them share one XCD's L2; with the placement verified, theta / objective granules are plain
+  // write-back stores that stay in that L2 (a neighbour's poll is an L2 hit, not a fabric round trip)
+  __shared__ int xcd_lds;
+  const bool packed = !SYS && a.xcd > 0;
+  if (packed && (blockIdx.x & 7u)) return;
+  const int bid = packed ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
+  bool local = false;
+  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds);
+  if (!SYS && bid == 0 && threadIdx.x == 0) a.ctl->placed = a.xcd > 0 ? (local ? 2 : 1) : 0;
   const RLds L;
 
   if (a.has_monitor && bid == a.n_local) {  // the monitor: the one-wave kernel's
@@ -993,15 +1004,28 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
   const double shift = lam + rho * (double)((left >= 0 ? 1 : 0) + (right >= 0 ? 1 : 0));
   const double* Xg = g.X + (long)li * m * d;
   double* const img0 = g.scratch + (long)li * RSLOTS * RIMG;
+  // per-step stamps of the first 24 segments (timeline_iters >= 512, tools/newton_rec_steps.py): row
+  // 128 + 16 (sg - 1) + k; cols 0 S posted s_k, 1 T posted y_{k+1}, 2 V posted v_k, 3 W posted w_k,
+  // 4 S got w_k, 5 T got s_k and v_k
+  long long* const stp = (a.timeline && a.timeline_iters >= 512) ? a.timeline + ((long)li * a.timeline_iters + 128) * 8
+                                                                 : nullptr;
+#define REC_STAMP(col, sg_, k_)                                                                      \
+  do {                                                                                             \
+    if (stp && (threadIdx.x & 63) == 0 && (sg_) >= 1 && (sg_) <= 24 && (k_) < 16)                   \
+      stp[((long)((sg_) - 1) * 16 + (k_)) * 8 + (col)] = (long long)__builtin_amdgcn_s_memrealtime(); \
+  } while (0)
   const bool inj = lane < d, ini = lane < m;
-  // set-up: X^T and X into LDS (quad-LDS layouts), protocol words, the exact margins and refresh
+  // set-up: X^T (row-major) and X (quad-LDS layout) into LDS, protocol words, the exact margins and refresh
   // weights at the start point theta^{start - 1}; the crew builds refresh 0 (Gauss-Jordan) from there
   for (int e = threadIdx.x; e < QB; e += RT) {
     const int blk = e >> 7, within = e & 127;
     const int r = blk & 3, th = blk >> 2, lq = within >> 1, t = 2 * th + (within & 1);
     const int row = (lq & 15) + 16 * r, col = (lq >> 4) + 4 * t;
-    lds[L.xt + e] = (row < d && col < m && t < QT) ? Xg[(long)col * d + row] : 0.0;  // (feature, sample)
     lds[L.xq + e] = (row < m && col < d && t < QT) ? Xg[(long)row * d + col] : 0.0;  // (sample, feature)
+  }
+  for (int e = threadIdx.x; e < 64 * 64; e += RT) {  // X^T row-major (feature j, sample i)
+    const int j = e >> 6, i = e & 63;
+    lds[L.xt + j * HS + i] = (j < d && i < m) ? Xg[(long)i * d + j] : 0.0;
   }
   if (threadIdx.x == 0) {
     nc.req = 0;
@@ -1080,7 +1104,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
         if ((spin & 63) == 63 && now_ticks() > deadline + 100000000ull) return;
         __builtin_amdgcn_s_sleep(1);
       }
-      long long* tl = (a.timeline && r < 64) ? a.timeline + ((long)li * 128 + r) * 8 : nullptr;
+      long long* tl = (a.timeline && r < 64) ? a.timeline + ((long)li * a.timeline_iters + r) * 8 : nullptr;
       if (tl && cw == 0 && lane == 0) tl[0] = (long long)__builtin_amdgcn_s_memrealtime();
       const int srcr = nc.src;
       crew_refresh_rec(lds, L, m, d, nc.shift, cw, &nc.cnt, gen, img0 + (long)(r % RSLOTS) * RIMG, tl,
@@ -1123,10 +1147,12 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
           double* slot = sring + (k % RR) * 4 * QX;
           slot[(lane & 3) * QX + (lane >> 2)] = sv;
           lds_store_rel(&pc[PC_S], base + k + 1);
+          REC_STAMP(0, sg, k);
           const double u = quad_gemv_staged<QT>(Mq, slot);  // (XB s_k)_i
           const int got = wait_step(PC_W, base + k + 1, sg);
           if (got < 0) return;
           if (got == 0) break;
+          REC_STAMP(4, sg, k);
           z = ini ? (z - wring[(k % RR) * 64 + lane]) + u : 0.0;
         }
       } else {  // V: v_k = P y_k;  W: w_k = XP y_k
@@ -1139,6 +1165,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
           const double v = quad_gemv_staged<QT>(Mq, yring + (k % RR) * 4 * QX);
           ring[(k % RR) * 64 + lane] = v;
           lds_store_rel(&pc[flag], base + k + 1);
+          REC_STAMP(wid, sg, k);
         }
         if (wid == 3) {  // W: the segment's end -- exact margins at its final iterate
           for (int spin = 0;; ++spin) {
@@ -1154,7 +1181,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
             const double partv = wave_sum_f64(ini ? softplus(-yv * z) : 0.0);
             const double xx = wave_sum_f64(inj ? x * x : 0.0);
             if (lane == 0)
-              store_granule<SYS>(rob, ((it % a.ring) * n + w) * 16, make_tag(a.epoch, it), lam * 0.5 * xx + partv);
+              put_granule<SYS>(local, rob, ((it % a.ring) * n + w) * 16, make_tag(a.epoch, it), lam * 0.5 * xx + partv);
           }
           if (req >= 0) {  // a refresh at this iterate (the crew is idle: see the iterate wave)
             const double pz = ini ? 1.0 / (1.0 + exp(yv * z)) : 0.5;
@@ -1223,6 +1250,9 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
     bool decided = !check;
     unsigned long long dv = 0;
     int outcome = 0;
+    const int kk_tl = it - a.start_iter;
+    long long* tls = (a.timeline && kk_tl < 64) ? a.timeline + ((long)li * a.timeline_iters + 64 + kk_tl) * 8 : nullptr;
+    long long t_nb = 0, t_dec = 0;  // (instrumented runs) when the neighbours' theta / the decision arrived
     for (int spin = 0;; ++spin) {
       bool nb = true;
       if (inj) {
@@ -1232,6 +1262,11 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
       if (!decided) {
         dv = __shfl(load_dec<SYS>(&a.decg[jdec % a.ring]), 0, 64);
         decided = (unsigned)(dv >> 32) == tj;
+      }
+      if (tls) {
+        const long long now = (long long)__builtin_amdgcn_s_memrealtime();
+        if (!t_nb && __all(nb)) t_nb = now;
+        if (!t_dec && decided) t_dec = now;
       }
       if (decided && (unsigned)(dv & 0xffffffffu) != 0u) { outcome = 2; break; }
       if (decided && __all(nb)) { outcome = 1; break; }
@@ -1260,9 +1295,11 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
       if (right >= 0) cv = cv - rho * tr;
       x = th;
     }
-    const int kk_tl = it - a.start_iter;
-    long long* tls = (a.timeline && kk_tl < 64) ? a.timeline + ((long)li * 128 + 64 + kk_tl) * 8 : nullptr;
-    if (tls && lane == 0) tls[0] = (long long)__builtin_amdgcn_s_memrealtime();
+    if (tls && lane == 0) {
+      tls[0] = (long long)__builtin_amdgcn_s_memrealtime();
+      tls[6] = t_nb;
+      tls[7] = t_dec;
+    }
     if (pend >= 0 && it - pend_it >= RLAG) {  // adopt the background refresh (preloaded by S, V, W)
       cur = pend;
       pend = -1;
@@ -1294,11 +1331,14 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
           __builtin_amdgcn_s_setprio(2);
         }
         if (!got) { abort = 1; break; }
+        REC_STAMP(5, sg, k);
         const double bs = quad_gemv_staged<QT>(Mq, sring + (k % RR) * 4 * QX);  // (B s_k)_j
         const double dxl = inj ? vring[(k % RR) * 64 + lane] - bs : 0.0;
         x = inj ? x - dxl : 0.0;
-        yring[((k + 1) % RR) * 4 * QX + (lane & 3) * QX + (lane >> 2)] = inj ? fma(shift, x, cv) : 0.0;
+        double* const ynext = yring + ((k + 1) % RR) * 4 * QX;
+        ynext[(lane & 3) * QX + (lane >> 2)] = inj ? fma(shift, x, cv) : 0.0;
         lds_store_rel(&pc[PC_Y], want + 1);
+        REC_STAMP(1, sg, k);
         const double mdx = wave_max_abs_dpp(dxl), mx = wave_max_abs_dpp(x);
         used = ++ks;
         if (mdx < NTOL * fmax(1.0, mx) || ks >= NMAX) { reason = 1; break; }
@@ -1340,7 +1380,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
     // publish theta^it first (the neighbours wait for it)
     const unsigned tag = make_tag(a.epoch, it);
     if (inj) {
-      store_granule<SYS>(rth, (w * d + lane) * 16, tag, x);
+      put_granule<SYS>(local, rth, (w * d + lane) * 16, tag, x);
       if (p0) store_granule<SYS>(rp0, (w * d + lane) * 16, tag, x);
       if (p1) store_granule<SYS>(rp1, (w * d + lane) * 16, tag, x);
     }
@@ -1408,6 +1448,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
 }
 
 extern "C" long gadmm_resident_capacity(const void* fn, int threads, size_t shm);
+extern "C" int gadmm_xcd_mode(const PersistArgs* a, int blocks, long cap_total);  // chain_persistent.hip
 
 // The pipeline kernel is the default; GADMM_NEWTON_REC=0 selects the one-wave solver kernel.
 static bool newton_rec(const LogiArgs& g) {
@@ -1462,6 +1503,8 @@ int gadmm_chain_persistent_newton_launch(const PersistArgs* args, const LogiArgs
   }
   if (shm > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   PersistArgs ka = a;
+  ka.xcd = newton_rec(g) ? gadmm_xcd_mode(&a, blocks, cap) : 0;  // the pipeline kernel packs onto one XCD
+  if (ka.xcd > 1) GADMM_CHECK(hipMemsetAsync(a.xchk, 0, (size_t)XCHK * 16, st));
   const char* fs = getenv("GADMM_NEWTON_FASTSIGM");
   if (fs && fs[0] == '0') ka.dbg |= 32;
   const char* rl = getenv("GADMM_NEWTON_RLAG");
@@ -1469,7 +1512,7 @@ int gadmm_chain_persistent_newton_launch(const PersistArgs* args, const LogiArgs
   const char* bg = getenv("GADMM_NEWTON_BG");
   if (bg && atoi(bg) > 0) ka.dbg |= (atoi(bg) & 15) << 12;
   void* kargs[] = {&ka, const_cast<LogiArgs*>(&g)};
-  GADMM_CHECK(hipLaunchKernel(fn, dim3(blocks), dim3(nt), kargs, shm, st));
+  GADMM_CHECK(hipLaunchKernel(fn, dim3(ka.xcd > 0 ? 8 * blocks : blocks), dim3(nt), kargs, shm, st));
   GADMM_CHECK(hipGetLastError());
   return 0;
 }

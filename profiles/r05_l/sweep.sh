@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${1:-r5ls}; mkdir -p $O
-for cfg in 2,1 3,1 2,2 3,2 2,3 3,3 4,2 4,3; do
+for cfg in ${CFGS:-2,1 3,1 2,2 3,2 2,3 3,3 4,2 4,3}; do
   rl=${cfg%,*}; bg=${cfg#*,}
   GADMM_NEWTON_RLAG=$rl GADMM_NEWTON_BG=$bg timeout -k 10 120 python bench.py --config logistic_exact --steps 20 --warmup 3 > $O/rl${rl}_bg${bg}.log 2>&1 || exit $?
 done

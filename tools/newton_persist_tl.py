@@ -93,6 +93,22 @@ def run(chord, bg, rho, gj=False, brief=False):
     # phase cadence: worker 0 (head) start-to-start
     st0 = so[0, :, 0][so[0, :, 0] > 0]
     print("worker 0 iteration period (us): median %.2f" % (np.median(np.diff(st0)) / 100.0))
+    # the hop: a worker's phase start against its neighbours' previous solve end (their theta publish)
+    if (so[:, :, 6] > 0).any():
+        hn, hd, hs = [], [], []
+        for w in range(1, 23):
+            for i in range(2, 63):
+                head = w % 2 == 0
+                j = i - 1 if head else i  # the neighbours' phase this one waits for
+                ref = max(so[w - 1, j, 2], so[w + 1, j, 2])
+                if ref <= 0 or so[w, i, 6] <= 0 or so[w, i, 0] <= 0:
+                    continue
+                hn.append((so[w, i, 6] - ref) / 100.0)
+                hd.append((so[w, i, 7] - ref) / 100.0 if so[w, i, 7] > 0 else np.nan)
+                hs.append((so[w, i, 0] - ref) / 100.0)
+        print("hop (us, median / p90): neighbours' theta seen %.2f / %.2f, decision seen %.2f / %.2f, phase start "
+              "%.2f / %.2f" % (np.median(hn), np.percentile(hn, 90), np.nanmedian(hd), np.nanpercentile(hd, 90),
+                               np.median(hs), np.percentile(hs, 90)))
     okl = oks & (so[:, :, 5] > 0)
     if okl.any():  # the pipeline kernel: end of the solve -> the next phase's matrix loaded
         ld = (so[:, :, 5] - so[:, :, 2])[okl] / 100.0
