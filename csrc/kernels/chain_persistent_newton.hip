@@ -646,10 +646,12 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
 //     dx_k = P y_k - B s_k,   x_{k+1} = x_k - dx_k,   z_{k+1} = X x_{k+1} = z_k - XP y_k + XB s_k,
 // so four waves, one register matrix each, run one GEMV per step in a pipeline:
 //     S (margins, XB):  s_k = y sigma(-y z_k) -> ring; z_{k+1} = (z_k - w_k) + XB s_k
-//     T (iterate, B):   dx_k = v_k - B s_k; x_{k+1}; y_{k+1} -> ring; the stop and chord rules
-//     V (P):            v_k = P y_k            W (XP):  w_k = XP y_k
-// The dependent chain of a step is S's sigmoid + one GEMV + one LDS hand-off; v_k and w_k are formed
-// while S works. Every segment (a local solve, or its continuation after an urgent refresh) restarts
+//     H (B):            b_k = B s_k -> ring
+//     T (iterate, P):   dx_k = v_k - b_k; x_{k+1}; y_{k+1} -> ring; the stop and chord rules; then
+//                       v_{k+1} = P y_{k+1} while H waits for s_{k+1}
+//     W (XP):           w_k = XP y_k
+// A step's dependent chain holds S's sigmoid and one GEMV; the loop s_k -> b_k -> y_{k+1} -> w_{k+1}
+// -> s_{k+2} spans two steps (profiles/r05_l: ~0.76 us per step against 1.65 us on one wave). Every segment (a local solve, or its continuation after an urgent refresh) restarts
 // the margins from the exact z_0 = X x_0 (wave W, X in LDS), which also gives the objective f_n and
 // the refresh weights. The crew (4 waves) builds P exactly as the one-wave kernel's crew (Hessian,
 // Gauss-Jordan or one Newton-Schulz step) plus the three products, into a per-worker global image
@@ -659,7 +661,7 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
 // rounding (host emulation, tools/newton_recursion_emul.py: 424 iterations, theta within 1e-15).
 namespace {
 
-constexpr int RT = 512;           // 8 waves: S, T, V, W (SIMDs 0-3) + the crew (waves 4-7)
+constexpr int RT = 512;           // 8 waves: S, T, H, W (SIMDs 0-3) + the crew (waves 4-7)
 constexpr int RR = 4;             // ring slots (a producer runs at most two steps ahead)
 constexpr int RSLOTS = 3;         // refresh images per worker
 constexpr int RIMG = 4 * QB;      // one image: P | B | XP | XB, quad-LDS layout each
@@ -678,7 +680,7 @@ struct RLds {  // doubles
     stage = slab + 512;        // W's quad GEMV staging
     sring = stage + QSTAGE;    // [RR][4 QX] s_k (quad_gemv broadcast layout)
     yring = sring + RR * 4 * QX;  // [RR][4 QX] y_k
-    vring = yring + RR * 4 * QX;  // [RR][64] v_k
+    vring = yring + RR * 4 * QX;  // [RR][64] b_k
     wring = vring + RR * 64;      // [RR][64] w_k
     z0v = wring + RR * 64;        // [64] exact margins of the next segment's start
     xfin = z0v + 64;              // [64] a segment's final iterate
@@ -1005,8 +1007,8 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
   const double* Xg = g.X + (long)li * m * d;
   double* const img0 = g.scratch + (long)li * RSLOTS * RIMG;
   // per-step stamps of the first 24 segments (timeline_iters >= 512, tools/newton_rec_steps.py): row
-  // 128 + 16 (sg - 1) + k; cols 0 S posted s_k, 1 T posted y_{k+1}, 2 V posted v_k, 3 W posted w_k,
-  // 4 S got w_k, 5 T got s_k and v_k
+  // 128 + 16 (sg - 1) + k; cols 0 S posted s_k, 1 T posted y_{k+1}, 2 H posted b_k, 3 W posted w_k,
+  // 4 S got w_k, 5 T got b_k
   long long* const stp = (a.timeline && a.timeline_iters >= 512) ? a.timeline + ((long)li * a.timeline_iters + 128) * 8
                                                                  : nullptr;
 #define REC_STAMP(col, sg_, k_)                                                                      \
@@ -1119,15 +1121,15 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
   double* const yring = lds + L.yring;
   double* const vring = lds + L.vring;
   double* const wring = lds + L.wring;
-  // This wave's register matrix (S: XB, T: B, V: P, W: XP), loaded at ONE place per loop (a conditional
+  // This wave's register matrix (S: XB, T: P, H: B, W: XP), loaded at ONE place per loop (a conditional
   // reload of a loop-carried register array made the compiler keep two copies and spill): refresh 0
   // before the first segment, then at the end of every segment the matrix of the next one (pc[PC_ENEXT],
   // the phase's idle time except after an urgent refresh).
   double Mq[4][QT];
-  const int part = wid == 0 ? 3 : wid == 1 ? 1 : wid == 2 ? 0 : 2;
+  const int part = wid == 0 ? 3 : wid == 1 ? 0 : wid == 2 ? 1 : 2;
   const double* const mimg = img0 + (long)part * QB;
   if (wid != 1) {
-    // ------------------------------------------------ S (wave 0), V (wave 2), W (wave 3)
+    // ------------------------------------------------ S (wave 0), H (wave 2), W (wave 3)
     const bool fast_sig = (a.dbg & 32) == 0;
     double* st = lds + L.stage;
     __builtin_amdgcn_s_setprio(2);
@@ -1155,14 +1157,16 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
           REC_STAMP(4, sg, k);
           z = ini ? (z - wring[(k % RR) * 64 + lane]) + u : 0.0;
         }
-      } else {  // V: v_k = P y_k;  W: w_k = XP y_k
+      } else {  // H (wave 2): b_k = B s_k;  W: w_k = XP y_k
         const int flag = wid == 2 ? PC_V : PC_W;
         double* ring = wid == 2 ? vring : wring;
+        const int src_flag = wid == 2 ? PC_S : PC_Y;
+        double* const src_ring = wid == 2 ? sring : yring;
         for (int k = 0;; ++k) {
-          const int got = wait_step(PC_Y, base + k + 1, sg);
+          const int got = wait_step(src_flag, base + k + 1, sg);
           if (got < 0) return;
           if (got == 0) break;
-          const double v = quad_gemv_staged<QT>(Mq, yring + (k % RR) * 4 * QX);
+          const double v = quad_gemv_staged<QT>(Mq, src_ring + (k % RR) * 4 * QX);
           ring[(k % RR) * 64 + lane] = v;
           lds_store_rel(&pc[flag], base + k + 1);
           REC_STAMP(wid, sg, k);
@@ -1192,7 +1196,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
           lds_store_rel(&pc[PC_WDONE], sg);  // T's quit waits for this (no request after the quit)
         }
       }
-      if (wid != 3) {  // S / V: the segment is over once T posted its end
+      if (wid != 3) {  // S / H: the segment is over once T posted its end
         for (int spin = 0;; ++spin) {
           if (lds_load_acq(&pc[PC_END]) >= sg) break;
           if ((spin & 63) == 63 && (lds_load_acq(&pc[PC_QUIT]) || now_ticks() > deadline)) return;
@@ -1224,6 +1228,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
   const int bg_steps = ((a.dbg >> 12) & 15) ? ((a.dbg >> 12) & 15)
                                             : (g.max_inner >= 1 && g.max_inner < NMAX) ? g.max_inner : REC_BG;
   const bool ns_bg = g.inner_tol >= 0.0;
+  const bool urgent_ns = ns_bg && (a.dbg & (1 << 16));  // GADMM_NEWTON_URGENT_NS=1
   auto wait_ready = [&](int r) -> bool {
     for (int spin = 0;; ++spin) {
       if (lds_load_acq(&nc.ready) >= r) {
@@ -1318,22 +1323,22 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
       lds_store_rel(&pc[PC_SEG], sg);
       yring[(lane & 3) * QX + (lane >> 2)] = inj ? fma(shift, x, cv) : 0.0;  // y_0 (slot 0)
       lds_store_rel(&pc[PC_Y], base + 1);
+      double v = quad_gemv_staged<QT>(Mq, yring);  // v_0 = P y_0 (T's register matrix: P)
       int reason = 0;  // 1: the solve ends, 2: urgent refresh
       for (int k = 0;; ++k) {
         const int want = base + k + 1;
-        bool got = lds_load_acq(&pc[PC_S]) >= want && lds_load_acq(&pc[PC_V]) >= want;
+        bool got = lds_load_acq(&pc[PC_V]) >= want;  // b_k = B s_k from H
         if (!got) {
           __builtin_amdgcn_s_setprio(0);
           for (int spin = 0;; ++spin) {
-            if (lds_load_acq(&pc[PC_S]) >= want && lds_load_acq(&pc[PC_V]) >= want) { got = true; break; }
+            if (lds_load_acq(&pc[PC_V]) >= want) { got = true; break; }
             if ((spin & 63) == 63 && now_ticks() > deadline) break;
           }
           __builtin_amdgcn_s_setprio(2);
         }
         if (!got) { abort = 1; break; }
         REC_STAMP(5, sg, k);
-        const double bs = quad_gemv_staged<QT>(Mq, sring + (k % RR) * 4 * QX);  // (B s_k)_j
-        const double dxl = inj ? vring[(k % RR) * 64 + lane] - bs : 0.0;
+        const double dxl = inj ? v - vring[(k % RR) * 64 + lane] : 0.0;  // dx_k = P y_k - B s_k
         x = inj ? x - dxl : 0.0;
         double* const ynext = yring + ((k + 1) % RR) * 4 * QX;
         ynext[(lane & 3) * QX + (lane >> 2)] = inj ? fma(shift, x, cv) : 0.0;
@@ -1345,6 +1350,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
         if (chord <= 0.0 || (!fresh && ks > 1 && mdx > chord * nd_prev)) { reason = 2; break; }
         fresh = false;
         nd_prev = mdx;
+        v = quad_gemv_staged<QT>(Mq, ynext);  // v_{k+1} = P y_{k+1}, while H waits for s_{k+1}
       }
       if (abort) break;
       lds[L.xfin + lane] = x;
@@ -1355,10 +1361,11 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
           if (!wait_ready(pend)) { abort = 1; break; }
           pend = -1;
         }
+        const int src_u = urgent_ns ? cur : -1;  // one Newton-Schulz step from the inverse in use, or exact
         cur = ++next_id;
         pc[PC_EKIND] = 0;
         pc[PC_EREQ] = cur;
-        pc[PC_ESRC] = -1;
+        pc[PC_ESRC] = src_u;
         pc[PC_ENEXT] = cur;
         pc[PC_EIT] = it;
         lds_store_rel(&pc[PC_END], sg);
@@ -1427,7 +1434,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  lds_store_rel(&pc[PC_QUIT], 1);  // S, V, W leave
+  lds_store_rel(&pc[PC_QUIT], 1);  // S, H, W leave
   lds_store_rel(&nc.quit, 1);      // the crew leaves after serving every request
   if (inj) {
     a.theta[(long)w * d + lane] = th;
@@ -1511,6 +1518,8 @@ int gadmm_chain_persistent_newton_launch(const PersistArgs* args, const LogiArgs
   if (rl && atoi(rl) > 0) ka.dbg |= (atoi(rl) & 15) << 8;
   const char* bg = getenv("GADMM_NEWTON_BG");
   if (bg && atoi(bg) > 0) ka.dbg |= (atoi(bg) & 15) << 12;
+  const char* un = getenv("GADMM_NEWTON_URGENT_NS");
+  if (un && un[0] == '1') ka.dbg |= 1 << 16;
   void* kargs[] = {&ka, const_cast<LogiArgs*>(&g)};
   GADMM_CHECK(hipLaunchKernel(fn, dim3(ka.xcd > 0 ? 8 * blocks : blocks), dim3(nt), kargs, shm, st));
   GADMM_CHECK(hipGetLastError());

@@ -2,7 +2,7 @@
 waits for whom inside a chord step. One exact-logistic solve (bench config logistic_exact) with
 timeline_iters = 512; for the first 24 segments of workers 0-7, the median over steps k >= 1 of
   S period (s_k post -> s_{k+1} post), T period (y post -> y post), and the hand-off lags
-  T got s_k & v_k  - S posted s_k        S got w_k - W posted w_k     V / W posted - T posted y_k
+  T got b_k - S posted s_k (H's b_k = B s_k between)   S got w_k - W posted w_k   W posted w - T posted y
 (s_memrealtime, 10 ns).  python tools/newton_rec_steps.py"""
 import os
 import sys
@@ -28,7 +28,7 @@ for rep in range(3):
     r = eng.run_persistent(timeline_iters=512)
     print("solve %d: %d iterations, %.2f ms" % (rep, r.iters, r.wall_ms))
 tl = eng.last_timeline[:8, 128:128 + 384, :].astype(np.float64).reshape(8, 24, 16, 8)
-names = ["S period", "T period", "T got s,v - S posted s", "T posted y -> V posted v", "T posted y -> W posted w",
+names = ["S period", "T period", "T got b - S posted s", "S posted s -> H posted b", "T posted y -> W posted w",
          "W posted w -> S got w", "S got w -> S posted next s"]
 vals = {k: [] for k in names}
 for w in range(8):
@@ -41,9 +41,9 @@ for w in range(8):
             if a[1] > 0 and b[1] > 0:
                 vals["T period"].append(b[1] - a[1])
             if a[5] > 0 and a[0] > 0:
-                vals["T got s,v - S posted s"].append(a[5] - a[0])
-            if a[1] > 0 and b[2] > 0:
-                vals["T posted y -> V posted v"].append(b[2] - a[1])
+                vals["T got b - S posted s"].append(a[5] - a[0])
+            if a[0] > 0 and a[2] > 0:
+                vals["S posted s -> H posted b"].append(a[2] - a[0])
             if a[1] > 0 and b[3] > 0:
                 vals["T posted y -> W posted w"].append(b[3] - a[1])
             if a[3] > 0 and a[4] > 0:
