@@ -1063,15 +1063,6 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
       __builtin_amdgcn_s_sleep(1);
     }
   };
-  // a pipeline wave's wait for segment `sg` to start (false: quit / deadline)
-  auto wait_seg = [&](int sg) -> bool {
-    for (int spin = 0;; ++spin) {
-      if (lds_load_acq(&pc[PC_SEG]) >= sg) return true;
-      if (lds_load_acq(&pc[PC_QUIT])) return false;
-      if ((spin & 63) == 63 && now_ticks() > deadline) return false;
-      __builtin_amdgcn_s_sleep(1);
-    }
-  };
   // a pipeline wave's wait for pc[flag] >= want; 1: there, 0: segment sg ended, -1: quit / deadline
   // Issue priorities: a pipeline wave computes at 2 and spins at 0, the crew runs at 1, so a spinning
   // wave never takes a SIMD's issue slot from the crew wave it shares the SIMD with, nor the crew one
@@ -1086,6 +1077,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
       if ((spin & 63) == 63) {
         if (lds_load_acq(&pc[PC_QUIT]) || now_ticks() > deadline) { res = -1; break; }
       }
+      if (spin >= 256) __builtin_amdgcn_s_sleep(1);  // a long wait (the idle phase): poll gently
     }
     __builtin_amdgcn_s_setprio(2);
     return res;
@@ -1135,8 +1127,10 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
     __builtin_amdgcn_s_setprio(2);
     if (!ready_or_quit(0)) return;
     load_img(Mq, mimg);
+    // No wait for the segment's start: s_0 = y sigma(-y z_0) and b_0 = B s_0 depend only on the start
+    // point (this worker's own iterate, exact margins from W) and the inverse announced at the previous
+    // segment's end, so S and H form them during the idle phase; W waits for y_0 (the neighbours' theta).
     for (int sg = 1;; ++sg) {
-      if (!wait_seg(sg)) return;
       const int base = sg * 1024;
       if (wid == 0) {  // S: the margins
         for (int spin = 0;; ++spin) {
@@ -1305,7 +1299,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
       tls[6] = t_nb;
       tls[7] = t_dec;
     }
-    if (pend >= 0 && it - pend_it >= RLAG) {  // adopt the background refresh (preloaded by S, V, W)
+    if (pend >= 0 && it - pend_it >= RLAG) {  // adopt the background refresh (preloaded by S, H, W)
       cur = pend;
       pend = -1;
       cur_fresh = false;
