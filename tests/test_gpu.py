@@ -303,6 +303,26 @@ def test_logistic_newton_kernel_matches_torch(log24, log_obj0, chord, persistent
           % (chord, persistent, a.wall_s * 1e3, t_torch * 1e3, a.iters))
 
 
+@pytest.mark.parametrize("rec,knobs", [("0", {}), ("1", {"GADMM_NEWTON_RLAG": "1", "GADMM_NEWTON_BG": "1"}),
+                                       ("1", {"GADMM_NEWTON_URGENT_NS": "1"})])
+def test_newton_persistent_variants_match_torch(log24, log_obj0, rec, knobs, monkeypatch):
+    """Both persistent exact-logistic kernels stay exact: the round-4 one-wave solver kernel
+    (GADMM_NEWTON_REC=0) and the four-wave pipeline under other refresh schedules (lag 1 / threshold 1,
+    urgent refreshes by Newton-Schulz) -- the schedule changes which inverse a chord step uses, never the
+    fixed point: 424 iterations and the torch trace to 1e-12."""
+    from gadmm_amd.models import LogisticRegression
+    from gadmm_amd.algorithms.gadmm import group_admm_logistic_exact
+    monkeypatch.setenv("GADMM_NEWTON_REC", rec)
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    m = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
+    a = group_admm_logistic_exact(m, 1e-3, log_obj0, 1e-8, 1000, engine_opts={"cache": False, "persistent": True})
+    assert a.extra["engine"] == "persistent", a.extra["engine"]
+    b = group_admm_logistic_exact(m, 1e-3, log_obj0, 1e-8, 1000, backend="torch")
+    assert a.iters == b.iters == 424 and a.converged
+    np.testing.assert_allclose(a.obj, b.obj, rtol=1e-12, atol=0)
+
+
 def test_lds_poison_lands():
     """The poison kernel really leaves NaN patterns in LDS: a probe kernel that reads LDS it never
     wrote finds them (otherwise the autouse poison fixture would be vacuous)."""
