@@ -666,7 +666,7 @@ constexpr int RR = 4;             // ring slots (a producer runs at most two ste
 constexpr int RSLOTS = 3;         // refresh images per worker
 constexpr int RIMG = 4 * QB;      // one image: P | B | XP | XB, quad-LDS layout each
 constexpr int REC_RLAG = 3;       // default refresh lag (iterations) and background-refresh step threshold: the
-constexpr int REC_BG = 3;         // best of a lag x threshold sweep (profiles/r05_l: 7.31 ms at 2 / 1, 6.02-6.07 at 3-4 / 3-4)
+constexpr int REC_BG = 4;         // best of lag x threshold sweeps (profiles/r05_l: r5ls4 5.48-5.49 ms at 3 / 4, 5.56 at 3 / 3)
 
 struct RLds {  // doubles
   int xt, xq, hs, hp, wq, slab, stage, sring, yring, vring, wring, z0v, xfin, total;
