@@ -688,7 +688,7 @@ struct RLds {  // doubles
   }
 };
 
-enum { PC_SEG, PC_CUR, PC_Z0, PC_S, PC_Y, PC_V, PC_W, PC_END, PC_QUIT, PC_EKIND, PC_EREQ, PC_ESRC, PC_ENEXT,
+enum { PC_Z0, PC_S, PC_Y, PC_V, PC_W, PC_END, PC_QUIT, PC_EKIND, PC_EREQ, PC_ESRC, PC_ENEXT,
        PC_EIT, PC_WDONE, PC_N };
 
 // Ordering of the refresh images, which never leave the CU (the crew stores them, waves of the same
@@ -1313,8 +1313,6 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
       if (tls && lane == 0 && ks == 0) tls[1] = (long long)__builtin_amdgcn_s_memrealtime();
       ++sg;
       const int base = sg * 1024;
-      pc[PC_CUR] = cur;
-      lds_store_rel(&pc[PC_SEG], sg);
       yring[(lane & 3) * QX + (lane >> 2)] = inj ? fma(shift, x, cv) : 0.0;  // y_0 (slot 0)
       lds_store_rel(&pc[PC_Y], base + 1);
       double v = quad_gemv_staged<QT>(Mq, yring);  // v_0 = P y_0 (T's register matrix: P)
