@@ -725,6 +725,19 @@ __device__ __forceinline__ double wave_max_abs_dpp(double v) {
   return fmax(a, b);
 }
 
+// A pipeline hand-off post without the release fence: a wave's LDS operations are performed in order,
+// so a flag written after the ring data cannot become visible before it (the fence's s_waitcnt only
+// held the flag back by one LDS round trip). The compiler barrier keeps the data stores first.
+// GADMM_NEWTON_POSTFENCE=1 (PersistArgs::dbg bit 17) restores the fenced post (A/B).
+__device__ __forceinline__ void lds_post(int* p, int v, bool fenced) {
+  if (fenced) {
+    lds_store_rel(p, v);
+    return;
+  }
+  asm volatile("" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // C (64 x 64 tile column cw) = A B over k < 4 QT (operands zero beyond d / m): acc[R][reg] =
 // C[16R + k4 + 4 reg][16 cw + c16]. The k loop is unrolled (a fixed 13 steps), so the operand LDS
 // reads of later steps are issued ahead of the MFMAs.
@@ -1052,6 +1065,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
   lds_barrier();  // the only workgroup-wide barrier
 
   const double yv = ini ? g.Y[(long)li * m + lane] : 0.0;
+  const bool post_fence = (a.dbg & (1 << 17)) != 0;
   auto ready_or_quit = [&](int r) -> bool {  // the crew finished refresh r (false: quit / deadline)
     for (int spin = 0;; ++spin) {
       if (lds_load_acq(&nc.ready) >= r) {
@@ -1142,7 +1156,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
           const double sv = ini ? (fast_sig ? yv * inv1pexp_fast(yv * z) : yv / (1.0 + exp(yv * z))) : 0.0;
           double* slot = sring + (k % RR) * 4 * QX;
           slot[(lane & 3) * QX + (lane >> 2)] = sv;
-          lds_store_rel(&pc[PC_S], base + k + 1);
+          lds_post(&pc[PC_S], base + k + 1, post_fence);
           REC_STAMP(0, sg, k);
           const double u = quad_gemv_staged<QT>(Mq, slot);  // (XB s_k)_i
           const int got = wait_step(PC_W, base + k + 1, sg);
@@ -1162,7 +1176,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
           if (got == 0) break;
           const double v = quad_gemv_staged<QT>(Mq, src_ring + (k % RR) * 4 * QX);
           ring[(k % RR) * 64 + lane] = v;
-          lds_store_rel(&pc[flag], base + k + 1);
+          lds_post(&pc[flag], base + k + 1, post_fence);
           REC_STAMP(wid, sg, k);
         }
         if (wid == 3) {  // W: the segment's end -- exact margins at its final iterate
@@ -1314,7 +1328,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
       ++sg;
       const int base = sg * 1024;
       yring[(lane & 3) * QX + (lane >> 2)] = inj ? fma(shift, x, cv) : 0.0;  // y_0 (slot 0)
-      lds_store_rel(&pc[PC_Y], base + 1);
+      lds_post(&pc[PC_Y], base + 1, post_fence);
       double v = quad_gemv_staged<QT>(Mq, yring);  // v_0 = P y_0 (T's register matrix: P)
       int reason = 0;  // 1: the solve ends, 2: urgent refresh
       for (int k = 0;; ++k) {
@@ -1334,7 +1348,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
         x = inj ? x - dxl : 0.0;
         double* const ynext = yring + ((k + 1) % RR) * 4 * QX;
         ynext[(lane & 3) * QX + (lane >> 2)] = inj ? fma(shift, x, cv) : 0.0;
-        lds_store_rel(&pc[PC_Y], want + 1);
+        lds_post(&pc[PC_Y], want + 1, post_fence);
         REC_STAMP(1, sg, k);
         const double mdx = wave_max_abs_dpp(dxl), mx = wave_max_abs_dpp(x);
         used = ++ks;
@@ -1510,6 +1524,8 @@ int gadmm_chain_persistent_newton_launch(const PersistArgs* args, const LogiArgs
   if (rl && atoi(rl) > 0) ka.dbg |= (atoi(rl) & 15) << 8;
   const char* bg = getenv("GADMM_NEWTON_BG");
   if (bg && atoi(bg) > 0) ka.dbg |= (atoi(bg) & 15) << 12;
+  const char* pf = getenv("GADMM_NEWTON_POSTFENCE");
+  if (pf && pf[0] == '1') ka.dbg |= 1 << 17;
   const char* un = getenv("GADMM_NEWTON_URGENT_NS");
   if (un && un[0] == '1') ka.dbg |= 1 << 16;
   void* kargs[] = {&ka, const_cast<LogiArgs*>(&g)};
