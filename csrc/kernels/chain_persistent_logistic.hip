@@ -571,6 +571,19 @@ __device__ __forceinline__ void zr_store_rel(int* p, int v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
+// The per-step ring posts (s produced, s consumed) without the release fence: a wave's LDS operations
+// are performed in order, so the flag cannot become visible before the slot data written (or read)
+// before it; the fence only held the flag back by one LDS round trip on the margins wave's chain.
+// GADMM_LOGISTIC_POSTFENCE=1 (PersistArgs::dbg bit 17) restores the fenced posts (A/B).
+__device__ __forceinline__ void zr_post(int* p, int v, bool fenced) {
+  if (fenced) {
+    zr_store_rel(p, v);
+    return;
+  }
+  asm volatile("" ::: "memory");
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // s = y / (1 + e^{y z}) on the margins wave's critical path: inv1pexp_fast (fast_sigm.h). Measured 5.64 ->
 // 5.21 ms on E3, one box (profiles/r05_j/r5jf); the default (GADMM_LOGISTIC_FASTSIGM=0: libm exp and
 // the IEEE quotient). The traces stay within 1e-12 of torch.
@@ -648,6 +661,7 @@ __global__ void __launch_bounds__(ZR_NT) chain_persistent_logistic_zrec_kernel(P
   const double* Xg = g.X + (long)li * m * d;
   const bool inj = lane < d, ini = lane < m;
   const double yv = ini ? g.Y[(long)li * m + lane] : 0.0;
+  const bool post_fence = (a.dbg & (1 << 17)) != 0;
   if (threadIdx.x < 8) ctl[threadIdx.x] = 0;
   __syncthreads();
 
@@ -691,7 +705,7 @@ __global__ void __launch_bounds__(ZR_NT) chain_persistent_logistic_zrec_kernel(P
         }
         double* slot = sring + (k % ZR_SLOTS) * 4 * QX;
         slot[(lane & 3) * QX + (lane >> 2)] = sv;  // quad_gemv's x layout: both waves' GEMVs read it in place
-        zr_store_rel(&ctl[1], sid * 1024 + k + 1);
+        zr_post(&ctl[1], sid * 1024 + k + 1, post_fence);
         const double u = quad_gemv_staged<T>(Kq, slot);  // (K s)_i
         if (k == 0) {  // c = X sh arrives after z_0 (the iterate wave posts z_0 first)
           for (int spin = 0;; ++spin) {
@@ -802,7 +816,7 @@ __global__ void __launch_bounds__(ZR_NT) chain_persistent_logistic_zrec_kernel(P
       }
       if (!got) { abort = 1; break; }
       const double gx = quad_gemv_staged<T>(XTq, sring + (k % ZR_SLOTS) * 4 * QX);
-      zr_store_rel(&ctl[2], want);  // (the release waits for this GEMV's reads of the slot)
+      zr_post(&ctl[2], want, post_fence);  // (after this GEMV's reads of the slot, LDS in order)
       bool conv = true;
       if (inj) {
         const double gr = -gx + lam * x + sh;
@@ -958,6 +972,8 @@ int gadmm_chain_persistent_logistic_launch(const PersistArgs* args, const LogiAr
   if (ka.xcd > 1) GADMM_CHECK(hipMemsetAsync(a.xchk, 0, (size_t)XCHK * 16, st));
   const char* fs = getenv("GADMM_LOGISTIC_FASTSIGM");
   if (fs && fs[0] == '0') ka.dbg |= 32;
+  const char* pf = getenv("GADMM_LOGISTIC_POSTFENCE");
+  if (pf && pf[0] == '1') ka.dbg |= 1 << 17;
   void* kargs[] = {&ka, const_cast<LogiArgs*>(&g)};
   GADMM_CHECK(hipLaunchKernel(fn, dim3(ka.xcd > 0 ? 8 * blocks : blocks), dim3(logi_threads()), kargs, shm, st));
   GADMM_CHECK(hipGetLastError());
