@@ -107,8 +107,11 @@ def main():
         sys.exit(2)
     # GADMM_BENCH_SHARE_GPU=1: rehearsal of the multi-rank path with every rank on cuda:0 (one-GPU
     # development box). RCCL refuses two ranks on one device, so there the fallback is the IPC transport.
-    share = os.environ.get("GADMM_BENCH_SHARE_GPU") == "1"
-    dev_index = 0 if share else local_rank
+    from gadmm_amd.parallel.node import select_device_index, share_requested
+    share = share_requested()
+    # local_rank % visible devices: every GPU visible -> rank r on device r; a per-process
+    # HIP_VISIBLE_DEVICES (one visible device) -> device 0 (counting devices does not initialise HIP)
+    dev_index = select_device_index(local_rank, share, torch.cuda.device_count())
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
     if world > 1:
@@ -171,10 +174,11 @@ def _headline_candidates(args, X_cpu, y_cpu, local, placement, rank, world, devi
             cands.append(dict(name="replicated-halo-k%d%s" % (k, "-pw2" if pw == 2 else ""), build=replicated(k, pw),
                               hops=1.0 / k, base="paired" if pw == 2 else "blocked"))
     if os.environ.get("GADMM_TOURNAMENT_GRAPH", "1") != "0":
-        # the graph-replayed phase kernels over the node's data planes (measured, never expected to win):
-        # the IPC transport always, RCCL on distinct GPUs (non-blocking, watchdog-bounded waits)
+        # the graph-replayed phase kernels over the node's default data plane, the IPC transport
+        # (measured, never expected to win). RCCL (graph-rccl) only on request -- GADMM_TOURNAMENT_RCCL=1
+        # or --fabric rccl, on distinct GPUs: the default run builds no RCCL communicator at all
         cands.append(dict(name="graph-ipc", build=make("graph", fabric="ipc"), hops=2.0, base=None))
-        if not share:
+        if not share and (args.fabric == "rccl" or os.environ.get("GADMM_TOURNAMENT_RCCL") == "1"):
             cands.append(dict(name="graph-rccl", build=make("graph", fabric="rccl"), hops=2.0, base=None))
     return cands
 
@@ -194,13 +198,14 @@ def run_headline(args, rank, world, device, share):
         # one-way hop latency of every chain boundary (the quantity that decides the engine ranking)
         from gadmm_amd.parallel.hop_probe import hop_probe
         hop = hop_probe(rank, world, device)
-    sol, tournament, winner = None, None, None
+    sol, tournament, winner, tour_wall_s = None, None, None, None
     if world > 1 and args.engine == "auto":
         # untimed: build and time every eligible multi-GPU engine, agree on the fastest (max over ranks).
         # A candidate that stalls (e.g. a persistent kernel whose peers cannot be co-resident with ranks
         # time-sharing one GPU) fails within the tournament's 5 s deadline instead of the full one; the
         # winner is then REBUILT with the requested --timeout for the warm-up and the timed solves.
         from gadmm_amd.engine.tournament import engine_tournament
+        t_tour = time.perf_counter()
         cands = _headline_candidates(args, X_cpu, y_cpu, local, placement, rank, world, device, share, obj0)
         log = (lambda msg: print("bench.py: " + msg, file=sys.stderr, flush=True)) if rank == 0 else None
         winner, sol, tournament = engine_tournament([(c["name"], (lambda b=c["build"]: b(tour_timeout_s)))
@@ -217,6 +222,7 @@ def run_headline(args, rank, world, device, share):
         if sol is not None:
             sol.close()  # rebuilt below with the requested hand-off deadline (collective)
             sol = info[winner]["build"](timeout_s)
+        tour_wall_s = time.perf_counter() - t_tour  # builds + untimed solves of every candidate + the rebuild
     if sol is None:
         halo = None
         if args.engine == "replicated-halo" and world > 1:
@@ -334,6 +340,8 @@ def run_headline(args, rank, world, device, share):
             out["engine_tournament"] = tournament  # every candidate's untimed-warm-up time (max over ranks)
             out["tournament_winner"] = winner
             out["tournament_deadline_s"] = tour_timeout_s
+            out["tournament_wall_s"] = round(tour_wall_s, 3)
+            out["rccl_built"] = any(c["name"] == "graph-rccl" for c in tournament)
         out["handoff_deadline_s"] = timeout_s  # the deadline of the warm-up and timed solves
         print(json.dumps(out), flush=True)
     sol.close()

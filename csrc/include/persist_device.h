@@ -14,6 +14,18 @@
 #include "gadmm_chain.h"
 #include "quad_gemv.h"
 
+// The fence-free LDS ring posts (chain_persistent_logistic.hip: zr_post, chain_persistent_newton.hip:
+// lds_post) rely on one hardware property: the LDS instructions of ONE wave are performed in issue order
+// (CDNA3 / CDNA4: the property every counted `s_waitcnt lgkmcnt(N)` on a wave's LDS traffic relies on,
+// cdna_hip_programming.md §5). The HIP / LLVM memory model does not promise it, so it is enabled only
+// for the architectures whose ISA documents it; any other target compiles the fenced (release) post.
+// tests/test_gpu.py::test_postfence_stress checks the two posts give bit-identical traces on gfx950.
+#if defined(__gfx950__) || defined(__gfx942__)
+#define GADMM_LDS_IN_ORDER 1
+#else
+#define GADMM_LDS_IN_ORDER 0
+#endif
+
 namespace persist {
 
 

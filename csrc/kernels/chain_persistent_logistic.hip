@@ -576,7 +576,7 @@ __device__ __forceinline__ void zr_store_rel(int* p, int v) {
 // before it; the fence only held the flag back by one LDS round trip on the margins wave's chain.
 // GADMM_LOGISTIC_POSTFENCE=1 (PersistArgs::dbg bit 17) restores the fenced posts (A/B).
 __device__ __forceinline__ void zr_post(int* p, int v, bool fenced) {
-  if (fenced) {
+  if (fenced || !GADMM_LDS_IN_ORDER) {  // fence-free only where in-order LDS is documented
     zr_store_rel(p, v);
     return;
   }

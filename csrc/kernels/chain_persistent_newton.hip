@@ -730,7 +730,7 @@ __device__ __forceinline__ double wave_max_abs_dpp(double v) {
 // held the flag back by one LDS round trip). The compiler barrier keeps the data stores first.
 // GADMM_NEWTON_POSTFENCE=1 (PersistArgs::dbg bit 17) restores the fenced post (A/B).
 __device__ __forceinline__ void lds_post(int* p, int v, bool fenced) {
-  if (fenced) {
+  if (fenced || !GADMM_LDS_IN_ORDER) {  // fence-free only where in-order LDS is documented
     lds_store_rel(p, v);
     return;
   }

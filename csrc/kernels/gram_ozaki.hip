@@ -75,11 +75,12 @@ __global__ void __launch_bounds__(CE_NT) oz_colmax_part(const double* X, const d
 
 // e_j with max |x_ij| <= (127/128) 2^{e_j}, 0 for an all-zero column: the first round-to-nearest digit
 // then stays within [-127, 127]
-__global__ void __launch_bounds__(CE_NT) oz_colexp(const double* part, int Dp, int* e) {
+__global__ void __launch_bounds__(CE_NT) oz_colexp(const double* part, int Dp, int* e, double* cm) {
   const int j = blockIdx.x * CE_NT + threadIdx.x;
   if (j >= Dp) return;
   double mx = 0.0;
   for (int r = 0; r < CE_R; ++r) mx = fmax(mx, part[(long)r * Dp + j]);
+  cm[j] = mx;
   int E = 0;
   if (mx > 0.0) {
     const double f = frexp(mx, &E);  // mx = f 2^E, f in [0.5, 1)
@@ -222,226 +223,6 @@ __global__ void __launch_bounds__(GEMM_NT, 2) oz_gemm(const signed char* S, int 
   }
 }
 
-// Variant 2 (GADMM_OZ_GEMM=2): one wave per SIMD with a 32 x 64 output (one A block against two B
-// blocks: each A fragment feeds 14 MFMAs, 0.375 fragment reads per MFMA instead of 0.5), 4 waves on a
-// 64 x 128 tile, the digit panels global -> LDS by LDS-DMA (global_load_lds_dwordx4, no staging
-// registers) through a 3-stage ring: per 32-sample step a counted vmcnt (this wave's DMAs of the step
-// retired, the next step's still in flight), a raw s_barrier (everyone's landed; everyone is done
-// reading the stage the step after next overwrites), then the DMAs of the step after next. A stage is
-// 42 fragments of 1 KB (A: 7 slices x 2 blocks, B: 7 x 4), 11 DMAs per wave (the last two of waves 2
-// and 3 repeat fragments 0 and 1: the same bytes to the same place).
-constexpr int G2_TA = 64, G2_TB = 128, G2_NT = 256;
-constexpr int G2_FRA = SL * 2, G2_FRB = SL * 4, G2_FR = G2_FRA + G2_FRB;  // fragments per stage
-constexpr int G2_DMA = (G2_FR + 3) / 4;                                    // per wave per stage (11)
-constexpr int G2_STAGE = G2_FR * 64;                                       // v4i per stage
-
-__global__ void __launch_bounds__(G2_NT) oz_gemm2(const signed char* S, int Dp, int tiles, const int2* list, int kbn,
-                                                  const int* e, double* C) {
-  extern __shared__ __attribute__((aligned(16))) v4i lds4[];  // 3 stages
-  const int per_xcd = (tiles + 7) / 8;
-  const int t = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
-  if (t >= tiles) return;
-  const int ti = list[t].x, tj = list[t].y;
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wa = wv >> 1, wb = wv & 1;  // wave-uniform
-  const int a0 = ti * G2_TA + wa * 32, b0 = tj * G2_TB + wb * 64;
-  const bool work = a0 >= b0;  // (a0, b0) on or below the diagonal; (a0, b0 + 32) may be above: harmless
-  const int r = lane & 31, h = lane >> 5;
-  // this wave's DMA fragments: f = wv + 4 u (f >= 42: f - 42), per-lane offsets without the step term
-  unsigned off[G2_DMA];
-#pragma unroll
-  for (int u = 0; u < G2_DMA; ++u) {
-    int f = wv + 4 * u;
-    if (f >= G2_FR) f -= G2_FR;
-    int p, j;
-    if (f < G2_FRA) {
-      p = f / 2;
-      j = ti * G2_TA + (f % 2) * 32 + r;
-    } else {
-      p = (f - G2_FRA) / 4;
-      j = tj * G2_TB + ((f - G2_FRA) % 4) * 32 + r;
-    }
-    off[u] = (unsigned)(((long)p * KBC * Dp + j) * 32 + 16 * h);
-  }
-  auto issue = [&](int kb, int st) {
-    const signed char* base = S + (long)kb * Dp * 32;  // wave-uniform
-#pragma unroll
-    for (int u = 0; u < G2_DMA; ++u) {
-      int f = wv + 4 * u;  // wave-uniform: the fragment's v4i offset in the stage (lane-linear: + lane)
-      if (f >= G2_FR) f -= G2_FR;
-      __builtin_amdgcn_global_load_lds(base + off[u], lds4 + st * G2_STAGE + f * 64, 16, 0, 0);
-    }
-  };
-  v16i acc[2][SL];
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int L = 0; L < SL; ++L) acc[q][L] = v16i{};
-  issue(0, 0);
-  if (kbn > 1) issue(1, 1);
-  int cur = 0;
-  for (int kb = 0; kb < kbn; ++kb) {
-    if (kb + 1 < kbn) {
-      asm volatile("s_waitcnt vmcnt(11)" ::: "memory");  // G2_DMA: this wave's DMAs of step kb + 1 may fly
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();  // everyone's DMAs of kb landed; everyone is done reading kb - 1
-    if (kb + 2 < kbn) issue(kb + 2, cur == 0 ? 2 : cur - 1);
-    {  // every wave multiplies (no branch around the MFMAs: across one, hipcc shuttled all 224
-       // accumulator registers between AGPRs and VGPRs every step); a wave above the diagonal discards
-      const v4i* PA = lds4 + cur * G2_STAGE;
-      const v4i* PB = PA + G2_FRA * 64;
-      v4i fa[SL], fb[2][SL];
-#pragma unroll
-      for (int p = 0; p < SL; ++p) {
-        fa[p] = PA[((p * 2 + wa) * 2 + h) * 32 + r];
-        fb[0][p] = PB[((p * 4 + 2 * wb) * 2 + h) * 32 + r];
-        fb[1][p] = PB[((p * 4 + 2 * wb + 1) * 2 + h) * 32 + r];
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int p = 0; p < SL; ++p)
-#pragma unroll
-        for (int q = 0; q < SL - p; ++q) {
-          acc[0][p + q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[p], fb[0][q], acc[0][p + q], 0, 0, 0);
-          acc[1][p + q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[p], fb[1][q], acc[1][p + q], 0, 0, 0);
-        }
-      __builtin_amdgcn_s_setprio(0);
-    }
-    cur = cur == 2 ? 0 : cur + 1;
-  }
-  if (!work) return;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int col = b0 + 32 * q + r;
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int row = a0 + (g & 3) + 8 * (g >> 2) + 4 * h;
-      double v = 0.0;
-#pragma unroll
-      for (int L = SL - 1; L >= 0; --L) v = fma((double)acc[q][L][g], ldexp(1.0, -7 * (L + 2)), v);
-      C[(long)row * Dp + col] += ldexp(v, e[row] + e[col]);
-    }
-  }
-}
-
-// Variant 3 (GADMM_OZ_GEMM=3): variant 2 with the fragment reads software-pipelined: step k's MFMAs run
-// on fragments read during step k - 1 (two register sets, 84 VGPRs each; the accumulators stay in
-// AGPRs), while stage k + 1 is read; the ring then holds stage k + 1 (being read), k + 2 (DMA in flight)
-// and k + 3 (issued into step k's buffer, whose reads the lgkmcnt before the barrier retired).
-struct OzFrag {
-  v4i a[SL], b[2][SL];
-};
-
-__device__ __forceinline__ void oz_read_frags(OzFrag& F, const v4i* stage, int wa, int wb, int h, int r) {
-  const v4i* PA = stage;
-  const v4i* PB = stage + G2_FRA * 64;
-#pragma unroll
-  for (int p = 0; p < SL; ++p) {
-    F.a[p] = PA[((p * 2 + wa) * 2 + h) * 32 + r];
-    F.b[0][p] = PB[((p * 4 + 2 * wb) * 2 + h) * 32 + r];
-    F.b[1][p] = PB[((p * 4 + 2 * wb + 1) * 2 + h) * 32 + r];
-  }
-}
-
-__device__ __forceinline__ void oz_mfma_frags(v16i (&acc)[2][SL], const OzFrag& F) {
-#pragma unroll
-  for (int p = 0; p < SL; ++p)
-#pragma unroll
-    for (int q = 0; q < SL - p; ++q) {
-      acc[0][p + q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(F.a[p], F.b[0][q], acc[0][p + q], 0, 0, 0);
-      acc[1][p + q] = __builtin_amdgcn_mfma_i32_32x32x32_i8(F.a[p], F.b[1][q], acc[1][p + q], 0, 0, 0);
-    }
-}
-
-__global__ void __launch_bounds__(G2_NT) oz_gemm3(const signed char* S, int Dp, int tiles, const int2* list, int kbn,
-                                                  const int* e, double* C) {
-  extern __shared__ __attribute__((aligned(16))) v4i lds4[];  // 3 stages
-  const int per_xcd = (tiles + 7) / 8;
-  const int t = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
-  if (t >= tiles) return;
-  const int ti = list[t].x, tj = list[t].y;
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), wa = wv >> 1, wb = wv & 1;
-  const int a0 = ti * G2_TA + wa * 32, b0 = tj * G2_TB + wb * 64;
-  const bool work = a0 >= b0;
-  const int r = lane & 31, h = lane >> 5;
-  unsigned off[G2_DMA];
-#pragma unroll
-  for (int u = 0; u < G2_DMA; ++u) {
-    int f = wv + 4 * u;
-    if (f >= G2_FR) f -= G2_FR;
-    int p, j;
-    if (f < G2_FRA) {
-      p = f / 2;
-      j = ti * G2_TA + (f % 2) * 32 + r;
-    } else {
-      p = (f - G2_FRA) / 4;
-      j = tj * G2_TB + ((f - G2_FRA) % 4) * 32 + r;
-    }
-    off[u] = (unsigned)(((long)p * KBC * Dp + j) * 32 + 16 * h);
-  }
-  auto issue = [&](int kb) {
-    const signed char* base = S + (long)kb * Dp * 32;
-    const int st = kb % 3;
-#pragma unroll
-    for (int u = 0; u < G2_DMA; ++u) {
-      int f = wv + 4 * u;
-      if (f >= G2_FR) f -= G2_FR;
-      __builtin_amdgcn_global_load_lds(base + off[u], lds4 + st * G2_STAGE + f * 64, 16, 0, 0);
-    }
-  };
-  v16i acc[2][SL];
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int L = 0; L < SL; ++L) acc[q][L] = v16i{};
-  for (int s = 0; s < 3 && s < kbn; ++s) issue(s);
-  // stage 0 landed (this wave: the later stages' DMAs may fly), everyone's: the barrier
-  if (kbn > 2) asm volatile("s_waitcnt vmcnt(22)" ::: "memory");
-  else if (kbn > 1) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  OzFrag F0, F1;
-  oz_read_frags(F0, lds4, wa, wb, h, r);
-  // one step: retire stage k + 1 (+ everyone's reads of stage k), issue k + 3 into stage k's buffer,
-  // read stage k + 1 into Fn, multiply Fc
-  auto step = [&](int k, OzFrag& Fc, OzFrag& Fn) {
-    if (k + 1 < kbn) {
-      if (k + 2 < kbn) asm volatile("s_waitcnt vmcnt(11)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this wave's reads of stage k are done
-    __builtin_amdgcn_s_barrier();
-    if (k + 3 < kbn) issue(k + 3);
-    if (k + 1 < kbn) oz_read_frags(Fn, lds4 + ((k + 1) % 3) * G2_STAGE, wa, wb, h, r);
-    __builtin_amdgcn_s_setprio(1);
-    oz_mfma_frags(acc, Fc);
-    __builtin_amdgcn_s_setprio(0);
-  };
-  int k = 0;
-  for (; k + 1 < kbn; k += 2) {
-    step(k, F0, F1);
-    step(k + 1, F1, F0);
-  }
-  if (k < kbn) step(k, F0, F1);
-  if (!work) return;
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const int col = b0 + 32 * q + r;
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int row = a0 + (g & 3) + 8 * (g >> 2) + 4 * h;
-      double v = 0.0;
-#pragma unroll
-      for (int L = SL - 1; L >= 0; --L) v = fma((double)acc[q][L][g], ldexp(1.0, -7 * (L + 2)), v);
-      C[(long)row * Dp + col] += ldexp(v, e[row] + e[col]);
-    }
-  }
-}
-
 // C (Dp x Dp, lower triangle) -> A (d x d, full symmetric), b (d), yy
 __global__ void __launch_bounds__(256) oz_finish(const double* C, int Dp, int d, double* A, double* b, double* yy) {
   const long idx = (long)blockIdx.x * 256 + threadIdx.x;
@@ -455,6 +236,27 @@ __global__ void __launch_bounds__(256) oz_finish(const double* C, int Dp, int d,
   } else if (idx == dd + d) {
     yy[0] = C[(long)d * Dp + d];
   }
+}
+
+// The column-range statistic of the gate (linalg.gram): max_j colmax_j / rms_j over the augmented
+// columns j <= d, rms_j = sqrt(C_jj / m) from the Gram's own diagonal. The digits keep 49 bits of every
+// value relative to its column's scale 2^{e_j} >= colmax_j, so an entry at the column's rms level keeps
+// about 49 - log2(range) bits; the caller recomputes with the f64-MFMA Gram past its threshold.
+__global__ void __launch_bounds__(256) oz_range(const double* cm, const double* C, int Dp, int d, long m,
+                                                double* out) {
+  __shared__ double red[256];
+  double r = 0.0;
+  for (int j = threadIdx.x; j <= d; j += 256) {
+    const double cjj = C[(long)j * Dp + j];
+    if (cjj > 0.0) r = fmax(r, cm[j] / sqrt(cjj / (double)m));
+  }
+  red[threadIdx.x] = r;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) red[threadIdx.x] = fmax(red[threadIdx.x], red[threadIdx.x + w]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
 }
 
 }  // namespace
@@ -486,53 +288,26 @@ const int2* oz_tile_list(int nt) {
   return d;
 }
 
-// Variant 2's tiles: (ti, tj) over 64-row x 128-column tiles with 128 tj <= 64 ti + 63 (some block on or
-// below the diagonal), in 8 x 4 super-blocks.
-const int2* oz_tile_list2(int nta, int ntb, int* count) {
-  static std::mutex mu;
-  static std::map<long, std::pair<int2*, int>> cache;
-  std::lock_guard<std::mutex> g(mu);
-  const long key = (long)nta * 100003 + ntb;
-  auto it = cache.find(key);
-  if (it != cache.end()) {
-    *count = it->second.second;
-    return it->second.first;
-  }
-  std::vector<int2> L;
-  for (int I = 0; I < (nta + 7) / 8; ++I)
-    for (int J = 0; J < (ntb + 3) / 4; ++J)
-      for (int i = I * 8; i < std::min((I + 1) * 8, nta); ++i)
-        for (int j = J * 4; j < std::min((J + 1) * 4, ntb); ++j)
-          if ((long)G2_TB * j <= (long)G2_TA * i + G2_TA - 1) L.push_back(int2{i, j});
-  int2* d = nullptr;
-  if (L.empty() || hipMalloc(&d, L.size() * sizeof(int2)) != hipSuccess) return nullptr;
-  if (hipMemcpy(d, L.data(), L.size() * sizeof(int2), hipMemcpyHostToDevice) != hipSuccess) {
-    (void)hipFree(d);
-    return nullptr;
-  }
-  cache[key] = {d, (int)L.size()};
-  *count = (int)L.size();
-  return d;
-}
-
 extern "C" {
 
 // Workspace bytes of gadmm_gram_ozaki_f64 for a shard of m x d (plus y): the f64 Gram of the padded
 // augmented matrix, two chunk buffers of digits, the column-max partials and exponents.
 long gadmm_gram_ozaki_workspace(long m, int d) {
   (void)m;
-  const long Dp = ((long)d + 1 + G2_TB - 1) / G2_TB * G2_TB;
-  return Dp * Dp * 8 + 2L * SL * KC * Dp + (long)CE_R * Dp * 8 + Dp * 4 + 256;
+  const long Dp = ((long)d + 1 + OT - 1) / OT * OT;
+  return Dp * Dp * 8 + 2L * SL * KC * Dp + (long)CE_R * Dp * 8 + Dp * 4 + Dp * 8 + 256;
 }
 
 // A_n = X_n^T X_n, b_n = X_n^T y_n, yy_n = y_n^T y_n for N shards X (N x m x d, row-major f64) on the
 // int8 matrix cores (see the file comment). Deterministic (fixed chunk order, exact int32 sums).
+// ``range_out`` (optional, N doubles): each shard's column-range statistic (oz_range) for the caller's
+// accuracy gate.
 // The memory-bound digit slicing of chunk c + 1 runs on a side stream into the other digit buffer
 // while the MFMA-bound oz_gemm of chunk c runs on `st` (r05_h3: slicing was 11 % of the serial time).
 int gadmm_gram_ozaki_f64(const double* X, const double* Y, int N, long m, int d, double* A, double* B, double* YY,
-                         void* ws, long ws_bytes, hipStream_t st) {
+                         void* ws, long ws_bytes, double* range_out, hipStream_t st) {
   if (N <= 0 || m <= 0 || d <= 0) return 0;
-  const int Dp = (d + 1 + G2_TB - 1) / G2_TB * G2_TB;  // a multiple of both variants' tiles
+  const int Dp = (d + 1 + OT - 1) / OT * OT;  // a multiple of the tile
   if (!X || !Y || !A || !B || !YY || !ws || ws_bytes < gadmm_gram_ozaki_workspace(m, d)) {
     gadmm_set_error("gram_ozaki: bad arguments or workspace (%ld < %ld bytes)", ws_bytes,
                     gadmm_gram_ozaki_workspace(m, d));
@@ -548,6 +323,7 @@ int gadmm_gram_ozaki_f64(const double* X, const double* Y, int N, long m, int d,
                           (signed char*)(w + (long)Dp * Dp * 8 + (long)SL * KC * Dp)};
   double* part = (double*)(w + (long)Dp * Dp * 8 + 2L * SL * KC * Dp);
   int* e = (int*)((char*)part + (long)CE_R * Dp * 8);
+  double* cm = (double*)((char*)e + ((long)Dp * 4 + 255) / 256 * 256);  // column maxima (the range gate)
   const int nt = Dp / OT;
   const int tiles = nt * (nt + 1) / 2;
   const int2* list = oz_tile_list(nt);
@@ -556,14 +332,6 @@ int gadmm_gram_ozaki_f64(const double* X, const double* Y, int N, long m, int d,
     return -1;
   }
   const size_t shm = (size_t)2 * 2 * SL * (OT / 32) * 2 * 32 * sizeof(v4i);  // 57,344 B: two per CU
-  const int variant = getenv("GADMM_OZ_GEMM") ? atoi(getenv("GADMM_OZ_GEMM")) : 1;  // A/B: read per call
-  const size_t shm2 = (size_t)3 * G2_STAGE * sizeof(v4i);  // 129,024 B: one per CU
-  int tiles2 = 0;
-  const int2* list2 = variant >= 2 ? oz_tile_list2(Dp / G2_TA, Dp / G2_TB, &tiles2) : nullptr;
-  if (variant >= 2 && !list2) {
-    gadmm_set_error("gram_ozaki: tile list allocation failed");
-    return -1;
-  }
   // side stream + events, per device and process-wide: one caller at a time (the lock spans fork ... join)
   static std::mutex mu;
   std::lock_guard<std::mutex> lock(mu);
@@ -582,8 +350,6 @@ int gadmm_gram_ozaki_f64(const double* X, const double* Y, int N, long m, int d,
   }
   if (!attr[dev]) {
     GADMM_CHECK(hipFuncSetAttribute((const void*)oz_gemm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
-    GADMM_CHECK(hipFuncSetAttribute((const void*)oz_gemm2, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm2));
-    GADMM_CHECK(hipFuncSetAttribute((const void*)oz_gemm3, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm2));
     attr[dev] = true;
   }
   hipStream_t s2 = side[dev];
@@ -594,7 +360,7 @@ int gadmm_gram_ozaki_f64(const double* X, const double* Y, int N, long m, int d,
     const double* Yn = Y + (long)n * m;
     hipLaunchKernelGGL(oz_colmax_part, dim3((Dp + CE_NT - 1) / CE_NT, CE_R), dim3(CE_NT), 0, st, Xn, Yn, (int)m, d,
                        Dp, part);
-    hipLaunchKernelGGL(oz_colexp, dim3((Dp + CE_NT - 1) / CE_NT), dim3(CE_NT), 0, st, part, Dp, e);
+    hipLaunchKernelGGL(oz_colexp, dim3((Dp + CE_NT - 1) / CE_NT), dim3(CE_NT), 0, st, part, Dp, e, cm);
     GADMM_CHECK(hipMemsetAsync(C, 0, (size_t)Dp * Dp * 8, st));
     GADMM_CHECK(hipEventRecord(ev_fork, st));
     hipError_t rc = hipStreamWaitEvent(s2, ev_fork, 0);
@@ -603,15 +369,8 @@ int gadmm_gram_ozaki_f64(const double* X, const double* Y, int N, long m, int d,
         rc = hipStreamWaitEvent(st, ev_s[c & 1], 0);
         if (rc != hipSuccess) break;
         const int kbn = (int)((std::min<long>(KC, m - (long)c * KC) + 31) / 32);
-        if (variant == 3)
-          hipLaunchKernelGGL(oz_gemm3, dim3(8 * ((tiles2 + 7) / 8)), dim3(G2_NT), shm2, st, Sbuf[c & 1], Dp, tiles2,
-                             list2, kbn, e, C);
-        else if (variant == 2)
-          hipLaunchKernelGGL(oz_gemm2, dim3(8 * ((tiles2 + 7) / 8)), dim3(G2_NT), shm2, st, Sbuf[c & 1], Dp, tiles2,
-                             list2, kbn, e, C);
-        else
-          hipLaunchKernelGGL(oz_gemm, dim3(8 * ((tiles + 7) / 8)), dim3(GEMM_NT), shm, st, Sbuf[c & 1], Dp, tiles,
-                             list, kbn, e, C);
+        hipLaunchKernelGGL(oz_gemm, dim3(8 * ((tiles + 7) / 8)), dim3(GEMM_NT), shm, st, Sbuf[c & 1], Dp, tiles,
+                           list, kbn, e, C);
         rc = hipGetLastError();
         if (rc == hipSuccess) rc = hipEventRecord(ev_g[c & 1], st);
         if (rc != hipSuccess) break;
@@ -638,6 +397,10 @@ int gadmm_gram_ozaki_f64(const double* X, const double* Y, int N, long m, int d,
     hipLaunchKernelGGL(oz_finish, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, C, Dp, d,
                        A + (long)n * d * d, B + (long)n * d, YY + n);
     GADMM_CHECK(hipGetLastError());
+    if (range_out) {
+      hipLaunchKernelGGL(oz_range, dim3(1), dim3(256), 0, st, cm, C, Dp, d, m, range_out + n);
+      GADMM_CHECK(hipGetLastError());
+    }
   }
   return 0;
 }

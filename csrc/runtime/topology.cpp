@@ -229,8 +229,9 @@ extern "C" int gadmm_pcg64_uniform(unsigned long long s_hi, unsigned long long s
 // while the caller keeps going (a D-GADMM solve draws its first launch's chains at the top of the
 // solve and joins them just before it builds the epoch tables: the greedy walks overlap the engine
 // refresh / reset / schedule set-up on the Python side instead of preceding the launch). One job at a
-// time: a submit while a job is pending first waits for it. The caller keeps uv / paths / costs alive
-// until gadmm_greedy_chains_wait returns.
+// time: a submit while a job is pending first waits for it, and a submit from another thread waits until
+// the owning thread's gadmm_greedy_chains_wait. The caller keeps uv / paths / costs alive until
+// gadmm_greedy_chains_wait returns.
 // Hand-offs are lock-free spins on an atomic state (a futex wake and a condition-variable round trip
 // cost tens of us on the sandboxed hosts measured, more than the walks themselves); the worker spins
 // for at most SPIN_NS after a job and then sleeps on the condition variable until the next submit.
@@ -256,6 +257,11 @@ struct GreedyPool {
   std::atomic<int> state{G_IDLE};
   std::atomic<bool> sleeping{false};
   std::once_flag started;
+  // One caller thread at a time owns the worker from its submit until its wait: a second thread's
+  // submit blocks until the owner has joined (it could otherwise overwrite the pending job, and the
+  // owner would read the other caller's paths / return code). Re-submitting by the owner is allowed.
+  std::atomic<bool> claimed{false};
+  std::atomic<std::thread::id> owner{};
 };
 GreedyPool& pool() {
   static GreedyPool* p = new GreedyPool();
@@ -298,6 +304,11 @@ namespace {
 int submit(const GreedyJob& nj) {
   GreedyPool& P = pool();
   std::call_once(P.started, [] { std::thread(greedy_worker).detach(); });  // lives for the process
+  const std::thread::id me = std::this_thread::get_id();
+  if (!(P.claimed.load(std::memory_order_acquire) && P.owner.load() == me)) {
+    while (P.claimed.exchange(true, std::memory_order_acquire)) std::this_thread::yield();
+    P.owner.store(me);
+  }
   wait_idle(P);
   P.job = nj;
   P.state.store(G_PENDING);  // seq_cst (see the worker's sleeping store)
@@ -357,5 +368,10 @@ extern "C" int gadmm_draw_chains_async(unsigned long long s_hi, unsigned long lo
 extern "C" int gadmm_greedy_chains_wait() {
   GreedyPool& P = pool();
   wait_idle(P);
-  return P.job.rc;
+  const int rc = P.job.rc;
+  if (P.claimed.load(std::memory_order_acquire) && P.owner.load() == std::this_thread::get_id()) {
+    P.owner.store(std::thread::id());
+    P.claimed.store(false, std::memory_order_release);  // the next caller's submit may take the worker
+  }
+  return rc;
 }

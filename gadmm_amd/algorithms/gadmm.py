@@ -329,46 +329,73 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
             and getenv("GADMM_DGADMM_EARLY", "1") != "0":
         early = _dyn_early_draw(eng, schedule, max_iter, fabric, n_total)
         _timing.host_stamp("native:early_draw")
-    if eng is not None and refresh:
-        eng.refresh(model.X, model.y)  # in place on the engine's stream (Gram, then inverses)
-    if eng is None:
-        eng = NativeChainEngine(model.X, model.y, local_ids, n_total, kind, rho=rho, obj0=obj0, tol=tol,
-                                max_iter=max_iter, lam=getattr(model, "lam", 0.0), step=step, max_inner=max_inner,
-                                inner_tol=inner_tol, comm=rcomm, block=block, precomputed=pre,
-                                local_solver="newton" if local_solver == "newton" else "gd",
-                                chord=None if opts.get("chord") is None else float(opts["chord"]),
-                                residual=bool(opts.get("residual", True)),
-                                obj_mode=str(opts.get("obj_mode", "auto")))
-        if rcomm is None and opts.get("cache", True):
-            if cache is None:
-                cache = {}
-                model._chain_engines = cache
-            cache[key] = eng
-    else:
-        eng.set_targets(obj0, tol)
-    _timing.host_stamp("native:engine")
-    eng.set_path(schedule.path, placement, rank)
-    _timing.host_stamp("native:set_path")
-    start = 1 if state is None else int(state[2])
-    static = _static_schedule(schedule, max_iter)
-    if state is not None and not (static and comm.nranks == 1):
-        raise ValueError("native resume: one rank, static chain")
+    try:
+        if eng is not None and refresh:
+            eng.refresh(model.X, model.y)  # in place on the engine's stream (Gram, then inverses)
+        if eng is None:
+            eng = NativeChainEngine(model.X, model.y, local_ids, n_total, kind, rho=rho, obj0=obj0, tol=tol,
+                                    max_iter=max_iter, lam=getattr(model, "lam", 0.0), step=step, max_inner=max_inner,
+                                    inner_tol=inner_tol, comm=rcomm, block=block, precomputed=pre,
+                                    local_solver="newton" if local_solver == "newton" else "gd",
+                                    chord=None if opts.get("chord") is None else float(opts["chord"]),
+                                    residual=bool(opts.get("residual", True)),
+                                    obj_mode=str(opts.get("obj_mode", "auto")))
+            if rcomm is None and opts.get("cache", True):
+                if cache is None:
+                    cache = {}
+                    model._chain_engines = cache
+                cache[key] = eng
+        else:
+            eng.set_targets(obj0, tol)
+        _timing.host_stamp("native:engine")
+        eng.set_path(schedule.path, placement, rank)
+        _timing.host_stamp("native:set_path")
+        start = 1 if state is None else int(state[2])
+        static = _static_schedule(schedule, max_iter)
+        if state is not None and not (static and comm.nranks == 1):
+            raise ValueError("native resume: one rank, static chain")
 
-    def load_state():  # fresh solve state, or the checkpoint's tables at start_iter (no pending duals)
-        eng.reset(start_iter=start)
-        if state is not None:
-            eng.stream.wait_stream(torch.cuda.current_stream(model.device))  # the state's producers
-            with torch.cuda.stream(eng.stream):
-                eng.theta.copy_(state[0].to(eng.theta.device, torch.float64).reshape(eng.theta.shape))
-                eng.mu.copy_(state[1].to(eng.mu.device, torch.float64).reshape(eng.mu.shape))
+        def load_state():  # fresh solve state, or the checkpoint's tables at start_iter (no pending duals)
+            eng.reset(start_iter=start)
+            if state is not None:
+                eng.stream.wait_stream(torch.cuda.current_stream(model.device))  # the state's producers
+                with torch.cuda.stream(eng.stream):
+                    eng.theta.copy_(state[0].to(eng.theta.device, torch.float64).reshape(eng.theta.shape))
+                    eng.mu.copy_(state[1].to(eng.mu.device, torch.float64).reshape(eng.mu.shape))
 
-    load_state()
-    _timing.host_stamp("native:reset")
-    stop_iter = int(opts.get("stop_iter", 0))
-    if fresh or state is not None:
-        # inputs made on other streams (a new engine's set-up, a loaded state) are complete before the
-        # solve; a cached engine's inputs are, and its own stream orders the reset before the kernel
-        torch.cuda.synchronize(model.device)
+        load_state()
+        _timing.host_stamp("native:reset")
+        stop_iter = int(opts.get("stop_iter", 0))
+        if fresh or state is not None:
+            # inputs made on other streams (a new engine's set-up, a loaded state) are complete before the
+            # solve; a cached engine's inputs are, and its own stream orders the reset before the kernel
+            torch.cuda.synchronize(model.device)
+    except BaseException:
+        # the early draw moved the schedule's RNG ahead of its chains: join the worker and rewind, so a
+        # re-run of this schedule draws the same chain sequence (seeded D-GADMM reproducibility)
+        if early is not None:
+            early[2]()
+            schedule.restore(early[0])
+        raise
+    if fabric is not None and comm.nranks > 1:
+        # the device-initiated kernels need every rank's launch: their eligibility is agreed, and a rank
+        # that cannot run them sends every rank to the graph engine over the session's data plane
+        import torch.distributed as dist
+        elig = opts.get("persistent", "auto") in (True, "auto") and (
+            eng.persistent_eligible(fabric) if static else eng.dynamic_eligible(fabric))
+        t = torch.tensor([0.0 if elig else 1.0], dtype=torch.float64)
+        dist.all_reduce(t, group=getattr(comm, "control_group", None))
+        if float(t.item()) != 0.0:
+            eng.close()
+            fb = opts.get("fallback_comm")
+            if fb is None:
+                raise RuntimeError("%s: the xGMI kernel is not eligible on some rank and no data-plane "
+                                   "fallback was given" % name)
+            o2 = {k: v for k, v in opts.items() if k not in ("fabric", "fallback_comm")}
+            res = _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, fb, placement, schedule,
+                                     local_solver, step, max_inner, inner_tol, cost_quirk, name, o2, state=state)
+            res.extra["fabric_fallback"] = "xgmi kernel not eligible on some rank: %s" % getattr(fb, "backend", "")
+            return res
     t0 = time.perf_counter()
     cc = 0.0
     com_cost = []
@@ -623,8 +650,22 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     res.extra["engine_obj"] = eng
     _timing.host_stamp("native:result")
     if opts.get("state", True):
-        # resumable state for checkpoints: apply the heads' pending (lazy) duals with the current
-        # chain, so (theta, mu) is the reference state after iteration next-1
+        # resumable state for checkpoints: (theta, mu) after the STOPPING iteration, whatever engine ran.
+        # A persistent kernel learns the monitor's decision `lag` iterations late and leaves its tables
+        # there; the same schedule is then replayed on the graph engine with no iteration past the stop
+        # (bit-identical to the persistent kernels on the linear chains, tests/test_gpu.py), so every engine
+        # hands back the state -- and next iteration -- of the graph engine (group_ADMM_closedForm.m:105-108)
+        state_from = engine_kind
+        if engine_kind == "persistent" and comm.nranks == 1 and static and done in (1, 2) \
+                and int(eng.ctl_state()["iter"]) != iters + 1:
+            load_state()
+            r2 = eng.run(stop_iter=iters, use_graph=opts.get("graph", True))
+            state_from = "graph replay to iteration %d" % iters
+            if int(r2.iters) != iters:
+                state_from += " (replay stopped at %d)" % int(r2.iters)
+        res.extra["state_from"] = state_from
+        # apply the heads' pending (lazy) duals with the current chain, so (theta, mu) is the reference
+        # state after iteration next-1
         eng.flush_duals()
         eng.stream.synchronize()  # the flush runs on the engine's stream; the copies below do not
         nxt = int(eng.ctl_state()["iter"])

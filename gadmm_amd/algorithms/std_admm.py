@@ -111,7 +111,12 @@ def _standard_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, c
     if eng is None:
         eng = StarEngine(model.X, model.y, local_ids, n_total, rho, obj0, tol, max_iter, hub_rank=hub_rank,
                          fabric=fabric, precomputed=(model.A, model.b, model.yy))
-        if not eng.eligible():
+        ok = eng.eligible()
+        if comm.nranks > 1:  # every rank's launch is needed: the choice is agreed (gloo)
+            from ..parallel.node import agree
+            ok = agree(ok, comm.nranks, getattr(comm, "control_group", None))
+        if not ok:
+            eng.close()
             return None
         cache[key] = eng
     elif opts.get("refresh"):

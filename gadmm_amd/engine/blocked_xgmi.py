@@ -166,6 +166,9 @@ class BlockedXgmiEngine:
             self.mu = torch.zeros((len(ext), self.d), dtype=f64, device=device)
             self.trace = torch.full((self.max_iter,), float("nan"), dtype=f64, device=device)
             self.ctl = torch.zeros((8,), dtype=torch.int32, device=device)
+            # per-iteration decision clock (s_memrealtime, written by rank 0's monitor) when ``stamps``
+            self.tstamp = torch.zeros((self.max_iter,), dtype=torch.int64, device=device)
+            self.t0stamp = torch.zeros((1,), dtype=torch.int64, device=device)
             slots = []
             for p in range(self.n):  # position == worker id (identity chain); li indexes the ext arrays
                 li = p - self.ext_lo if self.ext_lo <= p <= self.ext_hi else -1
@@ -239,6 +242,7 @@ class BlockedXgmiEngine:
         self.peer_tab_t = torch.tensor(self.peer_ptrs + [0], dtype=torch.int64, device=device)
         self.dec_push_t = torch.tensor(self.dec_all, dtype=torch.int64, device=device)
         self.epoch = 0
+        self.stamps = False  # record the decision clock per iteration (entry runs: the time trace)
         if self.data_local:
             W = (self.seg_hi - self.seg_lo + self.L) // self.L
             hosted = self._halo_mode() and dl_halo_hosted(self.seg_lo, self.seg_hi, self.n)
@@ -336,6 +340,8 @@ class BlockedXgmiEngine:
         pa.dl_halo = 1 if self._halo_mode() else 0
         pa.dl_tab[0], pa.dl_tab[1] = self.dl_ptrs[0] or None, self.dl_ptrs[1] or None
         pa.dbg = int(dbg)
+        if self.stamps:
+            pa.tstamp = self.tstamp.data_ptr()
         tl = None
         if timeline_iters > 0:
             tl = torch.zeros((256, int(timeline_iters), 8), dtype=torch.int64, device=self.device)
@@ -344,6 +350,9 @@ class BlockedXgmiEngine:
             self.theta.zero_()
             self.mu.zero_()
             self.ctl.zero_()
+            if self.stamps:
+                native.check(self.lib.gadmm_write_stamp(self.t0stamp.data_ptr(), self.stream.cuda_stream),
+                             "write_stamp")
             t0 = time.perf_counter()
             native.check(self.lib.gadmm_chain_blocked_launch(ctypes.byref(pa), self.stream.cuda_stream),
                          "chain_blocked_launch")
@@ -386,6 +395,14 @@ class BlockedXgmiEngine:
 
     def objective_trace(self, upto: int):
         return self.trace.cpu().numpy()[:upto]
+
+    def time_trace(self, upto: int):
+        """Seconds from the solve start to each iteration's stop decision (rank 0's monitor clock;
+        needs ``stamps``; zeros on other ranks)."""
+        import numpy as np
+        t = self.tstamp[:upto].cpu().numpy().astype(np.int64)
+        t0 = int(self.t0stamp.cpu().item())
+        return np.maximum(t - t0, 0).astype(np.float64) / 1e8
 
     def close(self):
         for p in self.opened.values():

@@ -78,11 +78,14 @@ class DistributedChainSolver:
                  rank: int, world: int, device: torch.device, rho: float, obj0: float, tol: float,
                  max_iter: int = 20000, engine: str = "auto", fabric: str = "auto", share: bool = False,
                  block: int = 0, halo_data=None, timeout_s: float = 20.0, use_graph: bool = True,
-                 dl_halo: Optional[bool] = None, strict: bool = False, halo_k: int = 0, halo_pw: int = 0):
+                 dl_halo: Optional[bool] = None, strict: bool = False, halo_k: int = 0, halo_pw: int = 0,
+                 plane=None):
         """``dl_halo`` (data-local blocked engine): None = the halo mode where eligible, True = only the
         halo mode, False = never. ``strict``: raise (on every rank together) when the requested
         persistent engine cannot run instead of falling back to the graph engine (the engine
-        tournament of bench.py builds each candidate this way)."""
+        tournament of bench.py builds each candidate this way). ``plane``: an existing data-plane comm
+        (an entry session's, ``parallel/node.NodeFabrics.data_plane``) for the graph engine instead of a
+        new one; it is the caller's, never closed here."""
         from .chain_engine import NativeChainEngine
 
         self.X, self.y = X_loc, y_loc
@@ -97,6 +100,7 @@ class DistributedChainSolver:
         self.kind, self.persistent, self.replicated_bytes = "local", False, 0
         self.fallbacks = []
         self.dl_halo = dl_halo
+        self.plane, self._own_comm = plane, True
         self.delay_next_s = 0.0  # test hook: sleep before the next launch (a slow / stalled peer)
         self._NCE = NativeChainEngine
         if world == 1:
@@ -181,8 +185,11 @@ class DistributedChainSolver:
         communicator; ``fall_back`` then moves every rank to IPC). Collective."""
         from ..parallel.dataplane import make_data_plane
         fabric = "ipc" if force_ipc else self.fabric_req
-        self.comm = make_data_plane(fabric, self.world, self.device, self.share, self.n, self.d, self.block,
-                                    timeout_s=self.timeout_s)
+        if getattr(self, "plane", None) is not None and not (force_ipc and getattr(self.plane, "backend", "") != "ipc"):
+            self.comm, self._own_comm = self.plane, False
+        else:
+            self.comm, self._own_comm = make_data_plane(fabric, self.world, self.device, self.share, self.n,
+                                                        self.d, self.block, timeout_s=self.timeout_s), True
         self.kind = self.comm.selection["data_plane"]
         self.eng = self._engine(self.comm)
         self.persistent = False
@@ -208,7 +215,11 @@ class DistributedChainSolver:
         if self.comm is not None:
             if from_rccl:
                 self.comm.abort()  # peers may be gone or aborted: never a collective destroy
-            self.comm.close()
+            own = getattr(self, "_own_comm", True)
+            if own or from_rccl:
+                self.comm.close()
+            if not own:
+                self.plane = None  # the caller's plane is dead: never hand it out again
             self.comm = None
         self._graph_engine(force_ipc=from_rccl)
 
@@ -220,7 +231,7 @@ class DistributedChainSolver:
             self.delay_next_s = 0.0
         if self.blk is not None:
             self.blk.refresh()
-            it, done, _ = self.blk.run(timeout_s=self.timeout_s)
+            it, done, self.last_wall_ms = self.blk.run(timeout_s=self.timeout_s)
             if done == 4:
                 raise RuntimeError("blocked kernel: a hand-off timed out")
             pay = self.blk.exchange_bytes_per_solve(it)
@@ -231,6 +242,7 @@ class DistributedChainSolver:
             r = self.eng.run_persistent(fabric=self.fab, timeout_s=self.timeout_s)
         else:
             r = self.eng.run(use_graph=self.use_graph)
+        self.last_wall_ms = float(getattr(r, "wall_ms", 0.0))
         return SolveOut(r.iters, r.done, r.p2p_bytes, r.wire_bytes, r.monitor_bytes)
 
     def guarded_solve(self) -> SolveOut:
@@ -267,7 +279,64 @@ class DistributedChainSolver:
         return self.blk.objective_trace(iters) if self.blk is not None else self.eng.objective_trace(iters)
 
     def close(self):
-        for o in (self.eng, self.blk, self.fab, self.comm):
+        for o in (self.eng, self.blk, self.fab, self.comm if getattr(self, "_own_comm", True) else None):
             if o is not None:
                 o.close()
         self.eng = self.blk = self.fab = self.comm = None
+
+
+def node_chain_admm(model, local_ids: Sequence[int], n_total: int, placement, rank: int, world: int,
+                    device: torch.device, rho: float, obj0: float, tol: float, max_iter: int,
+                    fabric: str = "auto", share: bool = False, plane=None, timeout_s: float = 20.0,
+                    name: str = "GADMM"):
+    """GADMM with closed-form local solves on a static identity chain (group_ADMM_closedForm.m:13-108)
+    over several GPUs, on the engines of the headline benchmark: this rank's contiguous segment of
+    ``model``'s shards goes to ``DistributedChainSolver`` (data-local blocked kernel over xGMI, with its
+    halo mode where eligible -> per-worker persistent kernel -> graph engine over the session's data
+    plane ``plane``). One solve from the raw shards (Gram, inverses, iterations), agreed by every rank;
+    a solve that fails on any rank (stalled hand-off) moves every rank to the next engine and runs again.
+    Returns a ``RunResult`` like ``chain_admm``'s: the objective trace of rank 0's monitor (identical on
+    every rank), the per-iteration decision clock, payload / wire / monitor bytes."""
+    import numpy as np
+    from ..algorithms.base import RunResult
+
+    local = [int(w) for w in local_ids]
+    sol = DistributedChainSolver(model.X, model.y, local, n_total, placement, rank, world, device, rho, obj0, tol,
+                                 max_iter=max_iter, fabric=fabric, share=share, timeout_s=timeout_s, plane=plane)
+    try:
+        if sol.blk is not None:
+            sol.blk.stamps = True
+        out = sol.guarded_solve()
+        if not all_ok(out.done in (1, 2), world) and sol.can_fall_back():
+            sol.fall_back("%s solve failed on some rank (done=%d here)" % (sol.kind, out.done))
+            out = sol.guarded_solve()
+        if not all_ok(out.done in (1, 2), world):
+            raise RuntimeError("node GADMM solve failed (done=%d here, engine %s)" % (out.done, sol.kind))
+        iters = int(out.iters)
+        if sol.blk is not None:
+            tr, tt = sol.blk.objective_trace(iters), sol.blk.time_trace(iters)
+        else:
+            tr, tt = sol.eng.traces(iters)
+        # rank 0's monitor decided: every rank reports its trace and clock
+        buf = torch.from_numpy(np.stack([np.asarray(tr, np.float64), np.asarray(tt, np.float64)]))
+        dist.broadcast(buf, src=0)
+        tr, tt = buf[0].numpy().copy(), buf[1].numpy().copy()
+        tot = torch.tensor([float(out.theta_bytes), float(out.wire_bytes), float(out.monitor_bytes),
+                            float(sol.replicated_bytes)], dtype=torch.float64)
+        dist.all_reduce(tot)
+        transport = "xgmi" if sol.persistent else sol.kind
+        res = RunResult(algorithm=name, obj=tr, loss=np.abs(tr - obj0), iters=iters, converged=(out.done == 1),
+                        wall_s=float(getattr(sol, "last_wall_ms", 0.0)) / 1e3, time_trace=tt,
+                        comm_units=np.arange(1, iters + 1, dtype=np.float64) * n_total,
+                        com_cost=np.zeros(iters), bytes_sent=int(out.theta_bytes), bytes_total=int(tot[0].item()),
+                        extra={"backend": "native", "engine": sol.engine_name(), "kernel": sol.kernel or "",
+                               "engine_kind": sol.kind, "transport": transport, "rank": rank, "nranks": world,
+                               "solver": "closed", "wire_bytes": int(out.wire_bytes),
+                               "monitor_bytes": int(out.monitor_bytes),
+                               "wire_bytes_all_ranks": int(tot[1].item()),
+                               "monitor_bytes_all_ranks": int(tot[2].item()),
+                               "replicated_shard_bytes": int(tot[3].item()),
+                               "fallbacks": "; ".join(sol.fallbacks)})
+        return res
+    finally:
+        sol.close()

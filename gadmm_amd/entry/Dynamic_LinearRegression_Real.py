@@ -17,8 +17,9 @@ def body(cfg, sess, args, writer):
     runs = {}
     for coh in cfg.coherences:
         r = dynamic_group_admm(prob.model, cfg.rhos[0], prob.obj0, cfg.acc, cfg.gadmm_iters, path, cost, coh,
-                               seed=cfg.path_seed, n_total=prob.n_total, local_ids=prob.local_ids, comm=sess.comm,
-                               placement=prob.placement, backend=args.backend)
+                               seed=cfg.path_seed, n_total=prob.n_total, local_ids=prob.local_ids,
+                               placement=prob.placement, backend=args.backend,
+                               **sess.chain_kw(prob.n_total, prob.d, dynamic=float(coh) < cfg.gadmm_iters + 1))
         r.extra.pop("engine_obj", None)
         r.extra.pop("state", None)
         runs["D-GADMM(coh=%g)" % coh] = r

@@ -29,13 +29,18 @@ def body(cfg, sess, args, writer):
         static_costs.append(T.calc_cost(g, path0))
     costs = np.asarray(costs)
     static_costs = np.asarray(static_costs)
-    kw = dict(n_total=N, local_ids=prob.local_ids, comm=sess.comm, placement=prob.placement, backend=args.backend)
+    kw = dict(n_total=N, local_ids=prob.local_ids, placement=prob.placement, backend=args.backend)
+
+    def fab(coh):  # several GPUs: the persistent kernels over xGMI (D-GADMM: a ring of table slots)
+        return sess.chain_kw(N, prob.d, dynamic=float(coh) < cfg.gadmm_iters + 1)
+
     runs = {}
     # the identity chain is the static GADMM of A6 (path0 only enters through the costs)
     runs["GADMM_static(coh=%g)" % cfg.coherence_v0] = static_group_admm(
-        prob.model, rho, prob.obj0, cfg.acc, cfg.gadmm_iters, cfg.coherence_v0, static_costs, **kw)
+        prob.model, rho, prob.obj0, cfg.acc, cfg.gadmm_iters, cfg.coherence_v0, static_costs, **kw,
+        **fab(cfg.coherence_v0))
     r0 = dynamic_group_admm_v0(prob.model, rho, prob.obj0, cfg.acc, cfg.gadmm_iters, paths, costs,
-                               cfg.coherence_v0, **kw)
+                               cfg.coherence_v0, **kw, **fab(cfg.coherence_v0))
     infl = 1.0 + cfg.overhead_inflation
     r0.com_cost = r0.com_cost * infl
     r0.time_trace = r0.time_trace * infl
@@ -44,7 +49,7 @@ def body(cfg, sess, args, writer):
     p1, c1, _ = T.find_path(N, rng)
     for coh in cfg.coherences:
         r = dynamic_group_admm(prob.model, rho, prob.obj0, cfg.acc, cfg.gadmm_iters, p1, c1, coh,
-                               seed=cfg.path_seed + int(min(coh, 1e6)), **kw)
+                               seed=cfg.path_seed + int(min(coh, 1e6)), **kw, **fab(coh))
         runs["D-GADMM(coh=%g)" % coh] = r
     for r in runs.values():
         r.extra.pop("engine_obj", None)

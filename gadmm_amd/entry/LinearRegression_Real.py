@@ -12,7 +12,7 @@ def body(cfg, sess, args, writer):
     runs = {}
     runs.update(baselines(prob, sess))
     runs.pop("_obj0_gd", None)
-    runs.update(gadmm_sweep(prob, sess, args.backend))
+    runs.update(gadmm_sweep(prob, sess, args.backend, state_rho=cfg.rhos[-1] if args.checkpoint else None))
     ck = maybe_checkpoint(args, sess, prob, runs["GADMM_rho%g" % cfg.rhos[-1]], cfg.rhos[-1], "GADMM")
     return {"runs": runs, "obj0": prob.obj0, "checkpoint": ck, "dataset": prob.dataset_meta,
             "figure_groups": {"LinearRegression_Real": runs}}

@@ -6,7 +6,8 @@ per worker, so no rank ever materialises another rank's data): with the defaults
 1.25M x 10k f64 = 100 GB per MI355X, i.e. 10M x 10k over 8 GPUs (weak scaling: per-GPU shard fixed).
 Set-up: augmented Gram on f64 MFMA (2.5e14 flop per GPU), cached inverses (A + c rho I)^{-1} (rocSOLVER
 Cholesky), the global optimum from the all-reduced d x d Gram. Then GADMM over the chain of workers on
-the row-blocked HIP engine (RCCL p2p of 80 KB theta per boundary per phase) until the relative gap
+the row-blocked HIP engine (80 KB theta per boundary per phase over the session's data plane: the IPC
+transport by default, RCCL with ``--fabric rccl``) until the relative gap
 |obj - obj*| / |obj*| < tol, and the star ADMM of the reference on the same fabric for comparison.
 
     torchrun --nproc-per-node 8 -m gadmm_amd LinearRegression_RealShaped
@@ -59,6 +60,7 @@ def body(cfg, sess, args, writer):
     if sess.device.type == "cuda":
         torch.cuda.synchronize(sess.device)
     t_gram = time.perf_counter() - t1
+    sess.ensure_plane(n_total, cfg.dim)  # several GPUs: the data plane (IPC default) of every solver below
     prob.obj0 = prob.model.optimum(sess.comm if sess.world > 1 else None, n_total=n_total)
     m = cfg.rows_per_worker
     rho = cfg.rhos[0] if cfg.rhos and cfg.rhos[0] > 0 else 0.5 * m   # A_n ~ m I for Gaussian rows

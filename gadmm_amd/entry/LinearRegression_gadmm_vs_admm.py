@@ -5,9 +5,9 @@ sum(P_central) + max(P_central), chain cost = sum(pathCost) of the *initial* cha
 variant (:128-179; the quirk that ignores D-GADMM's own com_cost is kept)."""
 import numpy as np
 
-from ..algorithms import chain_admm, dynamic_group_admm, standard_admm
+from ..algorithms import dynamic_group_admm, standard_admm
 from ..parallel import topology as T
-from .common import Problem, run_entry
+from .common import Problem, gadmm_solve, run_entry
 
 ENTRY = "LinearRegression_gadmm_vs_admm"
 
@@ -19,18 +19,20 @@ def body(cfg, sess, args, writer):
     path, cost, grid, p_central, center = T.find_path2(prob.n_total, rng)
     star = T.star_cost(p_central)
     chain = float(np.sum(cost))
-    kw = dict(comm=sess.comm, placement=prob.placement)
     runs = {}
-    r = standard_admm(prob.model, prob.local_ids, prob.n_total, rho, prob.obj0, cfg.acc, cfg.gadmm_iters, **kw)
+    # several GPUs: each comparator on its persistent kernel (star hub fan-in / the data-local chain /
+    # D-GADMM's re-chaining kernel) over xGMI, the IPC transport as data plane (parallel/node.py)
+    r = standard_admm(prob.model, prob.local_ids, prob.n_total, rho, prob.obj0, cfg.acc, cfg.gadmm_iters,
+                      placement=prob.placement, backend=args.backend, **sess.star_kw(prob.n_total, prob.d))
     r.com_cost = np.arange(1, len(r.loss) + 1) * star
     runs["ADMM(star)"] = r
-    g = chain_admm(prob.model, prob.local_ids, prob.n_total, rho, prob.obj0, cfg.acc, cfg.gadmm_iters,
-                   backend=args.backend, name="GADMM", **kw)
+    g = gadmm_solve(prob, sess, rho, cfg.acc, cfg.gadmm_iters, args.backend, name="GADMM")
     runs["GADMM"] = g
     for coh in cfg.coherences:
         runs["D-GADMM(coh=%g)" % coh] = dynamic_group_admm(
             prob.model, rho, prob.obj0, cfg.acc, cfg.gadmm_iters, path, cost, coh, seed=cfg.path_seed + int(coh),
-            n_total=prob.n_total, local_ids=prob.local_ids, backend=args.backend, **kw)
+            n_total=prob.n_total, local_ids=prob.local_ids, placement=prob.placement, backend=args.backend,
+            **sess.chain_kw(prob.n_total, prob.d, dynamic=float(coh) < cfg.gadmm_iters + 1))
     for k, v in runs.items():
         v.extra.pop("engine_obj", None)
         v.extra.pop("state", None)

@@ -14,7 +14,7 @@ def body(cfg, sess, args, writer):
     b = baselines(prob, sess)
     obj0_gd = b.pop("_obj0_gd", None)
     runs.update(b)
-    runs.update(gadmm_sweep(prob, sess, args.backend))
+    runs.update(gadmm_sweep(prob, sess, args.backend, state_rho=cfg.rhos[-1] if args.checkpoint else None))
     ck = maybe_checkpoint(args, sess, prob, runs["GADMM_rho%g" % cfg.rhos[-1]], cfg.rhos[-1], "GADMM-logistic")
     return {"runs": runs, "obj0": prob.obj0, "obj0_gd": obj0_gd, "checkpoint": ck, "dataset": prob.dataset_meta,
             "figure_groups": {"LogisticRegression_Real": runs}}

@@ -29,14 +29,22 @@ def gram_torch(X: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.Te
     return A, b, yy
 
 
-_OZ_WS: dict = {}
+# The Ozaki digits keep 49 bits of every value relative to its column's scale (>= the column maximum), so
+# an entry at the column's rms level keeps ~49 - log2(colmax / rms) bits; past 2^4 (45 bits, against the
+# 53 of an f64 operand) ``gram`` recomputes the shard on the f64-MFMA kernel. Gaussian columns of a
+# million rows sit near 5; one outlier row, or a heavy-tailed (e.g. lognormal) column, exceeds it.
+OZ_MAX_RANGE = 16.0
+LAST_GRAM: dict = {}  # path of the last CUDA ``gram`` call (``path``, ``range``): benchmarks report it
 
 
-def gram_ozaki(X: torch.Tensor, y: torch.Tensor, out=None) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+def gram_ozaki(X: torch.Tensor, y: torch.Tensor, out=None, with_range: bool = False):
     """Batched augmented Gram on the INT8 matrix cores (csrc/kernels/gram_ozaki.hip: the Ozaki scheme --
     7 int8 digits per f64 value after a per-column power-of-two scaling, exact int32 MFMA products of the
     28 digit pairs that reach f64 precision, f64 recombination). Same outputs as ``gram``; not bit-equal
-    to the f64-MFMA Gram (a different, exactly summed evaluation), as accurate or more."""
+    to the f64-MFMA Gram (a different, exactly summed evaluation). ``with_range``: also return each
+    shard's column-range statistic max_j colmax_j / rms_j (an (N,) device tensor; the accuracy gate of
+    ``gram``). The workspace (about 2.0 GB at d = 10k: the padded f64 Gram 0.82 GB + two digit chunks
+    1.16 GB) is taken from torch's caching allocator per call and returned after it, not held."""
     lib = native.require()
     X = X.contiguous()
     y = y.contiguous()
@@ -47,24 +55,22 @@ def gram_ozaki(X: torch.Tensor, y: torch.Tensor, out=None) -> Tuple[torch.Tensor
         A = torch.empty((N, d, d), dtype=torch.float64, device=X.device)
         b = torch.empty((N, d), dtype=torch.float64, device=X.device)
         yy = torch.empty((N,), dtype=torch.float64, device=X.device)
+    rng = torch.empty((N,), dtype=torch.float64, device=X.device)
     nb = int(lib.gadmm_gram_ozaki_workspace(int(m), int(d)))
-    key = (X.device, nb)
-    ws = _OZ_WS.get(key)
-    if ws is None:
-        _OZ_WS.clear()  # one workspace at a time (up to ~1.4 GB at d = 10k)
-        ws = torch.empty((nb,), dtype=torch.uint8, device=X.device)
-        _OZ_WS[key] = ws
+    ws = torch.empty((nb,), dtype=torch.uint8, device=X.device)
     native.check(lib.gadmm_gram_ozaki_f64(X.data_ptr(), y.data_ptr(), int(N), int(m), int(d), A.data_ptr(),
-                                          b.data_ptr(), yy.data_ptr(), ws.data_ptr(), nb, native.stream_handle()),
+                                          b.data_ptr(), yy.data_ptr(), ws.data_ptr(), nb, rng.data_ptr(),
+                                          native.stream_handle()),
                  "gram_ozaki_f64")
-    return A, b, yy
+    del ws  # back to the caching allocator once the stream has used it (stream-ordered reuse)
+    return (A, b, yy, rng) if with_range else (A, b, yy)
 
 
 def gram_uses_ozaki(m: int, d: int) -> bool:
-    """Whether ``gram`` takes the int8 Ozaki path. ``GADMM_GRAM_OZAKI``: ``auto`` (default) for shards of
+    """Whether ``gram`` tries the int8 Ozaki path. ``GADMM_GRAM_OZAKI``: ``auto`` (default) for shards of
     d >= 3072 features and m >= 65536 samples, where it measured faster than the f64-MFMA Gram (1.11x at
     100k x 4096, 1.10x at 312k x 10k; real10m 2.11 -> 1.92 s at the same 25 iterations: profiles/r05_h);
-    ``1`` for every d > 256; ``0`` never."""
+    ``1`` for every d > 256; ``0`` never. The range gate (``OZ_MAX_RANGE``) still applies."""
     mode = getenv("GADMM_GRAM_OZAKI", "auto")
     if mode == "0":
         return False
@@ -76,11 +82,20 @@ def gram_uses_ozaki(m: int, d: int) -> bool:
 def gram(X: torch.Tensor, y: torch.Tensor, ksplit: Optional[int] = None, out=None
          ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Batched augmented Gram. ``X``: (N, m, d) f64 contiguous, ``y``: (N, m).
-    ``out``: optional preallocated ``(A, b, yy)`` written in place."""
+    ``out``: optional preallocated ``(A, b, yy)`` written in place. Shards the Ozaki path would serve with
+    fewer kept bits than ``OZ_MAX_RANGE`` allows (an outlier row, a heavy-tailed column) are recomputed on
+    the f64-MFMA kernel (one host read of the N range statistics: set-up code, never graph-captured)."""
     if X.dtype != torch.float64 or y.dtype != torch.float64:
         raise TypeError("gram expects float64")
     if X.is_cuda and ksplit is None and gram_uses_ozaki(int(X.shape[1]), int(X.shape[2])):
-        return gram_ozaki(X, y, out=out)
+        A, b, yy, rng = gram_ozaki(X, y, out=out, with_range=True)
+        r = float(rng.max().item())
+        limit = float(getenv("GADMM_OZ_MAX_RANGE", str(OZ_MAX_RANGE)))
+        if r <= limit:
+            LAST_GRAM.update(path="ozaki-int8", range=r)
+            return A, b, yy
+        LAST_GRAM.update(path="f64-mfma (ozaki range gate: %.3g > %g)" % (r, limit), range=r)
+        return _gram_f64(X, y, None, (A, b, yy))
     if not X.is_cuda:
         res = gram_torch(X, y)
         if out is not None:
@@ -88,6 +103,11 @@ def gram(X: torch.Tensor, y: torch.Tensor, ksplit: Optional[int] = None, out=Non
                 o.copy_(r)
             return out
         return res
+    LAST_GRAM.update(path="f64-mfma", range=None)
+    return _gram_f64(X, y, ksplit, out)
+
+
+def _gram_f64(X, y, ksplit, out):
     lib = native.require()
     X = X.contiguous()
     y = y.contiguous()

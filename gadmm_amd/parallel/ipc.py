@@ -115,6 +115,40 @@ class IpcComm(Comm):
         torch.cuda.synchronize(self.device)
         dist.barrier(group=self.group)
 
+    # host-called point-to-point (the torch loops: DGD / dual averaging / chain ADMM fallbacks), staged
+    # through host memory over the gloo control plane; the engines use ``exchange_rows_dev``
+    def exchange_rows(self, table, ops):
+        if not ops:
+            return
+        p2p, recv_bufs = [], []
+        for peer, row, snd in ops:
+            if snd:
+                buf = table[row].detach().to("cpu").contiguous()
+                p2p.append(dist.P2POp(dist.isend, buf, int(peer), self.group))
+                self.stats.bytes_sent += buf.numel() * buf.element_size()
+                self.stats.msgs_sent += 1
+            else:
+                buf = torch.empty(table[row].shape, dtype=table.dtype)
+                recv_bufs.append((row, buf))
+                p2p.append(dist.P2POp(dist.irecv, buf, int(peer), self.group))
+                self.stats.bytes_recv += buf.numel() * buf.element_size()
+        for r in dist.batch_isend_irecv(p2p):
+            r.wait()
+        for row, buf in recv_bufs:
+            table[row].copy_(buf)
+
+    def send_tensor(self, t, peer):
+        h = t.detach().to("cpu").contiguous()
+        dist.send(h, int(peer), group=self.group)
+        self.stats.bytes_sent += h.numel() * h.element_size()
+        self.stats.msgs_sent += 1
+
+    def recv_tensor(self, t, peer):
+        h = torch.empty(t.shape, dtype=t.dtype)
+        dist.recv(h, int(peer), group=self.group)
+        t.copy_(h)
+        self.stats.bytes_recv += h.numel() * h.element_size()
+
     def _allreduce_max(self, t):
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
         return t

@@ -3,8 +3,8 @@
 * ``spawn(fn, world_size)``: run ``fn(rank, world_size, *args)`` in ``world_size`` processes on this
   host with a gloo process group (127.0.0.1 rendezvous, free port). Used by the CPU multi-process
   tests (BASELINE.json configs[0]) and by ``python -m gadmm_amd ... --cpu-ranks N``.
-* ``setup_rank(...)``: torchrun-style set-up for GPU jobs — gloo control plane + native RCCL
-  communicator, one process per MI355X.
+* ``setup_rank(...)``: torchrun-style set-up for GPU jobs — the gloo control plane, one process per
+  MI355X; data planes and fabrics come later, on demand (parallel/node.py).
 """
 from __future__ import annotations
 
@@ -73,13 +73,18 @@ def spawn(fn: Callable, world_size: int, *args, timeout: float = 600.0) -> List[
     return results
 
 
-def setup_rank(backend: str = "rccl", device: Optional[int] = None):
+def setup_rank(backend: str = "node", device: Optional[int] = None):
     """torchrun-style per-process set-up. Returns (rank, world, local_rank, device, comm).
 
-    ``backend='rccl'``: gloo control plane + native RCCL communicator (GPU);
+    ``backend='node'`` (GPU ranks): the gloo control plane only -- the data plane and the xGMI fabrics
+    are built on demand by ``parallel/node.NodeFabrics`` (IPC by default, RCCL opt-in); ``comm`` is None
+    for several ranks until the caller builds it. The device is ``select_device_index``: device 0 when the
+    ranks share one GPU (GADMM_SHARE_GPU / GADMM_BENCH_SHARE_GPU), else ``local_rank % visible devices``.
+    ``'rccl'``: as 'node' plus an eager native RCCL communicator (explicit opt-in only);
     ``'nccl'``: torch.distributed nccl (= RCCL) process group used through TorchDistComm;
     ``'gloo'``: CPU plumbing."""
     from .comm import LocalComm, RcclComm, TorchDistComm
+    from .node import select_device_index, share_requested
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -87,13 +92,17 @@ def setup_rank(backend: str = "rccl", device: Optional[int] = None):
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29511")
     dev = torch.device("cpu")
-    if backend in ("rccl", "nccl"):
-        dev = torch.device("cuda", local_rank if device is None else device)
+    if backend in ("node", "rccl", "nccl"):
+        idx = device if device is not None else select_device_index(local_rank, share_requested(),
+                                                                    torch.cuda.device_count())
+        dev = torch.device("cuda", idx)
         torch.cuda.set_device(dev)
     if world == 1:
         return rank, world, local_rank, dev, LocalComm()
     if not dist.is_initialized():
         dist.init_process_group("nccl" if backend == "nccl" else "gloo", rank=rank, world_size=world)
+    if backend == "node":
+        return rank, world, local_rank, dev, None
     if backend == "rccl":
         comm = RcclComm(dev)
     else:

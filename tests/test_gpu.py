@@ -1181,12 +1181,126 @@ def test_gram_ozaki_matches_f64(N, m, d):
     assert ea < 1e-14 and eb < 1e-14 and ey < 1e-14, (ea, eb, ey, e64)
     A2, _, _ = gram_ozaki(X, y)
     assert torch.equal(A, A2)  # deterministic
-    # the LDS-DMA one-wave-per-SIMD GEMM (GADMM_OZ_GEMM=2): the same exact int32 chunk sums and the same
-    # f64 flush order, so bit-identical
-    for variant in ("2", "3"):  # the LDS-DMA GEMMs, plain and with pipelined fragment reads
-        os.environ["GADMM_OZ_GEMM"] = variant
-        try:
-            A3, b3, yy3 = gram_ozaki(X, y)
-        finally:
-            del os.environ["GADMM_OZ_GEMM"]
-        assert torch.equal(A, A3) and torch.equal(b, b3) and torch.equal(yy, yy3), variant
+
+
+def _strict_err(A, Ar, eps=1e-12, rows=None):
+    """Entrywise error relative to |A_ab| + eps sqrt(A_aa A_bb): an outlier that
+    dominates a diagonal cannot hide the loss on the entries it does not touch. ``rows``: only those rows."""
+    sc = torch.sqrt(torch.diagonal(Ar, dim1=1, dim2=2).clamp_min(0))
+    den = Ar.abs() + eps * sc.unsqueeze(2) * sc.unsqueeze(1)
+    e = (A - Ar).abs() / den.clamp_min(1e-300)
+    if rows is not None:
+        e = e[:, rows]
+    return float(e.max())
+
+
+def _ref_gram(X, y):
+    """f64 reference on the CPU (torch's blocked f64 GEMM, independent of both device kernels)."""
+    Xc, yc = X.cpu(), y.cpu()
+    return torch.bmm(Xc.transpose(1, 2), Xc), torch.bmm(Xc.transpose(1, 2), yc.unsqueeze(-1)).squeeze(-1)
+
+
+@pytest.mark.parametrize("case", ["outlier_row", "lognormal"])
+def test_gram_ozaki_range_gate_hard_columns(case):
+    """Within-column dynamic range: a column whose maximum is one row 1e6 times the
+    rest (that row zero elsewhere, so the entries A_0b are NOT dominated by it), or lognormal columns. The
+    digits keep 49 bits relative to the column maximum, so the raw Ozaki Gram loses ~20 bits on A_0b; the
+    gate (linalg.OZ_MAX_RANGE on max colmax / rms) sends these shards to the f64-MFMA kernel."""
+    from gadmm_amd.ops import linalg
+    g = torch.Generator(device=DEV)
+    g.manual_seed(7)
+    N, m, d = 1, 20000, 300
+    X = torch.randn((N, m, d), dtype=torch.float64, device=DEV, generator=g)
+    if case == "outlier_row":
+        X[:, 1234, :] = 0.0
+        X[:, 1234, 0] = 1e6
+    else:
+        X = torch.exp(1.5 * X)  # heavy-tailed positive columns
+    y = torch.randn((N, m), dtype=torch.float64, device=DEV, generator=g)
+    Ar, br = _ref_gram(X, y)
+    Araw, _, _, rng = linalg.gram_ozaki(X, y, with_range=True)
+    assert float(rng.max()) > linalg.OZ_MAX_RANGE, float(rng.max())
+    os.environ["GADMM_GRAM_OZAKI"] = "1"  # d > 256: the auto rule would not try Ozaki at m = 20000
+    try:
+        A, b, yy = linalg.gram(X, y)
+        path = linalg.LAST_GRAM["path"]
+    finally:
+        del os.environ["GADMM_GRAM_OZAKI"]
+    assert path.startswith("f64-mfma (ozaki range gate"), path
+    A64 = linalg._gram_f64(X, y, None, None)[0]
+    assert torch.equal(A, A64)  # the gate's fallback IS the f64 kernel
+    rows = [0] if case == "outlier_row" else None
+    e_gate, e_raw = _strict_err(A.cpu(), Ar, rows=rows), _strict_err(Araw.cpu(), Ar, rows=rows)
+    print("case %s: range %.3g, strict error gated %.3g raw ozaki %.3g" % (case, float(rng.max()), e_gate, e_raw))
+    assert e_gate < 1e-10, e_gate
+    if case == "outlier_row":
+        assert e_raw > 10 * e_gate  # the loss the gate exists for
+
+
+def test_gram_ozaki_auto_shape_matches_f64():
+    """the auto-selected shape (d >= 3072, m >= 65536: several 8192-sample chunks) through
+    ``gram`` itself, Gaussian columns plus one Laplace (heavier-tailed) column: the range gate keeps the
+    Ozaki path, every entry within 1e-14 of sqrt(A_aa A_bb) of the CPU f64 reference."""
+    from gadmm_amd.ops import linalg
+    g = torch.Generator(device=DEV)
+    g.manual_seed(11)
+    N, m, d = 1, 70000, 3072
+    X = torch.randn((N, m, d), dtype=torch.float64, device=DEV, generator=g)
+    u = torch.rand((N, m), dtype=torch.float64, device=DEV, generator=g) - 0.5
+    X[:, :, 5] = -torch.sign(u) * torch.log1p(-2 * u.abs())  # Laplace column
+    y = torch.randn((N, m), dtype=torch.float64, device=DEV, generator=g)
+    A, b, yy = linalg.gram(X, y)
+    assert linalg.LAST_GRAM["path"] == "ozaki-int8", linalg.LAST_GRAM
+    Ar, br = _ref_gram(X, y)
+    sc = torch.sqrt(torch.diagonal(Ar, dim1=1, dim2=2))
+    ea = float(((A.cpu() - Ar).abs() / (sc.unsqueeze(2) * sc.unsqueeze(1))).max())
+    eb = float(((b.cpu() - br).abs() / (sc * yy.cpu().sqrt().unsqueeze(1))).max())
+    assert ea < 1e-14 and eb < 1e-14, (ea, eb)
+
+
+def test_gram_ozaki_gadmm_iterations_match_f64(monkeypatch):
+    """End to end: GADMM on a real-shaped problem (2 workers x 20000 x 300, one Laplace column) to a 1e-8
+    relative gap takes the same number of iterations with the Ozaki Gram (forced) as with the f64 one."""
+    from gadmm_amd.models import LinearRegression
+    from gadmm_amd.algorithms import chain_admm
+    g = torch.Generator(device=DEV)
+    g.manual_seed(3)
+    X = torch.randn((2, 20000, 300), dtype=torch.float64, device=DEV, generator=g)
+    u = torch.rand((2, 20000), dtype=torch.float64, device=DEV, generator=g) - 0.5
+    X[:, :, 7] = -torch.sign(u) * torch.log1p(-2 * u.abs())
+    th = torch.randn((300,), dtype=torch.float64, device=DEV, generator=g)
+    y = X @ th + 0.1 * torch.randn((2, 20000), dtype=torch.float64, device=DEV, generator=g)
+    its = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("GADMM_GRAM_OZAKI", mode)
+        m = LinearRegression(X, y)
+        obj0 = m.optimum()
+        r = chain_admm(m, [0, 1], 2, 10000.0, obj0, 1e-8 * abs(obj0), 2000, engine_opts={"cache": False})
+        assert r.converged
+        its[mode] = r.iters
+    assert its["1"] == its["0"], its
+
+
+@pytest.mark.parametrize("kind", ["linear", "logistic", "newton"])
+def test_persistent_state_at_stop_equals_graph(lin24, lin_obj0, log24, log_obj0, kind):
+    """the persistent kernels learn the stop decision `lag` iterations late; the
+    state a solve returns (checkpoints, resume) is nevertheless the state after the STOPPING iteration,
+    equal to the graph engine's: same next_iter = iters + 1 and the same (theta, mu)."""
+    from gadmm_amd.models import LinearRegression, LogisticRegression
+    from gadmm_amd.algorithms import chain_admm
+    if kind == "linear":
+        m = LinearRegression(lin24.X.to(DEV), lin24.y.to(DEV))
+        args, kw, expect = (3.0, lin_obj0, 1e-4, 3000), {}, 784
+    elif kind == "logistic":
+        m = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
+        args, kw, expect = (2e-4, log_obj0, 1e-4, 400), dict(local_solver="gd", step=2.2), 53
+    else:
+        m = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
+        args, kw, expect = (1e-3, log_obj0, 1e-8, 2000), dict(local_solver="newton"), 424
+    a = chain_admm(m, list(range(24)), 24, *args, engine_opts={"cache": False}, **kw)
+    b = chain_admm(m, list(range(24)), 24, *args, engine_opts={"cache": False, "persistent": False}, **kw)
+    assert a.extra["engine"] == "persistent" and b.extra["engine"] in ("graph", "eager")
+    assert a.iters == b.iters == expect
+    (ta, ma, na), (tb, mb, nb) = a.extra["state"], b.extra["state"]
+    assert na == nb == expect + 1, (na, nb, a.extra.get("state_from"))
+    assert torch.equal(ta, tb) and torch.equal(ma, mb)
