@@ -244,308 +244,6 @@ __global__ void __launch_bounds__(64) chain_persistent_logistic_kernel(PersistAr
 }
 
 // ------------------------------------------------------------------------------------------------
-// The same solve with FOUR waves per worker (one per SIMD), split by SAMPLE CLASS, ONE workgroup barrier
-// per inner GD step. The one-wave kernel above issues ~250 dependent instructions per inner step on one
-// SIMD (two 52-FMA quad GEMVs, exp / divide, the update): ~0.6 us, the whole logistic solve. Here wave
-// w owns the samples k = w + 4t (t < T):
-//   margins:  lane (s, c) = (lane & 15, lane >> 4) sums X[w + 4s][c + 4t] x[c + 4t] over t (T FMAs,
-//             x from wave-private LDS staging), the four column classes c meet by a permlane butterfly
-//             in the order ((c0 + c1) + c2) + c3 -- quad_gemv's order for row w + 4s;
-//   gradient: lane j sums X[w + 4t][j] s[w + 4t] over t (T FMAs, s broadcast from wave-private LDS):
-//             quad_gemv(X^T)'s partial of sample class c = w; the four waves' partials meet in
-//             workgroup LDS (the step's one barrier) and every wave adds ((g0 + g1) + g2) + g3 -- again
-//             quad_gemv's order. Every wave then holds the same x bits and takes the same break decision.
-// So each step is ~4x fewer FMAs per SIMD and the objective trace is bit-identical to the one-wave kernel
-// and the graph engine. Control (neighbour / decision polls) runs on wave 0 and reaches the others
-// through LDS; wave 0 publishes theta and the objective (whose softplus terms are gathered by sample
-// and reduced by wave 0's wave_sum, as in the one-wave kernel).
-constexpr int SPLIT_NT = 256;
-
-__device__ __forceinline__ double perm16_pair(double v, double* other) {  // rows (0,1,2,3) -> a=(0,0,2,2), b=(1,1,3,3)
-  const long long u = __double_as_longlong(v);
-  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)u, (unsigned)u, false, false);
-  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(u >> 32), (unsigned)(u >> 32), false, false);
-  *other = __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
-  return __longlong_as_double(((long long)hi[0] << 32) | lo[0]);
-}
-__device__ __forceinline__ double perm32_hi(double v) {  // rows (0,1,2,3) -> (2,3,2,3)
-  const long long u = __double_as_longlong(v);
-  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)u, (unsigned)u, false, false);
-  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(u >> 32), (unsigned)(u >> 32), false, false);
-  return __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
-}
-// lane (s, 0) of the result: ((p(s,0) + p(s,1)) + p(s,2)) + p(s,3) (rows c = 0..3 of 16 lanes each)
-__device__ __forceinline__ double class_reduce(double p) {
-  double b;
-  const double a = perm16_pair(p, &b);  // row 0: a = p0, b = p1; row 2: a = p2, b = p3
-  const double p2 = perm32_hi(a), p3 = perm32_hi(b);
-  return ((a + b) + p2) + p3;
-}
-
-template <int T, bool SYS>
-__global__ void __launch_bounds__(SPLIT_NT) chain_persistent_logistic_split_kernel(PersistArgs a, LogiArgs g) {
-  extern __shared__ __attribute__((aligned(16))) double lds[];
-  // workgroup LDS: [0, 4 * 64 * 2) gradient partials (double-buffered by step parity); then per wave
-  // 4 * QX x staging + 16 s values; then 64 objective terms, 2 x 64 neighbour rows, control words
-  double* gbuf = lds;                                   // [2][4][64]
-  const int d = a.d, n = a.n, m = g.m;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  double* xst = lds + 512 + wv * (4 * QX + 16);         // this wave's x staging
-  double* sst = xst + 4 * QX;                            // this wave's 16 s values
-  double* objv = lds + 512 + 4 * (4 * QX + 16);          // [64] softplus terms by sample
-  double* nbl = objv + 64;                               // [64] left neighbour's theta (wave 0 -> all)
-  double* nbr = nbl + 64;                                // [64] right neighbour's theta
-  int* ctrl = (int*)(nbr + 64);                          // [4] outcome, stop code, stop iteration
-  const __amdgpu_buffer_rsrc_t rth = rsrc_of(a.thg);
-  const __amdgpu_buffer_rsrc_t rob = rsrc_of(a.objg);
-  const unsigned long long deadline = now_ticks() + (unsigned long long)a.timeout_ticks;
-  __shared__ int xcd_lds;
-  const bool packed = !SYS && a.xcd > 0;
-  if (packed && (blockIdx.x & 7u)) return;
-  const int bid = packed ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
-  bool local = false;
-  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds);
-  if (!SYS && bid == 0 && threadIdx.x == 0) a.ctl->placed = a.xcd > 0 ? (local ? 2 : 1) : 0;
-
-  if (a.has_monitor && bid == a.n_local) {
-    if (wv != 0) return;  // the monitor is one wave (the one-wave kernel's code)
-    double* vals = lds;
-    for (int it = a.start_iter;; ++it) {
-      const unsigned tag = make_tag(a.epoch, it);
-      const int slot = it % a.ring;
-      bool okall = true;
-      for (int w = lane; w < n; w += 64) {
-        double v = 0.0;
-        for (int spin = 0;; ++spin) {
-          if (load_granule<SYS>(rob, (slot * n + w) * 16, tag, &v)) break;
-          if ((spin & 7) == 7 && now_ticks() > deadline) {
-            okall = false;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        vals[w] = v;
-      }
-      const bool ok = __all(okall);
-      unsigned code = 0;
-      if (lane == 0) {
-        if (!ok) {
-          code = 4;
-        } else {
-          double s = 0.0;
-          for (int w = 0; w < n; ++w) s += vals[w];
-          if (it - 1 < a.max_iter) a.trace[it - 1] = s;
-          if (!(s == s) || isinf(s)) code = 3;
-          else if (fabs(s - a.obj0) < a.tol) code = 1;
-          else if (it >= a.max_iter) code = 2;
-          if (a.tstamp && it - 1 < a.max_iter) a.tstamp[it - 1] = (long long)now_ticks();
-        }
-        const unsigned long long dv = ((unsigned long long)tag << 32) | code;
-        for (int r = 0; r < a.nranks; ++r) store_dec<SYS>(a.dec_push[r] + slot, dv);
-      }
-      if (__shfl((int)code, 0, 64)) return;
-    }
-  }
-
-  // ------------------------------------------------------------------ worker (four waves)
-  const PhaseSlot sl = a.slots[bid];
-  const int li = sl.li, w = sl.gid, left = sl.left, right = sl.right;
-  const bool head = (a.pos[bid] % 2) == 0;
-  const double rho = a.rho, lam = g.lam, step = g.step;
-  const bool w0 = wv == 0;
-  u32x4* const p0 = a.push ? a.push[2 * bid] : nullptr;
-  u32x4* const p1 = a.push ? a.push[2 * bid + 1] : nullptr;
-  const __amdgpu_buffer_rsrc_t rp0 = rsrc_of(p0 ? (const void*)p0 : (const void*)a.thg);
-  const __amdgpu_buffer_rsrc_t rp1 = rsrc_of(p1 ? (const void*)p1 : (const void*)a.thg);
-  const double* Xg = g.X + (long)li * m * d;
-  const int qs = lane & 15, qc = lane >> 4;
-  const int ks = wv + 4 * qs;  // this lane's sample in the margin layout
-  double Xm[T], Xt[T];         // X[ks][qc + 4t] (margins), X[wv + 4t][lane] (gradient partial)
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    const int col = qc + 4 * t, smp = wv + 4 * t;
-    Xm[t] = (ks < m && col < d) ? Xg[(long)ks * d + col] : 0.0;
-    Xt[t] = (smp < m && lane < d) ? Xg[(long)smp * d + lane] : 0.0;
-  }
-  const bool inj = lane < d;
-  const bool ink = qc == 0 && ks < m;  // lane (s, 0) carries sample ks
-  const double yk = ks < m ? g.Y[(long)li * m + ks] : 0.0;
-  double th = inj ? a.theta[(long)w * d + lane] : 0.0;
-  double mu = inj ? a.mu[(long)li * d + lane] : 0.0;
-  double tl = (inj && left >= 0) ? a.theta[(long)left * d + lane] : 0.0;
-  double tr = (inj && right >= 0) ? a.theta[(long)right * d + lane] : 0.0;
-  int pending = a.pending_in;
-  int stop_code = 0, stop_iter = 0, abort = 0, used = 0;
-
-  // margin z of sample ks (valid in lanes (s, 0)) for the x held in lane j of every wave
-  auto margin = [&](double x) -> double {
-    xst[(lane & 3) * QX + (lane >> 2)] = x;  // x_j at class j & 3, position j >> 2 (zero beyond d)
-    asm volatile("" ::: "memory");
-    const double* xs = xst + qc * QX;
-    double p = 0.0;
-#pragma unroll
-    for (int t = 0; t < T; t += 2) {
-      const double2 xp = *reinterpret_cast<const double2*>(xs + t);
-      p = fma(Xm[t], xp.x, p);
-      if (t + 1 < T) p = fma(Xm[t + 1], xp.y, p);
-    }
-    asm volatile("" ::: "memory");
-    return class_reduce(p);
-  };
-
-  int it = a.start_iter;
-  int kstep = 0;  // inner steps run so far (gradient buffer parity)
-  for (;; ++it) {
-    if (it > a.max_iter + a.lag) break;
-    // -- wave 0 polls the neighbours' theta and the decision of it - lag; the others read the result
-    if (w0) {
-      const bool check = it - a.start_iter >= a.lag;
-      const int jdec = it - a.lag;
-      const bool need_nb = head ? it > a.start_iter : true;
-      const int jnb = head ? it - 1 : it;
-      const unsigned tnb = make_tag(a.epoch, jnb), tj = make_tag(a.epoch, jdec);
-      const int ra = need_nb ? left : -1, rb = need_nb ? right : -1;
-      bool decided = !check;
-      unsigned long long dv = 0;
-      int outcome = 0;
-      for (int spin = 0;; ++spin) {
-        bool nb = true;
-        if (inj) {
-          if (ra >= 0) nb &= load_granule<SYS>(rth, (ra * d + lane) * 16, tnb, &tl);
-          if (rb >= 0) nb &= load_granule<SYS>(rth, (rb * d + lane) * 16, tnb, &tr);
-        }
-        if (!decided) {
-          dv = __shfl(load_dec<SYS>(&a.decg[jdec % a.ring]), 0, 64);
-          decided = (unsigned)(dv >> 32) == tj;
-        }
-        if (decided && (unsigned)(dv & 0xffffffffu) != 0u) { outcome = 2; break; }
-        if (decided && __all(nb)) { outcome = 1; break; }
-        if ((spin & 7) == 7 && now_ticks() > deadline) { outcome = 3; break; }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      nbl[lane] = tl;
-      nbr[lane] = tr;
-      if (lane == 0) {
-        ctrl[0] = outcome;
-        ctrl[1] = (int)(unsigned)(dv & 0xffffffffu);
-        ctrl[2] = jdec;
-      }
-    }
-    lds_barrier();
-    const int outcome = ctrl[0];
-    if (!w0) {
-      tl = nbl[lane];
-      tr = nbr[lane];
-    }
-    if (outcome != 1) {
-      if (outcome == 2) {
-        stop_code = ctrl[1];
-        stop_iter = ctrl[2];
-      } else {
-        abort = 1;
-      }
-      break;
-    }
-    // -- lazy dual (heads), frozen proximal shift (every wave: the same bits)
-    double sh = 0.0, x = 0.0;
-    if (inj) {
-      double mm = mu;
-      if (head && pending) {
-        if (left >= 0) mm = mm - rho * (tl - th);
-        if (right >= 0) mm = mm + rho * (th - tr);
-        mu = mm;
-      }
-      double s = mm;
-      if (left >= 0) s = s + rho * (th - tl);
-      if (right >= 0) s = s + rho * (th - tr);
-      sh = s;
-      x = th;
-    }
-    used = 0;
-    for (int k = 0; k < g.max_inner; ++k) {
-      const double z = margin(x);
-      const double sv = ink ? yk / (1.0 + exp(yk * z)) : 0.0;  // y_i / (1 + e^{y_i z_i})
-      if (qc == 0) sst[qs] = sv;
-      asm volatile("" ::: "memory");
-      double gp = 0.0;
-#pragma unroll
-      for (int t = 0; t < T; t += 2) {
-        const double2 sp = *reinterpret_cast<const double2*>(sst + t);
-        gp = fma(Xt[t], sp.x, gp);
-        if (t + 1 < T) gp = fma(Xt[t + 1], sp.y, gp);
-      }
-      asm volatile("" ::: "memory");
-      double* gb = gbuf + (kstep & 1) * 256;
-      gb[wv * 64 + lane] = gp;
-      lds_barrier();  // the step's one barrier: the four sample classes' partials
-      const double gx = ((gb[lane] + gb[64 + lane]) + gb[128 + lane]) + gb[192 + lane];
-      ++kstep;
-      bool conv = true;
-      if (inj) {
-        const double gr = -gx + lam * x + sh;
-        const double xn = x - step * gr;
-        conv = fabs(xn - x) < g.inner_tol;
-        x = xn;
-      }
-      used = k + 1;
-      if (__all(conv)) break;  // the same bits in every wave: the same decision
-    }
-    // -- publish theta^it (wave 0): own table + the remote neighbours' tables
-    const unsigned tag = make_tag(a.epoch, it);
-    if (w0 && inj) {
-      put_granule<SYS>(local, rth, (w * d + lane) * 16, tag, x);
-      if (p0) store_granule<SYS>(rp0, (w * d + lane) * 16, tag, x);
-      if (p1) store_granule<SYS>(rp1, (w * d + lane) * 16, tag, x);
-    }
-    if (!head) {
-      double rp = 0.0;
-      if (inj) {
-        double mm = mu;
-        if (left >= 0) mm = mm - rho * (tl - x);
-        if (right >= 0) mm = mm + rho * (x - tr);
-        mu = mm;
-        if (left >= 0) rp = fma(tl - x, tl - x, rp);
-        if (right >= 0) rp = fma(x - tr, x - tr, rp);
-      }
-      if (a.rres && w0) {
-        const double rs = wave_sum_f64(rp);
-        if (lane == 0 && it - 1 < a.max_iter) a.rres[(long)(it - 1) * n + w] = rs;
-      }
-    } else {
-      pending = 1;
-    }
-    th = x;
-    // -- f_n(theta^it): softplus terms by sample into LDS, wave 0 reduces them in sample-lane order
-    const double z = margin(x);
-    if (ink) objv[ks] = softplus(-yk * z);
-    lds_barrier();
-    if (w0) {
-      const double part = wave_sum_f64(lane < m ? objv[lane] : 0.0);
-      const double xx = wave_sum_f64(inj ? x * x : 0.0);
-      if (lane == 0) put_granule<SYS>(local, rob, ((it % a.ring) * n + w) * 16, tag, lam * 0.5 * xx + part);
-    }
-  }
-  if (w0) {
-    if (inj) {
-      a.theta[(long)w * d + lane] = th;
-      a.mu[(long)li * d + lane] = mu;
-    }
-    if (lane == 0) {
-      if (g.inner_iters) g.inner_iters[li] = used;
-      if (abort) {
-        a.ctl->done = 4;
-      } else if (bid == 0 && stop_code) {
-        a.ctl->done = stop_code;
-        a.ctl->conv_iter = stop_iter;
-        a.ctl->iter = it;
-        a.ctl->pending = 1;
-        a.ctl->monitored = stop_iter;
-      }
-    }
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
 // GADMM_LOGISTIC_ZREC=1: the inner GD with the margins carried by a recursion on a SECOND wave. A step
 //   z = X x,  s = y / (1 + e^{y z}),  x' = x - step (-X^T s + lam x + sh)
 // has two dependent GEMVs. Since z' = X x' = z - step (-K s + lam z + c) with K = X X^T (m x m, built
@@ -880,21 +578,15 @@ __global__ void __launch_bounds__(ZR_NT) chain_persistent_logistic_zrec_kernel(P
 extern "C" long gadmm_resident_capacity(const void* fn, int threads, size_t shm);
 extern "C" int gadmm_xcd_mode(const PersistArgs* a, int blocks, long cap_total);  // chain_persistent.hip
 
-// GADMM_LOGISTIC_SPLIT=1: four waves per worker (opt-in). Measured on MI355X (profiles/r05_c, E3, same
-// box, alternating): 6.60 / 6.71 ms vs 6.37 / 6.39 ms for the one-wave kernel -- bit-identical, but slower:
-// the inner step is bound by its dependent chain (13-deep FMA chains, exp, divide, the LDS staging of x),
-// not by FMA issue, so a quarter of the FMAs per SIMD gains nothing and the step barrier adds latency.
-static bool logi_split() {
-  const char* e = getenv("GADMM_LOGISTIC_SPLIT");
-  return e && e[0] == '1';
-}
-
+// (Round 5's four-wave sample-class split kernel, GADMM_LOGISTIC_SPLIT=1, was bit-identical but slower --
+// 6.60 / 6.71 vs 6.37 / 6.39 ms, profiles/r05_c: the inner step is bound by its dependent chain, not FMA
+// issue -- and was removed in round 6.)
 // The margins recursion (two waves per worker) is the default: 6.3 -> 5.0-5.3 ms on E3 at the reference's
 // 53 iterations (profiles/r05_j); GADMM_LOGISTIC_ZREC=0 selects the one-wave kernel, bit-identical to
 // the graph engine.
 static bool logi_zrec() {
   const char* e = getenv("GADMM_LOGISTIC_ZREC");
-  return !(e && e[0] == '0') && !logi_split();
+  return !(e && e[0] == '0');
 }
 
 static const void* logi_variant(const PersistArgs& a, const LogiArgs& g) {
@@ -908,14 +600,6 @@ static const void* logi_variant(const PersistArgs& a, const LogiArgs& g) {
     if (mx <= 52) return (const void*)chain_persistent_logistic_zrec_kernel<13, false>;
     return (const void*)chain_persistent_logistic_zrec_kernel<16, false>;
   }
-  if (logi_split()) {
-    if (a.sys_scope) {
-      if (mx <= 52) return (const void*)chain_persistent_logistic_split_kernel<13, true>;
-      return (const void*)chain_persistent_logistic_split_kernel<16, true>;
-    }
-    if (mx <= 52) return (const void*)chain_persistent_logistic_split_kernel<13, false>;
-    return (const void*)chain_persistent_logistic_split_kernel<16, false>;
-  }
   if (a.sys_scope) {
     if (mx <= 52) return (const void*)chain_persistent_logistic_kernel<13, true>;
     return (const void*)chain_persistent_logistic_kernel<16, true>;
@@ -924,13 +608,12 @@ static const void* logi_variant(const PersistArgs& a, const LogiArgs& g) {
   return (const void*)chain_persistent_logistic_kernel<16, false>;
 }
 
-static int logi_threads() { return logi_zrec() ? ZR_NT : logi_split() ? SPLIT_NT : 64; }
+static int logi_threads() { return logi_zrec() ? ZR_NT : 64; }
 
 static size_t logi_shm(const PersistArgs& a) {
   const size_t mon = (size_t)a.n * 8;
   const size_t wk = logi_zrec() ? (size_t)(2 * QSTAGE + 128 + ZR_SLOTS * 4 * QX + 64 * 64) * 8 + 32
-                    : logi_split() ? (size_t)(512 + 4 * (4 * QX + 16) + 3 * 64) * 8 + 16
-                                   : (size_t)QSTAGE * 8;
+                                 : (size_t)QSTAGE * 8;
   return mon > wk ? mon : wk;
 }
 

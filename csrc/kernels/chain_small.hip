@@ -586,161 +586,6 @@ __global__ void __launch_bounds__(64) chain_phase_logistic_quad(PhaseArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// Logistic phase, FOUR waves per worker (d, m <= 4T <= 64; opt-in GADMM_LOGISTIC_QUAD4=1). Wave w keeps only
-// row group w of the quad layout: lane (i, c) holds X[i + 16w][c + 4t] (margins) and
-// X[c + 4t][i + 16w] (gradient), 2T doubles instead of 8T, so each inner-GD GEMV is T FMAs per lane
-// instead of 4T; the four lanes of a row meet by a v_permlane32/16_swap butterfly (identical sums
-// on all four, hence identical redundant copies of x). x and s cross the waves through permuted
-// LDS staging: two workgroup barriers per inner step. Same semantics as logReg_GD.m:3-25 (frozen
-// proximal shift, all-coordinate |dx| < tol break, here a vote of the four waves).
-__device__ __forceinline__ double sum4_rows(double v) {  // v_l + v_(l^16) + v_(l^32) + v_(l^48)
-  const long long u = __double_as_longlong(v);
-  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)u, (unsigned)u, false, false);
-  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(u >> 32), (unsigned)(u >> 32), false, false);
-  const bool up = (threadIdx.x & 32) != 0;
-  const double p32 = __longlong_as_double(((long long)(up ? hi[0] : hi[1]) << 32) | (up ? lo[0] : lo[1]));
-  const double s1 = v + p32;
-  const long long u1 = __double_as_longlong(s1);
-  const auto lo1 = __builtin_amdgcn_permlane16_swap((unsigned)u1, (unsigned)u1, false, false);
-  const auto hi1 = __builtin_amdgcn_permlane16_swap((unsigned)(u1 >> 32), (unsigned)(u1 >> 32), false, false);
-  const bool odd = (threadIdx.x & 16) != 0;
-  const double p16 = __longlong_as_double(((long long)(odd ? hi1[0] : hi1[1]) << 32) | (odd ? lo1[0] : lo1[1]));
-  return s1 + p16;
-}
-
-template <int T>
-__global__ void __launch_bounds__(256) chain_phase_logistic_quad4(PhaseArgs a) {
-  __shared__ __attribute__((aligned(16))) double xs[4 * QX];  // x, permuted: x_j at (j & 3) * QX + (j >> 2)
-  __shared__ __attribute__((aligned(16))) double ss[4 * QX];  // s, same permutation over samples
-  __shared__ int vote[2][4];
-  __shared__ double red[12];
-  __shared__ int flag_lds;
-  ChainCtl* ctl = a.ctl;
-  if (ctl->done) return;
-  const int it = ctl->iter;
-  const int pending = ctl->pending;
-  const PhaseSlot sl = a.slots[blockIdx.x];
-  const int d = a.d, m = a.m;
-  const double rho = a.rho, lam = a.lam, step = a.step;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, qi = lane & 15, qc = lane >> 4;
-  const int row = qi + 16 * w;  // this lane's sample (margins) and coordinate (gradient)
-  const int pidx = (row & 3) * QX + (row >> 2);
-  double* th = a.theta;
-  const double* thw = th + (long)sl.gid * d;
-  const double* thl = sl.left >= 0 ? th + (long)sl.left * d : nullptr;
-  const double* thr = sl.right >= 0 ? th + (long)sl.right * d : nullptr;
-  double* mu = a.mu + (long)sl.li * d;
-  const double* Xg = a.X + (long)sl.li * m * d;
-  const double* Yg = a.Y + (long)sl.li * m;
-  double Xr[T], XTr[T];
-#pragma unroll
-  for (int t = 0; t < T; ++t) {
-    const int col = qc + 4 * t;
-    Xr[t] = (row < m && col < d) ? Xg[(long)row * d + col] : 0.0;   // X[row][col]
-    XTr[t] = (col < m && row < d) ? Xg[(long)col * d + row] : 0.0;  // X^T[row][col]
-  }
-  const bool inj = row < d, ini = row < m;
-  double x = 0.0, sh = 0.0, yv = 0.0;
-  if (inj) {
-    double mm = mu[row];
-    if ((a.flags & PH_PRE_DUAL) && pending) {
-      if (thl) mm = mm - rho * (thl[row] - thw[row]);
-      if (thr) mm = mm + rho * (thw[row] - thr[row]);
-    }
-    const double x0 = thw[row];
-    double s = mm;  // -C1 + C2 (edge form) == mu
-    if (thl) s = s + rho * (x0 - thl[row]);
-    if (thr) s = s + rho * (x0 - thr[row]);
-    sh = s;
-    x = x0;
-    if ((a.flags & PH_PRE_DUAL) && pending && qc == 0) mu[row] = mm;
-  }
-  if (ini) yv = Yg[row];
-  if (qc == 0) xs[pidx] = x;  // zero beyond d
-  lds_barrier();
-  int used = 0;
-  for (int k = 0; k < a.max_inner; ++k) {
-    const double* xb = xs + qc * QX;
-    double z0 = 0.0, z1 = 0.0;
-#pragma unroll
-    for (int t = 0; t < T; t += 2) {
-      const double2 xp = *reinterpret_cast<const double2*>(xb + t);
-      z0 = fma(Xr[t], xp.x, z0);
-      if (t + 1 < T) z1 = fma(Xr[t + 1], xp.y, z1);
-    }
-    const double z = sum4_rows(z0 + z1);                      // margin z_row = X[row, :] x
-    const double sv = ini ? yv / (1.0 + exp(yv * z)) : 0.0;  // y_i / (1 + e^{y_i z_i})
-    if (qc == 0) ss[pidx] = sv;
-    lds_barrier();  // s of every sample visible
-    const double* sb = ss + qc * QX;
-    double g0 = 0.0, g1 = 0.0;
-#pragma unroll
-    for (int t = 0; t < T; t += 2) {
-      const double2 sp = *reinterpret_cast<const double2*>(sb + t);
-      g0 = fma(XTr[t], sp.x, g0);
-      if (t + 1 < T) g1 = fma(XTr[t + 1], sp.y, g1);
-    }
-    const double gx = sum4_rows(g0 + g1);  // (X^T s)_row
-    bool conv = true;
-    if (inj) {
-      const double g = -gx + lam * x + sh;
-      const double xn = x - step * g;
-      conv = fabs(xn - x) < a.inner_tol;
-      x = xn;
-    }
-    const bool wc = __all(conv);
-    if (qc == 0) xs[pidx] = x;  // every wave read xs before the barrier above
-    if (lane == 0) vote[k & 1][w] = wc ? 1 : 0;
-    lds_barrier();  // x and the four votes visible
-    used = k + 1;
-    if (vote[k & 1][0] & vote[k & 1][1] & vote[k & 1][2] & vote[k & 1][3]) break;
-  }
-  // local objective lam/2 |x|^2 + sum softplus(-y z) at the new iterate
-  const double* xb = xs + qc * QX;
-  double z0 = 0.0, z1 = 0.0;
-#pragma unroll
-  for (int t = 0; t < T; t += 2) {
-    const double2 xp = *reinterpret_cast<const double2*>(xb + t);
-    z0 = fma(Xr[t], xp.x, z0);
-    if (t + 1 < T) z1 = fma(Xr[t + 1], xp.y, z1);
-  }
-  const double z = sum4_rows(z0 + z1);
-  const double part = wave_sum_f64((ini && qc == 0) ? softplus(-yv * z) : 0.0);
-  const double xx = wave_sum_f64((inj && qc == 0) ? x * x : 0.0);
-  if (lane == 0) {
-    red[w] = part;
-    red[4 + w] = xx;
-  }
-  double rp = 0.0;
-  if (inj && qc == 0) {
-    th[(long)sl.gid * d + row] = x;
-    if (a.flags & PH_POST_DUAL) {
-      double mm = mu[row];
-      if (thl) mm = mm - rho * (thl[row] - x);
-      if (thr) mm = mm + rho * (x - thr[row]);
-      mu[row] = mm;
-      if (thl) rp = fma(thl[row] - x, thl[row] - x, rp);  // K4 primal residual of the tail's edges
-      if (thr) rp = fma(x - thr[row], x - thr[row], rp);
-    }
-  }
-  if (a.rres && (a.flags & PH_POST_DUAL)) {
-    const double rs = wave_sum_f64(rp);
-    if (lane == 0) red[8 + w] = rs;
-  }
-  lds_barrier();
-  if (threadIdx.x == 0) {
-    if (a.rres && (a.flags & PH_POST_DUAL) && it - 1 < a.max_iter)
-      a.rres[(long)(it - 1) * a.n_total + sl.gid] = ((red[8] + red[9]) + red[10]) + red[11];
-    const double pt = ((red[0] + red[1]) + red[2]) + red[3], x2 = ((red[4] + red[5]) + red[6]) + red[7];
-    a.objw[sl.li] = lam * 0.5 * x2 + pt;
-    if (a.inner_iters) a.inner_iters[sl.li] = used;
-  }
-  if (a.flags & PH_FINISH) {
-    if (phase_arrive(ctl, a.n_slots, &flag_lds)) finish_iteration(a, it);
-  }
-}
-
-// ------------------------------------------------------------------------------------------------
 // Apply the pending heads' dual updates with the chain they were computed on (used before a
 // re-chain and before checkpointing). One workgroup per slot of the OLD head plan.
 __global__ void __launch_bounds__(NT) chain_dual_flush_kernel(const PhaseSlot* slots, int n_slots, int d,
@@ -848,15 +693,9 @@ int gadmm_chain_phase(const PhaseArgs* args, hipStream_t st) {
       // GADMM_LOGISTIC_QUAD=0: the LDS-staged one-wave kernel (A/B measurements)
       static const bool quad = !(getenv("GADMM_LOGISTIC_QUAD") && getenv("GADMM_LOGISTIC_QUAD")[0] == '0');
       const int dm = a.d > a.m ? a.d : a.m;
-      // GADMM_LOGISTIC_QUAD4=1: the four-wave variant. Measured on MI355X (E3, same call): 7.20 vs 6.96 ms
-      // per solve -- the two barriers per inner step cost more than the 3T FMAs they save per lane.
-      const char* q4e = getenv("GADMM_LOGISTIC_QUAD4");
-      const bool quad4 = q4e && q4e[0] == '1';
-      if (!block4 && quad && quad4 && dm <= 64) {
-        if (dm <= 32) hipLaunchKernelGGL(chain_phase_logistic_quad4<8>, dim3(a.n_slots), dim3(256), 0, st, a);
-        else if (dm <= 52) hipLaunchKernelGGL(chain_phase_logistic_quad4<13>, dim3(a.n_slots), dim3(256), 0, st, a);
-        else hipLaunchKernelGGL(chain_phase_logistic_quad4<16>, dim3(a.n_slots), dim3(256), 0, st, a);
-      } else if (!block4 && quad && dm <= 64) {
+      // (the four-wave quad variant, GADMM_LOGISTIC_QUAD4=1, measured 7.20 vs 6.96 ms per solve -- its two
+      // barriers per inner step cost more than the 3T FMAs they save per lane -- was removed in round 6)
+      if (!block4 && quad && dm <= 64) {
         if (dm <= 32) hipLaunchKernelGGL(chain_phase_logistic_quad<8>, dim3(a.n_slots), dim3(64), 0, st, a);
         else if (dm <= 52) hipLaunchKernelGGL(chain_phase_logistic_quad<13>, dim3(a.n_slots), dim3(64), 0, st, a);
         else hipLaunchKernelGGL(chain_phase_logistic_quad<16>, dim3(a.n_slots), dim3(64), 0, st, a);

@@ -320,174 +320,6 @@ gram_aug_kernel(const double* __restrict__ X, const double* __restrict__ Y, int 
       }
 }
 
-// LDS-DMA variant (GADMM_GRAM_GLDS=1, BT = 128): the shard rows go global -> LDS with
-// global_load_lds_dwordx4 (one wave instruction = one 128-double K row of a panel, 1 KB contiguous
-// both sides; the padded LDS row stride is allowed because no instruction crosses a row) through a
-// 3-stage ring, so slab s + 2 is in flight while slab s is multiplied and no VGPR holds staging
-// data. Per slab: a counted vmcnt (this wave's DMAs of slab s retired, s + 1's may still fly), a raw
-// s_barrier (everyone's DMAs of s landed, everyone is done reading s - 1), then slab s + 2 is issued
-// into s - 1's stage. Tiles with a column past the shard (the y column, the zero padding) and the
-// partial last slab take a synchronous register-staged step with clamped loads. Same MFMA order as
-// gram_aug_kernel (bit-identical results).
-// one wave instruction: 64 lanes x 16 B from per-lane global addresses into LDS at lds_row + 16 lane
-__device__ __forceinline__ void glds16(const double* src, double* lds_row) {
-  __builtin_amdgcn_global_load_lds(src, lds_row, 16, 0, 0);
-}
-
-template <int BT, int NT, int NS>
-__global__ void __launch_bounds__(NT)
-gram_glds_kernel(const double* __restrict__ X, const double* __restrict__ Y, int m, int d,
-                 int ntiles, int ksplit, long rows_per_split,
-                 double* __restrict__ A, double* __restrict__ B, double* __restrict__ YY,
-                 double* __restrict__ slab, int nt, int ST) {
-  using T = GramTile<BT, NT>;
-  static_assert(NS == 2 || NS == 3, "two- or three-stage ring");
-  constexpr int STAGE = 2 * BK * T::LDSROW;  // doubles per stage (two panels)
-  extern __shared__ __attribute__((aligned(16))) double lds[];  // NS * STAGE doubles (dynamic: > 64 KB)
-
-  const int nwg = gridDim.x;
-  const int gid = xcd_remap(blockIdx.x, nwg);
-  const int tile = gid % ntiles;
-  const int rest = gid / ntiles;
-  const int split = rest % ksplit;
-  const int n = rest / ksplit;
-  int ti, tj;
-  tile_of(tile, nt, ST, ti, tj);
-  const bool diag = (ti == tj);
-  const int row0 = ti * BT, col0 = tj * BT;
-  const double* H = X + (long)n * m * d;
-  const double* yv = Y + (long)n * m;
-  const long kbeg = (long)split * rows_per_split;
-  long kend = kbeg + rows_per_split;
-  if (kend > m) kend = m;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wr = wid >> 1, wc = wid & 1;
-  const int D = d + 1;
-
-  f64x4 acc[T::TMR][T::TMC];
-#pragma unroll
-  for (int a = 0; a < T::TMR; ++a)
-#pragma unroll
-    for (int b = 0; b < T::TMC; ++b) acc[a][b] = f64x4{0.0, 0.0, 0.0, 0.0};
-
-  auto compute = [&](const double* Ci) {
-    const double* Cb = diag ? Ci : Ci + BK * T::LDSROW;
-#pragma unroll
-    for (int ks = 0; ks < BK / 4; ++ks) {
-      const int kr = ks * 4 + (lane >> 4);
-      double a[T::TMR], b[T::TMC];
-#pragma unroll
-      for (int t = 0; t < T::TMR; ++t) a[t] = Ci[kr * T::LDSROW + wr * T::WTR + t * 16 + (lane & 15)];
-#pragma unroll
-      for (int t = 0; t < T::TMC; ++t) b[t] = Cb[kr * T::LDSROW + wc * T::WTC + t * 16 + (lane & 15)];
-#pragma unroll
-      for (int x = 0; x < T::TMR; ++x)
-#pragma unroll
-        for (int yq = 0; yq < T::TMC; ++yq)
-          acc[x][yq] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[x], b[yq], acc[x][yq], 0, 0, 0);
-    }
-  };
-
-  const bool cols_in = (row0 + BT <= d) && (diag || col0 + BT <= d);
-  const long nfull = cols_in ? (kend - kbeg) / BK : 0;  // slabs through the DMA ring
-  constexpr int NW = NT / 64;
-  // this wave's DMA rows of a slab: q = wid * QPW + i over (panel, row) pairs; diagonal tiles read one panel
-  auto issue = [&](long k0, int st) {
-    double* base = lds + st * STAGE;
-    const int qpw = (diag ? BK : 2 * BK) / NW;
-    for (int i = 0; i < qpw; ++i) {
-      const int q = wid * qpw + i;
-      const int panel = q / BK, r = q % BK;
-      const double* src = H + (k0 + r) * (long)d + (panel ? col0 : row0) + 2 * lane;
-      glds16(src, base + (panel * BK + r) * T::LDSROW);
-    }
-  };
-  if (nfull > 0 && NS == 2) {
-    // two stages (two workgroups per CU): slab s + 1's DMAs fly during slab s's MFMAs; at the top of
-    // slab s every wave has only slab s's own DMAs outstanding
-    issue(kbeg, 0);
-    for (long s = 0; s < nfull; ++s) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();  // everyone's DMAs of s landed, everyone is done reading s - 1
-      if (s + 1 < nfull) issue(kbeg + (s + 1) * BK, (int)((s + 1) & 1));
-      compute(lds + (s & 1) * STAGE);
-    }
-  } else if (nfull > 0) {
-    issue(kbeg, 0);
-    if (nfull > 1) issue(kbeg + BK, 1);
-    int cur = 0;
-    for (long s = 0; s < nfull; ++s) {
-      if (s + 1 < nfull) {  // slab s + 1's DMAs of this wave may stay in flight
-        if (diag) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();
-      if (s + 2 < nfull) issue(kbeg + (s + 2) * BK, cur == 0 ? 2 : cur - 1);
-      compute(lds + cur * STAGE);
-      cur = cur == NS - 1 ? 0 : cur + 1;
-    }
-  }
-  // remaining rows (a tile with columns past the shard: all of them; else the partial last slab):
-  // synchronous register-staged slabs with clamped loads into stage 0
-  for (long k0 = kbeg + nfull * BK; k0 < kend; k0 += BK) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();  // everyone is done reading stage 0
-    double* Si = lds;
-    double* Sj = lds + BK * T::LDSROW;
-#pragma unroll
-    for (int p = 0; p < T::PER_THREAD / 2; ++p) {
-      const int e2 = tid + NT * p;
-      const int r = e2 / (BT / 2), c = (e2 % (BT / 2)) * 2;
-      const long k = k0 + r;
-      const long kk = k < kend ? k : (kend - 1);
-      const double yk = yv[kk];
-      const bool kin = k < kend;
-      double vi[2], vj[2];
-#pragma unroll
-      for (int q = 0; q < 2; ++q) {
-        const int ca = row0 + c + q, cb = col0 + c + q;
-        const double va = H[kk * d + (ca < d ? ca : d - 1)];
-        vi[q] = kin ? (ca < d ? va : (ca == d ? yk : 0.0)) : 0.0;
-        const double vb = H[kk * d + (cb < d ? cb : d - 1)];
-        vj[q] = kin ? (cb < d ? vb : (cb == d ? yk : 0.0)) : 0.0;
-      }
-      *reinterpret_cast<double2*>(Si + r * T::LDSROW + c) = make_double2(vi[0], vi[1]);
-      if (!diag) *reinterpret_cast<double2*>(Sj + r * T::LDSROW + c) = make_double2(vj[0], vj[1]);
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    compute(lds);
-  }
-
-#pragma unroll
-  for (int x = 0; x < T::TMR; ++x)
-#pragma unroll
-    for (int yq = 0; yq < T::TMC; ++yq)
-#pragma unroll
-      for (int reg = 0; reg < 4; ++reg) {
-        const int lr = wr * T::WTR + x * 16 + (lane >> 4) + 4 * reg;
-        const int lc = wc * T::WTC + yq * 16 + (lane & 15);
-        const double v = acc[x][yq][reg];
-        if (ksplit > 1) {
-          slab[(((long)n * ntiles + tile) * ksplit + split) * (BT * BT) + lr * BT + lc] = v;
-          continue;
-        }
-        const int r = row0 + lr, c = col0 + lc;
-        if (r >= D || c >= D || c > r) continue;
-        if (r < d && c < d) {
-          double* An = A + (long)n * d * d;
-          An[(long)r * d + c] = v;
-          An[(long)c * d + r] = v;
-        } else if (r == d && c < d) {
-          B[(long)n * d + c] = v;
-        } else if (r == d && c == d) {
-          YY[n] = v;
-        }
-      }
-}
-
 // Fixed-order reduction of the split-K slabs + symmetric scatter into (A, b, yy).
 template <int BT>
 __global__ void __launch_bounds__(256)
@@ -516,13 +348,6 @@ gram_reduce_kernel(const double* __restrict__ slab, int d, int ntiles, int kspli
   }
 }
 
-// GADMM_GRAM_GLDS=1: the LDS-DMA kernel for 128-wide tiles with a 3-stage ring (one workgroup per CU);
-// =2: a 2-stage ring (two workgroups per CU). A/B switches; 0 = the register-staged kernel.
-int gram_glds() {
-  static const int v = getenv("GADMM_GRAM_GLDS") ? atoi(getenv("GADMM_GRAM_GLDS")) : 0;
-  return v == 1 || v == 2 ? v : 0;
-}
-
 template <int BT>
 int launch_gram(const double* X, const double* Y, int N, int m, int d, int ksplit, double* A,
                 double* B, double* YY, double* slab, hipStream_t st) {
@@ -537,32 +362,11 @@ int launch_gram(const double* X, const double* Y, int N, int m, int d, int kspli
   const long nwg = (long)ntiles * ksplit * N;
   static const int nt_env = getenv("GADMM_GRAM_NT") ? atoi(getenv("GADMM_GRAM_NT")) : 0;  // A/B switch
   const int nthr = nt_env == 256 || nt_env == 512 ? nt_env : (BT == 128 ? 512 : 256);
-  // tile order: row-major over the triangle by default; GADMM_GRAM_ST = 8 selects the supertile order
-  // (tile_of: 8 x 8 blocks of tiles), measured 0.5 % slower at 2 x 625000 x 10000 (profiles/r03_gram)
-  static const int st_env = getenv("GADMM_GRAM_ST") ? atoi(getenv("GADMM_GRAM_ST")) : -1;
-  const int ST = st_env >= 0 ? st_env : 0;
-  bool launched = false;
-  if constexpr (BT == 128) {
-    if (gram_glds()) {
-      const int ns = gram_glds() == 1 ? 3 : 2;
-      const size_t lds = (size_t)ns * 2 * BK * (BT + PAD) * sizeof(double);
-      const void* fn = ns == 3 ? (const void*)gram_glds_kernel<BT, 512, 3> : (const void*)gram_glds_kernel<BT, 512, 2>;
-      static bool attr = false;
-      if (!attr) {
-        GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        attr = true;
-      }
-      if (ns == 3)
-        hipLaunchKernelGGL((gram_glds_kernel<BT, 512, 3>), dim3((unsigned)nwg), dim3(512), lds, st, X, Y, m, d,
-                           ntiles, ksplit, rows, A, B, YY, slab, nt, ST);
-      else
-        hipLaunchKernelGGL((gram_glds_kernel<BT, 512, 2>), dim3((unsigned)nwg), dim3(512), lds, st, X, Y, m, d,
-                           ntiles, ksplit, rows, A, B, YY, slab, nt, ST);
-      launched = true;
-    }
-  }
-  if (launched) {
-  } else if (nthr == 512)
+  // tile order: row-major over the triangle (tile_of's supertile order, ST = 8, measured 0.5 % slower
+  // at 2 x 625000 x 10000: profiles/r03_gram; the LDS-DMA ring variants measured ~1 % slower:
+  // profiles/r03_gram_glds, r04_gram -- both removed in round 6)
+  const int ST = 0;
+  if (nthr == 512)
     hipLaunchKernelGGL((gram_aug_kernel<BT, 512>), dim3((unsigned)nwg), dim3(512), 0, st, X, Y, m, d, ntiles, ksplit,
                        rows, A, B, YY, slab, nt, ST);
   else
@@ -601,8 +405,8 @@ int gadmm_gram_pick_ksplit(int N, int m, int d) {
   const long tiles = (long)N * (nt * (nt + 1) / 2);
   int cus = gadmm_cu_count();
   if (cus <= 0) cus = 256;
-  // 2 resident workgroups per CU (LDS / VGPR bound); 1 for the LDS-DMA kernel's 3-stage ring
-  const long slots = (long)cus * (BT == 128 && gram_glds() == 1 ? 1 : 2);
+  // 2 resident workgroups per CU (LDS / VGPR bound)
+  const long slots = (long)cus * 2;
   long maxk = (m + 255) / 256;       // keep >= 256 rows per split
   if (maxk > 64) maxk = 64;
   if (maxk < 1) maxk = 1;

@@ -377,13 +377,10 @@ def test_logistic_newton_kernel_odd_shapes(n, m, d):
     np.testing.assert_allclose(a.obj, b.obj, rtol=1e-12, atol=0)
 
 
-@pytest.mark.parametrize("quad4", ["0", "1"])
-def test_logistic_register_kernel_trace_matches_torch(log24, log_obj0, quad4, monkeypatch):
-    """chain_phase_logistic_quad (shard + transpose in VGPRs; quad4 = 1: the four-wave variant) follows
-    the torch inexact-GD path (logReg_GD.m semantics) iteration by iteration, not only in the final
-    count."""
+def test_logistic_register_kernel_trace_matches_torch(log24, log_obj0):
+    """chain_phase_logistic_quad (shard + transpose in VGPRs) follows the torch inexact-GD path
+    (logReg_GD.m semantics) iteration by iteration, not only in the final count."""
     import numpy as np
-    monkeypatch.setenv("GADMM_LOGISTIC_QUAD4", quad4)
     from gadmm_amd.models import LogisticRegression
     from gadmm_amd.algorithms import chain_admm
     eng = _engine(log24, 2e-4, log_obj0, 1e-4, model="logistic", lam=1e-5, step=2.2, max_inner=100, inner_tol=1e-4,
