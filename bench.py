@@ -341,7 +341,7 @@ def run_headline(args, rank, world, device, share):
             out["tournament_winner"] = winner
             out["tournament_deadline_s"] = tour_timeout_s
             out["tournament_wall_s"] = round(tour_wall_s, 3)
-            out["rccl_built"] = any(c["name"] == "graph-rccl" for c in tournament)
+            out["rccl_built"] = any(row.get("engine") == "graph-rccl" for row in tournament)
         out["handoff_deadline_s"] = timeout_s  # the deadline of the warm-up and timed solves
         print(json.dumps(out), flush=True)
     sol.close()

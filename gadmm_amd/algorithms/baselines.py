@@ -183,6 +183,8 @@ def model_bytes(units: np.ndarray, d: int) -> int:
 
 
 def _native_result(name, out, obj0, units, d: int, **extra) -> RunResult:
+    """``extra['transport']``: 'xgmi' when the run spanned ranks (FoFabric: device-initiated granule pushes
+    into IPC-mapped fine-grained memory), 'local' on one rank."""
     obj = out["obj"]
     n = len(obj)
     return RunResult(algorithm=name, obj=obj, loss=np.abs(obj - obj0), iters=out["iters"] if out["converged"] else n,
@@ -211,7 +213,7 @@ def gradient_descent(model, local_ids, n_total, num_iter, obj0, stepsize, comm=N
         out = eng.run("GD", num_iter, stepsize, obj0, tol, faithful)
         n = len(out["obj"])
         return _native_result("GD", out, obj0, np.arange(1, n + 1, dtype=np.float64) * (n_total + 1), ctx.d,
-                              final_theta=None)
+                              final_theta=None, transport="xgmi" if ctx.comm.nranks > 1 else "local")
     d = ctx.d
     theta = torch.zeros(d, dtype=torch.float64, device=ctx.dev)
     stop = Stopper(obj0, tol if tol is not None else -1.0, num_iter)
@@ -246,7 +248,8 @@ def decentralized_gd(model, local_ids, n_total, num_iter, obj0, stepsize, comm=N
     if eng is not None:
         out = eng.run("DGD", num_iter, stepsize / 100.0, obj0, tol, faithful)
         n = len(out["obj"])
-        return _native_result("DGD", out, obj0, np.arange(1, n + 1, dtype=np.float64) * n_total, ctx.d)
+        return _native_result("DGD", out, obj0, np.arange(1, n + 1, dtype=np.float64) * n_total, ctx.d,
+                              transport="xgmi" if ctx.comm.nranks > 1 else "local")
     d, dev = ctx.d, ctx.dev
     nl = len(ctx.local_ids)
     theta = torch.zeros((nl, d), dtype=torch.float64, device=dev)
@@ -358,7 +361,7 @@ def lag(model, local_ids, n_total, num_iter, obj0, stepsize, hmax_full: torch.Te
         out = eng.run("LAG-" + variant, num_iter, stepsize, obj0, tol, faithful, thrd=thrd,
                       hsq=hmax_full.to(dev, torch.float64) ** 2)
         return _native_result("LAG-" + variant, out, obj0, _lag_units(out["cnt"]), ctx.d,
-                              uploads=int(round(out["uploads"])))
+                              uploads=int(round(out["uploads"])), transport="xgmi" if ctx.comm.nranks > 1 else "local")
     ids = torch.tensor(ctx.local_ids, dtype=torch.long, device=dev)
     nl = len(ctx.local_ids)
     server = _Server(ctx, torch.ones((N, d), dtype=torch.float64, device=dev))
@@ -458,7 +461,8 @@ def iag(model, local_ids, n_total, num_iter, obj0, stepsize, mode: str = "cyclic
     if eng is not None:
         out = eng.run("IAG", num_iter, stepsize / n_total, obj0, tol, faithful, sched=sched)
         n = len(out["obj"])
-        return _native_result(name, out, obj0, np.arange(1, n + 1, dtype=np.float64) * 2, ctx.d)
+        return _native_result(name, out, obj0, np.arange(1, n + 1, dtype=np.float64) * 2, ctx.d,
+                              transport="xgmi" if ctx.comm.nranks > 1 else "local")
     d, dev = ctx.d, ctx.dev
     N = n_total
     step = stepsize / N

@@ -44,6 +44,7 @@ def dual_averaging(model, local_ids: Sequence[int], n_total: int, alpha: float, 
                              comm_units=np.arange(1, n + 1, dtype=np.float64) * n_total,
                              bytes_sent=int(out["payload_bytes"]), bytes_total=int(out["payload_bytes"]),
                              extra={"jacobi": jacobi, "nranks": comm.nranks, "engine": "native-persistent",
+                                    "transport": "xgmi" if comm.nranks > 1 else "local",
                                     "rows_pushed": out["rows_pushed"], "wire_bytes": out["wire_bytes"],
                                     "model_bytes": n * n_total * model.d * 8, "dim": model.d})
         from ..engine.first_order_big import FirstOrderBigEngine

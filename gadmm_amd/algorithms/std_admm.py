@@ -138,7 +138,7 @@ def _standard_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, c
                      bytes_sent=int(pay), bytes_total=int(pay),
                      extra={"hub": n_total - 1, "hub_rank": hub_rank, "nranks": comm.nranks, "backend": "native",
                             "engine": eng.last_kernel, "wire_bytes": int(wire), "monitor_bytes": int(mon),
-                            "engine_obj": eng})
+                            "transport": "xgmi" if fabric is not None else "local", "engine_obj": eng})
 
 
 def _standard_admm_big(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement, name, opts):

@@ -242,10 +242,10 @@ def _run(entry, body, cfg, sess, args) -> Dict:
     if sess.is_root:
         for k, r in res.get("runs", {}).items():
             s = r.summary()
-            print("  %-34s iters=%-7s converged=%-5s gap=%-10.3g wall=%.3fs comm_units=%s bytes=%s engine=%s "
+            print("  %-34s iters=%-7s converged=%-5s gap=%-10.3g wall=%.3fms comm_units=%s bytes=%s engine=%s "
                   "transport=%s" % (
                       k, s["iters"], s["converged"], s["final_loss"] if s["final_loss"] is not None else float("nan"),
-                      s["wall_s"], s["comm_units"], s["bytes_total"], s.get("engine", "torch"),
+                      1e3 * s["wall_s"], s["comm_units"], s["bytes_total"], s.get("engine", "torch"),
                       s.get("transport", _transport_of(sess))), flush=True)
         print("[%s] summary -> %s" % (entry, summary), flush=True)
     res["summary_path"] = summary

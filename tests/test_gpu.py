@@ -1191,10 +1191,22 @@ def _strict_err(A, Ar, eps=1e-12, rows=None):
     return float(e.max())
 
 
-def _ref_gram(X, y):
-    """f64 reference on the CPU (torch's blocked f64 GEMM, independent of both device kernels)."""
-    Xc, yc = X.cpu(), y.cpu()
-    return torch.bmm(Xc.transpose(1, 2), Xc), torch.bmm(Xc.transpose(1, 2), yc.unsqueeze(-1)).squeeze(-1)
+def _ref_gram(X, y, chunk: int = 1024):
+    """A more accurate f64 reference than one long GEMM (whose own error at m = 70000 is ~3e-14 of
+    sqrt(A_aa A_bb)): torch GEMMs over chunks of ``chunk`` rows, summed with Kahan compensation. Returned
+    on the CPU."""
+    N, m, d = X.shape
+    Xa = torch.cat([X, y.unsqueeze(-1)], dim=2)
+    S = torch.zeros((N, d + 1, d + 1), dtype=torch.float64, device=X.device)
+    c = torch.zeros_like(S)
+    for i0 in range(0, m, chunk):
+        blk = Xa[:, i0:i0 + chunk]
+        t = torch.bmm(blk.transpose(1, 2), blk) - c
+        s2 = S + t
+        c = (s2 - S) - t
+        S = s2
+    S = S.cpu()
+    return S[:, :d, :d].contiguous(), S[:, :d, d].contiguous()
 
 
 @pytest.mark.parametrize("case", ["outlier_row", "lognormal"])
@@ -1252,7 +1264,10 @@ def test_gram_ozaki_auto_shape_matches_f64():
     sc = torch.sqrt(torch.diagonal(Ar, dim1=1, dim2=2))
     ea = float(((A.cpu() - Ar).abs() / (sc.unsqueeze(2) * sc.unsqueeze(1))).max())
     eb = float(((b.cpu() - br).abs() / (sc * yy.cpu().sqrt().unsqueeze(1))).max())
-    assert ea < 1e-14 and eb < 1e-14, (ea, eb)
+    A64, b64, _ = linalg._gram_f64(X, y, None, None)
+    e64 = float(((A64.cpu() - Ar).abs() / (sc.unsqueeze(2) * sc.unsqueeze(1))).max())
+    print("auto shape: ozaki %.3g, f64-mfma %.3g (of sqrt(A_aa A_bb))" % (ea, e64))
+    assert ea < 1e-14 and eb < 1e-14, (ea, eb, e64)
 
 
 def test_gram_ozaki_gadmm_iterations_match_f64(monkeypatch):
@@ -1301,3 +1316,33 @@ def test_persistent_state_at_stop_equals_graph(lin24, lin_obj0, log24, log_obj0,
     (ta, ma, na), (tb, mb, nb) = a.extra["state"], b.extra["state"]
     assert na == nb == expect + 1, (na, nb, a.extra.get("state_from"))
     assert torch.equal(ta, tb) and torch.equal(ma, mb)
+
+
+@pytest.mark.parametrize("kernel", ["logistic", "newton"])
+def test_postfence_stress(log24, log_obj0, kernel, monkeypatch):
+    """the fence-free LDS ring posts (chain_persistent_logistic.hip zr_post,
+    chain_persistent_newton.hip lds_post) rely on a wave's LDS operations being performed in order, which
+    gfx950 provides (persist_device.h: GADMM_LDS_IN_ORDER). Stress: many back-to-back solves with the
+    fence-free posts and with the fenced ones (GADMM_*_POSTFENCE=1) give ONE bit-identical objective trace
+    and primal residual -- a post seen before its ring data would change a margin or a chord step."""
+    from gadmm_amd.models import LogisticRegression
+    from gadmm_amd.algorithms import chain_admm
+    m = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
+    if kernel == "logistic":
+        env, reps, expect = "GADMM_LOGISTIC_POSTFENCE", 16, 53
+        kw = dict(local_solver="gd", step=2.2)
+        rho, tol, it = 2e-4, 1e-4, 400
+    else:
+        env, reps, expect = "GADMM_NEWTON_POSTFENCE", 8, 424
+        kw = dict(local_solver="newton")
+        rho, tol, it = 1e-3, 1e-8, 2000
+    traces = {}
+    for fenced in ("0", "1"):
+        monkeypatch.setenv(env, fenced)
+        for _ in range(reps):
+            r = chain_admm(m, list(range(24)), 24, rho, log_obj0, tol, it,
+                           engine_opts={"cache": False, "state": False}, **kw)
+            assert r.extra["engine"] == "persistent" and r.iters == expect and r.converged
+            key = (r.obj.tobytes(), r.primal_res.tobytes() if r.primal_res is not None else b"")
+            traces[key] = traces.get(key, 0) + 1
+    assert len(traces) == 1, "%d distinct traces over %d solves" % (len(traces), 2 * reps)
