@@ -17,7 +17,8 @@ struct ChainCtl {
   int monitored;   // last iteration whose global objective has been checked
   int placed;      // persistent kernels' XCD placement (PersistArgs::xcd): 0 not packed, 1 packed
                   // (blocks b % 8 dealt) but not verified on one XCD (system-scope stores), 2 verified
-  int pad;
+  int inner_fail;  // local Newton solves that stopped at the step cap without converging (sticky; reset
+                   // zeroes it): the host re-solves with exact Newton (no chord steps) when it is set
 };
 
 // One slot of a phase plan: the local worker that updates in this phase and its chain neighbours.

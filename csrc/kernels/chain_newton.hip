@@ -299,6 +299,7 @@ __global__ void __launch_bounds__(NTN) chain_phase_logistic_newton(PhaseArgs a) 
     if (conv_lds) break;
     refresh = refresh_lds != 0;
   }
+  if (t == 0 && !conv_lds) atomicAdd(&ctl->inner_fail, 1);  // the step cap ended the solve unconverged
   if (hg && refreshed && chord > 0.0) {  // keep the newest inverse for this worker's next solve
 #pragma unroll
     for (int c = 0; c < NCW; ++c) hg[(c * NWV + wid) * 64 + lane] = h[c];

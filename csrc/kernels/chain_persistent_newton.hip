@@ -443,7 +443,7 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
   double tl = (inj && left >= 0) ? a.theta[(long)left * d + lane] : 0.0;
   double tr = (inj && right >= 0) ? a.theta[(long)right * d + lane] : 0.0;
   int pending = a.pending_in;
-  int stop_code = 0, stop_iter = 0, abort = 0, used = 0;
+  int stop_code = 0, stop_iter = 0, abort = 0, used = 0, nfail = 0;
   // Inverse bookkeeping (refresh ids are consecutive; refresh r lives in buffer r % 3):
   //   cur   the inverse the chord steps use (refresh 0, at the start point, requested in the set-up)
   //   pend  a background refresh in progress (-1: none), requested at iteration pend_it at the
@@ -545,6 +545,7 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
       const double mdx = wave_max_abs(dxl), mx = wave_max_abs(x);
       used = k + 1;
       if (mdx < NTOL * fmax(1.0, mx)) break;
+      if (k + 1 == NMAX) ++nfail;  // the step cap ends this solve unconverged
       if (chord <= 0.0 || (!fresh && k > 0 && mdx > chord * nd_prev)) {
         // contraction too slow: an inverse at the current x, from the crew (idle in this phase)
         const double z2 = quad_gemv<QT>(Xq, x, st);
@@ -624,6 +625,7 @@ __global__ void __launch_bounds__(NT) chain_persistent_newton_kernel(PersistArgs
   }
   if (lane == 0) {
     if (g.inner_iters) g.inner_iters[li] = used;
+    if (nfail) atomicAdd(&a.ctl->inner_fail, nfail);  // read by the host after the launch
     if (abort) {
       a.ctl->done = 4;
     } else if (bid == 0 && stop_code) {
@@ -1226,7 +1228,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
   double tl = (inj && left >= 0) ? a.theta[(long)left * d + lane] : 0.0;
   double tr = (inj && right >= 0) ? a.theta[(long)right * d + lane] : 0.0;
   int pending = a.pending_in;
-  int stop_code = 0, stop_iter = 0, abort = 0, used = 0;
+  int stop_code = 0, stop_iter = 0, abort = 0, used = 0, nfail = 0;
   // a background refresh requested at iteration i is adopted at i + RLAG; one is requested when a solve
   // took more than bg_steps chord steps (PersistArgs::dbg bits 8-11 / 12-15 override: GADMM_NEWTON_RLAG,
   // GADMM_NEWTON_BG)
@@ -1352,7 +1354,11 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
         REC_STAMP(1, sg, k);
         const double mdx = wave_max_abs_dpp(dxl), mx = wave_max_abs_dpp(x);
         used = ++ks;
-        if (mdx < NTOL * fmax(1.0, mx) || ks >= NMAX) { reason = 1; break; }
+        if (mdx < NTOL * fmax(1.0, mx) || ks >= NMAX) {
+          if (!(mdx < NTOL * fmax(1.0, mx))) ++nfail;  // the step cap ends this solve unconverged
+          reason = 1;
+          break;
+        }
         if (chord <= 0.0 || (!fresh && ks > 1 && mdx > chord * nd_prev)) { reason = 2; break; }
         fresh = false;
         nd_prev = mdx;
@@ -1448,6 +1454,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
   }
   if (lane == 0) {
     if (g.inner_iters) g.inner_iters[li] = used;
+    if (nfail) atomicAdd(&a.ctl->inner_fail, nfail);  // read by the host after the launch
     if (abort) {
       a.ctl->done = 4;
     } else if (bid == 0 && stop_code) {

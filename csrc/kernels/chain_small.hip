@@ -650,6 +650,7 @@ __global__ void chain_reset_kernel(ChainCtl* ctl, int start_iter, int pending) {
   ctl->pending = pending;
   ctl->ticket = 0u;
   ctl->monitored = start_iter - 1;
+  ctl->inner_fail = 0;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -768,6 +769,7 @@ __global__ void chain_reset_state_kernel(ChainCtl* ctl, int start_iter, int pend
     ctl->pending = pending;
     ctl->ticket = 0u;
     ctl->monitored = start_iter - 1;
+    ctl->inner_fail = 0;
   }
 }
 

@@ -427,6 +427,24 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         p2p, mon, wire = r.p2p_bytes, r.monitor_bytes, r.wire_bytes
         per = float(np.sum(schedule.cost)) * (n_heads if cost_quirk else 1)
         com_cost = np.arange(1, iters - start + 2) * per
+        if local_solver == "newton" and not opts.get("_exact_retry"):
+            # chord-Newton safety net: a local solve that reached the 50-step cap unconverged (a stale
+            # inverse can send the first chord steps far off: the derm-shaped E4 problem at rho = 0.02) means
+            # the iterates are not the exact prox the spec asks for (group_ADMM_logistic.m:26-49) -- the
+            # whole solve is re-run with exact Newton steps (every step refreshes its inverse), as torch does
+            fails = int(eng.ctl[7].item())
+            chord_used = eng.chord_persistent if engine_kind == "persistent" else eng.chord
+            if comm.nranks > 1:
+                import torch.distributed as dist
+                t = torch.tensor([float(fails)], dtype=torch.float64)
+                dist.all_reduce(t, group=getattr(comm, "control_group", None))
+                fails = int(t.item())
+            if fails > 0 and chord_used > 0.0:
+                res2 = _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm, placement,
+                                          schedule, local_solver, step, max_inner, inner_tol, cost_quirk, name,
+                                          dict(opts, chord=0.0, cache=False, _exact_retry=fails), state=state)
+                res2.extra["chord_fallback"] = "%d unconverged chord-Newton local solves: re-run exact" % fails
+                return res2
     elif want_persistent and eng.dynamic_eligible(fabric) \
             and len(_rechains(max_iter, schedule.coherence)) < (1 << 20):
         # D-GADMM in persistent launches of up to `epoch_chunk` epochs each: the seeded chain sequence

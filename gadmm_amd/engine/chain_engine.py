@@ -1017,7 +1017,8 @@ class NativeChainEngine:
 
     def ctl_state(self) -> dict:
         c = self.ctl.cpu().tolist()
-        return {"iter": c[0], "done": c[1], "conv_iter": c[2], "pending": c[3], "ticket": c[4], "monitored": c[5]}
+        return {"iter": c[0], "done": c[1], "conv_iter": c[2], "pending": c[3], "ticket": c[4], "monitored": c[5],
+                "placed": c[6], "inner_fail": c[7]}
 
     def objective_trace(self, upto: Optional[int] = None) -> np.ndarray:
         return (self.trace if upto is None else self.trace[:upto]).cpu().numpy()

@@ -1346,3 +1346,29 @@ def test_postfence_stress(log24, log_obj0, kernel, monkeypatch):
             key = (r.obj.tobytes(), r.primal_res.tobytes() if r.primal_res is not None else b"")
             traces[key] = traces.get(key, 0) + 1
     assert len(traces) == 1, "%d distinct traces over %d solves" % (len(traces), 2 * reps)
+
+
+@pytest.mark.parametrize("persistent", [True, False])
+def test_newton_chord_safety_net_e4_shape(log24, log_obj0, persistent):
+    """Chord-Newton reuses a worker's inverse Hessian across ADMM iterations; on the derm-shaped E4 problem
+    (LogisticRegression_Real stand-in: N = 10, d = 34, m = 35, rho = 0.02) a stale inverse sends the first
+    chord steps so far off that local solves hit the 50-step cap unconverged. The kernels count such solves
+    (ChainCtl::inner_fail) and the solve is re-run with exact Newton: the trace then follows torch's exact
+    prox (group_ADMM_logistic.m:26-49) -- and the E3 problem, where chord steps converge, never re-runs."""
+    from gadmm_amd.config import get_preset
+    from gadmm_amd.entry.common import full_dataset
+    from gadmm_amd.models import LogisticRegression
+    from gadmm_amd.algorithms import chain_admm
+    cfg = get_preset("LogisticRegression_Real")
+    ds = full_dataset(cfg)
+    m = LogisticRegression(ds.X.to(DEV).contiguous(), ds.y.to(DEV).contiguous(), lam=cfg.lam)
+    n = ds.num_workers
+    obj0 = m.optimum(None, n_total=n)
+    opts = {"cache": False, "persistent": persistent}
+    a = chain_admm(m, list(range(n)), n, 0.02, obj0, 1e-8, 60, local_solver="newton", engine_opts=opts)
+    t = chain_admm(m, list(range(n)), n, 0.02, obj0, 1e-8, 60, local_solver="newton", backend="torch")
+    assert "chord_fallback" in a.extra, a.extra
+    np.testing.assert_allclose(a.obj, t.obj, rtol=1e-10, atol=0)
+    e3 = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
+    b = chain_admm(e3, list(range(24)), 24, 1e-3, log_obj0, 1e-8, 2000, local_solver="newton", engine_opts=opts)
+    assert b.iters == 424 and "chord_fallback" not in b.extra
