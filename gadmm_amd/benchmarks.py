@@ -58,7 +58,7 @@ EXPECTED_OTHER = {("dgadmm", 24, 10): 510, ("dgadmm", 24, 1): 252, ("dgadmm", 8,
 # the 1e-8 relative gap -- keyed by (GPUs, rows per GPU, features); measured on an MI355X with
 # bench.py --config real10m (its iterations_torch_reference; profiles/r06_real10m). Shapes not listed are
 # checked against the torch path inline, untimed (it runs in every real10m bench anyway).
-EXPECTED_REAL10M: Dict = {}
+EXPECTED_REAL10M: Dict = {(1, 1_250_000, 10_000): 25}
 
 
 def reference_expected(config: str, n: int, coherence: int = 10):
