@@ -35,6 +35,7 @@ import time
 from dataclasses import dataclass
 from typing import Optional, Sequence
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -191,7 +192,11 @@ class DistributedChainSolver:
             self.comm, self._own_comm = make_data_plane(fabric, self.world, self.device, self.share, self.n,
                                                         self.d, self.block, timeout_s=self.timeout_s), True
         self.kind = self.comm.selection["data_plane"]
-        self.eng = self._engine(self.comm)
+        if getattr(self.comm, "backend", "") == "host-gloo":  # no device transport came up anywhere
+            self.eng = TorchPathEngine(self.X, self.y, self.local, self.n, self.placement, self.comm, self.rho,
+                                       self.obj0, self.tol, self.max_iter)
+        else:
+            self.eng = self._engine(self.comm)
         self.persistent = False
 
     def can_fall_back(self) -> bool:
@@ -283,6 +288,60 @@ class DistributedChainSolver:
             if o is not None:
                 o.close()
         self.eng = self.blk = self.fab = self.comm = None
+
+
+class TorchPathEngine:
+    """The last-resort engine of a multi-GPU solve (``HostStagedComm`` data plane: neither the IPC
+    transport nor RCCL came up): the torch GADMM loop (algorithms/gadmm._chain_admm_torch, the executable
+    spec of group_ADMM_closedForm.m) on the device shards, neighbour theta staged through host memory
+    over gloo. Same interface as the parts of NativeChainEngine that DistributedChainSolver uses."""
+
+    def __init__(self, X, y, local, n_total, placement, comm, rho, obj0, tol, max_iter):
+        from ..models import LinearRegression
+        self.X, self.y, self.local, self.n, self.placement, self.comm = X, y, list(local), n_total, placement, comm
+        self.rho, self.obj0, self.tol, self.max_iter = rho, obj0, tol, max_iter
+        self.model = LinearRegression(X, y)
+        self.last = None
+
+    def refresh(self, X, y):
+        from ..ops.linalg import gram
+        gram(X, y, out=(self.model.A, self.model.b, self.model.yy))
+        self.model._chol = {}
+
+    def reset(self, start_iter: int = 1):
+        self.last = None
+
+    def run(self, stop_iter: int = 0, use_graph: bool = True):
+        import time as _t
+        from ..algorithms.gadmm import chain_admm
+        t0 = _t.perf_counter()
+        snap = self.comm.stats.snapshot()
+        r = chain_admm(self.model, self.local, self.n, self.rho, self.obj0, self.tol, self.max_iter, comm=self.comm,
+                       placement=self.placement, backend="torch")
+        self.last = r
+        pay = int(self.comm.stats.delta(snap)["bytes_sent"])
+        mon = int(self.comm.stats.delta(snap)["monitor_bytes"])
+
+        class _R:
+            pass
+        o = _R()
+        o.iters, o.done = int(r.iters), (1 if r.converged else 2)
+        o.p2p_bytes, o.wire_bytes, o.monitor_bytes = pay, pay, mon
+        o.wall_ms = (_t.perf_counter() - t0) * 1e3
+        return o
+
+    def objective_trace(self, upto=None):
+        tr = self.last.obj if self.last is not None else np.zeros(0)
+        return tr if upto is None else tr[:upto]
+
+    def traces(self, upto: int):
+        return self.objective_trace(upto), np.asarray(self.last.time_trace[:upto])
+
+    def graph_ok(self) -> bool:
+        return False
+
+    def close(self):
+        self.last = None
 
 
 def node_chain_admm(model, local_ids: Sequence[int], n_total: int, placement, rank: int, world: int,

@@ -195,6 +195,75 @@ class TorchDistComm(Comm):
         return t
 
 
+class HostStagedComm(TorchDistComm):
+    """The last-resort data plane of a GPU run: torch.distributed over the gloo control plane, device
+    tensors staged through host memory. Used only when neither the IPC transport nor RCCL comes up on
+    every rank (parallel/dataplane.py); the engines then run the torch loops (slow, but a result)."""
+
+    def __init__(self, group=None):
+        super().__init__(group)
+        self.backend = "host-gloo"
+        self.control_group = group
+
+    @staticmethod
+    def _host(t):
+        return t.detach().to("cpu").contiguous()
+
+    def exchange_rows(self, table, ops):
+        if not ops:
+            return
+        p2p, recv_bufs = [], []
+        for peer, row, snd in ops:
+            if snd:
+                buf = self._host(table[row])
+                p2p.append(dist.P2POp(dist.isend, buf, int(peer), self.group))
+                self.stats.bytes_sent += buf.numel() * buf.element_size()
+                self.stats.msgs_sent += 1
+            else:
+                buf = torch.empty(table[row].shape, dtype=table.dtype)
+                recv_bufs.append((row, buf))
+                p2p.append(dist.P2POp(dist.irecv, buf, int(peer), self.group))
+                self.stats.bytes_recv += buf.numel() * buf.element_size()
+        for r in dist.batch_isend_irecv(p2p):
+            r.wait()
+        for row, buf in recv_bufs:
+            table[row].copy_(buf)
+
+    def send_tensor(self, t, peer):
+        h = self._host(t)
+        dist.send(h, int(peer), group=self.group)
+        self.stats.bytes_sent += h.numel() * h.element_size()
+        self.stats.msgs_sent += 1
+
+    def recv_tensor(self, t, peer):
+        h = torch.empty(t.shape, dtype=t.dtype)
+        dist.recv(h, int(peer), group=self.group)
+        t.copy_(h)
+        self.stats.bytes_recv += h.numel() * h.element_size()
+
+    def allreduce_sum(self, t):
+        h = self._host(t)
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
+        t.copy_(h)
+        self.stats.coll_bytes += t.numel() * t.element_size()
+        return t
+
+    def reduce_sum(self, t, root):
+        h = self._host(t)
+        dist.reduce(h, dst=root, op=dist.ReduceOp.SUM, group=self.group)
+        if self.rank == root:
+            t.copy_(h)
+        self.stats.coll_bytes += t.numel() * t.element_size()
+        return t
+
+    def broadcast(self, t, root):
+        h = self._host(t)
+        dist.broadcast(h, src=root, group=self.group)
+        t.copy_(h)
+        self.stats.coll_bytes += t.numel() * t.element_size()
+        return t
+
+
 class RcclComm(Comm):
     """Native RCCL communicator (libgadmm_native). The unique id travels over an existing
     torch.distributed group (the gloo control plane).

@@ -15,7 +15,9 @@ framework has three ways to move those bytes:
   ranks on one device, so ranks sharing a GPU (the one-box rehearsal) never get it.
 
 ``choose_data_plane`` is the pure selection rule (CPU-tested); ``make_data_plane`` builds the comm
-collectively, with the RCCL -> IPC fallback agreed over the gloo control plane.
+collectively, with the RCCL -> IPC fallback agreed over the gloo control plane, and -- if the IPC
+transport itself fails on any rank -- a last-resort host-staged gloo comm (``HostStagedComm``) on which
+the engines run their torch loops.
 """
 from __future__ import annotations
 
@@ -77,6 +79,22 @@ def make_data_plane(fabric: str, world: int, device, share: bool, n_total: int, 
         reason = "RCCL unavailable on some rank (%s); IPC transport" % (err or "another rank")
         (log or (lambda m: print(m, file=sys.stderr, flush=True)))("data plane: " + reason)
     from .ipc import IpcComm
-    c = IpcComm(n_total, d, ring, device, group=group, timeout_s=timeout_s)
-    c.selection = {"requested": fabric, "data_plane": "ipc", "reason": reason}
-    return c
+    c, err = None, ""
+    try:
+        c = IpcComm(n_total, d, ring, device, group=group, timeout_s=timeout_s)
+    except Exception as e:  # collective inside: a failure anywhere raises on every rank
+        err = "%s: %s" % (type(e).__name__, e)
+    if _agree(c is not None, world, group):
+        c.selection = {"requested": fabric, "data_plane": "ipc", "reason": reason}
+        return c
+    if c is not None:
+        c.close()
+    # last resort: the gloo control plane with device tensors staged through host memory -- slow, but
+    # every algorithm still runs (the engines take their torch loops)
+    from .comm import HostStagedComm
+    (log or (lambda m: print(m, file=sys.stderr, flush=True)))(
+        "data plane: IPC transport unavailable (%s); host-staged gloo" % (err or "another rank"))
+    h = HostStagedComm(group)
+    h.selection = {"requested": fabric, "data_plane": "host-gloo",
+                   "reason": "IPC transport unavailable on some rank (%s)" % (err or "another rank")}
+    return h

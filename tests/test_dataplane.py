@@ -134,3 +134,38 @@ def test_rccl_watchdog_abort_on_one_rank_falls_back_collectively():
         assert r["old"] == (True, True)        # the RCCL communicator aborted, then closed
         assert len(r["fallbacks"]) == 1 and "rccl solve failed" in r["fallbacks"][0]
         assert r["can"] is False               # nothing further to fall back to
+
+
+def _host_fallback_rank(rank, world):
+    """IPC transport fails on rank 1 -> every rank gets the host-staged gloo plane, and the last-resort
+    torch-path engine solves the headline problem over it (1373 iterations, like every engine)."""
+    import gadmm_amd.parallel.ipc as I
+    from gadmm_amd.parallel.dataplane import make_data_plane
+    from gadmm_amd.engine.multigpu import TorchPathEngine
+    from gadmm_amd.benchmarks import headline_rank_problem
+
+    class FailIpc:
+        def __init__(self, n_total, d, ring, device, group=None, timeout_s=20.0):
+            if rank == 1:
+                raise RuntimeError("hipIpcOpenMemHandle: invalid argument")
+            self.closed = False
+
+        def close(self):
+            self.closed = True
+
+    I.IpcComm = FailIpc
+    c = make_data_plane("auto", world, "cpu", False, 24, 50, 16, timeout_s=3.0, log=lambda m: None)
+    X, y, local, pl, obj0 = headline_rank_problem(24, rank, world)
+    eng = TorchPathEngine(X, y, local, 24, pl, c, 3.0, obj0, 1e-8, 2000)
+    eng.refresh(X, y)
+    r = eng.run()
+    return {"backend": c.backend, "sel": c.selection["data_plane"], "iters": r.iters, "done": r.done,
+            "bytes": r.p2p_bytes}
+
+
+def test_ipc_failure_falls_back_to_host_staged_plane():
+    res = spawn(_host_fallback_rank, 2, timeout=300)
+    for r in res:
+        assert r["backend"] == "host-gloo" and r["sel"] == "host-gloo"
+        assert r["iters"] == 1373 and r["done"] == 1
+        assert r["bytes"] == 1373 * 50 * 8  # one boundary: each rank sends its edge worker's theta once per iteration
