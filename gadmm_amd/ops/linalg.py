@@ -66,6 +66,35 @@ def gram_ozaki(X: torch.Tensor, y: torch.Tensor, out=None, with_range: bool = Fa
     return (A, b, yy, rng) if with_range else (A, b, yy)
 
 
+def gram_crt(X: torch.Tensor, y: torch.Tensor, out=None, with_range: bool = False):
+    """Batched augmented Gram on the INT8 matrix cores by CRT slicing (csrc/kernels/gram_crt.hip: 49-bit
+    integer images of the column-scaled values, one int8 GEMM with exact int32 sums per modulus for 19
+    coprime moduli <= 127, Garner reconstruction of the exact integer Gram, one final rounding). Same
+    outputs and accuracy class as ``gram_ozaki`` (the digit scheme keeps the same 49 bits); one accumulator
+    per output element instead of seven, so 256 x 256 tiles. m <= 2^21 rows per shard. ``with_range``:
+    also the (N,) column-range statistics of the accuracy gate."""
+    lib = native.require()
+    X = X.contiguous()
+    y = y.contiguous()
+    N, m, d = X.shape
+    if m > int(lib.gadmm_gram_crt_max_rows()):
+        raise ValueError("gram_crt: %d rows per shard exceed the exact-reconstruction bound" % m)
+    if out is not None:
+        A, b, yy = out
+    else:
+        A = torch.empty((N, d, d), dtype=torch.float64, device=X.device)
+        b = torch.empty((N, d), dtype=torch.float64, device=X.device)
+        yy = torch.empty((N,), dtype=torch.float64, device=X.device)
+    rng = torch.empty((N,), dtype=torch.float64, device=X.device)
+    nb = int(lib.gadmm_gram_crt_workspace(int(m), int(d)))
+    ws = torch.empty((nb,), dtype=torch.uint8, device=X.device)
+    native.check(lib.gadmm_gram_crt_f64(X.data_ptr(), y.data_ptr(), int(N), int(m), int(d), A.data_ptr(),
+                                        b.data_ptr(), yy.data_ptr(), ws.data_ptr(), nb, rng.data_ptr(),
+                                        native.stream_handle()), "gram_crt_f64")
+    del ws
+    return (A, b, yy, rng) if with_range else (A, b, yy)
+
+
 def gram_uses_ozaki(m: int, d: int) -> bool:
     """Whether ``gram`` tries the int8 Ozaki path. ``GADMM_GRAM_OZAKI``: ``auto`` (default) for shards of
     d >= 3072 features and m >= 65536 samples, where it measured faster than the f64-MFMA Gram (1.11x at

@@ -250,6 +250,10 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_rccl_wait": (c_int, [c_void_p, c_void_p, ctypes.c_double]),
         "gadmm_debug_busy_wait": (c_int, [ctypes.c_double, c_void_p]),
         "gadmm_gram_ozaki_workspace": (c_long, [c_long, c_int]),
+        "gadmm_gram_crt_workspace": (c_long, [c_long, c_int]),
+        "gadmm_gram_crt_max_rows": (c_long, []),
+        "gadmm_gram_crt_f64": (c_int, [c_void_p, c_void_p, c_int, c_long, c_int, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_long, c_void_p, c_void_p]),
         "gadmm_gram_ozaki_f64": (c_int, [c_void_p, c_void_p, c_int, c_long, c_int, c_void_p, c_void_p, c_void_p,
                                          c_void_p, c_long, c_void_p, c_void_p]),
         "gadmm_chain_engine_set_timeout": (c_int, [c_void_p, ctypes.c_double]),

@@ -1372,3 +1372,32 @@ def test_newton_chord_safety_net_e4_shape(log24, log_obj0, persistent):
     e3 = LogisticRegression(log24.X.to(DEV), log24.y.to(DEV), lam=1e-5)
     b = chain_admm(e3, list(range(24)), 24, 1e-3, log_obj0, 1e-8, 2000, local_solver="newton", engine_opts=opts)
     assert b.iters == 424 and "chord_fallback" not in b.extra
+
+
+@pytest.mark.parametrize("N,m,d", [(2, 5000, 300), (1, 20000, 97), (1, 9000, 1000), (1, 70000, 600)])
+def test_gram_crt_matches_f64(N, m, d):
+    """The CRT int8 Gram (gram_crt.hip: 49-bit integer images, 19 modular int8 GEMMs with exact int32 sums,
+    Garner reconstruction): every entry within 1e-14 of sqrt(A_aa A_bb) of the Kahan-chunked f64 reference
+    (chunk boundaries at 32768 samples and padded 256-feature tiles included), b and y'y likewise, exactly
+    symmetric, deterministic; the range statistic equals the digit kernel's."""
+    from gadmm_amd.ops.linalg import gram_crt, gram_ozaki
+    g = torch.Generator(device=DEV)
+    g.manual_seed(N * 1000 + d)
+    X = torch.randn((N, m, d), dtype=torch.float64, device=DEV, generator=g) * 3.0
+    X[:, :, 0] *= 1e-3
+    y = torch.randn((N, m), dtype=torch.float64, device=DEV, generator=g)
+    A, b, yy, rng = gram_crt(X, y, with_range=True)
+    Ar, br = _ref_gram(X, y)
+    sc = torch.sqrt(torch.diagonal(Ar, dim1=1, dim2=2))
+    assert torch.equal(A, A.transpose(1, 2))
+    ea = float(((A.cpu() - Ar).abs() / (sc.unsqueeze(2) * sc.unsqueeze(1))).max())
+    eb = float(((b.cpu() - br).abs() / (sc * yy.cpu().sqrt().unsqueeze(1))).max())
+    yr = (y.cpu() * y.cpu()).sum(1)
+    ey = float(((yy.cpu() - yr).abs() / yr).max())
+    Ao, _, _, rng_o = gram_ozaki(X, y, with_range=True)
+    eo = float(((Ao.cpu() - Ar).abs() / (sc.unsqueeze(2) * sc.unsqueeze(1))).max())
+    print("crt %.3g, digits %.3g (of sqrt(A_aa A_bb)); range %.4g / %.4g" % (ea, eo, float(rng.max()), float(rng_o.max())))
+    assert ea < 1e-14 and eb < 1e-14 and ey < 1e-14, (ea, eb, ey, eo)
+    assert torch.allclose(rng, rng_o, rtol=1e-12)
+    A2 = gram_crt(X, y)[0]
+    assert torch.equal(A, A2)
