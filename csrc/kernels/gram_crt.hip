@@ -7,9 +7,9 @@
 // by its power-of-two exponent e_j, |x_ij| <= (127/128) 2^{e_j}) becomes the integer
 //   N_ij = rint(x_ij 2^{KB - e_j}),   |N_ij| < 2^KB,  KB = 49   (the digit scheme keeps the same 49 bits)
 // and the integer Gram  G_ab = sum_i N_ia N_ib  (|G| < m 2^98 <= 2^119 for m <= 2^21) is computed modulo
-// 19 pairwise coprime moduli p <= 127 (product ~2^121.8): for each p, the symmetric residues
-// R_p = N mod p in [-63, 63] are int8, and  G mod p = R_p^T R_p mod p  is ONE int8 GEMM with exact int32
-// accumulation (a chunk of KC samples: KC * 63^2 < 2^31), reduced mod p after every chunk. Garner's
+// 19 pairwise coprime moduli p <= 127 (product ~2^121.8): for each p, residues R_p == N mod p with
+// |R_p| <= 68 are int8, and  G mod p = R_p^T R_p mod p  is ONE int8 GEMM with exact int32 accumulation
+// (a chunk of KC samples: KC * 68^2 < 2^31), reduced mod p after every chunk. Garner's
 // mixed-radix reconstruction then gives G_ab exactly, and
 //   A_ab = 2^{e_a + e_b - 2 KB} G_ab
 // with one rounding (the final double). So the result is exact for the 49-bit images of the inputs -- the
@@ -19,8 +19,9 @@
 //
 // Kernels (host driver gadmm_gram_crt_f64 below, per shard, one chunk of KC samples at a time):
 //   crt_colmax / crt_colexp   column exponents e_j of the augmented [X | y] (one pass)
-//   crt_slice     residues of a chunk: R[p][kb][j][32] int8 -- modulus p, 32-sample block kb, feature j,
-//                 the block's 32 samples contiguous (one MFMA operand half-fragment = 16 contiguous bytes)
+//   crt_slice     residues of a chunk: R[p][kb][h][j][16] int8 -- modulus p, 32-sample block kb, half h of
+//                 the block (samples 16 h ..), feature j: one MFMA operand half-fragment = 16 contiguous
+//                 bytes, and the 64 features of one LDS-DMA piece 1 KB contiguous
 //   crt_gemm      one workgroup per (lower-triangle 256 x 256 tile, modulus): LDS-DMA double-buffered
 //                 panels (64 samples per stage), 16 v_mfma_i32_32x32x32_i8 per wave per stage; the chunk's
 //                 sums go into the int16 residue matrices C_p (reduced mod p)
@@ -29,6 +30,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <algorithm>
+#include <utility>
 #include <map>
 #include <mutex>
 #include <vector>
@@ -67,13 +69,11 @@ __constant__ int kModDev[NMOD] = {127, 125, 121, 113, 109, 107, 103, 101, 97, 89
 
 constexpr int KB = 49;            // bits of every value's integer image (|N| < 2^KB)
 constexpr long MAX_ROWS = 1L << 21;  // m 2^{2 KB} < M / 2 (the product of the moduli): exact reconstruction
-constexpr int KC = 32768;         // samples per chunk: KC * 63^2 < 2^31 (exact int32 sums)
+constexpr int KC = 32768;         // samples per chunk: KC * 68^2 < 2^31 (exact int32 sums)
 constexpr int KBC = KC / 32;      // 32-sample blocks per chunk
+constexpr int KBCP = KBC + 4;     // residue-buffer slots per modulus: a chunk zero-filled to whole stages
 constexpr int TT = 256;           // output tile (features) per workgroup
 constexpr int GNT = 512;          // 8 waves: 2 (rows of 128) x 4 (columns of 64)
-constexpr int BKS = 2;            // 32-sample blocks per pipeline stage (64 samples)
-constexpr int PANEL = BKS * TT * 32;           // bytes of one operand panel per stage (16 KB)
-constexpr int STAGE = 2 * PANEL;               // A + B (32 KB)
 constexpr int CE_NT = 256;        // column-exponent threads per workgroup
 constexpr int CE_R = 128;         // row splits of the column-exponent pass
 constexpr int SLT = 128;          // features per slicing workgroup
@@ -112,42 +112,81 @@ __global__ void __launch_bounds__(CE_NT) crt_colexp(const double* part, int Dp, 
   e[j] = E;
 }
 
-// Residues of samples [i0, i0 + 32 kbn) into R[p][kb][j][32]: a workgroup takes 32 samples x SLT
-// features; the integer images go through LDS (each thread reads back only its own column), then per
-// modulus every thread writes its feature's 32-byte run.
-__global__ void __launch_bounds__(SLT) crt_slice(const double* X, const double* y, long i0, long m, int d, int Dp,
+// Residues of samples [i0, i0 + 32 kbn) (zero from iend on) into R[p][kb][h][j][16]: a thread takes one
+// feature and 16 samples (one half h) at a time, so a wave's store per modulus is 1 KB contiguous (with
+// [j][32] rows, each store covered half of a 2 KB span: the slicer ran at ~2.4 TB/s). Each integer image N is split
+// once into 13-bit digits, N = d3 2^39 + d2 2^26 + d1 2^13 + d0 (d3 in [-2^10, 2^10), the others in
+// [0, 2^13); exact double floor / fma), held as floats with d0 offset by MAGIC = 1.5 2^23. Then per modulus,
+// in f32 only (exact: every intermediate is an integer below 2^24):
+//   S' = MAGIC + d0 + d1 (2^13 mod p) + d2 (2^26 mod p) + d3 (2^39 mod p)   in [2^23, 2^24), S' - MAGIC == N mod p
+//   q  = rint(S' / p - MAGIC / p)         (one fma with rounded constants: within 0.041 of (S' - MAGIC) / p)
+//   t  = S' - q p = MAGIC + r,  |r| <= 68 (|(S' - MAGIC) / p - q| <= 0.541)
+// and the low byte of t's bit pattern IS r as int8 (the exponent is fixed at 2^23 over the whole range).
+// r is a valid int8 representative of N mod p (not always the balanced one, which nothing needs: the GEMM
+// epilogue reduces mod p, and the chunk sums stay exact, KC 68^2 < 2^31). Six f32 instructions per residue;
+// round 6's first version (a per-modulus f64 divide-and-correct) made the slicer 12 % of the Gram, and
+// plain int products compile to quarter-rate v_mul_lo_u32 / v_mad_u64_u32 (profiles/r06_crt).
+constexpr float MAGIC = 12582912.0f;  // 1.5 2^23
+constexpr int p2mod(int k, int p) {
+  int r = 1 % p;
+  for (int i = 0; i < k; ++i) r = (r * 2) % p;
+  return r;
+}
+template <int P>
+__device__ __forceinline__ unsigned crt_res(float D0, float d1, float d2, float d3) {
+  constexpr int mp = kMod[P];
+  constexpr float w1 = (float)p2mod(13, mp), w2 = (float)p2mod(26, mp), w3 = (float)p2mod(39, mp);
+  constexpr float fp = (float)mp, ip = 1.0f / (float)mp, nm = -MAGIC / (float)mp;
+  const float S = __builtin_fmaf(d3, w3, __builtin_fmaf(d2, w2, __builtin_fmaf(d1, w1, D0)));
+  const float q = __builtin_rintf(__builtin_fmaf(S, ip, nm));
+  return __float_as_uint(__builtin_fmaf(-q, fp, S));  // low byte = r
+}
+template <int P>
+__device__ __forceinline__ void crt_res_store(const float (&D)[4][16], signed char* dst) {
+  int w[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    unsigned u[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) u[b] = crt_res<P>(D[0][4 * q + b], D[1][4 * q + b], D[2][4 * q + b], D[3][4 * q + b]);
+    // v_perm_b32 (selector bytes 0-3: src1's bytes, 4-7: src0's, 0x0c: zero): the four low bytes in order
+    const unsigned lo = __builtin_amdgcn_perm(u[1], u[0], 0x0c0c0400u);
+    const unsigned hi = __builtin_amdgcn_perm(u[3], u[2], 0x0c0c0400u);
+    w[q] = (int)__builtin_amdgcn_perm(hi, lo, 0x05040100u);
+  }
+  *reinterpret_cast<v4i*>(dst) = v4i{w[0], w[1], w[2], w[3]};
+}
+template <int... Ps>
+__device__ __forceinline__ void crt_res_all(const float (&D)[4][16], signed char* dst, long pstride,
+                                            std::integer_sequence<int, Ps...>) {
+  (crt_res_store<Ps>(D, dst + Ps * pstride), ...);
+}
+__global__ void __launch_bounds__(SLT) crt_slice(const double* X, const double* y, long i0, long iend, int d, int Dp,
                                                  const int* e, signed char* R) {
-  __shared__ double xs[32][SLT];
+  // iend: the chunk's end (min(m, i0 + KC)); the blocks padded up to a whole stage beyond it are zeros
   const int kb = blockIdx.y;
   const int j = blockIdx.x * SLT + threadIdx.x;
-  const bool on = j < Dp;
-  const int ej = on ? e[j] : 0;
-  for (int t = 0; t < 32; ++t) {
-    const long i = i0 + (long)kb * 32 + t;
-    xs[t][threadIdx.x] = on ? rint(ldexp(aug_at(X, y, i, j, m, d), KB - ej)) : 0.0;  // exact: |N| < 2^49
-  }
-  if (!on) return;
-  for (int p = 0; p < NMOD; ++p) {
-    const double mp = (double)kModDev[p], ip = 1.0 / mp, half = 0.5 * (mp - 1.0);
-    int w[8];
+  if (j >= Dp) return;
+  const int ej = e[j];
+#pragma unroll 1
+  for (int hh = 0; hh < 2; ++hh) {
+    float D[4][16];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      unsigned word = 0;
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        const double nv = xs[4 * q + b][threadIdx.x];
-        const double qq = floor(nv * ip);  // within one of floor(nv / p): |nv ip| < 2^43, error < 2^-9
-        double r = fma(-qq, mp, nv);        // exact integer in [-p, 2p)
-        if (r < 0.0) r += mp;
-        if (r >= mp) r -= mp;
-        if (r > half) r -= mp;              // symmetric residue in [-63, 63]
-        word |= ((unsigned)(int)r & 0xffu) << (8 * b);
-      }
-      w[q] = (int)word;
+    for (int t = 0; t < 16; ++t) {
+      const long i = i0 + (long)kb * 32 + hh * 16 + t;
+      const double n = rint(ldexp(aug_at(X, y, i, j, iend, d), KB - ej));  // exact: |N| < 2^49
+      const double a3 = floor(n * 0x1p-39);
+      const double r3 = fma(-a3, 0x1p39, n);
+      const double a2 = floor(r3 * 0x1p-26);
+      const double r2 = fma(-a2, 0x1p26, r3);
+      const double a1 = floor(r2 * 0x1p-13);
+      D[3][t] = (float)a3;
+      D[2][t] = (float)a2;
+      D[1][t] = (float)a1;
+      D[0][t] = (float)fma(-a1, 0x1p13, r2) + MAGIC;
     }
-    v4i* d4 = reinterpret_cast<v4i*>(R + (((long)p * KBC + kb) * Dp + j) * 32);
-    d4[0] = v4i{w[0], w[1], w[2], w[3]};
-    d4[1] = v4i{w[4], w[5], w[6], w[7]};
+    crt_res_all(D, R + (long)kb * Dp * 32 + (long)hh * Dp * 16 + (long)j * 16, (long)KBCP * Dp * 32,
+                std::make_integer_sequence<int, NMOD>{});
   }
 }
 
@@ -156,12 +195,27 @@ __global__ void __launch_bounds__(SLT) crt_slice(const double* X, const double* 
 // 128 wr .. +127 (4 blocks of 32) and columns 64 wc .. +63 (2 blocks). Per stage (64 samples = 2 MFMA
 // K-steps) the A and B panels (each 2 x 256 features x 32 samples, 16 KB, contiguous in global memory
 // and in LDS) come in by LDS-DMA (global_load_lds_dwordx4: a wave instruction moves 1 KB; 32 per stage,
-// 4 per wave), double-buffered: stage s + 1's DMAs fly while stage s's 16 MFMAs per wave issue. A
+// 4 per wave) through a 4-buffer ring, three stages ahead of the 16 MFMAs per wave of the current one. A
 // fragment read (ds_read_b128 of 64 lanes: 32 consecutive features x 2 halves) covers 1 KB contiguous:
 // conflict-free.
+// s_waitcnt through the builtin (not inline asm: the compiler's wait-count pass treats an asm statement
+// as unknown LDS / memory traffic and then drains every later use to lgkmcnt(0), which would put the
+// stage's fragment reads back in front of the MFMAs they are meant to overlap). gfx9 encoding: vmcnt
+// bits [3:0] and [15:14], expcnt [6:4], lgkmcnt [11:8]; unnamed counters at their maxima.
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4)); }
+
+// BKS: 32-sample blocks per pipeline stage; NSTG: LDS ring of stage buffers (NSTG - 1 stages in flight)
+template <int BKS, int NSTG>
 __global__ void __launch_bounds__(GNT, 1) crt_gemm(const signed char* R, int Dp, int total, const int4* list,
                                                    int kbn, short* C, int first) {
-  extern __shared__ __attribute__((aligned(16))) signed char lds[];  // 2 stages x STAGE bytes
+  constexpr int PANEL = BKS * TT * 32;  // bytes of one operand panel per stage
+  constexpr int STAGE = 2 * PANEL;      // A + B
+  constexpr int P = 2 * BKS;            // DMA pieces (1 KB) per wave per stage
+  extern __shared__ __attribute__((aligned(16))) signed char lds[];  // NSTG stages x STAGE bytes
   const int per_xcd = (total + 7) / 8;
   const int t = (int)(blockIdx.x & 7) * per_xcd + (int)(blockIdx.x >> 3);
   if (t >= total) return;
@@ -171,18 +225,22 @@ __global__ void __launch_bounds__(GNT, 1) crt_gemm(const signed char* R, int Dp,
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int wr = wv >> 2, wc = wv & 3;
   const int r = lane & 31, h = lane >> 5;
-  const signed char* gA = R + ((long)p * KBC * Dp + (long)ti * TT) * 32;  // + kb * Dp * 32
-  const signed char* gB = R + ((long)p * KBC * Dp + (long)tj * TT) * 32;
+  const signed char* gA = R + (long)p * KBCP * Dp * 32 + (long)ti * TT * 16;  // + kb * Dp * 32 + h * Dp * 16
+  const signed char* gB = R + (long)p * KBCP * Dp * 32 + (long)tj * TT * 16;
   const long kbstride = (long)Dp * 32;
-  // this wave's 4 DMA pieces per stage: piece c = 4 wv + u (0..31): panel c >> 4 (A / B), block
-  // (c >> 3) & 1 of the stage, 1 KB part c & 7 of the 8 KB (256 features x 32 B) run
+  // LDS image of a stage: [panel A / B][32-sample block][half of the block: samples 16 h ..][feature][16 B]
+  // -- the global layout's order, so every DMA piece is 1 KB contiguous on both sides, and a fragment
+  // read (32 consecutive features of one half per 32 lanes) is 512 B contiguous and conflict-free in
+  // ds_read_b128's lane groups (with [feature][32 B] rows the 32-B stride used only half of the banks:
+  // 2-way conflicts). This wave's P pieces per stage: piece c = P wv + u: panel c / (8 BKS), block
+  // (c / 8) % BKS, half (c / 4) % 2, features 64 (c % 4) .. + 63 (1 KB of LDS).
   auto issue = [&](int kb0, int buf) {
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const int c = 4 * wv + u;
-      const int pn = c >> 4, blk = (c >> 3) & 1, part = c & 7;
-      const signed char* src = (pn ? gB : gA) + (long)(kb0 + blk) * kbstride + part * 1024 + lane * 16;
-      signed char* dst = lds + buf * STAGE + pn * PANEL + blk * (TT * 32) + part * 1024;
+    for (int u = 0; u < P; ++u) {
+      const int c = P * wv + u;
+      const int pn = c / (8 * BKS), blk = (c >> 3) % BKS, hh = (c >> 2) & 1, q = c & 3;
+      const signed char* src = (pn ? gB : gA) + (long)(kb0 + blk) * kbstride + (long)hh * (kbstride / 2) + (q * 64 + lane) * 16;
+      signed char* dst = lds + buf * STAGE + pn * PANEL + blk * (TT * 32) + hh * (TT * 16) + q * 1024;
       __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
     }
   };
@@ -191,24 +249,31 @@ __global__ void __launch_bounds__(GNT, 1) crt_gemm(const signed char* R, int Dp,
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b) acc[a][b] = v16i{};
-  const int nst = kbn / BKS;  // kbn is even (the slicer zero-fills to a stage boundary)
-  issue(0, 0);
-  for (int s = 0; s < nst; ++s) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // stage s landed (every wave's DMAs); every wave is done reading stage s - 1
-    if (s + 1 < nst) issue((s + 1) * BKS, (s + 1) & 1);
-    const signed char* SA = lds + (s & 1) * STAGE;
+  const int nst = kbn / BKS;  // kbn is a multiple of BKS (the slicer zero-fills to a stage boundary)
+  // Software pipeline over stages, two levels deep:
+  //  * LDS-DMA: a ring of NSTG stage buffers, NSTG - 1 stages in flight (stage s + NSTG - 1 is issued at
+  //    the top of stage s into stage s - 1's buffer); at the top of stage s this wave's DMAs of later
+  //    stages may still fly (counted vmcnt), and a raw s_barrier -- not __syncthreads(), whose fence would
+  //    drain them (cdna_hip_programming.md §5, "Pipelining across barriers") -- makes every wave's stage s
+  //    visible and every wave's fragment reads of stage s - 1 complete;
+  //  * fragments: stage s's 6 BKS ds_read_b128 go into one register set while the 8 BKS MFMAs of stage
+  //    s - 1 run from the other, so the LDS reads (and the barrier) hide behind the matrix pipe instead
+  //    of idling it at the top of every stage.
+  v4i fa0[BKS][4], fb0[BKS][2], fa1[BKS][4], fb1[BKS][2];
+  auto load = [&](int s, v4i (&fa)[BKS][4], v4i (&fb)[BKS][2]) {
+    const signed char* SA = lds + (s % NSTG) * STAGE;
     const signed char* SB = SA + PANEL;
-    v4i fa[BKS][4], fb[BKS][2];
 #pragma unroll
     for (int k = 0; k < BKS; ++k) {
 #pragma unroll
       for (int a = 0; a < 4; ++a)
-        fa[k][a] = *reinterpret_cast<const v4i*>(SA + k * (TT * 32) + (wr * 128 + 32 * a + r) * 32 + 16 * h);
+        fa[k][a] = *reinterpret_cast<const v4i*>(SA + k * (TT * 32) + h * (TT * 16) + (wr * 128 + 32 * a + r) * 16);
 #pragma unroll
       for (int b = 0; b < 2; ++b)
-        fb[k][b] = *reinterpret_cast<const v4i*>(SB + k * (TT * 32) + (wc * 64 + 32 * b + r) * 32 + 16 * h);
+        fb[k][b] = *reinterpret_cast<const v4i*>(SB + k * (TT * 32) + h * (TT * 16) + (wc * 64 + 32 * b + r) * 16);
     }
+  };
+  auto mma = [&](v4i (&fa)[BKS][4], v4i (&fb)[BKS][2]) {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int k = 0; k < BKS; ++k)
@@ -218,8 +283,50 @@ __global__ void __launch_bounds__(GNT, 1) crt_gemm(const signed char* R, int Dp,
         for (int b = 0; b < 2; ++b)
           acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa[k][a], fb[k][b], acc[a][b], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
+  };
+  auto top = [&](int s) {  // stage s landed everywhere; stage s - 1's buffer is free for stage s + NSTG - 1
+    const int rem = nst - 1 - s;
+    if constexpr (NSTG >= 4) {
+      if (rem >= 2) wait_vm<2 * P>();
+      else if (rem == 1) wait_vm<P>();
+      else wait_vm<0>();
+    } else if constexpr (NSTG == 3) {
+      if (rem >= 1) wait_vm<P>();
+      else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    wait_lgkm0();
+    __builtin_amdgcn_s_barrier();
+    if (s + NSTG - 1 < nst) issue((s + NSTG - 1) * BKS, (s + NSTG - 1) % NSTG);
+  };
+  for (int s0 = 0; s0 < NSTG - 1 && s0 < nst; ++s0) issue(s0 * BKS, s0);
+  if (nst > 0) {
+    top(0);
+    load(0, fa0, fb0);
   }
-  // epilogue: C_p = (C_p + chunk sum) mod p, symmetric, as int16
+  int s = 1;
+  for (; s + 1 < nst; s += 2) {
+    top(s);
+    load(s, fa1, fb1);
+    mma(fa0, fb0);  // stage s - 1
+    top(s + 1);
+    load(s + 1, fa0, fb0);
+    mma(fa1, fb1);  // stage s
+  }
+  if (s < nst) {  // nst even: stage nst - 1 still to load
+    top(s);
+    load(s, fa1, fb1);
+    mma(fa0, fb0);
+    wait_lgkm0();
+    mma(fa1, fb1);
+  } else if (nst > 0) {  // nst odd: stage nst - 1 is in fa0 / fb0
+    wait_lgkm0();
+    mma(fa0, fb0);
+  }
+  // epilogue: C_p = (C_p + chunk sum) mod p, symmetric, as int16. The previous chunks' residues are read
+  // 16 at a time (one 32 x 32 block) before any is used: a per-element load behind the `first` test would
+  // make hipcc branch around each load and wait for it alone (cdna_hip_programming.md §5, trap (c))
   short* Cp = C + (long)p * Dp * Dp;
   const int hm = mp >> 1;
 #pragma unroll
@@ -227,16 +334,22 @@ __global__ void __launch_bounds__(GNT, 1) crt_gemm(const signed char* R, int Dp,
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
       const int col = tj * TT + wc * 64 + 32 * b + r;
+      const long base = (long)(ti * TT + wr * 128 + 32 * a + 4 * h) * Dp + col;  // row offset (g&3) + 8 (g>>2)
+      int old[16];
+      if (first) {
+#pragma unroll
+        for (int g = 0; g < 16; ++g) old[g] = 0;
+      } else {
+#pragma unroll
+        for (int g = 0; g < 16; ++g) old[g] = Cp[base + (long)((g & 3) + 8 * (g >> 2)) * Dp];
+      }
 #pragma unroll
       for (int g = 0; g < 16; ++g) {
-        const int row = ti * TT + wr * 128 + 32 * a + (g & 3) + 8 * (g >> 2) + 4 * h;
-        const long idx = (long)row * Dp + col;
-        int v = acc[a][b][g] % mp;
-        if (!first) v += Cp[idx];
+        int v = acc[a][b][g] % mp + old[g];
         v %= mp;
         if (v > hm) v -= mp;
         if (v < -hm) v += mp;
-        Cp[idx] = (short)v;
+        Cp[base + (long)((g & 3) + 8 * (g >> 2)) * Dp] = (short)v;
       }
     }
 }
@@ -344,7 +457,7 @@ static long crt_dp(int d) { return ((long)d + 1 + TT - 1) / TT * TT; }
 long gadmm_gram_crt_workspace(long m, int d) {
   (void)m;
   const long Dp = crt_dp(d);
-  return (long)NMOD * Dp * Dp * 2 + 2L * NMOD * KC * Dp + (long)CE_R * Dp * 8 + Dp * 4 + Dp * 8 + 1024;
+  return (long)NMOD * Dp * Dp * 2 + 2L * NMOD * KBCP * 32 * Dp + (long)CE_R * Dp * 8 + Dp * 4 + Dp * 8 + 1024;
 }
 
 long gadmm_gram_crt_max_rows() { return MAX_ROWS; }
@@ -367,9 +480,10 @@ int gadmm_gram_crt_f64(const double* X, const double* Y, int N, long m, int d, d
   }
   char* w = (char*)ws;
   short* C = (short*)w;
+  const long rbytes = (long)NMOD * KBCP * 32 * Dp;
   signed char* Rbuf[2] = {(signed char*)(w + (long)NMOD * Dp * Dp * 2),
-                          (signed char*)(w + (long)NMOD * Dp * Dp * 2 + (long)NMOD * KC * Dp)};
-  double* part = (double*)(w + (long)NMOD * Dp * Dp * 2 + 2L * NMOD * KC * Dp);
+                          (signed char*)(w + (long)NMOD * Dp * Dp * 2 + rbytes)};
+  double* part = (double*)(w + (long)NMOD * Dp * Dp * 2 + 2L * rbytes);
   int* e = (int*)((char*)part + (long)CE_R * Dp * 8);
   double* cm = (double*)((char*)e + ((long)Dp * 4 + 255) / 256 * 256);
   const int nt = (int)(Dp / TT);
@@ -379,7 +493,18 @@ int gadmm_gram_crt_f64(const double* X, const double* Y, int N, long m, int d, d
     gadmm_set_error("gram_crt: job list allocation failed");
     return -1;
   }
-  const size_t shm = (size_t)2 * STAGE;  // 64 KB
+  // pipeline configuration (GADMM_CRT_STAGES=BKSxNSTG, read per call: A/B of the stage depth / count)
+  int bks = 2, nstg = 4;
+  if (const char* cfg = getenv("GADMM_CRT_STAGES")) {
+    if (!strcmp(cfg, "4x2")) bks = 4, nstg = 2;
+    else if (!strcmp(cfg, "3x3")) bks = 3, nstg = 3;
+    else if (!strcmp(cfg, "2x3")) bks = 2, nstg = 3;
+    else if (!strcmp(cfg, "1x4")) bks = 1, nstg = 4;
+  }
+  const void* kfn = bks == 4 ? (const void*)crt_gemm<4, 2> : bks == 3 ? (const void*)crt_gemm<3, 3>
+                    : bks == 1 ? (const void*)crt_gemm<1, 4> : nstg == 3 ? (const void*)crt_gemm<2, 3>
+                                                                         : (const void*)crt_gemm<2, 4>;
+  const size_t shm = (size_t)nstg * 2 * bks * TT * 32;  // 96-144 KB
   static std::mutex mu;                  // the side stream and events: one caller at a time
   std::lock_guard<std::mutex> lock(mu);
   int dev = 0;
@@ -396,12 +521,15 @@ int gadmm_gram_crt_f64(const double* X, const double* Y, int N, long m, int d, d
     for (int k = 0; k < 6; ++k) GADMM_CHECK(hipEventCreateWithFlags(&ev[dev][k], hipEventDisableTiming));
   }
   if (!attr[dev]) {
-    GADMM_CHECK(hipFuncSetAttribute((const void*)crt_gemm, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
+    for (const void* f : {(const void*)crt_gemm<4, 2>, (const void*)crt_gemm<3, 3>, (const void*)crt_gemm<2, 3>,
+                          (const void*)crt_gemm<2, 4>, (const void*)crt_gemm<1, 4>})
+      GADMM_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr[dev] = true;
   }
-  hipStream_t s2 = side[dev];
+  hipStream_t s2 = getenv("GADMM_CRT_SERIAL") ? st : side[dev];
   hipEvent_t ev_fork = ev[dev][0], ev_join = ev[dev][1], *ev_s = &ev[dev][2], *ev_g = &ev[dev][4];
   const int nc = (int)((m + KC - 1) / KC);
+  int Dp32 = (int)Dp;
   for (int n = 0; n < N; ++n) {
     const double* Xn = X + (long)n * m * d;
     const double* Yn = Y + (long)n * m;
@@ -416,10 +544,13 @@ int gadmm_gram_crt_f64(const double* X, const double* Y, int N, long m, int d, d
         if (rc != hipSuccess) break;
         long rows = std::min<long>(KC, m - (long)c * KC);
         int kbn = (int)((rows + 31) / 32);
-        kbn += kbn & 1;  // whole stages (the slicer zero-fills the extra block)
-        hipLaunchKernelGGL(crt_gemm, dim3((unsigned)(8 * ((total + 7) / 8))), dim3(GNT), shm, st, Rbuf[c & 1],
-                           (int)Dp, total, list, kbn, C, c == 0 ? 1 : 0);
-        rc = hipGetLastError();
+        kbn = (kbn + bks - 1) / bks * bks;  // whole stages (the slicer zero-fills the extra blocks)
+        const signed char* Rc = Rbuf[c & 1];
+        int total_ = total, first_ = c == 0 ? 1 : 0;
+        void* kargs[] = {(void*)&Rc, (void*)&Dp32, (void*)&total_, (void*)&list, (void*)&kbn, (void*)&C,
+                         (void*)&first_};
+        rc = hipLaunchKernel(kfn, dim3((unsigned)(8 * ((total + 7) / 8))), dim3(GNT), kargs, shm, st);
+        if (rc == hipSuccess) rc = hipGetLastError();
         if (rc == hipSuccess) rc = hipEventRecord(ev_g[c & 1], st);
         if (rc != hipSuccess) break;
       }
@@ -429,9 +560,9 @@ int gadmm_gram_crt_f64(const double* X, const double* Y, int N, long m, int d, d
         if (rc != hipSuccess) break;
         long rows = std::min<long>(KC, m - (long)(c + 1) * KC);
         int kbn = (int)((rows + 31) / 32);
-        kbn += kbn & 1;
+        kbn = (kbn + bks - 1) / bks * bks;
         hipLaunchKernelGGL(crt_slice, dim3((unsigned)((Dp + SLT - 1) / SLT), (unsigned)kbn), dim3(SLT), 0, s2, Xn, Yn,
-                           (long)(c + 1) * KC, m, d, (int)Dp, e, Rbuf[bsel]);
+                           (long)(c + 1) * KC, std::min<long>(m, (long)(c + 2) * KC), d, (int)Dp, e, Rbuf[bsel]);
         rc = hipGetLastError();
         if (rc == hipSuccess) rc = hipEventRecord(ev_s[bsel], s2);
       }

@@ -29,7 +29,7 @@ def gram_torch(X: torch.Tensor, y: torch.Tensor) -> Tuple[torch.Tensor, torch.Te
     return A, b, yy
 
 
-# The Ozaki digits keep 49 bits of every value relative to its column's scale (>= the column maximum), so
+# The int8 schemes (Ozaki digits, CRT) keep 49 bits of every value relative to its column's scale (>= the column maximum), so
 # an entry at the column's rms level keeps ~49 - log2(colmax / rms) bits; past 2^4 (45 bits, against the
 # 53 of an f64 operand) ``gram`` recomputes the shard on the f64-MFMA kernel. Gaussian columns of a
 # million rows sit near 5; one outlier row, or a heavy-tailed (e.g. lognormal) column, exceeds it.
@@ -96,10 +96,11 @@ def gram_crt(X: torch.Tensor, y: torch.Tensor, out=None, with_range: bool = Fals
 
 
 def gram_uses_ozaki(m: int, d: int) -> bool:
-    """Whether ``gram`` tries the int8 Ozaki path. ``GADMM_GRAM_OZAKI``: ``auto`` (default) for shards of
-    d >= 3072 features and m >= 65536 samples, where it measured faster than the f64-MFMA Gram (1.11x at
-    100k x 4096, 1.10x at 312k x 10k; real10m 2.11 -> 1.92 s at the same 25 iterations: profiles/r05_h);
-    ``1`` for every d > 256; ``0`` never. The range gate (``OZ_MAX_RANGE``) still applies."""
+    """Whether ``gram`` takes an int8 matrix-core path. ``GADMM_GRAM_OZAKI``: ``auto`` (default) for shards
+    of d >= 3072 features and m >= 65536 samples, where the digit scheme already measured faster than the
+    f64-MFMA Gram (1.11x at 100k x 4096, 1.10x at 312k x 10k: profiles/r05_h) and the CRT scheme is faster
+    still (profiles/r06_crt); ``1`` for every d > 256; ``0`` never. The range gate (``OZ_MAX_RANGE``)
+    applies to both schemes."""
     mode = getenv("GADMM_GRAM_OZAKI", "auto")
     if mode == "0":
         return False
@@ -108,22 +109,47 @@ def gram_uses_ozaki(m: int, d: int) -> bool:
     return d >= 3072 and m >= 65536
 
 
+def gram_int8_scheme(m: int) -> str:
+    """``crt`` (csrc/kernels/gram_crt.hip, default) or ``digits`` (gram_ozaki.hip). ``GADMM_GRAM_INT8``
+    forces one; the CRT reconstruction bound caps it at 2^21 rows per shard, past which the digits run."""
+    mode = getenv("GADMM_GRAM_INT8", "crt")
+    if mode == "digits":
+        return "digits"
+    return "crt" if m <= _crt_max_rows() else "digits"
+
+
+def _crt_max_rows() -> int:
+    return int(native.require().gadmm_gram_crt_max_rows())
+
+
 def gram(X: torch.Tensor, y: torch.Tensor, ksplit: Optional[int] = None, out=None
          ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Batched augmented Gram. ``X``: (N, m, d) f64 contiguous, ``y``: (N, m).
-    ``out``: optional preallocated ``(A, b, yy)`` written in place. Shards the Ozaki path would serve with
-    fewer kept bits than ``OZ_MAX_RANGE`` allows (an outlier row, a heavy-tailed column) are recomputed on
-    the f64-MFMA kernel (one host read of the N range statistics: set-up code, never graph-captured)."""
+    ``out``: optional preallocated ``(A, b, yy)`` written in place. Large shards go to the int8 matrix
+    cores (``gram_crt``, or ``gram_ozaki`` past its row bound or when the CRT workspace -- ~17 GB at
+    d = 10k -- cannot be allocated). Shards that path would serve with fewer kept bits than
+    ``OZ_MAX_RANGE`` allows (an outlier row, a heavy-tailed column) are recomputed on the f64-MFMA kernel
+    (one host read of the N range statistics: set-up code, never graph-captured)."""
     if X.dtype != torch.float64 or y.dtype != torch.float64:
         raise TypeError("gram expects float64")
     if X.is_cuda and ksplit is None and gram_uses_ozaki(int(X.shape[1]), int(X.shape[2])):
-        A, b, yy, rng = gram_ozaki(X, y, out=out, with_range=True)
+        scheme = gram_int8_scheme(int(X.shape[1]))
+        res = None
+        if scheme == "crt":
+            try:
+                res = gram_crt(X, y, out=out, with_range=True)
+            except torch.cuda.OutOfMemoryError:
+                scheme = "digits"
+        if res is None:
+            res = gram_ozaki(X, y, out=out, with_range=True)
+        A, b, yy, rng = res
         r = float(rng.max().item())
         limit = float(getenv("GADMM_OZ_MAX_RANGE", str(OZ_MAX_RANGE)))
+        name = "crt-int8" if scheme == "crt" else "ozaki-int8"
         if r <= limit:
-            LAST_GRAM.update(path="ozaki-int8", range=r)
+            LAST_GRAM.update(path=name, range=r)
             return A, b, yy
-        LAST_GRAM.update(path="f64-mfma (ozaki range gate: %.3g > %g)" % (r, limit), range=r)
+        LAST_GRAM.update(path="f64-mfma (%s range gate: %.3g > %g)" % (name, r, limit), range=r)
         return _gram_f64(X, y, None, (A, b, yy))
     if not X.is_cuda:
         res = gram_torch(X, y)

@@ -1209,8 +1209,9 @@ def _ref_gram(X, y, chunk: int = 1024):
     return S[:, :d, :d].contiguous(), S[:, :d, d].contiguous()
 
 
+@pytest.mark.parametrize("scheme", ["crt", "digits"])
 @pytest.mark.parametrize("case", ["outlier_row", "lognormal"])
-def test_gram_ozaki_range_gate_hard_columns(case):
+def test_gram_ozaki_range_gate_hard_columns(case, scheme, monkeypatch):
     """Within-column dynamic range: a column whose maximum is one row 1e6 times the
     rest (that row zero elsewhere, so the entries A_0b are NOT dominated by it), or lognormal columns. The
     digits keep 49 bits relative to the column maximum, so the raw Ozaki Gram loses ~20 bits on A_0b; the
@@ -1227,15 +1228,14 @@ def test_gram_ozaki_range_gate_hard_columns(case):
         X = torch.exp(1.5 * X)  # heavy-tailed positive columns
     y = torch.randn((N, m), dtype=torch.float64, device=DEV, generator=g)
     Ar, br = _ref_gram(X, y)
-    Araw, _, _, rng = linalg.gram_ozaki(X, y, with_range=True)
+    raw = linalg.gram_crt if scheme == "crt" else linalg.gram_ozaki
+    Araw, _, _, rng = raw(X, y, with_range=True)
     assert float(rng.max()) > linalg.OZ_MAX_RANGE, float(rng.max())
-    os.environ["GADMM_GRAM_OZAKI"] = "1"  # d > 256: the auto rule would not try Ozaki at m = 20000
-    try:
-        A, b, yy = linalg.gram(X, y)
-        path = linalg.LAST_GRAM["path"]
-    finally:
-        del os.environ["GADMM_GRAM_OZAKI"]
-    assert path.startswith("f64-mfma (ozaki range gate"), path
+    monkeypatch.setenv("GADMM_GRAM_OZAKI", "1")  # d > 256: the auto rule would not try int8 at m = 20000
+    monkeypatch.setenv("GADMM_GRAM_INT8", scheme)
+    A, b, yy = linalg.gram(X, y)
+    path = linalg.LAST_GRAM["path"]
+    assert path.startswith("f64-mfma (%s-int8 range gate" % ("crt" if scheme == "crt" else "ozaki")), path
     A64 = linalg._gram_f64(X, y, None, None)[0]
     assert torch.equal(A, A64)  # the gate's fallback IS the f64 kernel
     rows = [0] if case == "outlier_row" else None
@@ -1246,7 +1246,8 @@ def test_gram_ozaki_range_gate_hard_columns(case):
         assert e_raw > 10 * e_gate  # the loss the gate exists for
 
 
-def test_gram_ozaki_auto_shape_matches_f64():
+@pytest.mark.parametrize("scheme", ["crt", "digits"])
+def test_gram_ozaki_auto_shape_matches_f64(scheme, monkeypatch):
     """the auto-selected shape (d >= 3072, m >= 65536: several 8192-sample chunks) through
     ``gram`` itself, Gaussian columns plus one Laplace (heavier-tailed) column: the range gate keeps the
     Ozaki path, every entry within 1e-14 of sqrt(A_aa A_bb) of the CPU f64 reference."""
@@ -1258,21 +1259,22 @@ def test_gram_ozaki_auto_shape_matches_f64():
     u = torch.rand((N, m), dtype=torch.float64, device=DEV, generator=g) - 0.5
     X[:, :, 5] = -torch.sign(u) * torch.log1p(-2 * u.abs())  # Laplace column
     y = torch.randn((N, m), dtype=torch.float64, device=DEV, generator=g)
+    monkeypatch.setenv("GADMM_GRAM_INT8", scheme)
     A, b, yy = linalg.gram(X, y)
-    assert linalg.LAST_GRAM["path"] == "ozaki-int8", linalg.LAST_GRAM
+    assert linalg.LAST_GRAM["path"] == ("crt-int8" if scheme == "crt" else "ozaki-int8"), linalg.LAST_GRAM
     Ar, br = _ref_gram(X, y)
     sc = torch.sqrt(torch.diagonal(Ar, dim1=1, dim2=2))
     ea = float(((A.cpu() - Ar).abs() / (sc.unsqueeze(2) * sc.unsqueeze(1))).max())
     eb = float(((b.cpu() - br).abs() / (sc * yy.cpu().sqrt().unsqueeze(1))).max())
     A64, b64, _ = linalg._gram_f64(X, y, None, None)
     e64 = float(((A64.cpu() - Ar).abs() / (sc.unsqueeze(2) * sc.unsqueeze(1))).max())
-    print("auto shape: ozaki %.3g, f64-mfma %.3g (of sqrt(A_aa A_bb))" % (ea, e64))
+    print("auto shape: %s %.3g, f64-mfma %.3g (of sqrt(A_aa A_bb))" % (scheme, ea, e64))
     assert ea < 1e-14 and eb < 1e-14, (ea, eb, e64)
 
 
 def test_gram_ozaki_gadmm_iterations_match_f64(monkeypatch):
     """End to end: GADMM on a real-shaped problem (2 workers x 20000 x 300, one Laplace column) to a 1e-8
-    relative gap takes the same number of iterations with the Ozaki Gram (forced) as with the f64 one."""
+    relative gap takes the same number of iterations with either int8 Gram (forced) as with the f64 one."""
     from gadmm_amd.models import LinearRegression
     from gadmm_amd.algorithms import chain_admm
     g = torch.Generator(device=DEV)
@@ -1283,14 +1285,15 @@ def test_gram_ozaki_gadmm_iterations_match_f64(monkeypatch):
     th = torch.randn((300,), dtype=torch.float64, device=DEV, generator=g)
     y = X @ th + 0.1 * torch.randn((2, 20000), dtype=torch.float64, device=DEV, generator=g)
     its = {}
-    for mode in ("1", "0"):
+    for mode, scheme in (("1", "crt"), ("1", "digits"), ("0", "crt")):
         monkeypatch.setenv("GADMM_GRAM_OZAKI", mode)
+        monkeypatch.setenv("GADMM_GRAM_INT8", scheme)
         m = LinearRegression(X, y)
         obj0 = m.optimum()
         r = chain_admm(m, [0, 1], 2, 10000.0, obj0, 1e-8 * abs(obj0), 2000, engine_opts={"cache": False})
         assert r.converged
-        its[mode] = r.iters
-    assert its["1"] == its["0"], its
+        its[(mode, scheme)] = r.iters
+    assert len(set(its.values())) == 1, its
 
 
 @pytest.mark.parametrize("kind", ["linear", "logistic", "newton"])

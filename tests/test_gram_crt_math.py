@@ -1,7 +1,8 @@
 """CPU emulation of the CRT int8 Gram (csrc/kernels/gram_crt.hip): the moduli are pairwise coprime with a
 product past 2 * 2^21 * 2^98 (exact reconstruction of any 2^21-row Gram of 49-bit integer images), the
 Garner table compiled into the kernel is the modular-inverse table, and the kernel's arithmetic -- the
-symmetric residues of the slicer (floor of n / p by a double product, one correction), the per-chunk
+slicer's int8 residues (13-bit digits, exact f32 sums, an f32 quotient estimate, the residue read
+from the low byte of a float's bit pattern; |r| <= 68), the per-chunk
 reduction mod p, balanced Garner digits and the Horner evaluation in doubles -- reproduces the exact
 integer Gram (Python integers) of random data including negative and boundary values."""
 import math
@@ -35,18 +36,37 @@ def test_moduli_and_inverse_table():
     assert max_rows * (2 ** kb) ** 2 < M // 2  # |G| < M / 2: the balanced reconstruction is exact
 
 
+def _f32(x) -> np.float32:
+    """Round an exact rational to the nearest f32 (an fma's single rounding)."""
+    return np.float32(float(x))
+
+
+MAGIC = 12582912  # 1.5 2^23
+
+
 def _residue(nv: float, p: int) -> int:
-    """crt_slice: floor(n / p) via a double product, an exact fma remainder, one correction, symmetric."""
-    mp, ip = float(p), 1.0 / p
-    qq = math.floor(nv * ip)
-    r = nv - qq * mp  # exact in the kernel (fma); exact here too: |qq mp| < 2^51 integers
-    if r < 0:
-        r += mp
-    if r >= mp:
-        r -= mp
-    if r > 0.5 * (mp - 1):
-        r -= mp
-    return int(r)
+    """crt_slice: N = d3 2^39 + d2 2^26 + d1 2^13 + d0 (13-bit digits, d3 signed), S' = MAGIC + d0 +
+    d1 (2^13 mod p) + d2 (2^26 mod p) + d3 (2^39 mod p) in f32 (exact integers < 2^24), q = rint(fma(S',
+    f32(1/p), f32(-MAGIC/p))), t = fma(-q, p, S') = MAGIC + r; r = the low byte of t's bits as int8."""
+    from fractions import Fraction
+    n = int(nv)
+    d3 = math.floor(nv * 2.0 ** -39)
+    r3 = n - d3 * 2 ** 39
+    d2 = r3 >> 26
+    r2 = r3 - (d2 << 26)
+    d1, d0 = r2 >> 13, r2 & 8191
+    assert -1024 <= d3 < 1024 and 0 <= d2 < 8192 and 0 <= d1 < 8192
+    S = MAGIC + d0 + d1 * pow(2, 13, p) + d2 * pow(2, 26, p) + d3 * pow(2, 39, p)
+    assert 2 ** 23 <= S < 2 ** 24  # exact in f32, exponent fixed
+    ip, nm = np.float32(1.0) / np.float32(p), _f32(Fraction(-MAGIC, p))
+    q = int(np.rint(_f32(Fraction(S) * Fraction(float(ip)) + Fraction(float(nm)))))
+    t = S - q * p  # the fma is exact: an integer in [2^23, 2^24)
+    assert 2 ** 23 <= t < 2 ** 24
+    bits = int(np.array([t], dtype=np.float32).view(np.uint32)[0])
+    r = bits & 0xFF
+    r = r - 256 if r >= 128 else r
+    assert r == t - MAGIC and (r - n) % p == 0 and abs(r) <= 68, (nv, p, r)
+    return r
 
 
 def _garner(res, mods, inv) -> float:
@@ -99,3 +119,15 @@ def test_emulated_gram_is_exact():
                 P *= p
             assert tot == exact, (a, b)
             assert abs(val - exact) <= 4e-16 * abs(exact) + 1.0, (a, b, val, exact)
+
+
+def test_slicer_residue_bound_dense():
+    """|r| <= 68 and r == N mod p over random and boundary 49-bit integers, every modulus."""
+    mods, _, kb, _ = _tables()
+    rng = np.random.default_rng(1)
+    vals = list(rng.integers(-(2 ** kb) + 1, 2 ** kb, size=4000, dtype=np.int64))
+    vals += [0, 1, -1, 2 ** kb - 1, -(2 ** kb) + 1, 2 ** 24, -(2 ** 24), 2 ** 34 - 1, -(2 ** 34) + 1]
+    vals += list(rng.integers(-2 ** 20, 2 ** 20, size=2000, dtype=np.int64))
+    for p in mods:
+        for v in vals:
+            _residue(float(v), p)
