@@ -323,6 +323,11 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     # D-GADMM on a cached engine: the first launch's chains start drawing now (geometries from the
     # schedule's RNG here, greedy walks on the native host worker) and are joined where the launch's
     # tables are built, so the walks overlap the refresh / set_path / reset below
+    if eng is not None and refresh:
+        # in place on the engine's stream (Gram, then inverses), launched first: the device works through
+        # them while the host draws chains and builds the launch below (profiles/r06_dgadmm)
+        eng.refresh(model.X, model.y)
+        _timing.host_stamp("native:refresh")
     early = None
     if eng is not None and state is None and not _static_schedule(schedule, max_iter) \
             and opts.get("persistent", "auto") in (True, "auto") and "epoch_chunk" not in opts \
@@ -330,8 +335,6 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         early = _dyn_early_draw(eng, schedule, max_iter, fabric, n_total)
         _timing.host_stamp("native:early_draw")
     try:
-        if eng is not None and refresh:
-            eng.refresh(model.X, model.y)  # in place on the engine's stream (Gram, then inverses)
         if eng is None:
             eng = NativeChainEngine(model.X, model.y, local_ids, n_total, kind, rho=rho, obj0=obj0, tol=tol,
                                     max_iter=max_iter, lam=getattr(model, "lam", 0.0), step=step, max_inner=max_inner,

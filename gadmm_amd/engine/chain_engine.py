@@ -82,18 +82,18 @@ def quad_pad_image(M: torch.Tensor, db: int, out: Optional[torch.Tensor] = None)
     qt = db // 4
     key = (d, db, M.device)
     idx = _QUAD_IDX.get(key)
-    if idx is None:
+    if idx is None:  # vectorised (a Python triple loop here cost ~45 ms on a process's first D-GADMM solve)
         n_el = 512 * ((qt + 1) // 2)
         src = np.full((n_el,), -1, dtype=np.int64)
-        for t in range(qt):
-            for r in range(4):
-                for lane in range(64):
-                    row, col = (lane & 15) + 16 * r, (lane >> 4) + 4 * t
-                    if row < d and col < d:
-                        src[((t >> 1) * 4 + r) * 128 + 2 * lane + (t & 1)] = row * d + col
+        t, r, lane = np.meshgrid(np.arange(qt), np.arange(4), np.arange(64), indexing="ij")
+        row, col = (lane & 15) + 16 * r, (lane >> 4) + 4 * t
+        ok = (row < d) & (col < d)
+        src[(((t >> 1) * 4 + r) * 128 + 2 * lane + (t & 1))[ok]] = (row * d + col)[ok]
         idx = (torch.from_numpy(np.maximum(src, 0)).to(M.device), torch.from_numpy(src >= 0).to(M.device))
         _QUAD_IDX[key] = idx
     gi, mask = idx
+    if out is None and M.is_cuda and M.dtype == torch.float64:  # the native gather (torch.where's first
+        out = torch.empty((B, int(gi.numel())), dtype=torch.float64, device=M.device)  # launch: ~90 ms)
     lib = native.require() if (out is not None and M.is_cuda) else None
     if lib is not None and hasattr(lib, "gadmm_pad_image_f64") and M.dtype == torch.float64 and M.is_contiguous():
         src = _QUAD_SRC.get(key)

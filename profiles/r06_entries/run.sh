@@ -8,7 +8,7 @@ O=gpurun_out/${1:-r6entries}; mkdir -p $O
 E="python -u -m gadmm_amd"
 TR="python -u -m torch.distributed.run --nnodes=1 --master-addr 127.0.0.1"
 Q="--quick --set gadmm_iters=1000 --no-plot"
-H="--no-baselines --no-plot --tol 1e-8 --set gadmm_iters=2000 rhos=3"
+H="--no-baselines --no-plot --tol 1e-8 --set gadmm_iters=2000 rhos=3,3"  # the second solve is warm
 timeout -k 10 300 $E LinearRegression_Synthetic $Q --out $O/e1_1gpu > $O/e1_1gpu.log 2>&1 || exit $?
 timeout -k 10 300 $E LinearRegression_Synthetic $H --out $O/e1h_1gpu > $O/e1h_1gpu.log 2>&1 || exit $?
 for n in 2 4; do
@@ -28,6 +28,7 @@ GADMM_SHARE_GPU=1 timeout -k 10 300 $TR --nproc-per-node 2 --master-port 29652 -
   Dynamic_LinearRegression_Synthetic --quick --no-plot --out $O/e5_share2 > $O/e5_share2.log 2>&1 || exit $?
 GADMM_SHARE_GPU=1 timeout -k 10 300 $TR --nproc-per-node 2 --master-port 29662 -m gadmm_amd \
   LinearRegression_Real --quick --no-plot --out $O/e2_share2 > $O/e2_share2.log 2>&1 || exit $?
+timeout -k 10 300 $E LogisticRegression_Real --quick --no-plot --out $O/e4_1gpu > $O/e4_1gpu.log 2>&1 || exit $?
 GADMM_SHARE_GPU=1 timeout -k 10 300 $TR --nproc-per-node 2 --master-port 29672 -m gadmm_amd \
   LogisticRegression_Real --quick --no-plot --out $O/e4_share2 > $O/e4_share2.log 2>&1 || exit $?
 GADMM_SHARE_GPU=1 timeout -k 10 300 $TR --nproc-per-node 2 --master-port 29682 -m gadmm_amd \

@@ -551,11 +551,12 @@ def test_quad_pad_image_native_matches_torch(d, db):
     == the torch-built image, bit for bit."""
     from gadmm_amd.engine.chain_engine import quad_pad_image
     M = torch.randn(6, d, d, dtype=torch.float64, device=DEV)
-    ref = quad_pad_image(M, db)
+    ref = quad_pad_image(M.cpu(), db).to(DEV)  # the torch gather (CUDA inputs always take the native one)
     out = torch.full_like(ref, float("nan"))
     got = quad_pad_image(M, db, out=out)
+    auto = quad_pad_image(M, db)  # no ``out``: allocated, same native gather
     torch.cuda.synchronize()
-    assert got.data_ptr() == out.data_ptr() and torch.equal(got, ref)
+    assert got.data_ptr() == out.data_ptr() and torch.equal(got, ref) and torch.equal(auto, ref)
 
 
 @pytest.mark.parametrize("d", [300, 301])
