@@ -97,15 +97,19 @@ def gram_crt(X: torch.Tensor, y: torch.Tensor, out=None, with_range: bool = Fals
 
 def gram_uses_ozaki(m: int, d: int) -> bool:
     """Whether ``gram`` takes an int8 matrix-core path. ``GADMM_GRAM_OZAKI``: ``auto`` (default) for shards
-    of d >= 3072 features and m >= 65536 samples, where the digit scheme already measured faster than the
-    f64-MFMA Gram (1.11x at 100k x 4096, 1.10x at 312k x 10k: profiles/r05_h) and the CRT scheme is faster
-    still (profiles/r06_crt); ``1`` for every d > 256; ``0`` never. The range gate (``OZ_MAX_RANGE``)
-    applies to both schemes."""
+    where the selected scheme measured faster than the f64-MFMA Gram -- the CRT scheme from d >= 1024 and
+    m d >= 2^26 (profiles/r06_crt, profiles/r06_dgadmm/crt_small.log), the digit scheme from d >= 3072 and
+    m >= 65536 (1.11x at 100k x 4096, 1.10x at 312k x 10k: profiles/r05_h); ``1`` for every d > 256; ``0``
+    never. The range gate (``OZ_MAX_RANGE``) applies to both schemes."""
     mode = getenv("GADMM_GRAM_OZAKI", "auto")
     if mode == "0":
         return False
     if mode == "1":
         return d > 256
+    if gram_int8_scheme(m) == "crt":
+        # measured crossover of the CRT kernel against the f64-MFMA Gram (profiles/r06_dgadmm/crt_small.log):
+        # faster at 65k x 1024 (2.3 vs 2.5 ms), 33k x 2048, 20k x 4096; slower at 262k x 512 (4.6 vs 3.1)
+        return d >= 1024 and m * d >= (1 << 26)
     return d >= 3072 and m >= 65536
 
 

@@ -363,6 +363,9 @@ class PathSchedule:
 # Placement and per-rank phase plans
 # -------------------------------------------------------------------------------------------------
 
+_CONTIGUOUS: Dict[Tuple[int, int], "Placement"] = {}
+
+
 @dataclass
 class Placement:
     """Logical worker -> rank map. Default: contiguous blocks of workers per rank (so a static
@@ -373,13 +376,21 @@ class Placement:
 
     @staticmethod
     def contiguous(n_workers: int, nranks: int) -> "Placement":
-        if nranks > n_workers:
-            raise ValueError("more ranks (%d) than workers (%d)" % (nranks, n_workers))
-        base, extra = divmod(n_workers, nranks)
-        owner = []
-        for r in range(nranks):
-            owner += [r] * (base + (1 if r < extra else 0))
-        return Placement(owner=np.asarray(owner, dtype=np.int64), nranks=nranks)
+        """Memoised per (n_workers, nranks): the same object on every call (placements are never
+        mutated), so per-solve callers skip the construction and identity-keyed memos hit."""
+        key = (int(n_workers), int(nranks))
+        pl = _CONTIGUOUS.get(key)
+        if pl is None:
+            if nranks > n_workers:
+                raise ValueError("more ranks (%d) than workers (%d)" % (nranks, n_workers))
+            base, extra = divmod(n_workers, nranks)
+            owner = []
+            for r in range(nranks):
+                owner += [r] * (base + (1 if r < extra else 0))
+            pl = Placement(owner=np.asarray(owner, dtype=np.int64), nranks=nranks)
+            pl.owner.setflags(write=False)
+            _CONTIGUOUS[key] = pl
+        return pl
 
     def local_workers(self, rank: int) -> List[int]:
         return [int(w) for w in np.nonzero(self.owner == rank)[0]]

@@ -13,6 +13,7 @@
 from __future__ import annotations
 
 import ctypes
+import os
 import time
 from typing import Optional
 
@@ -103,9 +104,22 @@ def reference_local_solve_s(model, rho: float, reps: int = 20) -> float:
 _roctx = None
 
 
+def _profiled() -> bool:
+    """roctx ranges only under a profiler (rocprofv3 preloads its tool library and exports ROCPROF_*
+    settings) or with GADMM_ROCTX=1: outside one a range push / pop is ~2 us of host time per solve for
+    nothing (GADMM_ROCTX=0 forces them off)."""
+    v = os.environ.get("GADMM_ROCTX")
+    if v is not None:
+        return v == "1"
+    return "rocprof" in os.environ.get("LD_PRELOAD", "") or any(k.startswith("ROCPROF") for k in os.environ)
+
+
 def _load_roctx():
     global _roctx
     if _roctx is None:
+        if not _profiled():
+            _roctx = False
+            return None
         for name in ("libroctx64.so", "/opt/rocm/lib/libroctx64.so"):
             try:
                 _roctx = ctypes.CDLL(name)
