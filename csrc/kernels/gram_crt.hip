@@ -7,13 +7,13 @@
 // by its power-of-two exponent e_j, |x_ij| <= (127/128) 2^{e_j}) becomes the integer
 //   N_ij = rint(x_ij 2^{KB - e_j}),   |N_ij| < 2^KB,  KB = 49   (the digit scheme keeps the same 49 bits)
 // and the integer Gram  G_ab = sum_i N_ia N_ib  (|G| < m 2^98 <= 2^119 for m <= 2^21) is computed modulo
-// 19 pairwise coprime moduli p <= 127 (product ~2^121.8): for each p, residues R_p == N mod p with
-// |R_p| <= 68 are int8, and  G mod p = R_p^T R_p mod p  is ONE int8 GEMM with exact int32 accumulation
-// (a chunk of KC samples: KC * 68^2 < 2^31), reduced mod p after every chunk. Garner's
+// 16 pairwise coprime moduli p <= 234 (product ~2^123.0): for each p, residues R_p == N mod p with
+// |R_p| <= 120 are int8, and  G mod p = R_p^T R_p mod p  is ONE int8 GEMM with exact int32 accumulation
+// (a chunk of KC samples: KC * 120^2 < 2^31), reduced mod p after every chunk. Garner's
 // mixed-radix reconstruction then gives G_ab exactly, and
 //   A_ab = 2^{e_a + e_b - 2 KB} G_ab
 // with one rounding (the final double). So the result is exact for the 49-bit images of the inputs -- the
-// digit scheme's accuracy, with 19 GEMMs instead of 28 digit-pair products, and a 256 x 256 tile per
+// digit scheme's accuracy, with 16 GEMMs instead of 28 digit-pair products, and a 256 x 256 tile per
 // workgroup (8 waves of 128 x 64, 128 accumulator registers each): half the panel bytes per MFMA of the
 // digit kernel's 64 x 64 tile.
 //
@@ -42,35 +42,35 @@ typedef int v16i __attribute__((ext_vector_type(16)));
 
 namespace {
 
-constexpr int NMOD = 19;
-constexpr int kMod[NMOD] = {127, 125, 121, 113, 109, 107, 103, 101, 97, 89, 83, 79, 73, 71, 67, 61, 59, 53, 47};
+constexpr int NMOD = 16;
+// pairwise coprime, each <= 234 so that the slicer's representatives |r| <= 0.511 p <= 120 fit int8 (below), product
+// 2^123.0 > 2 * 2^21 * 2^98 (greedy from 234 down: 16 moduli instead of the 19 moduli <= 127 of the first cut,
+// ~16 % fewer int8 GEMMs, profiles/r06_crt)
+constexpr int kMod[NMOD] = {234, 233, 229, 227, 223, 217, 215, 211, 209, 199, 197, 193, 191, 181, 179, 173};
 // kInv[i][j] = (kMod[j] mod kMod[i])^{-1} mod kMod[i], j < i (Garner); generated and checked by
 // tests/test_gram_crt_math.py
 constexpr int kInv[NMOD][NMOD] = {
-    {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-    {63, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-    {101, 91, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-    {105, 66, 99, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-    {103, 75, 100, 82, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-    {91, 6, 23, 18, 54, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-    {73, 89, 63, 31, 86, 26, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-    {35, 80, 96, 59, 38, 17, 51, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-    {55, 52, 93, 91, 89, 68, 81, 73, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-    {82, 47, 64, 26, 49, 5, 70, 52, 78, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-    {17, 2, 59, 36, 16, 45, 54, 60, 6, 14, 0, 0, 0, 0, 0, 0, 0, 0, 0},
-    {28, 67, 32, 7, 29, 48, 56, 18, 22, 8, 20, 0, 0, 0, 0, 0, 0, 0, 0},
-    {23, 66, 35, 42, 71, 58, 56, 60, 70, 32, 22, 61, 0, 0, 0, 0, 0, 0, 0},
-    {52, 25, 27, 22, 43, 2, 20, 45, 41, 4, 6, 9, 36, 0, 0, 0, 0, 0, 0},
-    {19, 52, 36, 51, 8, 62, 54, 2, 38, 64, 21, 28, 56, 17, 0, 0, 0, 0, 0},
-    {49, 41, 60, 27, 14, 4, 16, 29, 39, 24, 25, 17, 56, 55, 51, 0, 0, 0, 0},
-    {46, 17, 20, 47, 13, 16, 55, 52, 14, 2, 32, 3, 38, 5, 37, 30, 0, 0, 0},
-    {48, 14, 46, 38, 18, 1, 35, 21, 47, 28, 23, 51, 8, 3, 19, 20, 9, 0, 0},
-    {10, 44, 7, 5, 22, 29, 21, 27, 16, 28, 17, 25, 38, 2, 40, 37, 4, 8, 0}};
-__constant__ int kModDev[NMOD] = {127, 125, 121, 113, 109, 107, 103, 101, 97, 89, 83, 79, 73, 71, 67, 61, 59, 53, 47};
+    {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+    {1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+    {46, 172, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+    {65, 38, 114, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+    {142, 67, 186, 56, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+    {166, 95, 199, 152, 181, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+    {34, 12, 169, 18, 27, 108, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+    {156, 48, 129, 66, 88, 176, 53, 0, 0, 0, 0, 0, 0, 0, 0, 0},
+    {92, 61, 115, 151, 15, 183, 35, 105, 0, 0, 0, 0, 0, 0, 0, 0},
+    {91, 41, 73, 64, 141, 188, 112, 83, 20, 0, 0, 0, 0, 0, 0, 0},
+    {16, 104, 117, 46, 144, 69, 11, 183, 115, 99, 0, 0, 0, 0, 0, 0},
+    {113, 111, 59, 176, 148, 185, 79, 118, 181, 161, 145, 0, 0, 0, 0, 0},
+    {40, 141, 186, 69, 6, 169, 8, 86, 138, 24, 32, 96, 0, 0, 0, 0},
+    {41, 94, 132, 122, 125, 176, 16, 175, 97, 171, 34, 166, 163, 0, 0, 0},
+    {166, 63, 111, 138, 118, 33, 5, 28, 6, 9, 10, 64, 15, 90, 0, 0},
+    {156, 124, 34, 157, 45, 59, 103, 41, 149, 20, 137, 26, 125, 65, 29, 0}};
+__constant__ int kModDev[NMOD] = {234, 233, 229, 227, 223, 217, 215, 211, 209, 199, 197, 193, 191, 181, 179, 173};
 
 constexpr int KB = 49;            // bits of every value's integer image (|N| < 2^KB)
 constexpr long MAX_ROWS = 1L << 21;  // m 2^{2 KB} < M / 2 (the product of the moduli): exact reconstruction
-constexpr int KC = 32768;         // samples per chunk: KC * 68^2 < 2^31 (exact int32 sums)
+constexpr int KC = 32768;         // samples per chunk: KC * 120^2 < 2^31 (exact int32 sums)
 constexpr int KBC = KC / 32;      // 32-sample blocks per chunk
 constexpr int KBCP = KBC + 4;     // residue-buffer slots per modulus: a chunk zero-filled to whole stages
 constexpr int TT = 256;           // output tile (features) per workgroup
@@ -118,13 +118,14 @@ __global__ void __launch_bounds__(CE_NT) crt_colexp(const double* part, int Dp, 
 // [j][32] rows, each store covered half of a 2 KB span: the slicer ran at ~2.4 TB/s). Each integer image N is split
 // once into 13-bit digits, N = d3 2^39 + d2 2^26 + d1 2^13 + d0 (d3 in [-2^10, 2^10), the others in
 // [0, 2^13); exact double floor / fma), held as floats with d0 offset by MAGIC = 1.5 2^23. Then per modulus,
-// in f32 only (exact: every intermediate is an integer below 2^24):
+// in f32 only (exact: every intermediate is an integer below 2^24; |S' - MAGIC| < 2^13 + 2^13 (233 + 233) +
+// 2^10 233 < 2^22 for every p <= 234):
 //   S' = MAGIC + d0 + d1 (2^13 mod p) + d2 (2^26 mod p) + d3 (2^39 mod p)   in [2^23, 2^24), S' - MAGIC == N mod p
-//   q  = rint(S' / p - MAGIC / p)         (one fma with rounded constants: within 0.041 of (S' - MAGIC) / p)
-//   t  = S' - q p = MAGIC + r,  |r| <= 68 (|(S' - MAGIC) / p - q| <= 0.541)
+//   q  = rint(S' / p - MAGIC / p)         (one fma with rounded constants: within 0.011 of (S' - MAGIC) / p)
+//   t  = S' - q p = MAGIC + r,  |r| <= 120 (|(S' - MAGIC) / p - q| <= 0.511 for 173 <= p <= 234)
 // and the low byte of t's bit pattern IS r as int8 (the exponent is fixed at 2^23 over the whole range).
 // r is a valid int8 representative of N mod p (not always the balanced one, which nothing needs: the GEMM
-// epilogue reduces mod p, and the chunk sums stay exact, KC 68^2 < 2^31). Six f32 instructions per residue;
+// epilogue reduces mod p, and the chunk sums stay exact, KC 120^2 < 2^31). Six f32 instructions per residue;
 // round 6's first version (a per-modulus f64 divide-and-correct) made the slicer 12 % of the Gram, and
 // plain int products compile to quarter-rate v_mul_lo_u32 / v_mad_u64_u32 (profiles/r06_crt).
 constexpr float MAGIC = 12582912.0f;  // 1.5 2^23

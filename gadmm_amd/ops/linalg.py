@@ -68,8 +68,8 @@ def gram_ozaki(X: torch.Tensor, y: torch.Tensor, out=None, with_range: bool = Fa
 
 def gram_crt(X: torch.Tensor, y: torch.Tensor, out=None, with_range: bool = False):
     """Batched augmented Gram on the INT8 matrix cores by CRT slicing (csrc/kernels/gram_crt.hip: 49-bit
-    integer images of the column-scaled values, one int8 GEMM with exact int32 sums per modulus for 19
-    coprime moduli <= 127, Garner reconstruction of the exact integer Gram, one final rounding). Same
+    integer images of the column-scaled values, one int8 GEMM with exact int32 sums per modulus for 16
+    coprime moduli <= 234, Garner reconstruction of the exact integer Gram, one final rounding). Same
     outputs and accuracy class as ``gram_ozaki`` (the digit scheme keeps the same 49 bits); one accumulator
     per output element instead of seven, so 256 x 256 tiles. m <= 2^21 rows per shard. ``with_range``:
     also the (N,) column-range statistics of the accuracy gate."""

@@ -1380,7 +1380,7 @@ def test_newton_chord_safety_net_e4_shape(log24, log_obj0, persistent):
 
 @pytest.mark.parametrize("N,m,d", [(2, 5000, 300), (1, 20000, 97), (1, 9000, 1000), (1, 70000, 600)])
 def test_gram_crt_matches_f64(N, m, d):
-    """The CRT int8 Gram (gram_crt.hip: 49-bit integer images, 19 modular int8 GEMMs with exact int32 sums,
+    """The CRT int8 Gram (gram_crt.hip: 49-bit integer images, 16 modular int8 GEMMs with exact int32 sums,
     Garner reconstruction): every entry within 1e-14 of sqrt(A_aa A_bb) of the Kahan-chunked f64 reference
     (chunk boundaries at 32768 samples and padded 256-feature tiles included), b and y'y likewise, exactly
     symmetric, deterministic; the range statistic equals the digit kernel's."""
