@@ -130,7 +130,7 @@ def gram(X: torch.Tensor, y: torch.Tensor, ksplit: Optional[int] = None, out=Non
          ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
     """Batched augmented Gram. ``X``: (N, m, d) f64 contiguous, ``y``: (N, m).
     ``out``: optional preallocated ``(A, b, yy)`` written in place. Large shards go to the int8 matrix
-    cores (``gram_crt``, or ``gram_ozaki`` past its row bound or when the CRT workspace -- ~17 GB at
+    cores (``gram_crt``, or ``gram_ozaki`` past its row bound or when the CRT workspace -- ~14 GB at
     d = 10k -- cannot be allocated). Shards that path would serve with fewer kept bits than
     ``OZ_MAX_RANGE`` allows (an outlier row, a heavy-tailed column) are recomputed on the f64-MFMA kernel
     (one host read of the N range statistics: set-up code, never graph-captured)."""
