@@ -14,18 +14,18 @@
 //   A_ab = 2^{e_a + e_b - 2 KB} G_ab
 // with one rounding (the final double). So the result is exact for the 49-bit images of the inputs -- the
 // digit scheme's accuracy, with 16 GEMMs instead of 28 digit-pair products, and a 256 x 256 tile per
-// workgroup (8 waves of 128 x 64, 128 accumulator registers each): half the panel bytes per MFMA of the
+// workgroup (8 waves of 128 x 64, 128 accumulator registers each): half the panel bytes per MAC of the
 // digit kernel's 64 x 64 tile.
 //
 // Kernels (host driver gadmm_gram_crt_f64 below, per shard, one chunk of KC samples at a time):
 //   crt_colmax / crt_colexp   column exponents e_j of the augmented [X | y] (one pass)
 //   crt_slice     residues of a chunk: R[p][kb][h][j][16] int8 -- modulus p, 32-sample block kb, half h of
-//                 the block (samples 16 h ..), feature j: one MFMA operand half-fragment = 16 contiguous
+//                 the block (samples 16 h ..), feature j: one MFMA operand fragment row = 16 contiguous
 //                 bytes, and the 64 features of one LDS-DMA piece 1 KB contiguous
 //   crt_gemm      one workgroup per (lower-triangle 256 x 256 tile, modulus): a 4-stage LDS-DMA ring of
-//                 panels (64 samples per stage), 16 v_mfma_i32_32x32x32_i8 per wave per stage with the next
+//                 panels (64 samples per stage), 32 v_mfma_i32_16x16x64_i8 per wave per stage with the next
 //                 stage's fragment reads and DMA pieces interleaved between them; the chunk's sums go into
-//                 the int16 residue matrices C_p (reduced mod p). 70 % MFMA busy (profiles/r06_crt)
+//                 the int16 residue matrices C_p (reduced mod p). 74 % MFMA busy (profiles/r06_crt)
 //   crt_finish    Garner per lower-triangle element -> A (full symmetric), b, y'y
 //   crt_range     the column-range statistic of linalg.gram's accuracy gate
 #include <stdlib.h>
@@ -38,7 +38,6 @@
 #include "gadmm_common.h"
 
 typedef int v4i __attribute__((ext_vector_type(4)));
-typedef int v16i __attribute__((ext_vector_type(16)));
 
 namespace {
 
@@ -210,10 +209,19 @@ __device__ __forceinline__ void wait_vm() {
 }
 __device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt((0xF) | (0x3 << 14) | (0x7 << 4)); }
 
-// BKS: 32-sample blocks per pipeline stage; NSTG: LDS ring of stage buffers (NSTG - 1 stages in flight)
+// BKS: 32-sample blocks per pipeline stage (even); NSTG: LDS ring of stage buffers (NSTG - 1 stages in
+// flight). The MFMA is v_mfma_i32_16x16x64_i8: per 64-sample K step a wave reads FA = 8 A and FB = 4 B
+// fragments (16 contiguous bytes per lane of the LDS image below) and runs 32 MFMAs into 32 accumulators
+// of 16 x 16 (128 registers). Against v_mfma_i32_32x32x32_i8 with the same reads and accumulator
+// registers per stage (4 + 2 fragments and 8 MFMAs per 32-sample step): 0.94 vs 1.12 s at
+// 2 x 625k x 10k, same box (profiles/r06_crt/mf) -- the MI355X_MICROARCH.md observation that the
+// 16 x 16 shapes deliver ~1.15x the 32 x 32 ones' rate, here for int8.
 template <int BKS, int NSTG>
 __global__ void __launch_bounds__(GNT, 1) crt_gemm(const signed char* R, int Dp, int per, const int4* list,
                                                    int kbn, short* C, int first) {
+  constexpr int MF = 16, FA = 8, FB = 4, FR = FA + FB, NACC = 4;
+  constexpr int KS = BKS / 2;  // MFMA K steps (64 samples) per stage
+  static_assert(KS * 2 == BKS, "whole K steps per stage");
   constexpr int PANEL = BKS * TT * 32;  // bytes of one operand panel per stage
   constexpr int STAGE = 2 * PANEL;      // A + B
   constexpr int P = 2 * BKS;            // DMA pieces (1 KB) per wave per stage
@@ -224,31 +232,20 @@ __global__ void __launch_bounds__(GNT, 1) crt_gemm(const signed char* R, int Dp,
   const int mp = kModDev[p];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int wr = wv >> 2, wc = wv & 3;
-  const int r = lane & 31, h = lane >> 5;
   const signed char* gA = R + (long)p * KBCP * Dp * 32 + (long)ti * TT * 16;  // + kb * Dp * 32 + h * Dp * 16
   const signed char* gB = R + (long)p * KBCP * Dp * 32 + (long)tj * TT * 16;
   const long kbstride = (long)Dp * 32;
   // LDS image of a stage: [panel A / B][32-sample block][half of the block: samples 16 h ..][feature][16 B]
   // -- the global layout's order, so every DMA piece is 1 KB contiguous on both sides, and a fragment
-  // read (32 consecutive features of one half per 32 lanes) is 512 B contiguous and conflict-free in
-  // ds_read_b128's lane groups (with [feature][32 B] rows the 32-B stride used only half of the banks:
-  // 2-way conflicts). This wave's P pieces per stage: piece c = P wv + u: panel c / (8 BKS), block
+  // read is conflict-free in ds_read_b128's lane groups: lanes 16 q .. 16 q + 15 read 16 consecutive
+  // features of the (block q / 2, half q % 2) plane, the planes 4 KB apart (with [feature][32 B] rows the
+  // 32-B stride used only half of the banks: 2-way conflicts). This wave's P pieces per stage: piece c = P wv + u: panel c / (8 BKS), block
   // (c / 8) % BKS, half (c / 4) % 2, features 64 (c % 4) .. + 63 (1 KB of LDS).
-  auto issue = [&](int kb0, int buf) {
+  // a fragment's lane offset inside a K step of a panel: lane l holds samples 16 (l / 16) .. + 15 of row l % 16
+  const int lane_off = (lane >> 5) * (TT * 32) + ((lane >> 4) & 1) * (TT * 16) + (lane & 15) * 16;
+  v4i acc[FA * FB];
 #pragma unroll
-    for (int u = 0; u < P; ++u) {
-      const int c = P * wv + u;
-      const int pn = c / (8 * BKS), blk = (c >> 3) % BKS, hh = (c >> 2) & 1, q = c & 3;
-      const signed char* src = (pn ? gB : gA) + (long)(kb0 + blk) * kbstride + (long)hh * (kbstride / 2) + (q * 64 + lane) * 16;
-      signed char* dst = lds + buf * STAGE + pn * PANEL + blk * (TT * 32) + hh * (TT * 16) + q * 1024;
-      __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
-    }
-  };
-  v16i acc[4][2];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b) acc[a][b] = v16i{};
+  for (int i = 0; i < FA * FB; ++i) acc[i] = v4i{};
   const int nst = kbn / BKS;  // kbn is a multiple of BKS (the slicer zero-fills to a stage boundary)
   // Software pipeline over stages, two levels deep:
   //  * LDS-DMA: a ring of NSTG stage buffers, NSTG - 1 stages in flight (stage s + NSTG - 1 is issued during
@@ -258,20 +255,26 @@ __global__ void __launch_bounds__(GNT, 1) crt_gemm(const signed char* R, int Dp,
   //    __syncthreads(), whose fence would drain them (cdna_hip_programming.md §5, "Pipelining across
   //    barriers") -- then makes every wave's stage s visible and every wave's fragment reads of stage s - 1
   //    complete;
-  //  * fragments: stage s's 6 BKS ds_read_b128 go into one register set while the 8 BKS MFMAs of stage
-  //    s - 1 run from the other;
+  //  * fragments: stage s's NR ds_read_b128 go into one register set while the NM MFMAs of stage s - 1 run
+  //    from the other;
   //  * one interleaved stream per step: MFMA, fragment read, MFMA, ..., with a DMA piece after every
-  //    8 BKS / P MFMAs (pinned by sched_group_barrier). An LDS-DMA piece costs its wave 60-185 issue cycles
+  //    NM / P MFMAs (pinned by sched_group_barrier). An LDS-DMA piece costs its wave 60-185 issue cycles
   //    (MI355X_MICROARCH.md, per-instruction constants): issued as a block at the top of the step, behind
   //    the barrier that lines both waves of a SIMD up, they idled the matrix pipe (51 % MFMA busy); between
-  //    MFMAs they overlap the pipe's 32 cycles per MFMA.
-  v4i fa0[BKS][4], fb0[BKS][2], fa1[BKS][4], fb1[BKS][2];
-  auto read_frag = [&](const signed char* SA, int i, v4i (&fa)[BKS][4], v4i (&fb)[BKS][2]) {
-    const int k = i / 6, f = i % 6;
-    if (f < 4)
-      fa[k][f] = *reinterpret_cast<const v4i*>(SA + k * (TT * 32) + h * (TT * 16) + (wr * 128 + 32 * f + r) * 16);
-    else
-      fb[k][f - 4] = *reinterpret_cast<const v4i*>(SA + PANEL + k * (TT * 32) + h * (TT * 16) + (wc * 64 + 32 * (f - 4) + r) * 16);
+  //    MFMAs they overlap the matrix pipe's work.
+  constexpr int NM = KS * FA * FB, NR = KS * FR, EVERY = NM / P;
+  static_assert(NR <= NM && NM % P == 0, "interleave shape");
+  v4i fr0[NR], fr1[NR];
+  auto read_frag = [&](const signed char* SA, int i, v4i (&fr)[NR]) {
+    const int ks = i / FR, f = i % FR;
+    const int step_off = ks * 2 * (TT * 32);
+    const signed char* q = f < FA ? SA + step_off + (wr * 128 + MF * f) * 16
+                                  : SA + PANEL + step_off + (wc * 64 + MF * (f - FA)) * 16;
+    fr[i] = *reinterpret_cast<const v4i*>(q + lane_off);
+  };
+  auto mma = [&](int m, const v4i (&fr)[NR]) {
+    const int ks = m / (FA * FB), a = (m / FB) % FA, b = m % FB;
+    acc[a * FB + b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fr[ks * FR + a], fr[ks * FR + FA + b], acc[a * FB + b], 0, 0, 0);
   };
   auto issue_piece = [&](int st, int u) {  // piece u of this wave for stage st (clamped to the last stage)
     const int sc = st < nst ? st : nst - 1;
@@ -286,18 +289,15 @@ __global__ void __launch_bounds__(GNT, 1) crt_gemm(const signed char* R, int Dp,
     wait_lgkm0();
     __builtin_amdgcn_s_barrier();
   };
-  constexpr int NM = 8 * BKS, NR = 6 * BKS, EVERY = NM / P;
-  static_assert(NR <= NM && NM % P == 0, "interleave shape");
-  // stage s: read its fragments into (fa, fb) while the MFMAs of stage s - 1 run from (ua, ub)
-  auto step = [&](int s, v4i (&fa)[BKS][4], v4i (&fb)[BKS][2], v4i (&ua)[BKS][4], v4i (&ub)[BKS][2]) {
+  // stage s: read its fragments into fr while the MFMAs of stage s - 1 run from fu
+  auto step = [&](int s, v4i (&fr)[NR], const v4i (&fu)[NR]) {
     top();
     const signed char* SA = lds + (s % NSTG) * STAGE;
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int m = 0; m < NM; ++m) {
-      const int k = m / 8, a = (m >> 1) & 3, b = m & 1;
-      acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(ua[k][a], ub[k][b], acc[a][b], 0, 0, 0);
-      if (m < NR) read_frag(SA, m, fa, fb);
+      mma(m, fu);
+      if (m < NR) read_frag(SA, m, fr);
       if (m % EVERY == EVERY - 1) issue_piece(s + NSTG - 1, m / EVERY);
     }
 #pragma unroll
@@ -315,58 +315,53 @@ __global__ void __launch_bounds__(GNT, 1) crt_gemm(const signed char* R, int Dp,
     top();
 #pragma unroll
     for (int u = 0; u < P; ++u) issue_piece(NSTG - 1, u);
-    const signed char* SA0 = lds;
 #pragma unroll
-    for (int i = 0; i < NR; ++i) read_frag(SA0, i, fa0, fb0);
+    for (int i = 0; i < NR; ++i) read_frag(lds, i, fr0);
     int s = 1;
     for (; s + 1 < nst; s += 2) {
-      step(s, fa1, fb1, fa0, fb0);
-      step(s + 1, fa0, fb0, fa1, fb1);
+      step(s, fr1, fr0);
+      step(s + 1, fr0, fr1);
     }
     wait_lgkm0();
     if (s < nst) {  // nst even: stage nst - 1 still to read
-      step(s, fa1, fb1, fa0, fb0);
+      step(s, fr1, fr0);
       wait_lgkm0();
 #pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        const int k = m / 8, a = (m >> 1) & 3, b = m & 1;
-        acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa1[k][a], fb1[k][b], acc[a][b], 0, 0, 0);
-      }
-    } else {  // nst odd: stage nst - 1 is in fa0 / fb0
+      for (int m = 0; m < NM; ++m) mma(m, fr1);
+    } else {  // nst odd: stage nst - 1 is in fr0
 #pragma unroll
-      for (int m = 0; m < NM; ++m) {
-        const int k = m / 8, a = (m >> 1) & 3, b = m & 1;
-        acc[a][b] = __builtin_amdgcn_mfma_i32_32x32x32_i8(fa0[k][a], fb0[k][b], acc[a][b], 0, 0, 0);
-      }
+      for (int m = 0; m < NM; ++m) mma(m, fr0);
     }
     wait_vm<0>();  // the clamped re-loads past the last stage land before the workgroup's LDS is released
   }
-  // epilogue: C_p = (C_p + chunk sum) mod p, symmetric, as int16. The previous chunks' residues are read
-  // 16 at a time (one 32 x 32 block) before any is used: a per-element load behind the `first` test would
-  // make hipcc branch around each load and wait for it alone (cdna_hip_programming.md §5, trap (c))
+  // epilogue: C_p = (C_p + chunk sum) mod p, symmetric, as int16. The previous chunks' residues of one
+  // accumulator are read before any is used: a per-element load behind the `first` test would make hipcc
+  // branch around each load and wait for it alone (cdna_hip_programming.md §5, trap (c)).
+  // Output element g of accumulator (a, b): row 16 a + 4 (lane / 16) + g, column 16 b + lane % 16.
   short* Cp = C + (long)p * Dp * Dp;
   const int hm = mp >> 1;
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < FA; ++a)
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      const int col = tj * TT + wc * 64 + 32 * b + r;
-      const long base = (long)(ti * TT + wr * 128 + 32 * a + 4 * h) * Dp + col;  // row offset (g&3) + 8 (g>>2)
-      int old[16];
+    for (int b = 0; b < FB; ++b) {
+      const int col = tj * TT + wc * 64 + MF * b + (lane & (MF - 1));
+      const long base = (long)(ti * TT + wr * 128 + MF * a + 4 * (lane / MF)) * Dp + col;
+      auto roff = [&](int g) -> long { return (long)g * Dp; };
+      int old[NACC];
       if (first) {
 #pragma unroll
-        for (int g = 0; g < 16; ++g) old[g] = 0;
+        for (int g = 0; g < NACC; ++g) old[g] = 0;
       } else {
 #pragma unroll
-        for (int g = 0; g < 16; ++g) old[g] = Cp[base + (long)((g & 3) + 8 * (g >> 2)) * Dp];
+        for (int g = 0; g < NACC; ++g) old[g] = Cp[base + roff(g)];
       }
 #pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        int v = acc[a][b][g] % mp + old[g];
+      for (int g = 0; g < NACC; ++g) {
+        int v = acc[a * FB + b][g] % mp + old[g];
         v %= mp;
         if (v > hm) v -= mp;
         if (v < -hm) v += mp;
-        Cp[base + (long)((g & 3) + 8 * (g >> 2)) * Dp] = (short)v;
+        Cp[base + roff(g)] = (short)v;
       }
     }
 }
