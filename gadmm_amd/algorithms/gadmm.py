@@ -323,11 +323,6 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
     # D-GADMM on a cached engine: the first launch's chains start drawing now (geometries from the
     # schedule's RNG here, greedy walks on the native host worker) and are joined where the launch's
     # tables are built, so the walks overlap the refresh / set_path / reset below
-    if eng is not None and refresh:
-        # in place on the engine's stream (Gram, then inverses), launched first: the device works through
-        # them while the host draws chains and builds the launch below (profiles/r06_dgadmm)
-        eng.refresh(model.X, model.y)
-        _timing.host_stamp("native:refresh")
     early = None
     if eng is not None and state is None and not _static_schedule(schedule, max_iter) \
             and opts.get("persistent", "auto") in (True, "auto") and "epoch_chunk" not in opts \
@@ -335,6 +330,12 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         early = _dyn_early_draw(eng, schedule, max_iter, fabric, n_total)
         _timing.host_stamp("native:early_draw")
     try:
+        if eng is not None and refresh:
+            # in place on the engine's stream (Gram, then inverses), while the native worker walks the
+            # early-drawn chains (launching the refresh before the draw exposed the walks at the join:
+            # profiles/r06_dgadmm)
+            eng.refresh(model.X, model.y)
+            _timing.host_stamp("native:refresh")
         if eng is None:
             eng = NativeChainEngine(model.X, model.y, local_ids, n_total, kind, rho=rho, obj0=obj0, tol=tol,
                                     max_iter=max_iter, lam=getattr(model, "lam", 0.0), step=step, max_inner=max_inner,
@@ -588,9 +589,12 @@ def _chain_admm_native(model, local_ids, n_total, rho, obj0, tol, max_iter, comm
         starts = ep_start
         P = Pall[:n_drawn[0]]
         com_cost = pre["com"][:iters]
-        # leave the schedule (and the engine's plan) where the epoch-by-epoch run would have left them
-        schedule.skip(saved, Pn, Cn, int(np.searchsorted(rechains, iters, side="right")))  # rechains ascend
-        eng.set_path(P[int(np.searchsorted(starts, max(last_launched, 1), side="right") - 1)], placement, rank)
+        # leave the schedule (and the engine's plan) where the epoch-by-epoch run would have left them --
+        # unless nobody can look: a schedule private to this call (dynamic_group_admm builds one per solve)
+        # with no state to flush (~6 us of host time per D-GADMM solve, profiles/r06_dgadmm)
+        if not getattr(schedule, "private", False) or opts.get("state", True):
+            schedule.skip(saved, Pn, Cn, int(np.searchsorted(rechains, iters, side="right")))  # rechains ascend
+            eng.set_path(P[int(np.searchsorted(starts, max(last_launched, 1), side="right") - 1)], placement, rank)
     else:
         # D-GADMM: run epoch by epoch; at a re-chain iteration flush the heads' pending duals with the
         # old chain, install the new chain, continue. Every rank draws the same chain sequence.
@@ -849,6 +853,7 @@ def dynamic_group_admm(model, rho, obj0, acc, max_iter, path, path_cost, coheren
     n_total = kw.pop("n_total", model.n_local)
     local_ids = kw.pop("local_ids", list(range(model.n_local)))
     sched = PathSchedule(n_total, path, path_cost, coherence, kind=kind, seed=seed)
+    sched.private = True  # never seen by the caller: the solve need not leave it at the stop
     return chain_admm(model, local_ids, n_total, rho, obj0, acc, max_iter, schedule=sched,
                       name="D-GADMM(coh=%s)" % coherence, **kw)
 
