@@ -256,8 +256,10 @@ __global__ void __launch_bounds__(64) chain_persistent_logistic_kernel(PersistAr
 // hand-offs are the one-wave kernel's; only s_k differs in rounding (z from the recursion), so traces
 // match the other engines to ~1e-13 instead of bit for bit.
 constexpr int ZR_NT = 128;
-constexpr int ZR_SLOTS = 8;  // s ring depth; the margins wave checks it every ZR_CHK steps
-constexpr int ZR_CHK = 4;
+constexpr int ZR_SLOTS = 64;  // s ring depth; the margins wave checks it every ZR_CHK steps
+// (same-box A/B, E3 bench: 8/4 5.34, 16/4 5.34, 16/8 5.17, 32/8 5.11, 64/8 4.93 ms; 128/8 with an early-end
+// check every 8 steps 5.41, 32/16 with one every step 5.43: profiles/r06_logistic)
+constexpr int ZR_CHK = 8;
 
 __device__ __forceinline__ int zr_load_acq(const int* p) {
   const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
