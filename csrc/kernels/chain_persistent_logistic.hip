@@ -584,8 +584,8 @@ extern "C" int gadmm_xcd_mode(const PersistArgs* a, int blocks, long cap_total);
 // 6.60 / 6.71 vs 6.37 / 6.39 ms, profiles/r05_c: the inner step is bound by its dependent chain, not FMA
 // issue -- and was removed in round 6.)
 // The margins recursion (two waves per worker) is the default: 6.3 -> 5.0-5.3 ms on E3 at the reference's
-// 53 iterations (profiles/r05_j); GADMM_LOGISTIC_ZREC=0 selects the one-wave kernel, bit-identical to
-// the graph engine.
+// 53 iterations (profiles/r05_j), 4.93 ms with the 64-slot ring (profiles/r06_logistic);
+// GADMM_LOGISTIC_ZREC=0 selects the one-wave kernel, bit-identical to the graph engine.
 static bool logi_zrec() {
   const char* e = getenv("GADMM_LOGISTIC_ZREC");
   return !(e && e[0] == '0');

@@ -1,5 +1,5 @@
 """Digest of the Gram kernel's output on fixed seeded shards (compare runs under different kernel
-switches, e.g. GADMM_GRAM_GLDS=0 / 1, for bit-identity): python tools/gram_digest.py"""
+switches, e.g. GADMM_GRAM_OZAKI=0 / 1 or GADMM_GRAM_INT8=crt / digits): python tools/gram_digest.py"""
 import hashlib
 import os
 import sys
