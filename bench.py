@@ -136,6 +136,43 @@ def main():
 ONE_GPU_US = {"blocked": 1.28, "per-worker": 2.24, "paired": 2.04}
 
 
+def _one_gpu_calibration(args, rank, world, device, obj0):
+    """The compute term of the tournament's model measured on THIS box (the
+    ONE_GPU_US constants come from other boxes' profiles): rank 0 times the whole chain on its own GPU
+    on the one-GPU temporally blocked kernel (3 solves after 2 warm ones; the other ranks wait at the
+    broadcast, so a shared GPU is not time-shared meanwhile) and every rank gets the microseconds per
+    iteration. 0 / None when it fails (the constants are used then)."""
+    us = 0.0
+    if rank == 0:
+        try:
+            from gadmm_amd.data import linear_synthetic
+            from gadmm_amd.models import LinearRegression
+            from gadmm_amd.algorithms import chain_admm
+            ds = linear_synthetic(args.workers)
+            mdl = LinearRegression(ds.X.to(device).contiguous(), ds.y.to(device).contiguous())
+            ids = list(range(args.workers))
+
+            def solve():
+                return chain_admm(mdl, ids, args.workers, args.rho, obj0, args.tol, 3000,
+                                  engine_opts={"state": False, "residual": False})
+            for _ in range(2):
+                solve()
+            torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            for _ in range(3):
+                r = solve()
+            torch.cuda.synchronize(device)
+            if r.extra.get("engine") == "persistent" and r.iters > 0:
+                us = (time.perf_counter() - t0) / 3 * 1e6 / r.iters
+            del mdl
+        except Exception as e:  # the model falls back to the constants
+            print("bench.py: one-GPU calibration failed: %s" % e, file=sys.stderr, flush=True)
+            us = 0.0
+    t = torch.tensor([us], dtype=torch.float64)
+    dist.broadcast(t, src=0)
+    return float(t.item()) or None
+
+
 def _headline_candidates(args, X_cpu, y_cpu, local, placement, rank, world, device, share, obj0):
     """Every multi-GPU engine the tournament times, in preference order: dicts with ``name``, ``build``
     (timeout_s -> solver; collective), ``hops`` (cross-GPU hand-offs on the critical cycle per iteration,
@@ -198,7 +235,7 @@ def run_headline(args, rank, world, device, share):
         # one-way hop latency of every chain boundary (the quantity that decides the engine ranking)
         from gadmm_amd.parallel.hop_probe import hop_probe
         hop = hop_probe(rank, world, device)
-    sol, tournament, winner, tour_wall_s = None, None, None, None
+    sol, tournament, winner, tour_wall_s, calib_us = None, None, None, None, None
     if world > 1 and args.engine == "auto":
         # untimed: build and time every eligible multi-GPU engine, agree on the fastest (max over ranks).
         # A candidate that stalls (e.g. a persistent kernel whose peers cannot be co-resident with ranks
@@ -211,14 +248,7 @@ def run_headline(args, rank, world, device, share):
         winner, sol, tournament = engine_tournament([(c["name"], (lambda b=c["build"]: b(tour_timeout_s)))
                                                      for c in cands], world, solves=3, warm=1, expect=expect,
                                                     sync=lambda: torch.cuda.synchronize(device), log=log)
-        hop_us = max([h for h in (hop or {}).get("hop_us", []) if h is not None], default=None)
         info = {c["name"]: c for c in cands}
-        for row in tournament:
-            c = info[row["engine"]]
-            row["hops_per_iter"] = round(c["hops"], 4)
-            its = row["iters"] if isinstance(row["iters"], int) else expect
-            row["predicted_ms"] = (round(its * (ONE_GPU_US[c["base"]] + c["hops"] * hop_us) / 1e3, 4)
-                                   if (c["base"] and hop_us is not None and its) else None)
         if sol is not None:
             sol.close()  # rebuilt below with the requested hand-off deadline (collective)
             sol = info[winner]["build"](timeout_s)
@@ -273,6 +303,25 @@ def run_headline(args, rank, world, device, share):
                       % sorted({r.done for r in results}))
         restarts += 1
     ms = (t1 - t0) * 1e3 / max(args.steps, 1)
+    if tournament is not None:
+        # the tournament's cost model, predicted_ms = iters x (one-GPU us + hops x hop us), reported per
+        # candidate next to its measured time. The compute term is rank 0's one-GPU blocked solve measured
+        # on this box AFTER the timed solves (run before them, its leftover stream slowed the later
+        # candidates of a 4-rank shared-GPU rehearsal by up to 11 %: profiles/r06_b/calib), the other
+        # families scaled by the ONE_GPU_US ratios; model_error = measured / predicted - 1 (ranks
+        # time-sharing one GPU inflate it: the model has no term for that)
+        if os.environ.get("GADMM_TOURNAMENT_CALIBRATE", "1") != "0":
+            calib_us = _one_gpu_calibration(args, rank, world, device, obj0)
+        hop_us = max([h for h in (hop or {}).get("hop_us", []) if h is not None], default=None)
+        scale = (calib_us / ONE_GPU_US["blocked"]) if calib_us else 1.0
+        for row in tournament:
+            c = info[row["engine"]]
+            row["hops_per_iter"] = round(c["hops"], 4)
+            its = row["iters"] if isinstance(row["iters"], int) else expect
+            row["predicted_ms"] = (round(its * (scale * ONE_GPU_US[c["base"]] + c["hops"] * hop_us) / 1e3, 4)
+                                   if (c["base"] and hop_us is not None and its) else None)
+            row["model_error"] = (round(row["ms"] / row["predicted_ms"] - 1.0, 3)
+                                  if row.get("predicted_ms") and row.get("ok") and row.get("ms") else None)
     last = results[-1]
     iters, p2p, wire, mon, repl = last.iters, last.theta_bytes, last.wire_bytes, last.monitor_bytes, sol.replicated_bytes
     if world > 1:
@@ -341,6 +390,7 @@ def run_headline(args, rank, world, device, share):
             out["tournament_winner"] = winner
             out["tournament_deadline_s"] = tour_timeout_s
             out["tournament_wall_s"] = round(tour_wall_s, 3)
+            out["one_gpu_us_per_iter_measured"] = round(calib_us, 4) if calib_us else None
             out["rccl_built"] = any(row.get("engine") == "graph-rccl" for row in tournament)
         out["handoff_deadline_s"] = timeout_s  # the deadline of the warm-up and timed solves
         print(json.dumps(out), flush=True)
