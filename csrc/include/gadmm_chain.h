@@ -171,11 +171,13 @@ struct PersistArgs {
   int hard_stop, cont;
   // XCD packing (one GPU, speed only): xcd = 1 launches an 8x wider grid whose blocks b % 8 != 0
   // exit at once, dealing every working block onto one XCD; xcd = 2 also has the blocks post their
-  // XCC_ID into xchk ([XCHK] granules, zeroed by the launcher) and, if all agree, publish granules
+  // XCC_ID into xchk ([XCHK] granules) and, if all agree, publish granules
   // with plain stores that stay in that XCD's L2 (MI355X_MICROARCH.md price list). The env
-  // GADMM_XCD overrides xcd (A/B runs).
+  // GADMM_XCD overrides xcd (A/B runs). xtag: the granules' tag, fresh per launch (set by the
+  // launcher, gadmm_next_xtag), so xchk needs no memset in front of the kernel (a 4.8 us fill on the
+  // GPU timeline of every solve, profiles/r06_dgadmm).
   u32x4* xchk;
-  int xcd, pad_xcd;
+  int xcd, xtag;
   // Data-local temporal blocking across GPUs (chain_blocked_kernel, blk_dl = 1; engine/blocked_xgmi.py
   // data_local=True): the workgroups of a rank compute ONLY its own segment [seg_lo, seg_hi] (no other
   // rank's shards), blocked inside it as on one GPU; a position at a rank boundary exchanges theta with

@@ -227,17 +227,19 @@ __device__ __forceinline__ double reg_gemv(const double (&Mr)[DB], const double*
   return ((a0 + a1) + a2) + a3;
 }
 
-constexpr unsigned XTAG = 0x5a5a0001u;  // placement-check granule tag (the launcher zeroes xchk first)
+constexpr unsigned XTAG = 0x5a5a0001u;  // placement-check granule tag of launchers that zero xchk first
 
 // XCD packing (PersistArgs::xcd): every working block posts its XCC_ID into xchk[bid] and waits for
 // all nb; true iff they are all equal, i.e. every reader of every granule shares this block's L2.
 // The verdict is identical in every block (same inputs); false on a deadline (the run then times
-// out through its normal path, with sc1 stores). lds_flag: one int of LDS.
-__device__ __forceinline__ bool xcd_verdict(u32x4* xchk, int bid, int nb, unsigned long long deadline, int* lds_flag) {
+// out through its normal path, with sc1 stores). lds_flag: one int of LDS. tag: XTAG behind a memset
+// of xchk, or the launch's own PersistArgs::xtag (no memset: earlier launches' granules never match).
+__device__ __forceinline__ bool xcd_verdict(u32x4* xchk, int bid, int nb, unsigned long long deadline, int* lds_flag,
+                                            unsigned tag = XTAG) {
   const __amdgpu_buffer_rsrc_t rs = rsrc_of(xchk);
   const int lane = threadIdx.x & 63;
   if (threadIdx.x < 64) {
-    if (lane == 0) store_granule<false>(rs, bid * 16, XTAG, (double)xcc_id());
+    if (lane == 0) store_granule<false>(rs, bid * 16, tag, (double)xcc_id());
     bool ok = true, same = true;
     double first = -1.0;
     for (int i0 = 0; i0 < nb; i0 += 64) {
@@ -245,7 +247,7 @@ __device__ __forceinline__ bool xcd_verdict(u32x4* xchk, int bid, int nb, unsign
       double x = 0.0;
       if (i < nb)
         for (int spin = 0;; ++spin) {
-          if (load_granule<false>(rs, i * 16, XTAG, &x)) break;
+          if (load_granule<false>(rs, i * 16, tag, &x)) break;
           if ((spin & 7) == 7 && now_ticks() > deadline) {
             ok = false;
             break;

@@ -253,7 +253,7 @@ __global__ void __launch_bounds__(64 * MAXW) chain_blocked_kernel(PersistArgs a)
   const long ring_base = 2L * n * 2 * d;  // theta ring [ring][n][d] after the exchange table
   const long etab_base = 2L * n * 2 * d + (long)a.ring * n * d;
   bool local = false;  // publish with plain stores (every block verified on this XCD)
-  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, W + Wo + 1, deadline, &stop_iter_lds);
+  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, W + Wo + 1, deadline, &stop_iter_lds, (unsigned)a.xtag);
   if (!SYS && bid == 0 && threadIdx.x == 0) a.ctl->placed = a.xcd > 0 ? (local ? 2 : 1) : 0;
 
   if (bid == W + Wo) {
@@ -1157,6 +1157,7 @@ long gadmm_chain_blocked_tab_granules_dyn(int n, int d, int ring) { return 4L * 
 
 long gadmm_resident_capacity(const void* fn, int threads, size_t shm);  // chain_persistent.hip
 int gadmm_xcd_mode(const PersistArgs* a, int blocks, long cap_total);  // chain_persistent.hip
+unsigned gadmm_next_xtag();  // chain_persistent.hip
 
 int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
   const PersistArgs& a = *args;
@@ -1269,7 +1270,7 @@ int gadmm_chain_blocked_launch(const PersistArgs* args, hipStream_t st) {
     ka.dbg = e ? atoi(e) : 0;
   }
   ka.xcd = xcd;
-  if (xcd > 1) GADMM_CHECK(hipMemsetAsync(a.xchk, 0, (size_t)XCHK * 16, st));
+  ka.xtag = (int)gadmm_next_xtag();  // fresh placement-check tag: no memset of xchk
   void* kargs[] = {&ka};
   GADMM_CHECK(hipLaunchKernel(fn, dim3(grid), dim3(64 * MAXW), kargs, (size_t)lds, st));
   GADMM_CHECK(hipGetLastError());

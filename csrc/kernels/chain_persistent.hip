@@ -33,6 +33,7 @@
 #include "persist_device.h"
 #include <stdlib.h>
 #include <string.h>
+#include <atomic>
 #include <mutex>
 
 namespace {
@@ -78,7 +79,7 @@ __global__ void __launch_bounds__(REG ? 64 : NT) chain_persistent_kernel(Persist
   }
   lds_barrier();
   bool local = false;  // publish with plain stores (every block verified on this XCD)
-  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds);
+  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds, (unsigned)a.xtag);
   if (!SYS && bid == 0 && threadIdx.x == 0) a.ctl->placed = a.xcd > 0 ? (local ? 2 : 1) : 0;
 
   if (a.has_monitor && bid == a.n_local) {
@@ -633,6 +634,13 @@ extern "C" int gadmm_xcd_mode(const PersistArgs* a, int blocks, long cap_total) 
   return gadmm_xcd_pick(a->xcd, a->sys_scope || a->nranks > 1, blocks, cap_total, a->xchk);
 }
 
+// PersistArgs::xtag of a launch: fresh per launch in this process (high bit set, so never XTAG nor a
+// zeroed granule), so the placement-check granules an earlier launch left in xchk never match.
+extern "C" unsigned gadmm_next_xtag() {
+  static std::atomic<unsigned> launches{0};
+  return 0x80000000u | ((launches.fetch_add(1, std::memory_order_relaxed) + 1u) & 0x7fffffffu);
+}
+
 extern "C" {
 
 // Workgroups the persistent kernel for `args` can keep resident (0: shape not eligible).
@@ -680,7 +688,7 @@ int gadmm_chain_persistent_launch(const PersistArgs* args, hipStream_t st) {
   if (v.shm > 65536) GADMM_CHECK(hipFuncSetAttribute(v.fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)v.shm));
   PersistArgs ka = a;
   ka.xcd = gadmm_xcd_mode(&a, blocks, cap);
-  if (ka.xcd > 1) GADMM_CHECK(hipMemsetAsync(a.xchk, 0, (size_t)XCHK * 16, st));
+  ka.xtag = (int)gadmm_next_xtag();  // fresh placement-check tag: no memset of xchk
   void* kargs[] = {&ka};
   GADMM_CHECK(hipLaunchKernel(v.fn, dim3(ka.xcd > 0 ? 8 * blocks : blocks), dim3(v.threads), kargs, v.shm, st));
   GADMM_CHECK(hipGetLastError());

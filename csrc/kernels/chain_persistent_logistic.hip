@@ -53,7 +53,7 @@ __global__ void __launch_bounds__(64) chain_persistent_logistic_kernel(PersistAr
   if (packed && (blockIdx.x & 7u)) return;  // a spacer block: only b % 8 == 0 work (one XCD)
   const int bid = packed ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   bool local = false;  // publish with plain stores (every block verified on this XCD)
-  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds);
+  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds, (unsigned)a.xtag);
   if (!SYS && bid == 0 && threadIdx.x == 0) a.ctl->placed = a.xcd > 0 ? (local ? 2 : 1) : 0;
 
   if (a.has_monitor && bid == a.n_local) {
@@ -311,7 +311,7 @@ __global__ void __launch_bounds__(ZR_NT) chain_persistent_logistic_zrec_kernel(P
   if (packed && (blockIdx.x & 7u)) return;
   const int bid = packed ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   bool local = false;
-  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds);
+  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds, (unsigned)a.xtag);
   if (!SYS && bid == 0 && threadIdx.x == 0) a.ctl->placed = a.xcd > 0 ? (local ? 2 : 1) : 0;
 
   if (a.has_monitor && bid == a.n_local) {
@@ -579,6 +579,7 @@ __global__ void __launch_bounds__(ZR_NT) chain_persistent_logistic_zrec_kernel(P
 
 extern "C" long gadmm_resident_capacity(const void* fn, int threads, size_t shm);
 extern "C" int gadmm_xcd_mode(const PersistArgs* a, int blocks, long cap_total);  // chain_persistent.hip
+extern "C" unsigned gadmm_next_xtag();  // chain_persistent.hip
 
 // (Round 5's four-wave sample-class split kernel, GADMM_LOGISTIC_SPLIT=1, was bit-identical but slower --
 // 6.60 / 6.71 vs 6.37 / 6.39 ms, profiles/r05_c: the inner step is bound by its dependent chain, not FMA
@@ -654,7 +655,7 @@ int gadmm_chain_persistent_logistic_launch(const PersistArgs* args, const LogiAr
   if (shm > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   PersistArgs ka = a;
   ka.xcd = gadmm_xcd_mode(&a, blocks, cap);
-  if (ka.xcd > 1) GADMM_CHECK(hipMemsetAsync(a.xchk, 0, (size_t)XCHK * 16, st));
+  ka.xtag = (int)gadmm_next_xtag();  // fresh placement-check tag: no memset of xchk
   const char* fs = getenv("GADMM_LOGISTIC_FASTSIGM");
   if (fs && fs[0] == '0') ka.dbg |= 32;
   const char* pf = getenv("GADMM_LOGISTIC_POSTFENCE");

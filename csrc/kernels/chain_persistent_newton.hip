@@ -969,7 +969,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
   if (packed && (blockIdx.x & 7u)) return;
   const int bid = packed ? (int)(blockIdx.x >> 3) : (int)blockIdx.x;
   bool local = false;
-  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds);
+  if (!SYS && a.xcd > 1) local = xcd_verdict(a.xchk, bid, a.n_local + (a.has_monitor ? 1 : 0), deadline, &xcd_lds, (unsigned)a.xtag);
   if (!SYS && bid == 0 && threadIdx.x == 0) a.ctl->placed = a.xcd > 0 ? (local ? 2 : 1) : 0;
   const RLds L;
 
@@ -1469,6 +1469,7 @@ __global__ void __launch_bounds__(RT) chain_persistent_newton_rec_kernel(Persist
 
 extern "C" long gadmm_resident_capacity(const void* fn, int threads, size_t shm);
 extern "C" int gadmm_xcd_mode(const PersistArgs* a, int blocks, long cap_total);  // chain_persistent.hip
+extern "C" unsigned gadmm_next_xtag();  // chain_persistent.hip
 
 // The pipeline kernel is the default; GADMM_NEWTON_REC=0 selects the one-wave solver kernel.
 static bool newton_rec(const LogiArgs& g) {
@@ -1524,7 +1525,7 @@ int gadmm_chain_persistent_newton_launch(const PersistArgs* args, const LogiArgs
   if (shm > 65536) GADMM_CHECK(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)shm));
   PersistArgs ka = a;
   ka.xcd = newton_rec(g) ? gadmm_xcd_mode(&a, blocks, cap) : 0;  // the pipeline kernel packs onto one XCD
-  if (ka.xcd > 1) GADMM_CHECK(hipMemsetAsync(a.xchk, 0, (size_t)XCHK * 16, st));
+  ka.xtag = (int)gadmm_next_xtag();  // fresh placement-check tag: no memset of xchk
   const char* fs = getenv("GADMM_NEWTON_FASTSIGM");
   if (fs && fs[0] == '0') ka.dbg |= 32;
   const char* rl = getenv("GADMM_NEWTON_RLAG");

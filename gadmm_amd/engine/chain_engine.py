@@ -346,6 +346,12 @@ class NativeChainEngine:
             native.check(lib.gadmm_gram_f64(*g_args), "gram_f64")
             native.check(lib.gadmm_spd_inverse_small_f64(*i_args), "spd_inverse_small_f64")
             self._minv_version = getattr(self, "_minv_version", 0) + 1
+            pf = getattr(self, "_pad_fast", None)
+            if pf is not None and pf[0] is self.Minv and pf[1] is getattr(self, "_minv_pad", None):
+                # the blocked D-GADMM inverse image follows at once, queued behind the inverses: built
+                # in run_persistent it sat between the epoch-table copy and the launch (profiles/r06_dgadmm)
+                native.check(lib.gadmm_pad_image_f64(*pf[2]), "pad_image")
+                self._minv_pad_version = self._minv_version
             return
         if (self.model == "linear" and X_loc.is_cuda and self.d <= 128 and X_loc.dtype == torch.float64
                 and y_loc.dtype == torch.float64 and X_loc.is_contiguous() and y_loc.is_contiguous()
@@ -746,7 +752,10 @@ class NativeChainEngine:
         pa.rres = native.ptr(self.rres)
         if fabric is None:  # XCD packing (one GPU): see PersistArgs::xcd
             if getattr(self, "_xchk", None) is None:
-                self._xchk = torch.zeros((256 * 4,), dtype=torch.int32, device=dev)
+                # zeroed on the engine stream, ordered before the kernel: a fill on torch's current stream
+                # could land while the blocks post their placement granules (they then spin to the deadline)
+                with torch.cuda.stream(self.stream):
+                    self._xchk = torch.zeros((256 * 4,), dtype=torch.int32, device=dev)
             pa.xchk, pa.xcd = self._xchk.data_ptr(), int(self.xcd)
         pa.hard_stop, pa.cont = int(hard_stop), 1 if cont else 0
         _timing.host_stamp("rp:args")
@@ -853,14 +862,16 @@ class NativeChainEngine:
         _timing.host_stamp("rp:tables")
         tl = None
         if timeline_iters > 0:
-            tl = torch.zeros((max(len(slots), 256) + 1, int(timeline_iters), 8), dtype=torch.int64, device=dev)
+            with torch.cuda.stream(self.stream):
+                tl = torch.zeros((max(len(slots), 256) + 1, int(timeline_iters), 8), dtype=torch.int64, device=dev)
             pa.timeline, pa.timeline_iters = tl.data_ptr(), int(timeline_iters)
         import time as _time
         if plan is not None:  # temporally blocked kernel: one halo hand-off per k iterations
             ng = int((self.lib.gadmm_chain_blocked_tab_granules_dyn if epochs is not None else
                       self.lib.gadmm_chain_blocked_tab_granules)(self.n_total, self.d, ring))
             if getattr(self, "_blk_tab", None) is None or self._blk_tab.numel() != ng * 4:
-                self._blk_tab = torch.zeros((ng * 4,), dtype=torch.int32, device=dev)
+                with torch.cuda.stream(self.stream):  # (ordered before the kernel, as _xchk)
+                    self._blk_tab = torch.zeros((ng * 4,), dtype=torch.int32, device=dev)
             pa.blk_k, pa.blk_len, pa.blk_pw = plan[0], plan[1], plan[3]
             pa.blk_tab = self._blk_tab.data_ptr()
             if epochs is not None:
@@ -930,11 +941,12 @@ class NativeChainEngine:
             self._rb_host = torch.empty(self._rb.shape, dtype=torch.float64, pin_memory=True)
             self._rb_host_np = self._rb_host.numpy()
             self._ctl_host = self._rb_host[0:4].view(torch.int32)
-        # native async copy on the engine stream (every launch above names that stream explicitly, so no
-        # torch stream context is needed around this block)
+        # queued on the engine stream (every launch above names that stream explicitly, so no torch stream
+        # context is needed around this block) as a small kernel writing the pinned buffer: an SDMA copy
+        # started ~10 us after the solve kernel ended (csrc/kernels/readback.hip)
         nb = self._rb.numel() * 8 if fetch else 32  # all of it, or the control block (8 x i32)
-        native.check(self.lib.gadmm_memcpy_d2h_async(self._rb_host.data_ptr(), self._rb.data_ptr(), nb,
-                                                     self.stream.cuda_stream), "d2h")
+        native.check(self.lib.gadmm_readback_d2h(self._rb_host.data_ptr(), self._rb.data_ptr(), nb,
+                                                 self.stream.cuda_stream), "readback")
         _timing.host_stamp("rp:copies_queued")
         if on_enqueued is not None:
             on_enqueued()

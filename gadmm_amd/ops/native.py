@@ -110,7 +110,7 @@ class PersistArgs(ctypes.Structure):
         ("blk_peer_lo", c_int * 8), ("blk_peer_hi", c_int * 8), ("blk_peer_tab", c_void_p),
         ("tstamp", c_void_p), ("ep_push", c_void_p), ("peer_thg", c_void_p), ("rres", c_void_p),
         ("hard_stop", c_int), ("cont", c_int),
-        ("xchk", c_void_p), ("xcd", c_int), ("pad_xcd", c_int),
+        ("xchk", c_void_p), ("xcd", c_int), ("xtag", c_int),
         ("blk_dl", c_int), ("dl_halo", c_int), ("dl_tab", c_void_p * 2), ("minv_pad", c_void_p),
         ("ep_flush", c_void_p),
     ]
@@ -220,6 +220,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "gadmm_chain_blocked_max_epochs": (c_int, []),
         "gadmm_memcpy_h2d_async": (c_int, [c_void_p, c_void_p, ctypes.c_size_t, c_void_p]),
         "gadmm_memcpy_d2h_async": (c_int, [c_void_p, c_void_p, ctypes.c_size_t, c_void_p]),
+        "gadmm_readback_d2h": (c_int, [c_void_p, c_void_p, ctypes.c_size_t, c_void_p]),
         "gadmm_chain_blocked_tab_granules": (c_long, [c_int, c_int, c_int]),
         "gadmm_chain_blocked_tab_granules_dyn": (c_long, [c_int, c_int, c_int]),
         "gadmm_epoch_tables": (c_int, [c_void_p, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p]),

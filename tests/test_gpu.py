@@ -990,11 +990,13 @@ def test_dgadmm_epoch_chunks_bit_identical(lin24, lin_obj0, coherence, chunk, bl
 
 
 def _xcc_ids(xchk):
-    """XCC_IDs the blocks of the last XCD-packed launch posted (placement-check granules)."""
+    """XCC_IDs the blocks of the last XCD-packed launch posted (placement-check granules: the launch's
+    own tag, PersistArgs::xtag, high bit set; granules past its blocks hold older launches' tags)."""
     g = xchk.view(-1, 4).cpu().numpy().astype(np.int64) & 0xffffffff
+    tag = int(g[0][0])
     ids = []
     for t, lo, t2, hi in g:
-        if t != 0x5a5a0001 or t2 != t:
+        if not (tag & 0x80000000) or t != tag or t2 != t:
             break
         ids.append(float(np.array([(int(hi) << 32) | int(lo)], dtype=np.uint64).view(np.float64)[0]))
     return ids
@@ -1405,3 +1407,24 @@ def test_gram_crt_matches_f64(N, m, d):
     assert torch.allclose(rng, rng_o, rtol=1e-12)
     A2 = gram_crt(X, y)[0]
     assert torch.equal(A, A2)
+
+
+def test_readback_kernel_copies_exactly():
+    """csrc/kernels/readback.hip: the persistent engines' result block goes to the pinned host buffer by
+    a kernel (then a system-scope release) instead of an SDMA copy; the host sees every word right
+    after the stream sync, for the full block, the 32-byte control block, and a non-16-byte size (the
+    copy-engine fallback)."""
+    from gadmm_amd.ops import native
+    lib = native.load()
+    s = torch.cuda.Stream(DEV)
+    # (doubles, doubles copied): kernel path, control block, copy-engine fallback (odd size), a prefix
+    for n, k in ((8 + 2 * 3001, 8 + 2 * 3001), (4, 4), (4097, 4097), (64, 32)):
+        src = torch.randn((n,), dtype=torch.float64, device=DEV)
+        torch.cuda.synchronize()
+        host = torch.full((n,), float("nan"), dtype=torch.float64, pin_memory=True)
+        nb = k * 8
+        native.check(lib.gadmm_readback_d2h(host.data_ptr(), src.data_ptr(), nb, s.cuda_stream), "readback")
+        s.synchronize()
+        assert torch.equal(host[:k], src[:k].cpu()), n
+        if k < n:
+            assert torch.isnan(host[k:]).all()
