@@ -357,3 +357,18 @@ def test_fast_getenv_tracks_os_environ(monkeypatch):
     assert getenv("GADMM_ENV_PROBE") == os.environ.get("GADMM_ENV_PROBE")
     monkeypatch.delenv("GADMM_ENV_PROBE")
     assert getenv("GADMM_ENV_PROBE", "x") == "x"
+
+
+def test_xcd_placement_tags_are_fresh_per_launch():
+    """PersistArgs::xtag (gadmm_next_xtag): every persistent launch tags its placement-check granules
+    with a new value (high bit set: never the memset launchers' XTAG 0x5a5a0001 nor a zeroed granule),
+    so granules an earlier launch left in xchk never match and the launcher needs no memset."""
+    lib = native.require()
+    fn = lib.gadmm_next_xtag
+    fn.restype = ctypes.c_uint
+    fn.argtypes = []
+    tags = [fn() for _ in range(1000)]
+    assert len(set(tags)) == len(tags)
+    assert all(t & 0x80000000 for t in tags) and 0x5a5a0001 not in tags
+    assert all(b == a + 1 for a, b in zip(tags, tags[1:]))
+    assert native.PersistArgs.xtag.offset == native.PersistArgs.xcd.offset + 4
