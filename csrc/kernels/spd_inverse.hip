@@ -191,13 +191,12 @@ extern "C" int gadmm_spd_inverse_small_f64(const double* A, const double* shift,
   if (N <= 0) return 0;
   const char* gje = getenv("GADMM_GJ64");  // A/B switch (read per call: set-up only)
   const bool gj64 = !(gje && gje[0] == '0');
-  const char* rge = getenv("GADMM_INV_REG");  // A/B switch: 0 = the LDS 64-wide kernel
+  // GADMM_INV_REG=0: the LDS 64-wide kernel (the tests' bit-identity cross-check). 8 waves per matrix:
+  // 4 and 16 measured 35.3 / 32.0 vs 29.3 us for the headline's 24 x 2 inverses (profiles/r06_final/inv_p2)
+  const char* rge = getenv("GADMM_INV_REG");
   const bool reg = !(rge && rge[0] == '0');
   if (d <= 64 && gj64 && reg) {
-    const int nw = rge ? atoi(rge) : 8;  // waves per matrix (A/B: GADMM_INV_REG=4/8/16)
-    if (nw == 4) hipLaunchKernelGGL(spd_inverse_reg64_kernel<4>, dim3(N, nvar), dim3(256), 0, st, A, shift, d, nvar, out, status);
-    else if (nw == 16) hipLaunchKernelGGL(spd_inverse_reg64_kernel<16>, dim3(N, nvar), dim3(1024), 0, st, A, shift, d, nvar, out, status);
-    else hipLaunchKernelGGL(spd_inverse_reg64_kernel<8>, dim3(N, nvar), dim3(512), 0, st, A, shift, d, nvar, out, status);
+    hipLaunchKernelGGL(spd_inverse_reg64_kernel<8>, dim3(N, nvar), dim3(512), 0, st, A, shift, d, nvar, out, status);
     GADMM_CHECK(hipGetLastError());
     return 0;
   }
