@@ -1,6 +1,6 @@
 #!/bin/bash
-# D-GADMM re-chain inverse prefetch: A (ab_libs/libA.so: image loaded at the re-chain) vs B (in-tree:
-# loaded in an idle phase), alternating, same box; D-GADMM / dynamic tests on B first
+# D-GADMM re-chain image loads: A (ab_libs/libA.so: every image at the re-chain) vs B (in-tree:
+# the variant under test), alternating, same box; D-GADMM / dynamic tests on B first
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 O=gpurun_out/${1:-dgab}; mkdir -p $O
